@@ -1,0 +1,235 @@
+"""bench.py — headline benchmark of the MI355X rasterizer.
+
+Metric (BASELINE.json): Mpixels/s shaded at 4096x4096, 1M triangles (+ Mtri/s),
+on 1/2/4/8 GPUs.  Workload = config C3b of SURVEY §8(d): 1M random front-facing
+triangles (vertex offsets +-16 px), Phong + 256^2 texture, one light, drawn with
+FillLineOptimized semantics (DrawModelOptimized(RenderQueue,...) +
+FillLineOptimized, projekt.cpp:3615-3871 / 1492-2320), per-triangle submission.
+
+One step = one frame: clear colour + z, then bin + raster + shade every
+triangle into the frame (inputs already resident in HBM).  With N GPUs the
+frame is split into N row bands (rank r owns rows [r*H/N, (r+1)*H/N)), every
+rank bins all triangles against its band, and the colour strips are gathered
+to rank 0 over RCCL ("scaling": "strong": total work fixed).
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cpu-renderer_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--width", type=int, default=4096)
+    ap.add_argument("--height", type=int, default=4096)
+    ap.add_argument("--tris", type=int, default=1_000_000)
+    ap.add_argument("--radius", type=float, default=16.0)
+    ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--tile", type=str, default="")
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU path (rank 0, N=1)")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-max-tris", type=int, default=1_000_000,
+                    help="bound on the CPU sample (triangles of the same scene)")
+    ap.add_argument("--check", type=int, default=0, help="compare the frame with the oracle")
+    return ap.parse_args()
+
+
+def algorithmic_bytes(T, W, rows, tex_texels):
+    """Bytes k_raster must move at minimum per frame:
+    positions+normals+uvs read once (96 B/triangle; FillLineOptimized never
+    reads vertex colours), prior z read + z and colour written (12 B/pixel),
+    the texture read once."""
+    return 96 * T + 12 * W * rows + 4 * tex_texels
+
+
+def load_traffic(cfg_key):
+    """HBM bytes per k_raster launch measured with rocprofv3 PMC passes
+    (tools/pmc_traffic.py writes profiles/pmc_traffic.json), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        e = d.get(cfg_key)
+        return None if e is None else float(e["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def cpu_baseline(scene, threads, max_tris):
+    """Oracle (CPU restatement, banded threads) on the same scene: frame time
+    for min(T, max_tris) triangles, scaled to the full T when sampled."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from prk import abi
+    T = scene.tri_count
+    n = min(T, max_tris)
+    sub = scene if n == T else scene.subset(0, n)
+    t0 = time.perf_counter()
+    O.render(sub, semantics=abi.PRK_SEM_AVX, phong=True, threads=threads, winners=False)
+    dt = time.perf_counter() - t0
+    frame = dt * (T / n)
+    return dict(value=scene.width * scene.height / frame / 1e6, unit="Mpixels/s", cores=threads,
+                kind="port",
+                sample="%d of %d triangles of the same %dx%d scene, oracle/prk_oracle.c banded over %d "
+                       "threads, %.2f s measured%s" % (n, T, scene.width, scene.height, threads, dt,
+                                                       "" if n == T else ", scaled linearly to T"),
+                frame_s=frame)
+
+
+def main():
+    a = parse()
+    import torch
+    import prk
+    from prk import abi, scenes
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            sys.stderr.write("bench: --gpus %d needs torch.distributed.run (WORLD_SIZE)\n" % a.gpus)
+            sys.exit(2)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+
+    W, H = a.width, a.height
+    scene = scenes.random_soup(a.tris, W, H, radius=a.radius, seed=a.seed, textured=True)
+    row0 = H * rank // world
+    row1 = H * (rank + 1) // world
+    rows = row1 - row0
+
+    color = torch.empty((rows, W), dtype=torch.int32, device=dev)
+    zbuf = torch.empty((rows, W), dtype=torch.float32, device=dev)
+    r = prk.Renderer(dev)
+    r.target_bind(color.data_ptr(), W * 4, zbuf.data_ptr(), W, H, row0, row1)
+    if a.tile:
+        tw, th = [int(x) for x in a.tile.split("x")]
+        r.set_tile(tw, th)
+    r.set_camera(scene.prk_transform(), scene.prk_lights())
+    geom = r.geometry(scene.vertices, None, scene.normals, scene.uvs)  # AVX path: no colours read
+    tex = r.texture(scene.texture)
+    stream = torch.cuda.current_stream().cuda_stream
+    full = None
+    if world > 1 and rank == 0:
+        full = [torch.empty((H // world if H % world == 0 else rows, W), dtype=torch.int32, device=dev)
+                for _ in range(world)]
+    zmin = -float(np.finfo(np.float32).max)
+
+    def step():
+        color.fill_(int(np.int32(np.uint32(0xFF000000).view(np.int32))))
+        zbuf.fill_(zmin)
+        r.draw_model_optimized(geom, scene.tri_count, bitmap=tex, phong=True)
+        r.complete_all_work(stream)
+        if world > 1:
+            dist.gather(color, full if rank == 0 else None, dst=0)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ms_bin = ms_raster = 0.0
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+        st = r.stats()  # HIP events recorded on the launch stream around each kernel
+        ms_bin += st["ms_bin"]
+        ms_raster += st["ms_raster"]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    stats = r.stats()
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms = dt * 1000.0 / a.steps
+    ms_raster /= a.steps
+    ms_bin /= a.steps
+
+    check = None
+    if a.check and rank == 0 and world == 1:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        oc, oz, _, _ = O.render(scene, threads=min(16, os.cpu_count() or 1), winners=False)
+        gc = color.cpu().numpy().view(np.uint32)
+        gz = zbuf.cpu().numpy()
+        check = dict(z_mismatch=int((gz.view(np.uint32) != oz.view(np.uint32)).sum()),
+                     color_mismatch=int((gc != oc).sum()))
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    T = scene.tri_count
+    tex_texels = scene.texture.width * (scene.texture.height + 1)
+    alg = algorithmic_bytes(T, W, rows, tex_texels)
+    achieved = alg / (ms_raster * 1e-3) / 1e9 if ms_raster > 0 else 0.0
+    cfg_key = "%dx%d_T%d_r%g_N%d" % (W, H, T, a.radius, world)
+    traffic = load_traffic(cfg_key)
+    out = {
+        "metric": "Mpixels/s shaded (+ Mtri/s) at 4096x4096, 1M tris; 1/2/4/8 GPUs",
+        "value": W * H / (ms * 1e-3) / 1e6,
+        "unit": "Mpixels/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": ms,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded random triangle soup + random 256x256 texture; SURVEY C3b)",
+        "config": {"workload": "C3b: %dx%d, %d random triangles (offsets +-%g px), Phong + texture, "
+                               "FillLineOptimized semantics, per-triangle submission"
+                               % (W, H, T, a.radius),
+                   "width": W, "height": H, "triangles": T, "radius_px": a.radius,
+                   "lights": len(scene.lights), "texture": "256x256",
+                   "parallelism": "row bands x%d + RCCL gather" % world if world > 1 else "1 GPU",
+                   "tile": a.tile or "64x32"},
+        "mtri_per_s": T / (ms * 1e-3) / 1e6,
+        "ms_bin": ms_bin,
+        "ms_raster": ms_raster,
+        "bin_entries": int(stats["bin_entries"]),
+        "roofline": {"bound": "hbm", "kernel": "k_raster", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "algorithmic_bytes": alg},
+    }
+    if check is not None:
+        out["check"] = check
+    if a.cpu_baseline and world == 1:
+        threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+        out["cpu_baseline"] = cpu_baseline(scene, threads, a.cpu_max_tris)
+        out["cpu_baseline"].pop("frame_s", None)
+    else:
+        out["cpu_baseline"] = None
+    print(json.dumps(out))
+    r.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,615 @@
+// prk_api.cpp — host side of libprk_hip.so: the C-ABI declared in include/prk.h.
+//
+// Owns device resources (geometry, textures, scratch for binning) and turns the
+// reference's draw calls into one GPU frame per prk_flush:
+//   FillEdgeTable + DrawModelOptimized / DrawModel (projekt.cpp:3882, 3615, 162)
+//   -> prk_draw records {geometry range, P, semantics, Phong, Bitmap}
+//   Platform.CompleteAllWork -> prk_flush runs bin + raster kernels.
+// There is no CPU fallback: every entry point that computes pixels needs the
+// HIP device and fails with PRK_ERR_DEVICE without one.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/prk.h"
+#include "prk_device.h"
+
+extern "C" {
+hipError_t prk_launch_tri_draw(const prk::DrawRec *, uint32_t, uint32_t *, uint32_t, hipStream_t);
+hipError_t prk_launch_bin(const prk::FrameParams *, uint32_t *, uint32_t *, uint32_t *, void *, uint32_t,
+                          hipStream_t);
+hipError_t prk_launch_fill(const prk::FrameParams *, const void *, const uint32_t *, uint32_t *, uint32_t *,
+                           hipStream_t);
+hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, const uint32_t *, hipStream_t);
+}
+
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes + bytes / 4 + 256;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct Geometry {
+    const float *V = nullptr, *C = nullptr, *N = nullptr, *UV = nullptr;
+    uint32_t vertex_count = 0;
+    bool owned = false;
+};
+
+struct Texture {
+    uint8_t *mem = nullptr;
+    int32_t w = 0, h = 0, pitch = 0;
+};
+
+int status_of(hipError_t e) {
+    if (e == hipSuccess) return PRK_OK;
+    if (e == hipErrorOutOfMemory) return PRK_ERR_NOMEM;
+    return PRK_ERR_DEVICE;
+}
+
+}  // namespace
+
+struct prk_context {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    // target
+    void *color = nullptr;
+    int32_t pitch = 0;
+    float *zbuf = nullptr;
+    int32_t W = 0, H = 0, row0 = 0, row1 = 0;
+    bool owns_target = false;
+    // camera + lights
+    prk_transform transform{};
+    prk_light_data lights{};
+    bool have_camera = false;
+    // resources
+    std::vector<Geometry> geoms;
+    std::vector<Texture> texs;
+    std::vector<prk::DrawRec> draws;
+    uint32_t pending_tris = 0;
+    // scratch
+    DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_counts, d_offs, d_cursor, d_bins, d_winners;
+    uint32_t *h_total = nullptr;  // pinned
+    int32_t tile_w = 64, tile_h = 32;
+    bool debug = false;
+    bool winners_valid = false;
+    prk_stats stats{};
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+
+#define PRK_TRY(expr)                              \
+    do {                                           \
+        hipError_t _e = (expr);                    \
+        if (_e != hipSuccess) return status_of(_e); \
+    } while (0)
+
+extern "C" {
+
+const char *prk_version(void) { return "prk 0.1 (gfx950)"; }
+
+int prk_device_count(int *out) {
+    if (!out) return PRK_ERR_ARG;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *out = n;
+    return PRK_OK;
+}
+
+int prk_create(int device, prk_context **out) {
+    if (!out) return PRK_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return PRK_ERR_DEVICE;
+    if (device < 0 || device >= n) return PRK_ERR_ARG;
+    PRK_TRY(hipSetDevice(device));
+    prk_context *c = new (std::nothrow) prk_context();
+    if (!c) return PRK_ERR_NOMEM;
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_total, sizeof(uint32_t), hipHostMallocDefault);
+    if (e != hipSuccess) {
+        prk_destroy(c);
+        return status_of(e);
+    }
+    *out = c;
+    return PRK_OK;
+}
+
+int prk_destroy(prk_context *c) {
+    if (!c) return PRK_ERR_ARG;
+    (void)hipSetDevice(c->device);
+    if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+    for (auto &g : c->geoms)
+        if (g.owned) {
+            (void)hipFree((void *)g.V);
+            (void)hipFree((void *)g.C);
+            (void)hipFree((void *)g.N);
+            (void)hipFree((void *)g.UV);
+        }
+    for (auto &t : c->texs) (void)hipFree(t.mem);
+    if (c->owns_target) {
+        (void)hipFree(c->color);
+        (void)hipFree(c->zbuf);
+    }
+    DevBuf *bufs[] = {&c->d_draws, &c->d_texs, &c->d_tri_draw, &c->d_ranges, &c->d_counts,
+                      &c->d_offs,  &c->d_cursor, &c->d_bins, &c->d_winners};
+    for (DevBuf *b : bufs) b->release();
+    if (c->h_total) (void)hipHostFree(c->h_total);
+    for (auto &e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    return PRK_OK;
+}
+
+static void drop_target(prk_context *c) {
+    if (c->owns_target) {
+        (void)hipFree(c->color);
+        (void)hipFree(c->zbuf);
+    }
+    c->color = nullptr;
+    c->zbuf = nullptr;
+    c->owns_target = false;
+    c->W = c->H = c->row0 = c->row1 = 0;
+}
+
+int prk_target_bind(prk_context *c, void *color, int32_t pitch_bytes, float *zbuf, int32_t width,
+                    int32_t height, int32_t row0, int32_t row1) {
+    if (!c || !color || !zbuf || width <= 0 || height <= 0 || row0 < 0 || row1 > height || row0 >= row1 ||
+        pitch_bytes < width * 4 || (pitch_bytes & 3))
+        return PRK_ERR_ARG;
+    drop_target(c);
+    c->color = color;
+    c->pitch = pitch_bytes;
+    c->zbuf = zbuf;
+    c->W = width;
+    c->H = height;
+    c->row0 = row0;
+    c->row1 = row1;
+    c->winners_valid = false;
+    return PRK_OK;
+}
+
+int prk_target_alloc(prk_context *c, int32_t width, int32_t height, int32_t row0, int32_t row1,
+                     void **color_out, float **zbuf_out) {
+    if (!c || width <= 0 || height <= 0 || row0 < 0 || row1 > height || row0 >= row1) return PRK_ERR_ARG;
+    PRK_TRY(hipSetDevice(c->device));
+    drop_target(c);
+    size_t px = (size_t)width * (row1 - row0);
+    void *col = nullptr;
+    float *z = nullptr;
+    hipError_t e = hipMalloc(&col, px * 4);
+    if (e == hipSuccess) e = hipMalloc((void **)&z, px * 4);
+    if (e != hipSuccess) {
+        (void)hipFree(col);
+        (void)hipFree(z);
+        return status_of(e);
+    }
+    c->color = col;
+    c->zbuf = z;
+    c->pitch = width * 4;
+    c->W = width;
+    c->H = height;
+    c->row0 = row0;
+    c->row1 = row1;
+    c->owns_target = true;
+    c->winners_valid = false;
+    if (color_out) *color_out = col;
+    if (zbuf_out) *zbuf_out = z;
+    return PRK_OK;
+}
+
+__global__ void k_fill_target(uint32_t *color, int32_t pitch, float *z, int32_t W, int32_t rows,
+                              uint32_t cval, float zval) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    size_t n = (size_t)W * rows;
+    if (i >= n) return;
+    size_t r = i / W, x = i % W;
+    reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(color) + r * pitch)[x] = cval;
+    z[i] = zval;
+}
+
+int prk_target_clear(prk_context *c, uint32_t color, float z) {
+    if (!c) return PRK_ERR_ARG;
+    if (!c->color) return PRK_ERR_NO_TARGET;
+    PRK_TRY(hipSetDevice(c->device));
+    size_t n = (size_t)c->W * (c->row1 - c->row0);
+    hipLaunchKernelGGL(k_fill_target, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->own_stream,
+                       (uint32_t *)c->color, c->pitch, c->zbuf, c->W, c->row1 - c->row0, color, z);
+    PRK_TRY(hipGetLastError());
+    return PRK_OK;
+}
+
+int prk_target_download(prk_context *c, uint32_t *color_host, int32_t host_pitch, float *z_host) {
+    if (!c) return PRK_ERR_ARG;
+    if (!c->color) return PRK_ERR_NO_TARGET;
+    PRK_TRY(hipSetDevice(c->device));
+    PRK_TRY(hipStreamSynchronize(c->own_stream));
+    PRK_TRY(hipDeviceSynchronize());
+    int rows = c->row1 - c->row0;
+    if (color_host)
+        PRK_TRY(hipMemcpy2D(color_host, host_pitch, c->color, c->pitch, (size_t)c->W * 4, rows,
+                            hipMemcpyDeviceToHost));
+    if (z_host) PRK_TRY(hipMemcpy(z_host, c->zbuf, (size_t)c->W * rows * 4, hipMemcpyDeviceToHost));
+    return PRK_OK;
+}
+
+int prk_target_upload(prk_context *c, const uint32_t *color_host, int32_t host_pitch, const float *z_host) {
+    if (!c) return PRK_ERR_ARG;
+    if (!c->color) return PRK_ERR_NO_TARGET;
+    PRK_TRY(hipSetDevice(c->device));
+    PRK_TRY(hipStreamSynchronize(c->own_stream));
+    int rows = c->row1 - c->row0;
+    if (color_host)
+        PRK_TRY(hipMemcpy2D(c->color, c->pitch, color_host, host_pitch, (size_t)c->W * 4, rows,
+                            hipMemcpyHostToDevice));
+    if (z_host) PRK_TRY(hipMemcpy(c->zbuf, z_host, (size_t)c->W * rows * 4, hipMemcpyHostToDevice));
+    return PRK_OK;
+}
+
+int prk_set_camera(prk_context *c, const prk_transform *t, const prk_light_data *l) {
+    if (!c || !t || !l || l->LightCount > PRK_MAX_LIGHTS) return PRK_ERR_ARG;
+    c->transform = *t;
+    c->lights = *l;
+    c->have_camera = true;
+    return PRK_OK;
+}
+
+int prk_texture_create(prk_context *c, const prk_bitmap *b, int32_t *handle_out) {
+    if (!c || !b || !b->Memory || !handle_out || b->Width <= 0 || b->Height <= 0 || b->Pitch < 4 * b->Width ||
+        (b->Pitch & 3))
+        return PRK_ERR_ARG;
+    PRK_TRY(hipSetDevice(c->device));
+    Texture t;
+    t.w = b->Width;
+    t.h = b->Height;
+    t.pitch = b->Pitch;
+    size_t bytes = (size_t)b->Pitch * (b->Height + 1);
+    PRK_TRY(hipMalloc((void **)&t.mem, bytes));
+    hipError_t e = hipMemcpy(t.mem, b->Memory, bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(t.mem);
+        return status_of(e);
+    }
+    *handle_out = (int32_t)c->texs.size();
+    c->texs.push_back(t);
+    return PRK_OK;
+}
+
+static int upload_array(const float *src, size_t n, const float **dst) {
+    *dst = nullptr;
+    if (!src) return PRK_OK;
+    float *d = nullptr;
+    PRK_TRY(hipMalloc((void **)&d, n * sizeof(float)));
+    hipError_t e = hipMemcpy(d, src, n * sizeof(float), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(d);
+        return status_of(e);
+    }
+    *dst = d;
+    return PRK_OK;
+}
+
+int prk_geometry_create(prk_context *c, const float *v, const float *col, const float *n, const float *uv,
+                        uint32_t vertex_count, int32_t *handle_out) {
+    if (!c || !v || !handle_out || vertex_count % 3) return PRK_ERR_ARG;
+    PRK_TRY(hipSetDevice(c->device));
+    Geometry g;
+    g.vertex_count = vertex_count;
+    g.owned = true;
+    int rc = upload_array(v, (size_t)vertex_count * 3, &g.V);
+    if (rc == PRK_OK) rc = upload_array(col, (size_t)vertex_count * 4, &g.C);
+    if (rc == PRK_OK) rc = upload_array(n, (size_t)vertex_count * 3, &g.N);
+    if (rc == PRK_OK) rc = upload_array(uv, (size_t)vertex_count * 2, &g.UV);
+    if (rc != PRK_OK) {
+        (void)hipFree((void *)g.V);
+        (void)hipFree((void *)g.C);
+        (void)hipFree((void *)g.N);
+        (void)hipFree((void *)g.UV);
+        return rc;
+    }
+    *handle_out = (int32_t)c->geoms.size();
+    c->geoms.push_back(g);
+    return PRK_OK;
+}
+
+int prk_geometry_wrap_device(prk_context *c, const float *v, const float *col, const float *n,
+                             const float *uv, uint32_t vertex_count, int32_t *handle_out) {
+    if (!c || !v || !handle_out || vertex_count % 3) return PRK_ERR_ARG;
+    Geometry g;
+    g.V = v;
+    g.C = col;
+    g.N = n;
+    g.UV = uv;
+    g.vertex_count = vertex_count;
+    g.owned = false;
+    *handle_out = (int32_t)c->geoms.size();
+    c->geoms.push_back(g);
+    return PRK_OK;
+}
+
+int prk_draw(prk_context *c, int32_t geometry, uint32_t first_tri, uint32_t tri_count, const float P[3],
+             int32_t semantics, int32_t phong, int32_t texture) {
+    if (!c || geometry < 0 || geometry >= (int32_t)c->geoms.size()) return PRK_ERR_ARG;
+    const Geometry &g = c->geoms[geometry];
+    if ((uint64_t)first_tri + tri_count > g.vertex_count / 3) return PRK_ERR_ARG;
+    if (texture >= (int32_t)c->texs.size()) return PRK_ERR_ARG;
+    const bool tex = texture >= 0;
+    int mode;
+    if (semantics == PRK_SEM_AVX) {
+        // FillLineOptimized dereferences Bitmap at entry (projekt.cpp:1506) and
+        // its non-Phong branch stores garbage (2285-2316): undefined -> rejected.
+        if (!tex || !phong) return PRK_ERR_UNSUPPORTED;
+        mode = prk::MODE_AVX;
+    } else if (semantics == PRK_SEM_SCALAR) {
+        mode = phong ? (tex ? prk::MODE_SC_PHONG_TEX : prk::MODE_SC_PHONG)
+                     : (tex ? prk::MODE_SC_GOURAUD_TEX : prk::MODE_SC_GOURAUD);
+    } else {
+        return PRK_ERR_ARG;
+    }
+    if ((phong || !tex) && !g.N) return PRK_ERR_ARG;
+    if (tex && !g.UV) return PRK_ERR_ARG;
+    if ((mode == prk::MODE_SC_GOURAUD || mode == prk::MODE_SC_PHONG) && !g.C) return PRK_ERR_ARG;
+    if (tri_count == 0) return PRK_OK;
+    if ((uint64_t)c->pending_tris + tri_count >= 0xFFFFFFF0ull) return PRK_ERR_ARG;
+    prk::DrawRec d{};
+    d.V = g.V;
+    d.C = g.C;
+    d.N = g.N;
+    d.UV = g.UV;
+    d.geom_tri0 = first_tri;
+    d.first_global = c->pending_tris;
+    d.tri_count = tri_count;
+    d.mode = mode;
+    d.tex = texture;
+    d.P[0] = P ? P[0] : 0.0f;
+    d.P[1] = P ? P[1] : 0.0f;
+    d.P[2] = P ? P[2] : 0.0f;
+    c->draws.push_back(d);
+    c->pending_tris += tri_count;
+    return PRK_OK;
+}
+
+int prk_reset_draws(prk_context *c) {
+    if (!c) return PRK_ERR_ARG;
+    c->draws.clear();
+    c->pending_tris = 0;
+    return PRK_OK;
+}
+
+int prk_set_tile(prk_context *c, int32_t tw, int32_t th) {
+    if (!c || tw <= 0 || th <= 0 || (tw % 8) || tw * th > 8192 || tw * th < 64) return PRK_ERR_ARG;
+    c->tile_w = tw;
+    c->tile_h = th;
+    return PRK_OK;
+}
+
+int prk_set_debug(prk_context *c, int32_t enable) {
+    if (!c) return PRK_ERR_ARG;
+    c->debug = enable != 0;
+    return PRK_OK;
+}
+
+int prk_flush(prk_context *c, void *stream) {
+    if (!c) return PRK_ERR_ARG;
+    if (!c->color) return PRK_ERR_NO_TARGET;
+    if (!c->have_camera) return PRK_ERR_ARG;
+    PRK_TRY(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->own_stream;
+    const uint32_t T = c->pending_tris;
+    bool any_avx = false;
+    int modeset = -2;
+    for (const auto &d : c->draws) {
+        any_avx |= d.mode == prk::MODE_AVX;
+        if (modeset == -2) modeset = d.mode;
+        else if (modeset != d.mode) modeset = -1;
+    }
+    if (any_avx && (c->W % 8)) return PRK_ERR_UNSUPPORTED;  // aligned 8-wide z load, projekt.cpp:2218
+    if (modeset != prk::MODE_AVX && modeset != prk::MODE_SC_GOURAUD && modeset != prk::MODE_SC_PHONG)
+        modeset = -1;
+
+    prk::FrameParams fp{};
+    fp.D = c->transform.DistanceAboveTarget;
+    fp.F = c->transform.FocalLength;
+    fp.M2P = c->transform.MetersToPixels;
+    fp.Cx = c->transform.ScreenCenter[0];
+    fp.Cy = c->transform.ScreenCenter[1];
+    fp.InvM2P = 1.0f / fp.M2P;
+    fp.light_count = c->lights.LightCount;
+    for (int k = 0; k < 4; ++k) fp.amb[k] = c->lights.AmbientIntensity[k];
+    for (uint32_t l = 0; l < PRK_MAX_LIGHTS; ++l) {
+        for (int k = 0; k < 3; ++k) fp.lp[l][k] = c->lights.Lights[l].P[k];
+        for (int k = 0; k < 4; ++k) fp.li[l][k] = c->lights.Lights[l].Intensity[k];
+    }
+    fp.W = c->W;
+    fp.H = c->H;
+    fp.row0 = c->row0;
+    fp.row1 = c->row1;
+    fp.pitch = c->pitch;
+    fp.color = (uint32_t *)c->color;
+    fp.zbuf = c->zbuf;
+    fp.tile_w = c->tile_w;
+    fp.tile_h = c->tile_h;
+    fp.tiles_x = (c->W + c->tile_w - 1) / c->tile_w;
+    fp.tiles_y = (c->row1 - c->row0 + c->tile_h - 1) / c->tile_h;
+    fp.tri_count = T;
+    fp.ndraws = (uint32_t)c->draws.size();
+    const uint32_t ntiles = (uint32_t)(fp.tiles_x * fp.tiles_y);
+    if (fp.tiles_x > 65535 || fp.tiles_y > 65535) return PRK_ERR_UNSUPPORTED;
+
+    c->stats = prk_stats{};
+    c->stats.triangles = T;
+    c->stats.tiles = ntiles;
+    if (c->debug) {
+        PRK_TRY(c->d_winners.ensure((size_t)c->W * (c->row1 - c->row0) * 4));
+        PRK_TRY(hipMemsetAsync(c->d_winners.p, 0xFF, (size_t)c->W * (c->row1 - c->row0) * 4, s));
+        fp.winners = (int32_t *)c->d_winners.p;
+        c->winners_valid = true;
+    }
+    if (T == 0) {
+        c->draws.clear();
+        c->pending_tris = 0;
+        return PRK_OK;
+    }
+    // Device-side draw + texture tables.
+    std::vector<prk::TexRec> texs(c->texs.size());
+    for (size_t i = 0; i < texs.size(); ++i) {
+        texs[i].mem = c->texs[i].mem;
+        texs[i].w = c->texs[i].w;
+        texs[i].h = c->texs[i].h;
+        texs[i].pitch = c->texs[i].pitch;
+        texs[i].pad = 0;
+    }
+    PRK_TRY(c->d_draws.ensure(c->draws.size() * sizeof(prk::DrawRec)));
+    PRK_TRY(hipMemcpyAsync(c->d_draws.p, c->draws.data(), c->draws.size() * sizeof(prk::DrawRec),
+                           hipMemcpyHostToDevice, s));
+    if (!texs.empty()) {
+        PRK_TRY(c->d_texs.ensure(texs.size() * sizeof(prk::TexRec)));
+        PRK_TRY(hipMemcpyAsync(c->d_texs.p, texs.data(), texs.size() * sizeof(prk::TexRec),
+                               hipMemcpyHostToDevice, s));
+    }
+    fp.draws = (const prk::DrawRec *)c->d_draws.p;
+    fp.texs = (const prk::TexRec *)c->d_texs.p;
+    fp.tri_draw = nullptr;
+    if (fp.ndraws > 1) {
+        PRK_TRY(c->d_tri_draw.ensure((size_t)T * 4));
+        PRK_TRY(prk_launch_tri_draw(fp.draws, fp.ndraws, (uint32_t *)c->d_tri_draw.p, T, s));
+        fp.tri_draw = (const uint32_t *)c->d_tri_draw.p;
+    }
+    PRK_TRY(c->d_ranges.ensure((size_t)T * 8));
+    PRK_TRY(c->d_counts.ensure((size_t)ntiles * 4));
+    PRK_TRY(c->d_offs.ensure((size_t)(ntiles + 1) * 4));
+    PRK_TRY(c->d_cursor.ensure((size_t)ntiles * 4));
+    PRK_TRY(hipMemsetAsync(c->d_counts.p, 0, (size_t)ntiles * 4, s));
+    PRK_TRY(hipMemsetAsync(c->d_cursor.p, 0, (size_t)ntiles * 4, s));
+    PRK_TRY(hipEventRecord(c->ev[0], s));
+    PRK_TRY(prk_launch_bin(&fp, (uint32_t *)c->d_counts.p, (uint32_t *)c->d_offs.p, (uint32_t *)c->d_cursor.p,
+                           c->d_ranges.p, ntiles, s));
+    // The bin array size is data dependent: read the total back (one small
+    // D2H copy per frame) and grow the buffer if needed.
+    PRK_TRY(hipMemcpyAsync(c->h_total, (uint32_t *)c->d_offs.p + ntiles, 4, hipMemcpyDeviceToHost, s));
+    PRK_TRY(hipStreamSynchronize(s));
+    const uint32_t total = *c->h_total;
+    c->stats.bin_entries = total;
+    PRK_TRY(c->d_bins.ensure((size_t)std::max<uint32_t>(total, 1) * 4));
+    PRK_TRY(prk_launch_fill(&fp, c->d_ranges.p, (const uint32_t *)c->d_offs.p, (uint32_t *)c->d_cursor.p,
+                            (uint32_t *)c->d_bins.p, s));
+    PRK_TRY(hipEventRecord(c->ev[1], s));
+    PRK_TRY(prk_launch_raster(&fp, modeset, (const uint32_t *)c->d_offs.p, (const uint32_t *)c->d_bins.p, s));
+    PRK_TRY(hipEventRecord(c->ev[2], s));
+    c->draws.clear();
+    c->pending_tris = 0;
+    return PRK_OK;
+}
+
+int prk_synchronize(prk_context *c) {
+    if (!c) return PRK_ERR_ARG;
+    PRK_TRY(hipSetDevice(c->device));
+    PRK_TRY(hipStreamSynchronize(c->own_stream));
+    PRK_TRY(hipDeviceSynchronize());
+    return PRK_OK;
+}
+
+int prk_get_stats(prk_context *c, prk_stats *out) {
+    if (!c || !out) return PRK_ERR_ARG;
+    if (c->stats.triangles) {
+        float a = 0, b = 0;
+        if (hipEventElapsedTime(&a, c->ev[0], c->ev[1]) == hipSuccess) c->stats.ms_bin = a;
+        if (hipEventElapsedTime(&b, c->ev[1], c->ev[2]) == hipSuccess) c->stats.ms_raster = b;
+        c->stats.ms_total = c->stats.ms_bin + c->stats.ms_raster;
+    }
+    *out = c->stats;
+    return PRK_OK;
+}
+
+int prk_download_winners(prk_context *c, int32_t *w) {
+    if (!c || !w) return PRK_ERR_ARG;
+    if (!c->winners_valid || !c->d_winners.p) return PRK_ERR_ARG;
+    PRK_TRY(hipSetDevice(c->device));
+    PRK_TRY(hipDeviceSynchronize());
+    PRK_TRY(hipMemcpy(w, c->d_winners.p, (size_t)c->W * (c->row1 - c->row0) * 4, hipMemcpyDeviceToHost));
+    return PRK_OK;
+}
+
+// ConstructSphere (projekt.cpp:4123-4289): the reference's only test mesh.
+// 24 inclination x 48 azimuth steps, r = 0.5, 6624 vertices.
+int prk_construct_sphere(float *V, float *Col, float *N, float *UV, uint32_t *count_out) {
+    if (!V || !Col || !N || !UV || !count_out) return PRK_ERR_ARG;
+    const float Pi32 = 3.14159265359f;
+    const float Radius = 0.5f;
+    const uint32_t StepCount = 24;
+    const float Up[4] = {1, 0, 0, 1}, Down[4] = {0, 1, 0, 1};
+    float Inc[4];
+    for (int k = 0; k < 4; ++k) Inc[k] = (Down[k] - Up[k]) / (float)StepCount;
+    const float IncI = Pi32 / StepCount;
+    const float IncA = (2.0f * Pi32) / (StepCount * 2);
+    float Cur[4] = {Up[0], Up[1], Up[2], Up[3]};
+    uint32_t n = 0;
+    auto emit = [&](float x, float y, float z, float u, float v, const float *c4, const float *blue, bool inc) {
+        V[3 * n] = Radius * x; V[3 * n + 1] = Radius * y; V[3 * n + 2] = Radius * z;
+        N[3 * n] = x; N[3 * n + 1] = y; N[3 * n + 2] = z;
+        UV[2 * n] = u; UV[2 * n + 1] = v;
+        for (int k = 0; k < 4; ++k) Col[4 * n + k] = inc ? (c4[k] + Inc[k]) + blue[k] : c4[k] + blue[k];
+        ++n;
+    };
+    for (uint32_t ii = 0; ii < StepCount; ++ii) {
+        for (uint32_t ai = 0; ai < StepCount * 2; ++ai) {
+            float I0 = (float)ii * IncI, I1 = (float)(ii + 1) * IncI;
+            float A0 = (float)ai * IncA, A1 = (float)(ai + 1) * IncA;
+            float Blue[4] = {0, 0, (1.0f + cosf(A0)) / 2.0f, 0};
+            float NBlue[4] = {0, 0, (1.0f + cosf(A1)) / 2.0f, 0};
+            if (ii == 0) {
+                float S[3] = {sinf(I1) * cosf(A0), cosf(I1), sinf(I1) * sinf(A0)};
+                float Tt[3] = {sinf(I1) * cosf(A1), cosf(I1), sinf(I1) * sinf(A1)};
+                emit(0, 1, 0, 0.5f, 0.5f, Cur, Blue, false);
+                emit(S[0], S[1], S[2], S[0], S[2], Cur, Blue, true);
+                emit(Tt[0], Tt[1], Tt[2], Tt[0], Tt[2], Cur, NBlue, true);
+            } else if (ii == StepCount - 1) {
+                float F[3] = {sinf(I0) * cosf(A0), cosf(I0), sinf(I0) * sinf(A0)};
+                float Tt[3] = {sinf(I0) * cosf(A1), cosf(I0), sinf(I0) * sinf(A1)};
+                emit(F[0], F[1], F[2], 0.5f, 0.5f, Cur, Blue, false);
+                emit(0, -1, 0, 0.0f, 0.0f, Cur, Blue, true);
+                emit(Tt[0], Tt[1], Tt[2], Tt[0], Tt[2], Cur, NBlue, true);
+            } else {
+                float F[3] = {sinf(I0) * cosf(A0), cosf(I0), sinf(I0) * sinf(A0)};
+                float S[3] = {sinf(I1) * cosf(A0), cosf(I1), sinf(I1) * sinf(A0)};
+                float Tt[3] = {sinf(I1) * cosf(A1), cosf(I1), sinf(I1) * sinf(A1)};
+                float Fo[3] = {sinf(I0) * cosf(A1), cosf(I0), sinf(I0) * sinf(A1)};
+                auto uvx = [](float a) { return (a + 1.0f) / 2.0f; };
+                emit(F[0], F[1], F[2], uvx(F[0]), uvx(F[1]), Cur, Blue, false);
+                emit(S[0], S[1], S[2], uvx(S[0]), uvx(S[1]), Cur, Blue, true);
+                emit(Tt[0], Tt[1], Tt[2], uvx(Tt[0]), uvx(Tt[1]), Cur, NBlue, true);
+                emit(F[0], F[1], F[2], uvx(F[0]), uvx(F[1]), Cur, Blue, false);
+                emit(Tt[0], Tt[1], Tt[2], uvx(Tt[0]), uvx(Tt[1]), Cur, NBlue, true);
+                emit(Fo[0], Fo[1], Fo[2], uvx(Fo[0]), uvx(Fo[1]), Cur, NBlue, false);
+            }
+        }
+        for (int k = 0; k < 4; ++k) Cur[k] = Cur[k] + Inc[k];
+    }
+    *count_out = n;
+    return PRK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,474 @@
+// prk_device.h — device-side restatement of the reference hot path for gfx950.
+//
+// Every function here reproduces a piece of projekt.cpp bit for bit: it must
+// be compiled with -ffp-contract=off (no FMA contraction) and
+// with IEEE division / square root (hipcc's default,
+// -fhip-fp32-correctly-rounded-divide-sqrt).  Pins for the reference's absent
+// math header follow SURVEY §8(c): RoundR32ToS32 = (s32)roundf,
+// Normalize(a) = (1/sqrtf(Inner(a,a)))*a, Inner = (ax*bx + ay*by) + az*bz.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace prk {
+
+constexpr int kMaxLights = 8;
+
+// Span-kernel flavours.  AVX = FillLineOptimized (projekt.cpp:1492-2320) with
+// texture + Phong (the only AVX configuration with defined output);
+// SC_* = scalar DrawModel (projekt.cpp:162-601).
+enum Mode : int {
+    MODE_AVX = 0,
+    MODE_SC_GOURAUD = 1,      // untextured, vertex-lit colour
+    MODE_SC_GOURAUD_TEX = 2,  // texel replaces colour, no lighting
+    MODE_SC_PHONG = 3,        // untextured Phong
+    MODE_SC_PHONG_TEX = 4,    // textured Phong
+    MODE_COUNT = 5
+};
+
+struct DrawRec {
+    const float *V, *C, *N, *UV;  // geometry base pointers (SoA, non-indexed)
+    uint32_t geom_tri0;           // first triangle of this draw inside the geometry
+    uint32_t first_global;        // global (submission-order) index of its first triangle
+    uint32_t tri_count;
+    int32_t mode;                 // Mode
+    int32_t tex;                  // texture index or -1
+    float P[3];                   // object offset (render_entry_3d_object::P)
+};
+
+struct TexRec {
+    const uint8_t *mem;  // (h+1) rows, last one the zeroed guard row
+    int32_t w, h, pitch;
+    int32_t pad;
+};
+
+struct FrameParams {
+    // projective_transform
+    float D, F, M2P, Cx, Cy, InvM2P;
+    // light_data
+    uint32_t light_count;
+    float amb[4];
+    float lp[kMaxLights][3];
+    float li[kMaxLights][4];
+    // target band: frame rows [row0,row1) of a W x H frame
+    int32_t W, H, row0, row1;
+    int32_t pitch;   // colour pitch in bytes
+    uint32_t *color; // points at frame row row0
+    float *zbuf;     // points at frame row row0 (row stride W floats)
+    int32_t *winners;// optional (debug): per pixel winning triangle, -1 none
+    // tiling
+    int32_t tile_w, tile_h, tiles_x, tiles_y;
+    // geometry
+    uint32_t tri_count;
+    uint32_t ndraws;
+    const DrawRec *draws;
+    const uint32_t *tri_draw;  // nullptr when ndraws == 1
+    const TexRec *texs;
+};
+
+// ---------------------------------------------------------------------------
+// Conversions with x86 semantics (the reference runs on x86).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int32_t cvtt_s32(float f) {
+    // cvttss2si / cvttps2dq: NaN and out-of-range give INT_MIN.
+    return (f >= -2147483648.0f && f < 2147483648.0f) ? (int32_t)f : INT32_MIN;
+}
+__device__ __forceinline__ int32_t round_s32(float f) { return cvtt_s32(roundf(f)); }
+__device__ __forceinline__ uint32_t round_u32(float f) {
+    // x86-64 (u32)float: 64-bit cvttss2si, keep the low 32 bits.
+    float r = roundf(f);
+    return (r >= -9223372036854775808.0f && r < 9223372036854775808.0f)
+               ? (uint32_t)(uint64_t)(int64_t)r
+               : 0u;
+}
+__device__ __forceinline__ int32_t cvt_rne_s32(float f) {
+    // _mm256_cvtps_epi32 with the default MXCSR: round to nearest even.
+    return (f >= -2147483648.0f && f < 2147483648.0f) ? (int32_t)__builtin_rintf(f) : INT32_MIN;
+}
+__device__ __forceinline__ float maxps(float a, float b) { return a > b ? a : b; }  // MAXPS
+__device__ __forceinline__ float minps(float a, float b) { return a < b ? a : b; }  // MINPS
+__device__ __forceinline__ float clamp01(float x) { return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x); }
+
+// Normalize (pinned scalar form) — used by the AET edge step and DrawModel.
+__device__ __forceinline__ void normalize_rcp(float &x, float &y, float &z) {
+    float s = 1.0f / sqrtf((x * x + y * y) + z * z);
+    x = s * x;
+    y = s * y;
+    z = s * z;
+}
+// NormalizeVector_8x (projekt.cpp:603-620), one lane: division form.
+__device__ __forceinline__ void normalize_div(float &x, float &y, float &z) {
+    float len = sqrtf((x * x + y * y) + z * z);
+    x = x / len;
+    y = y / len;
+    z = z / len;
+}
+
+// _mm_mullo_epi16/_mm_mulhi_epi16 pitch multiply (projekt.cpp:1916-1920).
+__device__ __forceinline__ int32_t mul16_trick(int32_t y, int32_t p) {
+    uint32_t ylo = (uint32_t)y & 0xFFFFu, yhi = (uint32_t)y >> 16;
+    uint32_t plo = (uint32_t)p & 0xFFFFu, phi = (uint32_t)p >> 16;
+    uint32_t lo = (ylo * plo) & 0xFFFFu;
+    uint32_t hi_mullo = (yhi * phi) & 0xFFFFu;
+    int32_t sprod = (int32_t)(int16_t)ylo * (int32_t)(int16_t)plo;
+    uint32_t hi_mulhi = ((uint32_t)sprod >> 16) & 0xFFFFu;
+    return (int32_t)(lo | ((hi_mullo | hi_mulhi) << 16));
+}
+
+// Texel read with the P2/P4 clamp: offsets outside [0, Pitch*(Th+1)-4] read
+// offset 0.  The texture holds its zeroed guard row.
+__device__ __forceinline__ uint32_t texel_at(const TexRec &t, int32_t off) {
+    int64_t limit = (int64_t)t.pitch * (t.h + 1) - 4;
+    if (off < 0 || (int64_t)off > limit) off = 0;
+    const uint8_t *p = t.mem + off;
+    if ((off & 3) == 0) return *(const uint32_t *)p;
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// Ordered 32-bit key of a float z for the visibility max (strict '>' with
+// submission order == max z, earliest triangle on ties).
+// +0 and -0 compare equal in the reference, so both map to one key.
+__device__ __forceinline__ uint32_t zkey(float z) {
+    uint32_t b = __float_as_uint(z);
+    if (z == 0.0f) b = 0u;
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+// ---------------------------------------------------------------------------
+// Edge record (edge_info, projekt.h:17-37) as registers.
+// ---------------------------------------------------------------------------
+struct Edge {
+    float X, G, Z, ZG, W, WG, U, UG, V, VG;
+    float N0, N1, N2, NG0, NG1, NG2;
+    float C0, C1, C2, C3, CG0, CG1, CG2, CG3;
+    int32_t YMin, YMax, Left;
+};
+
+__device__ __forceinline__ Edge sel(bool c, const Edge &a, const Edge &b) {
+    Edge r;
+    r.X = c ? a.X : b.X; r.G = c ? a.G : b.G; r.Z = c ? a.Z : b.Z; r.ZG = c ? a.ZG : b.ZG;
+    r.W = c ? a.W : b.W; r.WG = c ? a.WG : b.WG; r.U = c ? a.U : b.U; r.UG = c ? a.UG : b.UG;
+    r.V = c ? a.V : b.V; r.VG = c ? a.VG : b.VG;
+    r.N0 = c ? a.N0 : b.N0; r.N1 = c ? a.N1 : b.N1; r.N2 = c ? a.N2 : b.N2;
+    r.NG0 = c ? a.NG0 : b.NG0; r.NG1 = c ? a.NG1 : b.NG1; r.NG2 = c ? a.NG2 : b.NG2;
+    r.C0 = c ? a.C0 : b.C0; r.C1 = c ? a.C1 : b.C1; r.C2 = c ? a.C2 : b.C2; r.C3 = c ? a.C3 : b.C3;
+    r.CG0 = c ? a.CG0 : b.CG0; r.CG1 = c ? a.CG1 : b.CG1; r.CG2 = c ? a.CG2 : b.CG2;
+    r.CG3 = c ? a.CG3 : b.CG3;
+    r.YMin = c ? a.YMin : b.YMin; r.YMax = c ? a.YMax : b.YMax; r.Left = c ? a.Left : b.Left;
+    return r;
+}
+
+// Which edge fields a mode actually reads.  Skipping dead fields changes no
+// output: the texel overwrites the AVX colour lanes (projekt.cpp:2029-2032);
+// untextured objects never read U/V/(1/z); non-Phong never reads normals.
+template <int M> struct ModeTraits;
+template <> struct ModeTraits<MODE_AVX> { static constexpr bool tex = true, phong = true, color = false; };
+template <> struct ModeTraits<MODE_SC_GOURAUD> { static constexpr bool tex = false, phong = false, color = true; };
+template <> struct ModeTraits<MODE_SC_GOURAUD_TEX> { static constexpr bool tex = true, phong = false, color = false; };
+template <> struct ModeTraits<MODE_SC_PHONG> { static constexpr bool tex = false, phong = true, color = true; };
+template <> struct ModeTraits<MODE_SC_PHONG_TEX> { static constexpr bool tex = true, phong = true, color = false; };
+
+struct V3 { float x, y, z; };
+
+// ProjectVertex (projekt.cpp:74-93).
+__device__ __forceinline__ V3 project_vertex(V3 c, const FrameParams &fp) {
+    V3 r = {0.0f, 0.0f, 0.0f};
+    float d = fp.D - c.z;
+    if (d > 0.2f) {
+        float k = (1.0f / d) * fp.F;
+        float px = k * c.x, py = k * c.y;
+        r.x = fp.Cx + fp.M2P * px;
+        r.y = fp.Cy + fp.M2P * py;
+        r.z = d + fp.M2P * 0.0f;
+    }
+    return r;
+}
+
+__device__ __forceinline__ V3 nrm_rcp(V3 a) {
+    normalize_rcp(a.x, a.y, a.z);
+    return a;
+}
+
+// Back-face test of FillEdgeTable (projekt.cpp:3926-3943):
+// Inner((0,0,-1), Cross(Normalize(P1-P0), Normalize(P2-P0))) > 0.
+__device__ __forceinline__ bool front_facing(const V3 *p) {
+    V3 a = nrm_rcp(V3{p[1].x - p[0].x, p[1].y - p[0].y, p[1].z - p[0].z});
+    V3 b = nrm_rcp(V3{p[2].x - p[0].x, p[2].y - p[0].y, p[2].z - p[0].z});
+    float cx = a.y * b.z - a.z * b.y;
+    float cy = a.z * b.x - a.x * b.z;
+    float cz = a.x * b.y - a.y * b.x;
+    float inner = (0.0f * cx + 0.0f * cy) + (-1.0f) * cz;
+    return inner > 0.0f;
+}
+
+struct TriVerts {
+    V3 cam[3], proj[3], nrm[3];
+    float col[3][4], uv[3][2];
+};
+
+__device__ __forceinline__ void resolve_draw(const FrameParams &fp, uint32_t g, const DrawRec *&d,
+                                             uint32_t &gt) {
+    uint32_t di = fp.ndraws == 1 ? 0u : fp.tri_draw[g];
+    d = fp.draws + di;
+    gt = d->geom_tri0 + (g - d->first_global);
+}
+
+// Camera + projected positions only (binning pass).
+__device__ __forceinline__ void load_positions(const DrawRec &d, uint32_t gt, const FrameParams &fp,
+                                               V3 *cam, V3 *proj) {
+    const float *v = d.V + 9 * (size_t)gt;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        cam[k] = V3{v[3 * k + 0] + d.P[0], v[3 * k + 1] + d.P[1], v[3 * k + 2] + d.P[2]};
+        proj[k] = project_vertex(cam[k], fp);
+    }
+}
+
+// FillEdgeTable (projekt.cpp:3882-4121) for ONE triangle followed by
+// MergeSort (2-72) of its <= 3 visible edges.  Returns the edge count.
+template <int M>
+__device__ __forceinline__ int setup_triangle(const DrawRec &d, uint32_t gt, const FrameParams &fp,
+                                              Edge &s0, Edge &s1, Edge &s2) {
+    using TR = ModeTraits<M>;
+    constexpr bool kTex = TR::tex;
+    constexpr bool kPhong = TR::phong;
+    constexpr bool kColor = TR::color;
+    V3 cam[3], proj[3];
+    load_positions(d, gt, fp, cam, proj);
+    if (!front_facing(proj)) return 0;
+
+    V3 nrm[3];
+    float col[3][4], uv[3][2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (kPhong) {
+            const float *n = d.N + 9 * (size_t)gt + 3 * k;
+            nrm[k] = V3{n[0], n[1], n[2]};
+        } else if (!kTex) {
+            const float *n = d.N + 9 * (size_t)gt + 3 * k;  // Gouraud lighting reads normals
+            nrm[k] = V3{n[0], n[1], n[2]};
+        } else {
+            nrm[k] = V3{0.0f, 0.0f, 0.0f};
+        }
+        if (kColor && d.C) {
+            const float *c = d.C + 12 * (size_t)gt + 4 * k;
+            col[k][0] = c[0]; col[k][1] = c[1]; col[k][2] = c[2]; col[k][3] = c[3];
+        } else {
+            col[k][0] = col[k][1] = col[k][2] = col[k][3] = 0.0f;
+        }
+        if (kTex) {
+            const float *u = d.UV + 6 * (size_t)gt + 2 * k;
+            uv[k][0] = u[0]; uv[k][1] = u[1];
+        } else {
+            uv[k][0] = uv[k][1] = 0.0f;
+        }
+    }
+
+    Edge e0, e1, e2;
+    bool vis[3];
+#pragma unroll
+    for (int ei = 0; ei < 3; ++ei) {
+        const int i0 = ei, i1 = (ei + 1) % 3;  // Indices {0,1},{1,2},{2,0}
+        const bool sw = proj[i0].y > proj[i1].y;  // 3957-3966
+        const int mi = sw ? i1 : i0, ma = sw ? i0 : i1;
+        V3 MinV = sw ? proj[i1] : proj[i0];
+        V3 MaxV = sw ? proj[i0] : proj[i1];
+        V3 FirstCam = sw ? cam[i1] : cam[i0];
+        V3 SecondCam = sw ? cam[i0] : cam[i1];
+        Edge E;
+        E.YMax = round_s32(MaxV.y);  // 3988
+        float ClippedY = 0.0f, t = 0.0f;
+        if (MinV.y < 0.0f) {  // 3993-3997
+            ClippedY = -MinV.y;
+            t = (-MinV.y) / (MaxV.y - MinV.y);
+        }
+        {
+            float r = (float)round_s32(MinV.y);
+            E.YMin = (int32_t)(0.0f > r ? 0.0f : r);  // Maximum(0, .) 3999
+        }
+        E.X = MinV.x;
+        E.Z = FirstCam.z;
+        E.U = E.V = E.W = E.UG = E.VG = E.WG = 0.0f;
+        E.N0 = E.N1 = E.N2 = E.NG0 = E.NG1 = E.NG2 = 0.0f;
+        E.C0 = E.C1 = E.C2 = E.C3 = E.CG0 = E.CG1 = E.CG2 = E.CG3 = 0.0f;
+        float FirstUV0 = 0, FirstUV1 = 0, SecondUV0 = 0, SecondUV1 = 0;
+        if (kTex) {
+            FirstUV0 = uv[mi][0]; FirstUV1 = uv[mi][1];
+            SecondUV0 = uv[ma][0]; SecondUV1 = uv[ma][1];
+            E.U = FirstUV0 / MinV.z;
+            E.V = FirstUV1 / MinV.z;
+            E.W = 1.0f / MinV.z;
+            float s2 = 1.0f / MaxV.z;  // 4010
+            SecondUV0 *= s2; SecondUV1 *= s2;
+            float s1 = 1.0f / MinV.z;  // 4012
+            FirstUV0 *= s1; FirstUV1 *= s1;
+        }
+        float MaxC[4] = {0, 0, 0, 0}, MinC[4] = {0, 0, 0, 0};
+        float MaxN[3] = {0, 0, 0};
+        if (kPhong) {  // 4014-4019
+            if (kColor) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) { MinC[c] = col[mi][c]; MaxC[c] = col[ma][c]; }
+            }
+            E.N0 = nrm[mi].x; E.N1 = nrm[mi].y; E.N2 = nrm[mi].z;
+            MaxN[0] = nrm[ma].x; MaxN[1] = nrm[ma].y; MaxN[2] = nrm[ma].z;
+        } else if (!kTex) {  // Gouraud vertex lighting 4020-4063 (untextured only reaches output)
+            for (uint32_t li = 0; li < fp.light_count; ++li) {
+                V3 LP = V3{fp.lp[li][0], fp.lp[li][1], fp.lp[li][2]};
+                V3 FVL = nrm_rcp(V3{LP.x - FirstCam.x, LP.y - FirstCam.y, LP.z - FirstCam.z});
+                V3 SVL = nrm_rcp(V3{LP.x - SecondCam.x, LP.y - SecondCam.y, LP.z - SecondCam.z});
+                if (li == 0) {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        MinC[c] = col[mi][c] * fp.amb[c];
+                        MaxC[c] = col[ma][c] * fp.amb[c];
+                    }
+                }
+                float FD = clamp01((FVL.x * nrm[mi].x + FVL.y * nrm[mi].y) + FVL.z * nrm[mi].z);
+                float SD = clamp01((SVL.x * nrm[ma].x + SVL.y * nrm[ma].y) + SVL.z * nrm[ma].z);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    MinC[c] = clamp01(MinC[c] + FD * (col[mi][c] * fp.li[li][c]));
+                    MaxC[c] = clamp01(MaxC[c] + SD * (col[ma][c] * fp.li[li][c]));
+                }
+            }
+        }
+        // Textured, non-Phong: the vertex colour is replaced by the texel in
+        // the span (projekt.cpp:445), so the lit colour never reaches output.
+        vis[ei] = (MaxV.y > 0) && (MinV.y - MaxV.y != 0);  // 3968, 4066
+        float YDiff = (float)E.YMax - (float)E.YMin;
+        E.ZG = (SecondCam.z - FirstCam.z) / YDiff;
+        E.G = (MaxV.x - MinV.x) / (MaxV.y - MinV.y);
+        E.X += ClippedY * E.G;
+        E.Z += ClippedY * E.ZG;
+        if (kTex) {  // 4078-4089
+            E.UG = (SecondUV0 - FirstUV0) / YDiff;
+            E.VG = (SecondUV1 - FirstUV1) / YDiff;
+            E.U += ClippedY * E.UG;
+            E.V += ClippedY * E.VG;
+            E.WG = ((1.0f / MaxV.z) - E.W) / YDiff;
+            E.W += ClippedY * E.WG;
+        }
+        if (kColor) {  // 4091, 4095-4101
+#pragma unroll
+            for (int c = 0; c < 4; ++c) MinC[c] = (1.0f - t) * MinC[c] + t * MaxC[c];
+            E.C0 = MinC[0]; E.C1 = MinC[1]; E.C2 = MinC[2]; E.C3 = MinC[3];
+            E.CG0 = (MaxC[0] - MinC[0]) / YDiff;
+            E.CG1 = (MaxC[1] - MinC[1]) / YDiff;
+            E.CG2 = (MaxC[2] - MinC[2]) / YDiff;
+            E.CG3 = (MaxC[3] - MinC[3]) / YDiff;
+        }
+        if (kPhong) {  // 4103-4108
+            E.NG0 = (MaxN[0] - E.N0) / YDiff;
+            E.NG1 = (MaxN[1] - E.N1) / YDiff;
+            E.NG2 = (MaxN[2] - E.N2) / YDiff;
+        }
+        E.Left = (E.YMin == round_s32(proj[i0].y)) ? 1 : 0;  // 4093
+        if (ei == 0) e0 = E; else if (ei == 1) e1 = E; else e2 = E;
+    }
+    // Compact visible edges in edge order, then MergeSort (projekt.cpp:2-72).
+    const int n = (int)vis[0] + (int)vis[1] + (int)vis[2];
+    const Edge a0 = sel(vis[0], e0, sel(vis[1], e1, e2));
+    const Edge a1 = sel(vis[0] && vis[1], e1, e2);
+    const Edge &a2 = e2;
+    // n == 2: swap if YMin descending.  n == 3: Half0 = [a0],
+    // Half1 = sort2([a1, a2]); the merge takes Half0 only on strict '<'.
+    const bool sw12 = a1.YMin > a2.YMin;
+    const Edge b1 = sel(sw12, a2, a1), b2 = sel(sw12, a1, a2);
+    const bool two_sw = a0.YMin > a1.YMin;
+    const bool h0_first = a0.YMin < b1.YMin;   // n == 3: a0 leads
+    const bool h0_second = a0.YMin < b2.YMin;  // n == 3, b1 leads: a0 second?
+    if (n == 3) {
+        s0 = sel(h0_first, a0, b1);
+        s1 = sel(h0_first, b1, sel(h0_second, a0, b2));
+        s2 = sel(h0_first, b2, sel(h0_second, b2, a0));
+    } else {
+        s0 = sel(n == 2 && two_sw, a1, a0);
+        s1 = sel(two_sw, a0, a1);
+        s2 = a2;
+    }
+    return n;
+}
+
+// AET edge step (projekt.cpp:3811-3829), only the fields mode M reads.
+template <int M>
+__device__ __forceinline__ void step_edge(Edge &E) {
+    using TR = ModeTraits<M>;
+    E.X += E.G;
+    E.Z += E.ZG;
+    if (TR::color) { E.C0 += E.CG0; E.C1 += E.CG1; E.C2 += E.CG2; E.C3 += E.CG3; }
+    if (TR::phong) {
+        float x = E.N0 + E.NG0, y = E.N1 + E.NG1, z = E.N2 + E.NG2;
+        normalize_rcp(x, y, z);
+        E.N0 = x; E.N1 = y; E.N2 = z;
+    }
+    if (TR::tex) { E.U += E.UG; E.V += E.VG; E.W += E.WG; }
+}
+
+// AET insertion order (projekt.cpp:3663-3667).
+__device__ __forceinline__ bool insert_before(const Edge &A, const Edge &B) {
+    return A.X < B.X || (A.X == B.X && (A.G < B.G || (A.G == B.G && A.Left < B.Left)));
+}
+
+// Per-triangle active edge table (DrawModelOptimized(RenderQueue,...),
+// projekt.cpp:3615-3871, with the P3 head/tail fix; DrawModel's AET
+// 168-598 is the same list logic).  The list is held in slots L0..L2 in list
+// order; `src` are the sorted setup edges.  For each row the walker calls
+// span(L, R, row) for the pair, exactly as the reference enqueues it.
+template <int M, typename SpanFn>
+__device__ __forceinline__ void aet_walk(int n, Edge s0, Edge s1, Edge s2, int32_t H,
+                                         int32_t row_begin, int32_t row_end, SpanFn &&span) {
+    if (n <= 0) return;
+    int32_t FirstRow = s0.YMin;
+    int32_t MaxRow = s0.YMax;
+    if (n > 1 && MaxRow < s1.YMax) MaxRow = s1.YMax;
+    if (n > 2 && MaxRow < s2.YMax) MaxRow = s2.YMax;
+    int32_t MaxY = MaxRow;
+    if (MaxY > H) MaxY = H;
+    if (MaxY > row_end) MaxY = row_end;
+    Edge L0 = s0, L1 = s0, L2 = s0;
+    int cnt = 0;
+    // Edges not yet inserted, in sorted-array order.
+    bool pend0 = true, pend1 = n > 1, pend2 = n > 2;
+    for (int32_t Row = FirstRow; Row < MaxY; ++Row) {
+        // Insertion (3654-3713): in array order, each before the first list
+        // entry it sorts before, else at the tail.
+        auto insert = [&](const Edge Ek) {
+            int pos = cnt;
+            if (cnt > 1 && insert_before(Ek, L1)) pos = 1;
+            if (cnt > 0 && insert_before(Ek, L0)) pos = 0;
+            L2 = sel(pos <= 1 && cnt >= 2, L1, sel(pos == 2, Ek, L2));
+            L1 = sel(pos == 0 && cnt >= 1, L0, sel(pos == 1, Ek, L1));
+            L0 = sel(pos == 0, Ek, L0);
+            ++cnt;
+        };
+        if (pend0 && s0.YMin == Row) { pend0 = false; insert(s0); }
+        if (pend1 && s1.YMin == Row) { pend1 = false; insert(s1); }
+        if (pend2 && s2.YMin == Row) { pend2 = false; insert(s2); }
+        // Expiry (3715-3749): drop every entry with YMax <= Row, keep order.
+        {
+            const bool k0 = cnt > 0 && !(L0.YMax <= Row);
+            const bool k1 = cnt > 1 && !(L1.YMax <= Row);
+            const bool k2 = cnt > 2 && !(L2.YMax <= Row);
+            const Edge n0 = sel(k0, L0, sel(k1, L1, L2));
+            const Edge n1 = sel(k0 && k1, L1, L2);
+            L0 = n0;
+            L1 = n1;
+            cnt = (int)k0 + (int)k1 + (int)k2;
+        }
+        if (cnt >= 2) {
+            // Pairing (3751-3869): one pair (L0, L1); with three entries the
+            // third is left unpaired and unstepped, as in the reference.
+            if (Row >= row_begin) span(L0, L1, Row);
+            step_edge<M>(L0);
+            step_edge<M>(L1);
+            const bool swp = L0.X > L1.X;  // 3831-3841 (+P3)
+            const Edge t0 = sel(swp, L1, L0);
+            L1 = sel(swp, L0, L1);
+            L0 = t0;
+        }
+    }
+}
+
+}  // namespace prk

@@ -1,0 +1,272 @@
+"""prk — Python binding of libprk_hip.so (the MI355X rasterizer C-ABI).
+
+Mirrors the reference's draw interface (projekt.cpp, MacSpain/cpu-renderer):
+
+    reference                                   here
+    ------------------------------------------  ---------------------------------
+    FillEdgeTable(Object, Commands, Phong)      Renderer.draw_* record the object
+    DrawModelOptimized(Queue, Buffer, Edges,    Renderer.draw_model_optimized()
+        EdgeCount, Commands, Bitmap, Phong)     (FillLineOptimized semantics)
+    DrawModel(Buffer, Edges, EdgeCount,         Renderer.draw_model()
+        Commands, Bitmap, Phong)                (scalar DrawModel semantics)
+    Platform.CompleteAllWork(Queue)             Renderer.complete_all_work()
+
+The HIP library is the only compute path: there is no CPU fallback, and every
+entry point raises PrkError if libprk_hip.so or the GPU is missing.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+from .abi import PRK_SEM_AVX, PRK_SEM_SCALAR  # noqa: F401
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libprk_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "prk.h")
+
+_LIB = None
+
+
+class PrkError(RuntimeError):
+    def __init__(self, fn, code):
+        super().__init__("%s failed: %s (%d)" % (fn, abi.STATUS_NAMES.get(code, "?"), code))
+        self.code = code
+
+
+_SIGS = {
+    "prk_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "prk_destroy": (C.c_int, [C.c_void_p]),
+    "prk_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "prk_version": (C.c_char_p, []),
+    "prk_target_bind": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_int32,
+                                  C.c_int32, C.c_int32]),
+    "prk_target_alloc": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                   C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
+    "prk_target_clear": (C.c_int, [C.c_void_p, C.c_uint32, C.c_float]),
+    "prk_target_download": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
+    "prk_target_upload": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
+    "prk_set_camera": (C.c_int, [C.c_void_p, C.POINTER(abi.PrkTransform), C.POINTER(abi.PrkLightData)]),
+    "prk_texture_create": (C.c_int, [C.c_void_p, C.POINTER(abi.PrkBitmap), C.POINTER(C.c_int32)]),
+    "prk_geometry_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_uint32, C.POINTER(C.c_int32)]),
+    "prk_geometry_wrap_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.c_uint32, C.POINTER(C.c_int32)]),
+    "prk_draw": (C.c_int, [C.c_void_p, C.c_int32, C.c_uint32, C.c_uint32, C.POINTER(C.c_float),
+                           C.c_int32, C.c_int32, C.c_int32]),
+    "prk_flush": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "prk_reset_draws": (C.c_int, [C.c_void_p]),
+    "prk_synchronize": (C.c_int, [C.c_void_p]),
+    "prk_get_stats": (C.c_int, [C.c_void_p, C.POINTER(abi.PrkStats)]),
+    "prk_set_debug": (C.c_int, [C.c_void_p, C.c_int32]),
+    "prk_download_winners": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "prk_set_tile": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+    "prk_construct_sphere": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.POINTER(C.c_uint32)]),
+}
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def lib(path=None):
+    """Load libprk_hip.so (fails loudly if it has not been built)."""
+    global _LIB
+    if _LIB is None:
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise PrkError("load libprk_hip.so (%s: not built; run __graft_entry__.build())" % p, -3)
+        L = C.CDLL(p)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def _check(fn, rc):
+    if rc != abi.PRK_OK:
+        raise PrkError(fn, rc)
+
+
+def _ptr(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def device_count():
+    n = C.c_int(0)
+    _check("prk_device_count", lib().prk_device_count(C.byref(n)))
+    return n.value
+
+
+def construct_sphere():
+    """ConstructSphere (projekt.cpp:4123-4289) -> (V[6624,3], C[6624,4], N[6624,3], UV[6624,2])."""
+    V = np.zeros((6624, 3), np.float32)
+    Cc = np.zeros((6624, 4), np.float32)
+    N = np.zeros((6624, 3), np.float32)
+    UV = np.zeros((6624, 2), np.float32)
+    n = C.c_uint32(0)
+    _check("prk_construct_sphere", lib().prk_construct_sphere(_ptr(V), _ptr(Cc), _ptr(N), _ptr(UV),
+                                                               C.byref(n)))
+    return V[: n.value], Cc[: n.value], N[: n.value], UV[: n.value]
+
+
+class Renderer:
+    """One GPU context: render target, camera/lights, resident geometry and
+    textures, and the list of recorded draws of the current frame."""
+
+    def __init__(self, device=0):
+        self._L = lib()
+        h = C.c_void_p()
+        _check("prk_create", self._L.prk_create(int(device), C.byref(h)))
+        self._h = h
+        self._keep = []
+        self.width = self.height = self.row0 = self.row1 = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.prk_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- target -----------------------------------------------------------
+    def target_alloc(self, width, height, row0=0, row1=None):
+        row1 = height if row1 is None else row1
+        _check("prk_target_alloc", self._L.prk_target_alloc(self._h, width, height, row0, row1, None, None))
+        self.width, self.height, self.row0, self.row1 = width, height, row0, row1
+
+    def target_bind(self, color_ptr, pitch_bytes, z_ptr, width, height, row0=0, row1=None):
+        """Bind caller-owned device memory (e.g. torch tensors' data_ptr())."""
+        row1 = height if row1 is None else row1
+        _check("prk_target_bind", self._L.prk_target_bind(self._h, C.c_void_p(color_ptr), pitch_bytes,
+                                                          C.c_void_p(z_ptr), width, height, row0, row1))
+        self.width, self.height, self.row0, self.row1 = width, height, row0, row1
+
+    def clear(self, color=0xFF000000, z=None):
+        z = -float(np.finfo(np.float32).max) if z is None else z
+        _check("prk_target_clear", self._L.prk_target_clear(self._h, C.c_uint32(color), C.c_float(z)))
+
+    def upload(self, color, z):
+        color = np.ascontiguousarray(color, np.uint32)
+        z = np.ascontiguousarray(z, np.float32)
+        _check("prk_target_upload", self._L.prk_target_upload(self._h, _ptr(color), self.width * 4, _ptr(z)))
+
+    def download(self):
+        rows = self.row1 - self.row0
+        color = np.empty((rows, self.width), np.uint32)
+        z = np.empty((rows, self.width), np.float32)
+        _check("prk_target_download", self._L.prk_target_download(self._h, _ptr(color), self.width * 4,
+                                                                  _ptr(z)))
+        return color, z
+
+    def winners(self):
+        rows = self.row1 - self.row0
+        w = np.empty((rows, self.width), np.int32)
+        _check("prk_download_winners", self._L.prk_download_winners(self._h, _ptr(w)))
+        return w
+
+    # ---- state ------------------------------------------------------------
+    def set_camera(self, transform, lights):
+        self._cam = (transform, lights)
+        _check("prk_set_camera", self._L.prk_set_camera(self._h, C.byref(transform), C.byref(lights)))
+
+    def texture(self, tex):
+        """tex: scenes.Texture (uint32 texels with the zeroed guard row)."""
+        texels = np.ascontiguousarray(tex.texels, np.uint32)
+        bm = abi.PrkBitmap(texels.ctypes.data, tex.width, tex.height, texels.shape[1] * 4)
+        h = C.c_int32(-1)
+        _check("prk_texture_create", self._L.prk_texture_create(self._h, C.byref(bm), C.byref(h)))
+        return h.value
+
+    def geometry(self, vertices, colors=None, normals=None, uvs=None):
+        arrs = [None if a is None else np.ascontiguousarray(a, np.float32)
+                for a in (vertices, colors, normals, uvs)]
+        h = C.c_int32(-1)
+        nv = arrs[0].shape[0]
+        _check("prk_geometry_create", self._L.prk_geometry_create(self._h, *[_ptr(a) for a in arrs],
+                                                                  nv, C.byref(h)))
+        return h.value
+
+    def geometry_device(self, v_ptr, c_ptr, n_ptr, uv_ptr, vertex_count):
+        h = C.c_int32(-1)
+        ptrs = [C.c_void_p(p) if p else None for p in (v_ptr, c_ptr, n_ptr, uv_ptr)]
+        _check("prk_geometry_wrap_device", self._L.prk_geometry_wrap_device(self._h, *ptrs, vertex_count,
+                                                                            C.byref(h)))
+        return h.value
+
+    def set_tile(self, tw, th):
+        _check("prk_set_tile", self._L.prk_set_tile(self._h, tw, th))
+
+    def set_debug(self, on=True):
+        _check("prk_set_debug", self._L.prk_set_debug(self._h, int(bool(on))))
+
+    # ---- draws (the reference's entry points) -----------------------------
+    def _draw(self, geom, first_tri, tri_count, P, semantics, phong, texture):
+        Pc = (C.c_float * 3)(*(P or (0.0, 0.0, 0.0)))
+        _check("prk_draw", self._L.prk_draw(self._h, geom, first_tri, tri_count, Pc, semantics,
+                                            int(bool(phong)), -1 if texture is None else texture))
+
+    def draw_model_optimized(self, geom, tri_count, first_tri=0, P=None, bitmap=None, phong=True):
+        """DrawModelOptimized(RenderQueue, ...) -> FillLineOptimized semantics
+        (projekt.cpp:3615-3871, 1492-2320).  Needs bitmap + phong."""
+        self._draw(geom, first_tri, tri_count, P, abi.PRK_SEM_AVX, phong, bitmap)
+
+    def draw_model(self, geom, tri_count, first_tri=0, P=None, bitmap=None, phong=False):
+        """DrawModel (projekt.cpp:162-601) scalar semantics."""
+        self._draw(geom, first_tri, tri_count, P, abi.PRK_SEM_SCALAR, phong, bitmap)
+
+    def complete_all_work(self, stream=None):
+        """Platform.CompleteAllWork: run every recorded draw (asynchronous)."""
+        _check("prk_flush", self._L.prk_flush(self._h, None if stream is None else C.c_void_p(stream)))
+
+    flush = complete_all_work
+
+    def reset_draws(self):
+        _check("prk_reset_draws", self._L.prk_reset_draws(self._h))
+
+    def synchronize(self):
+        _check("prk_synchronize", self._L.prk_synchronize(self._h))
+
+    def stats(self):
+        s = abi.PrkStats()
+        _check("prk_get_stats", self._L.prk_get_stats(self._h, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in abi.PrkStats._fields_}
+
+
+def render_scene(scene, semantics=abi.PRK_SEM_AVX, phong=True, device=0, tile=None, debug=True,
+                 color=None, z=None, rows=None):
+    """Convenience: draw a whole scenes.Scene (per-triangle submission) and
+    return (color, z, winners or None, stats)."""
+    r = Renderer(device)
+    try:
+        r0, r1 = (0, scene.height) if rows is None else rows
+        r.target_alloc(scene.width, scene.height, r0, r1)
+        if color is None and z is None:
+            r.clear()
+        else:
+            r.upload(color[r0:r1], z[r0:r1])
+        if tile:
+            r.set_tile(*tile)
+        r.set_debug(debug)
+        r.set_camera(scene.prk_transform(), scene.prk_lights())
+        g = r.geometry(scene.vertices, scene.colors, scene.normals, scene.uvs)
+        tex = r.texture(scene.texture) if scene.texture is not None else None
+        if semantics == abi.PRK_SEM_AVX:
+            r.draw_model_optimized(g, scene.tri_count, P=scene.P, bitmap=tex, phong=phong)
+        else:
+            r.draw_model(g, scene.tri_count, P=scene.P, bitmap=tex, phong=phong)
+        r.complete_all_work()
+        r.synchronize()
+        col, zb = r.download()
+        win = r.winners() if debug else None
+        return col, zb, win, r.stats()
+    finally:
+        r.close()

@@ -1,0 +1,180 @@
+/*
+ * prk.h — C-ABI of the MI355X-native rasterizer (libprk_hip.so).
+ *
+ * This is the drop-in boundary for the reference's ONE hot path:
+ *
+ *     FillEdgeTable            projekt.cpp:3882-4121   (triangle setup)
+ *     DrawModelOptimized(Queue) projekt.cpp:3615-3871  (AET walk, per-span tasks)
+ *       -> FillLineOptimized   projekt.cpp:1492-2320   (8-px AVX span kernel)
+ *     DrawModel                projekt.cpp:162-601     (scalar span kernel)
+ *     Platform.CompleteAllWork (absent platform layer, inferred from
+ *                               projekt.cpp:3609,3809)
+ *
+ * The reference exports nothing (every function is `internal`), so the
+ * boundary is the set of C++ signatures above plus the caller-owned types
+ * they take.  `include/projekt.h` re-declares those C++ signatures and
+ * forwards them to the plain-C entry points below.  Signatures here use only
+ * plain pointers, sizes and POD structs; no torch or HIP types.
+ *
+ * Every prk_* function returns an int status (PRK_OK == 0, negative on
+ * error) — the reference has no error convention at all (Assert only,
+ * projekt.cpp:2327), and crashes on several ordinary inputs;
+ * here those inputs are rejected with a status code instead.
+ *
+ * Semantics: every triangle is its own AET, submitted in index
+ * order and sharing one z-buffer ("per-triangle submission").
+ */
+#ifndef PRK_H
+#define PRK_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PRK_MAX_LIGHTS 8
+
+enum prk_status {
+    PRK_OK = 0,
+    PRK_ERR_ARG = -1,          /* bad pointer / size / handle            */
+    PRK_ERR_UNSUPPORTED = -2,  /* combination the reference leaves undefined */
+    PRK_ERR_DEVICE = -3,       /* HIP runtime error                      */
+    PRK_ERR_NOMEM = -4,        /* device allocation failed               */
+    PRK_ERR_NO_TARGET = -5     /* flush without a render target          */
+};
+
+/* Which of the reference's span kernels a draw reproduces. */
+enum prk_semantics {
+    PRK_SEM_SCALAR = 0,  /* DrawModel            projekt.cpp:162-601   */
+    PRK_SEM_AVX = 1      /* FillLineOptimized    projekt.cpp:1492-2320, driven by
+                            DrawModelOptimized(RenderQueue,...) 3615-3871 */
+};
+
+/* projective_transform (absent header; fields as used at projekt.cpp:77-90,
+ * 122-141, 152-155). */
+typedef struct prk_transform {
+    float DistanceAboveTarget;
+    float FocalLength;
+    float MetersToPixels;
+    float ScreenCenter[2];
+} prk_transform;
+
+/* light_info / light_data (absent header; projekt.cpp:452-484, 2046-2128,
+ * 3885, 4025-4061). */
+typedef struct prk_light_info {
+    float P[3];
+    float Intensity[4]; /* r g b a */
+} prk_light_info;
+
+typedef struct prk_light_data {
+    uint32_t LightCount;
+    float AmbientIntensity[4]; /* r g b a */
+    prk_light_info Lights[PRK_MAX_LIGHTS];
+} prk_light_data;
+
+/* loaded_bitmap (absent header): 0xAARRGGBB texels, Pitch in bytes.  For a
+ * texture, Memory must hold Height+1 rows: the extra zeroed "guard" row is
+ * what the reference's u==1 / v==1 over-read lands on. */
+typedef struct prk_bitmap {
+    void *Memory;
+    int32_t Width;
+    int32_t Height;
+    int32_t Pitch;
+} prk_bitmap;
+
+/* Frame statistics of the last prk_flush. */
+typedef struct prk_stats {
+    uint64_t triangles;      /* triangles submitted                    */
+    uint64_t bin_entries;    /* (triangle, tile) pairs rasterised      */
+    uint32_t tiles;          /* tiles in the render target band        */
+    uint32_t max_bin;        /* largest per-tile bin                   */
+    float ms_bin;            /* device time: project/cull/bin          */
+    float ms_raster;         /* device time: tile raster+shade kernel  */
+    float ms_total;          /* device time: whole flush               */
+} prk_stats;
+
+typedef struct prk_context prk_context;
+
+/* Library / device lifetime. */
+int prk_create(int device, prk_context **out);
+int prk_destroy(prk_context *ctx);
+int prk_device_count(int *out);
+const char *prk_version(void);
+
+/* Render target: device memory owned by the caller (e.g. a torch tensor) or
+ * by the library (prk_target_alloc).  The target covers frame rows
+ * [row0, row1) of a frame `height` rows tall; `color` and `zbuf` point at
+ * frame row row0.  z-buffer row stride is `width` floats (Commands->Width,
+ * projekt.cpp:170,1511); colour row stride is `pitch_bytes`.
+ * A target for the AVX semantics needs width % 8 == 0 (the reference's
+ * aligned 8-wide z load, projekt.cpp:2218). */
+int prk_target_bind(prk_context *ctx, void *color, int32_t pitch_bytes, float *zbuf,
+                    int32_t width, int32_t height, int32_t row0, int32_t row1);
+int prk_target_alloc(prk_context *ctx, int32_t width, int32_t height, int32_t row0,
+                     int32_t row1, void **color_out, float **zbuf_out);
+/* Fill the bound target: colour with `color`, z with `z` (reference callers
+ * clear z to -FLT_MAX). */
+int prk_target_clear(prk_context *ctx, uint32_t color, float z);
+/* Copy the bound target to/from host memory (rows [row0,row1)). */
+int prk_target_download(prk_context *ctx, uint32_t *color_host, int32_t host_pitch_bytes,
+                        float *z_host);
+int prk_target_upload(prk_context *ctx, const uint32_t *color_host, int32_t host_pitch_bytes,
+                      const float *z_host);
+
+/* Camera and lights (game_render_commands::Transform / LightData). */
+int prk_set_camera(prk_context *ctx, const prk_transform *transform,
+                   const prk_light_data *lights);
+
+/* Textures.  `bitmap->Memory` is host memory of (Height+1)*Pitch bytes, the
+ * last row being the guard row (zero it).  Returns a handle >= 0. */
+int prk_texture_create(prk_context *ctx, const prk_bitmap *bitmap, int32_t *handle_out);
+
+/* Geometry: non-indexed SoA vertex arrays exactly as render_entry_3d_object
+ * (projekt.h:2-15): positions v3, colours v4, normals v3, uvs v2, three
+ * vertices per triangle.  Copied to HBM once; a draw references a range. */
+int prk_geometry_create(prk_context *ctx, const float *vertices, const float *colors,
+                        const float *normals, const float *uvs, uint32_t vertex_count,
+                        int32_t *handle_out);
+/* Same, but from device pointers the caller keeps alive (no copy). */
+int prk_geometry_wrap_device(prk_context *ctx, const float *vertices, const float *colors,
+                             const float *normals, const float *uvs, uint32_t vertex_count,
+                             int32_t *handle_out);
+
+/* Record one draw: triangles [first_tri, first_tri+tri_count) of a geometry,
+ * object offset P (render_entry_3d_object::P), semantics PRK_SEM_*,
+ * PhongShading flag, texture handle (-1 = no Bitmap).
+ * PRK_SEM_AVX requires a texture and PhongShading != 0: the reference
+ * dereferences Bitmap unconditionally (projekt.cpp:1506) and its non-Phong
+ * branch writes garbage (projekt.cpp:2285-2316). */
+int prk_draw(prk_context *ctx, int32_t geometry, uint32_t first_tri, uint32_t tri_count,
+             const float P[3], int32_t semantics, int32_t phong, int32_t texture);
+
+/* Execute every recorded draw, in submission order, into the bound target
+ * (the reference's Platform.CompleteAllWork).  `stream` is a hipStream_t or
+ * NULL for the library's own stream.  Asynchronous w.r.t. the host. */
+int prk_flush(prk_context *ctx, void *stream);
+/* Drop recorded draws without executing them. */
+int prk_reset_draws(prk_context *ctx);
+int prk_synchronize(prk_context *ctx);
+int prk_get_stats(prk_context *ctx, prk_stats *out);
+
+/* Debug/test: per-pixel winning triangle index of the last flush (-1 = none),
+ * rows [row0,row1).  Requires prk_set_debug(ctx, 1) before the flush. */
+int prk_set_debug(prk_context *ctx, int32_t enable);
+int prk_download_winners(prk_context *ctx, int32_t *winners_host);
+
+/* Tunables (testing / benchmarking). tile_w must be a multiple of 8. */
+int prk_set_tile(prk_context *ctx, int32_t tile_w, int32_t tile_h);
+
+/* Host utility: the reference's test mesh, ConstructSphere
+ * (projekt.cpp:4123-4289).  Arrays must hold 6624 vertices; returns the
+ * vertex count through *count_out. */
+int prk_construct_sphere(float *vertices, float *colors, float *normals, float *uvs,
+                         uint32_t *count_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PRK_H */

@@ -1,0 +1,140 @@
+"""ctypes loader for liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module, and only as the checker / the timed CPU baseline.  The product
+path (cpu-renderer_amd/prk, libprk_hip.so) never imports it.
+
+PARITY UNPINNED: see the header of oracle/prk_oracle.c and DESIGN.md §3.
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(_HERE), "cpu-renderer_amd"))
+from prk import abi  # noqa: E402
+from prk.scenes import CLEAR_COLOR, CLEAR_Z  # noqa: E402
+
+_LIB = None
+
+
+class OrDrawDesc(C.Structure):
+    _fields_ = [("Vertices", C.c_void_p), ("Colors", C.c_void_p), ("Normals", C.c_void_p),
+                ("UVs", C.c_void_p), ("TriCount", C.c_uint32), ("TrisPerObject", C.c_uint32),
+                ("P", C.c_float * 3), ("Semantics", C.c_int32), ("Phong", C.c_int32),
+                ("Bitmap", C.POINTER(abi.PrkBitmap)), ("TriIndexBase", C.c_int32)]
+
+
+class OrTarget(C.Structure):
+    _fields_ = [("Color", C.c_void_p), ("Pitch", C.c_int32), ("Z", C.c_void_p),
+                ("Width", C.c_int32), ("Height", C.c_int32), ("Winners", C.c_void_p)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        _LIB = C.CDLL(path)
+        for fn in ("oracle_draw", "oracle_draw_band", "oracle_draw_mt",
+                   "oracle_fill_edge_table"):
+            getattr(_LIB, fn).restype = C.c_int
+    return _LIB
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class _Keep:
+    """Holds ctypes objects alive for the duration of a call."""
+
+    def __init__(self, scene, semantics, phong, tris_per_object, tri_base=0):
+        self.arrays = [np.ascontiguousarray(scene.vertices, np.float32),
+                       np.ascontiguousarray(scene.colors, np.float32),
+                       np.ascontiguousarray(scene.normals, np.float32),
+                       np.ascontiguousarray(scene.uvs, np.float32)]
+        self.bitmap = None
+        if scene.texture is not None:
+            self.tex = np.ascontiguousarray(scene.texture.texels)
+            self.bitmap = abi.PrkBitmap(self.tex.ctypes.data_as(C.c_void_p).value,
+                                        scene.texture.width, scene.texture.height,
+                                        scene.texture.pitch)
+        d = OrDrawDesc()
+        d.Vertices, d.Colors, d.Normals, d.UVs = [_ptr(a) for a in self.arrays]
+        d.TriCount = scene.tri_count
+        d.TrisPerObject = tris_per_object
+        for i in range(3):
+            d.P[i] = scene.P[i]
+        d.Semantics = semantics
+        d.Phong = int(bool(phong))
+        d.Bitmap = C.pointer(self.bitmap) if self.bitmap is not None else None
+        d.TriIndexBase = tri_base
+        self.desc = d
+        self.transform = scene.prk_transform()
+        self.lights = scene.prk_lights()
+
+
+def render(scene, semantics=abi.PRK_SEM_AVX, phong=True, tris_per_object=1, threads=1,
+           color=None, z=None, winners=True, rows=None):
+    """Draw `scene` with the oracle.  Returns (color u32[H,W], z f32[H,W],
+    winners i32[H,W] or None, stats dict).  `color`/`z` (optional) are the
+    prior target contents (default: reference clear values)."""
+    W, H = scene.width, scene.height
+    col = np.full((H, W), CLEAR_COLOR, np.uint32) if color is None else np.array(color, np.uint32)
+    zb = np.full((H, W), CLEAR_Z, np.float32) if z is None else np.array(z, np.float32)
+    win = np.full((H, W), -1, np.int32) if winners else None
+    k = _Keep(scene, semantics, phong, tris_per_object)
+    tg = OrTarget(_ptr(col), W * 4, _ptr(zb), W, H, _ptr(win))
+    stats = (C.c_uint64 * 3)()
+    L = lib()
+    if rows is not None:
+        rc = L.oracle_draw_band(C.byref(k.desc), C.byref(tg), C.byref(k.transform),
+                                C.byref(k.lights), int(rows[0]), int(rows[1]), stats)
+    elif threads > 1:
+        rc = L.oracle_draw_mt(C.byref(k.desc), C.byref(tg), C.byref(k.transform),
+                              C.byref(k.lights), int(threads), stats)
+    else:
+        rc = L.oracle_draw(C.byref(k.desc), C.byref(tg), C.byref(k.transform),
+                           C.byref(k.lights), stats)
+    if rc != 0:
+        raise RuntimeError("oracle failed: %s" % abi.STATUS_NAMES.get(rc, rc))
+    return col, zb, win, dict(spans=stats[0], span_pixels=stats[1], writes=stats[2])
+
+
+EDGE_FIELDS = ["YMax", "XMin", "ZMin", "OneOverZMin", "Gradient", "ZGradient",
+               "OneOverZGradient", "YMin", "UMin", "VMin", "UGradient", "VGradient", "Left",
+               "MinColor", "ColorGradient", "MinNormal", "NormalGradient"]
+
+
+def fill_edge_table(scene, tri0=0, n=1, phong=True, semantics=abi.PRK_SEM_AVX):
+    """FillEdgeTable (projekt.cpp:3882-4121) on triangles [tri0, tri0+n) as one
+    object; returns the sorted edge list as dicts."""
+    k = _Keep(scene, semantics, phong, n)
+    words = np.zeros(27 * 3 * n, np.uint32)
+    cnt = C.c_uint32(0)
+    rc = lib().oracle_fill_edge_table(C.byref(k.desc), C.c_uint32(tri0), C.c_uint32(n),
+                                      C.byref(k.transform), C.byref(k.lights),
+                                      _ptr(words), C.byref(cnt))
+    if rc != 0:
+        raise RuntimeError("oracle_fill_edge_table failed: %d" % rc)
+    out = []
+    w = words.reshape(-1, 27)[: cnt.value]
+    f = w.view(np.float32)
+    i32 = w.view(np.int32)
+    for r in range(cnt.value):
+        out.append(dict(YMax=int(i32[r, 0]), XMin=f[r, 1], ZMin=f[r, 2], OneOverZMin=f[r, 3],
+                        Gradient=f[r, 4], ZGradient=f[r, 5], OneOverZGradient=f[r, 6],
+                        YMin=int(i32[r, 7]), UMin=f[r, 8], VMin=f[r, 9], UGradient=f[r, 10],
+                        VGradient=f[r, 11], Left=int(i32[r, 12]), MinColor=f[r, 13:17].copy(),
+                        ColorGradient=f[r, 17:21].copy(), MinNormal=f[r, 21:24].copy(),
+                        NormalGradient=f[r, 24:27].copy()))
+    return out

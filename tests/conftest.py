@@ -1,0 +1,30 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "cpu-renderer_amd"), os.path.join(ROOT, "oracle"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libprk_hip.so on the device)")
+
+
+def gpu_available():
+    try:
+        import prk
+        return prk.device_count() > 0
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    import prk
+    n = prk.device_count()  # raises if libprk_hip.so is missing: the HIP path must load
+    if n <= 0:
+        pytest.fail("gpu-marked test but no HIP device visible")
+    return n

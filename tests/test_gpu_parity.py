@@ -1,0 +1,196 @@
+"""GPU parity: libprk_hip.so on an MI355X vs the CPU restatement (oracle/).
+
+Bar (BASELINE.json north_star): z-buffer bit-exact, winning-triangle map
+bit-exact, RGBA within +-1 LSB per channel.  The kernels replay the
+reference's float recurrences op for op, so colours are expected to be exact
+as well; `COLOR_TOL` is the contract, exact equality is additionally checked
+where every colour op is IEEE-exact (all but the scalar path's double pow).
+
+Oracle parity is UNPINNED: the reference cannot be built here.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import prk
+from prk import abi, scenes
+
+pytestmark = pytest.mark.gpu
+
+COLOR_TOL = 1  # LSB per channel (north_star)
+
+
+def channel_diff(a, b):
+    a = a.view(np.uint8).reshape(a.shape + (4,)).astype(np.int16)
+    b = b.view(np.uint8).reshape(b.shape + (4,)).astype(np.int16)
+    return np.abs(a - b).max(-1)
+
+
+def compare(g, o, exact_color=True, label=""):
+    gc, gz, gw, _ = g
+    oc, oz, ow, _ = o
+    zbad = gz.view(np.uint32) != oz.view(np.uint32)
+    wbad = gw != ow
+    cd = channel_diff(gc, oc)
+    msg = "%s: z mismatches %d, winner mismatches %d, colour >%d LSB %d, colour inexact %d" % (
+        label, zbad.sum(), wbad.sum(), COLOR_TOL, (cd > COLOR_TOL).sum(), (cd > 0).sum())
+    if zbad.any():
+        ys, xs = np.nonzero(zbad)
+        msg += "; first z diff at (%d,%d) gpu=%r ora=%r gw=%d ow=%d" % (
+            ys[0], xs[0], gz[ys[0], xs[0]], oz[ys[0], xs[0]], gw[ys[0], xs[0]], ow[ys[0], xs[0]])
+    assert not zbad.any() and not wbad.any() and not (cd > COLOR_TOL).any(), msg
+    if exact_color:
+        assert not (cd > 0).any(), msg
+
+
+def run_both(scene, semantics=abi.PRK_SEM_AVX, phong=True, tile=None, threads=8, exact_color=True,
+             label=""):
+    o = O.render(scene, semantics=semantics, phong=phong, threads=threads)
+    g = prk.render_scene(scene, semantics=semantics, phong=phong, tile=tile)
+    compare(g, o, exact_color=exact_color, label=label or scene.name)
+    return g, o
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_avx_soup_256(gpu, seed):
+    run_both(scenes.random_soup(2000, 256, 256, radius=16, seed=seed))
+
+
+def test_avx_soup_512_20k(gpu):
+    g, o = run_both(scenes.random_soup(20000, 512, 512, radius=16, seed=7))
+    assert (g[2] >= 0).sum() > 100000  # the scene actually covers the screen
+
+
+def test_avx_two_lights_r40(gpu):
+    run_both(scenes.random_soup(20000, 512, 512, radius=40, seed=3, lights=scenes.LIGHTS_TWO,
+                                ambient=scenes.AMBIENT_TWO))
+
+
+def test_avx_big_triangles_clipping(gpu):
+    # Spans up to ~600 px crossing many tiles, heavy clipping on every side.
+    run_both(scenes.random_soup(3000, 1024, 1024, radius=300, seed=5, centroid_margin=200))
+
+
+def test_avx_zero_lights(gpu):
+    run_both(scenes.random_soup(5000, 256, 256, radius=16, seed=11, lights=[]))
+
+
+def test_avx_1024_100k(gpu):
+    run_both(scenes.random_soup(100000, 1024, 1024, radius=64, seed=9))
+
+
+@pytest.mark.parametrize("phong,textured", [(False, False), (True, False), (False, True), (True, True)])
+def test_scalar_modes(gpu, phong, textured):
+    s = scenes.random_soup(20000, 512, 512, radius=16, seed=21, textured=textured,
+                           lights=scenes.LIGHTS_TWO, ambient=scenes.AMBIENT_TWO)
+    run_both(s, semantics=abi.PRK_SEM_SCALAR, phong=phong, exact_color=not phong,
+             label="scalar phong=%d tex=%d" % (phong, textured))
+
+
+def test_scalar_big_triangles(gpu):
+    s = scenes.random_soup(1500, 1024, 1024, radius=120, seed=4, textured=False)
+    run_both(s, semantics=abi.PRK_SEM_SCALAR, phong=False)
+
+
+def test_single_triangle_c1(gpu):
+    s = scenes.single_triangle()
+    g, o = run_both(s, semantics=abi.PRK_SEM_SCALAR, phong=False)
+    assert (g[2] == 0).sum() == o[3]["writes"] > 10000
+    s2 = scenes.single_triangle(textured=True, gouraud_only=False)
+    run_both(s2, semantics=abi.PRK_SEM_AVX, phong=True)
+
+
+def test_construct_sphere(gpu):
+    V, Cc, N, UV = prk.construct_sphere()
+    assert V.shape == (6624, 3)
+    base = scenes.random_soup(1, 512, 512, seed=0)
+    s = scenes.Scene(512, 512, V, Cc, N, UV, base.transform, scenes.LIGHTS_ONE, scenes.AMBIENT_ONE,
+                     base.texture, P=(0.0, 0.0, 2.0), name="sphere")
+    run_both(s, semantics=abi.PRK_SEM_AVX, phong=True)
+    run_both(s, semantics=abi.PRK_SEM_SCALAR, phong=False)
+
+
+@pytest.mark.parametrize("tile", [(8, 8), (32, 16), (64, 32), (128, 64)])
+def test_tile_sizes(gpu, tile):
+    run_both(scenes.random_soup(8000, 512, 384, radius=24, seed=13), tile=tile)
+
+
+def test_prior_contents_two_flushes(gpu):
+    """Second frame draws over the first one's colour/z (strict '>' against
+    the prior z-buffer, untouched pixels keep their colour)."""
+    a = scenes.random_soup(4000, 256, 256, radius=16, seed=1)
+    b = scenes.random_soup(4000, 256, 256, radius=16, seed=2)
+    oc, oz, _, _ = O.render(a)
+    oc2, oz2, ow2, _ = O.render(b, color=oc, z=oz)
+    gc, gz, _, _ = prk.render_scene(a)
+    gc2, gz2, gw2, st = prk.render_scene(b, color=gc, z=gz)
+    assert (gz2.view(np.uint32) == oz2.view(np.uint32)).all()
+    assert (gc2 == oc2).all()
+    assert (gw2 == ow2).all()
+
+
+def test_row_band(gpu):
+    s = scenes.random_soup(10000, 512, 512, radius=20, seed=17)
+    oc, oz, ow, _ = O.render(s)
+    for r0, r1 in [(0, 128), (128, 300), (300, 512), (37, 91)]:
+        gc, gz, gw, _ = prk.render_scene(s, rows=(r0, r1))
+        assert (gz.view(np.uint32) == oz[r0:r1].view(np.uint32)).all(), (r0, r1)
+        assert (gc == oc[r0:r1]).all(), (r0, r1)
+        assert (gw == ow[r0:r1]).all(), (r0, r1)
+
+
+def test_mixed_semantics_one_frame(gpu):
+    """Draws of different semantics in one flush share the z-buffer in order."""
+    a = scenes.random_soup(3000, 256, 256, radius=16, seed=31)
+    b = scenes.random_soup(3000, 256, 256, radius=16, seed=32, textured=False)
+    oc, oz, ow, _ = O.render(a)
+    oc, oz, ow2, _ = O.render(b, semantics=abi.PRK_SEM_SCALAR, phong=False, color=oc, z=oz)
+    ow = np.where(ow2 >= 0, ow2 + a.tri_count, ow)
+    r = prk.Renderer()
+    try:
+        r.target_alloc(256, 256)
+        r.clear()
+        r.set_debug(True)
+        r.set_camera(a.prk_transform(), a.prk_lights())
+        ga = r.geometry(a.vertices, a.colors, a.normals, a.uvs)
+        gb = r.geometry(b.vertices, b.colors, b.normals, b.uvs)
+        tex = r.texture(a.texture)
+        r.draw_model_optimized(ga, a.tri_count, bitmap=tex)
+        r.draw_model(gb, b.tri_count, phong=False)
+        r.complete_all_work()
+        gc, gz = r.download()
+        gw = r.winners()
+    finally:
+        r.close()
+    assert (gz.view(np.uint32) == oz.view(np.uint32)).all()
+    assert (gc == oc).all()
+    assert (gw == ow).all()
+
+
+def test_unsupported_combinations(gpu):
+    s = scenes.random_soup(10, 64, 64, seed=0)
+    r = prk.Renderer()
+    try:
+        g = r.geometry(s.vertices, s.colors, s.normals, s.uvs)
+        with pytest.raises(prk.PrkError) as e:
+            r.draw_model_optimized(g, 10, bitmap=None)  # projekt.cpp:1506 needs a Bitmap
+        assert e.value.code == abi.PRK_ERR_UNSUPPORTED
+        tex = r.texture(s.texture)
+        with pytest.raises(prk.PrkError) as e:
+            r.draw_model_optimized(g, 10, bitmap=tex, phong=False)  # broken branch 2285-2316
+        assert e.value.code == abi.PRK_ERR_UNSUPPORTED
+        r.target_alloc(60, 64)  # AVX needs width % 8 == 0 (projekt.cpp:2218)
+        r.set_camera(s.prk_transform(), s.prk_lights())
+        r.draw_model_optimized(g, 10, bitmap=tex)
+        with pytest.raises(prk.PrkError) as e:
+            r.complete_all_work()
+        assert e.value.code == abi.PRK_ERR_UNSUPPORTED
+    finally:
+        r.close()
+
+
+def test_full_c3b_4096_1m(gpu):
+    """The headline config (4096^2, 1M triangles, Phong + texture) against the
+    oracle on the host cores: every pixel, bit for bit."""
+    s = scenes.random_soup(1_000_000, 4096, 4096, radius=16, seed=2024)
+    run_both(s, threads=16)
