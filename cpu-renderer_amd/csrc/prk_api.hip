@@ -25,7 +25,8 @@ hipError_t prk_launch_bin(const prk::FrameParams *, uint32_t *, uint32_t *, uint
                           hipStream_t);
 hipError_t prk_launch_fill(const prk::FrameParams *, const void *, const uint32_t *, uint32_t *, uint32_t *,
                            hipStream_t);
-hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, const uint32_t *, hipStream_t);
+hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, const uint32_t *, uint32_t *,
+                             hipStream_t);
 }
 
 namespace {
@@ -88,13 +89,18 @@ struct prk_context {
     std::vector<prk::DrawRec> draws;
     uint32_t pending_tris = 0;
     // scratch
-    DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_counts, d_offs, d_cursor, d_bins, d_winners;
+    DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_counts, d_offs, d_cursor, d_bins, d_winners, d_anomaly;
     uint32_t *h_total = nullptr;  // pinned
     int32_t tile_w = 64, tile_h = 32;
     bool debug = false;
     bool winners_valid = false;
     prk_stats stats{};
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // Timing ring: 3 events per flush (before bin, before raster, after raster).
+    static constexpr int kRing = 32;
+    hipEvent_t ev[kRing][3] = {};
+    bool pending[kRing] = {};
+    uint32_t frame = 0;
+    int last_slot = -1;
 };
 
 #define PRK_TRY(expr)                              \
@@ -127,7 +133,8 @@ int prk_create(int device, prk_context **out) {
     if (!c) return PRK_ERR_NOMEM;
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
-    for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
+    for (int i = 0; i < prk_context::kRing && e == hipSuccess; ++i)
+        for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreate(&c->ev[i][k]);
     if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_total, sizeof(uint32_t), hipHostMallocDefault);
     if (e != hipSuccess) {
         prk_destroy(c);
@@ -154,11 +161,12 @@ int prk_destroy(prk_context *c) {
         (void)hipFree(c->zbuf);
     }
     DevBuf *bufs[] = {&c->d_draws, &c->d_texs, &c->d_tri_draw, &c->d_ranges, &c->d_counts,
-                      &c->d_offs,  &c->d_cursor, &c->d_bins, &c->d_winners};
+                      &c->d_offs,  &c->d_cursor, &c->d_bins, &c->d_winners, &c->d_anomaly};
     for (DevBuf *b : bufs) b->release();
     if (c->h_total) (void)hipHostFree(c->h_total);
-    for (auto &e : c->ev)
-        if (e) (void)hipEventDestroy(e);
+    for (auto &slot : c->ev)
+        for (auto &e : slot)
+            if (e) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
     return PRK_OK;
@@ -412,6 +420,31 @@ int prk_set_debug(prk_context *c, int32_t enable) {
     return PRK_OK;
 }
 
+// Accumulate the kernel times of a timed flush slot (waits for its last event).
+static void harvest(prk_context *c, int slot) {
+    if (!c->pending[slot]) return;
+    c->pending[slot] = false;
+    if (hipEventSynchronize(c->ev[slot][2]) != hipSuccess) return;
+    float a = 0, b = 0;
+    if (hipEventElapsedTime(&a, c->ev[slot][0], c->ev[slot][1]) != hipSuccess) a = 0;
+    if (hipEventElapsedTime(&b, c->ev[slot][1], c->ev[slot][2]) != hipSuccess) b = 0;
+    c->stats.sum_ms_bin += a;
+    c->stats.sum_ms_raster += b;
+    c->stats.frames_timed += 1;
+    if (slot == c->last_slot) {
+        c->stats.ms_bin = a;
+        c->stats.ms_raster = b;
+    }
+}
+
+int prk_timing_reset(prk_context *c) {
+    if (!c) return PRK_ERR_ARG;
+    for (int i = 0; i < prk_context::kRing; ++i) c->pending[i] = false;
+    c->stats.frames_timed = 0;
+    c->stats.sum_ms_bin = c->stats.sum_ms_raster = 0.0;
+    return PRK_OK;
+}
+
 int prk_flush(prk_context *c, void *stream) {
     if (!c) return PRK_ERR_ARG;
     if (!c->color) return PRK_ERR_NO_TARGET;
@@ -459,9 +492,11 @@ int prk_flush(prk_context *c, void *stream) {
     const uint32_t ntiles = (uint32_t)(fp.tiles_x * fp.tiles_y);
     if (fp.tiles_x > 65535 || fp.tiles_y > 65535) return PRK_ERR_UNSUPPORTED;
 
-    c->stats = prk_stats{};
     c->stats.triangles = T;
     c->stats.tiles = ntiles;
+    c->stats.bin_entries = 0;
+    const int slot = (int)(c->frame % prk_context::kRing);
+    harvest(c, slot);  // a flush kRing frames old: long finished
     if (c->debug) {
         PRK_TRY(c->d_winners.ensure((size_t)c->W * (c->row1 - c->row0) * 4));
         PRK_TRY(hipMemsetAsync(c->d_winners.p, 0xFF, (size_t)c->W * (c->row1 - c->row0) * 4, s));
@@ -498,13 +533,13 @@ int prk_flush(prk_context *c, void *stream) {
         PRK_TRY(prk_launch_tri_draw(fp.draws, fp.ndraws, (uint32_t *)c->d_tri_draw.p, T, s));
         fp.tri_draw = (const uint32_t *)c->d_tri_draw.p;
     }
-    PRK_TRY(c->d_ranges.ensure((size_t)T * 8));
+    PRK_TRY(c->d_ranges.ensure((size_t)T * 16));
     PRK_TRY(c->d_counts.ensure((size_t)ntiles * 4));
     PRK_TRY(c->d_offs.ensure((size_t)(ntiles + 1) * 4));
     PRK_TRY(c->d_cursor.ensure((size_t)ntiles * 4));
     PRK_TRY(hipMemsetAsync(c->d_counts.p, 0, (size_t)ntiles * 4, s));
     PRK_TRY(hipMemsetAsync(c->d_cursor.p, 0, (size_t)ntiles * 4, s));
-    PRK_TRY(hipEventRecord(c->ev[0], s));
+    PRK_TRY(hipEventRecord(c->ev[slot][0], s));
     PRK_TRY(prk_launch_bin(&fp, (uint32_t *)c->d_counts.p, (uint32_t *)c->d_offs.p, (uint32_t *)c->d_cursor.p,
                            c->d_ranges.p, ntiles, s));
     // The bin array size is data dependent: read the total back (one small
@@ -516,9 +551,17 @@ int prk_flush(prk_context *c, void *stream) {
     PRK_TRY(c->d_bins.ensure((size_t)std::max<uint32_t>(total, 1) * 4));
     PRK_TRY(prk_launch_fill(&fp, c->d_ranges.p, (const uint32_t *)c->d_offs.p, (uint32_t *)c->d_cursor.p,
                             (uint32_t *)c->d_bins.p, s));
-    PRK_TRY(hipEventRecord(c->ev[1], s));
-    PRK_TRY(prk_launch_raster(&fp, modeset, (const uint32_t *)c->d_offs.p, (const uint32_t *)c->d_bins.p, s));
-    PRK_TRY(hipEventRecord(c->ev[2], s));
+    PRK_TRY(hipEventRecord(c->ev[slot][1], s));
+    if (!c->d_anomaly.p) {
+        PRK_TRY(c->d_anomaly.ensure(4));
+        PRK_TRY(hipMemsetAsync(c->d_anomaly.p, 0, 4, s));
+    }
+    PRK_TRY(prk_launch_raster(&fp, modeset, (const uint32_t *)c->d_offs.p, (const uint32_t *)c->d_bins.p,
+                              (uint32_t *)c->d_anomaly.p, s));
+    PRK_TRY(hipEventRecord(c->ev[slot][2], s));
+    c->pending[slot] = true;
+    c->last_slot = slot;
+    c->frame++;
     c->draws.clear();
     c->pending_tris = 0;
     return PRK_OK;
@@ -534,11 +577,12 @@ int prk_synchronize(prk_context *c) {
 
 int prk_get_stats(prk_context *c, prk_stats *out) {
     if (!c || !out) return PRK_ERR_ARG;
-    if (c->stats.triangles) {
-        float a = 0, b = 0;
-        if (hipEventElapsedTime(&a, c->ev[0], c->ev[1]) == hipSuccess) c->stats.ms_bin = a;
-        if (hipEventElapsedTime(&b, c->ev[1], c->ev[2]) == hipSuccess) c->stats.ms_raster = b;
-        c->stats.ms_total = c->stats.ms_bin + c->stats.ms_raster;
+    (void)hipSetDevice(c->device);
+    for (int i = 1; i <= prk_context::kRing; ++i)  // oldest first
+        harvest(c, (int)((c->frame + i) % prk_context::kRing));
+    if (c->d_anomaly.p) {
+        PRK_TRY(hipDeviceSynchronize());
+        PRK_TRY(hipMemcpy(&c->stats.anomalies, c->d_anomaly.p, 4, hipMemcpyDeviceToHost));
     }
     *out = c->stats;
     return PRK_OK;

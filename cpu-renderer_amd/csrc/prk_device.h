@@ -391,14 +391,15 @@ __device__ __forceinline__ int setup_triangle(const DrawRec &d, uint32_t gt, con
     return n;
 }
 
-// AET edge step (projekt.cpp:3811-3829), only the fields mode M reads.
-template <int M>
+// AET edge step (projekt.cpp:3811-3829), only the fields mode M reads
+// (normals only when NRM: the visibility sweep never reads them).
+template <int M, bool NRM>
 __device__ __forceinline__ void step_edge(Edge &E) {
     using TR = ModeTraits<M>;
     E.X += E.G;
     E.Z += E.ZG;
-    if (TR::color) { E.C0 += E.CG0; E.C1 += E.CG1; E.C2 += E.CG2; E.C3 += E.CG3; }
-    if (TR::phong) {
+    if (TR::color && NRM) { E.C0 += E.CG0; E.C1 += E.CG1; E.C2 += E.CG2; E.C3 += E.CG3; }
+    if (TR::phong && NRM) {
         float x = E.N0 + E.NG0, y = E.N1 + E.NG1, z = E.N2 + E.NG2;
         normalize_rcp(x, y, z);
         E.N0 = x; E.N1 = y; E.N2 = z;
@@ -411,64 +412,86 @@ __device__ __forceinline__ bool insert_before(const Edge &A, const Edge &B) {
     return A.X < B.X || (A.X == B.X && (A.G < B.G || (A.G == B.G && A.Left < B.Left)));
 }
 
-// Per-triangle active edge table (DrawModelOptimized(RenderQueue,...),
-// projekt.cpp:3615-3871, with the P3 head/tail fix; DrawModel's AET
-// 168-598 is the same list logic).  The list is held in slots L0..L2 in list
-// order; `src` are the sorted setup edges.  For each row the walker calls
-// span(L, R, row) for the pair, exactly as the reference enqueues it.
-template <int M, typename SpanFn>
-__device__ __forceinline__ void aet_walk(int n, Edge s0, Edge s1, Edge s2, int32_t H,
-                                         int32_t row_begin, int32_t row_end, SpanFn &&span) {
-    if (n <= 0) return;
-    int32_t FirstRow = s0.YMin;
-    int32_t MaxRow = s0.YMax;
-    if (n > 1 && MaxRow < s1.YMax) MaxRow = s1.YMax;
-    if (n > 2 && MaxRow < s2.YMax) MaxRow = s2.YMax;
-    int32_t MaxY = MaxRow;
-    if (MaxY > H) MaxY = H;
-    if (MaxY > row_end) MaxY = row_end;
-    Edge L0 = s0, L1 = s0, L2 = s0;
-    int cnt = 0;
-    // Edges not yet inserted, in sorted-array order.
-    bool pend0 = true, pend1 = n > 1, pend2 = n > 2;
-    for (int32_t Row = FirstRow; Row < MaxY; ++Row) {
-        // Insertion (3654-3713): in array order, each before the first list
-        // entry it sorts before, else at the tail.
-        auto insert = [&](const Edge Ek) {
-            int pos = cnt;
-            if (cnt > 1 && insert_before(Ek, L1)) pos = 1;
-            if (cnt > 0 && insert_before(Ek, L0)) pos = 0;
-            L2 = sel(pos <= 1 && cnt >= 2, L1, sel(pos == 2, Ek, L2));
-            L1 = sel(pos == 0 && cnt >= 1, L0, sel(pos == 1, Ek, L1));
-            L0 = sel(pos == 0, Ek, L0);
-            ++cnt;
-        };
-        if (pend0 && s0.YMin == Row) { pend0 = false; insert(s0); }
-        if (pend1 && s1.YMin == Row) { pend1 = false; insert(s1); }
-        if (pend2 && s2.YMin == Row) { pend2 = false; insert(s2); }
-        // Expiry (3715-3749): drop every entry with YMax <= Row, keep order.
-        {
-            const bool k0 = cnt > 0 && !(L0.YMax <= Row);
-            const bool k1 = cnt > 1 && !(L1.YMax <= Row);
-            const bool k2 = cnt > 2 && !(L2.YMax <= Row);
-            const Edge n0 = sel(k0, L0, sel(k1, L1, L2));
-            const Edge n1 = sel(k0 && k1, L1, L2);
-            L0 = n0;
-            L1 = n1;
-            cnt = (int)k0 + (int)k1 + (int)k2;
+// Per-triangle active edge table of DrawModelOptimized(RenderQueue,...)
+// (projekt.cpp:3615-3871, with the P3 head/tail fix; DrawModel's AET,
+// 168-598, is the same list logic) as a row-by-row state machine.
+//
+// The list is held in slots L0..L2 in list order.  For ONE triangle the two
+// sorted edges with the smallest YMin always share it, so all
+// insertions of FirstRow happen in init() and at most one edge (P) is still
+// pending afterwards.  `anomaly` counts triangles violating that (never
+// observed; the host reports it as an error).
+template <int M, bool NRM>
+struct Walker {
+    Edge L0, L1, L2, P;
+    int cnt;
+    bool hasP;
+    int32_t FirstRow, MaxY, Row;
+
+    __device__ __forceinline__ void insert(const Edge E) {  // 3654-3713
+        int pos = cnt;
+        if (cnt > 1 && insert_before(E, L1)) pos = 1;
+        if (cnt > 0 && insert_before(E, L0)) pos = 0;
+        L2 = sel(pos <= 1 && cnt >= 2, L1, sel(pos == 2, E, L2));
+        L1 = sel(pos == 0 && cnt >= 1, L0, sel(pos == 1, E, L1));
+        L0 = sel(pos == 0, E, L0);
+        ++cnt;
+    }
+
+    __device__ __forceinline__ void init(int n, const Edge &s0, const Edge &s1, const Edge &s2, int32_t H,
+                                         int32_t row_end, uint32_t &anomaly) {
+        FirstRow = s0.YMin;
+        int32_t MaxRow = s0.YMax;
+        if (n > 1 && MaxRow < s1.YMax) MaxRow = s1.YMax;
+        if (n > 2 && MaxRow < s2.YMax) MaxRow = s2.YMax;
+        MaxY = min(min(MaxRow, H), row_end);
+        Row = FirstRow;
+        L0 = s0; L1 = s0; L2 = s0; P = s0;
+        cnt = 1;
+        hasP = false;
+        if (n > 1) {
+            if (s1.YMin == FirstRow) insert(s1);
+            else ++anomaly;
         }
-        if (cnt >= 2) {
-            // Pairing (3751-3869): one pair (L0, L1); with three entries the
-            // third is left unpaired and unstepped, as in the reference.
-            if (Row >= row_begin) span(L0, L1, Row);
-            step_edge<M>(L0);
-            step_edge<M>(L1);
-            const bool swp = L0.X > L1.X;  // 3831-3841 (+P3)
+        if (n > 2) {
+            if (s2.YMin == FirstRow) insert(s2);
+            else { P = s2; hasP = true; }
+        }
+    }
+
+    // Insertion + expiry of this->Row; true when a pair (L0, L1) is emitted.
+    __device__ __forceinline__ bool begin_row() {
+        if (hasP && P.YMin == Row) {
+            insert(P);
+            hasP = false;
+        }
+        // Expiry (3715-3749): drop every entry with YMax <= Row, keep order.
+        const bool k0 = cnt > 0 && !(L0.YMax <= Row);
+        const bool k1 = cnt > 1 && !(L1.YMax <= Row);
+        const bool k2 = cnt > 2 && !(L2.YMax <= Row);
+        const Edge n0 = sel(k0, L0, sel(k1, L1, L2));
+        const Edge n1 = sel(k0 && k1, L1, L2);
+        L0 = n0;
+        L1 = n1;
+        cnt = (int)k0 + (int)k1 + (int)k2;
+        // Pairing (3751-3869): one pair (L0, L1); a third entry is left
+        // unpaired and unstepped, as in the reference.
+        return cnt >= 2;
+    }
+
+    // Edge step of the emitted pair (3811-3829) and the crossing swap
+    // (3831-3841 + P3), then move to the next row.
+    __device__ __forceinline__ void end_row(bool paired) {
+        if (paired) {
+            step_edge<M, NRM>(L0);
+            step_edge<M, NRM>(L1);
+            const bool swp = L0.X > L1.X;
             const Edge t0 = sel(swp, L1, L0);
             L1 = sel(swp, L0, L1);
             L0 = t0;
         }
+        ++Row;
     }
-}
+};
 
 }  // namespace prk

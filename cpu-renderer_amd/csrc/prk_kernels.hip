@@ -23,6 +23,10 @@
 //                every pixel that got a winner.
 #include "prk_device.h"
 
+#ifndef PRK_RASTER_MIN_WAVES
+#define PRK_RASTER_MIN_WAVES 2  // waves per SIMD the raster kernel is register-budgeted for
+#endif
+
 namespace prk {
 
 __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
@@ -37,7 +41,10 @@ __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
     tri_draw[g] = lo;
 }
 
-struct TileRange { uint16_t tx0, ty0, tx1, ty1; };
+// Tiles a triangle may touch: the rectangle [tx0..tx1] x [ty0..ty1], plus
+// for scalar semantics the column-0 tiles of rows [oty0..oty1] that receive
+// DrawModel's one-past-the-row store (see span_scalar).
+struct TileRange { uint16_t tx0, ty0, tx1, ty1, oty0, oty1, pad0, pad1; };
 
 // Conservative tile range of a triangle's covered pixels.  Span end points
 // are edge-DDA values that stay on their segment up to float error
@@ -61,13 +68,36 @@ __device__ __forceinline__ bool tri_tile_range(const FrameParams &fp, uint32_t g
     float maxabs = fmaxf(fabsf(xmin), fabsf(xmax));
     float slack = 2.0f + ((ymax - ymin) + 4.0f) * maxabs * (1.0f / 2097152.0f);  // 2^-21
     float fc0 = floorf(xmin - slack), fc1 = ceilf(xmax + slack) + 1.0f;
-    int32_t c0 = fc0 < 0.0f ? 0 : (fc0 >= (float)fp.W ? fp.W : (int32_t)fc0);
-    int32_t c1 = fc1 > (float)fp.W ? fp.W : (fc1 <= 0.0f ? 0 : (int32_t)fc1);
+    int32_t c0, c1;
+    if (d->mode == MODE_AVX) {
+        // Half-open [MinX, MaxX): a span clamped wholly to one side is empty.
+        c0 = fc0 < 0.0f ? 0 : (fc0 >= (float)fp.W ? fp.W : (int32_t)fc0);
+        c1 = fc1 > (float)fp.W ? fp.W : (fc1 <= 0.0f ? 0 : (int32_t)fc1);
+    } else {
+        // DrawModel's inclusive [MinX, MaxX] after clamping both ends to
+        // [0, W-1] (projekt.cpp:381-425): a triangle left of the screen still
+        // draws column 0, one right of it column W-1.
+        c0 = fc0 < 0.0f ? 0 : (fc0 >= (float)(fp.W - 1) ? fp.W - 1 : (int32_t)fc0);
+        c1 = fc1 > (float)fp.W ? fp.W : (fc1 <= 1.0f ? 1 : (int32_t)fc1);
+    }
     if (c0 >= c1) return false;
     tr.tx0 = (uint16_t)(c0 / fp.tile_w);
     tr.tx1 = (uint16_t)((c1 - 1) / fp.tile_w);
     tr.ty0 = (uint16_t)((r0 - fp.row0) / fp.tile_h);
     tr.ty1 = (uint16_t)((r1 - 1 - fp.row0) / fp.tile_h);
+    tr.oty0 = 1;
+    tr.oty1 = 0;
+    if (d->mode != MODE_AVX && fc1 >= (float)fp.W) {
+        // A span ending at MaxX == W stores pixel (row+1, 0): rows shift by one.
+        const float lim = (float)min(fp.row1, fp.H);
+        float g0 = fr0 + 1.0f, g1 = fr1 + 1.0f;
+        int32_t o0 = g0 < (float)fp.row0 ? fp.row0 : (g0 >= lim ? (int32_t)lim : (int32_t)g0);
+        int32_t o1 = g1 > lim ? (int32_t)lim : (g1 <= (float)fp.row0 ? fp.row0 : (int32_t)g1);
+        if (o0 < o1) {
+            tr.oty0 = (uint16_t)((o0 - fp.row0) / fp.tile_h);
+            tr.oty1 = (uint16_t)((o1 - 1 - fp.row0) / fp.tile_h);
+        }
+    }
     return true;
 }
 
@@ -77,11 +107,14 @@ __global__ void k_bin_count(FrameParams fp, uint32_t *__restrict__ counts,
     if (g >= fp.tri_count) return;
     TileRange tr;
     if (!tri_tile_range(fp, g, tr)) {
-        tr.tx0 = 1; tr.tx1 = 0; tr.ty0 = 1; tr.ty1 = 0;
+        tr.tx0 = 1; tr.tx1 = 0; tr.ty0 = 1; tr.ty1 = 0; tr.oty0 = 1; tr.oty1 = 0;
     } else {
         for (int ty = tr.ty0; ty <= tr.ty1; ++ty)
             for (int tx = tr.tx0; tx <= tr.tx1; ++tx)
                 atomicAdd(&counts[ty * fp.tiles_x + tx], 1u);
+        for (int ty = tr.oty0; ty <= tr.oty1; ++ty)
+            if (!(tr.tx0 == 0 && ty >= tr.ty0 && ty <= tr.ty1))
+                atomicAdd(&counts[ty * fp.tiles_x], 1u);
     }
     ranges[g] = tr;
 }
@@ -123,11 +156,45 @@ __global__ void k_bin_fill(FrameParams fp, const TileRange *__restrict__ ranges,
             uint32_t p = atomicAdd(&cursor[t], 1u);
             bins[offs[t] + p] = g;
         }
+    for (int ty = tr.oty0; ty <= tr.oty1; ++ty)
+        if (!(tr.tx0 == 0 && ty >= tr.ty0 && ty <= tr.ty1)) {
+            int t = ty * fp.tiles_x;
+            uint32_t p = atomicAdd(&cursor[t], 1u);
+            bins[offs[t] + p] = g;
+        }
 }
 
 // ---------------------------------------------------------------------------
 // Tile raster.
+//
+// One workgroup (4 waves) per tile.  A wave takes 64 bin entries at a time,
+// one triangle per lane: the lane runs FillEdgeTable for it and then all 64
+// lanes walk their AETs row by row in lock step.  At each row a lane's span
+// (the reference's line_render_work, projekt.cpp:3756-3809) goes to the
+// wave's LDS slots, and the wave splits the row's spans into work items:
+//   AVX    : item j of a span = pixels xa+j, xa+j+8, ... < xb, i.e. ONE of the
+//            8 lane chains of FillLineOptimized (each chain is an independent
+//            float recurrence: lane init + one step per 8-px block);
+//   scalar : one item per span (DrawModel's recurrence runs pixel by pixel).
+// Items are spread over the 64 lanes (prefix sum + binary search), so the
+// pixel work no longer serialises on the lane that owns the triangle.
 // ---------------------------------------------------------------------------
+constexpr int kWaves = 4;
+constexpr int kSpanF = 22;  // float fields per span slot
+constexpr int kSpanI = 8;   // int fields per span slot
+enum { SI_XA = 0, SI_XB, SI_LEFT, SI_PRE, SI_TAG, SI_ROW, SI_OVF, SI_TEX };
+// AVX float slots
+enum { SF_XOFF = 0, SF_LW, SF_LU, SF_LV, SF_LZ, SF_IW, SF_IU, SF_IV, SF_IZ, SF_LN0, SF_LN1, SF_LN2,
+       SF_IN0, SF_IN1, SF_IN2 };
+// scalar float slots
+enum { SS_Z = 0, SS_IZ, SS_W, SS_U, SS_V, SS_IW, SS_IU, SS_IV, SS_N0, SS_N1, SS_N2, SS_IN0, SS_IN1, SS_IN2,
+       SS_C0, SS_C1, SS_C2, SS_C3, SS_IC0, SS_IC1, SS_IC2, SS_IC3 };
+
+struct WaveSlots {
+    float f[kSpanF][64];
+    int32_t i[kSpanI][64];
+};
+
 struct TileCtx {
     int32_t x0, x1, y0, y1, tw;  // tile pixel rectangle [x0,x1) x [y0,y1), LDS row stride tw
     unsigned long long *key;     // LDS: visibility keys
@@ -147,20 +214,24 @@ __device__ __forceinline__ void put_winner(const TileCtx &tc, int p, float z, ui
     reinterpret_cast<uint32_t *>(tc.key + p)[1] = __float_as_uint(z);  // raw z bits
 }
 
-// ----- FillLineOptimized span (projekt.cpp:1492-2320) -----------------------
+// ----- span setup --------------------------------------------------------
+// FillLineOptimized span setup (projekt.cpp:1543-1835) for row Row; writes the
+// lane's slot and returns its item count (pixels of [MinX, MaxX) in the tile,
+// at most 8 chains).
 template <bool SHADE>
-__device__ __forceinline__ void span_avx(const FrameParams &fp, const TexRec &tex, const TileCtx &tc,
-                                         uint32_t tag, const Edge &L, const Edge &R, int32_t Row) {
+__device__ __forceinline__ int span_setup_avx(const FrameParams &fp, const TileCtx &tc, WaveSlots &ws, int lane,
+                                              uint32_t tag, int32_t texi, const Edge &L, const Edge &R,
+                                              int32_t Row) {
+    if (Row < tc.y0) return 0;
     const int32_t W = fp.W;
     float XOffset = 0.0f;
-    if (Row < 0) return;
     float LeftX = L.X;  // 1545-1565
     if (LeftX < 0) { XOffset = -L.X; LeftX = 0; }
     else if (LeftX >= W) LeftX = (float)W - 1;
     float RightX = R.X;
     if (RightX < 0) RightX = 0;
     else if (RightX >= W) RightX = (float)W - 1;
-    if (LeftX != LeftX || RightX != RightX) return;  // pinned: NaN edge X draws nothing
+    if (LeftX != LeftX || RightX != RightX) return 0;  // pinned: NaN edge X draws nothing
     const int32_t XDiff = (int32_t)((uint32_t)round_s32(R.X) - (uint32_t)round_s32(L.X));  // 1568-1570
     const int32_t MinX = round_s32(LeftX), MaxX = round_s32(RightX);  // 1588-1592
     int32_t LeftXa = MinX;
@@ -168,16 +239,9 @@ __device__ __forceinline__ void span_avx(const FrameParams &fp, const TexRec &te
         LeftXa = MinX & ~7;
         XOffset -= (float)(MinX & 7) * 1.0f;
     }
-    // Coverage of the clip masks is exactly [MinX, MaxX).
+    // The clip masks of 1594-1664 / 2241-2256 cover exactly [MinX, MaxX).
     const int32_t xa = max(MinX, tc.x0), xb = min(MaxX, tc.x1);
-    if (xa >= xb) return;
-    const int rowoff = (Row - tc.y0) * tc.tw - tc.x0;
-
-    if (SHADE) {  // any winner of this triangle on this span?
-        bool any = false;
-        for (int32_t x = xa; x < xb; ++x) any |= is_winner(tc, rowoff + x, tag);
-        if (!any) return;
-    }
+    if (xa >= xb) return 0;
     const float fXD = (float)XDiff;
     float IW = 0, IU = 0, IV = 0, IZ = 0, IN0 = 0, IN1 = 0, IN2 = 0;
     if (XDiff != 0) {  // 1666-1835
@@ -191,116 +255,45 @@ __device__ __forceinline__ void span_avx(const FrameParams &fp, const TexRec &te
         }
         IZ = (R.Z - L.Z) / fXD;
     }
-    const float IW8 = IW * 8.0f, IU8 = IU * 8.0f, IV8 = IV * 8.0f, IZ8 = 8.0f * IZ;
-    const float IN08 = IN0 * 8.0f, IN18 = IN1 * 8.0f, IN28 = IN2 * 8.0f;
-    const float Tw = (float)tex.w, Th = (float)tex.h;
-
-    for (int i = 0; i < 8; ++i) {
-        // pixels x = LeftXa + 8b + i inside [xa, xb)
-        int32_t rel = xa - LeftXa - i;
-        int32_t b0 = rel <= 0 ? 0 : (rel + 7) >> 3;
-        int32_t x = LeftXa + 8 * b0 + i;
-        if (x >= xb) continue;
-        const float o = XOffset + (float)i;  // lane init (XOffset + i)*inc, 1712-1835
-        float w = L.W + o * IW, u = L.U + o * IU, v = L.V + o * IV, z = L.Z + o * IZ;
-        float n0 = 0, n1 = 0, n2 = 0;
-        if (SHADE) {
-            n0 = L.N0 + o * IN0; n1 = L.N1 + o * IN1; n2 = L.N2 + o * IN2;
-            normalize_div(n0, n1, n2);  // 1754
-        }
-        for (int32_t k = 0; k < b0; ++k) {  // block steps 2262-2282
-            if (SHADE) {
-                float a = n0 + IN08, b = n1 + IN18, c = n2 + IN28;
-                normalize_div(a, b, c);
-                n0 = a; n1 = b; n2 = c;
-            }
-            z = z + IZ8; w = w + IW8; u = u + IU8; v = v + IV8;
-        }
-        for (; x < xb; x += 8) {
-            const float iw = 1.0f / w;  // 1865-1866
-            const float fu = iw * u, fv = iw * v;
-            const int p = rowoff + x;
-            if (!SHADE) {
-                if (fu >= 0.0f && fu <= 1.0f && fv >= 0.0f && fv <= 1.0f && z == z)
-                    atomicMax(&tc.key[p], make_key(z, tag));
-            } else if (is_winner(tc, p, tag)) {
-                // Texel (1881-2032): trunc, <<2, 16-bit pitch multiply, P2 clamp.
-                const int32_t FX = (int32_t)((uint32_t)cvtt_s32(Tw * fu) << 2);
-                const int32_t FY = mul16_trick(cvtt_s32(Th * fv), tex.pitch);
-                const uint32_t t = texel_at(tex, (int32_t)((uint32_t)FX + (uint32_t)FY));
-                const float CA = (float)((t >> 24) & 0xFF) / 255.0f;
-                const float CR = (float)((t >> 16) & 0xFF) / 255.0f;
-                const float CG = (float)((t >> 8) & 0xFF) / 255.0f;
-                const float CB = (float)(t & 0xFF) / 255.0f;
-                // Phong (2040-2128) at UnprojectVertex_8x (102-145).
-                const float d = fp.D - z;
-                const float Xf = (float)(x - i) + (float)i, Yf = (float)Row + 0.0f;
-                const float AX = (Xf - fp.Cx) * fp.InvM2P, AY = (Yf - fp.Cy) * fp.InvM2P;
-                const float PX = (d / fp.F) * AX, PY = (d / fp.F) * AY, PZ = z;
-                float Fr = 0, Fg = 0, Fb = 0, Fa = 0;
-                for (uint32_t li = 0; li < fp.light_count; ++li) {
-                    if (li == 0) {
-                        Fr = CR * fp.amb[0]; Fg = CG * fp.amb[1];
-                        Fb = CB * fp.amb[2]; Fa = CA * fp.amb[3];
-                    }
-                    float Lx = fp.lp[li][0] - PX, Ly = fp.lp[li][1] - PY, Lz = fp.lp[li][2] - PZ;
-                    normalize_div(Lx, Ly, Lz);
-                    const float Cos = minps(1.0f, maxps(0.0f, (n0 * Lx + n1 * Ly) + n2 * Lz));
-                    float Vx = 0.0f - PX, Vy = 0.0f - PY, Vz = 0.0f - PZ;
-                    normalize_div(Vx, Vy, Vz);
-                    float Hx = Lx + Vx, Hy = Ly + Vy, Hz = Lz + Vz;
-                    normalize_div(Hx, Hy, Hz);
-                    float Ph = minps(1.0f, maxps(0.0f, (n0 * Hx + n1 * Hy) + n2 * Hz));
-                    Ph = Ph * Ph; Ph = Ph * Ph; Ph = Ph * Ph; Ph = Ph * Ph;
-                    const float *I = fp.li[li];
-                    Fr = Fr + ((Cos * (CR * I[0])) + (Ph * (1.0f * I[0])));
-                    Fg = Fg + ((Cos * (CG * I[1])) + (Ph * (1.0f * I[1])));
-                    Fb = Fb + ((Cos * (CB * I[2])) + (Ph * (1.0f * I[2])));
-                    Fa = Fa + ((Cos * (CA * I[3])) + (Ph * (1.0f * I[3])));
-                }
-                Fr = maxps(minps(Fr, 1.0f), 0.0f);  // 2131-2134
-                Fg = maxps(minps(Fg, 1.0f), 0.0f);
-                Fb = maxps(minps(Fb, 1.0f), 0.0f);
-                Fa = maxps(minps(Fa, 1.0f), 0.0f);
-                const uint32_t packed = ((uint32_t)cvt_rne_s32(Fr * 255.0f) << 16) |
-                                        ((uint32_t)cvt_rne_s32(Fg * 255.0f) << 8) |
-                                        ((uint32_t)cvt_rne_s32(Fb * 255.0f)) |
-                                        ((uint32_t)cvt_rne_s32(Fa * 255.0f) << 24);
-                put_winner(tc, p, z, packed);
-            }
-            if (SHADE) {
-                float a = n0 + IN08, b = n1 + IN18, c = n2 + IN28;
-                normalize_div(a, b, c);
-                n0 = a; n1 = b; n2 = c;
-            }
-            z = z + IZ8; w = w + IW8; u = u + IU8; v = v + IV8;
-        }
+    ws.i[SI_XA][lane] = xa;
+    ws.i[SI_XB][lane] = xb;
+    ws.i[SI_LEFT][lane] = LeftXa;
+    ws.i[SI_TAG][lane] = (int32_t)tag;
+    ws.i[SI_ROW][lane] = Row;
+    ws.i[SI_TEX][lane] = texi;
+    ws.f[SF_XOFF][lane] = XOffset;
+    ws.f[SF_LW][lane] = L.W; ws.f[SF_LU][lane] = L.U; ws.f[SF_LV][lane] = L.V; ws.f[SF_LZ][lane] = L.Z;
+    ws.f[SF_IW][lane] = IW; ws.f[SF_IU][lane] = IU; ws.f[SF_IV][lane] = IV; ws.f[SF_IZ][lane] = IZ;
+    if (SHADE) {
+        ws.f[SF_LN0][lane] = L.N0; ws.f[SF_LN1][lane] = L.N1; ws.f[SF_LN2][lane] = L.N2;
+        ws.f[SF_IN0][lane] = IN0; ws.f[SF_IN1][lane] = IN1; ws.f[SF_IN2][lane] = IN2;
     }
+    return min(8, xb - xa);
 }
 
-// ----- DrawModel span (projekt.cpp:298-538) ---------------------------------
+// DrawModel span setup (projekt.cpp:298-412).  One item per span.
 template <int M, bool SHADE>
-__device__ __forceinline__ void span_scalar(const FrameParams &fp, const TexRec &tex, const TileCtx &tc,
-                                            uint32_t tag, const Edge &L, const Edge &R, int32_t Row) {
+__device__ __forceinline__ int span_setup_scalar(const FrameParams &fp, const TileCtx &tc, WaveSlots &ws, int lane,
+                                                 uint32_t tag, int32_t texi, const Edge &L, const Edge &R,
+                                                 int32_t Row) {
     using TR = ModeTraits<M>;
     const int32_t W = fp.W;
     float XOffset = 0.0f;
-    if (Row < 0) return;
     const float XDiff = roundf(R.X - L.X);  // 311-312
     float IW = 0, IU = 0, IV = 0, IZ = 0, IN0 = 0, IN1 = 0, IN2 = 0;
     float IC0 = 0, IC1 = 0, IC2 = 0, IC3 = 0;
     if (XDiff != 0.0f) {  // 329-360
-        if (TR::tex) {
+        if (SHADE && TR::tex) {
             IW = (R.W - L.W) / XDiff;
             IU = (R.U - L.U) / XDiff;
             IV = (R.V - L.V) / XDiff;
         }
-        if (TR::phong) {
+        if (SHADE && TR::phong) {
             IN0 = (R.N0 - L.N0) / XDiff;
             IN1 = (R.N1 - L.N1) / XDiff;
             IN2 = (R.N2 - L.N2) / XDiff;
         }
-        if (TR::color) {
+        if (SHADE && TR::color) {
             IC0 = (R.C0 - L.C0) / XDiff;
             IC1 = (R.C1 - L.C1) / XDiff;
             IC2 = (R.C2 - L.C2) / XDiff;
@@ -314,37 +307,203 @@ __device__ __forceinline__ void span_scalar(const FrameParams &fp, const TexRec 
     float RightX = R.X;
     if (RightX < 0) RightX = 0;
     else if (RightX >= W) RightX = (float)W - 1;
-    if (LeftX != LeftX || RightX != RightX) return;
+    if (LeftX != LeftX || RightX != RightX) return 0;
     const int32_t MinX = round_s32(LeftX), MaxX = round_s32(RightX);  // 402-406
-    const int32_t xa = max(MinX, tc.x0), xb = min(MaxX + 1, tc.x1);     // inclusive [MinX, MaxX]
-    if (xa >= xb) return;
+    // Inclusive [MinX, MaxX].  RightX in [W-0.5, W) is not clamped (389-399),
+    // so MaxX can be W: the reference then stores linear pixel Row*W + W,
+    // i.e. (Row+1, 0), which belongs to a column-0 tile one row down; on the
+    // frame's last row it would fall outside the buffers (dropped).
+    const bool in_rows = Row >= tc.y0;
+    const int32_t xa = in_rows ? max(MinX, tc.x0) : 0;
+    const int32_t xb = in_rows ? min(MaxX + 1, tc.x1) : 0;
+    const bool ovf = tc.x0 == 0 && MaxX >= W && Row + 1 >= tc.y0 && Row + 1 < tc.y1;
+    if (xa >= xb && !ovf) return 0;
+    ws.i[SI_XA][lane] = xa;
+    ws.i[SI_XB][lane] = xb;
+    ws.i[SI_LEFT][lane] = MinX;
+    ws.i[SI_TAG][lane] = (int32_t)tag;
+    ws.i[SI_ROW][lane] = Row;
+    ws.i[SI_OVF][lane] = ovf ? (Row + 1 - tc.y0) * tc.tw : -1;
+    ws.i[SI_TEX][lane] = texi;
+    ws.f[SS_Z][lane] = L.Z + XOffset * IZ;  // 408-412: Current* += XOffset*Increment
+    ws.f[SS_IZ][lane] = IZ;
+    if (SHADE) {
+        if (TR::tex) {
+            ws.f[SS_W][lane] = L.W + XOffset * IW; ws.f[SS_IW][lane] = IW;
+            ws.f[SS_U][lane] = L.U + XOffset * IU; ws.f[SS_IU][lane] = IU;
+            ws.f[SS_V][lane] = L.V + XOffset * IV; ws.f[SS_IV][lane] = IV;
+        }
+        if (TR::phong) {
+            ws.f[SS_N0][lane] = L.N0 + XOffset * IN0; ws.f[SS_IN0][lane] = IN0;
+            ws.f[SS_N1][lane] = L.N1 + XOffset * IN1; ws.f[SS_IN1][lane] = IN1;
+            ws.f[SS_N2][lane] = L.N2 + XOffset * IN2; ws.f[SS_IN2][lane] = IN2;
+        }
+        if (TR::color) {
+            ws.f[SS_C0][lane] = L.C0 + XOffset * IC0; ws.f[SS_IC0][lane] = IC0;
+            ws.f[SS_C1][lane] = L.C1 + XOffset * IC1; ws.f[SS_IC1][lane] = IC1;
+            ws.f[SS_C2][lane] = L.C2 + XOffset * IC2; ws.f[SS_IC2][lane] = IC2;
+            ws.f[SS_C3][lane] = L.C3 + XOffset * IC3; ws.f[SS_IC3][lane] = IC3;
+        }
+    }
+    return 1;
+}
+
+// ----- work items ----------------------------------------------------------
+// Phong + texel of one FillLineOptimized lane (projekt.cpp:1865-2200).
+__device__ __forceinline__ uint32_t shade_avx(const FrameParams &fp, const TexRec &tex, float fu, float fv,
+                                              float z, float n0, float n1, float n2, int32_t x, int32_t i,
+                                              int32_t Row) {
+    // Texel (1881-2032): trunc, <<2, 16-bit pitch multiply, P2 clamp.
+    const int32_t FX = (int32_t)((uint32_t)cvtt_s32((float)tex.w * fu) << 2);
+    const int32_t FY = mul16_trick(cvtt_s32((float)tex.h * fv), tex.pitch);
+    const uint32_t t = texel_at(tex, (int32_t)((uint32_t)FX + (uint32_t)FY));
+    const float CA = (float)((t >> 24) & 0xFF) / 255.0f;
+    const float CR = (float)((t >> 16) & 0xFF) / 255.0f;
+    const float CG = (float)((t >> 8) & 0xFF) / 255.0f;
+    const float CB = (float)(t & 0xFF) / 255.0f;
+    // Phong (2040-2128) at UnprojectVertex_8x (102-145).
+    const float d = fp.D - z;
+    const float Xf = (float)(x - i) + (float)i, Yf = (float)Row + 0.0f;
+    const float AX = (Xf - fp.Cx) * fp.InvM2P, AY = (Yf - fp.Cy) * fp.InvM2P;
+    const float PX = (d / fp.F) * AX, PY = (d / fp.F) * AY, PZ = z;
+    float Fr = 0, Fg = 0, Fb = 0, Fa = 0;
+    for (uint32_t li = 0; li < fp.light_count; ++li) {
+        if (li == 0) {
+            Fr = CR * fp.amb[0]; Fg = CG * fp.amb[1];
+            Fb = CB * fp.amb[2]; Fa = CA * fp.amb[3];
+        }
+        float Lx = fp.lp[li][0] - PX, Ly = fp.lp[li][1] - PY, Lz = fp.lp[li][2] - PZ;
+        normalize_div(Lx, Ly, Lz);
+        const float Cos = minps(1.0f, maxps(0.0f, (n0 * Lx + n1 * Ly) + n2 * Lz));
+        float Vx = 0.0f - PX, Vy = 0.0f - PY, Vz = 0.0f - PZ;
+        normalize_div(Vx, Vy, Vz);
+        float Hx = Lx + Vx, Hy = Ly + Vy, Hz = Lz + Vz;
+        normalize_div(Hx, Hy, Hz);
+        float Ph = minps(1.0f, maxps(0.0f, (n0 * Hx + n1 * Hy) + n2 * Hz));
+        Ph = Ph * Ph; Ph = Ph * Ph; Ph = Ph * Ph; Ph = Ph * Ph;
+        const float *I = fp.li[li];
+        Fr = Fr + ((Cos * (CR * I[0])) + (Ph * (1.0f * I[0])));
+        Fg = Fg + ((Cos * (CG * I[1])) + (Ph * (1.0f * I[1])));
+        Fb = Fb + ((Cos * (CB * I[2])) + (Ph * (1.0f * I[2])));
+        Fa = Fa + ((Cos * (CA * I[3])) + (Ph * (1.0f * I[3])));
+    }
+    Fr = maxps(minps(Fr, 1.0f), 0.0f);  // 2131-2134
+    Fg = maxps(minps(Fg, 1.0f), 0.0f);
+    Fb = maxps(minps(Fb, 1.0f), 0.0f);
+    Fa = maxps(minps(Fa, 1.0f), 0.0f);
+    return ((uint32_t)cvt_rne_s32(Fr * 255.0f) << 16) | ((uint32_t)cvt_rne_s32(Fg * 255.0f) << 8) |
+           ((uint32_t)cvt_rne_s32(Fb * 255.0f)) | ((uint32_t)cvt_rne_s32(Fa * 255.0f) << 24);
+}
+
+// Item j of an AVX span: lane chain i = (xa + j - LeftXa) & 7 from block b.
+template <bool SHADE>
+__device__ __forceinline__ void item_avx(const FrameParams &fp, const TileCtx &tc, const WaveSlots &ws, int s,
+                                         int j) {
+    const int32_t xa = ws.i[SI_XA][s], xb = ws.i[SI_XB][s], LeftXa = ws.i[SI_LEFT][s];
+    const uint32_t tag = (uint32_t)ws.i[SI_TAG][s];
+    const int32_t Row = ws.i[SI_ROW][s];
     const int rowoff = (Row - tc.y0) * tc.tw - tc.x0;
+    int32_t x = xa + j;
     if (SHADE) {
         bool any = false;
+        for (int32_t xx = x; xx < xb; xx += 8) any |= is_winner(tc, rowoff + xx, tag);
+        if (!any) return;
+    }
+    // The texture of the span's draw (the item may run on any lane).
+    TexRec tex;
+    if (SHADE) tex = fp.texs[ws.i[SI_TEX][s]];
+    else { tex.mem = nullptr; tex.w = tex.h = tex.pitch = tex.pad = 0; }
+    const int32_t rel = x - LeftXa, i = rel & 7, b = rel >> 3;
+    const float IW = ws.f[SF_IW][s], IU = ws.f[SF_IU][s], IV = ws.f[SF_IV][s], IZ = ws.f[SF_IZ][s];
+    const float IW8 = IW * 8.0f, IU8 = IU * 8.0f, IV8 = IV * 8.0f, IZ8 = 8.0f * IZ;
+    const float o = ws.f[SF_XOFF][s] + (float)i;  // lane init (XOffset + i)*inc, 1712-1835
+    float w = ws.f[SF_LW][s] + o * IW, u = ws.f[SF_LU][s] + o * IU;
+    float v = ws.f[SF_LV][s] + o * IV, z = ws.f[SF_LZ][s] + o * IZ;
+    float n0 = 0, n1 = 0, n2 = 0, IN08 = 0, IN18 = 0, IN28 = 0;
+    if (SHADE) {
+        const float IN0 = ws.f[SF_IN0][s], IN1 = ws.f[SF_IN1][s], IN2 = ws.f[SF_IN2][s];
+        IN08 = IN0 * 8.0f; IN18 = IN1 * 8.0f; IN28 = IN2 * 8.0f;
+        n0 = ws.f[SF_LN0][s] + o * IN0; n1 = ws.f[SF_LN1][s] + o * IN1; n2 = ws.f[SF_LN2][s] + o * IN2;
+        normalize_div(n0, n1, n2);  // 1754
+    }
+    for (int32_t k = 0; k < b; ++k) {  // block steps 2262-2282
+        if (SHADE) {
+            float a = n0 + IN08, bb = n1 + IN18, c = n2 + IN28;
+            normalize_div(a, bb, c);
+            n0 = a; n1 = bb; n2 = c;
+        }
+        z = z + IZ8; w = w + IW8; u = u + IU8; v = v + IV8;
+    }
+    for (; x < xb; x += 8) {
+        const float iw = 1.0f / w;  // 1865-1866
+        const float fu = iw * u, fv = iw * v;
+        const int p = rowoff + x;
+        if (!SHADE) {
+            if (fu >= 0.0f && fu <= 1.0f && fv >= 0.0f && fv <= 1.0f && z == z)
+                atomicMax(&tc.key[p], make_key(z, tag));
+        } else {
+            if (is_winner(tc, p, tag)) put_winner(tc, p, z, shade_avx(fp, tex, fu, fv, z, n0, n1, n2, x, i, Row));
+            if (x + 8 < xb) {
+                float a = n0 + IN08, bb = n1 + IN18, c = n2 + IN28;
+                normalize_div(a, bb, c);
+                n0 = a; n1 = bb; n2 = c;
+            }
+        }
+        z = z + IZ8; w = w + IW8; u = u + IU8; v = v + IV8;
+    }
+}
+
+// A whole DrawModel span (projekt.cpp:423-538) restricted to the tile.
+template <int M, bool SHADE>
+__device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx &tc, const WaveSlots &ws, int s) {
+    using TR = ModeTraits<M>;
+    const int32_t W = fp.W;
+    const int32_t xa = ws.i[SI_XA][s], xb = ws.i[SI_XB][s], MinX = ws.i[SI_LEFT][s];
+    const uint32_t tag = (uint32_t)ws.i[SI_TAG][s];
+    const int32_t Row = ws.i[SI_ROW][s];
+    const int povf = ws.i[SI_OVF][s];
+    const int rowoff = (Row - tc.y0) * tc.tw - tc.x0;
+    const int32_t xend = povf >= 0 ? W + 1 : xb;
+    if (SHADE) {
+        bool any = povf >= 0 && is_winner(tc, povf, tag);
         for (int32_t x = xa; x < xb; ++x) any |= is_winner(tc, rowoff + x, tag);
         if (!any) return;
     }
-    float z = L.Z + XOffset * IZ;  // 408-412 (CurrentZ += XOffset*ZIncrement)
-    float w = L.W, u = L.U, v = L.V, n0 = L.N0, n1 = L.N1, n2 = L.N2;
-    float c0 = L.C0, c1 = L.C1, c2 = L.C2, c3 = L.C3;
+    TexRec tex;
+    if (SHADE && TR::tex) tex = fp.texs[ws.i[SI_TEX][s]];  // the span's draw, not this lane's
+    else { tex.mem = nullptr; tex.w = tex.h = tex.pitch = tex.pad = 0; }
+    float z = ws.f[SS_Z][s];
+    const float IZ = ws.f[SS_IZ][s];
+    float w = 0, u = 0, v = 0, IW = 0, IU = 0, IV = 0, n0 = 0, n1 = 0, n2 = 0, IN0 = 0, IN1 = 0, IN2 = 0;
+    float c0 = 0, c1 = 0, c2 = 0, c3 = 0, IC0 = 0, IC1 = 0, IC2 = 0, IC3 = 0;
     if (SHADE) {
-        w += XOffset * IW; u += XOffset * IU; v += XOffset * IV;
-        n0 += XOffset * IN0; n1 += XOffset * IN1; n2 += XOffset * IN2;
-        c0 += XOffset * IC0; c1 += XOffset * IC1; c2 += XOffset * IC2; c3 += XOffset * IC3;
+        if (TR::tex) {
+            w = ws.f[SS_W][s]; u = ws.f[SS_U][s]; v = ws.f[SS_V][s];
+            IW = ws.f[SS_IW][s]; IU = ws.f[SS_IU][s]; IV = ws.f[SS_IV][s];
+        }
+        if (TR::phong) {
+            n0 = ws.f[SS_N0][s]; n1 = ws.f[SS_N1][s]; n2 = ws.f[SS_N2][s];
+            IN0 = ws.f[SS_IN0][s]; IN1 = ws.f[SS_IN1][s]; IN2 = ws.f[SS_IN2][s];
+        }
+        if (TR::color) {
+            c0 = ws.f[SS_C0][s]; c1 = ws.f[SS_C1][s]; c2 = ws.f[SS_C2][s]; c3 = ws.f[SS_C3][s];
+            IC0 = ws.f[SS_IC0][s]; IC1 = ws.f[SS_IC1][s]; IC2 = ws.f[SS_IC2][s]; IC3 = ws.f[SS_IC3][s];
+        }
     }
-    for (int32_t x = MinX; x < xb; ++x) {  // 423: sequential per-pixel stepping
-        if (x >= xa) {
-            const int p = rowoff + x;
+    for (int32_t x = MinX; x < xend; ++x) {  // 423: sequential per-pixel stepping
+        if ((x >= xa && x < xb) || x == W) {
+            const int p = x == W ? povf : rowoff + x;
             if (!SHADE) {
                 if (z == z) atomicMax(&tc.key[p], make_key(z, tag));
             } else if (is_winner(tc, p, tag)) {
                 float C[4] = {c0, c1, c2, c3};
                 if (TR::tex) {  // 427-446
-                    const float s = 1.0f / w;
-                    const float FU = s * u, FV = s * v;
+                    const float sc = 1.0f / w;
+                    const float FU = sc * u, FV = sc * v;
                     const int32_t TX = round_s32(FU * (float)(tex.w - 1));
                     const int32_t TY = round_s32(FV * (float)(tex.h - 1));
-                    const uint32_t t = texel_at(tex, (int32_t)((uint32_t)TX * 4u + (uint32_t)TY * (uint32_t)tex.pitch));
+                    const uint32_t t =
+                        texel_at(tex, (int32_t)((uint32_t)TX * 4u + (uint32_t)TY * (uint32_t)tex.pitch));
                     C[3] = (float)((t >> 24) & 0xFF) / 255.0f;
                     C[0] = (float)((t >> 16) & 0xFF) / 255.0f;
                     C[1] = (float)((t >> 8) & 0xFF) / 255.0f;
@@ -381,8 +540,7 @@ __device__ __forceinline__ void span_scalar(const FrameParams &fp, const TexRec 
                 put_winner(tc, p, z, packed);
             }
         }
-        // per-pixel step (504-510 / 530-535)
-        if (SHADE) {
+        if (SHADE) {  // per-pixel step (504-510 / 530-535)
             if (TR::phong) {
                 float a = n0 + IN0, b = n1 + IN1, c = n2 + IN2;
                 normalize_rcp(a, b, c);
@@ -395,42 +553,99 @@ __device__ __forceinline__ void span_scalar(const FrameParams &fp, const TexRec 
     }
 }
 
-template <int M, bool SHADE>
-__device__ __forceinline__ void raster_tri(const FrameParams &fp, const TileCtx &tc, uint32_t g) {
-    const DrawRec *d;
-    uint32_t gt;
-    resolve_draw(fp, g, d, gt);
-    Edge s0, s1, s2;
-    const int n = setup_triangle<M>(*d, gt, fp, s0, s1, s2);
-    if (n < 2) return;
-    const uint32_t tag = 0xFFFFFFFEu - g;
-    TexRec tex;
-    if (ModeTraits<M>::tex) tex = fp.texs[d->tex];
-    else { tex.mem = nullptr; tex.w = tex.h = tex.pitch = 0; tex.pad = 0; }
-    aet_walk<M>(n, s0, s1, s2, fp.H, tc.y0, tc.y1, [&](const Edge &L, const Edge &R, int32_t Row) {
-        if (M == MODE_AVX) span_avx<SHADE>(fp, tex, tc, tag, L, R, Row);
-        else span_scalar<M, SHADE>(fp, tex, tc, tag, L, R, Row);
-    });
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
 }
 
-template <bool SHADE>
-__device__ __forceinline__ void raster_entry(const FrameParams &fp, const TileCtx &tc, uint32_t g) {
-    const DrawRec *d;
-    uint32_t gt;
-    resolve_draw(fp, g, d, gt);
-    switch (d->mode) {
-        case MODE_AVX: raster_tri<MODE_AVX, SHADE>(fp, tc, g); break;
-        case MODE_SC_GOURAUD: raster_tri<MODE_SC_GOURAUD, SHADE>(fp, tc, g); break;
-        case MODE_SC_GOURAUD_TEX: raster_tri<MODE_SC_GOURAUD_TEX, SHADE>(fp, tc, g); break;
-        case MODE_SC_PHONG: raster_tri<MODE_SC_PHONG, SHADE>(fp, tc, g); break;
-        case MODE_SC_PHONG_TEX: raster_tri<MODE_SC_PHONG_TEX, SHADE>(fp, tc, g); break;
-        default: break;
+// One sweep over the tile's bin for mode M.  SHADE=false: visibility keys;
+// SHADE=true: shade the winners.
+template <int M, bool SHADE>
+__device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, WaveSlots &ws,
+                                      const uint32_t *__restrict__ bins, uint32_t b0, uint32_t b1,
+                                      uint32_t *anomaly) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const bool col0 = tc.x0 == 0 && M != MODE_AVX;
+    const int32_t ystart = col0 ? tc.y0 - 1 : tc.y0;  // scalar: (row-1) may store into (row, 0)
+    for (uint32_t base = b0 + wave * 64; base < b1; base += 64 * kWaves) {
+        const uint32_t e = base + lane;
+        bool active = e < b1;
+        uint32_t g = 0;
+        const DrawRec *d = fp.draws;
+        Walker<M, SHADE> wk;
+        uint32_t anom = 0;
+        if (active) {
+            g = bins[e];
+            uint32_t gt;
+            resolve_draw(fp, g, d, gt);
+            Edge s0, s1, s2;
+            // (mixed frames sweep the bin once per mode)
+            const int n = d->mode == M ? setup_triangle<M>(*d, gt, fp, s0, s1, s2) : 0;
+            active = n >= 2;
+            if (active) {
+                wk.init(n, s0, s1, s2, fp.H, tc.y1, anom);
+                // Replay the rows above the tile (edge DDA only).
+                while (wk.Row < ystart && wk.Row < wk.MaxY) wk.end_row(wk.begin_row());
+                active = wk.Row < wk.MaxY;
+            }
+        }
+        if (anom) atomicAdd(anomaly, anom);
+        const int32_t texi = (ModeTraits<M>::tex && active) ? d->tex : 0;
+        const uint32_t tag = 0xFFFFFFFEu - g;
+        for (int32_t r = ystart; r < tc.y1; ++r) {
+            int items = 0;
+            if (active && wk.Row == r) {
+                const bool paired = wk.begin_row();
+                if (paired) {
+                    if (M == MODE_AVX) items = span_setup_avx<SHADE>(fp, tc, ws, lane, tag, texi, wk.L0, wk.L1, r);
+                    else items = span_setup_scalar<M, SHADE>(fp, tc, ws, lane, tag, texi, wk.L0, wk.L1, r);
+                }
+                wk.end_row(paired);
+                active = wk.Row < wk.MaxY;
+            }
+            const int incl = wave_incl_scan(items, lane);
+            const int total = __shfl(incl, 63, 64);
+            ws.i[SI_PRE][lane] = incl;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int it0 = 0; it0 < total; it0 += 64) {
+                const int it = it0 + lane;
+                if (it < total) {
+                    int lo = 0, hi = 63;  // first slot whose inclusive prefix exceeds it
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        if (ws.i[SI_PRE][mid] > it) hi = mid; else lo = mid + 1;
+                    }
+                    const int j = it - (lo ? ws.i[SI_PRE][lo - 1] : 0);
+                    if (M == MODE_AVX) item_avx<SHADE>(fp, tc, ws, lo, j);
+                    else item_scalar<M, SHADE>(fp, tc, ws, lo);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (!__any(active)) break;
+        }
     }
 }
 
-template <int MODESET>  // MODESET: MODE_AVX..MODE_SC_PHONG_TEX (single mode) or -1 (any)
-__global__ void __launch_bounds__(256) k_raster(FrameParams fp, const uint32_t *__restrict__ offs,
-                                                const uint32_t *__restrict__ bins) {
+template <int M>
+__device__ __forceinline__ void raster_mode(const FrameParams &fp, const TileCtx &tc, WaveSlots &ws,
+                                            const uint32_t *bins, uint32_t b0, uint32_t b1, uint32_t *anomaly,
+                                            bool shade) {
+    if (!shade) sweep<M, false>(fp, tc, ws, bins, b0, b1, anomaly);
+    else sweep<M, true>(fp, tc, ws, bins, b0, b1, anomaly);
+}
+
+template <int MODESET>  // a single Mode, or -1: any mode (per-draw dispatch)
+__global__ void __launch_bounds__(256, PRK_RASTER_MIN_WAVES) k_raster(FrameParams fp, const uint32_t *__restrict__ offs,
+                                                const uint32_t *__restrict__ bins,
+                                                uint32_t *__restrict__ anomaly) {
     extern __shared__ unsigned long long lds[];
     const int ntile = fp.tiles_x * fp.tiles_y;
     const int t = blockIdx.x;
@@ -447,6 +662,8 @@ __global__ void __launch_bounds__(256) k_raster(FrameParams fp, const uint32_t *
     const int npx = fp.tile_w * fp.tile_h;
     tc.key = lds;
     tc.ocol = reinterpret_cast<uint32_t *>(lds + npx);
+    WaveSlots *slots = reinterpret_cast<WaveSlots *>(tc.ocol + npx);
+    WaveSlots &ws = slots[threadIdx.x >> 6];
 
     // Prior z of the target: a fragment must beat it strictly.
     for (int p = threadIdx.x; p < npx; p += blockDim.x) {
@@ -460,16 +677,20 @@ __global__ void __launch_bounds__(256) k_raster(FrameParams fp, const uint32_t *
         tc.key[p] = k;
     }
     __syncthreads();
-    for (uint32_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
-        if constexpr (MODESET >= 0) raster_tri<(MODESET >= 0 ? MODESET : 0), false>(fp, tc, bins[i]);
-        else raster_entry<false>(fp, tc, bins[i]);
+    for (int pass = 0; pass < 2; ++pass) {
+        const bool shade = pass == 1;
+        if constexpr (MODESET >= 0) {
+            raster_mode<(MODESET >= 0 ? MODESET : 0)>(fp, tc, ws, bins, b0, b1, anomaly, shade);
+        } else {
+            // Mixed frame: each mode sweeps the bin and skips other modes' entries.
+            raster_mode<MODE_AVX>(fp, tc, ws, bins, b0, b1, anomaly, shade);
+            raster_mode<MODE_SC_GOURAUD>(fp, tc, ws, bins, b0, b1, anomaly, shade);
+            raster_mode<MODE_SC_GOURAUD_TEX>(fp, tc, ws, bins, b0, b1, anomaly, shade);
+            raster_mode<MODE_SC_PHONG>(fp, tc, ws, bins, b0, b1, anomaly, shade);
+            raster_mode<MODE_SC_PHONG_TEX>(fp, tc, ws, bins, b0, b1, anomaly, shade);
+        }
+        __syncthreads();
     }
-    __syncthreads();
-    for (uint32_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
-        if constexpr (MODESET >= 0) raster_tri<(MODESET >= 0 ? MODESET : 0), true>(fp, tc, bins[i]);
-        else raster_entry<true>(fp, tc, bins[i]);
-    }
-    __syncthreads();
     // Flush: every pixel with a winner gets its z and colour.
     for (int p = threadIdx.x; p < npx; p += blockDim.x) {
         const int lx = p % fp.tile_w, ly = p / fp.tile_w;
@@ -488,10 +709,10 @@ __global__ void __launch_bounds__(256) k_raster(FrameParams fp, const uint32_t *
 }
 
 // Explicit instantiations used by the host.
-template __global__ void k_raster<-1>(FrameParams, const uint32_t *, const uint32_t *);
-template __global__ void k_raster<MODE_AVX>(FrameParams, const uint32_t *, const uint32_t *);
-template __global__ void k_raster<MODE_SC_GOURAUD>(FrameParams, const uint32_t *, const uint32_t *);
-template __global__ void k_raster<MODE_SC_PHONG>(FrameParams, const uint32_t *, const uint32_t *);
+template __global__ void k_raster<-1>(FrameParams, const uint32_t *, const uint32_t *, uint32_t *);
+template __global__ void k_raster<MODE_AVX>(FrameParams, const uint32_t *, const uint32_t *, uint32_t *);
+template __global__ void k_raster<MODE_SC_GOURAUD>(FrameParams, const uint32_t *, const uint32_t *, uint32_t *);
+template __global__ void k_raster<MODE_SC_PHONG>(FrameParams, const uint32_t *, const uint32_t *, uint32_t *);
 
 }  // namespace prk
 
@@ -529,24 +750,26 @@ hipError_t prk_launch_fill(const prk::FrameParams *fp, const void *ranges, const
 }
 
 hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint32_t *offs,
-                             const uint32_t *bins, hipStream_t s) {
+                             const uint32_t *bins, uint32_t *anomaly, hipStream_t s) {
     const uint32_t ntile = (uint32_t)(fp->tiles_x * fp->tiles_y);
     if (ntile == 0) return hipSuccess;
-    const size_t lds = (size_t)fp->tile_w * fp->tile_h * (sizeof(unsigned long long) + sizeof(uint32_t));
+    const size_t lds = (size_t)fp->tile_w * fp->tile_h * (sizeof(unsigned long long) + sizeof(uint32_t)) +
+                       prk::kWaves * sizeof(prk::WaveSlots);
     switch (modeset) {
         case prk::MODE_AVX:
-            hipLaunchKernelGGL(prk::k_raster<prk::MODE_AVX>, dim3(ntile), dim3(256), lds, s, *fp, offs, bins);
+            hipLaunchKernelGGL(prk::k_raster<prk::MODE_AVX>, dim3(ntile), dim3(256), lds, s, *fp, offs, bins,
+                               anomaly);
             break;
         case prk::MODE_SC_GOURAUD:
             hipLaunchKernelGGL(prk::k_raster<prk::MODE_SC_GOURAUD>, dim3(ntile), dim3(256), lds, s, *fp, offs,
-                               bins);
+                               bins, anomaly);
             break;
         case prk::MODE_SC_PHONG:
             hipLaunchKernelGGL(prk::k_raster<prk::MODE_SC_PHONG>, dim3(ntile), dim3(256), lds, s, *fp, offs,
-                               bins);
+                               bins, anomaly);
             break;
         default:
-            hipLaunchKernelGGL(prk::k_raster<-1>, dim3(ntile), dim3(256), lds, s, *fp, offs, bins);
+            hipLaunchKernelGGL(prk::k_raster<-1>, dim3(ntile), dim3(256), lds, s, *fp, offs, bins, anomaly);
             break;
     }
     return hipGetLastError();

@@ -23,7 +23,7 @@ from . import abi
 from .abi import PRK_SEM_AVX, PRK_SEM_SCALAR  # noqa: F401
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "libprk_hip.so")
+LIB_PATH = os.environ.get("PRK_LIB") or os.path.join(os.path.dirname(_HERE), "libprk_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "prk.h")
 
 _LIB = None
@@ -59,6 +59,7 @@ _SIGS = {
     "prk_reset_draws": (C.c_int, [C.c_void_p]),
     "prk_synchronize": (C.c_int, [C.c_void_p]),
     "prk_get_stats": (C.c_int, [C.c_void_p, C.POINTER(abi.PrkStats)]),
+    "prk_timing_reset": (C.c_int, [C.c_void_p]),
     "prk_set_debug": (C.c_int, [C.c_void_p, C.c_int32]),
     "prk_download_winners": (C.c_int, [C.c_void_p, C.c_void_p]),
     "prk_set_tile": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
@@ -234,6 +235,9 @@ class Renderer:
 
     def synchronize(self):
         _check("prk_synchronize", self._L.prk_synchronize(self._h))
+
+    def timing_reset(self):
+        _check("prk_timing_reset", self._L.prk_timing_reset(self._h))
 
     def stats(self):
         s = abi.PrkStats()

@@ -83,15 +83,22 @@ typedef struct prk_bitmap {
     int32_t Pitch;
 } prk_bitmap;
 
-/* Frame statistics of the last prk_flush. */
+/* Frame statistics.  Kernel times come from HIP events recorded on the
+ * launch stream around the binning and raster kernels of every flush; they
+ * are harvested without stalling the stream and accumulated until
+ * prk_timing_reset. */
 typedef struct prk_stats {
-    uint64_t triangles;      /* triangles submitted                    */
-    uint64_t bin_entries;    /* (triangle, tile) pairs rasterised      */
+    uint64_t triangles;      /* triangles of the last flush            */
+    uint64_t bin_entries;    /* (triangle, tile) pairs of the last flush */
     uint32_t tiles;          /* tiles in the render target band        */
-    uint32_t max_bin;        /* largest per-tile bin                   */
-    float ms_bin;            /* device time: project/cull/bin          */
-    float ms_raster;         /* device time: tile raster+shade kernel  */
-    float ms_total;          /* device time: whole flush               */
+    uint32_t frames_timed;   /* flushes accumulated in sum_ms_*        */
+    float ms_bin;            /* last flush: project/cull/bin kernels   */
+    float ms_raster;         /* last flush: tile raster+shade kernel   */
+    double sum_ms_bin;       /* accumulated since prk_timing_reset     */
+    double sum_ms_raster;
+    uint32_t anomalies;      /* triangles whose AET left the proven
+                                per-triangle shape (always 0) */
+    uint32_t pad;
 } prk_stats;
 
 typedef struct prk_context prk_context;
@@ -157,7 +164,8 @@ int prk_flush(prk_context *ctx, void *stream);
 /* Drop recorded draws without executing them. */
 int prk_reset_draws(prk_context *ctx);
 int prk_synchronize(prk_context *ctx);
-int prk_get_stats(prk_context *ctx, prk_stats *out);
+int prk_get_stats(prk_context *ctx, prk_stats *out); /* waits for timed flushes */
+int prk_timing_reset(prk_context *ctx);
 
 /* Debug/test: per-pixel winning triangle index of the last flush (-1 = none),
  * rows [row0,row1).  Requires prk_set_debug(ctx, 1) before the flush. */

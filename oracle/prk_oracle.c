@@ -135,6 +135,12 @@ typedef struct or_ctx {
     uint64_t Spans, SpanPixels, Writes;
 } or_ctx;
 
+/* Does this call draw frame row r?  (band filter used by the threaded driver) */
+static inline int or_owns(const or_ctx *X_, int32_t r)
+{
+    return r >= X_->RowLo && r < X_->RowHi && (r / X_->BandH) % X_->BandMod == X_->BandRem;
+}
+
 /* ------------------------------------------------------------------ */
 /* ProjectVertex (projekt.cpp:74-93).                                  */
 /* ------------------------------------------------------------------ */
@@ -328,6 +334,7 @@ static inline uint32_t or_texel(const prk_bitmap *B, int32_t off)
 /* ------------------------------------------------------------------ */
 static void or_fill_line_optimized(or_ctx *X_, const or_edge *L, const or_edge *R, int32_t Row)
 {
+    if (!or_owns(X_, Row)) return;
     const prk_bitmap *Bm = X_->Bitmap;
     const prk_transform *T = X_->T;
     const int32_t W = X_->Width;
@@ -515,13 +522,23 @@ static void or_fill_line_scalar(or_ctx *X_, const or_edge *L, const or_edge *R, 
     for (int c = 0; c < 3; ++c) CurN[c] += XOffset * IncN[c];
     for (int c = 0; c < 4; ++c) CurC[c] += XOffset * IncC[c];
 
-    if (MaxX >= MinX) X_->SpanPixels += (uint64_t)(MaxX - MinX + 1);
-    X_->Spans++;
+    if (or_owns(X_, Row)) {
+        if (MaxX >= MinX) X_->SpanPixels += (uint64_t)(MaxX - MinX + 1);
+        X_->Spans++;
+    }
     uint32_t *rowp = (uint32_t *)((uint8_t *)X_->Color + (size_t)Row * X_->Pitch);
     float *zrow = X_->Z + (size_t)Row * W;
     const float InvM2P = 1.0f / T->MetersToPixels;
 
+    /* MaxX can round to Width (RightX in [W-0.5, W) is not clamped, 389-399),
+     * so the inclusive loop stores one pixel past the row: linear index
+     * Row*W + W, i.e. pixel (Row+1, 0) of the z-buffer (and of the colour
+     * buffer when Pitch == 4*W).  On the last row that store lands outside
+     * the buffers (undefined in the reference): pinned as dropped. */
+    const int own_row = or_owns(X_, Row);
+    const int own_next = Row + 1 < X_->Height && or_owns(X_, Row + 1);
     for (int32_t X = MinX; X <= MaxX; ++X) { /* 423 */
+        const int draw = X < W ? own_row : own_next;
         if (Bm) { /* 427-446 */
             float s = 1.0f / CurW;
             float FU = s * CurU, FV = s * CurV;
@@ -561,7 +578,7 @@ static void or_fill_line_scalar(or_ctx *X_, const or_edge *L, const or_edge *R, 
         }
         uint32_t Packed = (or_round_u32(F[3] * 255.0f) << 24) | (or_round_u32(F[0] * 255.0f) << 16) |
                           (or_round_u32(F[1] * 255.0f) << 8) | (or_round_u32(F[2] * 255.0f) << 0);
-        if (CurZ > zrow[X]) { /* 495 / 525 */
+        if (draw && CurZ > zrow[X]) { /* 495 / 525 */
             zrow[X] = CurZ;
             rowp[X] = Packed;
             if (X_->Winners) X_->Winners[(size_t)Row * W + X] = X_->TriIndex;
@@ -680,7 +697,7 @@ static void or_aet_walk(or_ctx *X_, or_edge *Edges, uint32_t EdgeCount, or_span_
         or_edge *PrevCur = NULL, *PrevNext = NULL; /* pairing 3751-3869 */
         or_edge *Cur = Head, *Next = Cur->Next;
         while (Next) {
-            if (Row >= X_->RowLo && (Row / X_->BandH) % X_->BandMod == X_->BandRem) {
+            if (or_owns(X_, Row) || (Span == or_fill_line_scalar && or_owns(X_, Row + 1))) {
                 or_edge a = *Cur, b = *Next; /* by-value copies (3759-3807) */
                 a.Next = b.Next = NULL;
                 Span(X_, &a, &b, Row);
@@ -786,6 +803,7 @@ static int or_draw_filtered(const or_draw_desc *D, const or_target *Tg, const pr
              * speed-up: the walk of such an object never reaches Span). */
             int32_t lo, hi;
             or_object_rows(D, t0, n, T, &lo, &hi);
+            if (D->Semantics == PRK_SEM_SCALAR && hi < INT32_MAX / 2) hi += 1; /* row-overflow pixel */
             if (lo < row_lo) lo = row_lo;
             if (hi > row_hi) hi = row_hi;
             if (lo >= hi) continue;
