@@ -113,8 +113,8 @@ def main():
 
     W, H = a.width, a.height
     scene = scenes.random_soup(a.tris, W, H, radius=a.radius, seed=a.seed, textured=True)
-    row0 = H * rank // world
-    row1 = H * (rank + 1) // world
+    from prk.dist import band_rows
+    row0, row1 = band_rows(rank, world, H)
     rows = row1 - row0
 
     color = torch.empty((rows, W), dtype=torch.int32, device=dev)
@@ -128,10 +128,8 @@ def main():
     geom = r.geometry(scene.vertices, None, scene.normals, scene.uvs)  # AVX path: no colours read
     tex = r.texture(scene.texture)
     stream = torch.cuda.current_stream().cuda_stream
-    full = None
-    if world > 1 and rank == 0:
-        full = [torch.empty((H // world if H % world == 0 else rows, W), dtype=torch.int32, device=dev)
-                for _ in range(world)]
+    from prk import dist as pdist
+    frame = torch.empty((H, W), dtype=torch.int32, device=dev) if (world > 1 and rank == 0) else None
     zmin = -float(np.finfo(np.float32).max)
 
     def step():
@@ -139,8 +137,8 @@ def main():
         zbuf.fill_(zmin)
         r.draw_model_optimized(geom, scene.tri_count, bitmap=tex, phong=True)
         r.complete_all_work(stream)
-        if world > 1:
-            dist.gather(color, full if rank == 0 else None, dst=0)
+        if world > 1:  # RCCL over xGMI: strips -> rank 0's frame
+            pdist.gather_strips(dist, color, rank, world, H, out=frame)
 
     for _ in range(a.warmup):
         step()

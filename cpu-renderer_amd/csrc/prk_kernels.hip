@@ -23,6 +23,11 @@
 //                every pixel that got a winner.
 #include "prk_device.h"
 
+// Diagnostic builds only (tools/diag): 1 = skip the shading sweep, 2 = skip
+// work items, 4 = skip the AET rows (setup only).  Never set in a product build.
+#ifndef PRK_DIAG
+#define PRK_DIAG 0
+#endif
 #ifndef PRK_RASTER_MIN_WAVES
 #define PRK_RASTER_MIN_WAVES 2  // waves per SIMD the raster kernel is register-budgeted for
 #endif
@@ -596,6 +601,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
         if (anom) atomicAdd(anomaly, anom);
         const int32_t texi = (ModeTraits<M>::tex && active) ? d->tex : 0;
         const uint32_t tag = 0xFFFFFFFEu - g;
+        if (PRK_DIAG & 4) active = false;
         for (int32_t r = ystart; r < tc.y1; ++r) {
             int items = 0;
             if (active && wk.Row == r) {
@@ -613,7 +619,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (int it0 = 0; it0 < total; it0 += 64) {
+            for (int it0 = 0; it0 < ((PRK_DIAG & 2) ? 0 : total); it0 += 64) {
                 const int it = it0 + lane;
                 if (it < total) {
                     int lo = 0, hi = 63;  // first slot whose inclusive prefix exceeds it
@@ -677,7 +683,7 @@ __global__ void __launch_bounds__(256, PRK_RASTER_MIN_WAVES) k_raster(FrameParam
         tc.key[p] = k;
     }
     __syncthreads();
-    for (int pass = 0; pass < 2; ++pass) {
+    for (int pass = 0; pass < ((PRK_DIAG & 1) ? 1 : 2); ++pass) {
         const bool shade = pass == 1;
         if constexpr (MODESET >= 0) {
             raster_mode<(MODESET >= 0 ? MODESET : 0)>(fp, tc, ws, bins, b0, b1, anomaly, shade);

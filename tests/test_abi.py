@@ -1,0 +1,94 @@
+"""CPU tests of the C-ABI boundary (no GPU compute).
+
+* libprk_hip.so loads and exports every entry point include/prk.h declares.
+* The product library does not link the oracle.
+* Host-only entry points work without a device (ConstructSphere, argument
+  checks); compute entry points fail loudly (PRK_ERR_DEVICE) when no GPU is
+  visible instead of falling back to the CPU.
+* The C++ drop-in header (include/projekt.h) compiles against the reference's
+  call pattern (examples/dropin_demo.cpp) and links against the library.
+"""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import prk
+from prk import abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared():
+    with open(os.path.join(ROOT, "include", "prk.h")) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(prk_[a-z_]+)\s*\(", src)))
+
+
+def test_every_declared_symbol_is_exported():
+    names = declared()
+    assert len(names) >= 20
+    lib = C.CDLL(prk.LIB_PATH)
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(prk.exported_symbols())
+    out = subprocess.run(["nm", "-D", "--defined-only", prk.LIB_PATH], capture_output=True, text=True).stdout
+    for n in names:
+        assert re.search(r"\bT %s$" % n, out, re.M), n
+
+
+def test_product_does_not_link_the_oracle():
+    out = subprocess.run(["readelf", "-d", prk.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle" not in out
+    assert "libamdhip64" in out  # the HIP runtime is the compute path
+
+
+def test_struct_layouts_match_header():
+    assert C.sizeof(abi.PrkTransform) == 20
+    assert C.sizeof(abi.PrkLightInfo) == 28
+    assert C.sizeof(abi.PrkLightData) == 4 + 16 + 8 * 28
+    assert C.sizeof(abi.PrkBitmap) == 8 + 12 + 4  # pointer + 3 ints (+ tail padding)
+
+
+def test_argument_errors_without_device():
+    L = prk.lib()
+    assert L.prk_destroy(None) == abi.PRK_ERR_ARG
+    assert L.prk_device_count(None) == abi.PRK_ERR_ARG
+    assert L.prk_create(0, None) == abi.PRK_ERR_ARG
+    assert L.prk_construct_sphere(None, None, None, None, None) == abi.PRK_ERR_ARG
+    assert L.prk_version() .startswith(b"prk")
+
+
+def test_construct_sphere_host():
+    V, Cc, N, UV = prk.construct_sphere()
+    assert V.shape == (6624, 3)
+    r = np.linalg.norm(V, axis=1)
+    assert np.allclose(r, 0.5, atol=1e-5)           # Radius*FirstVertex, r = 0.5 (4127)
+    assert np.allclose(np.linalg.norm(N, axis=1), 1.0, atol=1e-5)
+    assert np.array_equal(Cc[0], np.array([1, 0, 1, 1], np.float32))  # UpColor + Blue(az 0)
+
+
+@pytest.mark.skipif(os.environ.get("PRK_EXPECT_GPU") == "1", reason="GPU box")
+def test_compute_fails_loudly_without_gpu():
+    if prk.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(prk.PrkError) as e:
+        prk.Renderer()
+    assert e.value.code == abi.PRK_ERR_DEVICE
+
+
+def test_dropin_header_builds_and_links(tmp_path):
+    exe = tmp_path / "dropin_demo"
+    r = subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "examples", "dropin_demo.cpp"), "-L",
+                        os.path.join(ROOT, "cpu-renderer_amd"), "-lprk_hip",
+                        "-Wl,-rpath," + os.path.join(ROOT, "cpu-renderer_amd"), "-o", str(exe)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    if prk.device_count() == 0:
+        run = subprocess.run([str(exe), str(tmp_path / "c"), str(tmp_path / "z")], capture_output=True, text=True)
+        assert run.returncode == 2 and "no HIP device" in run.stderr
