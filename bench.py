@@ -206,7 +206,7 @@ def main():
                    "width": W, "height": H, "triangles": T, "radius_px": a.radius,
                    "lights": len(scene.lights), "texture": "256x256",
                    "parallelism": "row bands x%d + RCCL gather" % world if world > 1 else "1 GPU",
-                   "tile": a.tile or "64x32"},
+                   "tile": a.tile or "256x8"},
         "mtri_per_s": T / (ms * 1e-3) / 1e6,
         "ms_bin": ms_bin,
         "ms_raster": ms_raster,

@@ -21,12 +21,11 @@
 
 extern "C" {
 hipError_t prk_launch_tri_draw(const prk::DrawRec *, uint32_t, uint32_t *, uint32_t, hipStream_t);
-hipError_t prk_launch_bin(const prk::FrameParams *, uint32_t *, uint32_t *, uint32_t *, void *, uint32_t,
-                          hipStream_t);
-hipError_t prk_launch_fill(const prk::FrameParams *, const void *, const uint32_t *, uint32_t *, uint32_t *,
-                           hipStream_t);
-hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, const uint32_t *, uint32_t *,
-                             hipStream_t);
+hipError_t prk_bin_phase1(const prk::FrameParams *, uint32_t *, uint32_t *, void *, void *, size_t *, hipStream_t);
+hipError_t prk_bin_phase2(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, uint32_t *, uint32_t *,
+                          uint32_t *, uint32_t *, uint32_t *, void *, size_t *, hipStream_t);
+hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, const uint32_t *, uint8_t *,
+                             uint32_t *, uint32_t *, hipStream_t);
 }
 
 namespace {
@@ -89,9 +88,10 @@ struct prk_context {
     std::vector<prk::DrawRec> draws;
     uint32_t pending_tris = 0;
     // scratch
-    DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_counts, d_offs, d_cursor, d_bins, d_winners, d_anomaly;
+    DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_tri_n, d_tri_off, d_keys_a, d_vals_a, d_keys_b, d_bins,
+        d_offs, d_won, d_list, d_temp, d_winners, d_anomaly;
     uint32_t *h_total = nullptr;  // pinned
-    int32_t tile_w = 64, tile_h = 32;
+    int32_t tile_w = 256, tile_h = 8;  // measured best for C3b
     bool debug = false;
     bool winners_valid = false;
     prk_stats stats{};
@@ -160,8 +160,9 @@ int prk_destroy(prk_context *c) {
         (void)hipFree(c->color);
         (void)hipFree(c->zbuf);
     }
-    DevBuf *bufs[] = {&c->d_draws, &c->d_texs, &c->d_tri_draw, &c->d_ranges, &c->d_counts,
-                      &c->d_offs,  &c->d_cursor, &c->d_bins, &c->d_winners, &c->d_anomaly};
+    DevBuf *bufs[] = {&c->d_draws,  &c->d_texs,   &c->d_tri_draw, &c->d_ranges, &c->d_tri_n, &c->d_tri_off,
+                      &c->d_keys_a, &c->d_vals_a, &c->d_keys_b,   &c->d_bins,   &c->d_offs,  &c->d_won,
+                      &c->d_list,   &c->d_temp,   &c->d_winners,  &c->d_anomaly};
     for (DevBuf *b : bufs) b->release();
     if (c->h_total) (void)hipHostFree(c->h_total);
     for (auto &slot : c->ev)
@@ -534,30 +535,44 @@ int prk_flush(prk_context *c, void *stream) {
         fp.tri_draw = (const uint32_t *)c->d_tri_draw.p;
     }
     PRK_TRY(c->d_ranges.ensure((size_t)T * 16));
-    PRK_TRY(c->d_counts.ensure((size_t)ntiles * 4));
+    PRK_TRY(c->d_tri_n.ensure((size_t)(T + 1) * 4));
+    PRK_TRY(c->d_tri_off.ensure((size_t)(T + 1) * 4));
     PRK_TRY(c->d_offs.ensure((size_t)(ntiles + 1) * 4));
-    PRK_TRY(c->d_cursor.ensure((size_t)ntiles * 4));
-    PRK_TRY(hipMemsetAsync(c->d_counts.p, 0, (size_t)ntiles * 4, s));
-    PRK_TRY(hipMemsetAsync(c->d_cursor.p, 0, (size_t)ntiles * 4, s));
+    size_t scan_bytes = 0;
+    PRK_TRY(prk_bin_phase1(&fp, nullptr, nullptr, nullptr, nullptr, &scan_bytes, s));
+    PRK_TRY(c->d_temp.ensure(scan_bytes));
     PRK_TRY(hipEventRecord(c->ev[slot][0], s));
-    PRK_TRY(prk_launch_bin(&fp, (uint32_t *)c->d_counts.p, (uint32_t *)c->d_offs.p, (uint32_t *)c->d_cursor.p,
-                           c->d_ranges.p, ntiles, s));
+    PRK_TRY(prk_bin_phase1(&fp, (uint32_t *)c->d_tri_n.p, (uint32_t *)c->d_tri_off.p, c->d_ranges.p, c->d_temp.p,
+                           &scan_bytes, s));
     // The bin array size is data dependent: read the total back (one small
-    // D2H copy per frame) and grow the buffer if needed.
-    PRK_TRY(hipMemcpyAsync(c->h_total, (uint32_t *)c->d_offs.p + ntiles, 4, hipMemcpyDeviceToHost, s));
+    // D2H copy per frame) and grow the buffers if needed.
+    PRK_TRY(hipMemcpyAsync(c->h_total, (uint32_t *)c->d_tri_off.p + T, 4, hipMemcpyDeviceToHost, s));
     PRK_TRY(hipStreamSynchronize(s));
     const uint32_t total = *c->h_total;
     c->stats.bin_entries = total;
-    PRK_TRY(c->d_bins.ensure((size_t)std::max<uint32_t>(total, 1) * 4));
-    PRK_TRY(prk_launch_fill(&fp, c->d_ranges.p, (const uint32_t *)c->d_offs.p, (uint32_t *)c->d_cursor.p,
-                            (uint32_t *)c->d_bins.p, s));
+    const size_t ne = (size_t)std::max<uint32_t>(total, 1);
+    PRK_TRY(c->d_keys_a.ensure(ne * 4));
+    PRK_TRY(c->d_vals_a.ensure(ne * 4));
+    PRK_TRY(c->d_keys_b.ensure(ne * 4));
+    PRK_TRY(c->d_bins.ensure(ne * 4));
+    PRK_TRY(c->d_list.ensure(ne * 4));
+    PRK_TRY(c->d_won.ensure(ne));
+    size_t sort_bytes = 0;
+    PRK_TRY(prk_bin_phase2(&fp, c->d_ranges.p, (const uint32_t *)c->d_tri_off.p, total, (uint32_t *)c->d_keys_a.p,
+                           (uint32_t *)c->d_vals_a.p, (uint32_t *)c->d_keys_b.p, (uint32_t *)c->d_bins.p,
+                           (uint32_t *)c->d_offs.p, nullptr, &sort_bytes, s));
+    PRK_TRY(c->d_temp.ensure(std::max(sort_bytes, scan_bytes)));
+    PRK_TRY(prk_bin_phase2(&fp, c->d_ranges.p, (const uint32_t *)c->d_tri_off.p, total, (uint32_t *)c->d_keys_a.p,
+                           (uint32_t *)c->d_vals_a.p, (uint32_t *)c->d_keys_b.p, (uint32_t *)c->d_bins.p,
+                           (uint32_t *)c->d_offs.p, c->d_temp.p, &sort_bytes, s));
+    PRK_TRY(hipMemsetAsync(c->d_won.p, 0, ne, s));
     PRK_TRY(hipEventRecord(c->ev[slot][1], s));
     if (!c->d_anomaly.p) {
         PRK_TRY(c->d_anomaly.ensure(4));
         PRK_TRY(hipMemsetAsync(c->d_anomaly.p, 0, 4, s));
     }
     PRK_TRY(prk_launch_raster(&fp, modeset, (const uint32_t *)c->d_offs.p, (const uint32_t *)c->d_bins.p,
-                              (uint32_t *)c->d_anomaly.p, s));
+                              (uint8_t *)c->d_won.p, (uint32_t *)c->d_list.p, (uint32_t *)c->d_anomaly.p, s));
     PRK_TRY(hipEventRecord(c->ev[slot][2], s));
     c->pending[slot] = true;
     c->last_slot = slot;

@@ -1,0 +1,180 @@
+// prk_bin.hip — triangle -> tile binning with bins in submission order.
+//
+//   k_bin_count   1 thread / triangle: ProjectVertex + back-face cull
+//                 (projekt.cpp:74-93, 3926-3943) -> conservative tile range ->
+//                 number of (triangle, tile) entries.
+//   scan          exclusive sum of the per-triangle counts (hipcub).
+//   k_bin_emit    1 thread / triangle: write (tile, triangle) pairs at the
+//                 triangle's offset, i.e. in triangle order.
+//   sort          stable LSD radix sort of the pairs by tile (hipcub), so every
+//                 tile's bin lists its triangles in submission order.
+//   k_tile_offsets  bin start of every tile (lower_bound on the sorted tiles).
+//
+// Triangle-ordered bins let k_raster name a triangle by its position in the
+// tile's bin (entry order == submission order), which it uses to skip, in the
+// shading sweep, every triangle that won no pixel of the tile.
+#include <hipcub/hipcub.hpp>
+
+#include "prk_device.h"
+
+namespace prk {
+
+// Conservative tile range of a triangle's covered pixels.  Span end points
+// are edge-DDA values that stay on their segment up to float error
+// (DESIGN.md §4.1), so [min x, max x] of the projected vertices widened by
+// that error bounds every covered pixel; rows lie in [floor(min y), ceil(max y)).
+__device__ __forceinline__ bool tri_tile_range(const FrameParams &fp, uint32_t g, TileRange &tr) {
+    const DrawRec *d;
+    uint32_t gt;
+    resolve_draw(fp, g, d, gt);
+    V3 cam[3], proj[3];
+    load_positions(*d, gt, fp, cam, proj);
+    if (!front_facing(proj)) return false;  // also rejects every non-finite vertex
+    const float xmin = fminf(proj[0].x, fminf(proj[1].x, proj[2].x));
+    const float xmax = fmaxf(proj[0].x, fmaxf(proj[1].x, proj[2].x));
+    const float ymin = fminf(proj[0].y, fminf(proj[1].y, proj[2].y));
+    const float ymax = fmaxf(proj[0].y, fmaxf(proj[1].y, proj[2].y));
+    const float fr0 = floorf(ymin), fr1 = ceilf(ymax);
+    const int32_t r0 = fr0 < (float)fp.row0 ? fp.row0 : (fr0 >= (float)fp.row1 ? fp.row1 : (int32_t)fr0);
+    const int32_t r1 = fr1 > (float)fp.row1 ? fp.row1 : (fr1 <= (float)fp.row0 ? fp.row0 : (int32_t)fr1);
+    const float maxabs = fmaxf(fabsf(xmin), fabsf(xmax));
+    const float slack = 2.0f + ((ymax - ymin) + 4.0f) * maxabs * (1.0f / 2097152.0f);  // 2^-21
+    const float fc0 = floorf(xmin - slack), fc1 = ceilf(xmax + slack) + 1.0f;
+    int32_t c0, c1;
+    if (d->mode == MODE_AVX) {
+        // Half-open [MinX, MaxX): a span clamped wholly to one side is empty.
+        c0 = fc0 < 0.0f ? 0 : (fc0 >= (float)fp.W ? fp.W : (int32_t)fc0);
+        c1 = fc1 > (float)fp.W ? fp.W : (fc1 <= 0.0f ? 0 : (int32_t)fc1);
+    } else {
+        // DrawModel's inclusive [MinX, MaxX] after clamping both ends to
+        // [0, W-1] (projekt.cpp:381-425): a triangle left of the screen still
+        // draws column 0, one right of it column W-1.
+        c0 = fc0 < 0.0f ? 0 : (fc0 >= (float)(fp.W - 1) ? fp.W - 1 : (int32_t)fc0);
+        c1 = fc1 > (float)fp.W ? fp.W : (fc1 <= 1.0f ? 1 : (int32_t)fc1);
+    }
+    tr.oty0 = 1;
+    tr.oty1 = 0;
+    const bool rect = r0 < r1 && c0 < c1;
+    if (rect) {
+        tr.tx0 = (uint16_t)(c0 / fp.tile_w);
+        tr.tx1 = (uint16_t)((c1 - 1) / fp.tile_w);
+        tr.ty0 = (uint16_t)((r0 - fp.row0) / fp.tile_h);
+        tr.ty1 = (uint16_t)((r1 - 1 - fp.row0) / fp.tile_h);
+    } else {
+        tr.tx0 = 1; tr.tx1 = 0; tr.ty0 = 1; tr.ty1 = 0;
+    }
+    if (d->mode != MODE_AVX && fc1 >= (float)fp.W) {
+        // A span ending at MaxX == W stores pixel (row+1, 0): rows shift by one.
+        const float lim = (float)min(fp.row1, fp.H);
+        const float g0 = fr0 + 1.0f, g1 = fr1 + 1.0f;
+        const int32_t o0 = g0 < (float)fp.row0 ? fp.row0 : (g0 >= lim ? (int32_t)lim : (int32_t)g0);
+        const int32_t o1 = g1 > lim ? (int32_t)lim : (g1 <= (float)fp.row0 ? fp.row0 : (int32_t)g1);
+        if (o0 < o1) {
+            tr.oty0 = (uint16_t)((o0 - fp.row0) / fp.tile_h);
+            tr.oty1 = (uint16_t)((o1 - 1 - fp.row0) / fp.tile_h);
+        }
+    }
+    return rect || tr.oty0 <= tr.oty1;
+}
+
+// Number of tiles in a range (rectangle + column-0 overflow tiles not in it).
+__device__ __forceinline__ uint32_t range_entries(const TileRange &tr) {
+    uint32_t n = 0;
+    if (tr.tx0 <= tr.tx1 && tr.ty0 <= tr.ty1) n = (uint32_t)(tr.tx1 - tr.tx0 + 1) * (tr.ty1 - tr.ty0 + 1);
+    for (int ty = tr.oty0; ty <= tr.oty1; ++ty)
+        if (!(tr.tx0 == 0 && tr.tx0 <= tr.tx1 && ty >= tr.ty0 && ty <= tr.ty1)) ++n;
+    return n;
+}
+
+__global__ void k_bin_count(FrameParams fp, uint32_t *__restrict__ tri_n, TileRange *__restrict__ ranges) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g > fp.tri_count) return;
+    if (g == fp.tri_count) {  // sentinel: the scan's last element is the total
+        tri_n[g] = 0;
+        return;
+    }
+    TileRange tr;
+    if (!tri_tile_range(fp, g, tr)) {
+        tr.tx0 = 1; tr.tx1 = 0; tr.ty0 = 1; tr.ty1 = 0; tr.oty0 = 1; tr.oty1 = 0;
+    }
+    ranges[g] = tr;
+    tri_n[g] = range_entries(tr);
+}
+
+__global__ void k_bin_emit(FrameParams fp, const TileRange *__restrict__ ranges, const uint32_t *__restrict__ off,
+                           uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= fp.tri_count) return;
+    const TileRange tr = ranges[g];
+    uint32_t o = off[g];
+    if (tr.tx0 <= tr.tx1 && tr.ty0 <= tr.ty1)
+        for (int ty = tr.ty0; ty <= tr.ty1; ++ty)
+            for (int tx = tr.tx0; tx <= tr.tx1; ++tx) {
+                keys[o] = (uint32_t)(ty * fp.tiles_x + tx);
+                vals[o] = g;
+                ++o;
+            }
+    for (int ty = tr.oty0; ty <= tr.oty1; ++ty)
+        if (!(tr.tx0 == 0 && tr.tx0 <= tr.tx1 && ty >= tr.ty0 && ty <= tr.ty1)) {
+            keys[o] = (uint32_t)(ty * fp.tiles_x);
+            vals[o] = g;
+            ++o;
+        }
+}
+
+// offs[t] = first sorted position whose tile is >= t, for t in [0, ntiles].
+__global__ void k_tile_offsets(const uint32_t *__restrict__ keys, uint32_t total, uint32_t ntiles,
+                               uint32_t *__restrict__ offs) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > ntiles) return;
+    uint32_t lo = 0, hi = total;
+    while (lo < hi) {
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        if (keys[mid] < t) lo = mid + 1; else hi = mid;
+    }
+    offs[t] = lo;
+}
+
+}  // namespace prk
+
+extern "C" {
+
+// Phase 1: counts + exclusive scan.  `scan_out` gets T+1 offsets; the caller
+// reads scan_out[T] (the number of entries) before phase 2.
+hipError_t prk_bin_phase1(const prk::FrameParams *fp, uint32_t *tri_n, uint32_t *scan_out, void *ranges,
+                          void *temp, size_t *temp_bytes, hipStream_t s) {
+    const uint32_t n = fp->tri_count + 1;
+    if (!temp) return hipcub::DeviceScan::ExclusiveSum(nullptr, *temp_bytes, tri_n, scan_out, n, s);
+    hipLaunchKernelGGL(prk::k_bin_count, dim3((n + 255) / 256), dim3(256), 0, s, *fp, tri_n,
+                       reinterpret_cast<prk::TileRange *>(ranges));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, tri_n, scan_out, n, s);
+}
+
+// Phase 2: emit pairs in triangle order, stable sort by tile, tile offsets.
+// With temp == nullptr only reports the temp storage the sort needs.
+hipError_t prk_bin_phase2(const prk::FrameParams *fp, const void *ranges, const uint32_t *scan_out, uint32_t total,
+                          uint32_t *keys_a, uint32_t *vals_a, uint32_t *keys_b, uint32_t *vals_b, uint32_t *offs,
+                          void *temp, size_t *temp_bytes, hipStream_t s) {
+    const uint32_t ntiles = (uint32_t)(fp->tiles_x * fp->tiles_y);
+    int bits = 1;
+    while ((1u << bits) < ntiles && bits < 32) ++bits;
+    if (!temp)
+        return hipcub::DeviceRadixSort::SortPairs(nullptr, *temp_bytes, keys_a, keys_b, vals_a, vals_b, total, 0,
+                                                  bits, s);
+    if (fp->tri_count)
+        hipLaunchKernelGGL(prk::k_bin_emit, dim3((fp->tri_count + 255) / 256), dim3(256), 0, s, *fp,
+                           reinterpret_cast<const prk::TileRange *>(ranges), scan_out, keys_a, vals_a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (total) {
+        e = hipcub::DeviceRadixSort::SortPairs(temp, *temp_bytes, keys_a, keys_b, vals_a, vals_b, total, 0, bits, s);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(prk::k_tile_offsets, dim3((ntiles + 1 + 255) / 256), dim3(256), 0, s, keys_b, total, ntiles,
+                       offs);
+    return hipGetLastError();
+}
+
+}  // extern "C"

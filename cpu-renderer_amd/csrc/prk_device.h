@@ -67,6 +67,11 @@ struct FrameParams {
     const TexRec *texs;
 };
 
+// Tiles a triangle may touch: the rectangle [tx0..tx1] x [ty0..ty1], plus
+// for scalar semantics the column-0 tiles of rows [oty0..oty1] that receive
+// DrawModel's one-past-the-row store (see span_setup_scalar).
+struct TileRange { uint16_t tx0, ty0, tx1, ty1, oty0, oty1, pad0, pad1; };
+
 // ---------------------------------------------------------------------------
 // Conversions with x86 semantics (the reference runs on x86).
 // ---------------------------------------------------------------------------
@@ -416,66 +421,92 @@ __device__ __forceinline__ bool insert_before(const Edge &A, const Edge &B) {
 // (projekt.cpp:3615-3871, with the P3 head/tail fix; DrawModel's AET,
 // 168-598, is the same list logic) as a row-by-row state machine.
 //
-// The list is held in slots L0..L2 in list order.  For ONE triangle the two
-// sorted edges with the smallest YMin always share it, so all
-// insertions of FirstRow happen in init() and at most one edge (P) is still
-// pending afterwards.  `anomaly` counts triangles violating that (never
-// observed; the host reports it as an error).
+// The three sorted setup edges stay in fixed registers E0..E2; the list is a
+// permutation `ord` (2 bits per list slot, head first) plus a count, so
+// insertion, expiry and the crossing swap move only a few integer bits.
+// For ONE triangle the two sorted edges with the smallest YMin always share
+// it, so all insertions of FirstRow happen in init() and at
+// most one edge is still pending afterwards; `anomaly` counts triangles
+// violating that (never observed; reported by the host).
 template <int M, bool NRM>
 struct Walker {
-    Edge L0, L1, L2, P;
-    int cnt;
-    bool hasP;
+    Edge E0, E1, E2;
+    uint32_t ord;     // list slot j holds edge (ord >> 2j) & 3
+    int cnt;          // list length
+    int pend;         // index of the pending edge, or -1
     int32_t FirstRow, MaxY, Row;
 
-    __device__ __forceinline__ void insert(const Edge E) {  // 3654-3713
+    __device__ __forceinline__ int slot(int j) const { return (int)((ord >> (2 * j)) & 3u); }
+    __device__ __forceinline__ Edge get(int k) const { return sel(k == 0, E0, sel(k == 1, E1, E2)); }
+    // (value selects: a conditional over lvalues would become a pointer select
+    // and push the walker to scratch memory)
+    template <typename T>
+    __device__ __forceinline__ static T pick(int k, T a, T b, T c) { return k == 0 ? a : (k == 1 ? b : c); }
+    __device__ __forceinline__ float X(int k) const { return pick<float>(k, E0.X, E1.X, E2.X); }
+    __device__ __forceinline__ float G(int k) const { return pick<float>(k, E0.G, E1.G, E2.G); }
+    __device__ __forceinline__ int32_t Lf(int k) const { return pick<int32_t>(k, E0.Left, E1.Left, E2.Left); }
+    __device__ __forceinline__ int32_t YMax(int k) const { return pick<int32_t>(k, E0.YMax, E1.YMax, E2.YMax); }
+
+    // AET insertion order (projekt.cpp:3663-3667) of edge a before edge b.
+    __device__ __forceinline__ bool before(int a, int b) const {
+        const float xa = X(a), xb = X(b), ga = G(a), gb = G(b);
+        return xa < xb || (xa == xb && (ga < gb || (ga == gb && Lf(a) < Lf(b))));
+    }
+
+    __device__ __forceinline__ void insert(int k) {  // 3654-3713
         int pos = cnt;
-        if (cnt > 1 && insert_before(E, L1)) pos = 1;
-        if (cnt > 0 && insert_before(E, L0)) pos = 0;
-        L2 = sel(pos <= 1 && cnt >= 2, L1, sel(pos == 2, E, L2));
-        L1 = sel(pos == 0 && cnt >= 1, L0, sel(pos == 1, E, L1));
-        L0 = sel(pos == 0, E, L0);
+        if (cnt > 1 && before(k, slot(1))) pos = 1;
+        if (cnt > 0 && before(k, slot(0))) pos = 0;
+        const uint32_t lowmask = (1u << (2 * pos)) - 1u;
+        ord = (ord & lowmask) | ((uint32_t)k << (2 * pos)) | ((ord & ~lowmask) << 2);
+        ord &= 0x3Fu;
         ++cnt;
     }
 
     __device__ __forceinline__ void init(int n, const Edge &s0, const Edge &s1, const Edge &s2, int32_t H,
                                          int32_t row_end, uint32_t &anomaly) {
+        E0 = s0; E1 = s1; E2 = s2;
         FirstRow = s0.YMin;
         int32_t MaxRow = s0.YMax;
         if (n > 1 && MaxRow < s1.YMax) MaxRow = s1.YMax;
         if (n > 2 && MaxRow < s2.YMax) MaxRow = s2.YMax;
         MaxY = min(min(MaxRow, H), row_end);
         Row = FirstRow;
-        L0 = s0; L1 = s0; L2 = s0; P = s0;
+        ord = 0u;
         cnt = 1;
-        hasP = false;
+        pend = -1;
         if (n > 1) {
-            if (s1.YMin == FirstRow) insert(s1);
+            if (s1.YMin == FirstRow) insert(1);
             else ++anomaly;
         }
         if (n > 2) {
-            if (s2.YMin == FirstRow) insert(s2);
-            else { P = s2; hasP = true; }
+            if (s2.YMin == FirstRow) insert(2);
+            else pend = 2;
         }
     }
 
-    // Insertion + expiry of this->Row; true when a pair (L0, L1) is emitted.
+    // Insertion + expiry of this->Row; true when a pair is emitted: the left
+    // edge is slot(0), the right edge slot(1).
     __device__ __forceinline__ bool begin_row() {
-        if (hasP && P.YMin == Row) {
-            insert(P);
-            hasP = false;
+        if (pend >= 0 && E2.YMin == Row) {
+            insert(2);
+            pend = -1;
         }
         // Expiry (3715-3749): drop every entry with YMax <= Row, keep order.
-        const bool k0 = cnt > 0 && !(L0.YMax <= Row);
-        const bool k1 = cnt > 1 && !(L1.YMax <= Row);
-        const bool k2 = cnt > 2 && !(L2.YMax <= Row);
-        const Edge n0 = sel(k0, L0, sel(k1, L1, L2));
-        const Edge n1 = sel(k0 && k1, L1, L2);
-        L0 = n0;
-        L1 = n1;
-        cnt = (int)k0 + (int)k1 + (int)k2;
-        // Pairing (3751-3869): one pair (L0, L1); a third entry is left
-        // unpaired and unstepped, as in the reference.
+        uint32_t o = 0u;
+        int c = 0;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int k = slot(j);
+            if (j < cnt && !(YMax(k) <= Row)) {
+                o |= (uint32_t)k << (2 * c);
+                ++c;
+            }
+        }
+        ord = o;
+        cnt = c;
+        // Pairing (3751-3869): one pair; a third entry is left unpaired and
+        // unstepped, as in the reference.
         return cnt >= 2;
     }
 
@@ -483,12 +514,15 @@ struct Walker {
     // (3831-3841 + P3), then move to the next row.
     __device__ __forceinline__ void end_row(bool paired) {
         if (paired) {
-            step_edge<M, NRM>(L0);
-            step_edge<M, NRM>(L1);
-            const bool swp = L0.X > L1.X;
-            const Edge t0 = sel(swp, L1, L0);
-            L1 = sel(swp, L0, L1);
-            L0 = t0;
+            const int a = slot(0), b = slot(1);
+            Edge t0 = E0, t1 = E1, t2 = E2;
+            step_edge<M, NRM>(t0);
+            step_edge<M, NRM>(t1);
+            step_edge<M, NRM>(t2);
+            E0 = sel(a == 0 || b == 0, t0, E0);
+            E1 = sel(a == 1 || b == 1, t1, E1);
+            E2 = sel(a == 2 || b == 2, t2, E2);
+            if (X(a) > X(b)) ord = (ord & ~0xFu) | ((uint32_t)a << 2) | (uint32_t)b;
         }
         ++Row;
     }

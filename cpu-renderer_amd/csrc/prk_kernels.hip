@@ -1,12 +1,7 @@
 // prk_kernels.hip — gfx950 kernels of the rasterizer hot path.
 //
-// Pipeline per flush:
-//   k_bin_count  one thread per triangle: ProjectVertex + back-face cull
-//                (projekt.cpp:74-93, 3926-3943) -> conservative pixel bbox ->
-//                per-tile counts.
-//   k_scan       exclusive scan of the per-tile counts (one workgroup).
-//   k_bin_fill   one thread per triangle: scatter its index into every tile
-//                bin it overlaps (order inside a bin does not matter, see below).
+// Pipeline per flush: binning in prk_bin.hip produces, for
+// every tile, the triangles that may touch it in submission order; then
 //   k_raster     one workgroup per screen tile; the tile's z/colour slab lives
 //                in LDS.  Each lane owns one bin entry (a triangle), re-runs
 //                FillEdgeTable for it (projekt.cpp:3882-4121), walks its AET
@@ -14,13 +9,15 @@
 //                reference's exact span arithmetic (FillLineOptimized
 //                1492-2320 or DrawModel 298-538).
 //                Sweep 1 resolves visibility with 64-bit LDS atomicMax on
-//                key = (ordered z << 32) | (0xFFFFFFFE - triangle): the
+//                key = (ordered z << 32) | (0xFFFFFFFE - bin entry): the
 //                reference's strict z '>' in submission order keeps exactly
-//                the EARLIEST fragment of maximal z, which is that max.
-//                Sweep 2 re-walks and shades only the winning fragments
-//                (texture + Phong), so shading runs once per pixel instead of
-//                once per fragment.  A coalesced flush writes z and colour of
-//                every pixel that got a winner.
+//                the EARLIEST fragment of maximal z, which is that max (bin
+//                entries are in submission order).  The triangles that won a
+//                pixel are then listed, and sweep 2 re-walks only those and
+//                shades only the winning fragments (texture + Phong), so
+//                shading runs once per pixel instead of once per fragment.
+//                A coalesced flush writes z and colour of every pixel that
+//                got a winner.
 #include "prk_device.h"
 
 // Diagnostic builds only (tools/diag): 1 = skip the shading sweep, 2 = skip
@@ -29,7 +26,7 @@
 #define PRK_DIAG 0
 #endif
 #ifndef PRK_RASTER_MIN_WAVES
-#define PRK_RASTER_MIN_WAVES 2  // waves per SIMD the raster kernel is register-budgeted for
+#define PRK_RASTER_MIN_WAVES 3  // waves per SIMD the raster kernel is register-budgeted for
 #endif
 
 namespace prk {
@@ -49,126 +46,6 @@ __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
 // Tiles a triangle may touch: the rectangle [tx0..tx1] x [ty0..ty1], plus
 // for scalar semantics the column-0 tiles of rows [oty0..oty1] that receive
 // DrawModel's one-past-the-row store (see span_scalar).
-struct TileRange { uint16_t tx0, ty0, tx1, ty1, oty0, oty1, pad0, pad1; };
-
-// Conservative tile range of a triangle's covered pixels.  Span end points
-// are edge-DDA values that stay on their segment up to float error
-// (DESIGN.md §4.1), so [min x, max x] of the projected vertices widened by
-// that error bounds every covered pixel; rows lie in [floor(min y), ceil(max y)).
-__device__ __forceinline__ bool tri_tile_range(const FrameParams &fp, uint32_t g, TileRange &tr) {
-    const DrawRec *d;
-    uint32_t gt;
-    resolve_draw(fp, g, d, gt);
-    V3 cam[3], proj[3];
-    load_positions(*d, gt, fp, cam, proj);
-    if (!front_facing(proj)) return false;  // also rejects every non-finite vertex
-    float xmin = fminf(proj[0].x, fminf(proj[1].x, proj[2].x));
-    float xmax = fmaxf(proj[0].x, fmaxf(proj[1].x, proj[2].x));
-    float ymin = fminf(proj[0].y, fminf(proj[1].y, proj[2].y));
-    float ymax = fmaxf(proj[0].y, fmaxf(proj[1].y, proj[2].y));
-    float fr0 = floorf(ymin), fr1 = ceilf(ymax);
-    int32_t r0 = fr0 < (float)fp.row0 ? fp.row0 : (fr0 >= (float)fp.row1 ? fp.row1 : (int32_t)fr0);
-    int32_t r1 = fr1 > (float)fp.row1 ? fp.row1 : (fr1 <= (float)fp.row0 ? fp.row0 : (int32_t)fr1);
-    if (r0 >= r1) return false;
-    float maxabs = fmaxf(fabsf(xmin), fabsf(xmax));
-    float slack = 2.0f + ((ymax - ymin) + 4.0f) * maxabs * (1.0f / 2097152.0f);  // 2^-21
-    float fc0 = floorf(xmin - slack), fc1 = ceilf(xmax + slack) + 1.0f;
-    int32_t c0, c1;
-    if (d->mode == MODE_AVX) {
-        // Half-open [MinX, MaxX): a span clamped wholly to one side is empty.
-        c0 = fc0 < 0.0f ? 0 : (fc0 >= (float)fp.W ? fp.W : (int32_t)fc0);
-        c1 = fc1 > (float)fp.W ? fp.W : (fc1 <= 0.0f ? 0 : (int32_t)fc1);
-    } else {
-        // DrawModel's inclusive [MinX, MaxX] after clamping both ends to
-        // [0, W-1] (projekt.cpp:381-425): a triangle left of the screen still
-        // draws column 0, one right of it column W-1.
-        c0 = fc0 < 0.0f ? 0 : (fc0 >= (float)(fp.W - 1) ? fp.W - 1 : (int32_t)fc0);
-        c1 = fc1 > (float)fp.W ? fp.W : (fc1 <= 1.0f ? 1 : (int32_t)fc1);
-    }
-    if (c0 >= c1) return false;
-    tr.tx0 = (uint16_t)(c0 / fp.tile_w);
-    tr.tx1 = (uint16_t)((c1 - 1) / fp.tile_w);
-    tr.ty0 = (uint16_t)((r0 - fp.row0) / fp.tile_h);
-    tr.ty1 = (uint16_t)((r1 - 1 - fp.row0) / fp.tile_h);
-    tr.oty0 = 1;
-    tr.oty1 = 0;
-    if (d->mode != MODE_AVX && fc1 >= (float)fp.W) {
-        // A span ending at MaxX == W stores pixel (row+1, 0): rows shift by one.
-        const float lim = (float)min(fp.row1, fp.H);
-        float g0 = fr0 + 1.0f, g1 = fr1 + 1.0f;
-        int32_t o0 = g0 < (float)fp.row0 ? fp.row0 : (g0 >= lim ? (int32_t)lim : (int32_t)g0);
-        int32_t o1 = g1 > lim ? (int32_t)lim : (g1 <= (float)fp.row0 ? fp.row0 : (int32_t)g1);
-        if (o0 < o1) {
-            tr.oty0 = (uint16_t)((o0 - fp.row0) / fp.tile_h);
-            tr.oty1 = (uint16_t)((o1 - 1 - fp.row0) / fp.tile_h);
-        }
-    }
-    return true;
-}
-
-__global__ void k_bin_count(FrameParams fp, uint32_t *__restrict__ counts,
-                            TileRange *__restrict__ ranges) {
-    uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= fp.tri_count) return;
-    TileRange tr;
-    if (!tri_tile_range(fp, g, tr)) {
-        tr.tx0 = 1; tr.tx1 = 0; tr.ty0 = 1; tr.ty1 = 0; tr.oty0 = 1; tr.oty1 = 0;
-    } else {
-        for (int ty = tr.ty0; ty <= tr.ty1; ++ty)
-            for (int tx = tr.tx0; tx <= tr.tx1; ++tx)
-                atomicAdd(&counts[ty * fp.tiles_x + tx], 1u);
-        for (int ty = tr.oty0; ty <= tr.oty1; ++ty)
-            if (!(tr.tx0 == 0 && ty >= tr.ty0 && ty <= tr.ty1))
-                atomicAdd(&counts[ty * fp.tiles_x], 1u);
-    }
-    ranges[g] = tr;
-}
-
-// Exclusive scan of n counts into offs[0..n]; offs[n] = total.  One workgroup.
-__global__ void __launch_bounds__(1024) k_scan(const uint32_t *__restrict__ counts,
-                                               uint32_t *__restrict__ offs, uint32_t n) {
-    __shared__ uint32_t part[1024];
-    const uint32_t t = threadIdx.x;
-    const uint32_t per = (n + 1023) / 1024;
-    const uint32_t b = t * per, e = min(n, b + per);
-    uint32_t s = 0;
-    for (uint32_t i = b; i < e; ++i) s += counts[i];
-    part[t] = s;
-    __syncthreads();
-    for (uint32_t off = 1; off < 1024; off <<= 1) {
-        uint32_t v = t >= off ? part[t - off] : 0u;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    uint32_t run = part[t] - s;  // exclusive prefix of this chunk
-    for (uint32_t i = b; i < e; ++i) {
-        offs[i] = run;
-        run += counts[i];
-    }
-    if (t == 1023) offs[n] = part[1023];
-}
-
-__global__ void k_bin_fill(FrameParams fp, const TileRange *__restrict__ ranges,
-                           const uint32_t *__restrict__ offs, uint32_t *__restrict__ cursor,
-                           uint32_t *__restrict__ bins) {
-    uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= fp.tri_count) return;
-    TileRange tr = ranges[g];
-    for (int ty = tr.ty0; ty <= tr.ty1; ++ty)
-        for (int tx = tr.tx0; tx <= tr.tx1; ++tx) {
-            int t = ty * fp.tiles_x + tx;
-            uint32_t p = atomicAdd(&cursor[t], 1u);
-            bins[offs[t] + p] = g;
-        }
-    for (int ty = tr.oty0; ty <= tr.oty1; ++ty)
-        if (!(tr.tx0 == 0 && ty >= tr.ty0 && ty <= tr.ty1)) {
-            int t = ty * fp.tiles_x;
-            uint32_t p = atomicAdd(&cursor[t], 1u);
-            bins[offs[t] + p] = g;
-        }
-}
-
 // ---------------------------------------------------------------------------
 // Tile raster.
 //
@@ -184,7 +61,10 @@ __global__ void k_bin_fill(FrameParams fp, const TileRange *__restrict__ ranges,
 // Items are spread over the 64 lanes (prefix sum + binary search), so the
 // pixel work no longer serialises on the lane that owns the triangle.
 // ---------------------------------------------------------------------------
-constexpr int kWaves = 4;
+#ifndef PRK_WAVES
+#define PRK_WAVES 2  // waves per tile workgroup; each takes whole 64-entry chunks of the bin
+#endif
+constexpr int kWaves = PRK_WAVES;
 constexpr int kSpanF = 22;  // float fields per span slot
 constexpr int kSpanI = 8;   // int fields per span slot
 enum { SI_XA = 0, SI_XB, SI_LEFT, SI_PRE, SI_TAG, SI_ROW, SI_OVF, SI_TEX };
@@ -203,7 +83,6 @@ struct WaveSlots {
 struct TileCtx {
     int32_t x0, x1, y0, y1, tw;  // tile pixel rectangle [x0,x1) x [y0,y1), LDS row stride tw
     unsigned long long *key;     // LDS: visibility keys
-    uint32_t *ocol;              // LDS: winner colours
 };
 
 __device__ __forceinline__ unsigned long long make_key(float z, uint32_t tag) {
@@ -214,9 +93,13 @@ __device__ __forceinline__ bool is_winner(const TileCtx &tc, int p, uint32_t tag
     return (uint32_t)tc.key[p] == tag;
 }
 
-__device__ __forceinline__ void put_winner(const TileCtx &tc, int p, float z, uint32_t col) {
-    tc.ocol[p] = col;
-    reinterpret_cast<uint32_t *>(tc.key + p)[1] = __float_as_uint(z);  // raw z bits
+// The winning fragment of tile pixel p: store its z and colour (each pixel
+// has exactly one winner, so these plain stores never race).
+__device__ __forceinline__ void put_winner(const FrameParams &fp, const TileCtx &tc, int p, float z, uint32_t col) {
+    const int32_t x = tc.x0 + p % tc.tw, y = tc.y0 + p / tc.tw;
+    const size_t row = (size_t)(y - fp.row0);
+    fp.zbuf[row * fp.W + x] = z;
+    reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(fp.color) + row * fp.pitch)[x] = col;
 }
 
 // ----- span setup --------------------------------------------------------
@@ -447,7 +330,7 @@ __device__ __forceinline__ void item_avx(const FrameParams &fp, const TileCtx &t
             if (fu >= 0.0f && fu <= 1.0f && fv >= 0.0f && fv <= 1.0f && z == z)
                 atomicMax(&tc.key[p], make_key(z, tag));
         } else {
-            if (is_winner(tc, p, tag)) put_winner(tc, p, z, shade_avx(fp, tex, fu, fv, z, n0, n1, n2, x, i, Row));
+            if (is_winner(tc, p, tag)) put_winner(fp, tc, p, z, shade_avx(fp, tex, fu, fv, z, n0, n1, n2, x, i, Row));
             if (x + 8 < xb) {
                 float a = n0 + IN08, bb = n1 + IN18, c = n2 + IN28;
                 normalize_div(a, bb, c);
@@ -542,7 +425,7 @@ __device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx
                 }
                 const uint32_t packed = (round_u32(F[3] * 255.0f) << 24) | (round_u32(F[0] * 255.0f) << 16) |
                                         (round_u32(F[1] * 255.0f) << 8) | (round_u32(F[2] * 255.0f));
-                put_winner(tc, p, z, packed);
+                put_winner(fp, tc, p, z, packed);
             }
         }
         if (SHADE) {  // per-pixel step (504-510 / 530-535)
@@ -571,28 +454,30 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 // SHADE=true: shade the winners.
 template <int M, bool SHADE>
 __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, WaveSlots &ws,
-                                      const uint32_t *__restrict__ bins, uint32_t b0, uint32_t b1,
-                                      uint32_t *anomaly) {
+                                      const uint32_t *__restrict__ bins, uint32_t b0, uint32_t n,
+                                      const uint32_t *__restrict__ list, uint32_t *anomaly) {
+    // Entries [0, n) of the tile's bin, or (list != nullptr) the n entries it names.
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const bool col0 = tc.x0 == 0 && M != MODE_AVX;
     const int32_t ystart = col0 ? tc.y0 - 1 : tc.y0;  // scalar: (row-1) may store into (row, 0)
-    for (uint32_t base = b0 + wave * 64; base < b1; base += 64 * kWaves) {
-        const uint32_t e = base + lane;
-        bool active = e < b1;
-        uint32_t g = 0;
+    for (uint32_t base = wave * 64; base < n; base += 64 * kWaves) {
+        const uint32_t i = base + lane;
+        bool active = i < n;
+        uint32_t e = 0;
         const DrawRec *d = fp.draws;
         Walker<M, SHADE> wk;
         uint32_t anom = 0;
         if (active) {
-            g = bins[e];
+            e = list ? list[b0 + i] : i;
+            const uint32_t g = bins[b0 + e];
             uint32_t gt;
             resolve_draw(fp, g, d, gt);
             Edge s0, s1, s2;
             // (mixed frames sweep the bin once per mode)
-            const int n = d->mode == M ? setup_triangle<M>(*d, gt, fp, s0, s1, s2) : 0;
-            active = n >= 2;
+            const int ne = d->mode == M ? setup_triangle<M>(*d, gt, fp, s0, s1, s2) : 0;
+            active = ne >= 2;
             if (active) {
-                wk.init(n, s0, s1, s2, fp.H, tc.y1, anom);
+                wk.init(ne, s0, s1, s2, fp.H, tc.y1, anom);
                 // Replay the rows above the tile (edge DDA only).
                 while (wk.Row < ystart && wk.Row < wk.MaxY) wk.end_row(wk.begin_row());
                 active = wk.Row < wk.MaxY;
@@ -600,15 +485,16 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
         }
         if (anom) atomicAdd(anomaly, anom);
         const int32_t texi = (ModeTraits<M>::tex && active) ? d->tex : 0;
-        const uint32_t tag = 0xFFFFFFFEu - g;
+        const uint32_t tag = 0xFFFFFFFEu - e;
         if (PRK_DIAG & 4) active = false;
         for (int32_t r = ystart; r < tc.y1; ++r) {
             int items = 0;
             if (active && wk.Row == r) {
                 const bool paired = wk.begin_row();
                 if (paired) {
-                    if (M == MODE_AVX) items = span_setup_avx<SHADE>(fp, tc, ws, lane, tag, texi, wk.L0, wk.L1, r);
-                    else items = span_setup_scalar<M, SHADE>(fp, tc, ws, lane, tag, texi, wk.L0, wk.L1, r);
+                    const Edge L = wk.get(wk.slot(0)), R = wk.get(wk.slot(1));
+                    if (M == MODE_AVX) items = span_setup_avx<SHADE>(fp, tc, ws, lane, tag, texi, L, R, r);
+                    else items = span_setup_scalar<M, SHADE>(fp, tc, ws, lane, tag, texi, L, R, r);
                 }
                 wk.end_row(paired);
                 active = wk.Row < wk.MaxY;
@@ -642,22 +528,39 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
 
 template <int M>
 __device__ __forceinline__ void raster_mode(const FrameParams &fp, const TileCtx &tc, WaveSlots &ws,
-                                            const uint32_t *bins, uint32_t b0, uint32_t b1, uint32_t *anomaly,
-                                            bool shade) {
-    if (!shade) sweep<M, false>(fp, tc, ws, bins, b0, b1, anomaly);
-    else sweep<M, true>(fp, tc, ws, bins, b0, b1, anomaly);
+                                            const uint32_t *bins, uint32_t b0, uint32_t n, const uint32_t *list,
+                                            uint32_t *anomaly, bool shade) {
+    if (!shade) sweep<M, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly);
+    else sweep<M, true>(fp, tc, ws, bins, b0, n, list, anomaly);
+}
+
+// Workgroup-wide exclusive scan of one value per thread.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *scratch, uint32_t &total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int incl = wave_incl_scan((int)v, lane);
+    if (lane == 63) scratch[wave] = (uint32_t)incl;
+    __syncthreads();
+    uint32_t before = 0;
+    total = 0;
+    for (int w = 0; w < kWaves; ++w) {
+        if (w < wave) before += scratch[w];
+        total += scratch[w];
+    }
+    __syncthreads();
+    return before + (uint32_t)incl - v;
 }
 
 template <int MODESET>  // a single Mode, or -1: any mode (per-draw dispatch)
-__global__ void __launch_bounds__(256, PRK_RASTER_MIN_WAVES) k_raster(FrameParams fp, const uint32_t *__restrict__ offs,
-                                                const uint32_t *__restrict__ bins,
-                                                uint32_t *__restrict__ anomaly) {
+__global__ void __launch_bounds__(64 * kWaves, PRK_RASTER_MIN_WAVES) k_raster(FrameParams fp, const uint32_t *__restrict__ offs,
+                                                const uint32_t *__restrict__ bins, uint8_t *__restrict__ won,
+                                                uint32_t *__restrict__ list, uint32_t *__restrict__ anomaly) {
     extern __shared__ unsigned long long lds[];
     const int ntile = fp.tiles_x * fp.tiles_y;
     const int t = blockIdx.x;
     if (t >= ntile) return;
     const uint32_t b0 = offs[t], b1 = offs[t + 1];
     if (b0 == b1) return;  // no triangle touches this tile: leave it untouched
+    const uint32_t n = b1 - b0;
     const int tx = t % fp.tiles_x, ty = t / fp.tiles_x;
     TileCtx tc;
     tc.tw = fp.tile_w;
@@ -667,9 +570,9 @@ __global__ void __launch_bounds__(256, PRK_RASTER_MIN_WAVES) k_raster(FrameParam
     tc.y1 = min(fp.row1, tc.y0 + fp.tile_h);
     const int npx = fp.tile_w * fp.tile_h;
     tc.key = lds;
-    tc.ocol = reinterpret_cast<uint32_t *>(lds + npx);
-    WaveSlots *slots = reinterpret_cast<WaveSlots *>(tc.ocol + npx);
+    WaveSlots *slots = reinterpret_cast<WaveSlots *>(lds + npx);
     WaveSlots &ws = slots[threadIdx.x >> 6];
+    uint32_t *scratch = reinterpret_cast<uint32_t *>(slots + kWaves);
 
     // Prior z of the target: a fragment must beat it strictly.
     for (int p = threadIdx.x; p < npx; p += blockDim.x) {
@@ -683,42 +586,67 @@ __global__ void __launch_bounds__(256, PRK_RASTER_MIN_WAVES) k_raster(FrameParam
         tc.key[p] = k;
     }
     __syncthreads();
-    for (int pass = 0; pass < ((PRK_DIAG & 1) ? 1 : 2); ++pass) {
-        const bool shade = pass == 1;
-        if constexpr (MODESET >= 0) {
-            raster_mode<(MODESET >= 0 ? MODESET : 0)>(fp, tc, ws, bins, b0, b1, anomaly, shade);
-        } else {
-            // Mixed frame: each mode sweeps the bin and skips other modes' entries.
-            raster_mode<MODE_AVX>(fp, tc, ws, bins, b0, b1, anomaly, shade);
-            raster_mode<MODE_SC_GOURAUD>(fp, tc, ws, bins, b0, b1, anomaly, shade);
-            raster_mode<MODE_SC_GOURAUD_TEX>(fp, tc, ws, bins, b0, b1, anomaly, shade);
-            raster_mode<MODE_SC_PHONG>(fp, tc, ws, bins, b0, b1, anomaly, shade);
-            raster_mode<MODE_SC_PHONG_TEX>(fp, tc, ws, bins, b0, b1, anomaly, shade);
-        }
-        __syncthreads();
+    // Sweep 1: visibility.
+    if constexpr (MODESET >= 0) {
+        raster_mode<(MODESET >= 0 ? MODESET : 0)>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
+    } else {
+        // Mixed frame: each mode sweeps the bin and skips other modes' entries.
+        raster_mode<MODE_AVX>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
+        raster_mode<MODE_SC_GOURAUD>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
+        raster_mode<MODE_SC_GOURAUD_TEX>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
+        raster_mode<MODE_SC_PHONG>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
+        raster_mode<MODE_SC_PHONG_TEX>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
     }
-    // Flush: every pixel with a winner gets its z and colour.
+    __syncthreads();
+    if (PRK_DIAG & 1) return;
+    // Which bin entries won at least one pixel of this tile?
     for (int p = threadIdx.x; p < npx; p += blockDim.x) {
-        const int lx = p % fp.tile_w, ly = p / fp.tile_w;
-        const int x = tc.x0 + lx, y = tc.y0 + ly;
-        if (x >= tc.x1 || y >= tc.y1) continue;
-        const unsigned long long k = tc.key[p];
-        const uint32_t low = (uint32_t)k;
-        const size_t row = (size_t)(y - fp.row0);
-        if (low != 0xFFFFFFFFu) {
-            fp.zbuf[row * fp.W + x] = __uint_as_float((uint32_t)(k >> 32));
-            reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(fp.color) + row * fp.pitch)[x] = tc.ocol[p];
+        const uint32_t low = (uint32_t)tc.key[p];
+        if (low != 0xFFFFFFFFu) won[b0 + (0xFFFFFFFEu - low)] = 1;
+    }
+    __threadfence_block();
+    __syncthreads();
+    uint32_t nwin = 0;
+    for (uint32_t base = 0; base < n; base += blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t f = (i < n && won[b0 + i]) ? 1u : 0u;
+        uint32_t tot;
+        const uint32_t pos = block_excl_scan(f, scratch, tot);
+        if (f) list[b0 + nwin + pos] = i;
+        nwin += tot;
+    }
+    __threadfence_block();
+    __syncthreads();
+    // Sweep 2: shade the winners.
+    if constexpr (MODESET >= 0) {
+        raster_mode<(MODESET >= 0 ? MODESET : 0)>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
+    } else {
+        raster_mode<MODE_AVX>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
+        raster_mode<MODE_SC_GOURAUD>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
+        raster_mode<MODE_SC_GOURAUD_TEX>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
+        raster_mode<MODE_SC_PHONG>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
+        raster_mode<MODE_SC_PHONG_TEX>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
+    }
+    __syncthreads();
+    // Winners wrote their z and colour in sweep 2; untouched pixels keep the
+    // prior contents.  Debug builds also export the winning triangle map.
+    if (fp.winners) {
+        for (int p = threadIdx.x; p < npx; p += blockDim.x) {
+            const int x = tc.x0 + p % fp.tile_w, y = tc.y0 + p / fp.tile_w;
+            if (x >= tc.x1 || y >= tc.y1) continue;
+            const uint32_t low = (uint32_t)tc.key[p];
+            fp.winners[(size_t)(y - fp.row0) * fp.W + x] =
+                low != 0xFFFFFFFFu ? (int32_t)bins[b0 + (0xFFFFFFFEu - low)] : -1;
         }
-        if (fp.winners)
-            fp.winners[row * fp.W + x] = low != 0xFFFFFFFFu ? (int32_t)(0xFFFFFFFEu - low) : -1;
     }
 }
 
 // Explicit instantiations used by the host.
-template __global__ void k_raster<-1>(FrameParams, const uint32_t *, const uint32_t *, uint32_t *);
-template __global__ void k_raster<MODE_AVX>(FrameParams, const uint32_t *, const uint32_t *, uint32_t *);
-template __global__ void k_raster<MODE_SC_GOURAUD>(FrameParams, const uint32_t *, const uint32_t *, uint32_t *);
-template __global__ void k_raster<MODE_SC_PHONG>(FrameParams, const uint32_t *, const uint32_t *, uint32_t *);
+#define PRK_RASTER_ARGS FrameParams, const uint32_t *, const uint32_t *, uint8_t *, uint32_t *, uint32_t *
+template __global__ void k_raster<-1>(PRK_RASTER_ARGS);
+template __global__ void k_raster<MODE_AVX>(PRK_RASTER_ARGS);
+template __global__ void k_raster<MODE_SC_GOURAUD>(PRK_RASTER_ARGS);
+template __global__ void k_raster<MODE_SC_PHONG>(PRK_RASTER_ARGS);
 
 }  // namespace prk
 
@@ -735,49 +663,21 @@ hipError_t prk_launch_tri_draw(const prk::DrawRec *draws, uint32_t ndraws, uint3
     return hipGetLastError();
 }
 
-hipError_t prk_launch_bin(const prk::FrameParams *fp, uint32_t *counts, uint32_t *offs, uint32_t *cursor,
-                          void *ranges, uint32_t ntiles, hipStream_t s) {
-    if (fp->tri_count == 0) return hipSuccess;
-    const dim3 grid((fp->tri_count + 255) / 256);
-    hipLaunchKernelGGL(prk::k_bin_count, grid, dim3(256), 0, s, *fp, counts,
-                       reinterpret_cast<prk::TileRange *>(ranges));
-    hipLaunchKernelGGL(prk::k_scan, dim3(1), dim3(1024), 0, s, counts, offs, ntiles);
-    (void)cursor;
-    return hipGetLastError();
-}
-
-hipError_t prk_launch_fill(const prk::FrameParams *fp, const void *ranges, const uint32_t *offs,
-                           uint32_t *cursor, uint32_t *bins, hipStream_t s) {
-    if (fp->tri_count == 0) return hipSuccess;
-    const dim3 grid((fp->tri_count + 255) / 256);
-    hipLaunchKernelGGL(prk::k_bin_fill, grid, dim3(256), 0, s, *fp,
-                       reinterpret_cast<const prk::TileRange *>(ranges), offs, cursor, bins);
-    return hipGetLastError();
-}
-
 hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint32_t *offs,
-                             const uint32_t *bins, uint32_t *anomaly, hipStream_t s) {
+                             const uint32_t *bins, uint8_t *won, uint32_t *list, uint32_t *anomaly, hipStream_t s) {
     const uint32_t ntile = (uint32_t)(fp->tiles_x * fp->tiles_y);
     if (ntile == 0) return hipSuccess;
-    const size_t lds = (size_t)fp->tile_w * fp->tile_h * (sizeof(unsigned long long) + sizeof(uint32_t)) +
-                       prk::kWaves * sizeof(prk::WaveSlots);
+    const size_t lds = (size_t)fp->tile_w * fp->tile_h * sizeof(unsigned long long) +
+                       prk::kWaves * sizeof(prk::WaveSlots) + 16 * sizeof(uint32_t);
+#define PRK_LAUNCH(MS) \
+    hipLaunchKernelGGL(prk::k_raster<MS>, dim3(ntile), dim3(64 * prk::kWaves), lds, s, *fp, offs, bins, won, list, anomaly)
     switch (modeset) {
-        case prk::MODE_AVX:
-            hipLaunchKernelGGL(prk::k_raster<prk::MODE_AVX>, dim3(ntile), dim3(256), lds, s, *fp, offs, bins,
-                               anomaly);
-            break;
-        case prk::MODE_SC_GOURAUD:
-            hipLaunchKernelGGL(prk::k_raster<prk::MODE_SC_GOURAUD>, dim3(ntile), dim3(256), lds, s, *fp, offs,
-                               bins, anomaly);
-            break;
-        case prk::MODE_SC_PHONG:
-            hipLaunchKernelGGL(prk::k_raster<prk::MODE_SC_PHONG>, dim3(ntile), dim3(256), lds, s, *fp, offs,
-                               bins, anomaly);
-            break;
-        default:
-            hipLaunchKernelGGL(prk::k_raster<-1>, dim3(ntile), dim3(256), lds, s, *fp, offs, bins, anomaly);
-            break;
+        case prk::MODE_AVX: PRK_LAUNCH(prk::MODE_AVX); break;
+        case prk::MODE_SC_GOURAUD: PRK_LAUNCH(prk::MODE_SC_GOURAUD); break;
+        case prk::MODE_SC_PHONG: PRK_LAUNCH(prk::MODE_SC_PHONG); break;
+        default: PRK_LAUNCH(-1); break;
     }
+#undef PRK_LAUNCH
     return hipGetLastError();
 }
 
