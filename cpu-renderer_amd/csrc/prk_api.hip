@@ -568,8 +568,8 @@ int prk_flush(prk_context *c, void *stream) {
     PRK_TRY(hipMemsetAsync(c->d_won.p, 0, ne, s));
     PRK_TRY(hipEventRecord(c->ev[slot][1], s));
     if (!c->d_anomaly.p) {
-        PRK_TRY(c->d_anomaly.ensure(4));
-        PRK_TRY(hipMemsetAsync(c->d_anomaly.p, 0, 4, s));
+        PRK_TRY(c->d_anomaly.ensure(8));  // [anomalies, slow replays]
+        PRK_TRY(hipMemsetAsync(c->d_anomaly.p, 0, 8, s));
     }
     PRK_TRY(prk_launch_raster(&fp, modeset, (const uint32_t *)c->d_offs.p, (const uint32_t *)c->d_bins.p,
                               (uint8_t *)c->d_won.p, (uint32_t *)c->d_list.p, (uint32_t *)c->d_anomaly.p, s));
@@ -597,7 +597,8 @@ int prk_get_stats(prk_context *c, prk_stats *out) {
         harvest(c, (int)((c->frame + i) % prk_context::kRing));
     if (c->d_anomaly.p) {
         PRK_TRY(hipDeviceSynchronize());
-        PRK_TRY(hipMemcpy(&c->stats.anomalies, c->d_anomaly.p, 4, hipMemcpyDeviceToHost));
+        static_assert(offsetof(prk_stats, slow_replays) == offsetof(prk_stats, anomalies) + 4, "counter pair");
+        PRK_TRY(hipMemcpy(&c->stats.anomalies, c->d_anomaly.p, 8, hipMemcpyDeviceToHost));
     }
     *out = c->stats;
     return PRK_OK;

@@ -412,6 +412,24 @@ __device__ __forceinline__ void step_edge(Edge &E) {
     if (TR::tex) { E.U += E.UG; E.V += E.VG; E.W += E.WG; }
 }
 
+// The list-order fields of an edge alone (X, its gradient and the keys of
+// insertion/expiry): Walker<M, NRM, EdgeX> replays only the AET order.
+struct EdgeX {
+    float X, G;
+    int32_t YMin, YMax, Left;
+};
+
+__device__ __forceinline__ EdgeX edge_x(const Edge &E, float X) { return EdgeX{X, E.G, E.YMin, E.YMax, E.Left}; }
+
+__device__ __forceinline__ EdgeX sel(bool c, const EdgeX &a, const EdgeX &b) {
+    return EdgeX{c ? a.X : b.X, c ? a.G : b.G, c ? a.YMin : b.YMin, c ? a.YMax : b.YMax, c ? a.Left : b.Left};
+}
+
+template <int M, bool NRM>
+__device__ __forceinline__ void step_edge(EdgeX &E) {
+    E.X += E.G;
+}
+
 // AET insertion order (projekt.cpp:3663-3667).
 __device__ __forceinline__ bool insert_before(const Edge &A, const Edge &B) {
     return A.X < B.X || (A.X == B.X && (A.G < B.G || (A.G == B.G && A.Left < B.Left)));
@@ -428,16 +446,16 @@ __device__ __forceinline__ bool insert_before(const Edge &A, const Edge &B) {
 // it, so all insertions of FirstRow happen in init() and at
 // most one edge is still pending afterwards; `anomaly` counts triangles
 // violating that (never observed; reported by the host).
-template <int M, bool NRM>
+template <int M, bool NRM, typename EdgeT = Edge>
 struct Walker {
-    Edge E0, E1, E2;
+    EdgeT E0, E1, E2;
     uint32_t ord;     // list slot j holds edge (ord >> 2j) & 3
     int cnt;          // list length
     int pend;         // index of the pending edge, or -1
     int32_t FirstRow, MaxY, Row;
 
     __device__ __forceinline__ int slot(int j) const { return (int)((ord >> (2 * j)) & 3u); }
-    __device__ __forceinline__ Edge get(int k) const { return sel(k == 0, E0, sel(k == 1, E1, E2)); }
+    __device__ __forceinline__ EdgeT get(int k) const { return sel(k == 0, E0, sel(k == 1, E1, E2)); }
     // (value selects: a conditional over lvalues would become a pointer select
     // and push the walker to scratch memory)
     template <typename T>
@@ -463,7 +481,7 @@ struct Walker {
         ++cnt;
     }
 
-    __device__ __forceinline__ void init(int n, const Edge &s0, const Edge &s1, const Edge &s2, int32_t H,
+    __device__ __forceinline__ void init(int n, const EdgeT &s0, const EdgeT &s1, const EdgeT &s2, int32_t H,
                                          int32_t row_end, uint32_t &anomaly) {
         E0 = s0; E1 = s1; E2 = s2;
         FirstRow = s0.YMin;
@@ -515,7 +533,7 @@ struct Walker {
     __device__ __forceinline__ void end_row(bool paired) {
         if (paired) {
             const int a = slot(0), b = slot(1);
-            Edge t0 = E0, t1 = E1, t2 = E2;
+            EdgeT t0 = E0, t1 = E1, t2 = E2;
             step_edge<M, NRM>(t0);
             step_edge<M, NRM>(t1);
             step_edge<M, NRM>(t2);
@@ -525,6 +543,56 @@ struct Walker {
             if (X(a) > X(b)) ord = (ord & ~0xFu) | ((uint32_t)a << 2) | (uint32_t)b;
         }
         ++Row;
+    }
+
+    // Rows [Row, min(ystart, MaxY)) above the tile, straight after init(n, ...):
+    // the same edge state and list order as begin_row/end_row row by row, at
+    // a few adds per edge and row.  Within one triangle the active set of a
+    // row follows from the edges' [YMin, YMax) alone; when exactly two edges
+    // are active on every replayed row, each edge is stepped on every row of
+    // its interval and the DDAs run independently.  The order entering row
+    // `stop` is then the strict X order of the last pair (the crossing swap,
+    // 3831-3841); an X tie (or NaN) leaves the order to history, which is
+    // replayed on X alone (returns 1).  Returns -1, changing nothing, when the
+    // rows are irregular (a row with fewer or more than two active edges): the
+    // caller then replays row by row.  0: replayed by the edge DDAs alone.
+    __device__ __forceinline__ int fast_replay(int32_t ystart, int n) {
+        if (MaxY <= ystart) {  // the triangle ends above the tile: nothing to draw
+            Row = max(Row, MaxY);
+            return 0;
+        }
+        const int32_t stop = ystart;
+        if (Row >= stop) return 0;
+        if (n < 2 || E1.YMin != FirstRow || cnt < 2 || Row != FirstRow) return -1;
+        const int32_t h0 = min(E0.YMax, stop), h1 = min(E1.YMax, stop);
+        const int32_t i2 = n > 2 ? E2.YMin : stop, h2 = n > 2 ? min(E2.YMax, stop) : stop;
+        const int32_t l0 = max(0, h0 - FirstRow), l1 = max(0, h1 - FirstRow), l2 = max(0, h2 - i2);
+        const bool three = n > 2 && i2 < min(min(h0, h1), h2);
+        if (three || l0 + l1 + l2 != 2 * (stop - FirstRow)) return -1;
+        const float ox0 = E0.X, ox1 = E1.X, ox2 = E2.X;
+        for (int32_t k = 0; k < l0; ++k) step_edge<M, NRM>(E0);
+        for (int32_t k = 0; k < l1; ++k) step_edge<M, NRM>(E1);
+        for (int32_t k = 0; k < l2; ++k) step_edge<M, NRM>(E2);
+        // The pair of row stop-1 (exactly two of these hold).
+        const bool act0 = E0.YMax >= stop, act1 = E1.YMax >= stop;
+        const int a = act0 ? 0 : 1, b = (act0 && act1) ? 1 : 2;
+        const float xa = X(a), xb = X(b);
+        int slow = 0;
+        if (xa < xb) ord = (uint32_t)a | ((uint32_t)b << 2);
+        else if (xa > xb) ord = (uint32_t)b | ((uint32_t)a << 2);
+        else {
+            Walker<M, NRM, EdgeX> w;
+            uint32_t unused = 0;
+            w.init(n, edge_x(E0, ox0), edge_x(E1, ox1), edge_x(E2, ox2), 0x7fffffff, MaxY, unused);
+            w.MaxY = MaxY;
+            while (w.Row < stop) w.end_row(w.begin_row());
+            ord = w.ord;
+            slow = 1;
+        }
+        cnt = 2;
+        pend = (n > 2 && i2 >= stop) ? 2 : -1;
+        Row = stop;
+        return slow;
     }
 };
 

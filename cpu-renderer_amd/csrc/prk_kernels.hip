@@ -21,7 +21,8 @@
 #include "prk_device.h"
 
 // Diagnostic builds only (tools/diag): 1 = skip the shading sweep, 2 = skip
-// work items, 4 = skip the AET rows (setup only).  Never set in a product build.
+// work items, 4 = skip the AET rows (setup only), 8 = skip the shading sweep's
+// work items.  Never set in a product build.
 #ifndef PRK_DIAG
 #define PRK_DIAG 0
 #endif
@@ -478,8 +479,12 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
             active = ne >= 2;
             if (active) {
                 wk.init(ne, s0, s1, s2, fp.H, tc.y1, anom);
-                // Replay the rows above the tile (edge DDA only).
-                while (wk.Row < ystart && wk.Row < wk.MaxY) wk.end_row(wk.begin_row());
+                // Replay the rows above the tile (edge DDA only); row by row
+                // only for irregular edge lists.
+                const int fr = wk.fast_replay(ystart, ne);
+                if (fr < 0)
+                    while (wk.Row < ystart && wk.Row < wk.MaxY) wk.end_row(wk.begin_row());
+                if (fr != 0 && !SHADE) atomicAdd(anomaly + 1, 1u);
                 active = wk.Row < wk.MaxY;
             }
         }
@@ -505,7 +510,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (int it0 = 0; it0 < ((PRK_DIAG & 2) ? 0 : total); it0 += 64) {
+            for (int it0 = 0; it0 < (((PRK_DIAG & 2) || ((PRK_DIAG & 8) && SHADE)) ? 0 : total); it0 += 64) {
                 const int it = it0 + lane;
                 if (it < total) {
                     int lo = 0, hi = 63;  // first slot whose inclusive prefix exceeds it

@@ -191,3 +191,44 @@ def displaced_sphere(n_target, width, height, seed=0, radius=0.9, bumps=0.08):
                  cam, LIGHTS_ONE, AMBIENT_ONE, None,
                  name="sphere%d_%dx%d" % (len(tris), width, height),
                  meta=dict(kind="displaced_sphere"))
+
+
+def slivers(n_tris, width, height, seed=0, textured=True):
+    """Edge cases of the AET order: near-vertical slivers far right on the
+    screen whose two top edges have gradients below half an ulp of X, so
+    X + G rounds back to X and the two edges tie in X on every row.  The list
+    order then comes from the insertion tie-break (G, then Left;
+    projekt.cpp:3663-3667) carried through rows without a crossing swap
+    (3831-3841).  DrawModel's inclusive span draws the one pixel at X with the
+    LEFT edge's attributes, so a wrong order shows in z and colour."""
+    rng = np.random.default_rng(seed)
+    cam = default_camera(width, height)
+    n = int(n_tris)
+    x0 = rng.uniform(width * 0.75, width - 4.0, n)
+    y0 = rng.uniform(0.0, height - 48.0, n)
+    h1 = rng.uniform(4.0, 24.0, n)
+    h2 = h1 + rng.uniform(4.0, 24.0, n)
+    ulp = np.spacing(np.float32(width)).astype(np.float64)
+    # |dx / h| well below half an ulp: both top edges stick at X = x0.
+    s = np.empty((n, 3, 2))
+    s[:, 0] = np.stack([x0, y0], 1)
+    s[:, 1] = np.stack([x0 + rng.uniform(0.5, 4.0, n) * ulp, y0 + h1], 1)
+    s[:, 2] = np.stack([x0 + rng.uniform(-4.0, 4.0, n) * ulp, y0 + h2], 1)
+    # a quarter of them widen below the middle vertex (spans of several pixels)
+    wide = rng.random(n) < 0.25
+    s[wide, 1, 0] += rng.uniform(2.0, 10.0, wide.sum())
+    e1 = s[:, 1] - s[:, 0]
+    e2 = s[:, 2] - s[:, 0]
+    flip = e1[:, 0] * e2[:, 1] - e1[:, 1] * e2[:, 0] > 0
+    s[flip, 1], s[flip, 2] = s[flip, 2].copy(), s[flip, 1].copy()
+    z = rng.uniform(-0.8, 0.8, n)[:, None] + rng.uniform(-0.1, 0.1, (n, 3))
+    x, y = _unproject(s[..., 0], s[..., 1], z, cam)
+    verts = np.stack([x, y, z], -1).reshape(-1, 3).astype(np.float32)
+    nrm = rng.normal(size=(3 * n, 3))
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    uvs = rng.uniform(0.0, 1.0, (3 * n, 2)).astype(np.float32)
+    cols = rng.uniform(0.0, 1.0, (3 * n, 4)).astype(np.float32)
+    cols[:, 3] = 1.0
+    tex = random_texture(rng, 64, 64) if textured else None
+    return Scene(width, height, verts, cols, nrm.astype(np.float32), uvs, cam, LIGHTS_ONE, AMBIENT_ONE, tex,
+                 name="slivers%d_%dx%d_s%d" % (n, width, height, seed), meta=dict(kind="slivers", seed=seed))

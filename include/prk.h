@@ -98,7 +98,10 @@ typedef struct prk_stats {
     double sum_ms_raster;
     uint32_t anomalies;      /* triangles whose AET left the proven
                                 per-triangle shape (always 0) */
-    uint32_t pad;
+    uint32_t slow_replays;   /* bin entries whose rows above their tile were
+                                replayed row by row (irregular edge list or
+                                an X tie); cumulative like
+                                anomalies */
 } prk_stats;
 
 typedef struct prk_context prk_context;

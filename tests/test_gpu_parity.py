@@ -244,3 +244,16 @@ def test_dropin_demo_matches_oracle(gpu, tmp_path, scalar):
     assert (gz.view(np.uint32) == oz.view(np.uint32)).all()
     assert (gc == oc).all()
     assert (ow >= 0).sum() > 2000
+
+
+@pytest.mark.parametrize("semantics,phong,textured", [(abi.PRK_SEM_SCALAR, False, False),
+                                                       (abi.PRK_SEM_SCALAR, True, True),
+                                                       (abi.PRK_SEM_AVX, True, True)])
+def test_sliver_x_ties(gpu, semantics, phong, textured):
+    # Two top edges tied in X on every row: the order entering each tile comes
+    # from history, which the fast replay must hand to the
+    # X-only row-by-row replay.
+    s = scenes.slivers(3000, 2048, 256, seed=4, textured=textured)
+    g, o = run_both(s, semantics=semantics, phong=phong, exact_color=semantics == abi.PRK_SEM_AVX)
+    assert (g[2] >= 0).sum() > 10000
+    assert g[3]["slow_replays"] > 0 and g[3]["anomalies"] == 0
