@@ -471,6 +471,12 @@ int prk_flush(prk_context *c, void *stream) {
     fp.Cx = c->transform.ScreenCenter[0];
     fp.Cy = c->transform.ScreenCenter[1];
     fp.InvM2P = 1.0f / fp.M2P;
+    {
+        int e = 0;
+        const float m = std::frexp(fp.F, &e);  // F = m * 2^e, |m| in [0.5, 1)
+        fp.f_pow2 = (std::isfinite(fp.F) && (m == 0.5f || m == -0.5f) && e - 1 >= -125 && e - 1 <= 126) ? 1 : 0;
+        fp.InvF = fp.f_pow2 ? 1.0f / fp.F : 0.0f;
+    }
     fp.light_count = c->lights.LightCount;
     for (int k = 0; k < 4; ++k) fp.amb[k] = c->lights.AmbientIntensity[k];
     for (uint32_t l = 0; l < PRK_MAX_LIGHTS; ++l) {
@@ -528,6 +534,9 @@ int prk_flush(prk_context *c, void *stream) {
     }
     fp.draws = (const prk::DrawRec *)c->d_draws.p;
     fp.texs = (const prk::TexRec *)c->d_texs.p;
+    fp.draw0 = c->draws[0];
+    fp.tex0 = prk::TexRec{};
+    if (fp.draw0.tex >= 0 && (size_t)fp.draw0.tex < texs.size()) fp.tex0 = texs[fp.draw0.tex];
     fp.tri_draw = nullptr;
     if (fp.ndraws > 1) {
         PRK_TRY(c->d_tri_draw.ensure((size_t)T * 4));

@@ -46,6 +46,8 @@ struct TexRec {
 struct FrameParams {
     // projective_transform
     float D, F, M2P, Cx, Cy, InvM2P;
+    float InvF;       // 1/F, exact when f_pow2
+    int32_t f_pow2;   // F = 2^k (k in [-125,126]): d/F == d*InvF bit for bit
     // light_data
     uint32_t light_count;
     float amb[4];
@@ -65,7 +67,30 @@ struct FrameParams {
     const DrawRec *draws;
     const uint32_t *tri_draw;  // nullptr when ndraws == 1
     const TexRec *texs;
+    // Single-draw frames (k_raster<M, true>): the draw and its texture as
+    // kernel arguments, i.e. wave-uniform scalar registers.
+    DrawRec draw0;
+    TexRec tex0;
 };
+
+// d / FocalLength of UnprojectVertex(_8x) (projekt.cpp:141-142, 157).  When
+// F is a power of two the quotient is the single rounding of d*2^-k, which
+// the multiply by the exact 1/F also produces.  (fp is uniform: a scalar
+// branch, no divergence.)
+__device__ __forceinline__ float div_focal(const FrameParams &fp, float d) {
+    if (fp.f_pow2) return d * fp.InvF;
+    return d / fp.F;
+}
+
+// (float)k / 255.0f for an integer k in [0, 255], bit for bit: k * RN(1/255)
+// plus one FMA residual correction is the correctly rounded quotient for
+// every such k (exhaustive check: tests/test_oracle.py::test_u8_unit_exact).
+__device__ __forceinline__ float u8_unit(uint32_t k) {
+    const float c = 0x1.010102p-8f;  // RN(1/255)
+    const float kf = (float)k, q0 = kf * c;
+    const float rem = __builtin_fmaf(-255.0f, q0, kf);  // exact residual
+    return __builtin_fmaf(rem, c, q0);
+}
 
 // Tiles a triangle may touch: the rectangle [tx0..tx1] x [ty0..ty1], plus
 // for scalar semantics the column-0 tiles of rows [oty0..oty1] that receive

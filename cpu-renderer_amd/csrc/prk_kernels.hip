@@ -22,7 +22,8 @@
 
 // Diagnostic builds only (tools/diag): 1 = skip the shading sweep, 2 = skip
 // work items, 4 = skip the AET rows (setup only), 8 = skip the shading sweep's
-// work items.  Never set in a product build.
+// work items, 16 = no Phong/texel (winners store a dummy colour).  Never set
+// in a product build.
 #ifndef PRK_DIAG
 #define PRK_DIAG 0
 #endif
@@ -62,13 +63,16 @@ __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
 // Items are spread over the 64 lanes (prefix sum + binary search), so the
 // pixel work no longer serialises on the lane that owns the triangle.
 // ---------------------------------------------------------------------------
+#ifndef PRK_ZPRE
+#define PRK_ZPRE 1  // sweep 1: skip 1/w and the UV mask of fragments that cannot raise the key
+#endif
 #ifndef PRK_WAVES
 #define PRK_WAVES 2  // waves per tile workgroup; each takes whole 64-entry chunks of the bin
 #endif
 constexpr int kWaves = PRK_WAVES;
 constexpr int kSpanF = 22;  // float fields per span slot
-constexpr int kSpanI = 8;   // int fields per span slot
-enum { SI_XA = 0, SI_XB, SI_LEFT, SI_PRE, SI_TAG, SI_ROW, SI_OVF, SI_TEX };
+constexpr int kSpanI = 7;   // int fields per span slot (the row is the sweep's current row)
+enum { SI_XA = 0, SI_XB, SI_LEFT, SI_PRE, SI_TAG, SI_OVF, SI_TEX };
 // AVX float slots
 enum { SF_XOFF = 0, SF_LW, SF_LU, SF_LV, SF_LZ, SF_IW, SF_IU, SF_IV, SF_IZ, SF_LN0, SF_LN1, SF_LN2,
        SF_IN0, SF_IN1, SF_IN2 };
@@ -148,7 +152,6 @@ __device__ __forceinline__ int span_setup_avx(const FrameParams &fp, const TileC
     ws.i[SI_XB][lane] = xb;
     ws.i[SI_LEFT][lane] = LeftXa;
     ws.i[SI_TAG][lane] = (int32_t)tag;
-    ws.i[SI_ROW][lane] = Row;
     ws.i[SI_TEX][lane] = texi;
     ws.f[SF_XOFF][lane] = XOffset;
     ws.f[SF_LW][lane] = L.W; ws.f[SF_LU][lane] = L.U; ws.f[SF_LV][lane] = L.V; ws.f[SF_LZ][lane] = L.Z;
@@ -211,7 +214,6 @@ __device__ __forceinline__ int span_setup_scalar(const FrameParams &fp, const Ti
     ws.i[SI_XB][lane] = xb;
     ws.i[SI_LEFT][lane] = MinX;
     ws.i[SI_TAG][lane] = (int32_t)tag;
-    ws.i[SI_ROW][lane] = Row;
     ws.i[SI_OVF][lane] = ovf ? (Row + 1 - tc.y0) * tc.tw : -1;
     ws.i[SI_TEX][lane] = texi;
     ws.f[SS_Z][lane] = L.Z + XOffset * IZ;  // 408-412: Current* += XOffset*Increment
@@ -246,15 +248,14 @@ __device__ __forceinline__ uint32_t shade_avx(const FrameParams &fp, const TexRe
     const int32_t FX = (int32_t)((uint32_t)cvtt_s32((float)tex.w * fu) << 2);
     const int32_t FY = mul16_trick(cvtt_s32((float)tex.h * fv), tex.pitch);
     const uint32_t t = texel_at(tex, (int32_t)((uint32_t)FX + (uint32_t)FY));
-    const float CA = (float)((t >> 24) & 0xFF) / 255.0f;
-    const float CR = (float)((t >> 16) & 0xFF) / 255.0f;
-    const float CG = (float)((t >> 8) & 0xFF) / 255.0f;
-    const float CB = (float)(t & 0xFF) / 255.0f;
+    const float CA = u8_unit((t >> 24) & 0xFF), CR = u8_unit((t >> 16) & 0xFF);
+    const float CG = u8_unit((t >> 8) & 0xFF), CB = u8_unit(t & 0xFF);
     // Phong (2040-2128) at UnprojectVertex_8x (102-145).
     const float d = fp.D - z;
     const float Xf = (float)(x - i) + (float)i, Yf = (float)Row + 0.0f;
     const float AX = (Xf - fp.Cx) * fp.InvM2P, AY = (Yf - fp.Cy) * fp.InvM2P;
-    const float PX = (d / fp.F) * AX, PY = (d / fp.F) * AY, PZ = z;
+    const float dF = div_focal(fp, d);
+    const float PX = dF * AX, PY = dF * AY, PZ = z;
     float Fr = 0, Fg = 0, Fb = 0, Fa = 0;
     for (uint32_t li = 0; li < fp.light_count; ++li) {
         if (li == 0) {
@@ -285,12 +286,11 @@ __device__ __forceinline__ uint32_t shade_avx(const FrameParams &fp, const TexRe
 }
 
 // Item j of an AVX span: lane chain i = (xa + j - LeftXa) & 7 from block b.
-template <bool SHADE>
+template <bool SHADE, bool UNI>
 __device__ __forceinline__ void item_avx(const FrameParams &fp, const TileCtx &tc, const WaveSlots &ws, int s,
-                                         int j) {
+                                         int j, int32_t Row) {
     const int32_t xa = ws.i[SI_XA][s], xb = ws.i[SI_XB][s], LeftXa = ws.i[SI_LEFT][s];
     const uint32_t tag = (uint32_t)ws.i[SI_TAG][s];
-    const int32_t Row = ws.i[SI_ROW][s];
     const int rowoff = (Row - tc.y0) * tc.tw - tc.x0;
     int32_t x = xa + j;
     if (SHADE) {
@@ -300,7 +300,7 @@ __device__ __forceinline__ void item_avx(const FrameParams &fp, const TileCtx &t
     }
     // The texture of the span's draw (the item may run on any lane).
     TexRec tex;
-    if (SHADE) tex = fp.texs[ws.i[SI_TEX][s]];
+    if (SHADE) tex = UNI ? fp.tex0 : fp.texs[ws.i[SI_TEX][s]];
     else { tex.mem = nullptr; tex.w = tex.h = tex.pitch = tex.pad = 0; }
     const int32_t rel = x - LeftXa, i = rel & 7, b = rel >> 3;
     const float IW = ws.f[SF_IW][s], IU = ws.f[SF_IU][s], IV = ws.f[SF_IV][s], IZ = ws.f[SF_IZ][s];
@@ -324,14 +324,23 @@ __device__ __forceinline__ void item_avx(const FrameParams &fp, const TileCtx &t
         z = z + IZ8; w = w + IW8; u = u + IU8; v = v + IV8;
     }
     for (; x < xb; x += 8) {
-        const float iw = 1.0f / w;  // 1865-1866
-        const float fu = iw * u, fv = iw * v;
         const int p = rowoff + x;
         if (!SHADE) {
-            if (fu >= 0.0f && fu <= 1.0f && fv >= 0.0f && fv <= 1.0f && z == z)
-                atomicMax(&tc.key[p], make_key(z, tag));
+            // A key not above the pixel's current maximum cannot change it,
+            // whatever the UV mask says: skip the 1/w and the mask.
+            const unsigned long long k = make_key(z, tag);
+            if (!PRK_ZPRE || k > tc.key[p]) {
+                const float iw = 1.0f / w;  // 1865-1866
+                const float fu = iw * u, fv = iw * v;
+                if (fu >= 0.0f && fu <= 1.0f && fv >= 0.0f && fv <= 1.0f && z == z) atomicMax(&tc.key[p], k);
+            }
         } else {
-            if (is_winner(tc, p, tag)) put_winner(fp, tc, p, z, shade_avx(fp, tex, fu, fv, z, n0, n1, n2, x, i, Row));
+            if (is_winner(tc, p, tag)) {
+                const float iw = 1.0f / w;  // 1865-1866
+                const float fu = iw * u, fv = iw * v;
+                put_winner(fp, tc, p, z, (PRK_DIAG & 16) ? __float_as_uint(fu + fv + n0 + n1 + n2)
+                                                         : shade_avx(fp, tex, fu, fv, z, n0, n1, n2, x, i, Row));
+            }
             if (x + 8 < xb) {
                 float a = n0 + IN08, bb = n1 + IN18, c = n2 + IN28;
                 normalize_div(a, bb, c);
@@ -343,13 +352,13 @@ __device__ __forceinline__ void item_avx(const FrameParams &fp, const TileCtx &t
 }
 
 // A whole DrawModel span (projekt.cpp:423-538) restricted to the tile.
-template <int M, bool SHADE>
-__device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx &tc, const WaveSlots &ws, int s) {
+template <int M, bool SHADE, bool UNI>
+__device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx &tc, const WaveSlots &ws, int s,
+                                            int32_t Row) {
     using TR = ModeTraits<M>;
     const int32_t W = fp.W;
     const int32_t xa = ws.i[SI_XA][s], xb = ws.i[SI_XB][s], MinX = ws.i[SI_LEFT][s];
     const uint32_t tag = (uint32_t)ws.i[SI_TAG][s];
-    const int32_t Row = ws.i[SI_ROW][s];
     const int povf = ws.i[SI_OVF][s];
     const int rowoff = (Row - tc.y0) * tc.tw - tc.x0;
     const int32_t xend = povf >= 0 ? W + 1 : xb;
@@ -359,7 +368,7 @@ __device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx
         if (!any) return;
     }
     TexRec tex;
-    if (SHADE && TR::tex) tex = fp.texs[ws.i[SI_TEX][s]];  // the span's draw, not this lane's
+    if (SHADE && TR::tex) tex = UNI ? fp.tex0 : fp.texs[ws.i[SI_TEX][s]];  // the span's draw, not this lane's
     else { tex.mem = nullptr; tex.w = tex.h = tex.pitch = tex.pad = 0; }
     float z = ws.f[SS_Z][s];
     const float IZ = ws.f[SS_IZ][s];
@@ -393,16 +402,17 @@ __device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx
                     const int32_t TY = round_s32(FV * (float)(tex.h - 1));
                     const uint32_t t =
                         texel_at(tex, (int32_t)((uint32_t)TX * 4u + (uint32_t)TY * (uint32_t)tex.pitch));
-                    C[3] = (float)((t >> 24) & 0xFF) / 255.0f;
-                    C[0] = (float)((t >> 16) & 0xFF) / 255.0f;
-                    C[1] = (float)((t >> 8) & 0xFF) / 255.0f;
-                    C[2] = (float)(t & 0xFF) / 255.0f;
+                    C[3] = u8_unit((t >> 24) & 0xFF);  // (r32)byte / 255.0f
+                    C[0] = u8_unit((t >> 16) & 0xFF);
+                    C[1] = u8_unit((t >> 8) & 0xFF);
+                    C[2] = u8_unit(t & 0xFF);
                 }
                 float F[4];
                 if (TR::phong) {  // 448-484 with UnprojectVertex (147-160)
                     const float d = fp.D - z;
-                    const float PX = (d / fp.F) * (((float)x - fp.Cx) * fp.InvM2P);
-                    const float PY = (d / fp.F) * (((float)Row - fp.Cy) * fp.InvM2P);
+                    const float dF = div_focal(fp, d);
+                    const float PX = dF * (((float)x - fp.Cx) * fp.InvM2P);
+                    const float PY = dF * (((float)Row - fp.Cy) * fp.InvM2P);
                     const float PZ = z;
                     F[0] = F[1] = F[2] = F[3] = 0.0f;
                     for (uint32_t li = 0; li < fp.light_count; ++li) {
@@ -453,7 +463,7 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 
 // One sweep over the tile's bin for mode M.  SHADE=false: visibility keys;
 // SHADE=true: shade the winners.
-template <int M, bool SHADE>
+template <int M, bool SHADE, bool UNI>
 __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, WaveSlots &ws,
                                       const uint32_t *__restrict__ bins, uint32_t b0, uint32_t n,
                                       const uint32_t *__restrict__ list, uint32_t *anomaly) {
@@ -465,17 +475,26 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
         const uint32_t i = base + lane;
         bool active = i < n;
         uint32_t e = 0;
-        const DrawRec *d = fp.draws;
+        int32_t texi = 0;
         Walker<M, SHADE> wk;
         uint32_t anom = 0;
         if (active) {
             e = list ? list[b0 + i] : i;
             const uint32_t g = bins[b0 + e];
-            uint32_t gt;
-            resolve_draw(fp, g, d, gt);
             Edge s0, s1, s2;
-            // (mixed frames sweep the bin once per mode)
-            const int ne = d->mode == M ? setup_triangle<M>(*d, gt, fp, s0, s1, s2) : 0;
+            int ne;
+            if constexpr (UNI) {  // one draw: its record is uniform (kernel arguments)
+                const uint32_t gt = fp.draw0.geom_tri0 + (g - fp.draw0.first_global);
+                ne = setup_triangle<M>(fp.draw0, gt, fp, s0, s1, s2);
+                texi = fp.draw0.tex;
+            } else {
+                const DrawRec *d;
+                uint32_t gt;
+                resolve_draw(fp, g, d, gt);
+                // (mixed frames sweep the bin once per mode)
+                ne = d->mode == M ? setup_triangle<M>(*d, gt, fp, s0, s1, s2) : 0;
+                texi = d->tex;
+            }
             active = ne >= 2;
             if (active) {
                 wk.init(ne, s0, s1, s2, fp.H, tc.y1, anom);
@@ -489,7 +508,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
             }
         }
         if (anom) atomicAdd(anomaly, anom);
-        const int32_t texi = (ModeTraits<M>::tex && active) ? d->tex : 0;
+        if (!(ModeTraits<M>::tex && active)) texi = 0;
         const uint32_t tag = 0xFFFFFFFEu - e;
         if (PRK_DIAG & 4) active = false;
         for (int32_t r = ystart; r < tc.y1; ++r) {
@@ -518,9 +537,9 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
                         const int mid = (lo + hi) >> 1;
                         if (ws.i[SI_PRE][mid] > it) hi = mid; else lo = mid + 1;
                     }
-                    const int j = it - (lo ? ws.i[SI_PRE][lo - 1] : 0);
-                    if (M == MODE_AVX) item_avx<SHADE>(fp, tc, ws, lo, j);
-                    else item_scalar<M, SHADE>(fp, tc, ws, lo);
+                    const int s = lo, j = it - (lo ? ws.i[SI_PRE][lo - 1] : 0);
+                    if (M == MODE_AVX) item_avx<SHADE, UNI>(fp, tc, ws, s, j, r);
+                    else item_scalar<M, SHADE, UNI>(fp, tc, ws, s, r);
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -531,12 +550,12 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
     }
 }
 
-template <int M>
+template <int M, bool UNI>
 __device__ __forceinline__ void raster_mode(const FrameParams &fp, const TileCtx &tc, WaveSlots &ws,
                                             const uint32_t *bins, uint32_t b0, uint32_t n, const uint32_t *list,
                                             uint32_t *anomaly, bool shade) {
-    if (!shade) sweep<M, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly);
-    else sweep<M, true>(fp, tc, ws, bins, b0, n, list, anomaly);
+    if (!shade) sweep<M, false, UNI>(fp, tc, ws, bins, b0, n, nullptr, anomaly);
+    else sweep<M, true, UNI>(fp, tc, ws, bins, b0, n, list, anomaly);
 }
 
 // Workgroup-wide exclusive scan of one value per thread.
@@ -555,7 +574,9 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *scratc
     return before + (uint32_t)incl - v;
 }
 
-template <int MODESET>  // a single Mode, or -1: any mode (per-draw dispatch)
+// MODESET: a single Mode, or -1: any mode (per-draw dispatch).  UNI: the frame
+// is one draw (then MODESET is its mode).
+template <int MODESET, bool UNI>
 __global__ void __launch_bounds__(64 * kWaves, PRK_RASTER_MIN_WAVES) k_raster(FrameParams fp, const uint32_t *__restrict__ offs,
                                                 const uint32_t *__restrict__ bins, uint8_t *__restrict__ won,
                                                 uint32_t *__restrict__ list, uint32_t *__restrict__ anomaly) {
@@ -593,14 +614,14 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_RASTER_MIN_WAVES) k_raster(Fr
     __syncthreads();
     // Sweep 1: visibility.
     if constexpr (MODESET >= 0) {
-        raster_mode<(MODESET >= 0 ? MODESET : 0)>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
+        raster_mode<(MODESET >= 0 ? MODESET : 0), UNI>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
     } else {
         // Mixed frame: each mode sweeps the bin and skips other modes' entries.
-        raster_mode<MODE_AVX>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
-        raster_mode<MODE_SC_GOURAUD>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
-        raster_mode<MODE_SC_GOURAUD_TEX>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
-        raster_mode<MODE_SC_PHONG>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
-        raster_mode<MODE_SC_PHONG_TEX>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
+        raster_mode<MODE_AVX, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
+        raster_mode<MODE_SC_GOURAUD, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
+        raster_mode<MODE_SC_GOURAUD_TEX, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
+        raster_mode<MODE_SC_PHONG, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
+        raster_mode<MODE_SC_PHONG_TEX, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
     }
     __syncthreads();
     if (PRK_DIAG & 1) return;
@@ -624,13 +645,13 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_RASTER_MIN_WAVES) k_raster(Fr
     __syncthreads();
     // Sweep 2: shade the winners.
     if constexpr (MODESET >= 0) {
-        raster_mode<(MODESET >= 0 ? MODESET : 0)>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
+        raster_mode<(MODESET >= 0 ? MODESET : 0), UNI>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
     } else {
-        raster_mode<MODE_AVX>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
-        raster_mode<MODE_SC_GOURAUD>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
-        raster_mode<MODE_SC_GOURAUD_TEX>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
-        raster_mode<MODE_SC_PHONG>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
-        raster_mode<MODE_SC_PHONG_TEX>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
+        raster_mode<MODE_AVX, false>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
+        raster_mode<MODE_SC_GOURAUD, false>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
+        raster_mode<MODE_SC_GOURAUD_TEX, false>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
+        raster_mode<MODE_SC_PHONG, false>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
+        raster_mode<MODE_SC_PHONG_TEX, false>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
     }
     __syncthreads();
     // Winners wrote their z and colour in sweep 2; untouched pixels keep the
@@ -648,10 +669,13 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_RASTER_MIN_WAVES) k_raster(Fr
 
 // Explicit instantiations used by the host.
 #define PRK_RASTER_ARGS FrameParams, const uint32_t *, const uint32_t *, uint8_t *, uint32_t *, uint32_t *
-template __global__ void k_raster<-1>(PRK_RASTER_ARGS);
-template __global__ void k_raster<MODE_AVX>(PRK_RASTER_ARGS);
-template __global__ void k_raster<MODE_SC_GOURAUD>(PRK_RASTER_ARGS);
-template __global__ void k_raster<MODE_SC_PHONG>(PRK_RASTER_ARGS);
+template __global__ void k_raster<-1, false>(PRK_RASTER_ARGS);
+template __global__ void k_raster<MODE_AVX, false>(PRK_RASTER_ARGS);
+template __global__ void k_raster<MODE_AVX, true>(PRK_RASTER_ARGS);
+template __global__ void k_raster<MODE_SC_GOURAUD, false>(PRK_RASTER_ARGS);
+template __global__ void k_raster<MODE_SC_GOURAUD, true>(PRK_RASTER_ARGS);
+template __global__ void k_raster<MODE_SC_PHONG, false>(PRK_RASTER_ARGS);
+template __global__ void k_raster<MODE_SC_PHONG, true>(PRK_RASTER_ARGS);
 
 }  // namespace prk
 
@@ -674,13 +698,19 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
     if (ntile == 0) return hipSuccess;
     const size_t lds = (size_t)fp->tile_w * fp->tile_h * sizeof(unsigned long long) +
                        prk::kWaves * sizeof(prk::WaveSlots) + 16 * sizeof(uint32_t);
-#define PRK_LAUNCH(MS) \
-    hipLaunchKernelGGL(prk::k_raster<MS>, dim3(ntile), dim3(64 * prk::kWaves), lds, s, *fp, offs, bins, won, list, anomaly)
+#define PRK_LAUNCH(MS, UNI) \
+    hipLaunchKernelGGL((prk::k_raster<MS, UNI>), dim3(ntile), dim3(64 * prk::kWaves), lds, s, *fp, offs, bins, won, \
+                       list, anomaly)
+    const bool uni = fp->ndraws == 1;
     switch (modeset) {
-        case prk::MODE_AVX: PRK_LAUNCH(prk::MODE_AVX); break;
-        case prk::MODE_SC_GOURAUD: PRK_LAUNCH(prk::MODE_SC_GOURAUD); break;
-        case prk::MODE_SC_PHONG: PRK_LAUNCH(prk::MODE_SC_PHONG); break;
-        default: PRK_LAUNCH(-1); break;
+        case prk::MODE_AVX: if (uni) PRK_LAUNCH(prk::MODE_AVX, true); else PRK_LAUNCH(prk::MODE_AVX, false); break;
+        case prk::MODE_SC_GOURAUD:
+            if (uni) PRK_LAUNCH(prk::MODE_SC_GOURAUD, true); else PRK_LAUNCH(prk::MODE_SC_GOURAUD, false);
+            break;
+        case prk::MODE_SC_PHONG:
+            if (uni) PRK_LAUNCH(prk::MODE_SC_PHONG, true); else PRK_LAUNCH(prk::MODE_SC_PHONG, false);
+            break;
+        default: PRK_LAUNCH(-1, false); break;
     }
 #undef PRK_LAUNCH
     return hipGetLastError();

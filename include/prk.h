@@ -100,7 +100,7 @@ typedef struct prk_stats {
                                 per-triangle shape (always 0) */
     uint32_t slow_replays;   /* bin entries whose rows above their tile were
                                 replayed row by row (irregular edge list or
-                                an X tie; DESIGN §4.4); cumulative like
+                                an X tie; DESIGN §4.3); cumulative like
                                 anomalies */
 } prk_stats;
 

@@ -251,7 +251,7 @@ def test_dropin_demo_matches_oracle(gpu, tmp_path, scalar):
                                                        (abi.PRK_SEM_AVX, True, True)])
 def test_sliver_x_ties(gpu, semantics, phong, textured):
     # Two top edges tied in X on every row: the order entering each tile comes
-    # from history (DESIGN.md §4.4), which the fast replay must hand to the
+    # from history (DESIGN.md §4.3), which the fast replay must hand to the
     # X-only row-by-row replay.
     s = scenes.slivers(3000, 2048, 256, seed=4, textured=textured)
     g, o = run_both(s, semantics=semantics, phong=phong, exact_color=semantics == abi.PRK_SEM_AVX)
