@@ -66,6 +66,9 @@ __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
 #ifndef PRK_ZPRE
 #define PRK_ZPRE 1  // sweep 1: skip 1/w and the UV mask of fragments that cannot raise the key
 #endif
+#ifndef PRK_PIXEL_ITEMS
+#define PRK_PIXEL_ITEMS 1  // shading sweep (AVX): one work item per won pixel, not per lane chain
+#endif
 #ifndef PRK_WAVES
 #define PRK_WAVES 2  // waves per tile workgroup; each takes whole 64-entry chunks of the bin
 #endif
@@ -159,6 +162,13 @@ __device__ __forceinline__ int span_setup_avx(const FrameParams &fp, const TileC
     if (SHADE) {
         ws.f[SF_LN0][lane] = L.N0; ws.f[SF_LN1][lane] = L.N1; ws.f[SF_LN2][lane] = L.N2;
         ws.f[SF_IN0][lane] = IN0; ws.f[SF_IN1][lane] = IN1; ws.f[SF_IN2][lane] = IN2;
+#if PRK_PIXEL_ITEMS
+        // Shading sweep: one item per pixel this span won.
+        const int rowoff = (Row - tc.y0) * tc.tw - tc.x0;
+        int won = 0;
+        for (int32_t x = xa; x < xb; ++x) won += is_winner(tc, rowoff + x, tag) ? 1 : 0;
+        return won;
+#endif
     }
     return min(8, xb - xa);
 }
@@ -351,6 +361,48 @@ __device__ __forceinline__ void item_avx(const FrameParams &fp, const TileCtx &t
     }
 }
 
+// Shading item j of an AVX span: the span's j-th won pixel.  Its lane chain
+// i = (x - LeftXa) & 7 is replayed from the lane init through b block steps
+// (the same recurrence item_avx walks), so every lane of the wave shades one
+// winning pixel instead of one chain that may hold none.
+template <bool UNI>
+__device__ __forceinline__ void item_avx_pixel(const FrameParams &fp, const TileCtx &tc, const WaveSlots &ws, int s,
+                                               int j, int32_t Row) {
+    const int32_t xa = ws.i[SI_XA][s], LeftXa = ws.i[SI_LEFT][s];
+    const uint32_t tag = (uint32_t)ws.i[SI_TAG][s];
+    const int rowoff = (Row - tc.y0) * tc.tw - tc.x0;
+    int32_t x = xa;
+    for (int k = j;; ++x) {
+        if (is_winner(tc, rowoff + x, tag)) {
+            if (k == 0) break;
+            --k;
+        }
+    }
+    const TexRec tex = UNI ? fp.tex0 : fp.texs[ws.i[SI_TEX][s]];
+    const int32_t rel = x - LeftXa, i = rel & 7, b = rel >> 3;
+    const float IW = ws.f[SF_IW][s], IU = ws.f[SF_IU][s], IV = ws.f[SF_IV][s], IZ = ws.f[SF_IZ][s];
+    const float IN0 = ws.f[SF_IN0][s], IN1 = ws.f[SF_IN1][s], IN2 = ws.f[SF_IN2][s];
+    const float o = ws.f[SF_XOFF][s] + (float)i;  // lane init (XOffset + i)*inc, 1712-1835
+    float w = ws.f[SF_LW][s] + o * IW, u = ws.f[SF_LU][s] + o * IU;
+    float v = ws.f[SF_LV][s] + o * IV, z = ws.f[SF_LZ][s] + o * IZ;
+    float n0 = ws.f[SF_LN0][s] + o * IN0, n1 = ws.f[SF_LN1][s] + o * IN1, n2 = ws.f[SF_LN2][s] + o * IN2;
+    normalize_div(n0, n1, n2);  // 1754
+    if (b > 0) {
+        const float IW8 = IW * 8.0f, IU8 = IU * 8.0f, IV8 = IV * 8.0f, IZ8 = 8.0f * IZ;
+        const float IN08 = IN0 * 8.0f, IN18 = IN1 * 8.0f, IN28 = IN2 * 8.0f;
+        for (int32_t k = 0; k < b; ++k) {  // block steps 2262-2282
+            float a = n0 + IN08, bb = n1 + IN18, c = n2 + IN28;
+            normalize_div(a, bb, c);
+            n0 = a; n1 = bb; n2 = c;
+            z = z + IZ8; w = w + IW8; u = u + IU8; v = v + IV8;
+        }
+    }
+    const float iw = 1.0f / w;  // 1865-1866
+    const float fu = iw * u, fv = iw * v;
+    put_winner(fp, tc, rowoff + x, z, (PRK_DIAG & 16) ? __float_as_uint(fu + fv + n0 + n1 + n2)
+                                                        : shade_avx(fp, tex, fu, fv, z, n0, n1, n2, x, i, Row));
+}
+
 // A whole DrawModel span (projekt.cpp:423-538) restricted to the tile.
 template <int M, bool SHADE, bool UNI>
 __device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx &tc, const WaveSlots &ws, int s,
@@ -538,7 +590,8 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
                         if (ws.i[SI_PRE][mid] > it) hi = mid; else lo = mid + 1;
                     }
                     const int s = lo, j = it - (lo ? ws.i[SI_PRE][lo - 1] : 0);
-                    if (M == MODE_AVX) item_avx<SHADE, UNI>(fp, tc, ws, s, j, r);
+                    if (M == MODE_AVX && SHADE && PRK_PIXEL_ITEMS) item_avx_pixel<UNI>(fp, tc, ws, s, j, r);
+                    else if (M == MODE_AVX) item_avx<SHADE, UNI>(fp, tc, ws, s, j, r);
                     else item_scalar<M, SHADE, UNI>(fp, tc, ws, s, r);
                 }
             }
