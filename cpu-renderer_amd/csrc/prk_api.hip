@@ -25,7 +25,7 @@ hipError_t prk_bin_phase1(const prk::FrameParams *, uint32_t *, uint32_t *, void
 hipError_t prk_bin_phase2(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, uint32_t *, uint32_t *,
                           uint32_t *, uint32_t *, uint32_t *, void *, size_t *, hipStream_t);
 hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, const uint32_t *, uint8_t *,
-                             uint32_t *, uint32_t *, hipStream_t);
+                             uint32_t *, uint32_t *, uint32_t *, uint32_t *, hipEvent_t, hipStream_t);
 }
 
 namespace {
@@ -89,7 +89,7 @@ struct prk_context {
     uint32_t pending_tris = 0;
     // scratch
     DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_tri_n, d_tri_off, d_keys_a, d_vals_a, d_keys_b, d_bins,
-        d_offs, d_won, d_list, d_temp, d_winners, d_anomaly;
+        d_offs, d_won, d_list, d_temp, d_winners, d_anomaly, d_nwin, d_wtag;
     uint32_t *h_total = nullptr;  // pinned
     int32_t tile_w = 256, tile_h = 8;  // measured best for C3b
     bool debug = false;
@@ -97,7 +97,7 @@ struct prk_context {
     prk_stats stats{};
     // Timing ring: 3 events per flush (before bin, before raster, after raster).
     static constexpr int kRing = 32;
-    hipEvent_t ev[kRing][3] = {};
+    hipEvent_t ev[kRing][4] = {};  // bin start, raster start, raster end, k_vis end
     bool pending[kRing] = {};
     uint32_t frame = 0;
     int last_slot = -1;
@@ -134,7 +134,7 @@ int prk_create(int device, prk_context **out) {
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     for (int i = 0; i < prk_context::kRing && e == hipSuccess; ++i)
-        for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreate(&c->ev[i][k]);
+        for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipEventCreate(&c->ev[i][k]);
     if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_total, sizeof(uint32_t), hipHostMallocDefault);
     if (e != hipSuccess) {
         prk_destroy(c);
@@ -162,7 +162,7 @@ int prk_destroy(prk_context *c) {
     }
     DevBuf *bufs[] = {&c->d_draws,  &c->d_texs,   &c->d_tri_draw, &c->d_ranges, &c->d_tri_n, &c->d_tri_off,
                       &c->d_keys_a, &c->d_vals_a, &c->d_keys_b,   &c->d_bins,   &c->d_offs,  &c->d_won,
-                      &c->d_list,   &c->d_temp,   &c->d_winners,  &c->d_anomaly};
+                      &c->d_list,   &c->d_temp,   &c->d_winners,  &c->d_anomaly, &c->d_nwin, &c->d_wtag};
     for (DevBuf *b : bufs) b->release();
     if (c->h_total) (void)hipHostFree(c->h_total);
     for (auto &slot : c->ev)
@@ -426,11 +426,13 @@ static void harvest(prk_context *c, int slot) {
     if (!c->pending[slot]) return;
     c->pending[slot] = false;
     if (hipEventSynchronize(c->ev[slot][2]) != hipSuccess) return;
-    float a = 0, b = 0;
+    float a = 0, b = 0, v = 0;
     if (hipEventElapsedTime(&a, c->ev[slot][0], c->ev[slot][1]) != hipSuccess) a = 0;
     if (hipEventElapsedTime(&b, c->ev[slot][1], c->ev[slot][2]) != hipSuccess) b = 0;
+    if (hipEventElapsedTime(&v, c->ev[slot][1], c->ev[slot][3]) != hipSuccess) v = 0;
     c->stats.sum_ms_bin += a;
     c->stats.sum_ms_raster += b;
+    c->stats.sum_ms_vis += v;
     c->stats.frames_timed += 1;
     if (slot == c->last_slot) {
         c->stats.ms_bin = a;
@@ -442,7 +444,7 @@ int prk_timing_reset(prk_context *c) {
     if (!c) return PRK_ERR_ARG;
     for (int i = 0; i < prk_context::kRing; ++i) c->pending[i] = false;
     c->stats.frames_timed = 0;
-    c->stats.sum_ms_bin = c->stats.sum_ms_raster = 0.0;
+    c->stats.sum_ms_bin = c->stats.sum_ms_raster = c->stats.sum_ms_vis = 0.0;
     return PRK_OK;
 }
 
@@ -580,8 +582,11 @@ int prk_flush(prk_context *c, void *stream) {
         PRK_TRY(c->d_anomaly.ensure(8));  // [anomalies, slow replays]
         PRK_TRY(hipMemsetAsync(c->d_anomaly.p, 0, 8, s));
     }
+    PRK_TRY(c->d_nwin.ensure((size_t)ntiles * 4));
+    PRK_TRY(c->d_wtag.ensure((size_t)ntiles * c->tile_w * c->tile_h * 4));
     PRK_TRY(prk_launch_raster(&fp, modeset, (const uint32_t *)c->d_offs.p, (const uint32_t *)c->d_bins.p,
-                              (uint8_t *)c->d_won.p, (uint32_t *)c->d_list.p, (uint32_t *)c->d_anomaly.p, s));
+                              (uint8_t *)c->d_won.p, (uint32_t *)c->d_list.p, (uint32_t *)c->d_nwin.p,
+                              (uint32_t *)c->d_wtag.p, (uint32_t *)c->d_anomaly.p, c->ev[slot][3], s));
     PRK_TRY(hipEventRecord(c->ev[slot][2], s));
     c->pending[slot] = true;
     c->last_slot = slot;

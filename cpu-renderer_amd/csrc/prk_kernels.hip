@@ -27,8 +27,11 @@
 #ifndef PRK_DIAG
 #define PRK_DIAG 0
 #endif
-#ifndef PRK_RASTER_MIN_WAVES
-#define PRK_RASTER_MIN_WAVES 3  // waves per SIMD the raster kernel is register-budgeted for
+#ifndef PRK_VIS_MIN_WAVES
+#define PRK_VIS_MIN_WAVES 3  // waves per SIMD k_vis is register-budgeted for
+#endif
+#ifndef PRK_SHADE_MIN_WAVES
+#define PRK_SHADE_MIN_WAVES 3  // waves per SIMD k_shade is register-budgeted for
 #endif
 
 namespace prk {
@@ -83,14 +86,19 @@ enum { SF_XOFF = 0, SF_LW, SF_LU, SF_LV, SF_LZ, SF_IW, SF_IU, SF_IV, SF_IZ, SF_L
 enum { SS_Z = 0, SS_IZ, SS_W, SS_U, SS_V, SS_IW, SS_IU, SS_IV, SS_N0, SS_N1, SS_N2, SS_IN0, SS_IN1, SS_IN2,
        SS_C0, SS_C1, SS_C2, SS_C3, SS_IC0, SS_IC1, SS_IC2, SS_IC3 };
 
-struct WaveSlots {
-    float f[kSpanF][64];
+template <int NF>
+struct WaveSlotsT {
+    float f[NF][64];
     int32_t i[kSpanI][64];
 };
+constexpr int kSpanFVis = 9;  // the visibility sweep reads no normals or colours (SF_IZ + 1)
+using VisSlots = WaveSlotsT<kSpanFVis>;
+using ShadeSlots = WaveSlotsT<kSpanF>;
 
 struct TileCtx {
     int32_t x0, x1, y0, y1, tw;  // tile pixel rectangle [x0,x1) x [y0,y1), LDS row stride tw
-    unsigned long long *key;     // LDS: visibility keys
+    unsigned long long *key;     // LDS (k_vis): visibility keys
+    const uint32_t *tags;        // LDS (k_shade): low key word = winning entry tag per pixel
 };
 
 __device__ __forceinline__ unsigned long long make_key(float z, uint32_t tag) {
@@ -98,7 +106,7 @@ __device__ __forceinline__ unsigned long long make_key(float z, uint32_t tag) {
 }
 
 __device__ __forceinline__ bool is_winner(const TileCtx &tc, int p, uint32_t tag) {
-    return (uint32_t)tc.key[p] == tag;
+    return tc.tags[p] == tag;
 }
 
 // The winning fragment of tile pixel p: store its z and colour (each pixel
@@ -114,8 +122,8 @@ __device__ __forceinline__ void put_winner(const FrameParams &fp, const TileCtx 
 // FillLineOptimized span setup (projekt.cpp:1543-1835) for row Row; writes the
 // lane's slot and returns its item count (pixels of [MinX, MaxX) in the tile,
 // at most 8 chains).
-template <bool SHADE>
-__device__ __forceinline__ int span_setup_avx(const FrameParams &fp, const TileCtx &tc, WaveSlots &ws, int lane,
+template <bool SHADE, class WS>
+__device__ __forceinline__ int span_setup_avx(const FrameParams &fp, const TileCtx &tc, WS &ws, int lane,
                                               uint32_t tag, int32_t texi, const Edge &L, const Edge &R,
                                               int32_t Row) {
     if (Row < tc.y0) return 0;
@@ -159,7 +167,7 @@ __device__ __forceinline__ int span_setup_avx(const FrameParams &fp, const TileC
     ws.f[SF_XOFF][lane] = XOffset;
     ws.f[SF_LW][lane] = L.W; ws.f[SF_LU][lane] = L.U; ws.f[SF_LV][lane] = L.V; ws.f[SF_LZ][lane] = L.Z;
     ws.f[SF_IW][lane] = IW; ws.f[SF_IU][lane] = IU; ws.f[SF_IV][lane] = IV; ws.f[SF_IZ][lane] = IZ;
-    if (SHADE) {
+    if constexpr (SHADE) {
         ws.f[SF_LN0][lane] = L.N0; ws.f[SF_LN1][lane] = L.N1; ws.f[SF_LN2][lane] = L.N2;
         ws.f[SF_IN0][lane] = IN0; ws.f[SF_IN1][lane] = IN1; ws.f[SF_IN2][lane] = IN2;
 #if PRK_PIXEL_ITEMS
@@ -174,8 +182,8 @@ __device__ __forceinline__ int span_setup_avx(const FrameParams &fp, const TileC
 }
 
 // DrawModel span setup (projekt.cpp:298-412).  One item per span.
-template <int M, bool SHADE>
-__device__ __forceinline__ int span_setup_scalar(const FrameParams &fp, const TileCtx &tc, WaveSlots &ws, int lane,
+template <int M, bool SHADE, class WS>
+__device__ __forceinline__ int span_setup_scalar(const FrameParams &fp, const TileCtx &tc, WS &ws, int lane,
                                                  uint32_t tag, int32_t texi, const Edge &L, const Edge &R,
                                                  int32_t Row) {
     using TR = ModeTraits<M>;
@@ -228,7 +236,7 @@ __device__ __forceinline__ int span_setup_scalar(const FrameParams &fp, const Ti
     ws.i[SI_TEX][lane] = texi;
     ws.f[SS_Z][lane] = L.Z + XOffset * IZ;  // 408-412: Current* += XOffset*Increment
     ws.f[SS_IZ][lane] = IZ;
-    if (SHADE) {
+    if constexpr (SHADE) {
         if (TR::tex) {
             ws.f[SS_W][lane] = L.W + XOffset * IW; ws.f[SS_IW][lane] = IW;
             ws.f[SS_U][lane] = L.U + XOffset * IU; ws.f[SS_IU][lane] = IU;
@@ -296,8 +304,8 @@ __device__ __forceinline__ uint32_t shade_avx(const FrameParams &fp, const TexRe
 }
 
 // Item j of an AVX span: lane chain i = (xa + j - LeftXa) & 7 from block b.
-template <bool SHADE, bool UNI>
-__device__ __forceinline__ void item_avx(const FrameParams &fp, const TileCtx &tc, const WaveSlots &ws, int s,
+template <bool SHADE, bool UNI, class WS>
+__device__ __forceinline__ void item_avx(const FrameParams &fp, const TileCtx &tc, const WS &ws, int s,
                                          int j, int32_t Row) {
     const int32_t xa = ws.i[SI_XA][s], xb = ws.i[SI_XB][s], LeftXa = ws.i[SI_LEFT][s];
     const uint32_t tag = (uint32_t)ws.i[SI_TAG][s];
@@ -319,7 +327,7 @@ __device__ __forceinline__ void item_avx(const FrameParams &fp, const TileCtx &t
     float w = ws.f[SF_LW][s] + o * IW, u = ws.f[SF_LU][s] + o * IU;
     float v = ws.f[SF_LV][s] + o * IV, z = ws.f[SF_LZ][s] + o * IZ;
     float n0 = 0, n1 = 0, n2 = 0, IN08 = 0, IN18 = 0, IN28 = 0;
-    if (SHADE) {
+    if constexpr (SHADE) {
         const float IN0 = ws.f[SF_IN0][s], IN1 = ws.f[SF_IN1][s], IN2 = ws.f[SF_IN2][s];
         IN08 = IN0 * 8.0f; IN18 = IN1 * 8.0f; IN28 = IN2 * 8.0f;
         n0 = ws.f[SF_LN0][s] + o * IN0; n1 = ws.f[SF_LN1][s] + o * IN1; n2 = ws.f[SF_LN2][s] + o * IN2;
@@ -366,7 +374,7 @@ __device__ __forceinline__ void item_avx(const FrameParams &fp, const TileCtx &t
 // (the same recurrence item_avx walks), so every lane of the wave shades one
 // winning pixel instead of one chain that may hold none.
 template <bool UNI>
-__device__ __forceinline__ void item_avx_pixel(const FrameParams &fp, const TileCtx &tc, const WaveSlots &ws, int s,
+__device__ __forceinline__ void item_avx_pixel(const FrameParams &fp, const TileCtx &tc, const ShadeSlots &ws, int s,
                                                int j, int32_t Row) {
     const int32_t xa = ws.i[SI_XA][s], LeftXa = ws.i[SI_LEFT][s];
     const uint32_t tag = (uint32_t)ws.i[SI_TAG][s];
@@ -404,8 +412,8 @@ __device__ __forceinline__ void item_avx_pixel(const FrameParams &fp, const Tile
 }
 
 // A whole DrawModel span (projekt.cpp:423-538) restricted to the tile.
-template <int M, bool SHADE, bool UNI>
-__device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx &tc, const WaveSlots &ws, int s,
+template <int M, bool SHADE, bool UNI, class WS>
+__device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx &tc, const WS &ws, int s,
                                             int32_t Row) {
     using TR = ModeTraits<M>;
     const int32_t W = fp.W;
@@ -426,7 +434,7 @@ __device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx
     const float IZ = ws.f[SS_IZ][s];
     float w = 0, u = 0, v = 0, IW = 0, IU = 0, IV = 0, n0 = 0, n1 = 0, n2 = 0, IN0 = 0, IN1 = 0, IN2 = 0;
     float c0 = 0, c1 = 0, c2 = 0, c3 = 0, IC0 = 0, IC1 = 0, IC2 = 0, IC3 = 0;
-    if (SHADE) {
+    if constexpr (SHADE) {
         if (TR::tex) {
             w = ws.f[SS_W][s]; u = ws.f[SS_U][s]; v = ws.f[SS_V][s];
             IW = ws.f[SS_IW][s]; IU = ws.f[SS_IU][s]; IV = ws.f[SS_IV][s];
@@ -516,7 +524,8 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 // One sweep over the tile's bin for mode M.  SHADE=false: visibility keys;
 // SHADE=true: shade the winners.
 template <int M, bool SHADE, bool UNI>
-__device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, WaveSlots &ws,
+__device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
+                                      std::conditional_t<SHADE, ShadeSlots, VisSlots> &ws,
                                       const uint32_t *__restrict__ bins, uint32_t b0, uint32_t n,
                                       const uint32_t *__restrict__ list, uint32_t *anomaly) {
     // Entries [0, n) of the tile's bin, or (list != nullptr) the n entries it names.
@@ -590,8 +599,8 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
                         if (ws.i[SI_PRE][mid] > it) hi = mid; else lo = mid + 1;
                     }
                     const int s = lo, j = it - (lo ? ws.i[SI_PRE][lo - 1] : 0);
-                    if (M == MODE_AVX && SHADE && PRK_PIXEL_ITEMS) item_avx_pixel<UNI>(fp, tc, ws, s, j, r);
-                    else if (M == MODE_AVX) item_avx<SHADE, UNI>(fp, tc, ws, s, j, r);
+                    if constexpr (M == MODE_AVX && SHADE && PRK_PIXEL_ITEMS) item_avx_pixel<UNI>(fp, tc, ws, s, j, r);
+                    else if constexpr (M == MODE_AVX) item_avx<SHADE, UNI>(fp, tc, ws, s, j, r);
                     else item_scalar<M, SHADE, UNI>(fp, tc, ws, s, r);
                 }
             }
@@ -601,14 +610,6 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
             if (!__any(active)) break;
         }
     }
-}
-
-template <int M, bool UNI>
-__device__ __forceinline__ void raster_mode(const FrameParams &fp, const TileCtx &tc, WaveSlots &ws,
-                                            const uint32_t *bins, uint32_t b0, uint32_t n, const uint32_t *list,
-                                            uint32_t *anomaly, bool shade) {
-    if (!shade) sweep<M, false, UNI>(fp, tc, ws, bins, b0, n, nullptr, anomaly);
-    else sweep<M, true, UNI>(fp, tc, ws, bins, b0, n, list, anomaly);
 }
 
 // Workgroup-wide exclusive scan of one value per thread.
@@ -627,19 +628,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *scratc
     return before + (uint32_t)incl - v;
 }
 
-// MODESET: a single Mode, or -1: any mode (per-draw dispatch).  UNI: the frame
-// is one draw (then MODESET is its mode).
-template <int MODESET, bool UNI>
-__global__ void __launch_bounds__(64 * kWaves, PRK_RASTER_MIN_WAVES) k_raster(FrameParams fp, const uint32_t *__restrict__ offs,
-                                                const uint32_t *__restrict__ bins, uint8_t *__restrict__ won,
-                                                uint32_t *__restrict__ list, uint32_t *__restrict__ anomaly) {
-    extern __shared__ unsigned long long lds[];
-    const int ntile = fp.tiles_x * fp.tiles_y;
-    const int t = blockIdx.x;
-    if (t >= ntile) return;
-    const uint32_t b0 = offs[t], b1 = offs[t + 1];
-    if (b0 == b1) return;  // no triangle touches this tile: leave it untouched
-    const uint32_t n = b1 - b0;
+__device__ __forceinline__ TileCtx tile_ctx(const FrameParams &fp, int t) {
     const int tx = t % fp.tiles_x, ty = t / fp.tiles_x;
     TileCtx tc;
     tc.tw = fp.tile_w;
@@ -647,10 +636,36 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_RASTER_MIN_WAVES) k_raster(Fr
     tc.x1 = min(fp.W, tc.x0 + fp.tile_w);
     tc.y0 = fp.row0 + ty * fp.tile_h;
     tc.y1 = min(fp.row1, tc.y0 + fp.tile_h);
+    tc.key = nullptr;
+    tc.tags = nullptr;
+    return tc;
+}
+
+// Visibility (sweep 1), one workgroup per tile.  MODESET: a single Mode, or
+// -1: any mode (a mixed frame sweeps the bin once per mode, each skipping the
+// other modes' entries).  UNI: the frame is one draw (then MODESET is its mode).
+// Output per tile: the winning entry tag of every pixel (wtag, tile-major),
+// the list of bin entries that won at least one pixel and its length.
+template <int MODESET, bool UNI>
+__global__ void __launch_bounds__(64 * kWaves, PRK_VIS_MIN_WAVES)
+    k_vis(FrameParams fp, const uint32_t *__restrict__ offs, const uint32_t *__restrict__ bins,
+          uint8_t *__restrict__ won, uint32_t *__restrict__ list, uint32_t *__restrict__ nwin_out,
+          uint32_t *__restrict__ wtag, uint32_t *__restrict__ anomaly) {
+    extern __shared__ unsigned long long lds[];
+    const int ntile = fp.tiles_x * fp.tiles_y;
+    const int t = blockIdx.x;
+    if (t >= ntile) return;
+    const uint32_t b0 = offs[t], b1 = offs[t + 1];
+    if (b0 == b1) {  // no triangle touches this tile: leave it untouched
+        if (threadIdx.x == 0) nwin_out[t] = 0;
+        return;
+    }
+    const uint32_t n = b1 - b0;
+    TileCtx tc = tile_ctx(fp, t);
     const int npx = fp.tile_w * fp.tile_h;
     tc.key = lds;
-    WaveSlots *slots = reinterpret_cast<WaveSlots *>(lds + npx);
-    WaveSlots &ws = slots[threadIdx.x >> 6];
+    VisSlots *slots = reinterpret_cast<VisSlots *>(lds + npx);
+    VisSlots &ws = slots[threadIdx.x >> 6];
     uint32_t *scratch = reinterpret_cast<uint32_t *>(slots + kWaves);
 
     // Prior z of the target: a fragment must beat it strictly.
@@ -665,23 +680,32 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_RASTER_MIN_WAVES) k_raster(Fr
         tc.key[p] = k;
     }
     __syncthreads();
-    // Sweep 1: visibility.
     if constexpr (MODESET >= 0) {
-        raster_mode<(MODESET >= 0 ? MODESET : 0), UNI>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
+        sweep<(MODESET >= 0 ? MODESET : 0), false, UNI>(fp, tc, ws, bins, b0, n, nullptr, anomaly);
     } else {
-        // Mixed frame: each mode sweeps the bin and skips other modes' entries.
-        raster_mode<MODE_AVX, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
-        raster_mode<MODE_SC_GOURAUD, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
-        raster_mode<MODE_SC_GOURAUD_TEX, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
-        raster_mode<MODE_SC_PHONG, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
-        raster_mode<MODE_SC_PHONG_TEX, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly, false);
+        sweep<MODE_AVX, false, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly);
+        sweep<MODE_SC_GOURAUD, false, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly);
+        sweep<MODE_SC_GOURAUD_TEX, false, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly);
+        sweep<MODE_SC_PHONG, false, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly);
+        sweep<MODE_SC_PHONG_TEX, false, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly);
     }
     __syncthreads();
-    if (PRK_DIAG & 1) return;
-    // Which bin entries won at least one pixel of this tile?
+    // Winner tags out, and which bin entries won at least one pixel.
+    uint32_t *tags_out = wtag + (size_t)t * npx;
     for (int p = threadIdx.x; p < npx; p += blockDim.x) {
         const uint32_t low = (uint32_t)tc.key[p];
+        tags_out[p] = low;
         if (low != 0xFFFFFFFFu) won[b0 + (0xFFFFFFFEu - low)] = 1;
+    }
+    // Debug builds also export the winning triangle map.
+    if (fp.winners) {
+        for (int p = threadIdx.x; p < npx; p += blockDim.x) {
+            const int x = tc.x0 + p % fp.tile_w, y = tc.y0 + p / fp.tile_w;
+            if (x >= tc.x1 || y >= tc.y1) continue;
+            const uint32_t low = (uint32_t)tc.key[p];
+            fp.winners[(size_t)(y - fp.row0) * fp.W + x] =
+                low != 0xFFFFFFFFu ? (int32_t)bins[b0 + (0xFFFFFFFEu - low)] : -1;
+        }
     }
     __threadfence_block();
     __syncthreads();
@@ -694,41 +718,60 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_RASTER_MIN_WAVES) k_raster(Fr
         if (f) list[b0 + nwin + pos] = i;
         nwin += tot;
     }
-    __threadfence_block();
+    if (threadIdx.x == 0) nwin_out[t] = (PRK_DIAG & 1) ? 0u : nwin;
+}
+
+// Shading (sweep 2), one workgroup per tile: re-walk only the entries that
+// won a pixel and shade exactly the winning fragments.  Winners store their
+// z and colour; untouched pixels keep the prior contents.
+template <int MODESET, bool UNI>
+__global__ void __launch_bounds__(64 * kWaves, PRK_SHADE_MIN_WAVES)
+    k_shade(FrameParams fp, const uint32_t *__restrict__ offs, const uint32_t *__restrict__ bins,
+            const uint32_t *__restrict__ list, const uint32_t *__restrict__ nwin_in,
+            const uint32_t *__restrict__ wtag, uint32_t *__restrict__ anomaly) {
+    extern __shared__ unsigned long long lds[];
+    const int ntile = fp.tiles_x * fp.tiles_y;
+    const int t = blockIdx.x;
+    if (t >= ntile) return;
+    const uint32_t nwin = nwin_in[t];
+    if (nwin == 0) return;
+    const uint32_t b0 = offs[t];
+    TileCtx tc = tile_ctx(fp, t);
+    const int npx = fp.tile_w * fp.tile_h;
+    uint32_t *tags = reinterpret_cast<uint32_t *>(lds);
+    tc.tags = tags;
+    ShadeSlots *slots = reinterpret_cast<ShadeSlots *>(tags + ((npx + 1) & ~1));
+    ShadeSlots &ws = slots[threadIdx.x >> 6];
+    const uint32_t *tags_in = wtag + (size_t)t * npx;
+    for (int p = threadIdx.x; p < npx; p += blockDim.x) tags[p] = tags_in[p];
     __syncthreads();
-    // Sweep 2: shade the winners.
     if constexpr (MODESET >= 0) {
-        raster_mode<(MODESET >= 0 ? MODESET : 0), UNI>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
+        sweep<(MODESET >= 0 ? MODESET : 0), true, UNI>(fp, tc, ws, bins, b0, nwin, list, anomaly);
     } else {
-        raster_mode<MODE_AVX, false>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
-        raster_mode<MODE_SC_GOURAUD, false>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
-        raster_mode<MODE_SC_GOURAUD_TEX, false>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
-        raster_mode<MODE_SC_PHONG, false>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
-        raster_mode<MODE_SC_PHONG_TEX, false>(fp, tc, ws, bins, b0, nwin, list, anomaly, true);
-    }
-    __syncthreads();
-    // Winners wrote their z and colour in sweep 2; untouched pixels keep the
-    // prior contents.  Debug builds also export the winning triangle map.
-    if (fp.winners) {
-        for (int p = threadIdx.x; p < npx; p += blockDim.x) {
-            const int x = tc.x0 + p % fp.tile_w, y = tc.y0 + p / fp.tile_w;
-            if (x >= tc.x1 || y >= tc.y1) continue;
-            const uint32_t low = (uint32_t)tc.key[p];
-            fp.winners[(size_t)(y - fp.row0) * fp.W + x] =
-                low != 0xFFFFFFFFu ? (int32_t)bins[b0 + (0xFFFFFFFEu - low)] : -1;
-        }
+        sweep<MODE_AVX, true, false>(fp, tc, ws, bins, b0, nwin, list, anomaly);
+        sweep<MODE_SC_GOURAUD, true, false>(fp, tc, ws, bins, b0, nwin, list, anomaly);
+        sweep<MODE_SC_GOURAUD_TEX, true, false>(fp, tc, ws, bins, b0, nwin, list, anomaly);
+        sweep<MODE_SC_PHONG, true, false>(fp, tc, ws, bins, b0, nwin, list, anomaly);
+        sweep<MODE_SC_PHONG_TEX, true, false>(fp, tc, ws, bins, b0, nwin, list, anomaly);
     }
 }
 
 // Explicit instantiations used by the host.
-#define PRK_RASTER_ARGS FrameParams, const uint32_t *, const uint32_t *, uint8_t *, uint32_t *, uint32_t *
-template __global__ void k_raster<-1, false>(PRK_RASTER_ARGS);
-template __global__ void k_raster<MODE_AVX, false>(PRK_RASTER_ARGS);
-template __global__ void k_raster<MODE_AVX, true>(PRK_RASTER_ARGS);
-template __global__ void k_raster<MODE_SC_GOURAUD, false>(PRK_RASTER_ARGS);
-template __global__ void k_raster<MODE_SC_GOURAUD, true>(PRK_RASTER_ARGS);
-template __global__ void k_raster<MODE_SC_PHONG, false>(PRK_RASTER_ARGS);
-template __global__ void k_raster<MODE_SC_PHONG, true>(PRK_RASTER_ARGS);
+#define PRK_VIS_ARGS FrameParams, const uint32_t *, const uint32_t *, uint8_t *, uint32_t *, uint32_t *, uint32_t *, \
+                     uint32_t *
+#define PRK_SHADE_ARGS FrameParams, const uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *, \
+                       const uint32_t *, uint32_t *
+#define PRK_INST(MS, UNI)                                  \
+    template __global__ void k_vis<MS, UNI>(PRK_VIS_ARGS); \
+    template __global__ void k_shade<MS, UNI>(PRK_SHADE_ARGS);
+PRK_INST(-1, false)
+PRK_INST(MODE_AVX, false)
+PRK_INST(MODE_AVX, true)
+PRK_INST(MODE_SC_GOURAUD, false)
+PRK_INST(MODE_SC_GOURAUD, true)
+PRK_INST(MODE_SC_PHONG, false)
+PRK_INST(MODE_SC_PHONG, true)
+#undef PRK_INST
 
 }  // namespace prk
 
@@ -745,16 +788,33 @@ hipError_t prk_launch_tri_draw(const prk::DrawRec *draws, uint32_t ndraws, uint3
     return hipGetLastError();
 }
 
-hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint32_t *offs,
-                             const uint32_t *bins, uint8_t *won, uint32_t *list, uint32_t *anomaly, hipStream_t s) {
+// Bytes of dynamic LDS per workgroup of k_vis / k_shade.
+static size_t vis_lds(const prk::FrameParams *fp) {
+    return (size_t)fp->tile_w * fp->tile_h * sizeof(unsigned long long) + prk::kWaves * sizeof(prk::VisSlots) +
+           16 * sizeof(uint32_t);
+}
+static size_t shade_lds(const prk::FrameParams *fp) {
+    const size_t npx = (size_t)fp->tile_w * fp->tile_h;
+    return ((npx + 1) & ~(size_t)1) * sizeof(uint32_t) + prk::kWaves * sizeof(prk::ShadeSlots);
+}
+
+// Sweep 1 (k_vis) then sweep 2 (k_shade) on stream s; `mid` (optional) is
+// recorded between them.
+hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint32_t *offs, const uint32_t *bins,
+                             uint8_t *won, uint32_t *list, uint32_t *nwin, uint32_t *wtag, uint32_t *anomaly,
+                             hipEvent_t mid, hipStream_t s) {
     const uint32_t ntile = (uint32_t)(fp->tiles_x * fp->tiles_y);
     if (ntile == 0) return hipSuccess;
-    const size_t lds = (size_t)fp->tile_w * fp->tile_h * sizeof(unsigned long long) +
-                       prk::kWaves * sizeof(prk::WaveSlots) + 16 * sizeof(uint32_t);
-#define PRK_LAUNCH(MS, UNI) \
-    hipLaunchKernelGGL((prk::k_raster<MS, UNI>), dim3(ntile), dim3(64 * prk::kWaves), lds, s, *fp, offs, bins, won, \
-                       list, anomaly)
+    const size_t lv = vis_lds(fp), ls = shade_lds(fp);
     const bool uni = fp->ndraws == 1;
+#define PRK_LAUNCH(MS, UNI)                                                                                          \
+    do {                                                                                                             \
+        hipLaunchKernelGGL((prk::k_vis<MS, UNI>), dim3(ntile), dim3(64 * prk::kWaves), lv, s, *fp, offs, bins, won, \
+                           list, nwin, wtag, anomaly);                                                               \
+        if (mid) (void)hipEventRecord(mid, s);                                                                       \
+        hipLaunchKernelGGL((prk::k_shade<MS, UNI>), dim3(ntile), dim3(64 * prk::kWaves), ls, s, *fp, offs, bins,    \
+                           list, nwin, wtag, anomaly);                                                               \
+    } while (0)
     switch (modeset) {
         case prk::MODE_AVX: if (uni) PRK_LAUNCH(prk::MODE_AVX, true); else PRK_LAUNCH(prk::MODE_AVX, false); break;
         case prk::MODE_SC_GOURAUD:

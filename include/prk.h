@@ -93,7 +93,7 @@ typedef struct prk_stats {
     uint32_t tiles;          /* tiles in the render target band        */
     uint32_t frames_timed;   /* flushes accumulated in sum_ms_*        */
     float ms_bin;            /* last flush: project/cull/bin kernels   */
-    float ms_raster;         /* last flush: tile raster+shade kernel   */
+    float ms_raster;         /* last flush: k_vis + k_shade            */
     double sum_ms_bin;       /* accumulated since prk_timing_reset     */
     double sum_ms_raster;
     uint32_t anomalies;      /* triangles whose AET left the proven
@@ -102,6 +102,8 @@ typedef struct prk_stats {
                                 replayed row by row (irregular edge list or
                                 an X tie); cumulative like
                                 anomalies */
+    double sum_ms_vis;       /* accumulated: the k_vis (visibility) part
+                                of sum_ms_raster */
 } prk_stats;
 
 typedef struct prk_context prk_context;
