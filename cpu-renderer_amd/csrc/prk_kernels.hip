@@ -77,8 +77,8 @@ __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
 #endif
 constexpr int kWaves = PRK_WAVES;
 constexpr int kSpanF = 22;  // float fields per span slot
-constexpr int kSpanI = 7;   // int fields per span slot (the row is the sweep's current row)
-enum { SI_XA = 0, SI_XB, SI_LEFT, SI_PRE, SI_TAG, SI_OVF, SI_TEX };
+constexpr int kSpanI = 8;   // int fields per span slot (the row is the sweep's current row)
+enum { SI_XA = 0, SI_XB, SI_LEFT, SI_PRE, SI_TAG, SI_OVF, SI_TEX, SI_MARK };
 // AVX float slots
 enum { SF_XOFF = 0, SF_LW, SF_LU, SF_LV, SF_LZ, SF_IW, SF_IU, SF_IV, SF_IZ, SF_LN0, SF_LN1, SF_LN2,
        SF_IN0, SF_IN1, SF_IN2 };
@@ -512,12 +512,25 @@ __device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx
     }
 }
 
+// Wave64 inclusive prefix sum / max in registers (DPP row shifts + row
+// broadcasts: no LDS round trips).
 __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int t = __shfl_up(v, d, 64);
-        if (lane >= d) v += t;
-    }
+    (void)lane;
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false); // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false); // row_bcast:31
+    return v;
+}
+__device__ __forceinline__ int wave_incl_max(int v) {  // v >= 0
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));
     return v;
 }
 
@@ -585,20 +598,28 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
                 active = wk.Row < wk.MaxY;
             }
             const int incl = wave_incl_scan(items, lane);
-            const int total = __shfl(incl, 63, 64);
-            ws.i[SI_PRE][lane] = incl;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const int total = __builtin_amdgcn_readlane(incl, 63);
+            const int excl = incl - items;
+            ws.i[SI_PRE][lane] = excl;
+            // Item -> span: the span lanes starting an item inside the window
+            // mark their start position; a prefix max over the window (plus
+            // the span carried over from the previous window) names the span
+            // of every item.
+            int carry = 0;
             for (int it0 = 0; it0 < (((PRK_DIAG & 2) || ((PRK_DIAG & 8) && SHADE)) ? 0 : total); it0 += 64) {
+                ws.i[SI_MARK][lane] = 0;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (items > 0 && excl >= it0 && excl < it0 + 64) ws.i[SI_MARK][excl - it0] = lane + 1;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const int m = max(wave_incl_max(ws.i[SI_MARK][lane]), carry);
+                carry = __builtin_amdgcn_readlane(m, 63);
                 const int it = it0 + lane;
                 if (it < total) {
-                    int lo = 0, hi = 63;  // first slot whose inclusive prefix exceeds it
-                    while (lo < hi) {
-                        const int mid = (lo + hi) >> 1;
-                        if (ws.i[SI_PRE][mid] > it) hi = mid; else lo = mid + 1;
-                    }
-                    const int s = lo, j = it - (lo ? ws.i[SI_PRE][lo - 1] : 0);
+                    const int s = m - 1, j = it - ws.i[SI_PRE][s];
                     if constexpr (M == MODE_AVX && SHADE && PRK_PIXEL_ITEMS) item_avx_pixel<UNI>(fp, tc, ws, s, j, r);
                     else if constexpr (M == MODE_AVX) item_avx<SHADE, UNI>(fp, tc, ws, s, j, r);
                     else item_scalar<M, SHADE, UNI>(fp, tc, ws, s, r);
