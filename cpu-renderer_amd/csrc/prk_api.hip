@@ -409,7 +409,8 @@ int prk_reset_draws(prk_context *c) {
 }
 
 int prk_set_tile(prk_context *c, int32_t tw, int32_t th) {
-    if (!c || tw <= 0 || th <= 0 || (tw % 8) || tw * th > 8192 || tw * th < 64) return PRK_ERR_ARG;
+    // tile_w: a power of two >= 8 (pixel index <-> (x, y) by shifts)
+    if (!c || tw < 8 || th <= 0 || (tw & (tw - 1)) || tw * th > 8192 || tw * th < 64) return PRK_ERR_ARG;
     c->tile_w = tw;
     c->tile_h = th;
     return PRK_OK;
@@ -494,6 +495,8 @@ int prk_flush(prk_context *c, void *stream) {
     fp.zbuf = c->zbuf;
     fp.tile_w = c->tile_w;
     fp.tile_h = c->tile_h;
+    fp.tile_w_log2 = 0;
+    while ((1 << fp.tile_w_log2) < c->tile_w) ++fp.tile_w_log2;
     fp.tiles_x = (c->W + c->tile_w - 1) / c->tile_w;
     fp.tiles_y = (c->row1 - c->row0 + c->tile_h - 1) / c->tile_h;
     fp.tri_count = T;

@@ -61,6 +61,7 @@ struct FrameParams {
     int32_t *winners;// optional (debug): per pixel winning triangle, -1 none
     // tiling
     int32_t tile_w, tile_h, tiles_x, tiles_y;
+    int32_t tile_w_log2;  // tile_w is a power of two
     // geometry
     uint32_t tri_count;
     uint32_t ndraws;

@@ -77,8 +77,8 @@ __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
 #endif
 constexpr int kWaves = PRK_WAVES;
 constexpr int kSpanF = 22;  // float fields per span slot
-constexpr int kSpanI = 8;   // int fields per span slot (the row is the sweep's current row)
-enum { SI_XA = 0, SI_XB, SI_LEFT, SI_PRE, SI_TAG, SI_OVF, SI_TEX, SI_MARK };
+constexpr int kSpanI = 10;  // int fields per span slot (the row is the sweep's current row)
+enum { SI_XA = 0, SI_XB, SI_LEFT, SI_PRE, SI_TAG, SI_OVF, SI_TEX, SI_MARK, SI_WM0, SI_WM1 };
 // AVX float slots
 enum { SF_XOFF = 0, SF_LW, SF_LU, SF_LV, SF_LZ, SF_IW, SF_IU, SF_IV, SF_IZ, SF_LN0, SF_LN1, SF_LN2,
        SF_IN0, SF_IN1, SF_IN2 };
@@ -109,10 +109,9 @@ __device__ __forceinline__ bool is_winner(const TileCtx &tc, int p, uint32_t tag
     return tc.tags[p] == tag;
 }
 
-// The winning fragment of tile pixel p: store its z and colour (each pixel
+// The winning fragment of pixel (x, y): store its z and colour (each pixel
 // has exactly one winner, so these plain stores never race).
-__device__ __forceinline__ void put_winner(const FrameParams &fp, const TileCtx &tc, int p, float z, uint32_t col) {
-    const int32_t x = tc.x0 + p % tc.tw, y = tc.y0 + p / tc.tw;
+__device__ __forceinline__ void put_winner(const FrameParams &fp, int32_t x, int32_t y, float z, uint32_t col) {
     const size_t row = (size_t)(y - fp.row0);
     fp.zbuf[row * fp.W + x] = z;
     reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(fp.color) + row * fp.pitch)[x] = col;
@@ -171,10 +170,18 @@ __device__ __forceinline__ int span_setup_avx(const FrameParams &fp, const TileC
         ws.f[SF_LN0][lane] = L.N0; ws.f[SF_LN1][lane] = L.N1; ws.f[SF_LN2][lane] = L.N2;
         ws.f[SF_IN0][lane] = IN0; ws.f[SF_IN1][lane] = IN1; ws.f[SF_IN2][lane] = IN2;
 #if PRK_PIXEL_ITEMS
-        // Shading sweep: one item per pixel this span won.
+        // Shading sweep: one item per pixel this span won; the won pixels of
+        // the span's first 64 columns as a bit mask.
         const int rowoff = (Row - tc.y0) * tc.tw - tc.x0;
         int won = 0;
-        for (int32_t x = xa; x < xb; ++x) won += is_winner(tc, rowoff + x, tag) ? 1 : 0;
+        uint64_t wm = 0;
+        for (int32_t x = xa; x < xb; ++x) {
+            const bool w = is_winner(tc, rowoff + x, tag);
+            won += w ? 1 : 0;
+            if (w && x - xa < 64) wm |= 1ull << (x - xa);
+        }
+        ws.i[SI_WM0][lane] = (int32_t)(uint32_t)wm;
+        ws.i[SI_WM1][lane] = (int32_t)(uint32_t)(wm >> 32);
         return won;
 #endif
     }
@@ -259,13 +266,16 @@ __device__ __forceinline__ int span_setup_scalar(const FrameParams &fp, const Ti
 
 // ----- work items ----------------------------------------------------------
 // Phong + texel of one FillLineOptimized lane (projekt.cpp:1865-2200).
-__device__ __forceinline__ uint32_t shade_avx(const FrameParams &fp, const TexRec &tex, float fu, float fv,
-                                              float z, float n0, float n1, float n2, int32_t x, int32_t i,
-                                              int32_t Row) {
-    // Texel (1881-2032): trunc, <<2, 16-bit pitch multiply, P2 clamp.
+// Texel of one FillLineOptimized lane (1881-2032): trunc, <<2, 16-bit pitch
+// multiply, P2 clamp.
+__device__ __forceinline__ uint32_t texel_avx(const TexRec &tex, float fu, float fv) {
     const int32_t FX = (int32_t)((uint32_t)cvtt_s32((float)tex.w * fu) << 2);
     const int32_t FY = mul16_trick(cvtt_s32((float)tex.h * fv), tex.pitch);
-    const uint32_t t = texel_at(tex, (int32_t)((uint32_t)FX + (uint32_t)FY));
+    return texel_at(tex, (int32_t)((uint32_t)FX + (uint32_t)FY));
+}
+
+__device__ __forceinline__ uint32_t shade_avx_texel(const FrameParams &fp, uint32_t t, float z, float n0, float n1,
+                                                    float n2, int32_t x, int32_t i, int32_t Row) {
     const float CA = u8_unit((t >> 24) & 0xFF), CR = u8_unit((t >> 16) & 0xFF);
     const float CG = u8_unit((t >> 8) & 0xFF), CB = u8_unit(t & 0xFF);
     // Phong (2040-2128) at UnprojectVertex_8x (102-145).
@@ -301,6 +311,12 @@ __device__ __forceinline__ uint32_t shade_avx(const FrameParams &fp, const TexRe
     Fa = maxps(minps(Fa, 1.0f), 0.0f);
     return ((uint32_t)cvt_rne_s32(Fr * 255.0f) << 16) | ((uint32_t)cvt_rne_s32(Fg * 255.0f) << 8) |
            ((uint32_t)cvt_rne_s32(Fb * 255.0f)) | ((uint32_t)cvt_rne_s32(Fa * 255.0f) << 24);
+}
+
+__device__ __forceinline__ uint32_t shade_avx(const FrameParams &fp, const TexRec &tex, float fu, float fv,
+                                              float z, float n0, float n1, float n2, int32_t x, int32_t i,
+                                              int32_t Row) {
+    return shade_avx_texel(fp, texel_avx(tex, fu, fv), z, n0, n1, n2, x, i, Row);
 }
 
 // Item j of an AVX span: lane chain i = (xa + j - LeftXa) & 7 from block b.
@@ -356,7 +372,7 @@ __device__ __forceinline__ void item_avx(const FrameParams &fp, const TileCtx &t
             if (is_winner(tc, p, tag)) {
                 const float iw = 1.0f / w;  // 1865-1866
                 const float fu = iw * u, fv = iw * v;
-                put_winner(fp, tc, p, z, (PRK_DIAG & 16) ? __float_as_uint(fu + fv + n0 + n1 + n2)
+                put_winner(fp, x, Row, z, (PRK_DIAG & 16) ? __float_as_uint(fu + fv + n0 + n1 + n2)
                                                          : shade_avx(fp, tex, fu, fv, z, n0, n1, n2, x, i, Row));
             }
             if (x + 8 < xb) {
@@ -378,37 +394,48 @@ __device__ __forceinline__ void item_avx_pixel(const FrameParams &fp, const Tile
                                                int j, int32_t Row) {
     const int32_t xa = ws.i[SI_XA][s], LeftXa = ws.i[SI_LEFT][s];
     const uint32_t tag = (uint32_t)ws.i[SI_TAG][s];
-    const int rowoff = (Row - tc.y0) * tc.tw - tc.x0;
     int32_t x = xa;
-    for (int k = j;; ++x) {
-        if (is_winner(tc, rowoff + x, tag)) {
-            if (k == 0) break;
-            --k;
+    uint64_t wm = (uint64_t)(uint32_t)ws.i[SI_WM0][s] | ((uint64_t)(uint32_t)ws.i[SI_WM1][s] << 32);
+    int k = j;
+    for (; k > 0 && wm; --k) wm &= wm - 1;  // drop the j lowest won columns
+    if (wm) {
+        x += (int32_t)__builtin_ctzll(wm);
+    } else {  // past the span's first 64 columns
+        const int rowoff = (Row - tc.y0) * tc.tw - tc.x0;
+        for (x = xa + 64;; ++x) {
+            if (is_winner(tc, rowoff + x, tag)) {
+                if (k == 0) break;
+                --k;
+            }
         }
     }
     const TexRec tex = UNI ? fp.tex0 : fp.texs[ws.i[SI_TEX][s]];
     const int32_t rel = x - LeftXa, i = rel & 7, b = rel >> 3;
     const float IW = ws.f[SF_IW][s], IU = ws.f[SF_IU][s], IV = ws.f[SF_IV][s], IZ = ws.f[SF_IZ][s];
-    const float IN0 = ws.f[SF_IN0][s], IN1 = ws.f[SF_IN1][s], IN2 = ws.f[SF_IN2][s];
     const float o = ws.f[SF_XOFF][s] + (float)i;  // lane init (XOffset + i)*inc, 1712-1835
     float w = ws.f[SF_LW][s] + o * IW, u = ws.f[SF_LU][s] + o * IU;
     float v = ws.f[SF_LV][s] + o * IV, z = ws.f[SF_LZ][s] + o * IZ;
+    {
+        const float IW8 = IW * 8.0f, IU8 = IU * 8.0f, IV8 = IV * 8.0f, IZ8 = 8.0f * IZ;
+        for (int32_t k = 0; k < b; ++k) { z = z + IZ8; w = w + IW8; u = u + IU8; v = v + IV8; }  // 2262-2282
+    }
+    const float iw = 1.0f / w;  // 1865-1866
+    const float fu = iw * u, fv = iw * v;
+    // The texel load goes out before the normal's block steps.
+    const uint32_t t = texel_avx(tex, fu, fv);
+    const float IN0 = ws.f[SF_IN0][s], IN1 = ws.f[SF_IN1][s], IN2 = ws.f[SF_IN2][s];
     float n0 = ws.f[SF_LN0][s] + o * IN0, n1 = ws.f[SF_LN1][s] + o * IN1, n2 = ws.f[SF_LN2][s] + o * IN2;
     normalize_div(n0, n1, n2);  // 1754
-    if (b > 0) {
-        const float IW8 = IW * 8.0f, IU8 = IU * 8.0f, IV8 = IV * 8.0f, IZ8 = 8.0f * IZ;
+    {
         const float IN08 = IN0 * 8.0f, IN18 = IN1 * 8.0f, IN28 = IN2 * 8.0f;
         for (int32_t k = 0; k < b; ++k) {  // block steps 2262-2282
             float a = n0 + IN08, bb = n1 + IN18, c = n2 + IN28;
             normalize_div(a, bb, c);
             n0 = a; n1 = bb; n2 = c;
-            z = z + IZ8; w = w + IW8; u = u + IU8; v = v + IV8;
         }
     }
-    const float iw = 1.0f / w;  // 1865-1866
-    const float fu = iw * u, fv = iw * v;
-    put_winner(fp, tc, rowoff + x, z, (PRK_DIAG & 16) ? __float_as_uint(fu + fv + n0 + n1 + n2)
-                                                        : shade_avx(fp, tex, fu, fv, z, n0, n1, n2, x, i, Row));
+    put_winner(fp, x, Row, z, (PRK_DIAG & 16) ? __float_as_uint(fu + fv + n0 + n1 + n2) + t
+                                               : shade_avx_texel(fp, t, z, n0, n1, n2, x, i, Row));
 }
 
 // A whole DrawModel span (projekt.cpp:423-538) restricted to the tile.
@@ -496,7 +523,8 @@ __device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx
                 }
                 const uint32_t packed = (round_u32(F[3] * 255.0f) << 24) | (round_u32(F[0] * 255.0f) << 16) |
                                         (round_u32(F[1] * 255.0f) << 8) | (round_u32(F[2] * 255.0f));
-                put_winner(fp, tc, p, z, packed);
+                if (x == W) put_winner(fp, 0, Row + 1, z, packed);  // DrawModel's one-past-the-row store
+                else put_winner(fp, x, Row, z, packed);
             }
         }
         if (SHADE) {  // per-pixel step (504-510 / 530-535)
@@ -691,7 +719,7 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_VIS_MIN_WAVES)
 
     // Prior z of the target: a fragment must beat it strictly.
     for (int p = threadIdx.x; p < npx; p += blockDim.x) {
-        const int lx = p % fp.tile_w, ly = p / fp.tile_w;
+        const int lx = p & (fp.tile_w - 1), ly = p >> fp.tile_w_log2;
         const int x = tc.x0 + lx, y = tc.y0 + ly;
         unsigned long long k = ~0ull;
         if (x < tc.x1 && y < tc.y1) {
@@ -721,7 +749,7 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_VIS_MIN_WAVES)
     // Debug builds also export the winning triangle map.
     if (fp.winners) {
         for (int p = threadIdx.x; p < npx; p += blockDim.x) {
-            const int x = tc.x0 + p % fp.tile_w, y = tc.y0 + p / fp.tile_w;
+            const int x = tc.x0 + (p & (fp.tile_w - 1)), y = tc.y0 + (p >> fp.tile_w_log2);
             if (x >= tc.x1 || y >= tc.y1) continue;
             const uint32_t low = (uint32_t)tc.key[p];
             fp.winners[(size_t)(y - fp.row0) * fp.W + x] =

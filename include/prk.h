@@ -177,7 +177,8 @@ int prk_timing_reset(prk_context *ctx);
 int prk_set_debug(prk_context *ctx, int32_t enable);
 int prk_download_winners(prk_context *ctx, int32_t *winners_host);
 
-/* Tunables (testing / benchmarking). tile_w must be a multiple of 8. */
+/* Tunables (testing / benchmarking). tile_w must be a power of two >= 8,
+ * 64 <= tile_w * tile_h <= 8192. */
 int prk_set_tile(prk_context *ctx, int32_t tile_w, int32_t tile_h);
 
 /* Host utility: the reference's test mesh, ConstructSphere
