@@ -622,4 +622,71 @@ struct Walker {
     }
 };
 
+// The same active edge table with the list held physically: S0, S1, S2 are
+// list slots 0..2 (a pending third edge waits in S2).  The emitted pair is
+// always (S0, S1), so the per-row edge step touches two edges and needs no
+// selects; edges move only on the rare rows of an insertion, an expiry or a
+// crossing swap.  Built from a Walker after its setup / fast replay.
+template <int M, bool NRM>
+struct RowWalker {
+    Edge S0, S1, S2;
+    int cnt;
+    bool pend;
+    int32_t MaxY, Row;
+
+    __device__ __forceinline__ void from(const Walker<M, NRM> &w) {
+        S0 = w.get(w.slot(0));
+        S1 = w.get(w.slot(1));
+        S2 = w.pend >= 0 ? w.E2 : w.get(w.slot(2));
+        cnt = w.cnt;
+        pend = w.pend >= 0;
+        MaxY = w.MaxY;
+        Row = w.Row;
+    }
+
+    // Insertion + expiry of this->Row; true when the pair (S0, S1) is emitted.
+    // (Edges move by value selects: a conditional struct copy would become a
+    // pointer select and push the walker to scratch memory.)
+    __device__ __forceinline__ bool begin_row() {
+        if (pend && S2.YMin == Row) {  // insertion (3654-3713)
+            const bool b0 = cnt > 0 && insert_before(S2, S0);
+            const bool b1 = cnt > 1 && insert_before(S2, S1);
+            // b0: [S2 S0 S1]  b1: [S0 S2 S1]  else: S2 appended at slot cnt
+            const Edge n0 = sel(b0 || cnt == 0, S2, S0);
+            const Edge n1 = sel(b0, S0, sel(b1 || cnt == 1, S2, S1));
+            const Edge n2 = sel(b0 || b1, S1, S2);
+            S0 = n0; S1 = n1; S2 = n2;
+            ++cnt;
+            pend = false;
+        }
+        // Expiry (3715-3749): drop every entry with YMax <= Row, keep order.
+        // (While an edge is pending cnt <= 2, so S2 is never read as a slot.)
+        const bool k0 = cnt > 0 && !(S0.YMax <= Row);
+        const bool k1 = cnt > 1 && !(S1.YMax <= Row);
+        const bool k2 = cnt > 2 && !(S2.YMax <= Row);
+        if ((!k0 && (k1 || k2)) || (!k1 && k2)) {  // a kept entry moves down
+            const Edge n0 = sel(k0, S0, sel(k1, S1, S2));
+            const Edge n1 = sel(k0 && k1, S1, S2);
+            S0 = n0; S1 = n1;
+        }
+        cnt = (int)k0 + (int)k1 + (int)k2;
+        // Pairing (3751-3869): one pair; a third entry stays unpaired.
+        return cnt >= 2;
+    }
+
+    // Edge step of the pair (3811-3829) and the crossing swap (3831-3841 + P3).
+    __device__ __forceinline__ void end_row(bool paired) {
+        if (paired) {
+            step_edge<M, NRM>(S0);
+            step_edge<M, NRM>(S1);
+            const bool sw = S0.X > S1.X;
+            if (sw) {
+                const Edge a = sel(sw, S1, S0), b = sel(sw, S0, S1);
+                S0 = a; S1 = b;
+            }
+        }
+        ++Row;
+    }
+};
+
 }  // namespace prk

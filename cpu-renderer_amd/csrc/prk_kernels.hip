@@ -578,7 +578,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
         bool active = i < n;
         uint32_t e = 0;
         int32_t texi = 0;
-        Walker<M, SHADE> wk;
+        RowWalker<M, SHADE> wk;
         uint32_t anom = 0;
         if (active) {
             e = list ? list[b0 + i] : i;
@@ -599,10 +599,12 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
             }
             active = ne >= 2;
             if (active) {
-                wk.init(ne, s0, s1, s2, fp.H, tc.y1, anom);
+                Walker<M, SHADE> w0;
+                w0.init(ne, s0, s1, s2, fp.H, tc.y1, anom);
                 // Replay the rows above the tile (edge DDA only); row by row
                 // only for irregular edge lists.
-                const int fr = wk.fast_replay(ystart, ne);
+                const int fr = w0.fast_replay(ystart, ne);
+                wk.from(w0);
                 if (fr < 0)
                     while (wk.Row < ystart && wk.Row < wk.MaxY) wk.end_row(wk.begin_row());
                 if (fr != 0 && !SHADE) atomicAdd(anomaly + 1, 1u);
@@ -618,7 +620,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
             if (active && wk.Row == r) {
                 const bool paired = wk.begin_row();
                 if (paired) {
-                    const Edge L = wk.get(wk.slot(0)), R = wk.get(wk.slot(1));
+                    const Edge &L = wk.S0, &R = wk.S1;
                     if (M == MODE_AVX) items = span_setup_avx<SHADE>(fp, tc, ws, lane, tag, texi, L, R, r);
                     else items = span_setup_scalar<M, SHADE>(fp, tc, ws, lane, tag, texi, L, R, r);
                 }
