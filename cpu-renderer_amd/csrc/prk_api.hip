@@ -89,7 +89,7 @@ struct prk_context {
     uint32_t pending_tris = 0;
     // scratch
     DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_tri_n, d_tri_off, d_keys_a, d_vals_a, d_keys_b, d_bins,
-        d_offs, d_won, d_list, d_temp, d_winners, d_anomaly, d_nwin, d_wtag;
+        d_offs, d_won, d_list, d_temp, d_winners, d_anomaly, d_nwin, d_wtag, d_prof;
     uint32_t *h_total = nullptr;  // pinned
     int32_t tile_w = 256, tile_h = 8;  // measured best for C3b
     bool debug = false;
@@ -162,7 +162,7 @@ int prk_destroy(prk_context *c) {
     }
     DevBuf *bufs[] = {&c->d_draws,  &c->d_texs,   &c->d_tri_draw, &c->d_ranges, &c->d_tri_n, &c->d_tri_off,
                       &c->d_keys_a, &c->d_vals_a, &c->d_keys_b,   &c->d_bins,   &c->d_offs,  &c->d_won,
-                      &c->d_list,   &c->d_temp,   &c->d_winners,  &c->d_anomaly, &c->d_nwin, &c->d_wtag};
+                      &c->d_list,   &c->d_temp,   &c->d_winners,  &c->d_anomaly, &c->d_nwin, &c->d_wtag, &c->d_prof};
     for (DevBuf *b : bufs) b->release();
     if (c->h_total) (void)hipHostFree(c->h_total);
     for (auto &slot : c->ev)
@@ -446,6 +446,16 @@ int prk_timing_reset(prk_context *c) {
     for (int i = 0; i < prk_context::kRing; ++i) c->pending[i] = false;
     c->stats.frames_timed = 0;
     c->stats.sum_ms_bin = c->stats.sum_ms_raster = c->stats.sum_ms_vis = 0.0;
+    if (c->d_prof.p) PRK_TRY(hipMemset(c->d_prof.p, 0, 16 * sizeof(uint64_t)));
+    return PRK_OK;
+}
+
+int prk_debug_counters(prk_context *c, uint64_t *out, int32_t n) {
+    if (!c || !out || n < 0 || n > 16) return PRK_ERR_ARG;
+    PRK_TRY(hipSetDevice(c->device));
+    PRK_TRY(hipDeviceSynchronize());
+    for (int i = 0; i < n; ++i) out[i] = 0;
+    if (c->d_prof.p && n) PRK_TRY(hipMemcpy(out, c->d_prof.p, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return PRK_OK;
 }
 
@@ -509,6 +519,11 @@ int prk_flush(prk_context *c, void *stream) {
     c->stats.bin_entries = 0;
     const int slot = (int)(c->frame % prk_context::kRing);
     harvest(c, slot);  // a flush kRing frames old: long finished
+    if (!c->d_prof.p) {
+        PRK_TRY(c->d_prof.ensure(16 * sizeof(uint64_t)));
+        PRK_TRY(hipMemsetAsync(c->d_prof.p, 0, 16 * sizeof(uint64_t), s));
+    }
+    fp.prof = (unsigned long long *)c->d_prof.p;
     if (c->debug) {
         PRK_TRY(c->d_winners.ensure((size_t)c->W * (c->row1 - c->row0) * 4));
         PRK_TRY(hipMemsetAsync(c->d_winners.p, 0xFF, (size_t)c->W * (c->row1 - c->row0) * 4, s));

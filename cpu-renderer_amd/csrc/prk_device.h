@@ -59,6 +59,7 @@ struct FrameParams {
     uint32_t *color; // points at frame row row0
     float *zbuf;     // points at frame row row0 (row stride W floats)
     int32_t *winners;// optional (debug): per pixel winning triangle, -1 none
+    unsigned long long *prof;  // 16 phase-cycle counters (PRK_PROF builds only write them)
     // tiling
     int32_t tile_w, tile_h, tiles_x, tiles_y;
     int32_t tile_w_log2;  // tile_w is a power of two

@@ -27,6 +27,14 @@
 #ifndef PRK_DIAG
 #define PRK_DIAG 0
 #endif
+#ifndef PRK_PROF
+#define PRK_PROF 0  // 1: accumulate per-phase s_memtime cycles into fp.prof (diagnostic builds)
+#endif
+#if PRK_PROF
+#define PRK_T() __builtin_amdgcn_s_memtime()
+#else
+#define PRK_T() 0ull
+#endif
 #ifndef PRK_VIS_MIN_WAVES
 #define PRK_VIS_MIN_WAVES 3  // waves per SIMD k_vis is register-budgeted for
 #endif
@@ -91,6 +99,7 @@ struct WaveSlotsT {
     float f[NF][64];
     int32_t i[kSpanI][64];
 };
+constexpr int kTagPad = 16;  // k_shade: tags past the tile's last pixel (chunked reads)
 constexpr int kSpanFVis = 9;  // the visibility sweep reads no normals or colours (SF_IZ + 1)
 using VisSlots = WaveSlotsT<kSpanFVis>;
 using ShadeSlots = WaveSlotsT<kSpanF>;
@@ -172,13 +181,24 @@ __device__ __forceinline__ int span_setup_avx(const FrameParams &fp, const TileC
 #if PRK_PIXEL_ITEMS
         // Shading sweep: one item per pixel this span won; the won pixels of
         // the span's first 64 columns as a bit mask.
+        // Tags are read 16 at a time (4 x ds_read_b128 from 16-B aligned
+        // chunks), so the loads of a chunk are in flight together.
         const int rowoff = (Row - tc.y0) * tc.tw - tc.x0;
         int won = 0;
         uint64_t wm = 0;
-        for (int32_t x = xa; x < xb; ++x) {
-            const bool w = is_winner(tc, rowoff + x, tag);
-            won += w ? 1 : 0;
-            if (w && x - xa < 64) wm |= 1ull << (x - xa);
+        for (int32_t x0 = xa & ~3; x0 < xb; x0 += 16) {
+            const uint4 *q = reinterpret_cast<const uint4 *>(tc.tags + rowoff + x0);
+            const uint4 c0 = q[0], c1 = q[1], c2 = q[2], c3 = q[3];
+            const uint32_t tg[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                                     c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int32_t x = x0 + k;
+                const bool w = tg[k] == tag && x >= xa && x < xb;
+                won += w ? 1 : 0;
+                const int32_t sh = x - xa;
+                if (w && sh < 64) wm |= 1ull << sh;
+            }
         }
         ws.i[SI_WM0][lane] = (int32_t)(uint32_t)wm;
         ws.i[SI_WM1][lane] = (int32_t)(uint32_t)(wm >> 32);
@@ -573,7 +593,9 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const bool col0 = tc.x0 == 0 && M != MODE_AVX;
     const int32_t ystart = col0 ? tc.y0 - 1 : tc.y0;  // scalar: (row-1) may store into (row, 0)
+    unsigned long long pt[4] = {0, 0, 0, 0};  // PRK_PROF: setup, walk, scan/map, items
     for (uint32_t base = wave * 64; base < n; base += 64 * kWaves) {
+        unsigned long long t0 = PRK_T();
         const uint32_t i = base + lane;
         bool active = i < n;
         uint32_t e = 0;
@@ -615,6 +637,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
         if (!(ModeTraits<M>::tex && active)) texi = 0;
         const uint32_t tag = 0xFFFFFFFEu - e;
         if (PRK_DIAG & 4) active = false;
+        if (PRK_PROF) { const unsigned long long t1 = PRK_T(); pt[0] += t1 - t0; t0 = t1; }
         for (int32_t r = ystart; r < tc.y1; ++r) {
             int items = 0;
             if (active && wk.Row == r) {
@@ -627,6 +650,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
                 wk.end_row(paired);
                 active = wk.Row < wk.MaxY;
             }
+            if (PRK_PROF) { const unsigned long long t1 = PRK_T(); pt[1] += t1 - t0; t0 = t1; }
             const int incl = wave_incl_scan(items, lane);
             const int total = __builtin_amdgcn_readlane(incl, 63);
             const int excl = incl - items;
@@ -636,6 +660,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
             // the span carried over from the previous window) names the span
             // of every item.
             int carry = 0;
+            if (PRK_PROF) { const unsigned long long t1 = PRK_T(); pt[2] += t1 - t0; t0 = t1; }
             for (int it0 = 0; it0 < (((PRK_DIAG & 2) || ((PRK_DIAG & 8) && SHADE)) ? 0 : total); it0 += 64) {
                 ws.i[SI_MARK][lane] = 0;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -658,9 +683,12 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (PRK_PROF) { const unsigned long long t1 = PRK_T(); pt[3] += t1 - t0; t0 = t1; }
             if (!__any(active)) break;
         }
     }
+    if (PRK_PROF && lane == 0)
+        for (int k = 0; k < 4; ++k) atomicAdd(fp.prof + (SHADE ? 4 : 0) + k, pt[k]);
 }
 
 // Workgroup-wide exclusive scan of one value per thread.
@@ -791,10 +819,11 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_SHADE_MIN_WAVES)
     const int npx = fp.tile_w * fp.tile_h;
     uint32_t *tags = reinterpret_cast<uint32_t *>(lds);
     tc.tags = tags;
-    ShadeSlots *slots = reinterpret_cast<ShadeSlots *>(tags + ((npx + 1) & ~1));
+    ShadeSlots *slots = reinterpret_cast<ShadeSlots *>(tags + npx + kTagPad);
     ShadeSlots &ws = slots[threadIdx.x >> 6];
     const uint32_t *tags_in = wtag + (size_t)t * npx;
     for (int p = threadIdx.x; p < npx; p += blockDim.x) tags[p] = tags_in[p];
+    if (threadIdx.x < kTagPad) tags[npx + threadIdx.x] = 0xFFFFFFFFu;  // chunked reads run past the end
     __syncthreads();
     if constexpr (MODESET >= 0) {
         sweep<(MODESET >= 0 ? MODESET : 0), true, UNI>(fp, tc, ws, bins, b0, nwin, list, anomaly);
@@ -846,7 +875,7 @@ static size_t vis_lds(const prk::FrameParams *fp) {
 }
 static size_t shade_lds(const prk::FrameParams *fp) {
     const size_t npx = (size_t)fp->tile_w * fp->tile_h;
-    return ((npx + 1) & ~(size_t)1) * sizeof(uint32_t) + prk::kWaves * sizeof(prk::ShadeSlots);
+    return (npx + prk::kTagPad) * sizeof(uint32_t) + prk::kWaves * sizeof(prk::ShadeSlots);
 }
 
 // Sweep 1 (k_vis) then sweep 2 (k_shade) on stream s; `mid` (optional) is

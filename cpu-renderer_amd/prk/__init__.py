@@ -62,6 +62,7 @@ _SIGS = {
     "prk_timing_reset": (C.c_int, [C.c_void_p]),
     "prk_set_debug": (C.c_int, [C.c_void_p, C.c_int32]),
     "prk_download_winners": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "prk_debug_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32]),
     "prk_set_tile": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     "prk_construct_sphere": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.POINTER(C.c_uint32)]),
@@ -238,6 +239,11 @@ class Renderer:
 
     def timing_reset(self):
         _check("prk_timing_reset", self._L.prk_timing_reset(self._h))
+
+    def debug_counters(self, n=16):
+        out = (C.c_uint64 * n)()
+        _check("prk_debug_counters", self._L.prk_debug_counters(self._h, out, n))
+        return list(out)
 
     def stats(self):
         s = abi.PrkStats()

@@ -176,6 +176,9 @@ int prk_timing_reset(prk_context *ctx);
  * rows [row0,row1).  Requires prk_set_debug(ctx, 1) before the flush. */
 int prk_set_debug(prk_context *ctx, int32_t enable);
 int prk_download_winners(prk_context *ctx, int32_t *winners_host);
+/* Debug: the raster kernels' phase cycle counters (written only by builds
+ * with -DPRK_PROF; zeroed by prk_timing_reset), n <= 16. */
+int prk_debug_counters(prk_context *ctx, uint64_t *out, int32_t n);
 
 /* Tunables (testing / benchmarking). tile_w must be a power of two >= 8,
  * 64 <= tile_w * tile_h <= 8192. */
