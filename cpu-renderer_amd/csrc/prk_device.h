@@ -257,44 +257,67 @@ __device__ __forceinline__ void load_positions(const DrawRec &d, uint32_t gt, co
     }
 }
 
+// The vertex attributes one triangle's setup reads (per mode), loaded
+// separately so a sweep can fetch the next triangle while it walks this one.
+template <int M>
+struct TriRaw {
+    float v[9], n[9], c[12], uv[6];
+};
+
+template <int M>
+__device__ __forceinline__ void load_tri(const DrawRec &d, uint32_t gt, TriRaw<M> &r) {
+    using TR = ModeTraits<M>;
+    const float *v = d.V + 9 * (size_t)gt;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) r.v[k] = v[k];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) r.n[k] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) r.c[k] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) r.uv[k] = 0.0f;
+    if (TR::phong || !TR::tex) {  // Phong normals, or Gouraud lighting's normals
+        const float *n = d.N + 9 * (size_t)gt;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) r.n[k] = n[k];
+    }
+    if (TR::color && d.C) {
+        const float *c = d.C + 12 * (size_t)gt;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) r.c[k] = c[k];
+    }
+    if (TR::tex) {
+        const float *u = d.UV + 6 * (size_t)gt;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) r.uv[k] = u[k];
+    }
+}
+
 // FillEdgeTable (projekt.cpp:3882-4121) for ONE triangle followed by
 // MergeSort (2-72) of its <= 3 visible edges.  Returns the edge count.
 template <int M>
-__device__ __forceinline__ int setup_triangle(const DrawRec &d, uint32_t gt, const FrameParams &fp,
+__device__ __forceinline__ int setup_from_raw(const TriRaw<M> &r, const DrawRec &d, const FrameParams &fp,
                                               Edge &s0, Edge &s1, Edge &s2) {
     using TR = ModeTraits<M>;
     constexpr bool kTex = TR::tex;
     constexpr bool kPhong = TR::phong;
     constexpr bool kColor = TR::color;
     V3 cam[3], proj[3];
-    load_positions(d, gt, fp, cam, proj);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {  // camera vertex = vertex + Object->P (3898-3903), ProjectVertex
+        cam[k] = V3{r.v[3 * k + 0] + d.P[0], r.v[3 * k + 1] + d.P[1], r.v[3 * k + 2] + d.P[2]};
+        proj[k] = project_vertex(cam[k], fp);
+    }
     if (!front_facing(proj)) return 0;
 
     V3 nrm[3];
     float col[3][4], uv[3][2];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        if (kPhong) {
-            const float *n = d.N + 9 * (size_t)gt + 3 * k;
-            nrm[k] = V3{n[0], n[1], n[2]};
-        } else if (!kTex) {
-            const float *n = d.N + 9 * (size_t)gt + 3 * k;  // Gouraud lighting reads normals
-            nrm[k] = V3{n[0], n[1], n[2]};
-        } else {
-            nrm[k] = V3{0.0f, 0.0f, 0.0f};
-        }
-        if (kColor && d.C) {
-            const float *c = d.C + 12 * (size_t)gt + 4 * k;
-            col[k][0] = c[0]; col[k][1] = c[1]; col[k][2] = c[2]; col[k][3] = c[3];
-        } else {
-            col[k][0] = col[k][1] = col[k][2] = col[k][3] = 0.0f;
-        }
-        if (kTex) {
-            const float *u = d.UV + 6 * (size_t)gt + 2 * k;
-            uv[k][0] = u[0]; uv[k][1] = u[1];
-        } else {
-            uv[k][0] = uv[k][1] = 0.0f;
-        }
+        nrm[k] = V3{r.n[3 * k + 0], r.n[3 * k + 1], r.n[3 * k + 2]};
+        col[k][0] = r.c[4 * k + 0]; col[k][1] = r.c[4 * k + 1];
+        col[k][2] = r.c[4 * k + 2]; col[k][3] = r.c[4 * k + 3];
+        uv[k][0] = r.uv[2 * k + 0]; uv[k][1] = r.uv[2 * k + 1];
     }
 
     Edge e0, e1, e2;
@@ -421,6 +444,14 @@ __device__ __forceinline__ int setup_triangle(const DrawRec &d, uint32_t gt, con
         s2 = a2;
     }
     return n;
+}
+
+template <int M>
+__device__ __forceinline__ int setup_triangle(const DrawRec &d, uint32_t gt, const FrameParams &fp,
+                                              Edge &s0, Edge &s1, Edge &s2) {
+    TriRaw<M> r;
+    load_tri<M>(d, gt, r);
+    return setup_from_raw<M>(r, d, fp, s0, s1, s2);
 }
 
 // AET edge step (projekt.cpp:3811-3829), only the fields mode M reads

@@ -77,6 +77,9 @@ __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
 #ifndef PRK_ZPRE
 #define PRK_ZPRE 1  // sweep 1: skip 1/w and the UV mask of fragments that cannot raise the key
 #endif
+#ifndef PRK_PREFETCH
+#define PRK_PREFETCH 1  // single-draw sweeps prefetch the next chunk's triangles
+#endif
 #ifndef PRK_PIXEL_ITEMS
 #define PRK_PIXEL_ITEMS 1  // shading sweep (AVX): one work item per won pixel, not per lane chain
 #endif
@@ -594,6 +597,20 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
     const bool col0 = tc.x0 == 0 && M != MODE_AVX;
     const int32_t ystart = col0 ? tc.y0 - 1 : tc.y0;  // scalar: (row-1) may store into (row, 0)
     unsigned long long pt[4] = {0, 0, 0, 0};  // PRK_PROF: setup, walk, scan/map, items
+    // Single-draw frames prefetch: the next chunk's bin entry is loaded at the
+    // top of a chunk and its vertex attributes before the row walk, so both
+    // loads are in flight while this chunk's setup and rows run.
+    constexpr bool kPre = UNI && PRK_PREFETCH && !SHADE;  // (k_shade has no registers to spare)
+    TriRaw<M> nraw;
+    uint32_t ne_e = 0, ne_g = 0;
+    if constexpr (kPre) {
+        const uint32_t i0 = wave * 64 + lane;
+        if (i0 < n) {
+            ne_e = list ? list[b0 + i0] : i0;
+            ne_g = bins[b0 + ne_e];
+            load_tri<M>(fp.draw0, fp.draw0.geom_tri0 + (ne_g - fp.draw0.first_global), nraw);
+        }
+    }
     for (uint32_t base = wave * 64; base < n; base += 64 * kWaves) {
         unsigned long long t0 = PRK_T();
         const uint32_t i = base + lane;
@@ -602,16 +619,30 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
         int32_t texi = 0;
         RowWalker<M, SHADE> wk;
         uint32_t anom = 0;
+        TriRaw<M> craw;
+        const uint32_t inext = i + 64 * kWaves;
+        if constexpr (kPre) {
+            craw = nraw;
+            e = ne_e;
+            if (inext < n) {
+                ne_e = list ? list[b0 + inext] : inext;
+                ne_g = bins[b0 + ne_e];
+            }
+        }
         if (active) {
-            e = list ? list[b0 + i] : i;
-            const uint32_t g = bins[b0 + e];
+            if constexpr (!kPre) e = list ? list[b0 + i] : i;
             Edge s0, s1, s2;
             int ne;
-            if constexpr (UNI) {  // one draw: its record is uniform (kernel arguments)
+            if constexpr (kPre) {
+                ne = setup_from_raw<M>(craw, fp.draw0, fp, s0, s1, s2);
+                texi = fp.draw0.tex;
+            } else if constexpr (UNI) {  // one draw: its record is uniform (kernel arguments)
+                const uint32_t g = bins[b0 + e];
                 const uint32_t gt = fp.draw0.geom_tri0 + (g - fp.draw0.first_global);
                 ne = setup_triangle<M>(fp.draw0, gt, fp, s0, s1, s2);
                 texi = fp.draw0.tex;
             } else {
+                const uint32_t g = bins[b0 + e];
                 const DrawRec *d;
                 uint32_t gt;
                 resolve_draw(fp, g, d, gt);
@@ -632,6 +663,9 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
                 if (fr != 0 && !SHADE) atomicAdd(anomaly + 1, 1u);
                 active = wk.Row < wk.MaxY;
             }
+        }
+        if constexpr (kPre) {
+            if (inext < n) load_tri<M>(fp.draw0, fp.draw0.geom_tri0 + (ne_g - fp.draw0.first_global), nraw);
         }
         if (anom) atomicAdd(anomaly, anom);
         if (!(ModeTraits<M>::tex && active)) texi = 0;
