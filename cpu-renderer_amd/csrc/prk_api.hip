@@ -24,8 +24,8 @@ hipError_t prk_launch_tri_draw(const prk::DrawRec *, uint32_t, uint32_t *, uint3
 hipError_t prk_bin_phase1(const prk::FrameParams *, uint32_t *, uint32_t *, void *, void *, size_t *, hipStream_t);
 hipError_t prk_bin_phase2(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, uint32_t *, uint32_t *,
                           uint32_t *, uint32_t *, uint32_t *, void *, size_t *, hipStream_t);
-hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, const uint32_t *, uint8_t *,
-                             uint32_t *, uint32_t *, uint32_t *, uint32_t *, hipEvent_t, hipStream_t);
+hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, const uint32_t *, uint32_t *,
+                             uint32_t *, uint32_t *, uint32_t *, void *, void *, uint32_t *, hipEvent_t, hipStream_t);
 }
 
 namespace {
@@ -89,7 +89,7 @@ struct prk_context {
     uint32_t pending_tris = 0;
     // scratch
     DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_tri_n, d_tri_off, d_keys_a, d_vals_a, d_keys_b, d_bins,
-        d_offs, d_won, d_list, d_temp, d_winners, d_anomaly, d_nwin, d_wtag, d_prof;
+        d_offs, d_won, d_list, d_temp, d_winners, d_anomaly, d_nwin, d_wtag, d_prof, d_recs, d_pmap;
     uint32_t *h_total = nullptr;  // pinned
     int32_t tile_w = 256, tile_h = 8;  // measured best for C3b
     bool debug = false;
@@ -162,7 +162,7 @@ int prk_destroy(prk_context *c) {
     }
     DevBuf *bufs[] = {&c->d_draws,  &c->d_texs,   &c->d_tri_draw, &c->d_ranges, &c->d_tri_n, &c->d_tri_off,
                       &c->d_keys_a, &c->d_vals_a, &c->d_keys_b,   &c->d_bins,   &c->d_offs,  &c->d_won,
-                      &c->d_list,   &c->d_temp,   &c->d_winners,  &c->d_anomaly, &c->d_nwin, &c->d_wtag, &c->d_prof};
+                      &c->d_list,   &c->d_temp,   &c->d_winners,  &c->d_anomaly, &c->d_nwin, &c->d_wtag, &c->d_prof, &c->d_recs, &c->d_pmap};
     for (DevBuf *b : bufs) b->release();
     if (c->h_total) (void)hipHostFree(c->h_total);
     for (auto &slot : c->ev)
@@ -602,9 +602,14 @@ int prk_flush(prk_context *c, void *stream) {
     }
     PRK_TRY(c->d_nwin.ensure((size_t)ntiles * 4));
     PRK_TRY(c->d_wtag.ensure((size_t)ntiles * c->tile_w * c->tile_h * 4));
+    if (modeset == prk::MODE_AVX) {  // span records (64 B) + record map (2 B) per tile pixel
+        PRK_TRY(c->d_recs.ensure((size_t)ntiles * c->tile_w * c->tile_h * 64));
+        PRK_TRY(c->d_pmap.ensure((size_t)ntiles * c->tile_w * c->tile_h * 2));
+    }
     PRK_TRY(prk_launch_raster(&fp, modeset, (const uint32_t *)c->d_offs.p, (const uint32_t *)c->d_bins.p,
-                              (uint8_t *)c->d_won.p, (uint32_t *)c->d_list.p, (uint32_t *)c->d_nwin.p,
-                              (uint32_t *)c->d_wtag.p, (uint32_t *)c->d_anomaly.p, c->ev[slot][3], s));
+                              (uint32_t *)c->d_won.p, (uint32_t *)c->d_list.p, (uint32_t *)c->d_nwin.p,
+                              (uint32_t *)c->d_wtag.p, c->d_recs.p, c->d_pmap.p, (uint32_t *)c->d_anomaly.p,
+                              c->ev[slot][3], s));
     PRK_TRY(hipEventRecord(c->ev[slot][2], s));
     c->pending[slot] = true;
     c->last_slot = slot;

@@ -38,6 +38,12 @@
 #ifndef PRK_VIS_MIN_WAVES
 #define PRK_VIS_MIN_WAVES 3  // waves per SIMD k_vis is register-budgeted for
 #endif
+#ifndef PRK_SPAN_MIN_WAVES
+#define PRK_SPAN_MIN_WAVES 3  // waves per SIMD k_span is register-budgeted for
+#endif
+#ifndef PRK_SPAN_RECORDS
+#define PRK_SPAN_RECORDS 1  // AVX frames shade through k_span + k_pix (else k_shade)
+#endif
 #ifndef PRK_SHADE_MIN_WAVES
 #define PRK_SHADE_MIN_WAVES 3  // waves per SIMD k_shade is register-budgeted for
 #endif
@@ -870,6 +876,220 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_SHADE_MIN_WAVES)
     }
 }
 
+// ---------------------------------------------------------------------------
+// AVX frames shade in two kernels instead of k_shade's in-wave work items:
+//   k_span  one workgroup per tile walks the entries that won a pixel (setup +
+//           AET rows as k_shade) and, for every row span that won a pixel,
+//           writes the span's FillLineOptimized lane-init record (64 B) and
+//           points the won pixels at it (LDS map, flushed coalesced);
+//   k_pix   one thread per pixel replays its lane chain from the record,
+//           shades (texel + Phong) and stores z and colour, coalesced.
+// The walk keeps no item state live and the shading runs at full lane
+// occupancy with no walker registers.
+// ---------------------------------------------------------------------------
+struct SpanRec {  // one won row span (FillLineOptimized span setup, 1543-1835)
+    int32_t left_tex;  // LeftXa (low 16 bits) | texture index << 16
+    float xoff, lw, lu, lv, lz, iw, iu, iv, iz, ln0, ln1, ln2, in0, in1, in2;
+};
+static_assert(sizeof(SpanRec) == 64, "span record is four dwordx4");
+constexpr uint32_t kNoRec = 0xFFFFu;
+
+// k_span: FillLineOptimized span setup (projekt.cpp:1543-1835) of one row;
+// when the span won a pixel of the tile, write its record and point the won
+// pixels (LDS map) at it.
+__device__ __forceinline__ void span_record(const FrameParams &fp, const TileCtx &tc, const Edge &L, const Edge &R,
+                                            int32_t Row, uint32_t tag, int32_t texi, SpanRec *trecs, uint16_t *map,
+                                            uint32_t *count) {
+    if (Row < tc.y0) return;
+    const int32_t W = fp.W;
+    float XOffset = 0.0f;
+    float LeftX = L.X;  // 1545-1565
+    if (LeftX < 0) { XOffset = -L.X; LeftX = 0; }
+    else if (LeftX >= W) LeftX = (float)W - 1;
+    float RightX = R.X;
+    if (RightX < 0) RightX = 0;
+    else if (RightX >= W) RightX = (float)W - 1;
+    if (LeftX != LeftX || RightX != RightX) return;  // pinned: NaN edge X draws nothing
+    const int32_t XDiff = (int32_t)((uint32_t)round_s32(R.X) - (uint32_t)round_s32(L.X));  // 1568-1570
+    const int32_t MinX = round_s32(LeftX), MaxX = round_s32(RightX);  // 1588-1592
+    int32_t LeftXa = MinX;
+    if (MinX & 7) {  // 1594-1609
+        LeftXa = MinX & ~7;
+        XOffset -= (float)(MinX & 7) * 1.0f;
+    }
+    const int32_t xa = max(MinX, tc.x0), xb = min(MaxX, tc.x1);  // [MinX, MaxX) in the tile
+    if (xa >= xb) return;
+    // Won pixels of the span (tags read 16 at a time).
+    const int rowoff = (Row - tc.y0) * tc.tw - tc.x0;
+    int won = 0;
+    uint64_t wm = 0;
+    for (int32_t x0 = xa & ~3; x0 < xb; x0 += 16) {
+        const uint4 *q = reinterpret_cast<const uint4 *>(tc.tags + rowoff + x0);
+        const uint4 c0 = q[0], c1 = q[1], c2 = q[2], c3 = q[3];
+        const uint32_t tg[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                                 c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int32_t x = x0 + k;
+            const bool w = tg[k] == tag && x >= xa && x < xb;
+            won += w ? 1 : 0;
+            const int32_t sh = x - xa;
+            if (w && sh < 64) wm |= 1ull << sh;
+        }
+    }
+    if (won == 0) return;
+    const float fXD = (float)XDiff;
+    float IW = 0, IU = 0, IV = 0, IZ = 0, IN0 = 0, IN1 = 0, IN2 = 0;
+    if (XDiff != 0) {  // 1666-1835
+        IW = (R.W - L.W) / fXD;
+        IU = (R.U - L.U) / fXD;
+        IV = (R.V - L.V) / fXD;
+        IN0 = (R.N0 - L.N0) / fXD;
+        IN1 = (R.N1 - L.N1) / fXD;
+        IN2 = (R.N2 - L.N2) / fXD;
+        IZ = (R.Z - L.Z) / fXD;
+    }
+    const uint32_t ridx = atomicAdd(count, 1u);  // < npx: every record owns a won pixel
+    float4 *q = reinterpret_cast<float4 *>(trecs + ridx);
+    q[0] = make_float4(__int_as_float((LeftXa & 0xFFFF) | (texi << 16)), XOffset, L.W, L.U);
+    q[1] = make_float4(L.V, L.Z, IW, IU);
+    q[2] = make_float4(IV, IZ, L.N0, L.N1);
+    q[3] = make_float4(L.N2, IN0, IN1, IN2);
+    for (uint64_t m = wm; m; m &= m - 1) map[rowoff + xa + (int32_t)__builtin_ctzll(m)] = (uint16_t)ridx;
+    if (won > __builtin_popcountll(wm))  // past the span's first 64 columns
+        for (int32_t x = xa + 64; x < xb; ++x)
+            if (is_winner(tc, rowoff + x, tag)) map[rowoff + x] = (uint16_t)ridx;
+}
+
+
+template <bool UNI>
+__global__ void __launch_bounds__(64 * kWaves, PRK_SPAN_MIN_WAVES)
+    k_span(FrameParams fp, const uint32_t *__restrict__ offs, const uint32_t *__restrict__ bins,
+           const uint32_t *__restrict__ list, const uint32_t *__restrict__ nwin_in,
+           const uint32_t *__restrict__ wtag, SpanRec *__restrict__ recs, uint16_t *__restrict__ pmap,
+           uint32_t *__restrict__ anomaly) {
+    constexpr int M = MODE_AVX;
+    extern __shared__ unsigned long long lds[];
+    const int ntile = fp.tiles_x * fp.tiles_y;
+    const int t = blockIdx.x;
+    if (t >= ntile) return;
+    const uint32_t nwin = nwin_in[t];
+    if (nwin == 0) return;
+    const uint32_t b0 = offs[t];
+    TileCtx tc = tile_ctx(fp, t);
+    const int npx = fp.tile_w * fp.tile_h;
+    uint32_t *tags = reinterpret_cast<uint32_t *>(lds);
+    uint16_t *map = reinterpret_cast<uint16_t *>(tags + npx + kTagPad);
+    uint32_t *count = reinterpret_cast<uint32_t *>(map + ((npx + 1) & ~1));
+    tc.tags = tags;
+    const uint32_t *tags_in = wtag + (size_t)t * npx;
+    for (int p = threadIdx.x; p < npx; p += blockDim.x) {
+        tags[p] = tags_in[p];
+        map[p] = (uint16_t)kNoRec;
+    }
+    if (threadIdx.x < kTagPad) tags[npx + threadIdx.x] = 0xFFFFFFFFu;  // chunked reads run past the end
+    if (threadIdx.x == 0) *count = 0;
+    __syncthreads();
+    SpanRec *trecs = recs + (size_t)t * npx;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t base = wave * 64; base < nwin; base += 64 * kWaves) {
+        const uint32_t i = base + lane;
+        bool active = i < nwin;
+        uint32_t e = 0;
+        int32_t texi = 0;
+        RowWalker<M, true> wk;
+        uint32_t anom = 0;
+        if (active) {
+            e = list[b0 + i];
+            const uint32_t g = bins[b0 + e];
+            Edge s0, s1, s2;
+            int ne;
+            if constexpr (UNI) {
+                const uint32_t gt = fp.draw0.geom_tri0 + (g - fp.draw0.first_global);
+                ne = setup_triangle<M>(fp.draw0, gt, fp, s0, s1, s2);
+                texi = fp.draw0.tex;
+            } else {
+                const DrawRec *d;
+                uint32_t gt;
+                resolve_draw(fp, g, d, gt);
+                ne = setup_triangle<M>(*d, gt, fp, s0, s1, s2);
+                texi = d->tex;
+            }
+            active = ne >= 2;
+            if (active) {
+                Walker<M, true> w0;
+                w0.init(ne, s0, s1, s2, fp.H, tc.y1, anom);
+                const int fr = w0.fast_replay(tc.y0, ne);
+                wk.from(w0);
+                if (fr < 0)
+                    while (wk.Row < tc.y0 && wk.Row < wk.MaxY) wk.end_row(wk.begin_row());
+                active = wk.Row < wk.MaxY;
+            }
+        }
+        if (anom) atomicAdd(anomaly, anom);
+        const uint32_t tag = 0xFFFFFFFEu - e;
+        // Each lane walks its own rows; no cross-lane work in the loop.
+        while (active) {
+            const int32_t Row = wk.Row;
+            const bool paired = wk.begin_row();
+            if (paired) span_record(fp, tc, wk.S0, wk.S1, Row, tag, texi, trecs, map, count);
+            wk.end_row(paired);
+            active = wk.Row < wk.MaxY && wk.Row < tc.y1;
+        }
+    }
+    __syncthreads();
+    uint16_t *map_out = pmap + (size_t)t * npx;
+    for (int p = threadIdx.x; p < npx; p += blockDim.x) map_out[p] = map[p];
+}
+
+// k_pix: shade the won pixels of one tile from their span records.
+template <bool UNI>
+__global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__restrict__ nwin_in,
+                                             const SpanRec *__restrict__ recs, const uint16_t *__restrict__ pmap) {
+    const int ntile = fp.tiles_x * fp.tiles_y;
+    const int t = blockIdx.x;
+    if (t >= ntile) return;
+    if (nwin_in[t] == 0) return;
+    const TileCtx tc = tile_ctx(fp, t);
+    const int npx = fp.tile_w * fp.tile_h;
+    const SpanRec *trecs = recs + (size_t)t * npx;
+    const uint16_t *map = pmap + (size_t)t * npx;
+    for (int p = threadIdx.x; p < npx; p += blockDim.x) {
+        const uint32_t m = map[p];
+        if (m == kNoRec) continue;
+        const int32_t x = tc.x0 + (p & (fp.tile_w - 1)), Row = tc.y0 + (p >> fp.tile_w_log2);
+        const float4 *q = reinterpret_cast<const float4 *>(trecs + m);
+        const float4 r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];
+        const int32_t lt = __float_as_int(r0.x);
+        const int32_t LeftXa = (int32_t)(int16_t)(lt & 0xFFFF);
+        const TexRec tex = UNI ? fp.tex0 : fp.texs[lt >> 16];
+        const int32_t rel = x - LeftXa, i = rel & 7, b = rel >> 3;
+        const float IW = r1.z, IU = r1.w, IV = r2.x, IZ = r2.y;
+        const float o = r0.y + (float)i;  // lane init (XOffset + i)*inc, 1712-1835
+        float w = r0.z + o * IW, u = r0.w + o * IU;
+        float v = r1.x + o * IV, z = r1.y + o * IZ;
+        {
+            const float IW8 = IW * 8.0f, IU8 = IU * 8.0f, IV8 = IV * 8.0f, IZ8 = 8.0f * IZ;
+            for (int32_t k = 0; k < b; ++k) { z = z + IZ8; w = w + IW8; u = u + IU8; v = v + IV8; }  // 2262-2282
+        }
+        const float iw = 1.0f / w;  // 1865-1866
+        const float fu = iw * u, fv = iw * v;
+        const uint32_t tx = texel_avx(tex, fu, fv);
+        const float IN0 = r3.y, IN1 = r3.z, IN2 = r3.w;
+        float n0 = r2.z + o * IN0, n1 = r2.w + o * IN1, n2 = r3.x + o * IN2;
+        normalize_div(n0, n1, n2);  // 1754
+        {
+            const float IN08 = IN0 * 8.0f, IN18 = IN1 * 8.0f, IN28 = IN2 * 8.0f;
+            for (int32_t k = 0; k < b; ++k) {  // block steps 2262-2282
+                float a = n0 + IN08, bb = n1 + IN18, c = n2 + IN28;
+                normalize_div(a, bb, c);
+                n0 = a; n1 = bb; n2 = c;
+            }
+        }
+        put_winner(fp, x, Row, z, shade_avx_texel(fp, tx, z, n0, n1, n2, x, i, Row));
+    }
+}
+
 // Explicit instantiations used by the host.
 #define PRK_VIS_ARGS FrameParams, const uint32_t *, const uint32_t *, uint8_t *, uint32_t *, uint32_t *, uint32_t *, \
                      uint32_t *
@@ -878,6 +1098,12 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_SHADE_MIN_WAVES)
 #define PRK_INST(MS, UNI)                                  \
     template __global__ void k_vis<MS, UNI>(PRK_VIS_ARGS); \
     template __global__ void k_shade<MS, UNI>(PRK_SHADE_ARGS);
+template __global__ void k_span<false>(FrameParams, const uint32_t *, const uint32_t *, const uint32_t *,
+                                       const uint32_t *, const uint32_t *, SpanRec *, uint16_t *, uint32_t *);
+template __global__ void k_span<true>(FrameParams, const uint32_t *, const uint32_t *, const uint32_t *,
+                                      const uint32_t *, const uint32_t *, SpanRec *, uint16_t *, uint32_t *);
+template __global__ void k_pix<false>(FrameParams, const uint32_t *, const SpanRec *, const uint16_t *);
+template __global__ void k_pix<true>(FrameParams, const uint32_t *, const SpanRec *, const uint16_t *);
 PRK_INST(-1, false)
 PRK_INST(MODE_AVX, false)
 PRK_INST(MODE_AVX, true)
@@ -914,32 +1140,61 @@ static size_t shade_lds(const prk::FrameParams *fp) {
 
 // Sweep 1 (k_vis) then sweep 2 (k_shade) on stream s; `mid` (optional) is
 // recorded between them.
+static size_t span_lds(const prk::FrameParams *fp) {
+    const size_t npx = (size_t)fp->tile_w * fp->tile_h;
+    return (npx + prk::kTagPad) * sizeof(uint32_t) + ((npx + 1) & ~(size_t)1) * sizeof(uint16_t) + 16;
+}
+
+// Sweep 1 (k_vis) then the shading: k_span + k_pix for AVX frames, k_shade
+// otherwise; `mid` (optional) is recorded after k_vis.  recs / pmap: the
+// span records (64 B per tile pixel) and the per-pixel record map (2 B).
 hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint32_t *offs, const uint32_t *bins,
-                             uint8_t *won, uint32_t *list, uint32_t *nwin, uint32_t *wtag, uint32_t *anomaly,
-                             hipEvent_t mid, hipStream_t s) {
+                             uint32_t *won, uint32_t *list, uint32_t *nwin, uint32_t *wtag, void *recs, void *pmap,
+                             uint32_t *anomaly, hipEvent_t mid, hipStream_t s) {
     const uint32_t ntile = (uint32_t)(fp->tiles_x * fp->tiles_y);
     if (ntile == 0) return hipSuccess;
-    const size_t lv = vis_lds(fp), ls = shade_lds(fp);
+    const size_t lv = vis_lds(fp), ls = shade_lds(fp), lsp = span_lds(fp);
     const bool uni = fp->ndraws == 1;
-#define PRK_LAUNCH(MS, UNI)                                                                                          \
+    prk::SpanRec *rp = reinterpret_cast<prk::SpanRec *>(recs);
+    uint16_t *mp = reinterpret_cast<uint16_t *>(pmap);
+#define PRK_VIS(MS, UNI)                                                                                             \
     do {                                                                                                             \
-        hipLaunchKernelGGL((prk::k_vis<MS, UNI>), dim3(ntile), dim3(64 * prk::kWaves), lv, s, *fp, offs, bins, won, \
-                           list, nwin, wtag, anomaly);                                                               \
+        hipLaunchKernelGGL((prk::k_vis<MS, UNI>), dim3(ntile), dim3(64 * prk::kWaves), lv, s, *fp, offs, bins,      \
+                           (uint8_t *)won, list, nwin, wtag, anomaly);                                               \
         if (mid) (void)hipEventRecord(mid, s);                                                                       \
-        hipLaunchKernelGGL((prk::k_shade<MS, UNI>), dim3(ntile), dim3(64 * prk::kWaves), ls, s, *fp, offs, bins,    \
-                           list, nwin, wtag, anomaly);                                                               \
+    } while (0)
+#define PRK_SHADE(MS, UNI)                                                                                           \
+    hipLaunchKernelGGL((prk::k_shade<MS, UNI>), dim3(ntile), dim3(64 * prk::kWaves), ls, s, *fp, offs, bins, list,  \
+                       nwin, wtag, anomaly)
+#define PRK_SPANPIX(UNI)                                                                                             \
+    do {                                                                                                             \
+        hipLaunchKernelGGL((prk::k_span<UNI>), dim3(ntile), dim3(64 * prk::kWaves), lsp, s, *fp, offs, bins, list,  \
+                           nwin, wtag, rp, mp, anomaly);                                                             \
+        hipLaunchKernelGGL((prk::k_pix<UNI>), dim3(ntile), dim3(256), 0, s, *fp, nwin, rp, mp);                      \
     } while (0)
     switch (modeset) {
-        case prk::MODE_AVX: if (uni) PRK_LAUNCH(prk::MODE_AVX, true); else PRK_LAUNCH(prk::MODE_AVX, false); break;
+        case prk::MODE_AVX:
+            if (uni) {
+                PRK_VIS(prk::MODE_AVX, true);
+                if (PRK_SPAN_RECORDS) PRK_SPANPIX(true); else PRK_SHADE(prk::MODE_AVX, true);
+            } else {
+                PRK_VIS(prk::MODE_AVX, false);
+                if (PRK_SPAN_RECORDS) PRK_SPANPIX(false); else PRK_SHADE(prk::MODE_AVX, false);
+            }
+            break;
         case prk::MODE_SC_GOURAUD:
-            if (uni) PRK_LAUNCH(prk::MODE_SC_GOURAUD, true); else PRK_LAUNCH(prk::MODE_SC_GOURAUD, false);
+            if (uni) { PRK_VIS(prk::MODE_SC_GOURAUD, true); PRK_SHADE(prk::MODE_SC_GOURAUD, true); }
+            else { PRK_VIS(prk::MODE_SC_GOURAUD, false); PRK_SHADE(prk::MODE_SC_GOURAUD, false); }
             break;
         case prk::MODE_SC_PHONG:
-            if (uni) PRK_LAUNCH(prk::MODE_SC_PHONG, true); else PRK_LAUNCH(prk::MODE_SC_PHONG, false);
+            if (uni) { PRK_VIS(prk::MODE_SC_PHONG, true); PRK_SHADE(prk::MODE_SC_PHONG, true); }
+            else { PRK_VIS(prk::MODE_SC_PHONG, false); PRK_SHADE(prk::MODE_SC_PHONG, false); }
             break;
-        default: PRK_LAUNCH(-1, false); break;
+        default: PRK_VIS(-1, false); PRK_SHADE(-1, false); break;
     }
-#undef PRK_LAUNCH
+#undef PRK_VIS
+#undef PRK_SHADE
+#undef PRK_SPANPIX
     return hipGetLastError();
 }
 

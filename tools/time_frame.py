@@ -42,8 +42,10 @@ print("lib=%s T=%d %dx%d R=%g tile=%s: frame %.3f ms  bin %.3f ms  raster %.3f m
           st["sum_ms_raster"] / n, st["sum_ms_vis"] / n, (st["sum_ms_raster"] - st["sum_ms_vis"]) / n,
           st["bin_entries"], st["anomalies"], st["slow_replays"]))
 if os.environ.get("PRK_PROF_PRINT"):
-    c = r.debug_counters(8)
+    c = r.debug_counters(16)
     for name, off in (("vis", 0), ("shade", 4)):
         tot = sum(c[off:off + 4]) or 1
         print("  %-5s cycles: setup %.3g (%.0f%%)  walk %.3g (%.0f%%)  scan %.3g (%.0f%%)  items %.3g (%.0f%%)" % (
             (name,) + tuple(v for k in range(4) for v in (c[off + k], 100.0 * c[off + k] / tot))))
+    print("  spans (per frame): vis %d (nonempty %d, items %d)  shade %d (won %d, won px %d, px of won spans %d)" % (
+        c[8] / 12, c[9] / 12, c[10] / 12, c[12] / 12, c[13] / 12, c[14] / 12, c[15] / 12))
