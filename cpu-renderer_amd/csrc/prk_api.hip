@@ -25,7 +25,8 @@ hipError_t prk_bin_phase1(const prk::FrameParams *, uint32_t *, uint32_t *, void
 hipError_t prk_bin_phase2(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, uint32_t *, uint32_t *,
                           uint32_t *, uint32_t *, uint32_t *, void *, size_t *, hipStream_t);
 hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, const uint32_t *, uint32_t *,
-                             uint32_t *, uint32_t *, uint32_t *, void *, void *, uint32_t *, hipEvent_t, hipStream_t);
+                             uint32_t *, uint32_t *, uint32_t *, void *, void *, uint32_t *, hipEvent_t, hipEvent_t,
+                             hipStream_t);
 }
 
 namespace {
@@ -97,8 +98,9 @@ struct prk_context {
     prk_stats stats{};
     // Timing ring: 3 events per flush (before bin, before raster, after raster).
     static constexpr int kRing = 32;
-    hipEvent_t ev[kRing][4] = {};  // bin start, raster start, raster end, k_vis end
+    hipEvent_t ev[kRing][5] = {};  // bin start, raster start, raster end, k_vis end, k_span end
     bool pending[kRing] = {};
+    bool split_span[kRing] = {};  // the slot's flush ran k_span + k_pix
     uint32_t frame = 0;
     int last_slot = -1;
 };
@@ -134,7 +136,7 @@ int prk_create(int device, prk_context **out) {
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     for (int i = 0; i < prk_context::kRing && e == hipSuccess; ++i)
-        for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipEventCreate(&c->ev[i][k]);
+        for (int k = 0; k < 5 && e == hipSuccess; ++k) e = hipEventCreate(&c->ev[i][k]);
     if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_total, sizeof(uint32_t), hipHostMallocDefault);
     if (e != hipSuccess) {
         prk_destroy(c);
@@ -427,13 +429,15 @@ static void harvest(prk_context *c, int slot) {
     if (!c->pending[slot]) return;
     c->pending[slot] = false;
     if (hipEventSynchronize(c->ev[slot][2]) != hipSuccess) return;
-    float a = 0, b = 0, v = 0;
+    float a = 0, b = 0, v = 0, sp = 0;
     if (hipEventElapsedTime(&a, c->ev[slot][0], c->ev[slot][1]) != hipSuccess) a = 0;
     if (hipEventElapsedTime(&b, c->ev[slot][1], c->ev[slot][2]) != hipSuccess) b = 0;
     if (hipEventElapsedTime(&v, c->ev[slot][1], c->ev[slot][3]) != hipSuccess) v = 0;
+    if (!c->split_span[slot] || hipEventElapsedTime(&sp, c->ev[slot][3], c->ev[slot][4]) != hipSuccess) sp = 0;
     c->stats.sum_ms_bin += a;
     c->stats.sum_ms_raster += b;
     c->stats.sum_ms_vis += v;
+    c->stats.sum_ms_span += sp;
     c->stats.frames_timed += 1;
     if (slot == c->last_slot) {
         c->stats.ms_bin = a;
@@ -445,7 +449,7 @@ int prk_timing_reset(prk_context *c) {
     if (!c) return PRK_ERR_ARG;
     for (int i = 0; i < prk_context::kRing; ++i) c->pending[i] = false;
     c->stats.frames_timed = 0;
-    c->stats.sum_ms_bin = c->stats.sum_ms_raster = c->stats.sum_ms_vis = 0.0;
+    c->stats.sum_ms_bin = c->stats.sum_ms_raster = c->stats.sum_ms_vis = c->stats.sum_ms_span = 0.0;
     if (c->d_prof.p) PRK_TRY(hipMemset(c->d_prof.p, 0, 16 * sizeof(uint64_t)));
     return PRK_OK;
 }
@@ -609,9 +613,10 @@ int prk_flush(prk_context *c, void *stream) {
     PRK_TRY(prk_launch_raster(&fp, modeset, (const uint32_t *)c->d_offs.p, (const uint32_t *)c->d_bins.p,
                               (uint32_t *)c->d_won.p, (uint32_t *)c->d_list.p, (uint32_t *)c->d_nwin.p,
                               (uint32_t *)c->d_wtag.p, c->d_recs.p, c->d_pmap.p, (uint32_t *)c->d_anomaly.p,
-                              c->ev[slot][3], s));
+                              c->ev[slot][3], modeset == prk::MODE_AVX ? c->ev[slot][4] : nullptr, s));
     PRK_TRY(hipEventRecord(c->ev[slot][2], s));
     c->pending[slot] = true;
+    c->split_span[slot] = modeset == prk::MODE_AVX;
     c->last_slot = slot;
     c->frame++;
     c->draws.clear();

@@ -1146,11 +1146,12 @@ static size_t span_lds(const prk::FrameParams *fp) {
 }
 
 // Sweep 1 (k_vis) then the shading: k_span + k_pix for AVX frames, k_shade
-// otherwise; `mid` (optional) is recorded after k_vis.  recs / pmap: the
+// otherwise; `mid` (optional) is recorded after k_vis, `mid2` between k_span
+// and k_pix.  recs / pmap: the
 // span records (64 B per tile pixel) and the per-pixel record map (2 B).
 hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint32_t *offs, const uint32_t *bins,
                              uint32_t *won, uint32_t *list, uint32_t *nwin, uint32_t *wtag, void *recs, void *pmap,
-                             uint32_t *anomaly, hipEvent_t mid, hipStream_t s) {
+                             uint32_t *anomaly, hipEvent_t mid, hipEvent_t mid2, hipStream_t s) {
     const uint32_t ntile = (uint32_t)(fp->tiles_x * fp->tiles_y);
     if (ntile == 0) return hipSuccess;
     const size_t lv = vis_lds(fp), ls = shade_lds(fp), lsp = span_lds(fp);
@@ -1170,6 +1171,7 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
     do {                                                                                                             \
         hipLaunchKernelGGL((prk::k_span<UNI>), dim3(ntile), dim3(64 * prk::kWaves), lsp, s, *fp, offs, bins, list,  \
                            nwin, wtag, rp, mp, anomaly);                                                             \
+        if (mid2) (void)hipEventRecord(mid2, s);                                                                     \
         hipLaunchKernelGGL((prk::k_pix<UNI>), dim3(ntile), dim3(256), 0, s, *fp, nwin, rp, mp);                      \
     } while (0)
     switch (modeset) {

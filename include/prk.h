@@ -104,6 +104,8 @@ typedef struct prk_stats {
                                 anomalies */
     double sum_ms_vis;       /* accumulated: the k_vis (visibility) part
                                 of sum_ms_raster */
+    double sum_ms_span;      /* accumulated: the k_span part (AVX frames:
+                                raster = k_vis + k_span + k_pix) */
 } prk_stats;
 
 typedef struct prk_context prk_context;

@@ -36,10 +36,11 @@ r.synchronize()
 dt = (time.perf_counter() - t0) / steps
 st = r.stats()
 n = max(1, st["frames_timed"])
-print("lib=%s T=%d %dx%d R=%g tile=%s: frame %.3f ms  bin %.3f ms  raster %.3f ms (vis %.3f shade %.3f)  "
+print("lib=%s T=%d %dx%d R=%g tile=%s: frame %.3f ms  bin %.3f ms  raster %.3f ms (vis %.3f shade %.3f [span %.3f])  "
       "entries %d anomalies %d slow_replays %d" % (
           os.path.basename(prk.LIB_PATH), T, W, H, R, tile or "default", dt * 1e3, st["sum_ms_bin"] / n,
           st["sum_ms_raster"] / n, st["sum_ms_vis"] / n, (st["sum_ms_raster"] - st["sum_ms_vis"]) / n,
+          st["sum_ms_span"] / n,
           st["bin_entries"], st["anomalies"], st["slow_replays"]))
 if os.environ.get("PRK_PROF_PRINT"):
     c = r.debug_counters(16)
