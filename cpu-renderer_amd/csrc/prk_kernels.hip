@@ -86,6 +86,9 @@ __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
 #ifndef PRK_PREFETCH
 #define PRK_PREFETCH 1  // single-draw sweeps prefetch the next chunk's triangles
 #endif
+#ifndef PRK_LANE_ROWS
+#define PRK_LANE_ROWS 1  // sweeps: each lane walks its own rows (no row lock step across the wave)
+#endif
 #ifndef PRK_PIXEL_ITEMS
 #define PRK_PIXEL_ITEMS 1  // shading sweep (AVX): one work item per won pixel, not per lane chain
 #endif
@@ -94,8 +97,9 @@ __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
 #endif
 constexpr int kWaves = PRK_WAVES;
 constexpr int kSpanF = 22;  // float fields per span slot
-constexpr int kSpanI = 10;  // int fields per span slot (the row is the sweep's current row)
-enum { SI_XA = 0, SI_XB, SI_LEFT, SI_PRE, SI_TAG, SI_OVF, SI_TEX, SI_MARK, SI_WM0, SI_WM1 };
+constexpr int kSpanI = 11;  // int fields per span slot
+// (the visibility sweep uses the first kSpanIVis int fields only)
+enum { SI_XA = 0, SI_XB, SI_LEFT, SI_PRE, SI_TAG, SI_OVF, SI_MARK, SI_ROW, SI_TEX, SI_WM0, SI_WM1 };
 // AVX float slots
 enum { SF_XOFF = 0, SF_LW, SF_LU, SF_LV, SF_LZ, SF_IW, SF_IU, SF_IV, SF_IZ, SF_LN0, SF_LN1, SF_LN2,
        SF_IN0, SF_IN1, SF_IN2 };
@@ -103,15 +107,16 @@ enum { SF_XOFF = 0, SF_LW, SF_LU, SF_LV, SF_LZ, SF_IW, SF_IU, SF_IV, SF_IZ, SF_L
 enum { SS_Z = 0, SS_IZ, SS_W, SS_U, SS_V, SS_IW, SS_IU, SS_IV, SS_N0, SS_N1, SS_N2, SS_IN0, SS_IN1, SS_IN2,
        SS_C0, SS_C1, SS_C2, SS_C3, SS_IC0, SS_IC1, SS_IC2, SS_IC3 };
 
-template <int NF>
+template <int NF, int NI>
 struct WaveSlotsT {
     float f[NF][64];
-    int32_t i[kSpanI][64];
+    int32_t i[NI][64];
 };
 constexpr int kTagPad = 16;  // k_shade: tags past the tile's last pixel (chunked reads)
 constexpr int kSpanFVis = 9;  // the visibility sweep reads no normals or colours (SF_IZ + 1)
-using VisSlots = WaveSlotsT<kSpanFVis>;
-using ShadeSlots = WaveSlotsT<kSpanF>;
+constexpr int kSpanIVis = 8;  // SI_ROW + 1
+using VisSlots = WaveSlotsT<kSpanFVis, kSpanIVis>;
+using ShadeSlots = WaveSlotsT<kSpanF, kSpanI>;
 
 struct TileCtx {
     int32_t x0, x1, y0, y1, tw;  // tile pixel rectangle [x0,x1) x [y0,y1), LDS row stride tw
@@ -180,7 +185,7 @@ __device__ __forceinline__ int span_setup_avx(const FrameParams &fp, const TileC
     ws.i[SI_XB][lane] = xb;
     ws.i[SI_LEFT][lane] = LeftXa;
     ws.i[SI_TAG][lane] = (int32_t)tag;
-    ws.i[SI_TEX][lane] = texi;
+    if constexpr (SHADE) ws.i[SI_TEX][lane] = texi;
     ws.f[SF_XOFF][lane] = XOffset;
     ws.f[SF_LW][lane] = L.W; ws.f[SF_LU][lane] = L.U; ws.f[SF_LV][lane] = L.V; ws.f[SF_LZ][lane] = L.Z;
     ws.f[SF_IW][lane] = IW; ws.f[SF_IU][lane] = IU; ws.f[SF_IV][lane] = IV; ws.f[SF_IZ][lane] = IZ;
@@ -269,7 +274,7 @@ __device__ __forceinline__ int span_setup_scalar(const FrameParams &fp, const Ti
     ws.i[SI_LEFT][lane] = MinX;
     ws.i[SI_TAG][lane] = (int32_t)tag;
     ws.i[SI_OVF][lane] = ovf ? (Row + 1 - tc.y0) * tc.tw : -1;
-    ws.i[SI_TEX][lane] = texi;
+    if constexpr (SHADE) ws.i[SI_TEX][lane] = texi;
     ws.f[SS_Z][lane] = L.Z + XOffset * IZ;  // 408-412: Current* += XOffset*Increment
     ws.f[SS_IZ][lane] = IZ;
     if constexpr (SHADE) {
@@ -363,7 +368,7 @@ __device__ __forceinline__ void item_avx(const FrameParams &fp, const TileCtx &t
     }
     // The texture of the span's draw (the item may run on any lane).
     TexRec tex;
-    if (SHADE) tex = UNI ? fp.tex0 : fp.texs[ws.i[SI_TEX][s]];
+    if constexpr (SHADE) tex = UNI ? fp.tex0 : fp.texs[ws.i[SI_TEX][s]];
     else { tex.mem = nullptr; tex.w = tex.h = tex.pitch = tex.pad = 0; }
     const int32_t rel = x - LeftXa, i = rel & 7, b = rel >> 3;
     const float IW = ws.f[SF_IW][s], IU = ws.f[SF_IU][s], IV = ws.f[SF_IV][s], IZ = ws.f[SF_IZ][s];
@@ -484,7 +489,7 @@ __device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx
         if (!any) return;
     }
     TexRec tex;
-    if (SHADE && TR::tex) tex = UNI ? fp.tex0 : fp.texs[ws.i[SI_TEX][s]];  // the span's draw, not this lane's
+    if constexpr (SHADE && TR::tex) tex = UNI ? fp.tex0 : fp.texs[ws.i[SI_TEX][s]];  // the span's draw, not this lane's
     else { tex.mem = nullptr; tex.w = tex.h = tex.pitch = tex.pad = 0; }
     float z = ws.f[SS_Z][s];
     const float IZ = ws.f[SS_IZ][s];
@@ -678,17 +683,22 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
         const uint32_t tag = 0xFFFFFFFEu - e;
         if (PRK_DIAG & 4) active = false;
         if (PRK_PROF) { const unsigned long long t1 = PRK_T(); pt[0] += t1 - t0; t0 = t1; }
-        for (int32_t r = ystart; r < tc.y1; ++r) {
+        // PRK_LANE_ROWS: every lane walks its own next row each iteration (the
+        // span's row travels in its slot); else all lanes step row r together.
+        if (PRK_LANE_ROWS && active) active = wk.Row < tc.y1;
+        for (int32_t r = ystart; PRK_LANE_ROWS || r < tc.y1; ++r) {
             int items = 0;
-            if (active && wk.Row == r) {
+            if (active && (PRK_LANE_ROWS || wk.Row == r)) {
+                const int32_t row = wk.Row;
                 const bool paired = wk.begin_row();
                 if (paired) {
                     const Edge &L = wk.S0, &R = wk.S1;
-                    if (M == MODE_AVX) items = span_setup_avx<SHADE>(fp, tc, ws, lane, tag, texi, L, R, r);
-                    else items = span_setup_scalar<M, SHADE>(fp, tc, ws, lane, tag, texi, L, R, r);
+                    if (M == MODE_AVX) items = span_setup_avx<SHADE>(fp, tc, ws, lane, tag, texi, L, R, row);
+                    else items = span_setup_scalar<M, SHADE>(fp, tc, ws, lane, tag, texi, L, R, row);
+                    ws.i[SI_ROW][lane] = row;
                 }
                 wk.end_row(paired);
-                active = wk.Row < wk.MaxY;
+                active = wk.Row < wk.MaxY && (!PRK_LANE_ROWS || wk.Row < tc.y1);
             }
             if (PRK_PROF) { const unsigned long long t1 = PRK_T(); pt[1] += t1 - t0; t0 = t1; }
             const int incl = wave_incl_scan(items, lane);
@@ -715,9 +725,10 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
                 const int it = it0 + lane;
                 if (it < total) {
                     const int s = m - 1, j = it - ws.i[SI_PRE][s];
-                    if constexpr (M == MODE_AVX && SHADE && PRK_PIXEL_ITEMS) item_avx_pixel<UNI>(fp, tc, ws, s, j, r);
-                    else if constexpr (M == MODE_AVX) item_avx<SHADE, UNI>(fp, tc, ws, s, j, r);
-                    else item_scalar<M, SHADE, UNI>(fp, tc, ws, s, r);
+                    const int32_t srow = ws.i[SI_ROW][s];
+                    if constexpr (M == MODE_AVX && SHADE && PRK_PIXEL_ITEMS) item_avx_pixel<UNI>(fp, tc, ws, s, j, srow);
+                    else if constexpr (M == MODE_AVX) item_avx<SHADE, UNI>(fp, tc, ws, s, j, srow);
+                    else item_scalar<M, SHADE, UNI>(fp, tc, ws, s, srow);
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
