@@ -60,6 +60,7 @@ struct Geometry {
 struct Texture {
     uint8_t *mem = nullptr;
     int32_t w = 0, h = 0, pitch = 0;
+    int32_t filter = 0;  // PRK_FILTER_*
 };
 
 int status_of(hipError_t e) {
@@ -309,6 +310,13 @@ int prk_texture_create(prk_context *c, const prk_bitmap *b, int32_t *handle_out)
     return PRK_OK;
 }
 
+int prk_texture_set_filter(prk_context *c, int32_t handle, int32_t filter) {
+    if (!c || handle < 0 || (size_t)handle >= c->texs.size()) return PRK_ERR_ARG;
+    if (filter != PRK_FILTER_NEAREST && filter != PRK_FILTER_BILINEAR) return PRK_ERR_ARG;
+    c->texs[handle].filter = filter;
+    return PRK_OK;
+}
+
 static int upload_array(const float *src, size_t n, const float **dst) {
     *dst = nullptr;
     if (!src) return PRK_OK;
@@ -546,7 +554,7 @@ int prk_flush(prk_context *c, void *stream) {
         texs[i].w = c->texs[i].w;
         texs[i].h = c->texs[i].h;
         texs[i].pitch = c->texs[i].pitch;
-        texs[i].pad = 0;
+        texs[i].filter = c->texs[i].filter;
     }
     PRK_TRY(c->d_draws.ensure(c->draws.size() * sizeof(prk::DrawRec)));
     PRK_TRY(hipMemcpyAsync(c->d_draws.p, c->draws.data(), c->draws.size() * sizeof(prk::DrawRec),

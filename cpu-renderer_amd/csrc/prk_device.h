@@ -40,7 +40,7 @@ struct DrawRec {
 struct TexRec {
     const uint8_t *mem;  // (h+1) rows, last one the zeroed guard row
     int32_t w, h, pitch;
-    int32_t pad;
+    int32_t filter;      // PRK_FILTER_* (bilinear: AVX semantics only, an extension)
 };
 
 struct FrameParams {

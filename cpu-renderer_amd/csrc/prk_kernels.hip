@@ -308,10 +308,44 @@ __device__ __forceinline__ uint32_t texel_avx(const TexRec &tex, float fu, float
     return texel_at(tex, (int32_t)((uint32_t)FX + (uint32_t)FY));
 }
 
-__device__ __forceinline__ uint32_t shade_avx_texel(const FrameParams &fp, uint32_t t, float z, float n0, float n1,
-                                                    float n2, int32_t x, int32_t i, int32_t Row) {
-    const float CA = u8_unit((t >> 24) & 0xFF), CR = u8_unit((t >> 16) & 0xFF);
-    const float CG = u8_unit((t >> 8) & 0xFF), CB = u8_unit(t & 0xFF);
+// A texel as the span's colour lanes (2029-2032): A, R, G, B in [0, 1].
+struct Texel4 { float a, r, g, b; };
+
+__device__ __forceinline__ Texel4 texel4(uint32_t t) {
+    return Texel4{u8_unit((t >> 24) & 0xFF), u8_unit((t >> 16) & 0xFF), u8_unit((t >> 8) & 0xFF), u8_unit(t & 0xFF)};
+}
+
+// Bilinear sampling: an EXTENSION (BASELINE config 4; the reference samples
+// nearest texels only).  Definition = oracle/prk_oracle.c:or_bilinear, op for
+// op: texel centres at +0.5, clamp to the edge, fp32, no contraction.
+__device__ __forceinline__ Texel4 bilinear(const TexRec &tex, float fu, float fv) {
+    const float x = (float)tex.w * fu - 0.5f, y = (float)tex.h * fv - 0.5f;
+    const float fx = floorf(x), fy = floorf(y);
+    const float ax = x - fx, ay = y - fy;
+    const int32_t wm = tex.w - 1, hm = tex.h - 1;
+    const int32_t xi = (int32_t)fx, yi = (int32_t)fy;
+    const int32_t x0 = min(max(xi, 0), wm), x1 = min(max(xi + 1, 0), wm);
+    const int32_t y0 = min(max(yi, 0), hm), y1 = min(max(yi + 1, 0), hm);
+    const uint32_t *r0 = reinterpret_cast<const uint32_t *>(tex.mem + (size_t)y0 * tex.pitch);
+    const uint32_t *r1 = reinterpret_cast<const uint32_t *>(tex.mem + (size_t)y1 * tex.pitch);
+    const Texel4 c00 = texel4(r0[x0]), c10 = texel4(r0[x1]), c01 = texel4(r1[x0]), c11 = texel4(r1[x1]);
+    const float bx = 1.0f - ax, by = 1.0f - ay;
+    Texel4 o;
+    o.a = by * (bx * c00.a + ax * c10.a) + ay * (bx * c01.a + ax * c11.a);
+    o.r = by * (bx * c00.r + ax * c10.r) + ay * (bx * c01.r + ax * c11.r);
+    o.g = by * (bx * c00.g + ax * c10.g) + ay * (bx * c01.g + ax * c11.g);
+    o.b = by * (bx * c00.b + ax * c10.b) + ay * (bx * c01.b + ax * c11.b);
+    return o;
+}
+
+__device__ __forceinline__ Texel4 sample_avx(const TexRec &tex, float fu, float fv) {
+    if (tex.filter == 1) return bilinear(tex, fu, fv);
+    return texel4(texel_avx(tex, fu, fv));
+}
+
+__device__ __forceinline__ uint32_t shade_avx_texel(const FrameParams &fp, const Texel4 &c4, float z, float n0,
+                                                    float n1, float n2, int32_t x, int32_t i, int32_t Row) {
+    const float CA = c4.a, CR = c4.r, CG = c4.g, CB = c4.b;
     // Phong (2040-2128) at UnprojectVertex_8x (102-145).
     const float d = fp.D - z;
     const float Xf = (float)(x - i) + (float)i, Yf = (float)Row + 0.0f;
@@ -350,7 +384,7 @@ __device__ __forceinline__ uint32_t shade_avx_texel(const FrameParams &fp, uint3
 __device__ __forceinline__ uint32_t shade_avx(const FrameParams &fp, const TexRec &tex, float fu, float fv,
                                               float z, float n0, float n1, float n2, int32_t x, int32_t i,
                                               int32_t Row) {
-    return shade_avx_texel(fp, texel_avx(tex, fu, fv), z, n0, n1, n2, x, i, Row);
+    return shade_avx_texel(fp, sample_avx(tex, fu, fv), z, n0, n1, n2, x, i, Row);
 }
 
 // Item j of an AVX span: lane chain i = (xa + j - LeftXa) & 7 from block b.
@@ -369,7 +403,7 @@ __device__ __forceinline__ void item_avx(const FrameParams &fp, const TileCtx &t
     // The texture of the span's draw (the item may run on any lane).
     TexRec tex;
     if constexpr (SHADE) tex = UNI ? fp.tex0 : fp.texs[ws.i[SI_TEX][s]];
-    else { tex.mem = nullptr; tex.w = tex.h = tex.pitch = tex.pad = 0; }
+    else { tex.mem = nullptr; tex.w = tex.h = tex.pitch = tex.filter = 0; }
     const int32_t rel = x - LeftXa, i = rel & 7, b = rel >> 3;
     const float IW = ws.f[SF_IW][s], IU = ws.f[SF_IU][s], IV = ws.f[SF_IV][s], IZ = ws.f[SF_IZ][s];
     const float IW8 = IW * 8.0f, IU8 = IU * 8.0f, IV8 = IV * 8.0f, IZ8 = 8.0f * IZ;
@@ -456,7 +490,7 @@ __device__ __forceinline__ void item_avx_pixel(const FrameParams &fp, const Tile
     const float iw = 1.0f / w;  // 1865-1866
     const float fu = iw * u, fv = iw * v;
     // The texel load goes out before the normal's block steps.
-    const uint32_t t = texel_avx(tex, fu, fv);
+    const Texel4 t = sample_avx(tex, fu, fv);
     const float IN0 = ws.f[SF_IN0][s], IN1 = ws.f[SF_IN1][s], IN2 = ws.f[SF_IN2][s];
     float n0 = ws.f[SF_LN0][s] + o * IN0, n1 = ws.f[SF_LN1][s] + o * IN1, n2 = ws.f[SF_LN2][s] + o * IN2;
     normalize_div(n0, n1, n2);  // 1754
@@ -468,7 +502,7 @@ __device__ __forceinline__ void item_avx_pixel(const FrameParams &fp, const Tile
             n0 = a; n1 = bb; n2 = c;
         }
     }
-    put_winner(fp, x, Row, z, (PRK_DIAG & 16) ? __float_as_uint(fu + fv + n0 + n1 + n2) + t
+    put_winner(fp, x, Row, z, (PRK_DIAG & 16) ? __float_as_uint(fu + fv + n0 + n1 + n2 + t.r)
                                                : shade_avx_texel(fp, t, z, n0, n1, n2, x, i, Row));
 }
 
@@ -490,7 +524,7 @@ __device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx
     }
     TexRec tex;
     if constexpr (SHADE && TR::tex) tex = UNI ? fp.tex0 : fp.texs[ws.i[SI_TEX][s]];  // the span's draw, not this lane's
-    else { tex.mem = nullptr; tex.w = tex.h = tex.pitch = tex.pad = 0; }
+    else { tex.mem = nullptr; tex.w = tex.h = tex.pitch = tex.filter = 0; }
     float z = ws.f[SS_Z][s];
     const float IZ = ws.f[SS_IZ][s];
     float w = 0, u = 0, v = 0, IW = 0, IU = 0, IV = 0, n0 = 0, n1 = 0, n2 = 0, IN0 = 0, IN1 = 0, IN2 = 0;
@@ -1085,7 +1119,7 @@ __global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__r
         }
         const float iw = 1.0f / w;  // 1865-1866
         const float fu = iw * u, fv = iw * v;
-        const uint32_t tx = texel_avx(tex, fu, fv);
+        const Texel4 tx = sample_avx(tex, fu, fv);
         const float IN0 = r3.y, IN1 = r3.z, IN2 = r3.w;
         float n0 = r2.z + o * IN0, n1 = r2.w + o * IN1, n2 = r3.x + o * IN2;
         normalize_div(n0, n1, n2);  // 1754

@@ -49,6 +49,7 @@ _SIGS = {
     "prk_target_upload": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
     "prk_set_camera": (C.c_int, [C.c_void_p, C.POINTER(abi.PrkTransform), C.POINTER(abi.PrkLightData)]),
     "prk_texture_create": (C.c_int, [C.c_void_p, C.POINTER(abi.PrkBitmap), C.POINTER(C.c_int32)]),
+    "prk_texture_set_filter": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     "prk_geometry_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_uint32, C.POINTER(C.c_int32)]),
     "prk_geometry_wrap_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -186,7 +187,14 @@ class Renderer:
         bm = abi.PrkBitmap(texels.ctypes.data, tex.width, tex.height, texels.shape[1] * 4)
         h = C.c_int32(-1)
         _check("prk_texture_create", self._L.prk_texture_create(self._h, C.byref(bm), C.byref(h)))
+        if getattr(tex, "filter", abi.PRK_FILTER_NEAREST) != abi.PRK_FILTER_NEAREST:
+            self.set_filter(h.value, tex.filter)
         return h.value
+
+    def set_filter(self, texture, filt):
+        """Texture sampling: PRK_FILTER_NEAREST (the reference's) or
+        PRK_FILTER_BILINEAR (an extension, AVX semantics only)."""
+        _check("prk_texture_set_filter", self._L.prk_texture_set_filter(self._h, texture, filt))
 
     def geometry(self, vertices, colors=None, normals=None, uvs=None):
         arrs = [None if a is None else np.ascontiguousarray(a, np.float32)
@@ -268,11 +276,18 @@ def render_scene(scene, semantics=abi.PRK_SEM_AVX, phong=True, device=0, tile=No
         r.set_debug(debug)
         r.set_camera(scene.prk_transform(), scene.prk_lights())
         g = r.geometry(scene.vertices, scene.colors, scene.normals, scene.uvs)
-        tex = r.texture(scene.texture) if scene.texture is not None else None
-        if semantics == abi.PRK_SEM_AVX:
-            r.draw_model_optimized(g, scene.tri_count, P=scene.P, bitmap=tex, phong=phong)
-        else:
-            r.draw_model(g, scene.tri_count, P=scene.P, bitmap=tex, phong=phong)
+        draws = scene.draws if scene.draws is not None else [(0, scene.tri_count, scene.texture)]
+        handles = {}
+        for first, count, texture in draws:
+            tex = None
+            if texture is not None:
+                if id(texture) not in handles:
+                    handles[id(texture)] = r.texture(texture)
+                tex = handles[id(texture)]
+            if semantics == abi.PRK_SEM_AVX:
+                r.draw_model_optimized(g, count, first_tri=first, P=scene.P, bitmap=tex, phong=phong)
+            else:
+                r.draw_model(g, count, first_tri=first, P=scene.P, bitmap=tex, phong=phong)
         r.complete_all_work()
         r.synchronize()
         col, zb = r.download()

@@ -30,6 +30,7 @@ class Texture:
     texels: np.ndarray  # uint32 [Height+1, Pitch//4], last row zero
     width: int
     height: int
+    filter: int = abi.PRK_FILTER_NEAREST  # PRK_FILTER_BILINEAR: extension (AVX only)
 
     @property
     def pitch(self):
@@ -51,6 +52,10 @@ class Scene:
     P: tuple = (0.0, 0.0, 0.0)
     name: str = "scene"
     meta: dict = field(default_factory=dict)
+    # Multi-draw scenes: [(first_tri, tri_count, Texture or None), ...] drawn
+    # in order into one frame (one DrawModel* call each); None = one draw of
+    # every triangle with `texture`.
+    draws: Optional[list] = None
 
     @property
     def tri_count(self):
@@ -232,3 +237,158 @@ def slivers(n_tris, width, height, seed=0, textured=True):
     tex = random_texture(rng, 64, 64) if textured else None
     return Scene(width, height, verts, cols, nrm.astype(np.float32), uvs, cam, LIGHTS_ONE, AMBIENT_ONE, tex,
                  name="slivers%d_%dx%d_s%d" % (n, width, height, seed), meta=dict(kind="slivers", seed=seed))
+
+
+def procedural_texture(rng, size, kind):
+    """A 1024^2-style material texture (uint32 ARGB, zeroed guard row):
+    checker / brick / stripes / noise patterns with per-texel noise."""
+    y, x = np.mgrid[0:size, 0:size]
+    base = rng.integers(40, 200, size=3)
+    alt = rng.integers(40, 220, size=3)
+    if kind == 0:    # checker
+        m = ((x // 64) + (y // 64)) & 1
+    elif kind == 1:  # bricks
+        row = y // 48
+        m = (((x + (row & 1) * 64) % 128) < 6) | ((y % 48) < 5)
+    elif kind == 2:  # stripes
+        m = ((x + y) // 40) & 1
+    else:            # blobs
+        m = (np.sin(x / 37.0) * np.cos(y / 23.0)) > 0.2
+    m = m.astype(np.int64)
+    noise = rng.integers(-18, 19, size=(size, size, 3))
+    rgb = np.clip(base[None, None, :] * (1 - m[..., None]) + alt[None, None, :] * m[..., None] + noise, 0, 255)
+    tex = np.zeros((size + 1, size), np.uint32)
+    tex[:size] = ((0xFF << 24) | (rgb[..., 0].astype(np.uint32) << 16) | (rgb[..., 1].astype(np.uint32) << 8)
+                  | rgb[..., 2].astype(np.uint32)).astype(np.uint32)
+    return Texture(tex, size, size)
+
+
+def _grid_quads(p0, du, dv, nu, nv, normal):
+    """nu x nv quads on the parallelogram p0 + s*du + t*dv; each quad maps the
+    whole texture (UVs in [0, 1], as the AVX path's UV mask requires)."""
+    s = np.arange(nu)[:, None]
+    t = np.arange(nv)[None, :]
+    a = p0 + (s[..., None] / nu) * du + (t[..., None] / nv) * dv
+    b = a + du / nu
+    c = b + dv / nv
+    d = a + dv / nv
+    quads = np.stack([a, b, c, d], 2).reshape(-1, 4, 3)
+    tris = np.concatenate([quads[:, [0, 1, 2]], quads[:, [0, 2, 3]]], 0)
+    uv = np.array([[0, 0], [1, 0], [1, 1], [0, 1]], np.float64)
+    tuv = np.concatenate([np.repeat(uv[None, [0, 1, 2]], len(quads), 0), np.repeat(uv[None, [0, 2, 3]], len(quads), 0)], 0)
+    nrm = np.repeat(np.asarray(normal, np.float64)[None, None, :], len(tris), 0).repeat(3, 1)
+    return tris, tuv, nrm
+
+
+def _cylinder(cx, cz, r, y0, y1, n_around, n_up, outward=True):
+    ang = np.linspace(0, 2 * np.pi, n_around + 1)
+    ys = np.linspace(y0, y1, n_up + 1)
+    A, Y = np.meshgrid(ang, ys, indexing="ij")
+    P = np.stack([cx + r * np.cos(A), Y, cz + r * np.sin(A)], -1)
+    N = np.stack([np.cos(A), np.zeros_like(A), np.sin(A)], -1)
+    UV = np.stack([A / (2 * np.pi), (Y - y0) / (y1 - y0)], -1)
+    return _mesh_from_grid(P, N, UV)
+
+
+def _arch(x0, x1, cz, y_base, thickness, n_seg, n_w):
+    """Half-torus-like arch spanning x0..x1 at depth cz (a curved band)."""
+    cx, rad = 0.5 * (x0 + x1), 0.5 * (x1 - x0)
+    ang = np.linspace(0, np.pi, n_seg + 1)
+    w = np.linspace(-thickness, thickness, n_w + 1)
+    A, Wd = np.meshgrid(ang, w, indexing="ij")
+    P = np.stack([cx + rad * np.cos(A), y_base + rad * np.sin(A), cz + Wd], -1)
+    N = np.stack([-np.cos(A), -np.sin(A), np.zeros_like(A)], -1)  # underside faces down/in
+    UV = np.stack([A / np.pi, (Wd + thickness) / (2 * thickness)], -1)
+    return _mesh_from_grid(P, N, UV)
+
+
+def _mesh_from_grid(P, N, UV):
+    """Triangles of a (nu+1) x (nv+1) vertex grid, two per cell, UVs rescaled
+    so that every cell maps the whole texture."""
+    nu, nv = P.shape[0] - 1, P.shape[1] - 1
+    i, j = np.meshgrid(np.arange(nu), np.arange(nv), indexing="ij")
+    i, j = i.ravel(), j.ravel()
+    cells = [(i, j), (i + 1, j), (i + 1, j + 1), (i, j + 1)]
+    cp = [P[a, b] for a, b in cells]
+    cn = [N[a, b] for a, b in cells]
+    uvc = np.array([[0, 0], [1, 0], [1, 1], [0, 1]], np.float64)
+    tris = np.concatenate([np.stack([cp[0], cp[1], cp[2]], 1), np.stack([cp[0], cp[2], cp[3]], 1)], 0)
+    nrm = np.concatenate([np.stack([cn[0], cn[1], cn[2]], 1), np.stack([cn[0], cn[2], cn[3]], 1)], 0)
+    tuv = np.concatenate([np.repeat(uvc[None, [0, 1, 2]], len(i), 0), np.repeat(uvc[None, [0, 2, 3]], len(i), 0)], 0)
+    return tris, tuv, nrm
+
+
+def sponza_like(width=3840, height=2160, seed=0, detail=1.56, tex_size=1024, filt=abi.PRK_FILTER_BILINEAR):
+    """C4 stand-in ("textured Sponza-style scene, ~250k tris", no asset files
+    exist here): a procedural atrium — floor, ceiling, side and back walls, two
+    rows of pillars and arches between them — in 8 materials of one
+    tex_size^2 texture each, drawn as 8 draws (one DrawModelOptimized call per
+    material).  Every triangle is oriented so that the reference's back-face
+    cull (projekt.cpp:3926-3943) keeps the faces toward the camera and drops
+    the rest (pillar backs, arch tops).  `filt`: texture sampling of all 8
+    materials (bilinear is the build's extension, BASELINE config 4)."""
+    rng = np.random.default_rng(seed)
+    cam = default_camera(width, height)
+    D = cam[0]
+    X, Yf, Yc, Z0, Z1 = 6.0, -2.5, 3.5, 3.0, -34.0
+    g = lambda n: max(2, int(round(n * detail)))  # noqa: E731
+    parts = []  # (tris, uv, nrm) per material
+    parts.append(_grid_quads(np.array([-X, Yf, Z0]), np.array([2 * X, 0, 0]), np.array([0, 0, Z1 - Z0]), g(60), g(110), (0, 1, 0)))    # floor
+    parts.append(_grid_quads(np.array([-X, Yc, Z0]), np.array([2 * X, 0, 0]), np.array([0, 0, Z1 - Z0]), g(40), g(80), (0, -1, 0)))   # ceiling
+    parts.append(_grid_quads(np.array([-X, Yf, Z0]), np.array([0, Yc - Yf, 0]), np.array([0, 0, Z1 - Z0]), g(40), g(110), (1, 0, 0)))  # left
+    parts.append(_grid_quads(np.array([X, Yf, Z0]), np.array([0, Yc - Yf, 0]), np.array([0, 0, Z1 - Z0]), g(40), g(110), (-1, 0, 0)))  # right
+    parts.append(_grid_quads(np.array([-X, Yf, Z1]), np.array([2 * X, 0, 0]), np.array([0, Yc - Yf, 0]), g(60), g(40), (0, 0, 1)))    # back
+    cols = []
+    zs = np.linspace(-2.0, -30.0, 8)
+    for side in (-3.5, 3.5):
+        for cz in zs:
+            cols.append(_cylinder(side, cz, 0.45, Yf, 1.5, g(48), g(32)))
+    parts.append(tuple(np.concatenate([c[k] for c in cols], 0) for k in range(3)))  # pillars
+    arches = []
+    for side in (-3.5, 3.5):
+        for a, b in zip(zs[:-1], zs[1:]):
+            # arch between consecutive pillars of one row (spans along z, rotate: swap axes)
+            t, uv, n = _arch(b, a, 0.0, 1.5, 0.4, g(40), g(8))
+            t = t[..., [2, 1, 0]].copy()
+            t[..., 0] += side
+            n = n[..., [2, 1, 0]].copy()
+            arches.append((t, uv, n))
+    parts.append(tuple(np.concatenate([c[k] for c in arches], 0) for k in range(3)))  # arches
+    # cross arches over the nave
+    xarch = [_arch(-3.5, 3.5, cz, 1.5, 0.3, g(64), g(6)) for cz in zs[::2]]
+    parts.append(tuple(np.concatenate([c[k] for c in xarch], 0) for k in range(3)))
+    verts, uvs, nrms, draws = [], [], [], []
+    first = 0
+    textures = [procedural_texture(rng, tex_size, k % 4) for k in range(len(parts))]
+    for k, (tris, tuv, nrm) in enumerate(parts):
+        # Screen rows grow with +y (projekt.cpp:86): build y-up, then flip.
+        tris = tris * np.array([1.0, -1.0, 1.0])
+        nrm = nrm * np.array([1.0, -1.0, 1.0])
+        # Orient: faces whose normal looks at the eye (origin after projection:
+        # distance D - z) keep the reference's front winding (projected
+        # cross.z < 0), the others get the back winding and are culled.
+        eye = np.array([0.0, 0.0, D])
+        cen = tris.mean(1)
+        front = (nrm.mean(1) * (eye - cen)).sum(-1) > 0
+        d = D - tris[..., 2]
+        sx = tris[..., 0] / d
+        sy = tris[..., 1] / d
+        cz = (sx[:, 1] - sx[:, 0]) * (sy[:, 2] - sy[:, 0]) - (sy[:, 1] - sy[:, 0]) * (sx[:, 2] - sx[:, 0])
+        flip = (cz > 0) == front
+        tris[flip, 1], tris[flip, 2] = tris[flip, 2].copy(), tris[flip, 1].copy()
+        tuv[flip, 1], tuv[flip, 2] = tuv[flip, 2].copy(), tuv[flip, 1].copy()
+        nrm[flip, 1], nrm[flip, 2] = nrm[flip, 2].copy(), nrm[flip, 1].copy()
+        textures[k].filter = filt
+        verts.append(tris.reshape(-1, 3))
+        uvs.append(tuv.reshape(-1, 2))
+        nrms.append(nrm.reshape(-1, 3))
+        draws.append((first, len(tris), textures[k]))
+        first += len(tris)
+    V = np.concatenate(verts).astype(np.float32)
+    N = np.concatenate(nrms).astype(np.float32)
+    UV = np.concatenate(uvs).astype(np.float32)
+    C = np.ones((V.shape[0], 4), np.float32)
+    lights = [((0.0, -2.5, -6.0), (0.9, 0.85, 0.7, 1.0)), ((-3.0, -1.0, -20.0), (0.4, 0.5, 0.9, 1.0))]
+    return Scene(width, height, V, C, N, UV, cam, lights, (0.25, 0.25, 0.25, 1.0), None,
+                 name="sponza_like%d_%dx%d" % (V.shape[0] // 3, width, height),
+                 meta=dict(kind="sponza_like", seed=seed), draws=draws)

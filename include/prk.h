@@ -51,6 +51,17 @@ enum prk_semantics {
                             DrawModelOptimized(RenderQueue,...) 3615-3871 */
 };
 
+/* Texture sampling of a texture handle (prk_texture_set_filter).  The
+ * reference samples the nearest texel only (projekt.cpp:1881-2032);
+ * PRK_FILTER_BILINEAR is an EXTENSION of this build for the AVX semantics
+ * (BASELINE config 4) with its own definition: weights from
+ * texel centres at +0.5, clamp to the edge, fp32.  DrawModel (scalar)
+ * draws always sample nearest. */
+enum prk_filter {
+    PRK_FILTER_NEAREST = 0,
+    PRK_FILTER_BILINEAR = 1
+};
+
 /* projective_transform (absent header; fields as used at projekt.cpp:77-90,
  * 122-141, 152-155). */
 typedef struct prk_transform {
@@ -143,6 +154,7 @@ int prk_set_camera(prk_context *ctx, const prk_transform *transform,
 /* Textures.  `bitmap->Memory` is host memory of (Height+1)*Pitch bytes, the
  * last row being the guard row (zero it).  Returns a handle >= 0. */
 int prk_texture_create(prk_context *ctx, const prk_bitmap *bitmap, int32_t *handle_out);
+int prk_texture_set_filter(prk_context *ctx, int32_t handle, int32_t filter);  /* PRK_FILTER_* */
 
 /* Geometry: non-indexed SoA vertex arrays exactly as render_entry_3d_object
  * (projekt.h:2-15): positions v3, colours v4, normals v3, uvs v2, three

@@ -25,7 +25,7 @@ class OrDrawDesc(C.Structure):
     _fields_ = [("Vertices", C.c_void_p), ("Colors", C.c_void_p), ("Normals", C.c_void_p),
                 ("UVs", C.c_void_p), ("TriCount", C.c_uint32), ("TrisPerObject", C.c_uint32),
                 ("P", C.c_float * 3), ("Semantics", C.c_int32), ("Phong", C.c_int32),
-                ("Bitmap", C.POINTER(abi.PrkBitmap)), ("TriIndexBase", C.c_int32)]
+                ("Bitmap", C.POINTER(abi.PrkBitmap)), ("TriIndexBase", C.c_int32), ("Filter", C.c_int32)]
 
 
 class OrTarget(C.Structure):
@@ -57,17 +57,17 @@ def _ptr(a):
 class _Keep:
     """Holds ctypes objects alive for the duration of a call."""
 
-    def __init__(self, scene, semantics, phong, tris_per_object, tri_base=0):
+    def __init__(self, scene, semantics, phong, tris_per_object, tri_base=0, texture="scene"):
         self.arrays = [np.ascontiguousarray(scene.vertices, np.float32),
                        np.ascontiguousarray(scene.colors, np.float32),
                        np.ascontiguousarray(scene.normals, np.float32),
                        np.ascontiguousarray(scene.uvs, np.float32)]
         self.bitmap = None
-        if scene.texture is not None:
-            self.tex = np.ascontiguousarray(scene.texture.texels)
+        texture = scene.texture if texture == "scene" else texture
+        if texture is not None:
+            self.tex = np.ascontiguousarray(texture.texels)
             self.bitmap = abi.PrkBitmap(self.tex.ctypes.data_as(C.c_void_p).value,
-                                        scene.texture.width, scene.texture.height,
-                                        scene.texture.pitch)
+                                        texture.width, texture.height, texture.pitch)
         d = OrDrawDesc()
         d.Vertices, d.Colors, d.Normals, d.UVs = [_ptr(a) for a in self.arrays]
         d.TriCount = scene.tri_count
@@ -78,6 +78,7 @@ class _Keep:
         d.Phong = int(bool(phong))
         d.Bitmap = C.pointer(self.bitmap) if self.bitmap is not None else None
         d.TriIndexBase = tri_base
+        d.Filter = getattr(texture, "filter", abi.PRK_FILTER_NEAREST) if texture is not None else 0
         self.desc = d
         self.transform = scene.prk_transform()
         self.lights = scene.prk_lights()
@@ -92,7 +93,21 @@ def render(scene, semantics=abi.PRK_SEM_AVX, phong=True, tris_per_object=1, thre
     col = np.full((H, W), CLEAR_COLOR, np.uint32) if color is None else np.array(color, np.uint32)
     zb = np.full((H, W), CLEAR_Z, np.float32) if z is None else np.array(z, np.float32)
     win = np.full((H, W), -1, np.int32) if winners else None
-    k = _Keep(scene, semantics, phong, tris_per_object)
+    if scene.draws is not None:  # multi-draw scene: the draws in order, one target
+        tot = [0, 0, 0]
+        for first, count, texture in scene.draws:
+            sub = scene.subset(first, first + count)
+            sub.texture, sub.draws = texture, None
+            _, _, _, st = _render_one(sub, semantics, phong, tris_per_object, threads, col, zb, win, rows,
+                                      tri_base=first)
+            tot = [tot[0] + st["spans"], tot[1] + st["span_pixels"], tot[2] + st["writes"]]
+        return col, zb, win, dict(spans=tot[0], span_pixels=tot[1], writes=tot[2])
+    return _render_one(scene, semantics, phong, tris_per_object, threads, col, zb, win, rows)
+
+
+def _render_one(scene, semantics, phong, tris_per_object, threads, col, zb, win, rows, tri_base=0):
+    W, H = scene.width, scene.height
+    k = _Keep(scene, semantics, phong, tris_per_object, tri_base=tri_base)
     tg = OrTarget(_ptr(col), W * 4, _ptr(zb), W, H, _ptr(win))
     stats = (C.c_uint64 * 3)()
     L = lib()

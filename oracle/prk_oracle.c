@@ -132,6 +132,7 @@ typedef struct or_ctx {
     int32_t RowLo, RowHi;      /* band filter [RowLo, RowHi) */
     int32_t BandH, BandMod, BandRem; /* interleaved bands: draw row r iff (r/BandH)%BandMod==BandRem */
     int Phong;
+    int Filter;                /* PRK_FILTER_*: texture sampling of the AVX span */
     uint64_t Spans, SpanPixels, Writes;
 } or_ctx;
 
@@ -329,6 +330,41 @@ static inline uint32_t or_texel(const prk_bitmap *B, int32_t off)
 }
 
 /* ------------------------------------------------------------------ */
+/* Bilinear texture sampling — an EXTENSION of this build (BASELINE    */
+/* config 4 asks for it; the reference samples nearest texels only,    */
+/* projekt.cpp:1881-2032), so it has no reference to match: this is    */
+/* its definition, restated op for op by the GPU kernel.  Texel        */
+/* centres at +0.5, clamp to the edge, fp32, no FMA contraction.        */
+/* ------------------------------------------------------------------ */
+static inline float or_u8(uint32_t t, int sh) { return (float)((t >> sh) & 0xFF) / 255.0f; }
+
+static void or_bilinear(const prk_bitmap *B, float FU, float FV, float *CA, float *CR, float *CG, float *CB)
+{
+    const float x = (float)B->Width * FU - 0.5f, y = (float)B->Height * FV - 0.5f;
+    const float fx = floorf(x), fy = floorf(y);
+    const float ax = x - fx, ay = y - fy;
+    int32_t x0 = (int32_t)fx, y0 = (int32_t)fy, x1 = x0 + 1, y1 = y0 + 1;
+    const int32_t wm = B->Width - 1, hm = B->Height - 1;
+    x0 = x0 < 0 ? 0 : (x0 > wm ? wm : x0); x1 = x1 < 0 ? 0 : (x1 > wm ? wm : x1);
+    y0 = y0 < 0 ? 0 : (y0 > hm ? hm : y0); y1 = y1 < 0 ? 0 : (y1 > hm ? hm : y1);
+    const uint8_t *m = (const uint8_t *)B->Memory;
+    uint32_t t00, t10, t01, t11;
+    memcpy(&t00, m + (size_t)y0 * B->Pitch + 4 * (size_t)x0, 4);
+    memcpy(&t10, m + (size_t)y0 * B->Pitch + 4 * (size_t)x1, 4);
+    memcpy(&t01, m + (size_t)y1 * B->Pitch + 4 * (size_t)x0, 4);
+    memcpy(&t11, m + (size_t)y1 * B->Pitch + 4 * (size_t)x1, 4);
+    const float bx = 1.0f - ax, by = 1.0f - ay;
+    float out[4];
+    const int sh[4] = {24, 16, 8, 0}; /* A R G B */
+    for (int c = 0; c < 4; ++c) {
+        const float top = bx * or_u8(t00, sh[c]) + ax * or_u8(t10, sh[c]);
+        const float bot = bx * or_u8(t01, sh[c]) + ax * or_u8(t11, sh[c]);
+        out[c] = by * top + ay * bot;
+    }
+    *CA = out[0]; *CR = out[1]; *CG = out[2]; *CB = out[3];
+}
+
+/* ------------------------------------------------------------------ */
 /* FillLineOptimized (projekt.cpp:1492-2320), one lane at a time.      */
 /* The non-Phong branch (2285-2316) is out of scope (prk rejects it).  */
 /* ------------------------------------------------------------------ */
@@ -412,14 +448,19 @@ static void or_fill_line_optimized(or_ctx *X_, const or_edge *L, const or_edge *
             int Mask = (FU >= 0.0f) && (FU <= 1.0f) && (FV >= 0.0f) && (FV <= 1.0f) && Clip[i];
             if (!Mask) continue;
             float zb = X_->Z[(size_t)Row * W + X + i];
-            int32_t FX = (int32_t)((uint32_t)or_cvtt_s32(TCX) << 2);
-            int32_t FY = or_mul16_trick(or_cvtt_s32(TCY), Bm->Pitch);
-            int32_t Off = (int32_t)((uint32_t)FX + (uint32_t)FY);
-            uint32_t Tx = or_texel(Bm, Off);
-            float CA = (float)((Tx >> 24) & 0xFF) / 255.0f;
-            float CR = (float)((Tx >> 16) & 0xFF) / 255.0f;
-            float CG = (float)((Tx >> 8) & 0xFF) / 255.0f;
-            float CB = (float)((Tx >> 0) & 0xFF) / 255.0f;
+            float CA, CR, CG, CB;
+            if (X_->Filter == PRK_FILTER_BILINEAR) {
+                or_bilinear(Bm, FU, FV, &CA, &CR, &CG, &CB);
+            } else {
+                int32_t FX = (int32_t)((uint32_t)or_cvtt_s32(TCX) << 2);
+                int32_t FY = or_mul16_trick(or_cvtt_s32(TCY), Bm->Pitch);
+                int32_t Off = (int32_t)((uint32_t)FX + (uint32_t)FY);
+                uint32_t Tx = or_texel(Bm, Off);
+                CA = (float)((Tx >> 24) & 0xFF) / 255.0f;
+                CR = (float)((Tx >> 16) & 0xFF) / 255.0f;
+                CG = (float)((Tx >> 8) & 0xFF) / 255.0f;
+                CB = (float)((Tx >> 0) & 0xFF) / 255.0f;
+            }
 
             /* Phong (2040-2128) with UnprojectVertex_8x (102-145). */
             float d = T->DistanceAboveTarget - Zl[i];
@@ -747,6 +788,7 @@ typedef struct or_draw_desc {
     int32_t Phong;
     const prk_bitmap *Bitmap; /* host memory with guard row, or NULL */
     int32_t TriIndexBase;     /* winner id of triangle 0 */
+    int32_t Filter;           /* PRK_FILTER_* (AVX semantics; extension) */
 } or_draw_desc;
 
 typedef struct or_target {
@@ -793,7 +835,7 @@ static int or_draw_filtered(const or_draw_desc *D, const or_target *Tg, const pr
     X_.T = T; X_.Lights = Lights; X_.Bitmap = D->Bitmap;
     X_.Color = Tg->Color; X_.Pitch = Tg->Pitch; X_.Z = Tg->Z;
     X_.Width = Tg->Width; X_.Height = Tg->Height; X_.Winners = Tg->Winners;
-    X_.RowLo = row_lo; X_.RowHi = row_hi; X_.Phong = D->Phong;
+    X_.RowLo = row_lo; X_.RowHi = row_hi; X_.Phong = D->Phong; X_.Filter = D->Filter;
     X_.BandH = band_h; X_.BandMod = band_mod; X_.BandRem = band_rem;
     or_span_fn Span = D->Semantics == PRK_SEM_AVX ? or_fill_line_optimized : or_fill_line_scalar;
     for (uint32_t t0 = 0; t0 < D->TriCount; t0 += per) {

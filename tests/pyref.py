@@ -89,6 +89,27 @@ def texel(tex, off):
     return int(flat[off:off + 4].view(np.uint32)[0])
 
 
+def bilinear(tex, fu, fv):
+    """The build's bilinear extension (no reference): centres at +0.5,
+    clamp to edge, fp32.  Returns [R, G, B, A] in [0, 1]."""
+    x = f32(tex.width) * fu - f32(0.5)
+    y = f32(tex.height) * fv - f32(0.5)
+    fx, fy = f32(np.floor(x)), f32(np.floor(y))
+    ax, ay = x - fx, y - fy
+    x0, y0 = int(fx), int(fy)
+    xs = [min(max(x0, 0), tex.width - 1), min(max(x0 + 1, 0), tex.width - 1)]
+    ys = [min(max(y0, 0), tex.height - 1), min(max(y0 + 1, 0), tex.height - 1)]
+    rows = tex.texels
+    bx, by = f32(1) - ax, f32(1) - ay
+    out = []
+    for sh in (16, 8, 0, 24):
+        c = [[f32((int(rows[yy, xx]) >> sh) & 255) / f32(255) for xx in xs] for yy in ys]
+        top = bx * c[0][0] + ax * c[0][1]
+        bot = bx * c[1][0] + ax * c[1][1]
+        out.append(by * top + ay * bot)
+    return out
+
+
 class Ctx:
     def __init__(self, scene, semantics, phong, color=None, z=None):
         self.s = scene
@@ -323,9 +344,12 @@ def span_avx(ctx, t, L, R, row):
             fy = mul16(cvtt(f32(tx.height) * fv) & 0xFFFFFFFF, tx.pitch) & 0xFFFFFFFF
             off = (fx + fy) & 0xFFFFFFFF
             off = off - (1 << 32) if off & 0x80000000 else off
-            tv = texel(tx, off)
-            C = [f32((tv >> 16) & 255) / f32(255), f32((tv >> 8) & 255) / f32(255), f32(tv & 255) / f32(255),
-                 f32((tv >> 24) & 255) / f32(255)]
+            if getattr(tx, "filter", 0) == 1:
+                C = bilinear(tx, fu, fv)
+            else:
+                tv = texel(tx, off)
+                C = [f32((tv >> 16) & 255) / f32(255), f32((tv >> 8) & 255) / f32(255), f32(tv & 255) / f32(255),
+                     f32((tv >> 24) & 255) / f32(255)]
             d = ctx.D - z
             X0 = x - i
             ax = ((f32(X0) + f32(i)) - ctx.cx) * (f32(1) / ctx.M2P)

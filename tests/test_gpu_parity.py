@@ -257,3 +257,47 @@ def test_sliver_x_ties(gpu, semantics, phong, textured):
     g, o = run_both(s, semantics=semantics, phong=phong, exact_color=semantics == abi.PRK_SEM_AVX)
     assert (g[2] >= 0).sum() > 10000
     assert g[3]["slow_replays"] > 0 and g[3]["anomalies"] == 0
+
+
+# ---- BASELINE configs as parity cases ----------------------
+
+def test_c2_bunny_standin_1080p(gpu):
+    """C2: ~70k-triangle closed displaced sphere (bunny stand-in), 1920x1080,
+    untextured Phong -> scalar DrawModel semantics."""
+    s = scenes.displaced_sphere(70000, 1920, 1080, seed=3)
+    g, o = run_both(s, semantics=abi.PRK_SEM_SCALAR, phong=True, threads=16, exact_color=False)
+    assert (g[2] >= 0).sum() > 100000
+
+
+def test_c3a_gouraud_4096_1m(gpu):
+    """C3a: 1M triangles at 4096^2, colour interpolation only (scalar Gouraud)."""
+    s = scenes.random_soup(1_000_000, 4096, 4096, radius=16, seed=2025, textured=False)
+    run_both(s, semantics=abi.PRK_SEM_SCALAR, phong=False, threads=16)
+
+
+@pytest.mark.parametrize("filt", [abi.PRK_FILTER_NEAREST, abi.PRK_FILTER_BILINEAR])
+def test_c4_sponza_like_4k(gpu, filt):
+    """C4: Sponza-style atrium (~250k triangles, 8 material draws of 1024^2
+    textures) at 3840x2160, Phong; nearest = the reference's sampling,
+    bilinear = the build's extension (defined by the oracle's restatement)."""
+    s = scenes.sponza_like(3840, 2160, seed=1, filt=filt)
+    g, o = run_both(s, threads=16)
+    assert (g[2] >= 0).mean() > 0.95
+
+
+def test_bilinear_soups_mixed_filters(gpu):
+    """Bilinear and nearest textures in one frame (multi-draw, mixed samplers)."""
+    s = scenes.random_soup(6000, 512, 384, radius=24, seed=11, tex_size=64)
+    t2 = scenes.Texture(s.texture.texels.copy(), 64, 64, abi.PRK_FILTER_BILINEAR)
+    s.draws = [(0, 3000, s.texture), (3000, 3000, t2)]
+    run_both(s)
+
+
+def test_c5_8192_two_bands(gpu):
+    """C5 geometry (1M triangles, offsets +-32 px, 8192^2) rendered as two row
+    bands (what two ranks draw before the gather) equals the full-frame oracle."""
+    s = scenes.random_soup(1_000_000, 8192, 8192, radius=32, seed=5)
+    oc, oz, ow, _ = O.render(s, threads=16)
+    for r0, r1 in ((0, 4096), (4096, 8192)):
+        gc, gz, gw, _ = prk.render_scene(s, rows=(r0, r1))
+        compare((gc, gz, gw, None), (oc[r0:r1], oz[r0:r1], ow[r0:r1], None), label="band %d-%d" % (r0, r1))

@@ -200,3 +200,41 @@ def test_golden_fixtures(path):
 
 def test_golden_fixtures_present():
     assert len(GOLDEN) >= 8
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_two_restatements_agree_bilinear(seed):
+    """The bilinear extension (no reference: BASELINE config 4) is defined by
+    oracle/prk_oracle.c:or_bilinear; tests/pyref.py restates it separately."""
+    s = scenes.random_soup(40, 96, 64, radius=14, seed=seed, tex_size=16)
+    s.texture.filter = abi.PRK_FILTER_BILINEAR
+    o = O.render(s)
+    p = pyref.render(s, abi.PRK_SEM_AVX, True)
+    assert same(o, p)
+    s.texture.filter = abi.PRK_FILTER_NEAREST
+    n = O.render(s)
+    assert (n[2] == o[2]).all() and (n[1].view(np.uint32) == o[1].view(np.uint32)).all()  # same coverage / z
+    assert (n[0] != o[0]).any()  # but a filtered colour
+
+
+def test_bilinear_known_answer():
+    """A 2x2 texture sampled at its centre is the mean of the four texels;
+    at a texel centre it is that texel (weights exactly 0/1)."""
+    tex = np.zeros((3, 2), np.uint32)
+    tex[0] = [0xFF000000, 0xFFFF0000]
+    tex[1] = [0xFF00FF00, 0xFF0000FF]
+    t = scenes.Texture(tex, 2, 2, abi.PRK_FILTER_BILINEAR)
+    c = pyref.bilinear(t, np.float32(0.5), np.float32(0.5))
+    assert [float(v) for v in c] == [0.25, 0.25, 0.25, 1.0]  # R, G, B, A
+    c = pyref.bilinear(t, np.float32(0.25), np.float32(0.25))
+    assert [float(v) for v in c] == [0.0, 0.0, 0.0, 1.0]
+
+
+def test_sponza_like_multi_draw_oracle():
+    """C4 stand-in: 8 material draws into one frame; the chained oracle draws
+    equal one oracle call per draw on the running target."""
+    s = scenes.sponza_like(320, 192, tex_size=64, detail=0.4)
+    assert len(s.draws) == 8 and s.tri_count > 10000
+    c, z, w, _ = O.render(s, threads=4)
+    assert (w >= 0).mean() > 0.9
+    assert len(np.unique(w[w >= 0])) > 1000
