@@ -117,7 +117,9 @@ def main():
     row0, row1 = band_rows(rank, world, H)
     rows = row1 - row0
 
-    color = torch.empty((rows, W), dtype=torch.int32, device=dev)
+    frame = torch.empty((H, W), dtype=torch.int32, device=dev) if (world > 1 and rank == 0) else None
+    # rank 0 renders its band straight into its slice of the gathered frame
+    color = frame[row0:row1] if frame is not None else torch.empty((rows, W), dtype=torch.int32, device=dev)
     zbuf = torch.empty((rows, W), dtype=torch.float32, device=dev)
     r = prk.Renderer(dev)
     r.target_bind(color.data_ptr(), W * 4, zbuf.data_ptr(), W, H, row0, row1)
@@ -129,7 +131,6 @@ def main():
     tex = r.texture(scene.texture)
     stream = torch.cuda.current_stream().cuda_stream
     from prk import dist as pdist
-    frame = torch.empty((H, W), dtype=torch.int32, device=dev) if (world > 1 and rank == 0) else None
     zmin = -float(np.finfo(np.float32).max)
 
     def step():

@@ -19,26 +19,28 @@ def max_band_rows(world, height):
 def gather_strips(dist, strip, rank, world, height, out=None):
     """Gather every rank's [rows_r, W] strip into rank 0's [H, W] frame.
 
-    Strips are padded to the largest band so one all_gather_into_tensor
-    moves them (one message per peer over xGMI); rank 0 then drops the
-    padding.  Returns the full frame on rank 0, None elsewhere."""
+    Point to point: every rank r > 0 sends its strip to rank 0, which
+    receives it straight into its slice of the frame (one message per peer,
+    each on its own xGMI link; no padding, no all-gather of the whole frame
+    to every rank).  Rank 0's own strip is copied unless it already is that
+    slice (bench.py renders rank 0's band in place).  Returns the frame on
+    rank 0, None elsewhere."""
     import torch
 
     W = strip.shape[1]
-    rows = strip.shape[0]
-    mr = max_band_rows(world, height)
-    if rows == mr:
-        send = strip.contiguous()
+    if rank == 0:
+        if out is None:
+            out = torch.empty((height, W), dtype=strip.dtype, device=strip.device)
+        a, b = band_rows(0, world, height)
+        if out[a:b].data_ptr() != strip.data_ptr():
+            out[a:b].copy_(strip)
+        ops = []
+        for r in range(1, world):
+            a, b = band_rows(r, world, height)
+            ops.append(dist.P2POp(dist.irecv, out[a:b], r))
     else:
-        send = torch.zeros((mr, W), dtype=strip.dtype, device=strip.device)
-        send[:rows] = strip
-    recv = torch.empty((world * mr, W), dtype=strip.dtype, device=strip.device)
-    dist.all_gather_into_tensor(recv, send)
-    if rank != 0:
-        return None
-    if out is None:
-        out = torch.empty((height, W), dtype=strip.dtype, device=strip.device)
-    for r in range(world):
-        a, b = band_rows(r, world, height)
-        out[a:b] = recv[r * mr: r * mr + (b - a)]
-    return out
+        ops = [dist.P2POp(dist.isend, strip.contiguous(), 0)]
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return out if rank == 0 else None
