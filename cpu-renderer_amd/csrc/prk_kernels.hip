@@ -89,6 +89,9 @@ __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
 #ifndef PRK_LANE_ROWS
 #define PRK_LANE_ROWS 1  // sweeps: each lane walks its own rows (no row lock step across the wave)
 #endif
+#ifndef PRK_VIS_GROUP
+#define PRK_VIS_GROUP 2  // visibility items: G consecutive pixels each (0: one lane chain each)
+#endif
 #ifndef PRK_PIXEL_ITEMS
 #define PRK_PIXEL_ITEMS 1  // shading sweep (AVX): one work item per won pixel, not per lane chain
 #endif
@@ -218,6 +221,10 @@ __device__ __forceinline__ int span_setup_avx(const FrameParams &fp, const TileC
         ws.i[SI_WM1][lane] = (int32_t)(uint32_t)(wm >> 32);
         return won;
 #endif
+    }
+    if constexpr (!SHADE && PRK_VIS_GROUP > 0) {
+        constexpr int G = PRK_VIS_GROUP > 0 ? PRK_VIS_GROUP : 1;
+        return (xb - xa + G - 1) / G;
     }
     return min(8, xb - xa);
 }
@@ -450,6 +457,42 @@ __device__ __forceinline__ void item_avx(const FrameParams &fp, const TileCtx &t
             }
         }
         z = z + IZ8; w = w + IW8; u = u + IU8; v = v + IV8;
+    }
+}
+
+// Visibility item j of an AVX span (PRK_VIS_GROUP = G > 0): the G consecutive
+// pixels xa + G*j ... of the span, each evaluated from its own lane chain
+// (lane init + b block steps, the recurrence item_avx walks), so one item's
+// slot reads and item->span mapping serve G fragments.
+template <class WS>
+__device__ __forceinline__ void item_vis_group(const TileCtx &tc, const WS &ws, int s, int j, int32_t Row) {
+    constexpr int G = PRK_VIS_GROUP > 0 ? PRK_VIS_GROUP : 1;
+    const int32_t xa = ws.i[SI_XA][s], xb = ws.i[SI_XB][s], LeftXa = ws.i[SI_LEFT][s];
+    const uint32_t tag = (uint32_t)ws.i[SI_TAG][s];
+    const int rowoff = (Row - tc.y0) * tc.tw - tc.x0;
+    const float IW = ws.f[SF_IW][s], IU = ws.f[SF_IU][s], IV = ws.f[SF_IV][s], IZ = ws.f[SF_IZ][s];
+    const float IW8 = IW * 8.0f, IU8 = IU * 8.0f, IV8 = IV * 8.0f, IZ8 = 8.0f * IZ;
+    const float XO = ws.f[SF_XOFF][s], LW = ws.f[SF_LW][s], LU = ws.f[SF_LU][s], LV = ws.f[SF_LV][s];
+    const float LZ = ws.f[SF_LZ][s];
+    const int32_t x0 = xa + G * j;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int32_t x = x0 + g;
+        if (x < xb) {
+            const int32_t rel = x - LeftXa, i = rel & 7, b = rel >> 3;
+            const float o = XO + (float)i;  // lane init (XOffset + i)*inc, 1712-1835
+            float w = LW + o * IW, u = LU + o * IU, v = LV + o * IV, z = LZ + o * IZ;
+            for (int32_t k = 0; k < b; ++k) { z = z + IZ8; w = w + IW8; u = u + IU8; v = v + IV8; }  // 2262-2282
+            const int p = rowoff + x;
+            // A key not above the pixel's current maximum cannot change it,
+            // whatever the UV mask says: skip the 1/w and the mask.
+            const unsigned long long k = make_key(z, tag);
+            if (!PRK_ZPRE || k > tc.key[p]) {
+                const float iw = 1.0f / w;  // 1865-1866
+                const float fu = iw * u, fv = iw * v;
+                if (fu >= 0.0f && fu <= 1.0f && fv >= 0.0f && fv <= 1.0f && z == z) atomicMax(&tc.key[p], k);
+            }
+        }
     }
 }
 
@@ -761,6 +804,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
                     const int s = m - 1, j = it - ws.i[SI_PRE][s];
                     const int32_t srow = ws.i[SI_ROW][s];
                     if constexpr (M == MODE_AVX && SHADE && PRK_PIXEL_ITEMS) item_avx_pixel<UNI>(fp, tc, ws, s, j, srow);
+                    else if constexpr (M == MODE_AVX && !SHADE && PRK_VIS_GROUP > 0) item_vis_group(tc, ws, s, j, srow);
                     else if constexpr (M == MODE_AVX) item_avx<SHADE, UNI>(fp, tc, ws, s, j, srow);
                     else item_scalar<M, SHADE, UNI>(fp, tc, ws, s, srow);
                 }
