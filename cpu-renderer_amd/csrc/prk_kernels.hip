@@ -858,14 +858,17 @@ template <int MODESET, bool UNI>
 __global__ void __launch_bounds__(64 * kWaves, PRK_VIS_MIN_WAVES)
     k_vis(FrameParams fp, const uint32_t *__restrict__ offs, const uint32_t *__restrict__ bins,
           uint8_t *__restrict__ won, uint32_t *__restrict__ list, uint32_t *__restrict__ nwin_out,
-          uint32_t *__restrict__ wtag, uint32_t *__restrict__ anomaly) {
+          uint32_t *__restrict__ wtag, uint32_t *__restrict__ slist, uint32_t *__restrict__ nwin_slice,
+          uint32_t *__restrict__ anomaly) {
     extern __shared__ unsigned long long lds[];
     const int ntile = fp.tiles_x * fp.tiles_y;
     const int t = blockIdx.x;
     if (t >= ntile) return;
     const uint32_t b0 = offs[t], b1 = offs[t + 1];
+    const int S = fp.span_split;
     if (b0 == b1) {  // no triangle touches this tile: leave it untouched
         if (threadIdx.x == 0) nwin_out[t] = 0;
+        if (threadIdx.x < S) nwin_slice[t * S + threadIdx.x] = 0;
         return;
     }
     const uint32_t n = b1 - b0;
@@ -903,7 +906,8 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_VIS_MIN_WAVES)
     for (int p = threadIdx.x; p < npx; p += blockDim.x) {
         const uint32_t low = (uint32_t)tc.key[p];
         tags_out[p] = low;
-        if (low != 0xFFFFFFFFu) won[b0 + (0xFFFFFFFEu - low)] = 1;
+        // flag (entry, row slice): k_span walks each slice separately
+        if (low != 0xFFFFFFFFu) won[(size_t)(b0 + (0xFFFFFFFEu - low)) * S + (p >> fp.tile_w_log2) / fp.slice_h] = 1;
     }
     // Debug builds also export the winning triangle map.
     if (fp.winners) {
@@ -917,16 +921,29 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_VIS_MIN_WAVES)
     }
     __threadfence_block();
     __syncthreads();
-    uint32_t nwin = 0;
-    for (uint32_t base = 0; base < n; base += blockDim.x) {
-        const uint32_t i = base + threadIdx.x;
-        const uint32_t f = (i < n && won[b0 + i]) ? 1u : 0u;
-        uint32_t tot;
-        const uint32_t pos = block_excl_scan(f, scratch, tot);
-        if (f) list[b0 + nwin + pos] = i;
-        nwin += tot;
+    // Entries that won in the tile (list) and in each row slice (slist).
+    for (int sl = -1; sl < S; ++sl) {
+        uint32_t nwin = 0;
+        uint32_t *out = sl < 0 ? list + b0 : slist + (size_t)b0 * S + (size_t)sl * n;
+        for (uint32_t base = 0; base < n; base += blockDim.x) {
+            const uint32_t i = base + threadIdx.x;
+            uint32_t f = 0;
+            if (i < n) {
+                const uint8_t *w = won + (size_t)(b0 + i) * S;
+                if (sl >= 0) f = w[sl];
+                else for (int k = 0; k < S; ++k) f |= w[k];
+            }
+            f = f ? 1u : 0u;
+            uint32_t tot;
+            const uint32_t pos = block_excl_scan(f, scratch, tot);
+            if (f) out[nwin + pos] = i;
+            nwin += tot;
+        }
+        if (threadIdx.x == 0) {
+            if (sl < 0) nwin_out[t] = (PRK_DIAG & 1) ? 0u : nwin;
+            else nwin_slice[t * S + sl] = (PRK_DIAG & 1) ? 0u : nwin;
+        }
     }
-    if (threadIdx.x == 0) nwin_out[t] = (PRK_DIAG & 1) ? 0u : nwin;
 }
 
 // Shading (sweep 2), one workgroup per tile: re-walk only the entries that
@@ -1054,24 +1071,37 @@ __device__ __forceinline__ void span_record(const FrameParams &fp, const TileCtx
 template <bool UNI>
 __global__ void __launch_bounds__(64 * kWaves, PRK_SPAN_MIN_WAVES)
     k_span(FrameParams fp, const uint32_t *__restrict__ offs, const uint32_t *__restrict__ bins,
-           const uint32_t *__restrict__ list, const uint32_t *__restrict__ nwin_in,
-           const uint32_t *__restrict__ wtag, SpanRec *__restrict__ recs, uint16_t *__restrict__ pmap,
-           uint32_t *__restrict__ anomaly) {
+           const uint32_t *__restrict__ slist, const uint32_t *__restrict__ nwin_slice,
+           const uint32_t *__restrict__ nwin_tile, const uint32_t *__restrict__ wtag, SpanRec *__restrict__ recs,
+           uint16_t *__restrict__ pmap, uint32_t *__restrict__ anomaly) {
+    // One workgroup per (tile, row slice): the slice's rows only, so every
+    // walk covers tile_h / span_split rows (fewer idle lanes per row step).
     constexpr int M = MODE_AVX;
     extern __shared__ unsigned long long lds[];
     const int ntile = fp.tiles_x * fp.tiles_y;
-    const int t = blockIdx.x;
+    const int S = fp.span_split;
+    const int t = blockIdx.x / S, sl = blockIdx.x - t * S;
     if (t >= ntile) return;
-    const uint32_t nwin = nwin_in[t];
-    if (nwin == 0) return;
-    const uint32_t b0 = offs[t];
+    if (nwin_tile[t] == 0) return;  // k_pix skips the whole tile
+    const uint32_t nwin = nwin_slice[blockIdx.x];
+    if (nwin == 0) {  // no winner in this slice: k_pix still reads its map
+        uint16_t *mo = pmap + (size_t)t * fp.tile_w * fp.tile_h + (size_t)sl * fp.tile_w * fp.slice_h;
+        for (int p = threadIdx.x; p < fp.tile_w * fp.slice_h; p += blockDim.x) mo[p] = (uint16_t)kNoRec;
+        return;
+    }
+    const uint32_t b0 = offs[t], n = offs[t + 1] - b0;
+    const uint32_t *list = slist + (size_t)b0 * S + (size_t)sl * n - b0;  // list[b0 + i]: the slice's i-th entry
     TileCtx tc = tile_ctx(fp, t);
-    const int npx = fp.tile_w * fp.tile_h;
+    const int npx = fp.tile_w * fp.slice_h;  // this slice's pixels
+    const int pbase = sl * npx;              // its first pixel within the tile
+    tc.y0 += sl * fp.slice_h;
+    tc.y1 = min(tc.y1, tc.y0 + fp.slice_h);
     uint32_t *tags = reinterpret_cast<uint32_t *>(lds);
     uint16_t *map = reinterpret_cast<uint16_t *>(tags + npx + kTagPad);
     uint32_t *count = reinterpret_cast<uint32_t *>(map + ((npx + 1) & ~1));
     tc.tags = tags;
-    const uint32_t *tags_in = wtag + (size_t)t * npx;
+    const size_t tpx = (size_t)t * fp.tile_w * fp.tile_h + pbase;
+    const uint32_t *tags_in = wtag + tpx;
     for (int p = threadIdx.x; p < npx; p += blockDim.x) {
         tags[p] = tags_in[p];
         map[p] = (uint16_t)kNoRec;
@@ -1079,7 +1109,7 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_SPAN_MIN_WAVES)
     if (threadIdx.x < kTagPad) tags[npx + threadIdx.x] = 0xFFFFFFFFu;  // chunked reads run past the end
     if (threadIdx.x == 0) *count = 0;
     __syncthreads();
-    SpanRec *trecs = recs + (size_t)t * npx;
+    SpanRec *trecs = recs + tpx;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t base = wave * 64; base < nwin; base += 64 * kWaves) {
         const uint32_t i = base + lane;
@@ -1127,8 +1157,11 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_SPAN_MIN_WAVES)
         }
     }
     __syncthreads();
-    uint16_t *map_out = pmap + (size_t)t * npx;
-    for (int p = threadIdx.x; p < npx; p += blockDim.x) map_out[p] = map[p];
+    uint16_t *map_out = pmap + tpx;  // tile-relative record indices for k_pix
+    for (int p = threadIdx.x; p < npx; p += blockDim.x) {
+        const uint32_t m = map[p];
+        map_out[p] = (uint16_t)(m == kNoRec ? kNoRec : m + (uint32_t)pbase);
+    }
 }
 
 // k_pix: shade the won pixels of one tile from their span records.
@@ -1181,16 +1214,16 @@ __global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__r
 
 // Explicit instantiations used by the host.
 #define PRK_VIS_ARGS FrameParams, const uint32_t *, const uint32_t *, uint8_t *, uint32_t *, uint32_t *, uint32_t *, \
-                     uint32_t *
+                     uint32_t *, uint32_t *, uint32_t *
 #define PRK_SHADE_ARGS FrameParams, const uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *, \
                        const uint32_t *, uint32_t *
 #define PRK_INST(MS, UNI)                                  \
     template __global__ void k_vis<MS, UNI>(PRK_VIS_ARGS); \
     template __global__ void k_shade<MS, UNI>(PRK_SHADE_ARGS);
-template __global__ void k_span<false>(FrameParams, const uint32_t *, const uint32_t *, const uint32_t *,
-                                       const uint32_t *, const uint32_t *, SpanRec *, uint16_t *, uint32_t *);
-template __global__ void k_span<true>(FrameParams, const uint32_t *, const uint32_t *, const uint32_t *,
-                                      const uint32_t *, const uint32_t *, SpanRec *, uint16_t *, uint32_t *);
+#define PRK_SPAN_ARGS FrameParams, const uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *, \
+                      const uint32_t *, const uint32_t *, SpanRec *, uint16_t *, uint32_t *
+template __global__ void k_span<false>(PRK_SPAN_ARGS);
+template __global__ void k_span<true>(PRK_SPAN_ARGS);
 template __global__ void k_pix<false>(FrameParams, const uint32_t *, const SpanRec *, const uint16_t *);
 template __global__ void k_pix<true>(FrameParams, const uint32_t *, const SpanRec *, const uint16_t *);
 PRK_INST(-1, false)
@@ -1239,8 +1272,9 @@ static size_t span_lds(const prk::FrameParams *fp) {
 // and k_pix.  recs / pmap: the
 // span records (64 B per tile pixel) and the per-pixel record map (2 B).
 hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint32_t *offs, const uint32_t *bins,
-                             uint32_t *won, uint32_t *list, uint32_t *nwin, uint32_t *wtag, void *recs, void *pmap,
-                             uint32_t *anomaly, hipEvent_t mid, hipEvent_t mid2, hipStream_t s) {
+                             uint32_t *won, uint32_t *list, uint32_t *nwin, uint32_t *wtag, uint32_t *slist,
+                             uint32_t *nwin_slice, void *recs, void *pmap, uint32_t *anomaly, hipEvent_t mid,
+                             hipEvent_t mid2, hipStream_t s) {
     const uint32_t ntile = (uint32_t)(fp->tiles_x * fp->tiles_y);
     if (ntile == 0) return hipSuccess;
     const size_t lv = vis_lds(fp), ls = shade_lds(fp), lsp = span_lds(fp);
@@ -1250,7 +1284,7 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
 #define PRK_VIS(MS, UNI)                                                                                             \
     do {                                                                                                             \
         hipLaunchKernelGGL((prk::k_vis<MS, UNI>), dim3(ntile), dim3(64 * prk::kWaves), lv, s, *fp, offs, bins,      \
-                           (uint8_t *)won, list, nwin, wtag, anomaly);                                               \
+                           (uint8_t *)won, list, nwin, wtag, slist, nwin_slice, anomaly);                            \
         if (mid) (void)hipEventRecord(mid, s);                                                                       \
     } while (0)
 #define PRK_SHADE(MS, UNI)                                                                                           \
@@ -1258,8 +1292,8 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
                        nwin, wtag, anomaly)
 #define PRK_SPANPIX(UNI)                                                                                             \
     do {                                                                                                             \
-        hipLaunchKernelGGL((prk::k_span<UNI>), dim3(ntile), dim3(64 * prk::kWaves), lsp, s, *fp, offs, bins, list,  \
-                           nwin, wtag, rp, mp, anomaly);                                                             \
+        hipLaunchKernelGGL((prk::k_span<UNI>), dim3(ntile * fp->span_split), dim3(64 * prk::kWaves), lsp, s, *fp,   \
+                           offs, bins, slist, nwin_slice, nwin, wtag, rp, mp, anomaly);                              \
         if (mid2) (void)hipEventRecord(mid2, s);                                                                     \
         hipLaunchKernelGGL((prk::k_pix<UNI>), dim3(ntile), dim3(256), 0, s, *fp, nwin, rp, mp);                      \
     } while (0)
