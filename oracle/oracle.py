@@ -19,6 +19,7 @@ from prk import abi  # noqa: E402
 from prk.scenes import CLEAR_COLOR, CLEAR_Z  # noqa: E402
 
 _LIB = None
+_CPU = None
 
 
 class OrDrawDesc(C.Structure):
@@ -48,6 +49,20 @@ def lib():
                    "oracle_fill_edge_table"):
             getattr(_LIB, fn).restype = C.c_int
     return _LIB
+
+
+def cpu_lib():
+    """liborcpu.so: the AVX2 CPU baseline (prk_cpu_avx.c), or None when the
+    host has no AVX2."""
+    global _CPU
+    if _CPU is None:
+        path = os.path.join(_HERE, "liborcpu.so")
+        if not os.path.exists(path):
+            build()
+        _CPU = C.CDLL(path)
+        for fn in ("cpu_avx_draw", "cpu_avx_draw_banded", "cpu_avx_draw_queue", "cpu_avx_supported"):
+            getattr(_CPU, fn).restype = C.c_int
+    return _CPU if _CPU.cpu_avx_supported() else None
 
 
 def _ptr(a):
@@ -85,10 +100,12 @@ class _Keep:
 
 
 def render(scene, semantics=abi.PRK_SEM_AVX, phong=True, tris_per_object=1, threads=1,
-           color=None, z=None, winners=True, rows=None):
+           color=None, z=None, winners=True, rows=None, cpu=None):
     """Draw `scene` with the oracle.  Returns (color u32[H,W], z f32[H,W],
     winners i32[H,W] or None, stats dict).  `color`/`z` (optional) are the
-    prior target contents (default: reference clear values)."""
+    prior target contents (default: reference clear values).
+    cpu: None = the scalar restatement (liboracle.so); "banded" / "queue" =
+    the AVX2 CPU baseline (liborcpu.so) with that schedule over `threads`."""
     W, H = scene.width, scene.height
     col = np.full((H, W), CLEAR_COLOR, np.uint32) if color is None else np.array(color, np.uint32)
     zb = np.full((H, W), CLEAR_Z, np.float32) if z is None else np.array(z, np.float32)
@@ -99,17 +116,26 @@ def render(scene, semantics=abi.PRK_SEM_AVX, phong=True, tris_per_object=1, thre
             sub = scene.subset(first, first + count)
             sub.texture, sub.draws = texture, None
             _, _, _, st = _render_one(sub, semantics, phong, tris_per_object, threads, col, zb, win, rows,
-                                      tri_base=first)
+                                      tri_base=first, cpu=cpu)
             tot = [tot[0] + st["spans"], tot[1] + st["span_pixels"], tot[2] + st["writes"]]
         return col, zb, win, dict(spans=tot[0], span_pixels=tot[1], writes=tot[2])
-    return _render_one(scene, semantics, phong, tris_per_object, threads, col, zb, win, rows)
+    return _render_one(scene, semantics, phong, tris_per_object, threads, col, zb, win, rows, cpu=cpu)
 
 
-def _render_one(scene, semantics, phong, tris_per_object, threads, col, zb, win, rows, tri_base=0):
+def _render_one(scene, semantics, phong, tris_per_object, threads, col, zb, win, rows, tri_base=0, cpu=None):
     W, H = scene.width, scene.height
     k = _Keep(scene, semantics, phong, tris_per_object, tri_base=tri_base)
     tg = OrTarget(_ptr(col), W * 4, _ptr(zb), W, H, _ptr(win))
     stats = (C.c_uint64 * 3)()
+    if cpu is not None:
+        L = cpu_lib()
+        if L is None:
+            raise RuntimeError("AVX2 CPU baseline: host has no AVX2")
+        fn = {"banded": L.cpu_avx_draw_banded, "queue": L.cpu_avx_draw_queue}[cpu]
+        rc = fn(C.byref(k.desc), C.byref(tg), C.byref(k.transform), C.byref(k.lights), int(threads), stats)
+        if rc != 0:
+            raise RuntimeError("cpu baseline failed: %s" % abi.STATUS_NAMES.get(rc, rc))
+        return col, zb, win, dict(spans=stats[0], span_pixels=stats[1], writes=stats[2])
     L = lib()
     if rows is not None:
         rc = L.oracle_draw_band(C.byref(k.desc), C.byref(tg), C.byref(k.transform),

@@ -649,6 +649,9 @@ static void or_fill_line_scalar(or_ctx *X_, const or_edge *L, const or_edge *R, 
 /* logic; the span body is the callback.  P3 applied at the swap.      */
 /* ------------------------------------------------------------------ */
 typedef void (*or_span_fn)(or_ctx *, const or_edge *, const or_edge *, int32_t);
+#ifndef OR_AVX_SPAN
+#define OR_AVX_SPAN or_fill_line_optimized
+#endif
 
 static inline int or_insert_before(const or_edge *A, const or_edge *B)
 {
@@ -837,7 +840,9 @@ static int or_draw_filtered(const or_draw_desc *D, const or_target *Tg, const pr
     X_.Width = Tg->Width; X_.Height = Tg->Height; X_.Winners = Tg->Winners;
     X_.RowLo = row_lo; X_.RowHi = row_hi; X_.Phong = D->Phong; X_.Filter = D->Filter;
     X_.BandH = band_h; X_.BandMod = band_mod; X_.BandRem = band_rem;
-    or_span_fn Span = D->Semantics == PRK_SEM_AVX ? or_fill_line_optimized : or_fill_line_scalar;
+    /* OR_AVX_SPAN: the AVX2 CPU baseline (prk_cpu_avx.c) substitutes its
+     * 8-wide span here; this file alone always uses the scalar restatement. */
+    or_span_fn Span = D->Semantics == PRK_SEM_AVX ? OR_AVX_SPAN : or_fill_line_scalar;
     for (uint32_t t0 = 0; t0 < D->TriCount; t0 += per) {
         uint32_t n = D->TriCount - t0 < per ? D->TriCount - t0 : per;
         if (band_mod > 1 || row_lo > 0 || row_hi < Tg->Height) {
