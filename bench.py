@@ -260,14 +260,14 @@ def main():
         "mtri_per_s": T / (ms * 1e-3) / 1e6,
         "ms_bin": ms_bin,
         "ms_raster": ms_raster,
-        "ms_kernels": {"k_vis": ms_vis, "k_span": ms_span, "k_pix": ms_pix},
+        "ms_kernels": {"k_vis": ms_vis, "k_walk": ms_span, "k_pix": ms_pix},
         "bin_entries": int(stats["bin_entries"]),
         "ms_upload": ms_upload,
         "ms_download": ms_download,
-        # The raster stage (k_vis -> k_span -> k_pix, back to back on one
+        # The raster stage (k_vis -> k_walk -> k_pix, back to back on one
         # stream) is priced as one unit: its algorithmic bytes over the stage's
         # HIP-event duration.
-        "roofline": {"bound": "hbm", "kernel": "raster stage (k_vis+k_span+k_pix)", "achieved": achieved,
+        "roofline": {"bound": "hbm", "kernel": "raster stage (k_vis+k_walk+k_pix)", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes": alg},
     }

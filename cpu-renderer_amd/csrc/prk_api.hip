@@ -12,7 +12,6 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
-#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -24,10 +23,10 @@ extern "C" {
 hipError_t prk_launch_tri_draw(const prk::DrawRec *, uint32_t, uint32_t *, uint32_t, hipStream_t);
 hipError_t prk_bin_phase1(const prk::FrameParams *, uint32_t *, uint32_t *, void *, void *, size_t *, hipStream_t);
 hipError_t prk_bin_phase2(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, uint32_t *, uint32_t *,
-                          uint32_t *, uint32_t *, uint32_t *, void *, size_t *, hipStream_t);
-hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, const uint32_t *, uint32_t *,
-                             uint32_t *, uint32_t *, uint32_t *, uint32_t *, uint32_t *, void *, void *, uint32_t *,
-                             hipEvent_t, hipEvent_t, hipStream_t);
+                          uint32_t *, uint32_t *, uint32_t *, uint32_t *, uint32_t *, void *, size_t *, hipStream_t);
+hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, const uint32_t *, const uint32_t *,
+                             const uint32_t *, const void *, uint8_t *, uint8_t *, uint32_t *, uint32_t *,
+                             uint32_t *, void *, uint32_t *, hipEvent_t, hipEvent_t, hipStream_t);
 }
 
 namespace {
@@ -92,10 +91,10 @@ struct prk_context {
     uint32_t pending_tris = 0;
     // scratch
     DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_tri_n, d_tri_off, d_keys_a, d_vals_a, d_keys_b, d_bins,
-        d_offs, d_won, d_list, d_temp, d_winners, d_anomaly, d_nwin, d_wtag, d_prof, d_recs, d_pmap, d_slist, d_nwin_slice;
+        d_offs, d_won, d_list, d_temp, d_winners, d_anomaly, d_nwin, d_wtag, d_prof, d_recs, d_jidx, d_jsorted,
+        d_trwon;
     uint32_t *h_total = nullptr;  // pinned
     int32_t tile_w = 256, tile_h = 8;  // measured best for C3b
-    int32_t span_split = 2;  // k_span row slices per tile (env PRK_SPAN_SPLIT overrides; A/B runs)
     bool debug = false;
     bool winners_valid = false;
     prk_stats stats{};
@@ -137,7 +136,6 @@ int prk_create(int device, prk_context **out) {
     prk_context *c = new (std::nothrow) prk_context();
     if (!c) return PRK_ERR_NOMEM;
     c->device = device;
-    if (const char *ss = std::getenv("PRK_SPAN_SPLIT")) c->span_split = std::max(1, std::atoi(ss));
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     for (int i = 0; i < prk_context::kRing && e == hipSuccess; ++i)
         for (int k = 0; k < 5 && e == hipSuccess; ++k) e = hipEventCreate(&c->ev[i][k]);
@@ -168,7 +166,7 @@ int prk_destroy(prk_context *c) {
     }
     DevBuf *bufs[] = {&c->d_draws,  &c->d_texs,   &c->d_tri_draw, &c->d_ranges, &c->d_tri_n, &c->d_tri_off,
                       &c->d_keys_a, &c->d_vals_a, &c->d_keys_b,   &c->d_bins,   &c->d_offs,  &c->d_won,
-                      &c->d_list,   &c->d_temp,   &c->d_winners,  &c->d_anomaly, &c->d_nwin, &c->d_wtag, &c->d_prof, &c->d_recs, &c->d_pmap, &c->d_slist, &c->d_nwin_slice};
+                      &c->d_list,   &c->d_temp,   &c->d_winners,  &c->d_anomaly, &c->d_nwin, &c->d_wtag, &c->d_prof, &c->d_recs, &c->d_jidx, &c->d_jsorted, &c->d_trwon};
     for (DevBuf *b : bufs) b->release();
     if (c->h_total) (void)hipHostFree(c->h_total);
     for (auto &slot : c->ev)
@@ -520,9 +518,6 @@ int prk_flush(prk_context *c, void *stream) {
     fp.zbuf = c->zbuf;
     fp.tile_w = c->tile_w;
     fp.tile_h = c->tile_h;
-    // k_span row slices: two per tile when the tile height allows it
-    fp.span_split = (c->span_split > 0 && c->tile_h % c->span_split == 0) ? c->span_split : 1;
-    fp.slice_h = c->tile_h / fp.span_split;
     fp.tile_w_log2 = 0;
     while ((1 << fp.tile_w_log2) < c->tile_w) ++fp.tile_w_log2;
     fp.tiles_x = (c->W + c->tile_w - 1) / c->tile_w;
@@ -602,35 +597,43 @@ int prk_flush(prk_context *c, void *stream) {
     PRK_TRY(c->d_vals_a.ensure(ne * 4));
     PRK_TRY(c->d_keys_b.ensure(ne * 4));
     PRK_TRY(c->d_bins.ensure(ne * 4));
+    PRK_TRY(c->d_jidx.ensure(ne * 4));
+    PRK_TRY(c->d_jsorted.ensure(ne * 4));
     PRK_TRY(c->d_list.ensure(ne * 4));
-    PRK_TRY(c->d_won.ensure(ne * fp.span_split));  // per (entry, row slice): won a pixel
-    PRK_TRY(c->d_slist.ensure(ne * fp.span_split * 4));
+    // won flags: per (pair, row in tile) for span-record (AVX) frames, per bin
+    // entry otherwise
+    const bool span_rec = modeset == prk::MODE_AVX;
+    const size_t won_bytes = span_rec ? ne * (size_t)c->tile_h : ne;
+    PRK_TRY(c->d_won.ensure(won_bytes));
     size_t sort_bytes = 0;
     PRK_TRY(prk_bin_phase2(&fp, c->d_ranges.p, (const uint32_t *)c->d_tri_off.p, total, (uint32_t *)c->d_keys_a.p,
-                           (uint32_t *)c->d_vals_a.p, (uint32_t *)c->d_keys_b.p, (uint32_t *)c->d_bins.p,
-                           (uint32_t *)c->d_offs.p, nullptr, &sort_bytes, s));
+                           (uint32_t *)c->d_vals_a.p, (uint32_t *)c->d_jidx.p, (uint32_t *)c->d_keys_b.p,
+                           (uint32_t *)c->d_jsorted.p, (uint32_t *)c->d_bins.p, (uint32_t *)c->d_offs.p, nullptr,
+                           &sort_bytes, s));
     PRK_TRY(c->d_temp.ensure(std::max(sort_bytes, scan_bytes)));
     PRK_TRY(prk_bin_phase2(&fp, c->d_ranges.p, (const uint32_t *)c->d_tri_off.p, total, (uint32_t *)c->d_keys_a.p,
-                           (uint32_t *)c->d_vals_a.p, (uint32_t *)c->d_keys_b.p, (uint32_t *)c->d_bins.p,
-                           (uint32_t *)c->d_offs.p, c->d_temp.p, &sort_bytes, s));
-    PRK_TRY(hipMemsetAsync(c->d_won.p, 0, ne * fp.span_split, s));
+                           (uint32_t *)c->d_vals_a.p, (uint32_t *)c->d_jidx.p, (uint32_t *)c->d_keys_b.p,
+                           (uint32_t *)c->d_jsorted.p, (uint32_t *)c->d_bins.p, (uint32_t *)c->d_offs.p, c->d_temp.p,
+                           &sort_bytes, s));
+    PRK_TRY(hipMemsetAsync(c->d_won.p, 0, won_bytes, s));
+    if (span_rec) {
+        PRK_TRY(c->d_trwon.ensure(T));
+        PRK_TRY(hipMemsetAsync(c->d_trwon.p, 0, T, s));
+    }
     PRK_TRY(hipEventRecord(c->ev[slot][1], s));
     if (!c->d_anomaly.p) {
         PRK_TRY(c->d_anomaly.ensure(8));  // [anomalies, slow replays]
         PRK_TRY(hipMemsetAsync(c->d_anomaly.p, 0, 8, s));
     }
     PRK_TRY(c->d_nwin.ensure((size_t)ntiles * 4));
-    PRK_TRY(c->d_nwin_slice.ensure((size_t)ntiles * fp.span_split * 4));
     PRK_TRY(c->d_wtag.ensure((size_t)ntiles * c->tile_w * c->tile_h * 4));
-    if (modeset == prk::MODE_AVX) {  // span records (64 B) + record map (2 B) per tile pixel
-        PRK_TRY(c->d_recs.ensure((size_t)ntiles * c->tile_w * c->tile_h * 64));
-        PRK_TRY(c->d_pmap.ensure((size_t)ntiles * c->tile_w * c->tile_h * 2));
-    }
+    // span records: 64 B per (pair, row in tile); only won ones are written
+    if (span_rec) PRK_TRY(c->d_recs.ensure(won_bytes * 64));
     PRK_TRY(prk_launch_raster(&fp, modeset, (const uint32_t *)c->d_offs.p, (const uint32_t *)c->d_bins.p,
-                              (uint32_t *)c->d_won.p, (uint32_t *)c->d_list.p, (uint32_t *)c->d_nwin.p,
-                              (uint32_t *)c->d_wtag.p, (uint32_t *)c->d_slist.p, (uint32_t *)c->d_nwin_slice.p,
-                              c->d_recs.p, c->d_pmap.p, (uint32_t *)c->d_anomaly.p,
-                              c->ev[slot][3], modeset == prk::MODE_AVX ? c->ev[slot][4] : nullptr, s));
+                              (const uint32_t *)c->d_jsorted.p, (const uint32_t *)c->d_tri_off.p, c->d_ranges.p,
+                              (uint8_t *)c->d_won.p, (uint8_t *)c->d_trwon.p, (uint32_t *)c->d_list.p,
+                              (uint32_t *)c->d_nwin.p, (uint32_t *)c->d_wtag.p, c->d_recs.p,
+                              (uint32_t *)c->d_anomaly.p, c->ev[slot][3], span_rec ? c->ev[slot][4] : nullptr, s));
     PRK_TRY(hipEventRecord(c->ev[slot][2], s));
     c->pending[slot] = true;
     c->split_span[slot] = modeset == prk::MODE_AVX;

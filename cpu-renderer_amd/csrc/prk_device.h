@@ -63,7 +63,6 @@ struct FrameParams {
     // tiling
     int32_t tile_w, tile_h, tiles_x, tiles_y;
     int32_t tile_w_log2;  // tile_w is a power of two
-    int32_t span_split, slice_h;  // k_span row slices per tile (slice_h = tile_h / span_split)
     // geometry
     uint32_t tri_count;
     uint32_t ndraws;

@@ -38,11 +38,8 @@
 #ifndef PRK_VIS_MIN_WAVES
 #define PRK_VIS_MIN_WAVES 3  // waves per SIMD k_vis is register-budgeted for
 #endif
-#ifndef PRK_SPAN_MIN_WAVES
-#define PRK_SPAN_MIN_WAVES 3  // waves per SIMD k_span is register-budgeted for
-#endif
 #ifndef PRK_SPAN_RECORDS
-#define PRK_SPAN_RECORDS 1  // AVX frames shade through k_span + k_pix (else k_shade)
+#define PRK_SPAN_RECORDS 1  // AVX frames shade through k_walk + k_pix (else k_shade)
 #endif
 #ifndef PRK_SHADE_MIN_WAVES
 #define PRK_SHADE_MIN_WAVES 3  // waves per SIMD k_shade is register-budgeted for
@@ -858,17 +855,18 @@ template <int MODESET, bool UNI>
 __global__ void __launch_bounds__(64 * kWaves, PRK_VIS_MIN_WAVES)
     k_vis(FrameParams fp, const uint32_t *__restrict__ offs, const uint32_t *__restrict__ bins,
           uint8_t *__restrict__ won, uint32_t *__restrict__ list, uint32_t *__restrict__ nwin_out,
-          uint32_t *__restrict__ wtag, uint32_t *__restrict__ slist, uint32_t *__restrict__ nwin_slice,
+          uint32_t *__restrict__ wtag, const uint32_t *__restrict__ jsorted, uint8_t *__restrict__ trwon,
           uint32_t *__restrict__ anomaly) {
+    // Span-record frames (all draws AVX): k_walk + k_pix shade from the
+    // winner tags; k_vis marks the won (pair, row)s and triangles for them.
+    constexpr bool kRec = MODESET == MODE_AVX && PRK_SPAN_RECORDS;
     extern __shared__ unsigned long long lds[];
     const int ntile = fp.tiles_x * fp.tiles_y;
     const int t = blockIdx.x;
     if (t >= ntile) return;
     const uint32_t b0 = offs[t], b1 = offs[t + 1];
-    const int S = fp.span_split;
     if (b0 == b1) {  // no triangle touches this tile: leave it untouched
         if (threadIdx.x == 0) nwin_out[t] = 0;
-        if (threadIdx.x < S) nwin_slice[t * S + threadIdx.x] = 0;
         return;
     }
     const uint32_t n = b1 - b0;
@@ -903,11 +901,19 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_VIS_MIN_WAVES)
     __syncthreads();
     // Winner tags out, and which bin entries won at least one pixel.
     uint32_t *tags_out = wtag + (size_t)t * npx;
+    int anyw = 0;
     for (int p = threadIdx.x; p < npx; p += blockDim.x) {
         const uint32_t low = (uint32_t)tc.key[p];
         tags_out[p] = low;
-        // flag (entry, row slice): k_span walks each slice separately
-        if (low != 0xFFFFFFFFu) won[(size_t)(b0 + (0xFFFFFFFEu - low)) * S + (p >> fp.tile_w_log2) / fp.slice_h] = 1;
+        if (low == 0xFFFFFFFFu) continue;
+        const uint32_t pe = b0 + (0xFFFFFFFEu - low);
+        if constexpr (kRec) {  // the winner's (pair, row) and triangle (benign same-value races)
+            anyw = 1;
+            won[(size_t)jsorted[pe] * fp.tile_h + (p >> fp.tile_w_log2)] = 1;
+            trwon[bins[pe]] = 1;
+        } else {
+            won[pe] = 1;
+        }
     }
     // Debug builds also export the winning triangle map.
     if (fp.winners) {
@@ -919,31 +925,24 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_VIS_MIN_WAVES)
                 low != 0xFFFFFFFFu ? (int32_t)bins[b0 + (0xFFFFFFFEu - low)] : -1;
         }
     }
+    if constexpr (kRec) {
+        anyw = __syncthreads_or(anyw);
+        if (threadIdx.x == 0) nwin_out[t] = (PRK_DIAG & 1) ? 0u : (uint32_t)anyw;
+        return;
+    }
     __threadfence_block();
     __syncthreads();
-    // Entries that won in the tile (list) and in each row slice (slist).
-    for (int sl = -1; sl < S; ++sl) {
-        uint32_t nwin = 0;
-        uint32_t *out = sl < 0 ? list + b0 : slist + (size_t)b0 * S + (size_t)sl * n;
-        for (uint32_t base = 0; base < n; base += blockDim.x) {
-            const uint32_t i = base + threadIdx.x;
-            uint32_t f = 0;
-            if (i < n) {
-                const uint8_t *w = won + (size_t)(b0 + i) * S;
-                if (sl >= 0) f = w[sl];
-                else for (int k = 0; k < S; ++k) f |= w[k];
-            }
-            f = f ? 1u : 0u;
-            uint32_t tot;
-            const uint32_t pos = block_excl_scan(f, scratch, tot);
-            if (f) out[nwin + pos] = i;
-            nwin += tot;
-        }
-        if (threadIdx.x == 0) {
-            if (sl < 0) nwin_out[t] = (PRK_DIAG & 1) ? 0u : nwin;
-            else nwin_slice[t * S + sl] = (PRK_DIAG & 1) ? 0u : nwin;
-        }
+    // Entries that won at least one pixel of the tile (k_shade walks these).
+    uint32_t nwin = 0;
+    for (uint32_t base = 0; base < n; base += blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t f = (i < n && won[b0 + i]) ? 1u : 0u;
+        uint32_t tot;
+        const uint32_t pos = block_excl_scan(f, scratch, tot);
+        if (f) list[b0 + nwin + pos] = i;
+        nwin += tot;
     }
+    if (threadIdx.x == 0) nwin_out[t] = (PRK_DIAG & 1) ? 0u : nwin;
 }
 
 // Shading (sweep 2), one workgroup per tile: re-walk only the entries that
@@ -984,29 +983,30 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_SHADE_MIN_WAVES)
 
 // ---------------------------------------------------------------------------
 // AVX frames shade in two kernels instead of k_shade's in-wave work items:
-//   k_span  one workgroup per tile walks the entries that won a pixel (setup +
-//           AET rows as k_shade) and, for every row span that won a pixel,
-//           writes the span's FillLineOptimized lane-init record (64 B) and
-//           points the won pixels at it (LDS map, flushed coalesced);
-//   k_pix   one thread per pixel replays its lane chain from the record,
-//           shades (texel + Phong) and stores z and colour, coalesced.
-// The walk keeps no item state live and the shading runs at full lane
-// occupancy with no walker registers.
+//   k_walk  one thread per triangle that won a pixel: setup once, walk the
+//           triangle's rows once (normals included) and, for every (pair, row)
+//           k_vis marked won, write the span's FillLineOptimized lane-init
+//           record (64 B) at recs[pair * tile_h + row in tile];
+//   k_pix   one thread per pixel: winner tag -> bin entry -> pair -> record;
+//           replays its lane chain from the record, shades (texel + Phong)
+//           and stores z and colour, coalesced.
+// Each triangle is set up and walked once for shading (a per-tile walk would
+// set it up per tile and replay the rows above every tile), and the shading
+// runs at full lane occupancy with no walker registers.
 // ---------------------------------------------------------------------------
 struct SpanRec {  // one won row span (FillLineOptimized span setup, 1543-1835)
     int32_t left_tex;  // LeftXa (low 16 bits) | texture index << 16
     float xoff, lw, lu, lv, lz, iw, iu, iv, iz, ln0, ln1, ln2, in0, in1, in2;
 };
 static_assert(sizeof(SpanRec) == 64, "span record is four dwordx4");
-constexpr uint32_t kNoRec = 0xFFFFu;
 
-// k_span: FillLineOptimized span setup (projekt.cpp:1543-1835) of one row;
-// when the span won a pixel of the tile, write its record and point the won
-// pixels (LDS map) at it.
-__device__ __forceinline__ void span_record(const FrameParams &fp, const TileCtx &tc, const Edge &L, const Edge &R,
-                                            int32_t Row, uint32_t tag, int32_t texi, SpanRec *trecs, uint16_t *map,
-                                            uint32_t *count) {
-    if (Row < tc.y0) return;
+// k_walk: FillLineOptimized span setup (projekt.cpp:1543-1835) of one row of
+// the triangle; for every tile the span crosses whose (pair, row) won a pixel
+// in k_vis, write the span's record at recs[pair * tile_h + row-in-tile].
+__device__ __forceinline__ void walk_record(const FrameParams &fp, const Edge &L, const Edge &R, int32_t Row,
+                                            int32_t texi, const TileRange &tr, uint32_t jb, int ntx,
+                                            const uint8_t *__restrict__ won, SpanRec *__restrict__ recs) {
+    if (Row < fp.row0) return;
     const int32_t W = fp.W;
     float XOffset = 0.0f;
     float LeftX = L.X;  // 1545-1565
@@ -1016,34 +1016,22 @@ __device__ __forceinline__ void span_record(const FrameParams &fp, const TileCtx
     if (RightX < 0) RightX = 0;
     else if (RightX >= W) RightX = (float)W - 1;
     if (LeftX != LeftX || RightX != RightX) return;  // pinned: NaN edge X draws nothing
-    const int32_t XDiff = (int32_t)((uint32_t)round_s32(R.X) - (uint32_t)round_s32(L.X));  // 1568-1570
     const int32_t MinX = round_s32(LeftX), MaxX = round_s32(RightX);  // 1588-1592
+    if (MinX >= MaxX) return;  // [MinX, MaxX) empty
+    const int32_t rr = Row - fp.row0, ty = rr / fp.tile_h, ly = rr - ty * fp.tile_h;
+    if (ty < (int)tr.ty0 || ty > (int)tr.ty1) return;  // (binning covers every span pixel)
+    const int tx0 = max((int)tr.tx0, MinX >> fp.tile_w_log2);
+    const int tx1 = min((int)tr.tx1, (MaxX - 1) >> fp.tile_w_log2);
+    const uint32_t jrow = jb + (uint32_t)((ty - (int)tr.ty0) * ntx - (int)tr.tx0);
+    bool any = false;
+    for (int tx = tx0; tx <= tx1; ++tx) any |= won[(size_t)(jrow + tx) * fp.tile_h + ly] != 0;
+    if (!any) return;
+    const int32_t XDiff = (int32_t)((uint32_t)round_s32(R.X) - (uint32_t)round_s32(L.X));  // 1568-1570
     int32_t LeftXa = MinX;
     if (MinX & 7) {  // 1594-1609
         LeftXa = MinX & ~7;
         XOffset -= (float)(MinX & 7) * 1.0f;
     }
-    const int32_t xa = max(MinX, tc.x0), xb = min(MaxX, tc.x1);  // [MinX, MaxX) in the tile
-    if (xa >= xb) return;
-    // Won pixels of the span (tags read 16 at a time).
-    const int rowoff = (Row - tc.y0) * tc.tw - tc.x0;
-    int won = 0;
-    uint64_t wm = 0;
-    for (int32_t x0 = xa & ~3; x0 < xb; x0 += 16) {
-        const uint4 *q = reinterpret_cast<const uint4 *>(tc.tags + rowoff + x0);
-        const uint4 c0 = q[0], c1 = q[1], c2 = q[2], c3 = q[3];
-        const uint32_t tg[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
-                                 c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int32_t x = x0 + k;
-            const bool w = tg[k] == tag && x >= xa && x < xb;
-            won += w ? 1 : 0;
-            const int32_t sh = x - xa;
-            if (w && sh < 64) wm |= 1ull << sh;
-        }
-    }
-    if (won == 0) return;
     const float fXD = (float)XDiff;
     float IW = 0, IU = 0, IV = 0, IZ = 0, IN0 = 0, IN1 = 0, IN2 = 0;
     if (XDiff != 0) {  // 1666-1835
@@ -1055,132 +1043,85 @@ __device__ __forceinline__ void span_record(const FrameParams &fp, const TileCtx
         IN2 = (R.N2 - L.N2) / fXD;
         IZ = (R.Z - L.Z) / fXD;
     }
-    const uint32_t ridx = atomicAdd(count, 1u);  // < npx: every record owns a won pixel
-    float4 *q = reinterpret_cast<float4 *>(trecs + ridx);
-    q[0] = make_float4(__int_as_float((LeftXa & 0xFFFF) | (texi << 16)), XOffset, L.W, L.U);
-    q[1] = make_float4(L.V, L.Z, IW, IU);
-    q[2] = make_float4(IV, IZ, L.N0, L.N1);
-    q[3] = make_float4(L.N2, IN0, IN1, IN2);
-    for (uint64_t m = wm; m; m &= m - 1) map[rowoff + xa + (int32_t)__builtin_ctzll(m)] = (uint16_t)ridx;
-    if (won > __builtin_popcountll(wm))  // past the span's first 64 columns
-        for (int32_t x = xa + 64; x < xb; ++x)
-            if (is_winner(tc, rowoff + x, tag)) map[rowoff + x] = (uint16_t)ridx;
+    const float4 q0 = make_float4(__int_as_float((LeftXa & 0xFFFF) | (texi << 16)), XOffset, L.W, L.U);
+    const float4 q1 = make_float4(L.V, L.Z, IW, IU);
+    const float4 q2 = make_float4(IV, IZ, L.N0, L.N1);
+    const float4 q3 = make_float4(L.N2, IN0, IN1, IN2);
+    for (int tx = tx0; tx <= tx1; ++tx) {  // a span crossing a tile border: one record per won tile
+        const size_t ri = (size_t)(jrow + tx) * fp.tile_h + ly;
+        if (!won[ri]) continue;
+        float4 *q = reinterpret_cast<float4 *>(recs + ri);
+        q[0] = q0; q[1] = q1; q[2] = q2; q[3] = q3;
+    }
 }
 
-
+// k_walk: one thread per triangle that won a pixel.  FillEdgeTable +
+// MergeSort once, then the triangle's whole AET walk (projekt.cpp:3615-3871,
+// normals included) from its first row of the band: no per-tile setup and no
+// replay of the rows above a tile.
 template <bool UNI>
-__global__ void __launch_bounds__(64 * kWaves, PRK_SPAN_MIN_WAVES)
-    k_span(FrameParams fp, const uint32_t *__restrict__ offs, const uint32_t *__restrict__ bins,
-           const uint32_t *__restrict__ slist, const uint32_t *__restrict__ nwin_slice,
-           const uint32_t *__restrict__ nwin_tile, const uint32_t *__restrict__ wtag, SpanRec *__restrict__ recs,
-           uint16_t *__restrict__ pmap, uint32_t *__restrict__ anomaly) {
-    // One workgroup per (tile, row slice): the slice's rows only, so every
-    // walk covers tile_h / span_split rows (fewer idle lanes per row step).
+__global__ void __launch_bounds__(256) k_walk(FrameParams fp, const uint8_t *__restrict__ trwon,
+                                              const uint32_t *__restrict__ tri_off,
+                                              const TileRange *__restrict__ ranges, const uint8_t *__restrict__ won,
+                                              SpanRec *__restrict__ recs, uint32_t *__restrict__ anomaly) {
     constexpr int M = MODE_AVX;
-    extern __shared__ unsigned long long lds[];
-    const int ntile = fp.tiles_x * fp.tiles_y;
-    const int S = fp.span_split;
-    const int t = blockIdx.x / S, sl = blockIdx.x - t * S;
-    if (t >= ntile) return;
-    if (nwin_tile[t] == 0) return;  // k_pix skips the whole tile
-    const uint32_t nwin = nwin_slice[blockIdx.x];
-    if (nwin == 0) {  // no winner in this slice: k_pix still reads its map
-        uint16_t *mo = pmap + (size_t)t * fp.tile_w * fp.tile_h + (size_t)sl * fp.tile_w * fp.slice_h;
-        for (int p = threadIdx.x; p < fp.tile_w * fp.slice_h; p += blockDim.x) mo[p] = (uint16_t)kNoRec;
-        return;
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= fp.tri_count || !trwon[g]) return;
+    Edge s0, s1, s2;
+    int ne;
+    int32_t texi;
+    if constexpr (UNI) {
+        ne = setup_triangle<M>(fp.draw0, fp.draw0.geom_tri0 + (g - fp.draw0.first_global), fp, s0, s1, s2);
+        texi = fp.draw0.tex;
+    } else {
+        const DrawRec *d;
+        uint32_t gt;
+        resolve_draw(fp, g, d, gt);
+        ne = setup_triangle<M>(*d, gt, fp, s0, s1, s2);
+        texi = d->tex;
     }
-    const uint32_t b0 = offs[t], n = offs[t + 1] - b0;
-    const uint32_t *list = slist + (size_t)b0 * S + (size_t)sl * n - b0;  // list[b0 + i]: the slice's i-th entry
-    TileCtx tc = tile_ctx(fp, t);
-    const int npx = fp.tile_w * fp.slice_h;  // this slice's pixels
-    const int pbase = sl * npx;              // its first pixel within the tile
-    tc.y0 += sl * fp.slice_h;
-    tc.y1 = min(tc.y1, tc.y0 + fp.slice_h);
-    uint32_t *tags = reinterpret_cast<uint32_t *>(lds);
-    uint16_t *map = reinterpret_cast<uint16_t *>(tags + npx + kTagPad);
-    uint32_t *count = reinterpret_cast<uint32_t *>(map + ((npx + 1) & ~1));
-    tc.tags = tags;
-    const size_t tpx = (size_t)t * fp.tile_w * fp.tile_h + pbase;
-    const uint32_t *tags_in = wtag + tpx;
-    for (int p = threadIdx.x; p < npx; p += blockDim.x) {
-        tags[p] = tags_in[p];
-        map[p] = (uint16_t)kNoRec;
-    }
-    if (threadIdx.x < kTagPad) tags[npx + threadIdx.x] = 0xFFFFFFFFu;  // chunked reads run past the end
-    if (threadIdx.x == 0) *count = 0;
-    __syncthreads();
-    SpanRec *trecs = recs + tpx;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (uint32_t base = wave * 64; base < nwin; base += 64 * kWaves) {
-        const uint32_t i = base + lane;
-        bool active = i < nwin;
-        uint32_t e = 0;
-        int32_t texi = 0;
-        RowWalker<M, true> wk;
-        uint32_t anom = 0;
-        if (active) {
-            e = list[b0 + i];
-            const uint32_t g = bins[b0 + e];
-            Edge s0, s1, s2;
-            int ne;
-            if constexpr (UNI) {
-                const uint32_t gt = fp.draw0.geom_tri0 + (g - fp.draw0.first_global);
-                ne = setup_triangle<M>(fp.draw0, gt, fp, s0, s1, s2);
-                texi = fp.draw0.tex;
-            } else {
-                const DrawRec *d;
-                uint32_t gt;
-                resolve_draw(fp, g, d, gt);
-                ne = setup_triangle<M>(*d, gt, fp, s0, s1, s2);
-                texi = d->tex;
-            }
-            active = ne >= 2;
-            if (active) {
-                Walker<M, true> w0;
-                w0.init(ne, s0, s1, s2, fp.H, tc.y1, anom);
-                const int fr = w0.fast_replay(tc.y0, ne);
-                wk.from(w0);
-                if (fr < 0)
-                    while (wk.Row < tc.y0 && wk.Row < wk.MaxY) wk.end_row(wk.begin_row());
-                active = wk.Row < wk.MaxY;
-            }
-        }
-        if (anom) atomicAdd(anomaly, anom);
-        const uint32_t tag = 0xFFFFFFFEu - e;
-        // Each lane walks its own rows; no cross-lane work in the loop.
-        while (active) {
-            const int32_t Row = wk.Row;
-            const bool paired = wk.begin_row();
-            if (paired) span_record(fp, tc, wk.S0, wk.S1, Row, tag, texi, trecs, map, count);
-            wk.end_row(paired);
-            active = wk.Row < wk.MaxY && wk.Row < tc.y1;
-        }
-    }
-    __syncthreads();
-    uint16_t *map_out = pmap + tpx;  // tile-relative record indices for k_pix
-    for (int p = threadIdx.x; p < npx; p += blockDim.x) {
-        const uint32_t m = map[p];
-        map_out[p] = (uint16_t)(m == kNoRec ? kNoRec : m + (uint32_t)pbase);
+    if (ne < 2) return;
+    uint32_t anom = 0;
+    Walker<M, true> w0;
+    w0.init(ne, s0, s1, s2, fp.H, fp.row1, anom);
+    const int fr = w0.fast_replay(fp.row0, ne);  // band above row0 (row bands only)
+    RowWalker<M, true> wk;
+    wk.from(w0);
+    if (fr < 0)
+        while (wk.Row < fp.row0 && wk.Row < wk.MaxY) wk.end_row(wk.begin_row());
+    if (anom) atomicAdd(anomaly, anom);
+    const TileRange tr = ranges[g];
+    const uint32_t jb = tri_off[g];
+    const int ntx = (int)tr.tx1 - (int)tr.tx0 + 1;
+    while (wk.Row < wk.MaxY) {
+        const int32_t Row = wk.Row;
+        const bool paired = wk.begin_row();
+        if (paired) walk_record(fp, wk.S0, wk.S1, Row, texi, tr, jb, ntx, won, recs);
+        wk.end_row(paired);
     }
 }
 
 // k_pix: shade the won pixels of one tile from their span records.
 template <bool UNI>
 __global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__restrict__ nwin_in,
-                                             const SpanRec *__restrict__ recs, const uint16_t *__restrict__ pmap) {
+                                             const uint32_t *__restrict__ offs, const uint32_t *__restrict__ wtag,
+                                             const uint32_t *__restrict__ jsorted,
+                                             const SpanRec *__restrict__ recs) {
     const int ntile = fp.tiles_x * fp.tiles_y;
     const int t = blockIdx.x;
     if (t >= ntile) return;
     if (nwin_in[t] == 0) return;
     const TileCtx tc = tile_ctx(fp, t);
     const int npx = fp.tile_w * fp.tile_h;
-    const SpanRec *trecs = recs + (size_t)t * npx;
-    const uint16_t *map = pmap + (size_t)t * npx;
+    const uint32_t b0 = offs[t];
+    const uint32_t *tags = wtag + (size_t)t * npx;
     for (int p = threadIdx.x; p < npx; p += blockDim.x) {
-        const uint32_t m = map[p];
-        if (m == kNoRec) continue;
-        const int32_t x = tc.x0 + (p & (fp.tile_w - 1)), Row = tc.y0 + (p >> fp.tile_w_log2);
-        const float4 *q = reinterpret_cast<const float4 *>(trecs + m);
+        const uint32_t tag = tags[p];
+        if (tag == 0xFFFFFFFFu) continue;  // no fragment beat the prior z
+        const int ly = p >> fp.tile_w_log2;
+        const int32_t x = tc.x0 + (p & (fp.tile_w - 1)), Row = tc.y0 + ly;
+        const uint32_t j = jsorted[b0 + (0xFFFFFFFEu - tag)];
+        const float4 *q = reinterpret_cast<const float4 *>(recs + (size_t)j * fp.tile_h + ly);
         const float4 r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];
         const int32_t lt = __float_as_int(r0.x);
         const int32_t LeftXa = (int32_t)(int16_t)(lt & 0xFFFF);
@@ -1214,18 +1155,20 @@ __global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__r
 
 // Explicit instantiations used by the host.
 #define PRK_VIS_ARGS FrameParams, const uint32_t *, const uint32_t *, uint8_t *, uint32_t *, uint32_t *, uint32_t *, \
-                     uint32_t *, uint32_t *, uint32_t *
+                     const uint32_t *, uint8_t *, uint32_t *
 #define PRK_SHADE_ARGS FrameParams, const uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *, \
                        const uint32_t *, uint32_t *
 #define PRK_INST(MS, UNI)                                  \
     template __global__ void k_vis<MS, UNI>(PRK_VIS_ARGS); \
     template __global__ void k_shade<MS, UNI>(PRK_SHADE_ARGS);
-#define PRK_SPAN_ARGS FrameParams, const uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *, \
-                      const uint32_t *, const uint32_t *, SpanRec *, uint16_t *, uint32_t *
-template __global__ void k_span<false>(PRK_SPAN_ARGS);
-template __global__ void k_span<true>(PRK_SPAN_ARGS);
-template __global__ void k_pix<false>(FrameParams, const uint32_t *, const SpanRec *, const uint16_t *);
-template __global__ void k_pix<true>(FrameParams, const uint32_t *, const SpanRec *, const uint16_t *);
+#define PRK_WALK_ARGS FrameParams, const uint8_t *, const uint32_t *, const TileRange *, const uint8_t *, SpanRec *, \
+                      uint32_t *
+#define PRK_PIX_ARGS FrameParams, const uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *, \
+                     const SpanRec *
+template __global__ void k_walk<false>(PRK_WALK_ARGS);
+template __global__ void k_walk<true>(PRK_WALK_ARGS);
+template __global__ void k_pix<false>(PRK_PIX_ARGS);
+template __global__ void k_pix<true>(PRK_PIX_ARGS);
 PRK_INST(-1, false)
 PRK_INST(MODE_AVX, false)
 PRK_INST(MODE_AVX, true)
@@ -1260,31 +1203,26 @@ static size_t shade_lds(const prk::FrameParams *fp) {
     return (npx + prk::kTagPad) * sizeof(uint32_t) + prk::kWaves * sizeof(prk::ShadeSlots);
 }
 
-// Sweep 1 (k_vis) then sweep 2 (k_shade) on stream s; `mid` (optional) is
-// recorded between them.
-static size_t span_lds(const prk::FrameParams *fp) {
-    const size_t npx = (size_t)fp->tile_w * fp->tile_h;
-    return (npx + prk::kTagPad) * sizeof(uint32_t) + ((npx + 1) & ~(size_t)1) * sizeof(uint16_t) + 16;
-}
-
-// Sweep 1 (k_vis) then the shading: k_span + k_pix for AVX frames, k_shade
-// otherwise; `mid` (optional) is recorded after k_vis, `mid2` between k_span
-// and k_pix.  recs / pmap: the
-// span records (64 B per tile pixel) and the per-pixel record map (2 B).
+// Sweep 1 (k_vis) then the shading: k_walk + k_pix for AVX frames, k_shade
+// otherwise; `mid` (optional) is recorded after k_vis, `mid2` between k_walk
+// and k_pix.  won: per bin entry (k_shade frames) or per (pair, row) (AVX
+// frames) won flags; trwon: per triangle; recs: span records, 64 B per
+// (pair, row); tri_off / ranges: the binning's pair offsets and tile ranges.
 hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint32_t *offs, const uint32_t *bins,
-                             uint32_t *won, uint32_t *list, uint32_t *nwin, uint32_t *wtag, uint32_t *slist,
-                             uint32_t *nwin_slice, void *recs, void *pmap, uint32_t *anomaly, hipEvent_t mid,
-                             hipEvent_t mid2, hipStream_t s) {
+                             const uint32_t *jsorted, const uint32_t *tri_off, const void *ranges, uint8_t *won,
+                             uint8_t *trwon, uint32_t *list, uint32_t *nwin, uint32_t *wtag, void *recs,
+                             uint32_t *anomaly, hipEvent_t mid, hipEvent_t mid2, hipStream_t s) {
     const uint32_t ntile = (uint32_t)(fp->tiles_x * fp->tiles_y);
     if (ntile == 0) return hipSuccess;
-    const size_t lv = vis_lds(fp), ls = shade_lds(fp), lsp = span_lds(fp);
+    const size_t lv = vis_lds(fp), ls = shade_lds(fp);
     const bool uni = fp->ndraws == 1;
     prk::SpanRec *rp = reinterpret_cast<prk::SpanRec *>(recs);
-    uint16_t *mp = reinterpret_cast<uint16_t *>(pmap);
+    const prk::TileRange *tr = reinterpret_cast<const prk::TileRange *>(ranges);
+    const uint32_t nblk = (fp->tri_count + 255) / 256;
 #define PRK_VIS(MS, UNI)                                                                                             \
     do {                                                                                                             \
-        hipLaunchKernelGGL((prk::k_vis<MS, UNI>), dim3(ntile), dim3(64 * prk::kWaves), lv, s, *fp, offs, bins,      \
-                           (uint8_t *)won, list, nwin, wtag, slist, nwin_slice, anomaly);                            \
+        hipLaunchKernelGGL((prk::k_vis<MS, UNI>), dim3(ntile), dim3(64 * prk::kWaves), lv, s, *fp, offs, bins, won, \
+                           list, nwin, wtag, jsorted, trwon, anomaly);                                              \
         if (mid) (void)hipEventRecord(mid, s);                                                                       \
     } while (0)
 #define PRK_SHADE(MS, UNI)                                                                                           \
@@ -1292,10 +1230,11 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
                        nwin, wtag, anomaly)
 #define PRK_SPANPIX(UNI)                                                                                             \
     do {                                                                                                             \
-        hipLaunchKernelGGL((prk::k_span<UNI>), dim3(ntile * fp->span_split), dim3(64 * prk::kWaves), lsp, s, *fp,   \
-                           offs, bins, slist, nwin_slice, nwin, wtag, rp, mp, anomaly);                              \
+        if (nblk)                                                                                                    \
+            hipLaunchKernelGGL((prk::k_walk<UNI>), dim3(nblk), dim3(256), 0, s, *fp, trwon, tri_off, tr, won, rp,    \
+                               anomaly);                                                                             \
         if (mid2) (void)hipEventRecord(mid2, s);                                                                     \
-        hipLaunchKernelGGL((prk::k_pix<UNI>), dim3(ntile), dim3(256), 0, s, *fp, nwin, rp, mp);                      \
+        hipLaunchKernelGGL((prk::k_pix<UNI>), dim3(ntile), dim3(256), 0, s, *fp, nwin, offs, wtag, jsorted, rp);     \
     } while (0)
     switch (modeset) {
         case prk::MODE_AVX:

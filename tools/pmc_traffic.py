@@ -6,7 +6,7 @@ FETCH_SIZE and WRITE_SIZE do not fit one TCC pass):
     rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d D -o write -- python3 bench.py ...
     python tools/pmc_traffic.py D <config-key> [out.json]
 
-Per frame, summed over the raster stage's kernels (k_vis, k_span, k_pix):
+Per frame, summed over the raster stage's kernels (k_vis, k_walk, k_pix):
 FETCH_SIZE and WRITE_SIZE are in KiB.  gfx950 correction (MI355X_MICROARCH.md
 §HBM): FETCH_SIZE reports half the bytes of a read, so the read side is
 doubled; WRITE_SIZE is taken as is.  The guide calibrates both only for
@@ -32,7 +32,7 @@ def per_launch(d, counter, kernel_substr):
     return vals
 
 
-STAGE = ("k_vis", "k_span", "k_pix")  # the raster stage of an AVX frame
+STAGE = ("k_vis", "k_walk", "k_pix")  # the raster stage of an AVX frame
 
 
 def main():
