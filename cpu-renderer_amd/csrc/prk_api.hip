@@ -25,8 +25,10 @@ hipError_t prk_bin_phase1(const prk::FrameParams *, uint32_t *, uint32_t *, void
 hipError_t prk_bin_phase2(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, uint32_t *, uint32_t *,
                           uint32_t *, uint32_t *, uint32_t *, uint32_t *, uint32_t *, void *, size_t *, hipStream_t);
 hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, const uint32_t *, const uint32_t *,
-                             const uint32_t *, const void *, uint8_t *, uint8_t *, uint32_t *, uint32_t *,
-                             uint32_t *, void *, uint32_t *, hipEvent_t, hipEvent_t, hipStream_t);
+                             const uint32_t *, const void *, uint8_t *, uint8_t *, uint32_t *, void *, size_t,
+                             uint32_t *, uint32_t *, uint32_t *, void *, uint32_t *, hipEvent_t, hipEvent_t,
+                             hipStream_t);
+hipError_t prk_walk_select_bytes(uint32_t, size_t *);
 }
 
 namespace {
@@ -92,7 +94,7 @@ struct prk_context {
     // scratch
     DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_tri_n, d_tri_off, d_keys_a, d_vals_a, d_keys_b, d_bins,
         d_offs, d_won, d_list, d_temp, d_winners, d_anomaly, d_nwin, d_wtag, d_prof, d_recs, d_jidx, d_jsorted,
-        d_trwon;
+        d_trwon, d_wlist, d_seltemp;
     uint32_t *h_total = nullptr;  // pinned
     int32_t tile_w = 256, tile_h = 8;  // measured best for C3b
     bool debug = false;
@@ -166,7 +168,7 @@ int prk_destroy(prk_context *c) {
     }
     DevBuf *bufs[] = {&c->d_draws,  &c->d_texs,   &c->d_tri_draw, &c->d_ranges, &c->d_tri_n, &c->d_tri_off,
                       &c->d_keys_a, &c->d_vals_a, &c->d_keys_b,   &c->d_bins,   &c->d_offs,  &c->d_won,
-                      &c->d_list,   &c->d_temp,   &c->d_winners,  &c->d_anomaly, &c->d_nwin, &c->d_wtag, &c->d_prof, &c->d_recs, &c->d_jidx, &c->d_jsorted, &c->d_trwon};
+                      &c->d_list,   &c->d_temp,   &c->d_winners,  &c->d_anomaly, &c->d_nwin, &c->d_wtag, &c->d_prof, &c->d_recs, &c->d_jidx, &c->d_jsorted, &c->d_trwon, &c->d_wlist, &c->d_seltemp};
     for (DevBuf *b : bufs) b->release();
     if (c->h_total) (void)hipHostFree(c->h_total);
     for (auto &slot : c->ev)
@@ -616,9 +618,13 @@ int prk_flush(prk_context *c, void *stream) {
                            (uint32_t *)c->d_jsorted.p, (uint32_t *)c->d_bins.p, (uint32_t *)c->d_offs.p, c->d_temp.p,
                            &sort_bytes, s));
     PRK_TRY(hipMemsetAsync(c->d_won.p, 0, won_bytes, s));
+    size_t sel_bytes = 0;
     if (span_rec) {
         PRK_TRY(c->d_trwon.ensure(T));
         PRK_TRY(hipMemsetAsync(c->d_trwon.p, 0, T, s));
+        PRK_TRY(c->d_wlist.ensure(((size_t)T + 1) * 4));  // won triangles + their count
+        PRK_TRY(prk_walk_select_bytes(T, &sel_bytes));
+        PRK_TRY(c->d_seltemp.ensure(std::max<size_t>(sel_bytes, 16)));
     }
     PRK_TRY(hipEventRecord(c->ev[slot][1], s));
     if (!c->d_anomaly.p) {
@@ -631,7 +637,8 @@ int prk_flush(prk_context *c, void *stream) {
     if (span_rec) PRK_TRY(c->d_recs.ensure(won_bytes * 64));
     PRK_TRY(prk_launch_raster(&fp, modeset, (const uint32_t *)c->d_offs.p, (const uint32_t *)c->d_bins.p,
                               (const uint32_t *)c->d_jsorted.p, (const uint32_t *)c->d_tri_off.p, c->d_ranges.p,
-                              (uint8_t *)c->d_won.p, (uint8_t *)c->d_trwon.p, (uint32_t *)c->d_list.p,
+                              (uint8_t *)c->d_won.p, (uint8_t *)c->d_trwon.p, (uint32_t *)c->d_wlist.p,
+                              c->d_seltemp.p, sel_bytes, (uint32_t *)c->d_list.p,
                               (uint32_t *)c->d_nwin.p, (uint32_t *)c->d_wtag.p, c->d_recs.p,
                               (uint32_t *)c->d_anomaly.p, c->ev[slot][3], span_rec ? c->ev[slot][4] : nullptr, s));
     PRK_TRY(hipEventRecord(c->ev[slot][2], s));

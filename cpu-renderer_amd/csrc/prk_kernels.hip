@@ -18,6 +18,8 @@
 //                shading runs once per pixel instead of once per fragment.
 //                A coalesced flush writes z and colour of every pixel that
 //                got a winner.
+#include <hipcub/hipcub.hpp>
+
 #include "prk_device.h"
 
 // Diagnostic builds only (tools/diag): 1 = skip the shading sweep, 2 = skip
@@ -1060,13 +1062,15 @@ __device__ __forceinline__ void walk_record(const FrameParams &fp, const Edge &L
 // normals included) from its first row of the band: no per-tile setup and no
 // replay of the rows above a tile.
 template <bool UNI>
-__global__ void __launch_bounds__(256) k_walk(FrameParams fp, const uint8_t *__restrict__ trwon,
+__global__ void __launch_bounds__(256) k_walk(FrameParams fp, const uint32_t *__restrict__ wlist,
+                                              const uint32_t *__restrict__ nwlist,
                                               const uint32_t *__restrict__ tri_off,
                                               const TileRange *__restrict__ ranges, const uint8_t *__restrict__ won,
                                               SpanRec *__restrict__ recs, uint32_t *__restrict__ anomaly) {
     constexpr int M = MODE_AVX;
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= fp.tri_count || !trwon[g]) return;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *nwlist) return;
+    const uint32_t g = wlist[i];  // the triangles that won a pixel (compacted)
     Edge s0, s1, s2;
     int ne;
     int32_t texi;
@@ -1092,11 +1096,31 @@ __global__ void __launch_bounds__(256) k_walk(FrameParams fp, const uint8_t *__r
     if (anom) atomicAdd(anomaly, anom);
     const TileRange tr = ranges[g];
     const uint32_t jb = tri_off[g];
-    const int ntx = (int)tr.tx1 - (int)tr.tx0 + 1;
+    const int ntx = (int)tr.tx1 - (int)tr.tx0 + 1, nty = (int)tr.ty1 - (int)tr.ty0 + 1;
+    // Rows that won a pixel in any tile, as bits over the triangle's tile rows
+    // (8-row tiles, <= 8 pairs): the won flags of a pair are 8 consecutive
+    // bytes, loaded together up front instead of one dependent load per row.
+    const int32_t rbase = fp.row0 + (int32_t)tr.ty0 * fp.tile_h;
+    const bool fast = fp.tile_h == 8 && ntx * nty <= 8;
+    uint64_t rows = ~0ull;
+    if (fast) {
+        uint64_t m[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            m[k] = k < ntx * nty ? *reinterpret_cast<const uint64_t *>(won + (size_t)(jb + k) * 8) : 0ull;
+        rows = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int ty = k / ntx;  // pair k = (ty, tx) row-major
+            rows |= ((m[k] * 0x0102040810204080ull) >> 56) << (8 * ty);  // bytes (0/1) -> bits
+        }
+    }
     while (wk.Row < wk.MaxY) {
         const int32_t Row = wk.Row;
         const bool paired = wk.begin_row();
-        if (paired) walk_record(fp, wk.S0, wk.S1, Row, texi, tr, jb, ntx, won, recs);
+        const int32_t rb = Row - rbase;
+        const bool want = !fast || (rb >= 0 && rb < 64 && ((rows >> rb) & 1ull));
+        if (paired && want) walk_record(fp, wk.S0, wk.S1, Row, texi, tr, jb, ntx, won, recs);
         wk.end_row(paired);
     }
 }
@@ -1161,8 +1185,8 @@ __global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__r
 #define PRK_INST(MS, UNI)                                  \
     template __global__ void k_vis<MS, UNI>(PRK_VIS_ARGS); \
     template __global__ void k_shade<MS, UNI>(PRK_SHADE_ARGS);
-#define PRK_WALK_ARGS FrameParams, const uint8_t *, const uint32_t *, const TileRange *, const uint8_t *, SpanRec *, \
-                      uint32_t *
+#define PRK_WALK_ARGS FrameParams, const uint32_t *, const uint32_t *, const uint32_t *, const TileRange *, \
+                      const uint8_t *, SpanRec *, uint32_t *
 #define PRK_PIX_ARGS FrameParams, const uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *, \
                      const SpanRec *
 template __global__ void k_walk<false>(PRK_WALK_ARGS);
@@ -1184,6 +1208,12 @@ PRK_INST(MODE_SC_PHONG, true)
 // Launchers (called from prk_api.cpp).
 // ---------------------------------------------------------------------------
 extern "C" {
+
+// Temp bytes hipcub's select over `n` triangle flags needs (k_walk's list).
+hipError_t prk_walk_select_bytes(uint32_t n, size_t *bytes) {
+    return hipcub::DeviceSelect::Flagged(nullptr, *bytes, hipcub::CountingInputIterator<uint32_t>(0u),
+                                         (const uint8_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr, n);
+}
 
 hipError_t prk_launch_tri_draw(const prk::DrawRec *draws, uint32_t ndraws, uint32_t *tri_draw,
                                uint32_t tri_count, hipStream_t s) {
@@ -1210,8 +1240,9 @@ static size_t shade_lds(const prk::FrameParams *fp) {
 // (pair, row); tri_off / ranges: the binning's pair offsets and tile ranges.
 hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint32_t *offs, const uint32_t *bins,
                              const uint32_t *jsorted, const uint32_t *tri_off, const void *ranges, uint8_t *won,
-                             uint8_t *trwon, uint32_t *list, uint32_t *nwin, uint32_t *wtag, void *recs,
-                             uint32_t *anomaly, hipEvent_t mid, hipEvent_t mid2, hipStream_t s) {
+                             uint8_t *trwon, uint32_t *wlist, void *sel_temp, size_t sel_bytes, uint32_t *list,
+                             uint32_t *nwin, uint32_t *wtag, void *recs, uint32_t *anomaly, hipEvent_t mid,
+                             hipEvent_t mid2, hipStream_t s) {
     const uint32_t ntile = (uint32_t)(fp->tiles_x * fp->tiles_y);
     if (ntile == 0) return hipSuccess;
     const size_t lv = vis_lds(fp), ls = shade_lds(fp);
@@ -1230,9 +1261,15 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
                        nwin, wtag, anomaly)
 #define PRK_SPANPIX(UNI)                                                                                             \
     do {                                                                                                             \
-        if (nblk)                                                                                                    \
-            hipLaunchKernelGGL((prk::k_walk<UNI>), dim3(nblk), dim3(256), 0, s, *fp, trwon, tri_off, tr, won, rp,    \
-                               anomaly);                                                                             \
+        if (nblk) {                                                                                                  \
+            /* compact the won triangles (order kept); the count stays on the device */                            \
+            uint32_t *nsel = wlist + fp->tri_count;                                                                  \
+            hipError_t e_ = hipcub::DeviceSelect::Flagged(sel_temp, sel_bytes, hipcub::CountingInputIterator<uint32_t>(0u), \
+                                                          trwon, wlist, nsel, fp->tri_count, s);                    \
+            if (e_ != hipSuccess) return e_;                                                                         \
+            hipLaunchKernelGGL((prk::k_walk<UNI>), dim3(nblk), dim3(256), 0, s, *fp, wlist, nsel, tri_off, tr, won, \
+                               rp, anomaly);                                                                         \
+        }                                                                                                            \
         if (mid2) (void)hipEventRecord(mid2, s);                                                                     \
         hipLaunchKernelGGL((prk::k_pix<UNI>), dim3(ntile), dim3(256), 0, s, *fp, nwin, offs, wtag, jsorted, rp);     \
     } while (0)
