@@ -293,8 +293,9 @@ __device__ __forceinline__ void load_tri(const DrawRec &d, uint32_t gt, TriRaw<M
     }
 }
 
-// FillEdgeTable (projekt.cpp:3882-4121) for ONE triangle followed by
-// MergeSort (2-72) of its <= 3 visible edges.  Returns the edge count.
+// FillEdgeTable (projekt.cpp:3882-4121) for ONE binned (front-facing)
+// triangle followed by MergeSort (2-72) of its <= 3 visible edges.  Returns
+// the edge count.
 template <int M>
 __device__ __forceinline__ int setup_from_raw(const TriRaw<M> &r, const DrawRec &d, const FrameParams &fp,
                                               Edge &s0, Edge &s1, Edge &s2) {
@@ -308,7 +309,9 @@ __device__ __forceinline__ int setup_from_raw(const TriRaw<M> &r, const DrawRec 
         cam[k] = V3{r.v[3 * k + 0] + d.P[0], r.v[3 * k + 1] + d.P[1], r.v[3 * k + 2] + d.P[2]};
         proj[k] = project_vertex(cam[k], fp);
     }
-    if (!front_facing(proj)) return 0;
+    // Back-face cull (3926-3943): every triangle reaching a raster kernel
+    // passed the identical test in k_bin_count (prk_bin.hip), so it is not
+    // repeated per bin entry.
 
     V3 nrm[3];
     float col[3][4], uv[3][2];
