@@ -22,9 +22,9 @@
 extern "C" {
 hipError_t prk_launch_tri_draw(const prk::DrawRec *, uint32_t, uint32_t *, uint32_t, hipStream_t);
 hipError_t prk_bin_phase1(const prk::FrameParams *, uint32_t *, uint32_t *, void *, void *, size_t *, hipStream_t);
-hipError_t prk_bin_phase2(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, uint32_t *, uint32_t *,
-                          uint32_t *, uint32_t *, uint32_t *, uint32_t *, uint32_t *, void *, size_t *, hipStream_t);
-hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, const uint32_t *, const uint32_t *,
+hipError_t prk_bin_phase2(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, uint32_t *, void *,
+                          uint32_t *, void *, uint32_t *, uint32_t *, void *, size_t *, hipStream_t);
+hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, const void *, const uint32_t *,
                              const uint32_t *, const void *, uint8_t *, uint8_t *, uint32_t *, void *, size_t,
                              uint32_t *, uint32_t *, uint32_t *, void *, uint32_t *, hipEvent_t, hipEvent_t,
                              hipStream_t);
@@ -92,8 +92,8 @@ struct prk_context {
     std::vector<prk::DrawRec> draws;
     uint32_t pending_tris = 0;
     // scratch
-    DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_tri_n, d_tri_off, d_keys_a, d_vals_a, d_keys_b, d_bins,
-        d_offs, d_won, d_list, d_temp, d_winners, d_anomaly, d_nwin, d_wtag, d_prof, d_recs, d_jidx, d_jsorted,
+    DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_tri_n, d_tri_off, d_pair_tri, d_keys_a, d_vals_a, d_keys_b, d_bins,
+        d_offs, d_won, d_list, d_temp, d_winners, d_anomaly, d_nwin, d_wtag, d_prof, d_recs,
         d_trwon, d_wlist, d_seltemp;
     uint32_t *h_total = nullptr;  // pinned
     int32_t tile_w = 256, tile_h = 8;  // measured best for C3b
@@ -167,8 +167,9 @@ int prk_destroy(prk_context *c) {
         (void)hipFree(c->zbuf);
     }
     DevBuf *bufs[] = {&c->d_draws,  &c->d_texs,   &c->d_tri_draw, &c->d_ranges, &c->d_tri_n, &c->d_tri_off,
-                      &c->d_keys_a, &c->d_vals_a, &c->d_keys_b,   &c->d_bins,   &c->d_offs,  &c->d_won,
-                      &c->d_list,   &c->d_temp,   &c->d_winners,  &c->d_anomaly, &c->d_nwin, &c->d_wtag, &c->d_prof, &c->d_recs, &c->d_jidx, &c->d_jsorted, &c->d_trwon, &c->d_wlist, &c->d_seltemp};
+                      &c->d_pair_tri, &c->d_keys_a, &c->d_vals_a, &c->d_keys_b, &c->d_bins, &c->d_offs, &c->d_won,
+                      &c->d_list,   &c->d_temp,   &c->d_winners,  &c->d_anomaly, &c->d_nwin, &c->d_wtag, &c->d_prof,
+                      &c->d_recs,   &c->d_trwon,  &c->d_wlist,    &c->d_seltemp};
     for (DevBuf *b : bufs) b->release();
     if (c->h_total) (void)hipHostFree(c->h_total);
     for (auto &slot : c->ev)
@@ -595,28 +596,25 @@ int prk_flush(prk_context *c, void *stream) {
     const uint32_t total = *c->h_total;
     c->stats.bin_entries = total;
     const size_t ne = (size_t)std::max<uint32_t>(total, 1);
-    PRK_TRY(c->d_keys_a.ensure(ne * 4));
-    PRK_TRY(c->d_vals_a.ensure(ne * 4));
-    PRK_TRY(c->d_keys_b.ensure(ne * 4));
-    PRK_TRY(c->d_bins.ensure(ne * 4));
-    PRK_TRY(c->d_jidx.ensure(ne * 4));
-    PRK_TRY(c->d_jsorted.ensure(ne * 4));
+    PRK_TRY(c->d_pair_tri.ensure(ne * 4));
+    PRK_TRY(c->d_bins.ensure(ne * 8));  // (triangle, pair) per bin slot
     PRK_TRY(c->d_list.ensure(ne * 4));
-    // won flags: per (pair, row in tile) for span-record (AVX) frames, per bin
-    // entry otherwise
+    // won flags: per (pair, row in tile) for span-record (AVX) frames, per
+    // pair otherwise
     const bool span_rec = modeset == prk::MODE_AVX;
     const size_t won_bytes = span_rec ? ne * (size_t)c->tile_h : ne;
     PRK_TRY(c->d_won.ensure(won_bytes));
+    PRK_TRY(c->d_keys_a.ensure(ne * 4));
+    PRK_TRY(c->d_vals_a.ensure(ne * 8));
+    PRK_TRY(c->d_keys_b.ensure(ne * 4));
     size_t sort_bytes = 0;
     PRK_TRY(prk_bin_phase2(&fp, c->d_ranges.p, (const uint32_t *)c->d_tri_off.p, total, (uint32_t *)c->d_keys_a.p,
-                           (uint32_t *)c->d_vals_a.p, (uint32_t *)c->d_jidx.p, (uint32_t *)c->d_keys_b.p,
-                           (uint32_t *)c->d_jsorted.p, (uint32_t *)c->d_bins.p, (uint32_t *)c->d_offs.p, nullptr,
-                           &sort_bytes, s));
+                           c->d_vals_a.p, (uint32_t *)c->d_keys_b.p, c->d_bins.p, (uint32_t *)c->d_pair_tri.p,
+                           (uint32_t *)c->d_offs.p, nullptr, &sort_bytes, s));
     PRK_TRY(c->d_temp.ensure(std::max(sort_bytes, scan_bytes)));
     PRK_TRY(prk_bin_phase2(&fp, c->d_ranges.p, (const uint32_t *)c->d_tri_off.p, total, (uint32_t *)c->d_keys_a.p,
-                           (uint32_t *)c->d_vals_a.p, (uint32_t *)c->d_jidx.p, (uint32_t *)c->d_keys_b.p,
-                           (uint32_t *)c->d_jsorted.p, (uint32_t *)c->d_bins.p, (uint32_t *)c->d_offs.p, c->d_temp.p,
-                           &sort_bytes, s));
+                           c->d_vals_a.p, (uint32_t *)c->d_keys_b.p, c->d_bins.p, (uint32_t *)c->d_pair_tri.p,
+                           (uint32_t *)c->d_offs.p, c->d_temp.p, &sort_bytes, s));
     PRK_TRY(hipMemsetAsync(c->d_won.p, 0, won_bytes, s));
     size_t sel_bytes = 0;
     if (span_rec) {
@@ -635,8 +633,8 @@ int prk_flush(prk_context *c, void *stream) {
     PRK_TRY(c->d_wtag.ensure((size_t)ntiles * c->tile_w * c->tile_h * 4));
     // span records: 64 B per (pair, row in tile); only won ones are written
     if (span_rec) PRK_TRY(c->d_recs.ensure(won_bytes * 64));
-    PRK_TRY(prk_launch_raster(&fp, modeset, (const uint32_t *)c->d_offs.p, (const uint32_t *)c->d_bins.p,
-                              (const uint32_t *)c->d_jsorted.p, (const uint32_t *)c->d_tri_off.p, c->d_ranges.p,
+    PRK_TRY(prk_launch_raster(&fp, modeset, (const uint32_t *)c->d_offs.p, c->d_bins.p,
+                              (const uint32_t *)c->d_pair_tri.p, (const uint32_t *)c->d_tri_off.p, c->d_ranges.p,
                               (uint8_t *)c->d_won.p, (uint8_t *)c->d_trwon.p, (uint32_t *)c->d_wlist.p,
                               c->d_seltemp.p, sel_bytes, (uint32_t *)c->d_list.p,
                               (uint32_t *)c->d_nwin.p, (uint32_t *)c->d_wtag.p, c->d_recs.p,

@@ -677,7 +677,7 @@ __device__ __forceinline__ int wave_incl_max(int v) {  // v >= 0
 template <int M, bool SHADE, bool UNI>
 __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
                                       std::conditional_t<SHADE, ShadeSlots, VisSlots> &ws,
-                                      const uint32_t *__restrict__ bins, uint32_t b0, uint32_t n,
+                                      const uint2 *__restrict__ bins, uint32_t b0, uint32_t n,
                                       const uint32_t *__restrict__ list, uint32_t *anomaly) {
     // Entries [0, n) of the tile's bin, or (list != nullptr) the n entries it names.
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -689,12 +689,14 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
     // loads are in flight while this chunk's setup and rows run.
     constexpr bool kPre = UNI && PRK_PREFETCH && !SHADE;  // (k_shade has no registers to spare)
     TriRaw<M> nraw;
-    uint32_t ne_e = 0, ne_g = 0;
+    uint32_t ne_e = 0, ne_g = 0, ne_j = 0;
     if constexpr (kPre) {
         const uint32_t i0 = wave * 64 + lane;
         if (i0 < n) {
             ne_e = list ? list[b0 + i0] : i0;
-            ne_g = bins[b0 + ne_e];
+            const uint2 be = bins[b0 + ne_e];
+            ne_g = be.x;
+            ne_j = be.y;
             load_tri<M>(fp.draw0, fp.draw0.geom_tri0 + (ne_g - fp.draw0.first_global), nraw);
         }
     }
@@ -702,7 +704,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
         unsigned long long t0 = PRK_T();
         const uint32_t i = base + lane;
         bool active = i < n;
-        uint32_t e = 0;
+        uint32_t e = 0, j = 0;  // bin entry, its pair index (the tie-break order)
         int32_t texi = 0;
         RowWalker<M, SHADE> wk;
         uint32_t anom = 0;
@@ -711,25 +713,31 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
         if constexpr (kPre) {
             craw = nraw;
             e = ne_e;
+            j = ne_j;
             if (inext < n) {
                 ne_e = list ? list[b0 + inext] : inext;
-                ne_g = bins[b0 + ne_e];
+                const uint2 be = bins[b0 + ne_e];
+                ne_g = be.x;
+                ne_j = be.y;
             }
         }
         if (active) {
-            if constexpr (!kPre) e = list ? list[b0 + i] : i;
+            if constexpr (!kPre) {
+                e = list ? list[b0 + i] : i;
+                j = bins[b0 + e].y;
+            }
             Edge s0, s1, s2;
             int ne;
             if constexpr (kPre) {
                 ne = setup_from_raw<M>(craw, fp.draw0, fp, s0, s1, s2);
                 texi = fp.draw0.tex;
             } else if constexpr (UNI) {  // one draw: its record is uniform (kernel arguments)
-                const uint32_t g = bins[b0 + e];
+                const uint32_t g = bins[b0 + e].x;
                 const uint32_t gt = fp.draw0.geom_tri0 + (g - fp.draw0.first_global);
                 ne = setup_triangle<M>(fp.draw0, gt, fp, s0, s1, s2);
                 texi = fp.draw0.tex;
             } else {
-                const uint32_t g = bins[b0 + e];
+                const uint32_t g = bins[b0 + e].x;
                 const DrawRec *d;
                 uint32_t gt;
                 resolve_draw(fp, g, d, gt);
@@ -756,7 +764,10 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
         }
         if (anom) atomicAdd(anomaly, anom);
         if (!(ModeTraits<M>::tex && active)) texi = 0;
-        const uint32_t tag = 0xFFFFFFFEu - e;
+        // Visibility tag: the pair index orders fragments of equal z exactly as
+        // submission order does (pairs are numbered in triangle order, one per
+        // triangle and tile), whatever order the bin lists them in.
+        const uint32_t tag = 0xFFFFFFFEu - j;
         if (PRK_DIAG & 4) active = false;
         if (PRK_PROF) { const unsigned long long t1 = PRK_T(); pt[0] += t1 - t0; t0 = t1; }
         // PRK_LANE_ROWS: every lane walks its own next row each iteration (the
@@ -855,9 +866,9 @@ __device__ __forceinline__ TileCtx tile_ctx(const FrameParams &fp, int t) {
 // the list of bin entries that won at least one pixel and its length.
 template <int MODESET, bool UNI>
 __global__ void __launch_bounds__(64 * kWaves, PRK_VIS_MIN_WAVES)
-    k_vis(FrameParams fp, const uint32_t *__restrict__ offs, const uint32_t *__restrict__ bins,
+    k_vis(FrameParams fp, const uint32_t *__restrict__ offs, const uint2 *__restrict__ bins,
           uint8_t *__restrict__ won, uint32_t *__restrict__ list, uint32_t *__restrict__ nwin_out,
-          uint32_t *__restrict__ wtag, const uint32_t *__restrict__ jsorted, uint8_t *__restrict__ trwon,
+          uint32_t *__restrict__ wtag, const uint32_t *__restrict__ pair_tri, uint8_t *__restrict__ trwon,
           uint32_t *__restrict__ anomaly) {
     // Span-record frames (all draws AVX): k_walk + k_pix shade from the
     // winner tags; k_vis marks the won (pair, row)s and triangles for them.
@@ -908,13 +919,13 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_VIS_MIN_WAVES)
         const uint32_t low = (uint32_t)tc.key[p];
         tags_out[p] = low;
         if (low == 0xFFFFFFFFu) continue;
-        const uint32_t pe = b0 + (0xFFFFFFFEu - low);
+        const uint32_t j = 0xFFFFFFFEu - low;  // the winning pair
         if constexpr (kRec) {  // the winner's (pair, row) and triangle (benign same-value races)
             anyw = 1;
-            won[(size_t)jsorted[pe] * fp.tile_h + (p >> fp.tile_w_log2)] = 1;
-            trwon[bins[pe]] = 1;
+            won[(size_t)j * fp.tile_h + (p >> fp.tile_w_log2)] = 1;
+            trwon[pair_tri[j]] = 1;
         } else {
-            won[pe] = 1;
+            won[j] = 1;
         }
     }
     // Debug builds also export the winning triangle map.
@@ -924,7 +935,7 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_VIS_MIN_WAVES)
             if (x >= tc.x1 || y >= tc.y1) continue;
             const uint32_t low = (uint32_t)tc.key[p];
             fp.winners[(size_t)(y - fp.row0) * fp.W + x] =
-                low != 0xFFFFFFFFu ? (int32_t)bins[b0 + (0xFFFFFFFEu - low)] : -1;
+                low != 0xFFFFFFFFu ? (int32_t)pair_tri[0xFFFFFFFEu - low] : -1;
         }
     }
     if constexpr (kRec) {
@@ -938,7 +949,7 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_VIS_MIN_WAVES)
     uint32_t nwin = 0;
     for (uint32_t base = 0; base < n; base += blockDim.x) {
         const uint32_t i = base + threadIdx.x;
-        const uint32_t f = (i < n && won[b0 + i]) ? 1u : 0u;
+        const uint32_t f = (i < n && won[bins[b0 + i].y]) ? 1u : 0u;
         uint32_t tot;
         const uint32_t pos = block_excl_scan(f, scratch, tot);
         if (f) list[b0 + nwin + pos] = i;
@@ -952,7 +963,7 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_VIS_MIN_WAVES)
 // z and colour; untouched pixels keep the prior contents.
 template <int MODESET, bool UNI>
 __global__ void __launch_bounds__(64 * kWaves, PRK_SHADE_MIN_WAVES)
-    k_shade(FrameParams fp, const uint32_t *__restrict__ offs, const uint32_t *__restrict__ bins,
+    k_shade(FrameParams fp, const uint32_t *__restrict__ offs, const uint2 *__restrict__ bins,
             const uint32_t *__restrict__ list, const uint32_t *__restrict__ nwin_in,
             const uint32_t *__restrict__ wtag, uint32_t *__restrict__ anomaly) {
     extern __shared__ unsigned long long lds[];
@@ -1128,23 +1139,20 @@ __global__ void __launch_bounds__(256) k_walk(FrameParams fp, const uint32_t *__
 // k_pix: shade the won pixels of one tile from their span records.
 template <bool UNI>
 __global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__restrict__ nwin_in,
-                                             const uint32_t *__restrict__ offs, const uint32_t *__restrict__ wtag,
-                                             const uint32_t *__restrict__ jsorted,
-                                             const SpanRec *__restrict__ recs) {
+                                             const uint32_t *__restrict__ wtag, const SpanRec *__restrict__ recs) {
     const int ntile = fp.tiles_x * fp.tiles_y;
     const int t = blockIdx.x;
     if (t >= ntile) return;
     if (nwin_in[t] == 0) return;
     const TileCtx tc = tile_ctx(fp, t);
     const int npx = fp.tile_w * fp.tile_h;
-    const uint32_t b0 = offs[t];
     const uint32_t *tags = wtag + (size_t)t * npx;
     for (int p = threadIdx.x; p < npx; p += blockDim.x) {
         const uint32_t tag = tags[p];
         if (tag == 0xFFFFFFFFu) continue;  // no fragment beat the prior z
         const int ly = p >> fp.tile_w_log2;
         const int32_t x = tc.x0 + (p & (fp.tile_w - 1)), Row = tc.y0 + ly;
-        const uint32_t j = jsorted[b0 + (0xFFFFFFFEu - tag)];
+        const uint32_t j = 0xFFFFFFFEu - tag;  // the winning pair
         const float4 *q = reinterpret_cast<const float4 *>(recs + (size_t)j * fp.tile_h + ly);
         const float4 r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];
         const int32_t lt = __float_as_int(r0.x);
@@ -1178,17 +1186,16 @@ __global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__r
 }
 
 // Explicit instantiations used by the host.
-#define PRK_VIS_ARGS FrameParams, const uint32_t *, const uint32_t *, uint8_t *, uint32_t *, uint32_t *, uint32_t *, \
+#define PRK_VIS_ARGS FrameParams, const uint32_t *, const uint2 *, uint8_t *, uint32_t *, uint32_t *, uint32_t *, \
                      const uint32_t *, uint8_t *, uint32_t *
-#define PRK_SHADE_ARGS FrameParams, const uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *, \
+#define PRK_SHADE_ARGS FrameParams, const uint32_t *, const uint2 *, const uint32_t *, const uint32_t *, \
                        const uint32_t *, uint32_t *
 #define PRK_INST(MS, UNI)                                  \
     template __global__ void k_vis<MS, UNI>(PRK_VIS_ARGS); \
     template __global__ void k_shade<MS, UNI>(PRK_SHADE_ARGS);
 #define PRK_WALK_ARGS FrameParams, const uint32_t *, const uint32_t *, const uint32_t *, const TileRange *, \
                       const uint8_t *, SpanRec *, uint32_t *
-#define PRK_PIX_ARGS FrameParams, const uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *, \
-                     const SpanRec *
+#define PRK_PIX_ARGS FrameParams, const uint32_t *, const uint32_t *, const SpanRec *
 template __global__ void k_walk<false>(PRK_WALK_ARGS);
 template __global__ void k_walk<true>(PRK_WALK_ARGS);
 template __global__ void k_pix<false>(PRK_PIX_ARGS);
@@ -1238,8 +1245,8 @@ static size_t shade_lds(const prk::FrameParams *fp) {
 // and k_pix.  won: per bin entry (k_shade frames) or per (pair, row) (AVX
 // frames) won flags; trwon: per triangle; recs: span records, 64 B per
 // (pair, row); tri_off / ranges: the binning's pair offsets and tile ranges.
-hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint32_t *offs, const uint32_t *bins,
-                             const uint32_t *jsorted, const uint32_t *tri_off, const void *ranges, uint8_t *won,
+hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint32_t *offs, const void *bins_,
+                             const uint32_t *pair_tri, const uint32_t *tri_off, const void *ranges, uint8_t *won,
                              uint8_t *trwon, uint32_t *wlist, void *sel_temp, size_t sel_bytes, uint32_t *list,
                              uint32_t *nwin, uint32_t *wtag, void *recs, uint32_t *anomaly, hipEvent_t mid,
                              hipEvent_t mid2, hipStream_t s) {
@@ -1250,10 +1257,11 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
     prk::SpanRec *rp = reinterpret_cast<prk::SpanRec *>(recs);
     const prk::TileRange *tr = reinterpret_cast<const prk::TileRange *>(ranges);
     const uint32_t nblk = (fp->tri_count + 255) / 256;
+    const uint2 *bins = reinterpret_cast<const uint2 *>(bins_);
 #define PRK_VIS(MS, UNI)                                                                                             \
     do {                                                                                                             \
         hipLaunchKernelGGL((prk::k_vis<MS, UNI>), dim3(ntile), dim3(64 * prk::kWaves), lv, s, *fp, offs, bins, won, \
-                           list, nwin, wtag, jsorted, trwon, anomaly);                                              \
+                           list, nwin, wtag, pair_tri, trwon, anomaly);                                              \
         if (mid) (void)hipEventRecord(mid, s);                                                                       \
     } while (0)
 #define PRK_SHADE(MS, UNI)                                                                                           \
@@ -1271,7 +1279,7 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
                                rp, anomaly);                                                                         \
         }                                                                                                            \
         if (mid2) (void)hipEventRecord(mid2, s);                                                                     \
-        hipLaunchKernelGGL((prk::k_pix<UNI>), dim3(ntile), dim3(256), 0, s, *fp, nwin, offs, wtag, jsorted, rp);     \
+        hipLaunchKernelGGL((prk::k_pix<UNI>), dim3(ntile), dim3(256), 0, s, *fp, nwin, wtag, rp);                   \
     } while (0)
     switch (modeset) {
         case prk::MODE_AVX:
