@@ -62,6 +62,8 @@ __device__ __forceinline__ bool tri_tile_range(const FrameParams &fp, uint32_t g
     }
     tr.oty0 = 1;
     tr.oty1 = 0;
+    tr.pad0 = (uint16_t)min(r0 - fp.row0, 65535);  // band rows [r0, r1): the bins' row classes
+    tr.pad1 = (uint16_t)min(r1 - fp.row0, 65535);
     const bool rect = r0 < r1 && c0 < c1;
     if (rect) {
         tr.tx0 = (uint16_t)(c0 / fp.tile_w);
@@ -94,6 +96,8 @@ __device__ __forceinline__ uint32_t range_entries(const TileRange &tr) {
     return n;
 }
 
+constexpr int kRowClassBits = 3;
+
 __global__ void k_bin_count(FrameParams fp, uint32_t *__restrict__ tri_n, TileRange *__restrict__ ranges) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g > fp.tri_count) return;
@@ -109,23 +113,32 @@ __global__ void k_bin_count(FrameParams fp, uint32_t *__restrict__ tri_n, TileRa
     tri_n[g] = range_entries(tr);
 }
 
+// Sort key = tile << kRowClassBits | row class: within a tile's bin the
+// pairs are grouped by how many of the tile's rows the triangle can cover
+// (bin order is free: the pair index breaks visibility ties), so the 64
+// triangles a k_vis wave walks together cover similar row counts.
 __global__ void k_bin_emit(FrameParams fp, const TileRange *__restrict__ ranges, const uint32_t *__restrict__ off,
                            uint32_t *__restrict__ keys, uint2 *__restrict__ vals, uint32_t *__restrict__ pair_tri) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= fp.tri_count) return;
     const TileRange tr = ranges[g];
     uint32_t o = off[g];
+    constexpr int kMaxClass = (1 << kRowClassBits) - 1;
     if (tr.tx0 <= tr.tx1 && tr.ty0 <= tr.ty1)
-        for (int ty = tr.ty0; ty <= tr.ty1; ++ty)
+        for (int ty = tr.ty0; ty <= tr.ty1; ++ty) {
+            const int y0 = ty * fp.tile_h;
+            const int rows = min((int)tr.pad1, y0 + fp.tile_h) - max((int)tr.pad0, y0);
+            const uint32_t cls = (uint32_t)min(kMaxClass, max(0, fp.tile_h - rows));
             for (int tx = tr.tx0; tx <= tr.tx1; ++tx) {
-                keys[o] = (uint32_t)(ty * fp.tiles_x + tx);
+                keys[o] = ((uint32_t)(ty * fp.tiles_x + tx) << kRowClassBits) | cls;
                 vals[o] = make_uint2(g, o);
                 pair_tri[o] = g;
                 ++o;
             }
+        }
     for (int ty = tr.oty0; ty <= tr.oty1; ++ty)
         if (!(tr.tx0 == 0 && tr.tx0 <= tr.tx1 && ty >= tr.ty0 && ty <= tr.ty1)) {
-            keys[o] = (uint32_t)(ty * fp.tiles_x);
+            keys[o] = ((uint32_t)(ty * fp.tiles_x) << kRowClassBits) | (uint32_t)kMaxClass;
             vals[o] = make_uint2(g, o);
             pair_tri[o] = g;
             ++o;
@@ -133,6 +146,7 @@ __global__ void k_bin_emit(FrameParams fp, const TileRange *__restrict__ ranges,
 }
 
 // offs[t] = first sorted position whose tile is >= t, for t in [0, ntiles].
+// (keys carry the row class in their low kRowClassBits bits)
 __global__ void k_tile_offsets(const uint32_t *__restrict__ keys, uint32_t total, uint32_t ntiles,
                                uint32_t *__restrict__ offs) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -140,7 +154,7 @@ __global__ void k_tile_offsets(const uint32_t *__restrict__ keys, uint32_t total
     uint32_t lo = 0, hi = total;
     while (lo < hi) {
         const uint32_t mid = lo + ((hi - lo) >> 1);
-        if (keys[mid] < t) lo = mid + 1; else hi = mid;
+        if ((keys[mid] >> kRowClassBits) < t) lo = mid + 1; else hi = mid;
     }
     offs[t] = lo;
 }
@@ -172,6 +186,7 @@ hipError_t prk_bin_phase2(const prk::FrameParams *fp, const void *ranges, const 
     const uint32_t ntiles = (uint32_t)(fp->tiles_x * fp->tiles_y);
     int bits = 1;
     while ((1u << bits) < ntiles && bits < 32) ++bits;
+    bits += prk::kRowClassBits;
     uint64_t *va = reinterpret_cast<uint64_t *>(vals_a), *vb = reinterpret_cast<uint64_t *>(bins);
     if (!temp)
         return hipcub::DeviceRadixSort::SortPairs(nullptr, *temp_bytes, keys_a, keys_b, va, vb, total, 0, bits, s);

@@ -97,6 +97,7 @@ __device__ __forceinline__ float u8_unit(uint32_t k) {
 // Tiles a triangle may touch: the rectangle [tx0..tx1] x [ty0..ty1], plus
 // for scalar semantics the column-0 tiles of rows [oty0..oty1] that receive
 // DrawModel's one-past-the-row store (see span_setup_scalar).
+// pad0 / pad1: the triangle's band rows [r0, r1) (prk_bin.hip: row classes)
 struct TileRange { uint16_t tx0, ty0, tx1, ty1, oty0, oty1, pad0, pad1; };
 
 // ---------------------------------------------------------------------------
