@@ -38,7 +38,7 @@
 #define PRK_T() 0ull
 #endif
 #ifndef PRK_VIS_MIN_WAVES
-#define PRK_VIS_MIN_WAVES 3  // waves per SIMD k_vis is register-budgeted for
+#define PRK_VIS_MIN_WAVES 4  // waves per SIMD k_vis is register-budgeted for (<= 128 VGPRs)
 #endif
 #ifndef PRK_SPAN_RECORDS
 #define PRK_SPAN_RECORDS 1  // AVX frames shade through k_walk + k_pix (else k_shade)
@@ -83,7 +83,8 @@ __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
 #define PRK_ZPRE 1  // sweep 1: skip 1/w and the UV mask of fragments that cannot raise the key
 #endif
 #ifndef PRK_PREFETCH
-#define PRK_PREFETCH 1  // single-draw sweeps prefetch the next chunk's triangles
+#define PRK_PREFETCH 0  // single-draw sweeps prefetch the next chunk's triangles (costs the
+                        // registers of a 4-wave-per-SIMD k_vis: measured slower)
 #endif
 #ifndef PRK_LANE_ROWS
 #define PRK_LANE_ROWS 1  // sweeps: each lane walks its own rows (no row lock step across the wave)
@@ -94,10 +95,15 @@ __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
 #ifndef PRK_PIXEL_ITEMS
 #define PRK_PIXEL_ITEMS 1  // shading sweep (AVX): one work item per won pixel, not per lane chain
 #endif
-#ifndef PRK_WAVES
-#define PRK_WAVES 2  // waves per tile workgroup; each takes whole 64-entry chunks of the bin
+#ifndef PRK_VIS_WAVES
+// waves per k_vis tile workgroup; each takes whole 64-entry chunks of the bin.
+// Four waves share one 16 KiB key array: 4 workgroups = 16 waves per CU.
+#define PRK_VIS_WAVES 4
 #endif
-constexpr int kWaves = PRK_WAVES;
+#ifndef PRK_SHADE_WAVES
+#define PRK_SHADE_WAVES 2  // waves per k_shade tile workgroup
+#endif
+constexpr int kVisWaves = PRK_VIS_WAVES, kShadeWaves = PRK_SHADE_WAVES;
 constexpr int kSpanF = 22;  // float fields per span slot
 constexpr int kSpanI = 11;  // int fields per span slot
 // (the visibility sweep uses the first kSpanIVis int fields only)
@@ -700,7 +706,8 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
             load_tri<M>(fp.draw0, fp.draw0.geom_tri0 + (ne_g - fp.draw0.first_global), nraw);
         }
     }
-    for (uint32_t base = wave * 64; base < n; base += 64 * kWaves) {
+    const uint32_t nwaves = blockDim.x >> 6;
+    for (uint32_t base = wave * 64; base < n; base += 64 * nwaves) {
         unsigned long long t0 = PRK_T();
         const uint32_t i = base + lane;
         bool active = i < n;
@@ -709,7 +716,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
         RowWalker<M, SHADE> wk;
         uint32_t anom = 0;
         TriRaw<M> craw;
-        const uint32_t inext = i + 64 * kWaves;
+        const uint32_t inext = i + 64 * nwaves;
         if constexpr (kPre) {
             craw = nraw;
             e = ne_e;
@@ -838,7 +845,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *scratc
     __syncthreads();
     uint32_t before = 0;
     total = 0;
-    for (int w = 0; w < kWaves; ++w) {
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
         if (w < wave) before += scratch[w];
         total += scratch[w];
     }
@@ -865,7 +872,7 @@ __device__ __forceinline__ TileCtx tile_ctx(const FrameParams &fp, int t) {
 // Output per tile: the winning entry tag of every pixel (wtag, tile-major),
 // the list of bin entries that won at least one pixel and its length.
 template <int MODESET, bool UNI>
-__global__ void __launch_bounds__(64 * kWaves, PRK_VIS_MIN_WAVES)
+__global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
     k_vis(FrameParams fp, const uint32_t *__restrict__ offs, const uint2 *__restrict__ bins,
           uint8_t *__restrict__ won, uint32_t *__restrict__ list, uint32_t *__restrict__ nwin_out,
           uint32_t *__restrict__ wtag, const uint32_t *__restrict__ pair_tri, uint8_t *__restrict__ trwon,
@@ -888,7 +895,7 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_VIS_MIN_WAVES)
     tc.key = lds;
     VisSlots *slots = reinterpret_cast<VisSlots *>(lds + npx);
     VisSlots &ws = slots[threadIdx.x >> 6];
-    uint32_t *scratch = reinterpret_cast<uint32_t *>(slots + kWaves);
+    uint32_t *scratch = reinterpret_cast<uint32_t *>(slots + kVisWaves);
 
     // Prior z of the target: a fragment must beat it strictly.
     for (int p = threadIdx.x; p < npx; p += blockDim.x) {
@@ -962,7 +969,7 @@ __global__ void __launch_bounds__(64 * kWaves, PRK_VIS_MIN_WAVES)
 // won a pixel and shade exactly the winning fragments.  Winners store their
 // z and colour; untouched pixels keep the prior contents.
 template <int MODESET, bool UNI>
-__global__ void __launch_bounds__(64 * kWaves, PRK_SHADE_MIN_WAVES)
+__global__ void __launch_bounds__(64 * kShadeWaves, PRK_SHADE_MIN_WAVES)
     k_shade(FrameParams fp, const uint32_t *__restrict__ offs, const uint2 *__restrict__ bins,
             const uint32_t *__restrict__ list, const uint32_t *__restrict__ nwin_in,
             const uint32_t *__restrict__ wtag, uint32_t *__restrict__ anomaly) {
@@ -1232,12 +1239,12 @@ hipError_t prk_launch_tri_draw(const prk::DrawRec *draws, uint32_t ndraws, uint3
 
 // Bytes of dynamic LDS per workgroup of k_vis / k_shade.
 static size_t vis_lds(const prk::FrameParams *fp) {
-    return (size_t)fp->tile_w * fp->tile_h * sizeof(unsigned long long) + prk::kWaves * sizeof(prk::VisSlots) +
+    return (size_t)fp->tile_w * fp->tile_h * sizeof(unsigned long long) + prk::kVisWaves * sizeof(prk::VisSlots) +
            16 * sizeof(uint32_t);
 }
 static size_t shade_lds(const prk::FrameParams *fp) {
     const size_t npx = (size_t)fp->tile_w * fp->tile_h;
-    return (npx + prk::kTagPad) * sizeof(uint32_t) + prk::kWaves * sizeof(prk::ShadeSlots);
+    return (npx + prk::kTagPad) * sizeof(uint32_t) + prk::kShadeWaves * sizeof(prk::ShadeSlots);
 }
 
 // Sweep 1 (k_vis) then the shading: k_walk + k_pix for AVX frames, k_shade
@@ -1260,12 +1267,12 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
     const uint2 *bins = reinterpret_cast<const uint2 *>(bins_);
 #define PRK_VIS(MS, UNI)                                                                                             \
     do {                                                                                                             \
-        hipLaunchKernelGGL((prk::k_vis<MS, UNI>), dim3(ntile), dim3(64 * prk::kWaves), lv, s, *fp, offs, bins, won, \
+        hipLaunchKernelGGL((prk::k_vis<MS, UNI>), dim3(ntile), dim3(64 * prk::kVisWaves), lv, s, *fp, offs, bins, won, \
                            list, nwin, wtag, pair_tri, trwon, anomaly);                                              \
         if (mid) (void)hipEventRecord(mid, s);                                                                       \
     } while (0)
 #define PRK_SHADE(MS, UNI)                                                                                           \
-    hipLaunchKernelGGL((prk::k_shade<MS, UNI>), dim3(ntile), dim3(64 * prk::kWaves), ls, s, *fp, offs, bins, list,  \
+    hipLaunchKernelGGL((prk::k_shade<MS, UNI>), dim3(ntile), dim3(64 * prk::kShadeWaves), ls, s, *fp, offs, bins, list,  \
                        nwin, wtag, anomaly)
 #define PRK_SPANPIX(UNI)                                                                                             \
     do {                                                                                                             \
