@@ -1075,72 +1075,152 @@ __device__ __forceinline__ void walk_record(const FrameParams &fp, const Edge &L
     }
 }
 
+// Per-wave queue of won row spans between k_walk's row walk and its record
+// writes: the walk finds a won row on only some lanes in a given step, so the
+// span setup (7 divisions) and the stores run once 64 spans are queued, one
+// per lane.  Entry: both edges' X, W, U, V, z and normal (16 floats), row |
+// texture << 16, the triangle's first pair, its tile rectangle (2 words).
+constexpr int kWalkWaves = 2, kWalkQ = 128;
+struct WalkQueue {
+    float f[16][kWalkQ];
+    int32_t i[4][kWalkQ];
+};
+
+__device__ __forceinline__ void walk_flush(const FrameParams &fp, const WalkQueue &q, int slot,
+                                           const uint8_t *__restrict__ won, SpanRec *__restrict__ recs) {
+    Edge L, R;
+    L.X = q.f[0][slot]; L.W = q.f[1][slot]; L.U = q.f[2][slot]; L.V = q.f[3][slot]; L.Z = q.f[4][slot];
+    L.N0 = q.f[5][slot]; L.N1 = q.f[6][slot]; L.N2 = q.f[7][slot];
+    R.X = q.f[8][slot]; R.W = q.f[9][slot]; R.U = q.f[10][slot]; R.V = q.f[11][slot]; R.Z = q.f[12][slot];
+    R.N0 = q.f[13][slot]; R.N1 = q.f[14][slot]; R.N2 = q.f[15][slot];
+    const int32_t rt = q.i[0][slot];
+    const uint32_t jb = (uint32_t)q.i[1][slot], t0 = (uint32_t)q.i[2][slot], t1 = (uint32_t)q.i[3][slot];
+    TileRange tr;
+    tr.tx0 = (uint16_t)(t0 & 0xFFFF); tr.ty0 = (uint16_t)(t0 >> 16);
+    tr.tx1 = (uint16_t)(t1 & 0xFFFF); tr.ty1 = (uint16_t)(t1 >> 16);
+    walk_record(fp, L, R, rt & 0xFFFF, rt >> 16, tr, jb, (int)tr.tx1 - (int)tr.tx0 + 1, won, recs);
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // k_walk: one thread per triangle that won a pixel.  FillEdgeTable +
 // MergeSort once, then the triangle's whole AET walk (projekt.cpp:3615-3871,
 // normals included) from its first row of the band: no per-tile setup and no
-// replay of the rows above a tile.
+// replay of the rows above a tile.  Won rows go through the wave's queue.
 template <bool UNI>
-__global__ void __launch_bounds__(256) k_walk(FrameParams fp, const uint32_t *__restrict__ wlist,
+__global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams fp, const uint32_t *__restrict__ wlist,
                                               const uint32_t *__restrict__ nwlist,
                                               const uint32_t *__restrict__ tri_off,
                                               const TileRange *__restrict__ ranges, const uint8_t *__restrict__ won,
                                               SpanRec *__restrict__ recs, uint32_t *__restrict__ anomaly) {
     constexpr int M = MODE_AVX;
+    __shared__ WalkQueue queues[kWalkWaves];
+    const int lane = threadIdx.x & 63;
+    WalkQueue &q = queues[threadIdx.x >> 6];
+    const uint32_t nw = *nwlist;
+    if (blockIdx.x * blockDim.x + (threadIdx.x & ~63u) >= nw) return;  // whole wave past the list
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= *nwlist) return;
-    const uint32_t g = wlist[i];  // the triangles that won a pixel (compacted)
-    Edge s0, s1, s2;
-    int ne;
-    int32_t texi;
-    if constexpr (UNI) {
-        ne = setup_triangle<M>(fp.draw0, fp.draw0.geom_tri0 + (g - fp.draw0.first_global), fp, s0, s1, s2);
-        texi = fp.draw0.tex;
-    } else {
-        const DrawRec *d;
-        uint32_t gt;
-        resolve_draw(fp, g, d, gt);
-        ne = setup_triangle<M>(*d, gt, fp, s0, s1, s2);
-        texi = d->tex;
-    }
-    if (ne < 2) return;
-    uint32_t anom = 0;
-    Walker<M, true> w0;
-    w0.init(ne, s0, s1, s2, fp.H, fp.row1, anom);
-    const int fr = w0.fast_replay(fp.row0, ne);  // band above row0 (row bands only)
+    bool active = i < nw;
+    const uint32_t g = active ? wlist[i] : 0u;  // the triangles that won a pixel (compacted)
     RowWalker<M, true> wk;
-    wk.from(w0);
-    if (fr < 0)
-        while (wk.Row < fp.row0 && wk.Row < wk.MaxY) wk.end_row(wk.begin_row());
-    if (anom) atomicAdd(anomaly, anom);
-    const TileRange tr = ranges[g];
-    const uint32_t jb = tri_off[g];
-    const int ntx = (int)tr.tx1 - (int)tr.tx0 + 1, nty = (int)tr.ty1 - (int)tr.ty0 + 1;
-    // Rows that won a pixel in any tile, as bits over the triangle's tile rows
-    // (8-row tiles, <= 8 pairs): the won flags of a pair are 8 consecutive
-    // bytes, loaded together up front instead of one dependent load per row.
-    const int32_t rbase = fp.row0 + (int32_t)tr.ty0 * fp.tile_h;
-    const bool fast = fp.tile_h == 8 && ntx * nty <= 8;
+    int32_t texi = 0;
+    TileRange tr{};
+    uint32_t jb = 0;
     uint64_t rows = ~0ull;
-    if (fast) {
-        uint64_t m[8];
+    int32_t rbase = 0;
+    bool fast = false;
+    if (active) {
+        Edge s0, s1, s2;
+        int ne;
+        if constexpr (UNI) {
+            ne = setup_triangle<M>(fp.draw0, fp.draw0.geom_tri0 + (g - fp.draw0.first_global), fp, s0, s1, s2);
+            texi = fp.draw0.tex;
+        } else {
+            const DrawRec *d;
+            uint32_t gt;
+            resolve_draw(fp, g, d, gt);
+            ne = setup_triangle<M>(*d, gt, fp, s0, s1, s2);
+            texi = d->tex;
+        }
+        active = ne >= 2;
+        if (active) {
+            uint32_t anom = 0;
+            Walker<M, true> w0;
+            w0.init(ne, s0, s1, s2, fp.H, fp.row1, anom);
+            const int fr = w0.fast_replay(fp.row0, ne);  // band above row0 (row bands only)
+            wk.from(w0);
+            if (fr < 0)
+                while (wk.Row < fp.row0 && wk.Row < wk.MaxY) wk.end_row(wk.begin_row());
+            if (anom) atomicAdd(anomaly, anom);
+            active = wk.Row < wk.MaxY;
+            tr = ranges[g];
+            jb = tri_off[g];
+            const int ntx = (int)tr.tx1 - (int)tr.tx0 + 1, nty = (int)tr.ty1 - (int)tr.ty0 + 1;
+            // Rows that won a pixel in any tile, as bits over the triangle's
+            // tile rows (8-row tiles, <= 8 pairs): the won flags of a pair are
+            // 8 consecutive bytes, loaded together up front.
+            rbase = fp.row0 + (int32_t)tr.ty0 * fp.tile_h;
+            fast = fp.tile_h == 8 && ntx * nty <= 8;
+            if (fast) {
+                uint64_t m[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-            m[k] = k < ntx * nty ? *reinterpret_cast<const uint64_t *>(won + (size_t)(jb + k) * 8) : 0ull;
-        rows = 0;
+                for (int k = 0; k < 8; ++k)
+                    m[k] = k < ntx * nty ? *reinterpret_cast<const uint64_t *>(won + (size_t)(jb + k) * 8) : 0ull;
+                rows = 0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int ty = k / ntx;  // pair k = (ty, tx) row-major
-            rows |= ((m[k] * 0x0102040810204080ull) >> 56) << (8 * ty);  // bytes (0/1) -> bits
+                for (int k = 0; k < 8; ++k) {
+                    const int ty = k / ntx;  // pair k = (ty, tx) row-major
+                    rows |= ((m[k] * 0x0102040810204080ull) >> 56) << (8 * ty);  // bytes (0/1) -> bits
+                }
+            }
         }
     }
-    while (wk.Row < wk.MaxY) {
-        const int32_t Row = wk.Row;
-        const bool paired = wk.begin_row();
-        const int32_t rb = Row - rbase;
-        const bool want = !fast || (rb >= 0 && rb < 64 && ((rows >> rb) & 1ull));
-        if (paired && want) walk_record(fp, wk.S0, wk.S1, Row, texi, tr, jb, ntx, won, recs);
-        wk.end_row(paired);
+    const int32_t t0 = (int32_t)((uint32_t)tr.tx0 | ((uint32_t)tr.ty0 << 16));
+    const int32_t t1 = (int32_t)((uint32_t)tr.tx1 | ((uint32_t)tr.ty1 << 16));
+    uint32_t head = 0, cnt = 0;  // wave-uniform queue state
+    while (__any(active)) {
+        bool push = false, paired = false;
+        int32_t Row = 0;
+        if (active) {
+            Row = wk.Row;
+            paired = wk.begin_row();
+            const int32_t rb = Row - rbase;
+            const bool want = !fast || (rb >= 0 && rb < 64 && ((rows >> rb) & 1ull));
+            push = paired && want && Row >= fp.row0;
+        }
+        const uint64_t bal = __ballot(push);
+        if (push) {
+            const uint32_t slot = (head + cnt + (uint32_t)__builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))) & (kWalkQ - 1);
+            const Edge &L = wk.S0, &R = wk.S1;
+            q.f[0][slot] = L.X; q.f[1][slot] = L.W; q.f[2][slot] = L.U; q.f[3][slot] = L.V; q.f[4][slot] = L.Z;
+            q.f[5][slot] = L.N0; q.f[6][slot] = L.N1; q.f[7][slot] = L.N2;
+            q.f[8][slot] = R.X; q.f[9][slot] = R.W; q.f[10][slot] = R.U; q.f[11][slot] = R.V; q.f[12][slot] = R.Z;
+            q.f[13][slot] = R.N0; q.f[14][slot] = R.N1; q.f[15][slot] = R.N2;
+            q.i[0][slot] = (Row & 0xFFFF) | (texi << 16);
+            q.i[1][slot] = (int32_t)jb;
+            q.i[2][slot] = t0;
+            q.i[3][slot] = t1;
+        }
+        cnt += (uint32_t)__popcll(bal);
+        if (active) {
+            wk.end_row(paired);
+            active = wk.Row < wk.MaxY;
+        }
+        if (cnt >= 64) {  // one queued span per lane
+            wave_lds_sync();
+            walk_flush(fp, q, (int)((head + lane) & (kWalkQ - 1)), won, recs);
+            wave_lds_sync();
+            head += 64;
+            cnt -= 64;
+        }
     }
+    wave_lds_sync();
+    if ((uint32_t)lane < cnt) walk_flush(fp, q, (int)((head + lane) & (kWalkQ - 1)), won, recs);
 }
 
 // k_pix: shade the won pixels of one tile from their span records.
@@ -1264,6 +1344,7 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
     prk::SpanRec *rp = reinterpret_cast<prk::SpanRec *>(recs);
     const prk::TileRange *tr = reinterpret_cast<const prk::TileRange *>(ranges);
     const uint32_t nblk = (fp->tri_count + 255) / 256;
+    const uint32_t nwblk = (fp->tri_count + 64 * prk::kWalkWaves - 1) / (64 * prk::kWalkWaves);
     const uint2 *bins = reinterpret_cast<const uint2 *>(bins_);
 #define PRK_VIS(MS, UNI)                                                                                             \
     do {                                                                                                             \
@@ -1282,7 +1363,8 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
             hipError_t e_ = hipcub::DeviceSelect::Flagged(sel_temp, sel_bytes, hipcub::CountingInputIterator<uint32_t>(0u), \
                                                           trwon, wlist, nsel, fp->tri_count, s);                    \
             if (e_ != hipSuccess) return e_;                                                                         \
-            hipLaunchKernelGGL((prk::k_walk<UNI>), dim3(nblk), dim3(256), 0, s, *fp, wlist, nsel, tri_off, tr, won, \
+            hipLaunchKernelGGL((prk::k_walk<UNI>), dim3(nwblk), dim3(64 * prk::kWalkWaves), 0, s, *fp, wlist, nsel,     \
+                               tri_off, tr, won,                                                                     \
                                rp, anomaly);                                                                         \
         }                                                                                                            \
         if (mid2) (void)hipEventRecord(mid2, s);                                                                     \
