@@ -43,6 +43,12 @@
 #ifndef PRK_SPAN_RECORDS
 #define PRK_SPAN_RECORDS 1  // AVX frames shade through k_walk + k_pix (else k_shade)
 #endif
+#ifndef PRK_WALK_MIN_WAVES
+#define PRK_WALK_MIN_WAVES 4  // waves per SIMD k_walk is register-budgeted for
+#endif
+#ifndef PRK_PIX_SPLIT
+#define PRK_PIX_SPLIT 1  // k_pix workgroups per tile
+#endif
 #ifndef PRK_SHADE_MIN_WAVES
 #define PRK_SHADE_MIN_WAVES 3  // waves per SIMD k_shade is register-budgeted for
 #endif
@@ -1112,7 +1118,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // normals included) from its first row of the band: no per-tile setup and no
 // replay of the rows above a tile.  Won rows go through the wave's queue.
 template <bool UNI>
-__global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams fp, const uint32_t *__restrict__ wlist,
+__global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(FrameParams fp, const uint32_t *__restrict__ wlist,
                                               const uint32_t *__restrict__ nwlist,
                                               const uint32_t *__restrict__ tri_off,
                                               const TileRange *__restrict__ ranges, const uint8_t *__restrict__ won,
@@ -1227,14 +1233,16 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams fp, const 
 template <bool UNI>
 __global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__restrict__ nwin_in,
                                              const uint32_t *__restrict__ wtag, const SpanRec *__restrict__ recs) {
+    // PRK_PIX_SPLIT workgroups per tile, each a contiguous share of its pixels
     const int ntile = fp.tiles_x * fp.tiles_y;
-    const int t = blockIdx.x;
+    const int t = blockIdx.x / PRK_PIX_SPLIT, part = blockIdx.x - t * PRK_PIX_SPLIT;
     if (t >= ntile) return;
     if (nwin_in[t] == 0) return;
     const TileCtx tc = tile_ctx(fp, t);
     const int npx = fp.tile_w * fp.tile_h;
     const uint32_t *tags = wtag + (size_t)t * npx;
-    for (int p = threadIdx.x; p < npx; p += blockDim.x) {
+    const int pend = (int)(((long long)npx * (part + 1)) / PRK_PIX_SPLIT);
+    for (int p = (int)(((long long)npx * part) / PRK_PIX_SPLIT) + threadIdx.x; p < pend; p += blockDim.x) {
         const uint32_t tag = tags[p];
         if (tag == 0xFFFFFFFFu) continue;  // no fragment beat the prior z
         const int ly = p >> fp.tile_w_log2;
@@ -1368,7 +1376,7 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
                                rp, anomaly);                                                                         \
         }                                                                                                            \
         if (mid2) (void)hipEventRecord(mid2, s);                                                                     \
-        hipLaunchKernelGGL((prk::k_pix<UNI>), dim3(ntile), dim3(256), 0, s, *fp, nwin, wtag, rp);                   \
+        hipLaunchKernelGGL((prk::k_pix<UNI>), dim3(ntile * PRK_PIX_SPLIT), dim3(256), 0, s, *fp, nwin, wtag, rp);   \
     } while (0)
     switch (modeset) {
         case prk::MODE_AVX:
