@@ -6,8 +6,9 @@ triangles (vertex offsets +-16 px), Phong + 256^2 texture, one light, drawn with
 FillLineOptimized semantics (DrawModelOptimized(RenderQueue,...) +
 FillLineOptimized, projekt.cpp:3615-3871 / 1492-2320), per-triangle submission.
 
-One step = one frame: clear colour + z, then bin + raster + shade every
-triangle into the frame (inputs already resident in HBM).  With N GPUs the
+One step = one frame: clear colour + z (fused into the frame's kernels,
+prk_target_clear_on_flush), then bin + raster + shade every triangle into the
+frame (inputs already resident in HBM).  With N GPUs the
 frame is split into N row bands (rank r owns rows [r*H/N, (r+1)*H/N)), every
 rank bins all triangles against its band, and the colour strips are gathered
 to rank 0 over RCCL ("scaling": "strong": total work fixed).
@@ -48,11 +49,12 @@ def parse():
 
 
 def algorithmic_bytes(T, W, rows, tex_texels):
-    """Bytes k_raster must move at minimum per frame:
-    positions+normals+uvs read once (96 B/triangle; FillLineOptimized never
-    reads vertex colours), prior z read + z and colour written (12 B/pixel),
+    """Bytes the frame must move at minimum: positions +
+    normals + uvs read once (96 B/triangle; FillLineOptimized never reads
+    vertex colours), z and colour of every pixel written once (8 B/pixel: the
+    frame starts from a clear, fused into its kernels, so no prior z is read),
     the texture read once."""
-    return 96 * T + 12 * W * rows + 4 * tex_texels
+    return 96 * T + 8 * W * rows + 4 * tex_texels
 
 
 def load_traffic(cfg_key):
@@ -170,8 +172,9 @@ def main():
     zmin = -float(np.finfo(np.float32).max)
 
     def step():
-        color.fill_(int(np.int32(np.uint32(0xFF000000).view(np.int32))))
-        zbuf.fill_(zmin)
+        # clear colour + z (the reference's clear values), fused into the
+        # frame's kernels: every pixel of the band is written by the frame
+        r.clear_on_flush(0xFF000000, zmin)
         r.draw_model_optimized(geom, scene.tri_count, bitmap=tex, phong=True)
         r.complete_all_work(stream)
         if world > 1:  # RCCL over xGMI: strips -> rank 0's frame

@@ -31,6 +31,10 @@ hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, co
 hipError_t prk_walk_select_bytes(uint32_t, size_t *);
 }
 
+// AVX frames shade through span records (k_walk + k_pix); must match
+// PRK_SPAN_RECORDS of prk_kernels.hip.
+#define PRK_SPAN_RECORDS_HOST 1
+
 namespace {
 
 struct DevBuf {
@@ -86,6 +90,9 @@ struct prk_context {
     prk_transform transform{};
     prk_light_data lights{};
     bool have_camera = false;
+    bool clear_pending = false;  // prk_target_clear_on_flush
+    uint32_t clear_color = 0;
+    float clear_z = 0.0f;
     // resources
     std::vector<Geometry> geoms;
     std::vector<Texture> texs;
@@ -255,6 +262,15 @@ int prk_target_clear(prk_context *c, uint32_t color, float z) {
     hipLaunchKernelGGL(k_fill_target, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->own_stream,
                        (uint32_t *)c->color, c->pitch, c->zbuf, c->W, c->row1 - c->row0, color, z);
     PRK_TRY(hipGetLastError());
+    return PRK_OK;
+}
+
+int prk_target_clear_on_flush(prk_context *c, uint32_t color, float z) {
+    if (!c) return PRK_ERR_ARG;
+    if (!c->color) return PRK_ERR_NO_TARGET;
+    c->clear_pending = true;
+    c->clear_color = color;
+    c->clear_z = z;
     return PRK_OK;
 }
 
@@ -546,6 +562,22 @@ int prk_flush(prk_context *c, void *stream) {
         fp.winners = (int32_t *)c->d_winners.p;
         c->winners_valid = true;
     }
+    // A pending fused clear: the span-record kernels (AVX frames) fold it in;
+    // every other frame fills the target first, on this stream.
+    const bool fuse = c->clear_pending && T > 0 && modeset == prk::MODE_AVX && PRK_SPAN_RECORDS_HOST;
+    if (c->clear_pending && !fuse) {
+        size_t n = (size_t)c->W * (c->row1 - c->row0);
+        if (n) {
+            hipLaunchKernelGGL(k_fill_target, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                               (uint32_t *)c->color, c->pitch, c->zbuf, c->W, c->row1 - c->row0, c->clear_color,
+                               c->clear_z);
+            PRK_TRY(hipGetLastError());
+        }
+    }
+    c->clear_pending = false;
+    fp.clear_fused = fuse ? 1 : 0;
+    fp.clear_color = c->clear_color;
+    fp.clear_z = c->clear_z;
     if (T == 0) {
         c->draws.clear();
         c->pending_tris = 0;

@@ -59,6 +59,10 @@ struct FrameParams {
     uint32_t *color; // points at frame row row0
     float *zbuf;     // points at frame row row0 (row stride W floats)
     int32_t *winners;// optional (debug): per pixel winning triangle, -1 none
+    // fused clear (prk_target_clear_on_flush): prior contents are (clear_color, clear_z)
+    int32_t clear_fused;
+    uint32_t clear_color;
+    float clear_z;
     unsigned long long *prof;  // 16 phase-cycle counters (PRK_PROF builds only write them)
     // tiling
     int32_t tile_w, tile_h, tiles_x, tiles_y;

@@ -909,7 +909,7 @@ __global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
         const int x = tc.x0 + lx, y = tc.y0 + ly;
         unsigned long long k = ~0ull;
         if (x < tc.x1 && y < tc.y1) {
-            const float z = fp.zbuf[(size_t)(y - fp.row0) * fp.W + x];
+            const float z = fp.clear_fused ? fp.clear_z : fp.zbuf[(size_t)(y - fp.row0) * fp.W + x];
             k = (z != z) ? ~0ull : (((unsigned long long)zkey(z) << 32) | 0xFFFFFFFFull);
         }
         tc.key[p] = k;
@@ -1237,16 +1237,20 @@ __global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__r
     const int ntile = fp.tiles_x * fp.tiles_y;
     const int t = blockIdx.x / PRK_PIX_SPLIT, part = blockIdx.x - t * PRK_PIX_SPLIT;
     if (t >= ntile) return;
-    if (nwin_in[t] == 0) return;
+    const bool any = nwin_in[t] != 0;  // (k_vis leaves the tags of a tile without entries unwritten)
+    if (!any && !fp.clear_fused) return;
     const TileCtx tc = tile_ctx(fp, t);
     const int npx = fp.tile_w * fp.tile_h;
     const uint32_t *tags = wtag + (size_t)t * npx;
     const int pend = (int)(((long long)npx * (part + 1)) / PRK_PIX_SPLIT);
     for (int p = (int)(((long long)npx * part) / PRK_PIX_SPLIT) + threadIdx.x; p < pend; p += blockDim.x) {
-        const uint32_t tag = tags[p];
-        if (tag == 0xFFFFFFFFu) continue;  // no fragment beat the prior z
+        const uint32_t tag = any ? tags[p] : 0xFFFFFFFFu;
         const int ly = p >> fp.tile_w_log2;
         const int32_t x = tc.x0 + (p & (fp.tile_w - 1)), Row = tc.y0 + ly;
+        if (tag == 0xFFFFFFFFu) {  // no fragment beat the prior z
+            if (fp.clear_fused && x < tc.x1 && Row < tc.y1) put_winner(fp, x, Row, fp.clear_z, fp.clear_color);
+            continue;
+        }
         const uint32_t j = 0xFFFFFFFEu - tag;  // the winning pair
         const float4 *q = reinterpret_cast<const float4 *>(recs + (size_t)j * fp.tile_h + ly);
         const float4 r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];

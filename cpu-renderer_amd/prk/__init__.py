@@ -45,6 +45,7 @@ _SIGS = {
     "prk_target_alloc": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                    C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
     "prk_target_clear": (C.c_int, [C.c_void_p, C.c_uint32, C.c_float]),
+    "prk_target_clear_on_flush": (C.c_int, [C.c_void_p, C.c_uint32, C.c_float]),
     "prk_target_download": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
     "prk_target_upload": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
     "prk_set_camera": (C.c_int, [C.c_void_p, C.POINTER(abi.PrkTransform), C.POINTER(abi.PrkLightData)]),
@@ -157,6 +158,12 @@ class Renderer:
         z = -float(np.finfo(np.float32).max) if z is None else z
         _check("prk_target_clear", self._L.prk_target_clear(self._h, C.c_uint32(color), C.c_float(z)))
 
+    def clear_on_flush(self, color=0xFF000000, z=None):
+        """The same fill, fused into the next complete_all_work()."""
+        z = -float(np.finfo(np.float32).max) if z is None else z
+        _check("prk_target_clear_on_flush",
+               self._L.prk_target_clear_on_flush(self._h, C.c_uint32(color), C.c_float(z)))
+
     def upload(self, color, z):
         color = np.ascontiguousarray(color, np.uint32)
         z = np.ascontiguousarray(z, np.float32)
@@ -260,9 +267,11 @@ class Renderer:
 
 
 def render_scene(scene, semantics=abi.PRK_SEM_AVX, phong=True, device=0, tile=None, debug=True,
-                 color=None, z=None, rows=None):
+                 color=None, z=None, rows=None, fused_clear=False):
     """Convenience: draw a whole scenes.Scene (per-triangle submission) and
-    return (color, z, winners or None, stats)."""
+    return (color, z, winners or None, stats).  fused_clear: upload
+    color / z, then clear through prk_target_clear_on_flush (the frame must
+    overwrite them)."""
     r = Renderer(device)
     try:
         r0, r1 = (0, scene.height) if rows is None else rows
@@ -271,6 +280,8 @@ def render_scene(scene, semantics=abi.PRK_SEM_AVX, phong=True, device=0, tile=No
             r.clear()
         else:
             r.upload(color[r0:r1], z[r0:r1])
+        if fused_clear:
+            r.clear_on_flush()
         if tile:
             r.set_tile(*tile)
         r.set_debug(debug)

@@ -141,6 +141,12 @@ int prk_target_alloc(prk_context *ctx, int32_t width, int32_t height, int32_t ro
 /* Fill the bound target: colour with `color`, z with `z` (reference callers
  * clear z to -FLT_MAX). */
 int prk_target_clear(prk_context *ctx, uint32_t color, float z);
+/* The same fill, fused into the next prk_flush: the frame's kernels take
+ * (color, z) as the target's prior contents and write every pixel of the
+ * target (the winners shaded, the rest the fill values), so no separate
+ * fill pass runs.  Frames that do not shade through span records (scalar or
+ * mixed semantics) and empty flushes fill first, on the flush's stream. */
+int prk_target_clear_on_flush(prk_context *ctx, uint32_t color, float z);
 /* Copy the bound target to/from host memory (rows [row0,row1)). */
 int prk_target_download(prk_context *ctx, uint32_t *color_host, int32_t host_pitch_bytes,
                         float *z_host);

@@ -129,6 +129,41 @@ def test_prior_contents_two_flushes(gpu):
     assert (gw2 == ow2).all()
 
 
+@pytest.mark.parametrize("tile", [None, (128, 64)])
+@pytest.mark.parametrize("W,H", [(256, 256), (200, 150)])
+def test_fused_clear(gpu, W, H, tile):
+    """prk_target_clear_on_flush: the AVX frame's kernels write every pixel of
+    the target (edge tiles, tiles no triangle touches) over stale contents."""
+    s = scenes.random_soup(3000, W, H, radius=16, seed=41)
+    rng = np.random.default_rng(5)
+    stale_c = rng.integers(0, 2**32, (H, W), dtype=np.uint32)
+    stale_z = np.full((H, W), 1e30, np.float32)  # would block every fragment if kept
+    g = prk.render_scene(s, color=stale_c, z=stale_z, fused_clear=True, tile=tile)
+    compare(g, O.render(s), label="fused clear %dx%d" % (W, H))
+
+
+def test_fused_clear_fallbacks(gpu):
+    """Scalar frames and empty flushes fill first instead of fusing."""
+    s = scenes.random_soup(2000, 256, 192, radius=16, seed=43, textured=False)
+    stale_c = np.full((192, 256), 0x12345678, np.uint32)
+    stale_z = np.full((192, 256), 1e30, np.float32)
+    g = prk.render_scene(s, semantics=abi.PRK_SEM_SCALAR, phong=False, color=stale_c, z=stale_z,
+                         fused_clear=True)
+    compare(g, O.render(s, semantics=abi.PRK_SEM_SCALAR, phong=False), label="fused clear scalar")
+    r = prk.Renderer(0)
+    try:
+        r.target_alloc(64, 32)
+        r.upload(np.full((32, 64), 7, np.uint32), np.full((32, 64), 3.0, np.float32))
+        r.set_camera(s.prk_transform(), s.prk_lights())
+        r.clear_on_flush(0xFF000000)
+        r.complete_all_work()
+        r.synchronize()
+        c, z = r.download()
+        assert (c == 0xFF000000).all() and (z == -np.finfo(np.float32).max).all()
+    finally:
+        r.close()
+
+
 def test_row_band(gpu):
     s = scenes.random_soup(10000, 512, 512, radius=20, seed=17)
     oc, oz, ow, _ = O.render(s)
