@@ -104,7 +104,7 @@ typedef struct prk_stats {
     uint32_t tiles;          /* tiles in the render target band        */
     uint32_t frames_timed;   /* flushes accumulated in sum_ms_*        */
     float ms_bin;            /* last flush: project/cull/bin kernels   */
-    float ms_raster;         /* last flush: k_vis + k_shade            */
+    float ms_raster;         /* last flush: k_vis + shading kernels    */
     double sum_ms_bin;       /* accumulated since prk_timing_reset     */
     double sum_ms_raster;
     uint32_t anomalies;      /* triangles whose AET left the proven
@@ -115,8 +115,8 @@ typedef struct prk_stats {
                                 anomalies */
     double sum_ms_vis;       /* accumulated: the k_vis (visibility) part
                                 of sum_ms_raster */
-    double sum_ms_span;      /* accumulated: the k_span part (AVX frames:
-                                raster = k_vis + k_span + k_pix) */
+    double sum_ms_span;      /* accumulated: the k_walk part (AVX frames:
+                                raster = k_vis + k_walk + k_pix) */
 } prk_stats;
 
 typedef struct prk_context prk_context;
