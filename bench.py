@@ -151,9 +151,16 @@ def main():
     row0, row1 = band_rows(rank, world, H)
     rows = row1 - row0
 
-    frame = torch.empty((H, W), dtype=torch.int32, device=dev) if (world > 1 and rank == 0) else None
+    # N > 1: two strip (and, on rank 0, frame) buffers, so frame k's RCCL
+    # gather runs on the communicator's stream while frame k+1 renders into the
+    # other buffer; a buffer is reused only after its gather completed.
+    nbuf = 2 if world > 1 else 1
+    frames = [torch.empty((H, W), dtype=torch.int32, device=dev) if (world > 1 and rank == 0) else None
+              for _ in range(nbuf)]
     # rank 0 renders its band straight into its slice of the gathered frame
-    color = frame[row0:row1] if frame is not None else torch.empty((rows, W), dtype=torch.int32, device=dev)
+    colors = [f[row0:row1] if f is not None else torch.empty((rows, W), dtype=torch.int32, device=dev)
+              for f in frames]
+    color = colors[0]
     zbuf = torch.empty((rows, W), dtype=torch.float32, device=dev)
     r = prk.Renderer(dev)
     r.target_bind(color.data_ptr(), W * 4, zbuf.data_ptr(), W, H, row0, row1)
@@ -171,17 +178,34 @@ def main():
     from prk import dist as pdist
     zmin = -float(np.finfo(np.float32).max)
 
+    pending = [[] for _ in range(nbuf)]
+    nstep = [0]
+
     def step():
+        b = nstep[0] % nbuf
+        nstep[0] += 1
+        for req in pending[b]:  # this buffer's previous gather has landed
+            req.wait()
+        pending[b] = []
+        if nbuf > 1:
+            r.target_bind(colors[b].data_ptr(), W * 4, zbuf.data_ptr(), W, H, row0, row1)
         # clear colour + z (the reference's clear values), fused into the
         # frame's kernels: every pixel of the band is written by the frame
         r.clear_on_flush(0xFF000000, zmin)
         r.draw_model_optimized(geom, scene.tri_count, bitmap=tex, phong=True)
         r.complete_all_work(stream)
         if world > 1:  # RCCL over xGMI: strips -> rank 0's frame
-            pdist.gather_strips(dist, color, rank, world, H, out=frame)
+            _, pending[b] = pdist.gather_strips_start(dist, colors[b], rank, world, H, out=frames[b])
+
+    def drain():
+        for b in range(nbuf):
+            for req in pending[b]:
+                req.wait()
+            pending[b] = []
 
     for _ in range(a.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -190,6 +214,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
+    drain()  # every frame's gather is inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -17,14 +17,26 @@ def max_band_rows(world, height):
 
 
 def gather_strips(dist, strip, rank, world, height, out=None):
+    """Blocking form of gather_strips_start: the current stream (GPU) or the
+    host (CPU) waits for the gather."""
+    out, reqs = gather_strips_start(dist, strip, rank, world, height, out=out)
+    for req in reqs:
+        req.wait()
+    return out
+
+
+def gather_strips_start(dist, strip, rank, world, height, out=None):
     """Gather every rank's [rows_r, W] strip into rank 0's [H, W] frame.
 
     Point to point: every rank r > 0 sends its strip to rank 0, which
     receives it straight into its slice of the frame (one message per peer,
     each on its own xGMI link; no padding, no all-gather of the whole frame
     to every rank).  Rank 0's own strip is copied unless it already is that
-    slice (bench.py renders rank 0's band in place).  Returns the frame on
-    rank 0, None elsewhere."""
+    slice (bench.py renders rank 0's band in place).  Returns (the frame on
+    rank 0 / None elsewhere, the pending requests): on RCCL the transfers run
+    on the communicator's stream, so rendering the next frame into another
+    strip buffer overlaps them; req.wait() orders the current stream after
+    them (call it before the strip or frame is reused)."""
     import torch
 
     W = strip.shape[1]
@@ -40,7 +52,5 @@ def gather_strips(dist, strip, rank, world, height, out=None):
             ops.append(dist.P2POp(dist.irecv, out[a:b], r))
     else:
         ops = [dist.P2POp(dist.isend, strip.contiguous(), 0)]
-    if ops:
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
-    return out if rank == 0 else None
+    reqs = dist.batch_isend_irecv(ops) if ops else []
+    return (out if rank == 0 else None), reqs

@@ -46,3 +46,15 @@ def test_gloo_band_gather_matches_single_rank(tmp_path, world, sem):
     assert (got["color"] == col).all()
     assert (got["z"].view(np.uint32) == z.view(np.uint32)).all()
     assert (got["winners"] == win).all()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_overlapped_double_buffered_gather(world):
+    """bench.py's N > 1 loop: gathers left in flight while the next frame is
+    drawn into the other buffer land intact."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "tests", "dist_overlap_worker.py"), "7"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
