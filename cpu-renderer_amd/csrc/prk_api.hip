@@ -98,10 +98,19 @@ struct prk_context {
     std::vector<Texture> texs;
     std::vector<prk::DrawRec> draws;
     uint32_t pending_tris = 0;
-    // scratch
-    DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_tri_n, d_tri_off, d_pair_tri, d_keys_a, d_vals_a, d_keys_b, d_bins,
-        d_offs, d_won, d_list, d_temp, d_winners, d_anomaly, d_nwin, d_wtag, d_prof, d_recs,
-        d_trwon, d_wlist, d_seltemp;
+    // Binning scratch, two sets: frame k bins into set k % 2 on bin_stream
+    // while frame k-1 rasterises on the flush's stream.
+    struct BinSet {
+        DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_tri_n, d_tri_off, d_pair_tri, d_keys_a, d_vals_a, d_keys_b,
+            d_bins, d_offs, d_temp;
+        hipEvent_t free_ev = nullptr;    // the raster that read this set is done
+        hipEvent_t binned_ev = nullptr;  // this set's binning is done
+        bool used = false;
+    };
+    BinSet bset[2];
+    hipStream_t bin_stream = nullptr;
+    // raster scratch (the flush's stream only)
+    DevBuf d_won, d_list, d_winners, d_anomaly, d_nwin, d_wtag, d_prof, d_recs, d_trwon, d_wlist, d_seltemp;
     uint32_t *h_total = nullptr;  // pinned
     int32_t tile_w = 256, tile_h = 8;  // measured best for C3b
     bool debug = false;
@@ -109,7 +118,9 @@ struct prk_context {
     prk_stats stats{};
     // Timing ring: 3 events per flush (before bin, before raster, after raster).
     static constexpr int kRing = 32;
-    hipEvent_t ev[kRing][5] = {};  // bin start, raster start, raster end, k_vis end, k_span end
+    // bin start, bin end (bin_stream); raster end, k_vis end, k_walk end,
+    // raster start (flush stream)
+    hipEvent_t ev[kRing][6] = {};
     bool pending[kRing] = {};
     bool split_span[kRing] = {};  // the slot's flush ran k_span + k_pix
     uint32_t frame = 0;
@@ -146,8 +157,13 @@ int prk_create(int device, prk_context **out) {
     if (!c) return PRK_ERR_NOMEM;
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->bin_stream, hipStreamNonBlocking);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+        e = hipEventCreateWithFlags(&c->bset[i].free_ev, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->bset[i].binned_ev, hipEventDisableTiming);
+    }
     for (int i = 0; i < prk_context::kRing && e == hipSuccess; ++i)
-        for (int k = 0; k < 5 && e == hipSuccess; ++k) e = hipEventCreate(&c->ev[i][k]);
+        for (int k = 0; k < 6 && e == hipSuccess; ++k) e = hipEventCreate(&c->ev[i][k]);
     if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_total, sizeof(uint32_t), hipHostMallocDefault);
     if (e != hipSuccess) {
         prk_destroy(c);
@@ -161,6 +177,7 @@ int prk_destroy(prk_context *c) {
     if (!c) return PRK_ERR_ARG;
     (void)hipSetDevice(c->device);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+    (void)hipDeviceSynchronize();
     for (auto &g : c->geoms)
         if (g.owned) {
             (void)hipFree((void *)g.V);
@@ -173,16 +190,22 @@ int prk_destroy(prk_context *c) {
         (void)hipFree(c->color);
         (void)hipFree(c->zbuf);
     }
-    DevBuf *bufs[] = {&c->d_draws,  &c->d_texs,   &c->d_tri_draw, &c->d_ranges, &c->d_tri_n, &c->d_tri_off,
-                      &c->d_pair_tri, &c->d_keys_a, &c->d_vals_a, &c->d_keys_b, &c->d_bins, &c->d_offs, &c->d_won,
-                      &c->d_list,   &c->d_temp,   &c->d_winners,  &c->d_anomaly, &c->d_nwin, &c->d_wtag, &c->d_prof,
-                      &c->d_recs,   &c->d_trwon,  &c->d_wlist,    &c->d_seltemp};
+    for (auto &B : c->bset) {
+        DevBuf *bb[] = {&B.d_draws, &B.d_texs, &B.d_tri_draw, &B.d_ranges, &B.d_tri_n, &B.d_tri_off, &B.d_pair_tri,
+                        &B.d_keys_a, &B.d_vals_a, &B.d_keys_b, &B.d_bins, &B.d_offs, &B.d_temp};
+        for (DevBuf *b : bb) b->release();
+        if (B.free_ev) (void)hipEventDestroy(B.free_ev);
+        if (B.binned_ev) (void)hipEventDestroy(B.binned_ev);
+    }
+    DevBuf *bufs[] = {&c->d_won,     &c->d_list, &c->d_winners, &c->d_anomaly, &c->d_nwin,  &c->d_wtag,
+                      &c->d_prof,    &c->d_recs, &c->d_trwon,   &c->d_wlist,   &c->d_seltemp};
     for (DevBuf *b : bufs) b->release();
     if (c->h_total) (void)hipHostFree(c->h_total);
     for (auto &slot : c->ev)
         for (auto &e : slot)
             if (e) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    if (c->bin_stream) (void)hipStreamDestroy(c->bin_stream);
     delete c;
     return PRK_OK;
 }
@@ -459,8 +482,8 @@ static void harvest(prk_context *c, int slot) {
     if (hipEventSynchronize(c->ev[slot][2]) != hipSuccess) return;
     float a = 0, b = 0, v = 0, sp = 0;
     if (hipEventElapsedTime(&a, c->ev[slot][0], c->ev[slot][1]) != hipSuccess) a = 0;
-    if (hipEventElapsedTime(&b, c->ev[slot][1], c->ev[slot][2]) != hipSuccess) b = 0;
-    if (hipEventElapsedTime(&v, c->ev[slot][1], c->ev[slot][3]) != hipSuccess) v = 0;
+    if (hipEventElapsedTime(&b, c->ev[slot][5], c->ev[slot][2]) != hipSuccess) b = 0;
+    if (hipEventElapsedTime(&v, c->ev[slot][5], c->ev[slot][3]) != hipSuccess) v = 0;
     if (!c->split_span[slot] || hipEventElapsedTime(&sp, c->ev[slot][3], c->ev[slot][4]) != hipSuccess) sp = 0;
     c->stats.sum_ms_bin += a;
     c->stats.sum_ms_raster += b;
@@ -583,6 +606,19 @@ int prk_flush(prk_context *c, void *stream) {
         c->pending_tris = 0;
         return PRK_OK;
     }
+    // Binning runs on bin_stream into scratch set k % 2, so it overlaps the
+    // previous frame's raster on the flush stream; the raster waits for it.
+    prk_context::BinSet &B = c->bset[c->frame & 1];
+    hipStream_t bs = c->bin_stream;
+    if (B.used) PRK_TRY(hipStreamWaitEvent(bs, B.free_ev, 0));  // the raster of frame k-2 read this set
+    // A set buffer that must grow is freed by the host: wait for its reader.
+    auto bset_ensure = [&](DevBuf &d, size_t n) -> hipError_t {
+        if (d.cap < n && B.used) {
+            hipError_t e = hipEventSynchronize(B.free_ev);
+            if (e != hipSuccess) return e;
+        }
+        return d.ensure(n);
+    };
     // Device-side draw + texture tables.
     std::vector<prk::TexRec> texs(c->texs.size());
     for (size_t i = 0; i < texs.size(); ++i) {
@@ -592,86 +628,105 @@ int prk_flush(prk_context *c, void *stream) {
         texs[i].pitch = c->texs[i].pitch;
         texs[i].filter = c->texs[i].filter;
     }
-    PRK_TRY(c->d_draws.ensure(c->draws.size() * sizeof(prk::DrawRec)));
-    PRK_TRY(hipMemcpyAsync(c->d_draws.p, c->draws.data(), c->draws.size() * sizeof(prk::DrawRec),
-                           hipMemcpyHostToDevice, s));
+    PRK_TRY(bset_ensure(B.d_draws, c->draws.size() * sizeof(prk::DrawRec)));
+    PRK_TRY(hipMemcpyAsync(B.d_draws.p, c->draws.data(), c->draws.size() * sizeof(prk::DrawRec),
+                           hipMemcpyHostToDevice, bs));
     if (!texs.empty()) {
-        PRK_TRY(c->d_texs.ensure(texs.size() * sizeof(prk::TexRec)));
-        PRK_TRY(hipMemcpyAsync(c->d_texs.p, texs.data(), texs.size() * sizeof(prk::TexRec),
-                               hipMemcpyHostToDevice, s));
+        PRK_TRY(bset_ensure(B.d_texs, texs.size() * sizeof(prk::TexRec)));
+        PRK_TRY(hipMemcpyAsync(B.d_texs.p, texs.data(), texs.size() * sizeof(prk::TexRec),
+                               hipMemcpyHostToDevice, bs));
     }
-    fp.draws = (const prk::DrawRec *)c->d_draws.p;
-    fp.texs = (const prk::TexRec *)c->d_texs.p;
+    fp.draws = (const prk::DrawRec *)B.d_draws.p;
+    fp.texs = (const prk::TexRec *)B.d_texs.p;
     fp.draw0 = c->draws[0];
     fp.tex0 = prk::TexRec{};
     if (fp.draw0.tex >= 0 && (size_t)fp.draw0.tex < texs.size()) fp.tex0 = texs[fp.draw0.tex];
     fp.tri_draw = nullptr;
     if (fp.ndraws > 1) {
-        PRK_TRY(c->d_tri_draw.ensure((size_t)T * 4));
-        PRK_TRY(prk_launch_tri_draw(fp.draws, fp.ndraws, (uint32_t *)c->d_tri_draw.p, T, s));
-        fp.tri_draw = (const uint32_t *)c->d_tri_draw.p;
+        PRK_TRY(bset_ensure(B.d_tri_draw, (size_t)T * 4));
+        PRK_TRY(prk_launch_tri_draw(fp.draws, fp.ndraws, (uint32_t *)B.d_tri_draw.p, T, bs));
+        fp.tri_draw = (const uint32_t *)B.d_tri_draw.p;
     }
-    PRK_TRY(c->d_ranges.ensure((size_t)T * 16));
-    PRK_TRY(c->d_tri_n.ensure((size_t)(T + 1) * 4));
-    PRK_TRY(c->d_tri_off.ensure((size_t)(T + 1) * 4));
-    PRK_TRY(c->d_offs.ensure((size_t)(ntiles + 1) * 4));
+    PRK_TRY(bset_ensure(B.d_ranges, (size_t)T * 16));
+    PRK_TRY(bset_ensure(B.d_tri_n, (size_t)(T + 1) * 4));
+    PRK_TRY(bset_ensure(B.d_tri_off, (size_t)(T + 1) * 4));
+    PRK_TRY(bset_ensure(B.d_offs, (size_t)(ntiles + 1) * 4));
     size_t scan_bytes = 0;
-    PRK_TRY(prk_bin_phase1(&fp, nullptr, nullptr, nullptr, nullptr, &scan_bytes, s));
-    PRK_TRY(c->d_temp.ensure(scan_bytes));
-    PRK_TRY(hipEventRecord(c->ev[slot][0], s));
-    PRK_TRY(prk_bin_phase1(&fp, (uint32_t *)c->d_tri_n.p, (uint32_t *)c->d_tri_off.p, c->d_ranges.p, c->d_temp.p,
-                           &scan_bytes, s));
+    PRK_TRY(prk_bin_phase1(&fp, nullptr, nullptr, nullptr, nullptr, &scan_bytes, bs));
+    PRK_TRY(bset_ensure(B.d_temp, scan_bytes));
+    PRK_TRY(hipEventRecord(c->ev[slot][0], bs));
+    PRK_TRY(prk_bin_phase1(&fp, (uint32_t *)B.d_tri_n.p, (uint32_t *)B.d_tri_off.p, B.d_ranges.p, B.d_temp.p,
+                           &scan_bytes, bs));
     // The bin array size is data dependent: read the total back (one small
-    // D2H copy per frame) and grow the buffers if needed.
-    PRK_TRY(hipMemcpyAsync(c->h_total, (uint32_t *)c->d_tri_off.p + T, 4, hipMemcpyDeviceToHost, s));
-    PRK_TRY(hipStreamSynchronize(s));
+    // D2H copy per frame; the host waits for the binning only, not for the
+    // previous frame's raster) and grow the buffers if needed.
+    PRK_TRY(hipMemcpyAsync(c->h_total, (uint32_t *)B.d_tri_off.p + T, 4, hipMemcpyDeviceToHost, bs));
+    PRK_TRY(hipStreamSynchronize(bs));
     const uint32_t total = *c->h_total;
     c->stats.bin_entries = total;
     const size_t ne = (size_t)std::max<uint32_t>(total, 1);
-    PRK_TRY(c->d_pair_tri.ensure(ne * 4));
-    PRK_TRY(c->d_bins.ensure(ne * 8));  // (triangle, pair) per bin slot
-    PRK_TRY(c->d_list.ensure(ne * 4));
+    PRK_TRY(bset_ensure(B.d_pair_tri, ne * 4));
+    PRK_TRY(bset_ensure(B.d_bins, ne * 8));  // (triangle, pair) per bin slot
+    PRK_TRY(bset_ensure(B.d_keys_a, ne * 4));
+    PRK_TRY(bset_ensure(B.d_vals_a, ne * 8));
+    PRK_TRY(bset_ensure(B.d_keys_b, ne * 4));
+    size_t sort_bytes = 0;
+    PRK_TRY(prk_bin_phase2(&fp, B.d_ranges.p, (const uint32_t *)B.d_tri_off.p, total, (uint32_t *)B.d_keys_a.p,
+                           B.d_vals_a.p, (uint32_t *)B.d_keys_b.p, B.d_bins.p, (uint32_t *)B.d_pair_tri.p,
+                           (uint32_t *)B.d_offs.p, nullptr, &sort_bytes, bs));
+    PRK_TRY(bset_ensure(B.d_temp, std::max(sort_bytes, scan_bytes)));
+    PRK_TRY(prk_bin_phase2(&fp, B.d_ranges.p, (const uint32_t *)B.d_tri_off.p, total, (uint32_t *)B.d_keys_a.p,
+                           B.d_vals_a.p, (uint32_t *)B.d_keys_b.p, B.d_bins.p, (uint32_t *)B.d_pair_tri.p,
+                           (uint32_t *)B.d_offs.p, B.d_temp.p, &sort_bytes, bs));
+    PRK_TRY(hipEventRecord(c->ev[slot][1], bs));
+    PRK_TRY(hipEventRecord(B.binned_ev, bs));
+
+    // Raster on the flush stream, after this frame's binning.
     // won flags: per (pair, row in tile) for span-record (AVX) frames, per
     // pair otherwise
     const bool span_rec = modeset == prk::MODE_AVX;
     const size_t won_bytes = span_rec ? ne * (size_t)c->tile_h : ne;
-    PRK_TRY(c->d_won.ensure(won_bytes));
-    PRK_TRY(c->d_keys_a.ensure(ne * 4));
-    PRK_TRY(c->d_vals_a.ensure(ne * 8));
-    PRK_TRY(c->d_keys_b.ensure(ne * 4));
-    size_t sort_bytes = 0;
-    PRK_TRY(prk_bin_phase2(&fp, c->d_ranges.p, (const uint32_t *)c->d_tri_off.p, total, (uint32_t *)c->d_keys_a.p,
-                           c->d_vals_a.p, (uint32_t *)c->d_keys_b.p, c->d_bins.p, (uint32_t *)c->d_pair_tri.p,
-                           (uint32_t *)c->d_offs.p, nullptr, &sort_bytes, s));
-    PRK_TRY(c->d_temp.ensure(std::max(sort_bytes, scan_bytes)));
-    PRK_TRY(prk_bin_phase2(&fp, c->d_ranges.p, (const uint32_t *)c->d_tri_off.p, total, (uint32_t *)c->d_keys_a.p,
-                           c->d_vals_a.p, (uint32_t *)c->d_keys_b.p, c->d_bins.p, (uint32_t *)c->d_pair_tri.p,
-                           (uint32_t *)c->d_offs.p, c->d_temp.p, &sort_bytes, s));
-    PRK_TRY(hipMemsetAsync(c->d_won.p, 0, won_bytes, s));
     size_t sel_bytes = 0;
-    if (span_rec) {
-        PRK_TRY(c->d_trwon.ensure(T));
-        PRK_TRY(hipMemsetAsync(c->d_trwon.p, 0, T, s));
-        PRK_TRY(c->d_wlist.ensure(((size_t)T + 1) * 4));  // won triangles + their count
-        PRK_TRY(prk_walk_select_bytes(T, &sel_bytes));
-        PRK_TRY(c->d_seltemp.ensure(std::max<size_t>(sel_bytes, 16)));
+    if (span_rec) PRK_TRY(prk_walk_select_bytes(T, &sel_bytes));
+    {
+        // Raster scratch that must grow is freed by the host: the previous
+        // frame's raster (same stream) must be done with it.
+        const bool grow = c->d_list.cap < ne * 4 || c->d_won.cap < won_bytes ||
+                          c->d_nwin.cap < (size_t)ntiles * 4 ||
+                          c->d_wtag.cap < (size_t)ntiles * c->tile_w * c->tile_h * 4 ||
+                          (span_rec && (c->d_trwon.cap < T || c->d_wlist.cap < ((size_t)T + 1) * 4 ||
+                                        c->d_seltemp.cap < std::max<size_t>(sel_bytes, 16) ||
+                                        c->d_recs.cap < won_bytes * 64));
+        if (grow) PRK_TRY(hipStreamSynchronize(s));
     }
-    PRK_TRY(hipEventRecord(c->ev[slot][1], s));
+    PRK_TRY(c->d_list.ensure(ne * 4));
+    PRK_TRY(c->d_won.ensure(won_bytes));
     if (!c->d_anomaly.p) {
         PRK_TRY(c->d_anomaly.ensure(8));  // [anomalies, slow replays]
         PRK_TRY(hipMemsetAsync(c->d_anomaly.p, 0, 8, s));
     }
     PRK_TRY(c->d_nwin.ensure((size_t)ntiles * 4));
     PRK_TRY(c->d_wtag.ensure((size_t)ntiles * c->tile_w * c->tile_h * 4));
-    // span records: 64 B per (pair, row in tile); only won ones are written
-    if (span_rec) PRK_TRY(c->d_recs.ensure(won_bytes * 64));
-    PRK_TRY(prk_launch_raster(&fp, modeset, (const uint32_t *)c->d_offs.p, c->d_bins.p,
-                              (const uint32_t *)c->d_pair_tri.p, (const uint32_t *)c->d_tri_off.p, c->d_ranges.p,
+    if (span_rec) {
+        PRK_TRY(c->d_trwon.ensure(T));
+        PRK_TRY(c->d_wlist.ensure(((size_t)T + 1) * 4));  // won triangles + their count
+        PRK_TRY(c->d_seltemp.ensure(std::max<size_t>(sel_bytes, 16)));
+        // span records: 64 B per (pair, row in tile); only won ones are written
+        PRK_TRY(c->d_recs.ensure(won_bytes * 64));
+    }
+    PRK_TRY(hipStreamWaitEvent(s, B.binned_ev, 0));
+    PRK_TRY(hipEventRecord(c->ev[slot][5], s));
+    PRK_TRY(hipMemsetAsync(c->d_won.p, 0, won_bytes, s));
+    if (span_rec) PRK_TRY(hipMemsetAsync(c->d_trwon.p, 0, T, s));
+    PRK_TRY(prk_launch_raster(&fp, modeset, (const uint32_t *)B.d_offs.p, B.d_bins.p,
+                              (const uint32_t *)B.d_pair_tri.p, (const uint32_t *)B.d_tri_off.p, B.d_ranges.p,
                               (uint8_t *)c->d_won.p, (uint8_t *)c->d_trwon.p, (uint32_t *)c->d_wlist.p,
                               c->d_seltemp.p, sel_bytes, (uint32_t *)c->d_list.p,
                               (uint32_t *)c->d_nwin.p, (uint32_t *)c->d_wtag.p, c->d_recs.p,
                               (uint32_t *)c->d_anomaly.p, c->ev[slot][3], span_rec ? c->ev[slot][4] : nullptr, s));
     PRK_TRY(hipEventRecord(c->ev[slot][2], s));
+    PRK_TRY(hipEventRecord(B.free_ev, s));
+    B.used = true;
     c->pending[slot] = true;
     c->split_span[slot] = modeset == prk::MODE_AVX;
     c->last_slot = slot;
