@@ -27,7 +27,7 @@ hipError_t prk_bin_phase2(const prk::FrameParams *, const void *, const uint32_t
 hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, const void *, const uint32_t *,
                              const uint32_t *, const void *, uint8_t *, uint8_t *, uint32_t *, void *, size_t,
                              uint32_t *, uint32_t *, uint32_t *, void *, uint32_t *, hipEvent_t, hipEvent_t,
-                             hipStream_t);
+                             hipStream_t, hipStream_t);
 hipError_t prk_walk_select_bytes(uint32_t, size_t *);
 }
 
@@ -98,19 +98,21 @@ struct prk_context {
     std::vector<Texture> texs;
     std::vector<prk::DrawRec> draws;
     uint32_t pending_tris = 0;
-    // Binning scratch, two sets: frame k bins into set k % 2 on bin_stream
-    // while frame k-1 rasterises on the flush's stream.
+    // Per-frame scratch, two sets: frame k bins (and, on span-record frames,
+    // runs k_vis) into set k % 2 on bin_stream while frame k-1 shades on the
+    // flush's stream.
     struct BinSet {
         DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_tri_n, d_tri_off, d_pair_tri, d_keys_a, d_vals_a, d_keys_b,
-            d_bins, d_offs, d_temp;
+            d_bins, d_offs, d_temp, d_won, d_list, d_nwin, d_wtag, d_recs, d_trwon, d_wlist, d_seltemp;
         hipEvent_t free_ev = nullptr;    // the raster that read this set is done
         hipEvent_t binned_ev = nullptr;  // this set's binning is done
         bool used = false;
     };
     BinSet bset[2];
     hipStream_t bin_stream = nullptr;
-    // raster scratch (the flush's stream only)
-    DevBuf d_won, d_list, d_winners, d_anomaly, d_nwin, d_wtag, d_prof, d_recs, d_trwon, d_wlist, d_seltemp;
+    hipStream_t vis_stream = nullptr;  // k_vis of span-record frames
+    DevBuf d_winners, d_anomaly, d_prof;
+    hipEvent_t s_mark = nullptr;  // flush-stream point the bin stream waits for (prior target contents)
     uint32_t *h_total = nullptr;  // pinned
     int32_t tile_w = 256, tile_h = 8;  // measured best for C3b
     bool debug = false;
@@ -158,6 +160,8 @@ int prk_create(int device, prk_context **out) {
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->bin_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->vis_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->s_mark, hipEventDisableTiming);
     for (int i = 0; i < 2 && e == hipSuccess; ++i) {
         e = hipEventCreateWithFlags(&c->bset[i].free_ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->bset[i].binned_ev, hipEventDisableTiming);
@@ -192,20 +196,22 @@ int prk_destroy(prk_context *c) {
     }
     for (auto &B : c->bset) {
         DevBuf *bb[] = {&B.d_draws, &B.d_texs, &B.d_tri_draw, &B.d_ranges, &B.d_tri_n, &B.d_tri_off, &B.d_pair_tri,
-                        &B.d_keys_a, &B.d_vals_a, &B.d_keys_b, &B.d_bins, &B.d_offs, &B.d_temp};
+                        &B.d_keys_a, &B.d_vals_a, &B.d_keys_b, &B.d_bins, &B.d_offs, &B.d_temp, &B.d_won,
+                        &B.d_list, &B.d_nwin, &B.d_wtag, &B.d_recs, &B.d_trwon, &B.d_wlist, &B.d_seltemp};
         for (DevBuf *b : bb) b->release();
         if (B.free_ev) (void)hipEventDestroy(B.free_ev);
         if (B.binned_ev) (void)hipEventDestroy(B.binned_ev);
     }
-    DevBuf *bufs[] = {&c->d_won,     &c->d_list, &c->d_winners, &c->d_anomaly, &c->d_nwin,  &c->d_wtag,
-                      &c->d_prof,    &c->d_recs, &c->d_trwon,   &c->d_wlist,   &c->d_seltemp};
+    DevBuf *bufs[] = {&c->d_winners, &c->d_anomaly, &c->d_prof};
     for (DevBuf *b : bufs) b->release();
+    if (c->s_mark) (void)hipEventDestroy(c->s_mark);
     if (c->h_total) (void)hipHostFree(c->h_total);
     for (auto &slot : c->ev)
         for (auto &e : slot)
             if (e) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     if (c->bin_stream) (void)hipStreamDestroy(c->bin_stream);
+    if (c->vis_stream) (void)hipStreamDestroy(c->vis_stream);
     delete c;
     return PRK_OK;
 }
@@ -681,49 +687,55 @@ int prk_flush(prk_context *c, void *stream) {
     PRK_TRY(hipEventRecord(c->ev[slot][1], bs));
     PRK_TRY(hipEventRecord(B.binned_ev, bs));
 
-    // Raster on the flush stream, after this frame's binning.
+    // Raster.  Span-record frames run k_vis on vis_stream once their binning
+    // is done (so it overlaps the previous frame's k_walk / k_pix on the
+    // flush stream, while the next frame bins on bin_stream) and shade on the
+    // flush stream after it; k_vis waits for the flush stream only when it
+    // reads the target's prior z (no fused clear) or the debug winner map.
+    // Other frames run on the flush stream.
     // won flags: per (pair, row in tile) for span-record (AVX) frames, per
     // pair otherwise
     const bool span_rec = modeset == prk::MODE_AVX;
     const size_t won_bytes = span_rec ? ne * (size_t)c->tile_h : ne;
     size_t sel_bytes = 0;
     if (span_rec) PRK_TRY(prk_walk_select_bytes(T, &sel_bytes));
-    {
-        // Raster scratch that must grow is freed by the host: the previous
-        // frame's raster (same stream) must be done with it.
-        const bool grow = c->d_list.cap < ne * 4 || c->d_won.cap < won_bytes ||
-                          c->d_nwin.cap < (size_t)ntiles * 4 ||
-                          c->d_wtag.cap < (size_t)ntiles * c->tile_w * c->tile_h * 4 ||
-                          (span_rec && (c->d_trwon.cap < T || c->d_wlist.cap < ((size_t)T + 1) * 4 ||
-                                        c->d_seltemp.cap < std::max<size_t>(sel_bytes, 16) ||
-                                        c->d_recs.cap < won_bytes * 64));
-        if (grow) PRK_TRY(hipStreamSynchronize(s));
+    PRK_TRY(bset_ensure(B.d_list, ne * 4));
+    PRK_TRY(bset_ensure(B.d_won, won_bytes));
+    PRK_TRY(bset_ensure(B.d_nwin, (size_t)ntiles * 4));
+    PRK_TRY(bset_ensure(B.d_wtag, (size_t)ntiles * c->tile_w * c->tile_h * 4));
+    if (span_rec) {
+        PRK_TRY(bset_ensure(B.d_trwon, T));
+        PRK_TRY(bset_ensure(B.d_wlist, ((size_t)T + 1) * 4));  // won triangles + their count
+        PRK_TRY(bset_ensure(B.d_seltemp, std::max<size_t>(sel_bytes, 16)));
+        // span records: 64 B per (pair, row in tile); only won ones are written
+        PRK_TRY(bset_ensure(B.d_recs, won_bytes * 64));
     }
-    PRK_TRY(c->d_list.ensure(ne * 4));
-    PRK_TRY(c->d_won.ensure(won_bytes));
     if (!c->d_anomaly.p) {
         PRK_TRY(c->d_anomaly.ensure(8));  // [anomalies, slow replays]
         PRK_TRY(hipMemsetAsync(c->d_anomaly.p, 0, 8, s));
+        PRK_TRY(hipStreamSynchronize(s));
     }
-    PRK_TRY(c->d_nwin.ensure((size_t)ntiles * 4));
-    PRK_TRY(c->d_wtag.ensure((size_t)ntiles * c->tile_w * c->tile_h * 4));
+    hipStream_t sv = s;
     if (span_rec) {
-        PRK_TRY(c->d_trwon.ensure(T));
-        PRK_TRY(c->d_wlist.ensure(((size_t)T + 1) * 4));  // won triangles + their count
-        PRK_TRY(c->d_seltemp.ensure(std::max<size_t>(sel_bytes, 16)));
-        // span records: 64 B per (pair, row in tile); only won ones are written
-        PRK_TRY(c->d_recs.ensure(won_bytes * 64));
+        sv = c->vis_stream;
+        PRK_TRY(hipStreamWaitEvent(sv, B.binned_ev, 0));
+        if (!fuse || c->debug) {  // prior z / winner map: after the flush stream's work so far
+            PRK_TRY(hipEventRecord(c->s_mark, s));
+            PRK_TRY(hipStreamWaitEvent(sv, c->s_mark, 0));
+        }
+    } else {
+        PRK_TRY(hipStreamWaitEvent(s, B.binned_ev, 0));
     }
-    PRK_TRY(hipStreamWaitEvent(s, B.binned_ev, 0));
-    PRK_TRY(hipEventRecord(c->ev[slot][5], s));
-    PRK_TRY(hipMemsetAsync(c->d_won.p, 0, won_bytes, s));
-    if (span_rec) PRK_TRY(hipMemsetAsync(c->d_trwon.p, 0, T, s));
+    PRK_TRY(hipEventRecord(c->ev[slot][5], sv));
+    PRK_TRY(hipMemsetAsync(B.d_won.p, 0, won_bytes, sv));
+    if (span_rec) PRK_TRY(hipMemsetAsync(B.d_trwon.p, 0, T, sv));
     PRK_TRY(prk_launch_raster(&fp, modeset, (const uint32_t *)B.d_offs.p, B.d_bins.p,
                               (const uint32_t *)B.d_pair_tri.p, (const uint32_t *)B.d_tri_off.p, B.d_ranges.p,
-                              (uint8_t *)c->d_won.p, (uint8_t *)c->d_trwon.p, (uint32_t *)c->d_wlist.p,
-                              c->d_seltemp.p, sel_bytes, (uint32_t *)c->d_list.p,
-                              (uint32_t *)c->d_nwin.p, (uint32_t *)c->d_wtag.p, c->d_recs.p,
-                              (uint32_t *)c->d_anomaly.p, c->ev[slot][3], span_rec ? c->ev[slot][4] : nullptr, s));
+                              (uint8_t *)B.d_won.p, (uint8_t *)B.d_trwon.p, (uint32_t *)B.d_wlist.p,
+                              B.d_seltemp.p, sel_bytes, (uint32_t *)B.d_list.p,
+                              (uint32_t *)B.d_nwin.p, (uint32_t *)B.d_wtag.p, B.d_recs.p,
+                              (uint32_t *)c->d_anomaly.p, c->ev[slot][3], span_rec ? c->ev[slot][4] : nullptr, sv,
+                              s));
     PRK_TRY(hipEventRecord(c->ev[slot][2], s));
     PRK_TRY(hipEventRecord(B.free_ev, s));
     B.used = true;

@@ -1348,8 +1348,11 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
                              const uint32_t *pair_tri, const uint32_t *tri_off, const void *ranges, uint8_t *won,
                              uint8_t *trwon, uint32_t *wlist, void *sel_temp, size_t sel_bytes, uint32_t *list,
                              uint32_t *nwin, uint32_t *wtag, void *recs, uint32_t *anomaly, hipEvent_t mid,
-                             hipEvent_t mid2, hipStream_t s) {
+                             hipEvent_t mid2, hipStream_t svis, hipStream_t s) {
+    // k_vis runs on svis, the shading on s (after k_vis: `mid` is recorded on
+    // svis and waited for on s); svis == s runs the frame on one stream.
     const uint32_t ntile = (uint32_t)(fp->tiles_x * fp->tiles_y);
+    if (svis != s && !mid) return hipErrorInvalidValue;
     if (ntile == 0) return hipSuccess;
     const size_t lv = vis_lds(fp), ls = shade_lds(fp);
     const bool uni = fp->ndraws == 1;
@@ -1360,9 +1363,10 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
     const uint2 *bins = reinterpret_cast<const uint2 *>(bins_);
 #define PRK_VIS(MS, UNI)                                                                                             \
     do {                                                                                                             \
-        hipLaunchKernelGGL((prk::k_vis<MS, UNI>), dim3(ntile), dim3(64 * prk::kVisWaves), lv, s, *fp, offs, bins, won, \
-                           list, nwin, wtag, pair_tri, trwon, anomaly);                                              \
-        if (mid) (void)hipEventRecord(mid, s);                                                                       \
+        hipLaunchKernelGGL((prk::k_vis<MS, UNI>), dim3(ntile), dim3(64 * prk::kVisWaves), lv, svis, *fp, offs, bins,  \
+                           won, list, nwin, wtag, pair_tri, trwon, anomaly);                                         \
+        if (mid) (void)hipEventRecord(mid, svis);                                                                    \
+        if (svis != s) (void)hipStreamWaitEvent(s, mid, 0);                                                          \
     } while (0)
 #define PRK_SHADE(MS, UNI)                                                                                           \
     hipLaunchKernelGGL((prk::k_shade<MS, UNI>), dim3(ntile), dim3(64 * prk::kShadeWaves), ls, s, *fp, offs, bins, list,  \
