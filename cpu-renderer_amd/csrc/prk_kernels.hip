@@ -46,6 +46,9 @@
 #ifndef PRK_WALK_MIN_WAVES
 #define PRK_WALK_MIN_WAVES 4  // waves per SIMD k_walk is register-budgeted for
 #endif
+#ifndef PRK_WALK_ON_VIS
+#define PRK_WALK_ON_VIS 0  // k_walk on k_vis's stream (k_pix alone on the flush stream)
+#endif
 #ifndef PRK_PIX_SPLIT
 #define PRK_PIX_SPLIT 1  // k_pix workgroups per tile
 #endif
@@ -1352,7 +1355,7 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
     // k_vis runs on svis, the shading on s (after k_vis: `mid` is recorded on
     // svis and waited for on s); svis == s runs the frame on one stream.
     const uint32_t ntile = (uint32_t)(fp->tiles_x * fp->tiles_y);
-    if (svis != s && !mid) return hipErrorInvalidValue;
+    if (svis != s && (!mid || (PRK_WALK_ON_VIS && modeset == prk::MODE_AVX && !mid2))) return hipErrorInvalidValue;
     if (ntile == 0) return hipSuccess;
     const size_t lv = vis_lds(fp), ls = shade_lds(fp);
     const bool uni = fp->ndraws == 1;
@@ -1373,17 +1376,20 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
                        nwin, wtag, anomaly)
 #define PRK_SPANPIX(UNI)                                                                                             \
     do {                                                                                                             \
+        /* PRK_WALK_ON_VIS: k_walk follows k_vis on svis, k_pix waits for it on s */                                 \
+        hipStream_t sw = PRK_WALK_ON_VIS ? svis : s;                                                                 \
         if (nblk) {                                                                                                  \
             /* compact the won triangles (order kept); the count stays on the device */                            \
             uint32_t *nsel = wlist + fp->tri_count;                                                                  \
             hipError_t e_ = hipcub::DeviceSelect::Flagged(sel_temp, sel_bytes, hipcub::CountingInputIterator<uint32_t>(0u), \
-                                                          trwon, wlist, nsel, fp->tri_count, s);                    \
+                                                          trwon, wlist, nsel, fp->tri_count, sw);                   \
             if (e_ != hipSuccess) return e_;                                                                         \
-            hipLaunchKernelGGL((prk::k_walk<UNI>), dim3(nwblk), dim3(64 * prk::kWalkWaves), 0, s, *fp, wlist, nsel,     \
+            hipLaunchKernelGGL((prk::k_walk<UNI>), dim3(nwblk), dim3(64 * prk::kWalkWaves), 0, sw, *fp, wlist, nsel,    \
                                tri_off, tr, won,                                                                     \
                                rp, anomaly);                                                                         \
         }                                                                                                            \
-        if (mid2) (void)hipEventRecord(mid2, s);                                                                     \
+        if (mid2) (void)hipEventRecord(mid2, sw);                                                                    \
+        if (sw != s) (void)hipStreamWaitEvent(s, mid2, 0);                                                           \
         hipLaunchKernelGGL((prk::k_pix<UNI>), dim3(ntile * PRK_PIX_SPLIT), dim3(256), 0, s, *fp, nwin, wtag, rp);   \
     } while (0)
     switch (modeset) {
