@@ -164,6 +164,35 @@ def test_fused_clear_fallbacks(gpu):
         r.close()
 
 
+def test_pipelined_frames_one_target(gpu):
+    """Back-to-back flushes without a host sync (the bench's pattern): frame k
+    bins while k-1 rasterises and k's k_vis overlaps k-1's shading, scratch
+    sets alternate.  Fused-clear frames must each end as their own frame; a
+    frame without a clear must see the previous frame's z and colour."""
+    scs = [scenes.random_soup(3000, 256, 192, radius=16, seed=50 + k) for k in range(4)]
+    r = prk.Renderer(0)
+    try:
+        r.target_alloc(256, 192)
+        r.set_camera(scs[0].prk_transform(), scs[0].prk_lights())
+        geoms = [r.geometry(s.vertices, s.colors, s.normals, s.uvs) for s in scs]
+        tex = r.texture(scs[0].texture)
+        for k, s in enumerate(scs):  # frames 0..2 fused-clear, frame 3 over frame 2
+            if k < 3:
+                r.clear_on_flush()
+            r.draw_model_optimized(geoms[k], s.tri_count, P=s.P, bitmap=tex, phong=True)
+            r.complete_all_work()
+        r.synchronize()
+        gc, gz = r.download()
+    finally:
+        r.close()
+    for s in scs:
+        s.texture = scs[0].texture
+    oc, oz, _, _ = O.render(scs[2])
+    oc, oz, _, _ = O.render(scs[3], color=oc, z=oz)
+    assert (gz.view(np.uint32) == oz.view(np.uint32)).all()
+    assert (gc == oc).all()
+
+
 def test_row_band(gpu):
     s = scenes.random_soup(10000, 512, 512, radius=20, seed=17)
     oc, oz, ow, _ = O.render(s)
