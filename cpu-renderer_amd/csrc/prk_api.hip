@@ -34,6 +34,10 @@ hipError_t prk_walk_select_bytes(uint32_t, size_t *);
 // AVX frames shade through span records (k_walk + k_pix); must match
 // PRK_SPAN_RECORDS of prk_kernels.hip.
 #define PRK_SPAN_RECORDS_HOST 1
+// Per-frame scratch sets in flight (frame k uses set k % PRK_FRAME_SETS).
+#ifndef PRK_FRAME_SETS
+#define PRK_FRAME_SETS 2  // (3 measured 1 % slower: more binning competes with k_vis)
+#endif
 
 namespace {
 
@@ -108,7 +112,8 @@ struct prk_context {
         hipEvent_t binned_ev = nullptr;  // this set's binning is done
         bool used = false;
     };
-    BinSet bset[2];
+    static constexpr int kSets = PRK_FRAME_SETS;
+    BinSet bset[kSets];
     hipStream_t bin_stream = nullptr;
     hipStream_t vis_stream = nullptr;  // k_vis of span-record frames
     DevBuf d_winners, d_anomaly, d_prof;
@@ -162,7 +167,7 @@ int prk_create(int device, prk_context **out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->bin_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->vis_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->s_mark, hipEventDisableTiming);
-    for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+    for (int i = 0; i < prk_context::kSets && e == hipSuccess; ++i) {
         e = hipEventCreateWithFlags(&c->bset[i].free_ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->bset[i].binned_ev, hipEventDisableTiming);
     }
@@ -614,7 +619,7 @@ int prk_flush(prk_context *c, void *stream) {
     }
     // Binning runs on bin_stream into scratch set k % 2, so it overlaps the
     // previous frame's raster on the flush stream; the raster waits for it.
-    prk_context::BinSet &B = c->bset[c->frame & 1];
+    prk_context::BinSet &B = c->bset[c->frame % prk_context::kSets];
     hipStream_t bs = c->bin_stream;
     if (B.used) PRK_TRY(hipStreamWaitEvent(bs, B.free_ev, 0));  // the raster of frame k-2 read this set
     // A set buffer that must grow is freed by the host: wait for its reader.
@@ -684,15 +689,6 @@ int prk_flush(prk_context *c, void *stream) {
     PRK_TRY(prk_bin_phase2(&fp, B.d_ranges.p, (const uint32_t *)B.d_tri_off.p, total, (uint32_t *)B.d_keys_a.p,
                            B.d_vals_a.p, (uint32_t *)B.d_keys_b.p, B.d_bins.p, (uint32_t *)B.d_pair_tri.p,
                            (uint32_t *)B.d_offs.p, B.d_temp.p, &sort_bytes, bs));
-    PRK_TRY(hipEventRecord(c->ev[slot][1], bs));
-    PRK_TRY(hipEventRecord(B.binned_ev, bs));
-
-    // Raster.  Span-record frames run k_vis on vis_stream once their binning
-    // is done (so it overlaps the previous frame's k_walk / k_pix on the
-    // flush stream, while the next frame bins on bin_stream) and shade on the
-    // flush stream after it; k_vis waits for the flush stream only when it
-    // reads the target's prior z (no fused clear) or the debug winner map.
-    // Other frames run on the flush stream.
     // won flags: per (pair, row in tile) for span-record (AVX) frames, per
     // pair otherwise
     const bool span_rec = modeset == prk::MODE_AVX;
@@ -710,6 +706,17 @@ int prk_flush(prk_context *c, void *stream) {
         // span records: 64 B per (pair, row in tile); only won ones are written
         PRK_TRY(bset_ensure(B.d_recs, won_bytes * 64));
     }
+    PRK_TRY(hipMemsetAsync(B.d_won.p, 0, won_bytes, bs));
+    if (span_rec) PRK_TRY(hipMemsetAsync(B.d_trwon.p, 0, T, bs));
+    PRK_TRY(hipEventRecord(c->ev[slot][1], bs));
+    PRK_TRY(hipEventRecord(B.binned_ev, bs));
+
+    // Raster.  Span-record frames run k_vis on vis_stream once their binning
+    // is done (so it overlaps the previous frame's k_walk / k_pix on the
+    // flush stream, while the next frame bins on bin_stream) and shade on the
+    // flush stream after it; k_vis waits for the flush stream only when it
+    // reads the target's prior z (no fused clear) or the debug winner map.
+    // Other frames run on the flush stream.
     if (!c->d_anomaly.p) {
         PRK_TRY(c->d_anomaly.ensure(8));  // [anomalies, slow replays]
         PRK_TRY(hipMemsetAsync(c->d_anomaly.p, 0, 8, s));
@@ -727,8 +734,6 @@ int prk_flush(prk_context *c, void *stream) {
         PRK_TRY(hipStreamWaitEvent(s, B.binned_ev, 0));
     }
     PRK_TRY(hipEventRecord(c->ev[slot][5], sv));
-    PRK_TRY(hipMemsetAsync(B.d_won.p, 0, won_bytes, sv));
-    if (span_rec) PRK_TRY(hipMemsetAsync(B.d_trwon.p, 0, T, sv));
     PRK_TRY(prk_launch_raster(&fp, modeset, (const uint32_t *)B.d_offs.p, B.d_bins.p,
                               (const uint32_t *)B.d_pair_tri.p, (const uint32_t *)B.d_tri_off.p, B.d_ranges.p,
                               (uint8_t *)B.d_won.p, (uint8_t *)B.d_trwon.p, (uint32_t *)B.d_wlist.p,
