@@ -114,7 +114,14 @@ def cpu_baseline(scene, threads, max_tris, frames=5):
     variants = {"banded": {"frame_ms": fb * 1e3, "mpixels_s": px / fb / 1e6},
                 "queue": {"frame_ms": fq * 1e3, "mpixels_s": px / fq / 1e6}}
     best = min(fb, fq)
-    return dict(value=px / best / 1e6, unit="Mpixels/s", cores=threads, kind="port",
+    cpu_model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
+    except OSError:
+        pass
+    return dict(value=px / best / 1e6, unit="Mpixels/s", cores=threads, kind="port", cpu_model=cpu_model,
+                host_cpus=os.cpu_count(),
                 sample="AVX2 restatement of FillLineOptimized (oracle/prk_cpu_avx.c) on %d threads; banded: "
                        "median of %d full frames (%d of %d triangles%s) after 1 warm-up; queue: median of 3 "
                        "frames of the first %d triangles after 1 warm-up, scaled to T; value = faster schedule "
