@@ -26,15 +26,20 @@ for tile in tiles:
     r.set_camera(s.prk_transform(), s.prk_lights())
     g = r.geometry(s.vertices, None, s.normals, s.uvs)
     tex = r.texture(s.texture)
+    host = 0.0
     for i in range(23):
         if i == 3:
             r.synchronize()
             t0 = time.perf_counter()
+            host = 0.0
+        h0 = time.perf_counter()
         r.clear_on_flush(0xFF000000, zmin)
         r.draw_model_optimized(g, s.tri_count, bitmap=tex)
         r.complete_all_work()
+        host += time.perf_counter() - h0
     r.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / 20
-    print("N=%d band rows %d tile %s: %.3f ms/frame per rank (x%d ranks -> %.0f Mpixels/s before the gather)"
-          % (N, H // N, tile, ms, N, W * H / (ms * 1e-3) / 1e6), flush=True)
+    print("N=%d band rows %d tile %s: %.3f ms/frame per rank (x%d ranks -> %.0f Mpixels/s before the gather); "
+          "host time in the draw calls %.3f ms/frame" % (N, H // N, tile, ms, N, W * H / (ms * 1e-3) / 1e6,
+                                                        host * 1e3 / 20), flush=True)
     r.close()
