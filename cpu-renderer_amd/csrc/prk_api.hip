@@ -129,7 +129,7 @@ struct prk_context {
     // raster start (flush stream)
     hipEvent_t ev[kRing][6] = {};
     bool pending[kRing] = {};
-    bool split_span[kRing] = {};  // the slot's flush ran k_span + k_pix
+    bool split_span[kRing] = {};  // the slot's flush ran k_walk + k_pix
     uint32_t frame = 0;
     int last_slot = -1;
 };
