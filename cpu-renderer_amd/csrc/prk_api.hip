@@ -123,7 +123,7 @@ struct prk_context {
     bool debug = false;
     bool winners_valid = false;
     prk_stats stats{};
-    // Timing ring: 3 events per flush (before bin, before raster, after raster).
+    // Timing ring: 6 events per flush.
     static constexpr int kRing = 32;
     // bin start, bin end (bin_stream); raster end, k_vis end, k_walk end,
     // raster start (flush stream)
