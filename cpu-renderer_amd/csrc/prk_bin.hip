@@ -37,12 +37,16 @@ __device__ __forceinline__ bool tri_tile_range(const FrameParams &fp, uint32_t g
     resolve_draw(fp, g, d, gt);
     V3 cam[3], proj[3];
     load_positions(*d, gt, fp, cam, proj);
-    if (!front_facing(proj)) return false;  // also rejects every non-finite vertex
-    const float xmin = fminf(proj[0].x, fminf(proj[1].x, proj[2].x));
-    const float xmax = fmaxf(proj[0].x, fmaxf(proj[1].x, proj[2].x));
     const float ymin = fminf(proj[0].y, fminf(proj[1].y, proj[2].y));
     const float ymax = fmaxf(proj[0].y, fmaxf(proj[1].y, proj[2].y));
     const float fr0 = floorf(ymin), fr1 = ceilf(ymax);
+    // No row of the band (nor, for scalar draws, the row-overflow store one
+    // row down): no entries whatever the cull says, so skip its two
+    // normalisations (row bands: most triangles lie outside a rank's band).
+    if (fr1 + 1.0f <= (float)fp.row0 || fr0 >= (float)fp.row1) return false;
+    if (!front_facing(proj)) return false;  // also rejects every non-finite vertex
+    const float xmin = fminf(proj[0].x, fminf(proj[1].x, proj[2].x));
+    const float xmax = fmaxf(proj[0].x, fmaxf(proj[1].x, proj[2].x));
     const int32_t r0 = fr0 < (float)fp.row0 ? fp.row0 : (fr0 >= (float)fp.row1 ? fp.row1 : (int32_t)fr0);
     const int32_t r1 = fr1 > (float)fp.row1 ? fp.row1 : (fr1 <= (float)fp.row0 ? fp.row0 : (int32_t)fr1);
     const float maxabs = fmaxf(fabsf(xmin), fabsf(xmax));
