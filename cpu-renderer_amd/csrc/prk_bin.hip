@@ -22,6 +22,7 @@
 // tile's bin (entry order == submission order), which it uses to skip, in the
 // shading sweep, every triangle that won no pixel of the tile.
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "prk_device.h"
 
@@ -165,6 +166,14 @@ __global__ void k_tile_offsets(const uint32_t *__restrict__ keys, uint32_t total
 
 }  // namespace prk
 
+// Bin sort: onesweep radix at every size above one block.  rocprim's
+// default switches to a block sort + merge sort below 1 M items, which is
+// the band size of a 4- or 8-rank frame (C3b at N = 8: 0.4 M entries, nine
+// merge passes of two launches each, 0.13 ms per frame on one MI355X against
+// two onesweep passes over the band's 13-bit keys).
+using BinSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                 rocprim::default_config, 0>;
+
 extern "C" {
 
 // Phase 1: counts + exclusive scan.  `scan_out` gets T+1 offsets; the caller
@@ -193,7 +202,8 @@ hipError_t prk_bin_phase2(const prk::FrameParams *fp, const void *ranges, const 
     bits += prk::kRowClassBits;
     uint64_t *va = reinterpret_cast<uint64_t *>(vals_a), *vb = reinterpret_cast<uint64_t *>(bins);
     if (!temp)
-        return hipcub::DeviceRadixSort::SortPairs(nullptr, *temp_bytes, keys_a, keys_b, va, vb, total, 0, bits, s);
+        return rocprim::radix_sort_pairs<BinSortConfig>(nullptr, *temp_bytes, keys_a, keys_b, va, vb, total, 0,
+                                                        (unsigned)bits, s);
     if (fp->tri_count)
         hipLaunchKernelGGL(prk::k_bin_emit, dim3((fp->tri_count + 255) / 256), dim3(256), 0, s, *fp,
                            reinterpret_cast<const prk::TileRange *>(ranges), scan_out, keys_a,
@@ -201,7 +211,8 @@ hipError_t prk_bin_phase2(const prk::FrameParams *fp, const void *ranges, const 
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (total) {
-        e = hipcub::DeviceRadixSort::SortPairs(temp, *temp_bytes, keys_a, keys_b, va, vb, total, 0, bits, s);
+        e = rocprim::radix_sort_pairs<BinSortConfig>(temp, *temp_bytes, keys_a, keys_b, va, vb, total, 0,
+                                                     (unsigned)bits, s);
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(prk::k_tile_offsets, dim3((ntiles + 1 + 255) / 256), dim3(256), 0, s, keys_b, total, ntiles,
