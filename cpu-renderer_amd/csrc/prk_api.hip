@@ -23,7 +23,8 @@ extern "C" {
 hipError_t prk_launch_tri_draw(const prk::DrawRec *, uint32_t, uint32_t *, uint32_t, hipStream_t);
 hipError_t prk_bin_phase1(const prk::FrameParams *, uint32_t *, uint32_t *, void *, void *, size_t *, hipStream_t);
 hipError_t prk_bin_phase2(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, uint32_t *, void *,
-                          uint32_t *, void *, uint32_t *, uint32_t *, void *, size_t *, hipStream_t);
+                          uint32_t *, void *, uint32_t *, uint32_t *, uint8_t *, uint32_t, uint8_t *, void *, size_t *,
+                          hipStream_t);
 hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, const void *, const uint32_t *,
                              const uint32_t *, const void *, uint8_t *, uint8_t *, uint32_t *, void *, size_t,
                              uint32_t *, uint32_t *, uint32_t *, void *, uint32_t *, hipEvent_t, hipEvent_t,
@@ -108,6 +109,10 @@ struct prk_context {
     struct BinSet {
         DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_tri_n, d_tri_off, d_pair_tri, d_keys_a, d_vals_a, d_keys_b,
             d_bins, d_offs, d_temp, d_won, d_list, d_nwin, d_wtag, d_recs, d_trwon, d_wlist, d_seltemp;
+        // bytes last uploaded into d_draws / d_texs and the buffer they went
+        // to: an unchanged table (every frame of a static scene) is not sent again
+        std::vector<uint8_t> h_draws, h_texs;
+        const void *h_draws_at = nullptr, *h_texs_at = nullptr;
         hipEvent_t free_ev = nullptr;    // the raster that read this set is done
         hipEvent_t binned_ev = nullptr;  // this set's binning is done
         bool used = false;
@@ -639,14 +644,21 @@ int prk_flush(prk_context *c, void *stream) {
         texs[i].pitch = c->texs[i].pitch;
         texs[i].filter = c->texs[i].filter;
     }
-    PRK_TRY(bset_ensure(B.d_draws, c->draws.size() * sizeof(prk::DrawRec)));
-    PRK_TRY(hipMemcpyAsync(B.d_draws.p, c->draws.data(), c->draws.size() * sizeof(prk::DrawRec),
-                           hipMemcpyHostToDevice, bs));
-    if (!texs.empty()) {
-        PRK_TRY(bset_ensure(B.d_texs, texs.size() * sizeof(prk::TexRec)));
-        PRK_TRY(hipMemcpyAsync(B.d_texs.p, texs.data(), texs.size() * sizeof(prk::TexRec),
-                               hipMemcpyHostToDevice, bs));
-    }
+    // Upload a table into this set unless the set already holds the same
+    // bytes (the set's previous reader, frame k-2's raster, is waited for above).
+    auto upload_table = [&](DevBuf &d, std::vector<uint8_t> &mirror, const void *&at, const void *src,
+                            size_t bytes) -> hipError_t {
+        hipError_t e = bset_ensure(d, bytes);
+        if (e != hipSuccess) return e;
+        if (at == d.p && mirror.size() == bytes && std::memcmp(mirror.data(), src, bytes) == 0) return hipSuccess;
+        mirror.assign((const uint8_t *)src, (const uint8_t *)src + bytes);
+        at = d.p;
+        return hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, bs);
+    };
+    PRK_TRY(upload_table(B.d_draws, B.h_draws, B.h_draws_at, c->draws.data(),
+                         c->draws.size() * sizeof(prk::DrawRec)));
+    if (!texs.empty())
+        PRK_TRY(upload_table(B.d_texs, B.h_texs, B.h_texs_at, texs.data(), texs.size() * sizeof(prk::TexRec)));
     fp.draws = (const prk::DrawRec *)B.d_draws.p;
     fp.texs = (const prk::TexRec *)B.d_texs.p;
     fp.draw0 = c->draws[0];
@@ -681,18 +693,11 @@ int prk_flush(prk_context *c, void *stream) {
     PRK_TRY(bset_ensure(B.d_keys_a, ne * 4));
     PRK_TRY(bset_ensure(B.d_vals_a, ne * 8));
     PRK_TRY(bset_ensure(B.d_keys_b, ne * 4));
-    size_t sort_bytes = 0;
-    PRK_TRY(prk_bin_phase2(&fp, B.d_ranges.p, (const uint32_t *)B.d_tri_off.p, total, (uint32_t *)B.d_keys_a.p,
-                           B.d_vals_a.p, (uint32_t *)B.d_keys_b.p, B.d_bins.p, (uint32_t *)B.d_pair_tri.p,
-                           (uint32_t *)B.d_offs.p, nullptr, &sort_bytes, bs));
-    PRK_TRY(bset_ensure(B.d_temp, std::max(sort_bytes, scan_bytes)));
-    PRK_TRY(prk_bin_phase2(&fp, B.d_ranges.p, (const uint32_t *)B.d_tri_off.p, total, (uint32_t *)B.d_keys_a.p,
-                           B.d_vals_a.p, (uint32_t *)B.d_keys_b.p, B.d_bins.p, (uint32_t *)B.d_pair_tri.p,
-                           (uint32_t *)B.d_offs.p, B.d_temp.p, &sort_bytes, bs));
     // won flags: per (pair, row in tile) for span-record (AVX) frames, per
-    // pair otherwise
+    // pair otherwise; k_bin_emit clears them (and trwon) for every pair.
     const bool span_rec = modeset == prk::MODE_AVX;
-    const size_t won_bytes = span_rec ? ne * (size_t)c->tile_h : ne;
+    const uint32_t won_stride = span_rec ? (uint32_t)c->tile_h : 1u;
+    const size_t won_bytes = ne * won_stride;
     size_t sel_bytes = 0;
     if (span_rec) PRK_TRY(prk_walk_select_bytes(T, &sel_bytes));
     PRK_TRY(bset_ensure(B.d_list, ne * 4));
@@ -706,8 +711,15 @@ int prk_flush(prk_context *c, void *stream) {
         // span records: 64 B per (pair, row in tile); only won ones are written
         PRK_TRY(bset_ensure(B.d_recs, won_bytes * 64));
     }
-    PRK_TRY(hipMemsetAsync(B.d_won.p, 0, won_bytes, bs));
-    if (span_rec) PRK_TRY(hipMemsetAsync(B.d_trwon.p, 0, T, bs));
+    uint8_t *won = (uint8_t *)B.d_won.p, *trwon = span_rec ? (uint8_t *)B.d_trwon.p : nullptr;
+    size_t sort_bytes = 0;
+    PRK_TRY(prk_bin_phase2(&fp, B.d_ranges.p, (const uint32_t *)B.d_tri_off.p, total, (uint32_t *)B.d_keys_a.p,
+                           B.d_vals_a.p, (uint32_t *)B.d_keys_b.p, B.d_bins.p, (uint32_t *)B.d_pair_tri.p,
+                           (uint32_t *)B.d_offs.p, won, won_stride, trwon, nullptr, &sort_bytes, bs));
+    PRK_TRY(bset_ensure(B.d_temp, std::max(sort_bytes, scan_bytes)));
+    PRK_TRY(prk_bin_phase2(&fp, B.d_ranges.p, (const uint32_t *)B.d_tri_off.p, total, (uint32_t *)B.d_keys_a.p,
+                           B.d_vals_a.p, (uint32_t *)B.d_keys_b.p, B.d_bins.p, (uint32_t *)B.d_pair_tri.p,
+                           (uint32_t *)B.d_offs.p, won, won_stride, trwon, B.d_temp.p, &sort_bytes, bs));
     PRK_TRY(hipEventRecord(c->ev[slot][1], bs));
     PRK_TRY(hipEventRecord(B.binned_ev, bs));
 

@@ -122,10 +122,20 @@ __global__ void k_bin_count(FrameParams fp, uint32_t *__restrict__ tri_n, TileRa
 // pairs are grouped by how many of the tile's rows the triangle can cover
 // (bin order is free: the pair index breaks visibility ties), so the 64
 // triangles a k_vis wave walks together cover similar row counts.
+// It also clears the frame's won flags of its pairs (won_stride bytes per
+// pair) and of its triangle (trwon, span-record frames), which k_vis sets.
+__device__ __forceinline__ void clear_won(uint8_t *__restrict__ won, uint32_t stride, uint32_t o) {
+    if (stride == 8) *reinterpret_cast<uint64_t *>(won + (size_t)o * 8) = 0;
+    else
+        for (uint32_t i = 0; i < stride; ++i) won[(size_t)o * stride + i] = 0;
+}
+
 __global__ void k_bin_emit(FrameParams fp, const TileRange *__restrict__ ranges, const uint32_t *__restrict__ off,
-                           uint32_t *__restrict__ keys, uint2 *__restrict__ vals, uint32_t *__restrict__ pair_tri) {
+                           uint32_t *__restrict__ keys, uint2 *__restrict__ vals, uint32_t *__restrict__ pair_tri,
+                           uint8_t *__restrict__ won, uint32_t won_stride, uint8_t *__restrict__ trwon) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= fp.tri_count) return;
+    if (trwon) trwon[g] = 0;
     const TileRange tr = ranges[g];
     uint32_t o = off[g];
     constexpr int kMaxClass = (1 << kRowClassBits) - 1;
@@ -138,6 +148,7 @@ __global__ void k_bin_emit(FrameParams fp, const TileRange *__restrict__ ranges,
                 keys[o] = ((uint32_t)(ty * fp.tiles_x + tx) << kRowClassBits) | cls;
                 vals[o] = make_uint2(g, o);
                 pair_tri[o] = g;
+                clear_won(won, won_stride, o);
                 ++o;
             }
         }
@@ -146,6 +157,7 @@ __global__ void k_bin_emit(FrameParams fp, const TileRange *__restrict__ ranges,
             keys[o] = ((uint32_t)(ty * fp.tiles_x) << kRowClassBits) | (uint32_t)kMaxClass;
             vals[o] = make_uint2(g, o);
             pair_tri[o] = g;
+            clear_won(won, won_stride, o);
             ++o;
         }
 }
@@ -191,11 +203,13 @@ hipError_t prk_bin_phase1(const prk::FrameParams *fp, uint32_t *tri_n, uint32_t 
 
 // Phase 2: emit pairs in triangle order, stable sort of the (triangle, pair)
 // values by tile, tile offsets.  keys_a / vals_a: pairs in triangle order;
-// keys_b / bins: sorted by tile; pair_tri: triangle per pair.
+// keys_b / bins: sorted by tile; pair_tri: triangle per pair; won (won_stride
+// bytes per pair) and trwon (T bytes, may be null) cleared.
 // With temp == nullptr only reports the temp storage the sort needs.
 hipError_t prk_bin_phase2(const prk::FrameParams *fp, const void *ranges, const uint32_t *scan_out, uint32_t total,
                           uint32_t *keys_a, void *vals_a, uint32_t *keys_b, void *bins, uint32_t *pair_tri,
-                          uint32_t *offs, void *temp, size_t *temp_bytes, hipStream_t s) {
+                          uint32_t *offs, uint8_t *won, uint32_t won_stride, uint8_t *trwon, void *temp,
+                          size_t *temp_bytes, hipStream_t s) {
     const uint32_t ntiles = (uint32_t)(fp->tiles_x * fp->tiles_y);
     int bits = 1;
     while ((1u << bits) < ntiles && bits < 32) ++bits;
@@ -207,7 +221,7 @@ hipError_t prk_bin_phase2(const prk::FrameParams *fp, const void *ranges, const 
     if (fp->tri_count)
         hipLaunchKernelGGL(prk::k_bin_emit, dim3((fp->tri_count + 255) / 256), dim3(256), 0, s, *fp,
                            reinterpret_cast<const prk::TileRange *>(ranges), scan_out, keys_a,
-                           reinterpret_cast<uint2 *>(vals_a), pair_tri);
+                           reinterpret_cast<uint2 *>(vals_a), pair_tri, won, won_stride, trwon);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (total) {
