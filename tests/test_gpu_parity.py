@@ -193,6 +193,38 @@ def test_pipelined_frames_one_target(gpu):
     assert (gc == oc).all()
 
 
+def test_draw_tables_change_between_frames(gpu):
+    """Each scratch set re-sends its draw / texture tables only when their
+    bytes change: frames that alternate geometry and texture on the same set
+    (frame k uses set k % 2) must each render their own draws."""
+    a = scenes.random_soup(3000, 256, 192, radius=16, seed=61)
+    b = scenes.random_soup(3000, 256, 192, radius=16, seed=62)
+    plan = [(a, a), (a, a), (b, b), (a, a), (a, b), (b, a), (b, a), (a, a)]  # (geometry, texture source)
+    r = prk.Renderer(0)
+    try:
+        r.target_alloc(256, 192)
+        r.set_camera(a.prk_transform(), a.prk_lights())
+        geo = {id(a): r.geometry(a.vertices, a.colors, a.normals, a.uvs),
+               id(b): r.geometry(b.vertices, b.colors, b.normals, b.uvs)}
+        tex = {id(a): r.texture(a.texture), id(b): r.texture(b.texture)}
+        got = []
+        for g, t in plan:
+            r.clear_on_flush()
+            r.draw_model_optimized(geo[id(g)], g.tri_count, P=g.P, bitmap=tex[id(t)], phong=True)
+            r.complete_all_work()
+            r.synchronize()
+            got.append(r.download())
+    finally:
+        r.close()
+    ta, tb = a.texture, b.texture
+    for k, ((g, t), (gc, gz)) in enumerate(zip(plan, got)):
+        g.texture = ta if t is a else tb
+        oc, oz, _, _ = O.render(g)
+        g.texture = ta if g is a else tb
+        assert (gz.view(np.uint32) == oz.view(np.uint32)).all(), k
+        assert (gc == oc).all(), k
+
+
 def test_row_band(gpu):
     s = scenes.random_soup(10000, 512, 512, radius=20, seed=17)
     oc, oz, ow, _ = O.render(s)
