@@ -35,9 +35,9 @@ hipError_t prk_walk_select_bytes(uint32_t, size_t *);
 // AVX frames shade through span records (k_walk + k_pix); must match
 // PRK_SPAN_RECORDS of prk_kernels.hip.
 #define PRK_SPAN_RECORDS_HOST 1
-// Per-frame scratch sets: at most PRK_FRAME_SETS in flight.  A frame whose
-// target band has at most kSmallBandPx pixels uses 3 sets (frame k: set
-// k % 3), larger ones 2: with three, frame k+1's binning need not wait for
+// Per-frame scratch sets in flight: a frame whose target band has at most
+// kSmallBandPx pixels cycles PRK_FRAME_SETS sets (frame k: set k % 3),
+// larger ones 2: with three, frame k+1's binning need not wait for
 // frame k-1's raster, which pays when binning is a large share of the frame
 // (band of 512 x 4096 px, one rank of 8: 0.284 -> 0.247 ms; 1024 rows:
 // 0.405 -> 0.378) and costs ~1-3 % on bigger frames, where the extra
@@ -632,8 +632,8 @@ int prk_flush(prk_context *c, void *stream) {
     // Binning runs on bin_stream into scratch set k % 2, so it overlaps the
     // previous frame's raster on the flush stream; the raster waits for it.
     // (any set may follow any: a set's reuse waits for its own last reader)
-    const int nsets = std::min(prk_context::kSets,
-                               (size_t)c->W * (size_t)(c->row1 - c->row0) <= kSmallBandPx ? 3 : 2);
+    const int nsets = (size_t)c->W * (size_t)(c->row1 - c->row0) <= kSmallBandPx ? prk_context::kSets
+                                                                                : std::min(prk_context::kSets, 2);
     prk_context::BinSet &B = c->bset[c->frame % nsets];
     hipStream_t bs = c->bin_stream;
     if (B.used) PRK_TRY(hipStreamWaitEvent(bs, B.free_ev, 0));  // the raster of frame k-2 read this set
