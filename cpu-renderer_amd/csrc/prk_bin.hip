@@ -8,7 +8,7 @@
 //                 triangle's offset, i.e. in triangle order (pair j), row-major
 //                 over the triangle's tile rectangle; pair_tri[j] = triangle.
 //   sort          stable LSD radix sort of the 8-byte (triangle, pair) values
-//                 by tile (hipcub), so every tile's bin lists its triangles in
+//                 by tile (rocprim onesweep), so every tile's bin lists its triangles in
 //                 submission order.
 //   k_tile_offsets  bin start of every tile (lower_bound on the sorted tiles).
 //
