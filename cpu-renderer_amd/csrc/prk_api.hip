@@ -663,7 +663,9 @@ int prk_flush(prk_context *c, void *stream) {
         if (at == d.p && mirror.size() == bytes && std::memcmp(mirror.data(), src, bytes) == 0) return hipSuccess;
         mirror.assign((const uint8_t *)src, (const uint8_t *)src + bytes);
         at = d.p;
-        return hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, bs);
+        // from the mirror: it outlives this call (the next frame's host sync
+        // on the bin stream precedes its next reassignment)
+        return hipMemcpyAsync(d.p, mirror.data(), bytes, hipMemcpyHostToDevice, bs);
     };
     PRK_TRY(upload_table(B.d_draws, B.h_draws, B.h_draws_at, c->draws.data(),
                          c->draws.size() * sizeof(prk::DrawRec)));
