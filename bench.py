@@ -49,85 +49,134 @@ def parse():
 
 
 def algorithmic_bytes(T, W, rows, tex_texels):
-    """Bytes the frame must move at minimum: positions +
-    normals + uvs read once (96 B/triangle; FillLineOptimized never reads
-    vertex colours), z and colour of every pixel written once (8 B/pixel: the
-    frame starts from a clear, fused into its kernels, so no prior z is read),
-    the texture read once."""
-    return 96 * T + 8 * W * rows + 4 * tex_texels
+    """Algorithmic bytes of one frame, SURVEY §8(d): the geometry read once
+    (144 B/triangle: v3 position + v4 colour + v3 normal + v2 uv per vertex),
+    z and colour of every pixel written once (8 B/pixel: the frame starts
+    from a clear fused into its kernels, so no prior z is read), each texel
+    read once.  (FillLineOptimized never reads vertex colours, so the bytes
+    the AVX path must move are 48 B/triangle fewer; DESIGN.md §5 gives both.)"""
+    return 144 * T + 8 * W * rows + 4 * tex_texels
 
 
 def load_traffic(cfg_key):
-    """HBM bytes per k_raster launch measured with rocprofv3 PMC passes
-    (tools/pmc_traffic.py writes profiles/pmc_traffic.json), or None."""
+    """HBM bytes per frame measured with rocprofv3 PMC passes
+    (tools/profile_round.sh -> tools/pmc_traffic.py -> profiles/pmc_traffic.json,
+    committed with the round's profiles), or (None, None).  NOT measured by
+    this run: the counters need their own rocprofv3 passes."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
         e = d.get(cfg_key)
-        return None if e is None else float(e["hbm_bytes_per_launch"])
+        if e is None:
+            return None, None
+        return float(e["hbm_bytes_per_frame"]), "profiles/pmc_traffic.json[%s] (%s)" % (cfg_key, e.get("round", "?"))
     except Exception:
-        return None
+        return None, None
 
 
-def cpu_baseline(scene, threads, max_tris, frames=5):
+def cpu_topology():
+    """Host CPUs this process may run on, their physical cores and SMT, and
+    the cgroup CPU quota (the box's share of the host)."""
+    aff = sorted(os.sched_getaffinity(0))
+    cores, model = set(), None
+    try:
+        cur = {}
+        with open("/proc/cpuinfo") as f:
+            for ln in f.read().split("\n\n"):
+                kv = dict((a.strip(), b.strip()) for a, b in
+                          (x.split(":", 1) for x in ln.split("\n") if ":" in x))
+                if "processor" not in kv:
+                    continue
+                model = model or kv.get("model name")
+                if int(kv["processor"]) in aff:
+                    cores.add((kv.get("physical id", "0"), kv.get("core id", kv["processor"])))
+                cur = kv
+        del cur
+    except (OSError, ValueError, KeyError):
+        pass
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            quota = None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    phys = len(cores) or None
+    return dict(affinity_cpus=len(aff), physical_cores=phys,
+                smt=(len(aff) / phys) if phys else None, cgroup_cpu_quota=quota, cpu_model=model,
+                host_cpus=os.cpu_count())
+
+
+def cpu_baseline(scene, threads, max_tris, frames=3, scan=(16, 64)):
     """The CPU path on the same scene, on the host cores (SURVEY §8(d) "CPU
     path timing"): the AVX2 restatement (oracle/prk_cpu_avx.c, bit-exact to
-    the scalar oracle) under both schedules — "banded" (row bands per thread,
-    no locks) and "queue" (the reference's producer AET -> per-span work queue
-    -> workers with the per-8-px ZMask spinlock).  Median of `frames` frames
-    after one warm-up; the queue schedule (the slow one) is timed on a bounded
-    sample of the scene and scaled linearly.  `value` is the faster one."""
+    the scalar oracle) on `threads` = every CPU of this process's affinity
+    mask, under three schedules:
+      banded  row bands per thread, no locks (median of `frames` full frames
+              after one warm-up);
+      queue   the reference's DrawModelOptimized(RenderQueue,...): a producer
+              AET posts one task per span, workers take the per-8-px ZMask
+              spinlock (projekt.cpp:3615-3871, 2202-2239);
+      rows    DrawModelOptimizedLines + FillLinesOptimized: one task per row
+              of an object (projekt.cpp:3362-3613, 629-1490).
+    queue / rows are timed on a bounded sample (the scene's first triangles)
+    and scaled to the scene.  `value` is the fastest schedule at `threads`;
+    `scan` has the banded schedule at fewer threads for context."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from prk import abi
     T = scene.tri_count
+    px = scene.width * scene.height
+    topo = cpu_topology()
     if O.cpu_lib() is None:  # no AVX2 on this host: the scalar port, banded
         n = min(T, max_tris)
         sub = scene if n == T else scene.subset(0, n)
         t0 = time.perf_counter()
         _, _, _, st = O.render(sub, semantics=abi.PRK_SEM_AVX, phong=True, threads=threads, winners=False)
         frame = (time.perf_counter() - t0) * (T / n)
-        return dict(value=scene.width * scene.height / frame / 1e6, unit="Mpixels/s", cores=threads, kind="port",
+        return dict(value=px / frame / 1e6, unit="Mpixels/s", cores=threads, kind="port",
                     sample="scalar oracle (no AVX2 on this host), %d of %d triangles, banded over %d threads"
-                           % (n, T, threads), frame_s=frame, span_pixels=st["span_pixels"] if n == T else None)
+                           % (n, T, threads), frame_s=frame, span_pixels=st["span_pixels"] if n == T else None,
+                    **topo)
 
-    def timed(sub, cpu, nframes):
+    def timed(sub, cpu, th, nframes):
         ts, st = [], None
         for i in range(nframes + 1):
             t0 = time.perf_counter()
-            _, _, _, st = O.render(sub, semantics=abi.PRK_SEM_AVX, phong=True, threads=threads, winners=False,
-                                   cpu=cpu)
+            _, _, _, st = O.render(sub, semantics=abi.PRK_SEM_AVX, phong=True, threads=th, winners=False, cpu=cpu)
             if i:
                 ts.append(time.perf_counter() - t0)
         return float(np.median(ts)), st
 
     n = min(T, max_tris)
     sub = scene if n == T else scene.subset(0, n)
-    fb, st = timed(sub, "banded", frames)
+    fb, st = timed(sub, "banded", threads, frames)
     fb *= T / n
-    nq = min(n, 200_000)
+    variants = {"banded": {"threads": threads, "frame_ms": fb * 1e3, "mpixels_s": px / fb / 1e6,
+                           "sample": "%d of %d triangles, median of %d frames" % (n, T, frames)}}
+    nq = min(n, 20_000)
     subq = scene.subset(0, nq) if nq < T else scene
-    fq, _ = timed(subq, "queue", 3)
-    fq *= T / nq
-    px = scene.width * scene.height
-    variants = {"banded": {"frame_ms": fb * 1e3, "mpixels_s": px / fb / 1e6},
-                "queue": {"frame_ms": fq * 1e3, "mpixels_s": px / fq / 1e6}}
-    best = min(fb, fq)
-    cpu_model = None
-    try:
-        with open("/proc/cpuinfo") as f:
-            cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
-    except OSError:
-        pass
-    return dict(value=px / best / 1e6, unit="Mpixels/s", cores=threads, kind="port", cpu_model=cpu_model,
-                host_cpus=os.cpu_count(),
-                sample="AVX2 restatement of FillLineOptimized (oracle/prk_cpu_avx.c) on %d threads; banded: "
-                       "median of %d full frames (%d of %d triangles%s) after 1 warm-up; queue: median of 3 "
-                       "frames of the first %d triangles after 1 warm-up, scaled to T; value = faster schedule "
-                       "(%s)" % (threads, frames, n, T, "" if n == T else ", scaled to T", nq,
-                                 "banded" if fb <= fq else "queue"),
-                variants=variants, frame_s=best, span_pixels=st["span_pixels"] if n == T else None)
+    for sched in ("queue", "rows"):
+        fq, _ = timed(subq, sched, threads, 2)
+        fq *= T / nq
+        variants[sched] = {"threads": threads, "frame_ms": fq * 1e3, "mpixels_s": px / fq / 1e6,
+                           "sample": "first %d triangles, median of 2 frames, scaled to T" % nq}
+    scan_out = {}
+    for th in scan:
+        if th < threads:
+            f, _ = timed(sub, "banded", th, frames)
+            f *= T / n
+            scan_out[str(th)] = {"frame_ms": f * 1e3, "mpixels_s": px / f / 1e6}
+    scan_out[str(threads)] = {"frame_ms": fb * 1e3, "mpixels_s": px / fb / 1e6}
+    best = min(variants, key=lambda k: variants[k]["frame_ms"])
+    frame = variants[best]["frame_ms"] * 1e-3
+    return dict(value=px / frame / 1e6, unit="Mpixels/s", cores=threads, kind="port",
+                sample="AVX2 restatement of FillLineOptimized (oracle/prk_cpu_avx.c) on all %d CPUs of the "
+                       "affinity mask; value = fastest schedule (%s); banded: %s; queue/rows: %s"
+                       % (threads, best, variants["banded"]["sample"], variants["queue"]["sample"]),
+                variants=variants, banded_thread_scan=scan_out, frame_s=frame,
+                span_pixels=st["span_pixels"] if n == T else None, **topo)
 
 
 def main():
@@ -227,8 +276,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    # Per-kernel device time: HIP events recorded on the launch stream around
-    # k_bin_* and k_raster in every flush of the timed region.
+    # Per-kernel device time in the timed (pipelined) frames: HIP events
+    # recorded on the launch streams; frames overlap, so these are stretched
+    # spans, not serial shares of a frame.
     stats = r.stats()
     nt = max(1, stats["frames_timed"])
     ms_bin = stats["sum_ms_bin"] / nt
@@ -236,6 +286,19 @@ def main():
     ms_vis = stats["sum_ms_vis"] / nt
     ms_span = stats["sum_ms_span"] / nt
     ms_pix = ms_raster - ms_vis - ms_span
+    # Serial kernel times (outside the timed region): the same frame with the
+    # host waiting for each frame, so no kernel overlaps another frame's.
+    r.timing_reset()
+    for _ in range(5):
+        step()
+        drain()
+        torch.cuda.synchronize()
+    ss = r.stats()
+    ns = max(1, ss["frames_timed"])
+    serial = {"k_bin_phase": ss["sum_ms_bin"] / ns, "k_vis": ss["sum_ms_vis"] / ns,
+              "k_walk": ss["sum_ms_span"] / ns,
+              "k_pix": (ss["sum_ms_raster"] - ss["sum_ms_vis"] - ss["sum_ms_span"]) / ns,
+              "raster": ss["sum_ms_raster"] / ns}
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -267,11 +330,13 @@ def main():
             dist.destroy_process_group()
         return
     T = scene.tri_count
-    tex_texels = scene.texture.width * (scene.texture.height + 1)
+    tex_texels = scene.texture.width * scene.texture.height
     alg = algorithmic_bytes(T, W, rows, tex_texels)
-    achieved = alg / (ms_raster * 1e-3) / 1e9 if ms_raster > 0 else 0.0
+    # Roofline of the whole frame (every kernel of the step): SURVEY §8(d)'s
+    # algorithmic bytes per frame over the measured time per frame.
+    achieved = alg / (ms * 1e-3) / 1e9
     cfg_key = "%dx%d_T%d_r%g_N%d" % (W, H, T, a.radius, world)
-    traffic = load_traffic(cfg_key)
+    traffic, traffic_src = load_traffic(cfg_key)
     out = {
         "metric": "Mpixels/s shaded (+ Mtri/s) at 4096x4096, 1M tris; 1/2/4/8 GPUs",
         "value": W * H / (ms * 1e-3) / 1e6,
@@ -295,23 +360,31 @@ def main():
         "mtri_per_s": T / (ms * 1e-3) / 1e6,
         # binning runs on its own stream, overlapping the previous frame's
         # raster: ms_bin is its (stretched) span, not a serial share of the frame
+        # pipelined frames: HIP-event spans stretched by the overlap with the
+        # neighbouring frames' kernels (not serial shares of ms_per_step)
         "ms_bin_overlapped": ms_bin,
-        "ms_raster": ms_raster,
-        "ms_kernels": {"k_vis": ms_vis, "k_walk": ms_span, "k_pix": ms_pix},
+        "ms_raster_overlapped": ms_raster,
+        "ms_kernels_overlapped": {"k_vis": ms_vis, "k_walk": ms_span, "k_pix": ms_pix},
+        # serial: 5 more frames with the host waiting after each one
+        "ms_kernels_serial": serial,
         "bin_entries": int(stats["bin_entries"]),
         "ms_upload": ms_upload,
         "ms_download": ms_download,
-        # The raster stage (k_vis -> k_walk -> k_pix, back to back on one
-        # stream) is priced as one unit: its algorithmic bytes over the stage's
-        # HIP-event duration.
-        "roofline": {"bound": "hbm", "kernel": "raster stage (k_vis+k_walk+k_pix)", "achieved": achieved,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "algorithmic_bytes": alg},
+        # Whole frame against HBM: SURVEY §8(d) algorithmic bytes / ms_per_step.
+        # The dominant kernel (k_vis) is VALU/latency-bound, not HBM-bound
+        # (profiles/*sq*): its serial time and the same bytes
+        # over it are reported beside the frame figure.
+        "roofline": {"bound": "hbm", "kernel": "whole frame (binning + k_vis + k_walk + k_pix)",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes": alg,
+                     "dominant_kernel": {"name": "k_vis", "ms_serial": serial["k_vis"],
+                                         "share_of_serial_frame": serial["k_vis"] / max(
+                                             1e-9, serial["raster"] + serial["k_bin_phase"])}},
     }
     if check is not None:
         out["check"] = check
     if a.cpu_baseline and world == 1:
-        threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+        threads = a.cpu_threads or len(os.sched_getaffinity(0))
         cb = cpu_baseline(scene, threads, a.cpu_max_tris)
         out["cpu_baseline"] = cb
         cb.pop("frame_s", None)

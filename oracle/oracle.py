@@ -60,7 +60,8 @@ def cpu_lib():
         if not os.path.exists(path):
             build()
         _CPU = C.CDLL(path)
-        for fn in ("cpu_avx_draw", "cpu_avx_draw_banded", "cpu_avx_draw_queue", "cpu_avx_supported"):
+        for fn in ("cpu_avx_draw", "cpu_avx_draw_banded", "cpu_avx_draw_queue", "cpu_avx_draw_rows",
+                   "cpu_avx_supported"):
             getattr(_CPU, fn).restype = C.c_int
     return _CPU if _CPU.cpu_avx_supported() else None
 
@@ -104,8 +105,9 @@ def render(scene, semantics=abi.PRK_SEM_AVX, phong=True, tris_per_object=1, thre
     """Draw `scene` with the oracle.  Returns (color u32[H,W], z f32[H,W],
     winners i32[H,W] or None, stats dict).  `color`/`z` (optional) are the
     prior target contents (default: reference clear values).
-    cpu: None = the scalar restatement (liboracle.so); "banded" / "queue" =
-    the AVX2 CPU baseline (liborcpu.so) with that schedule over `threads`."""
+    cpu: None = the scalar restatement (liboracle.so); "banded" / "queue" /
+    "rows" = the AVX2 CPU baseline (liborcpu.so) with that schedule over
+    `threads`."""
     W, H = scene.width, scene.height
     col = np.full((H, W), CLEAR_COLOR, np.uint32) if color is None else np.array(color, np.uint32)
     zb = np.full((H, W), CLEAR_Z, np.float32) if z is None else np.array(z, np.float32)
@@ -131,7 +133,7 @@ def _render_one(scene, semantics, phong, tris_per_object, threads, col, zb, win,
         L = cpu_lib()
         if L is None:
             raise RuntimeError("AVX2 CPU baseline: host has no AVX2")
-        fn = {"banded": L.cpu_avx_draw_banded, "queue": L.cpu_avx_draw_queue}[cpu]
+        fn = {"banded": L.cpu_avx_draw_banded, "queue": L.cpu_avx_draw_queue, "rows": L.cpu_avx_draw_rows}[cpu]
         rc = fn(C.byref(k.desc), C.byref(tg), C.byref(k.transform), C.byref(k.lights), int(threads), stats)
         if rc != 0:
             raise RuntimeError("cpu baseline failed: %s" % abi.STATUS_NAMES.get(rc, rc))

@@ -25,6 +25,13 @@
  *     done (Platform.CompleteAllWork).  Strict `z > zbuf` makes the result
  *     independent of the order spans run in, except for exactly equal z
  *     (the earlier fragment wins sequentially, whichever runs first here).
+ *   * rows (cpu_avx_draw_rows): DrawModelOptimizedLines (3362-3613) +
+ *     FillLinesOptimized (629-1490): the same producer AET, but every row of
+ *     an object becomes ONE task carrying the row's span end points
+ *     (thread_edge_info: left/right X, z, 1/z, U, V, normal; projekt.h:39-63,
+ *     3518-3544) and a worker fills the row's spans in order under the same
+ *     ZMask spinlock.  FillLinesOptimized's block math is FillLineOptimized's
+ *     (SURVEY §2 #12), so the frame is identical; only the task grain differs.
  */
 #include <immintrin.h>
 #include <stdatomic.h>
@@ -272,16 +279,27 @@ int cpu_avx_draw(const or_draw_desc *D, const or_target *Tg, const prk_transform
 typedef struct cpu_work { /* line_render_work: both edges by value + row (3759-3809) */
     or_edge L, R;
     int32_t Row, TriIndex;
+    int32_t NPairs;          /* rows schedule: pairs of the row's task (0: one span in L/R) */
+    int32_t First;           /* rows schedule: first pair in the pair ring */
 } cpu_work;
+
+/* rows schedule: span end points of one pair (thread_edge_info, projekt.h:39-63) */
+typedef struct cpu_pair {
+    float LX, RX, LZ, RZ, LW, RW, LU, RU, LV, RV, LN[3], RN[3];
+} cpu_pair;
+#define CPU_PBITS 20
+#define CPU_PSIZE (1u << CPU_PBITS)
 
 #define CPU_QBITS 16
 #define CPU_QSIZE (1u << CPU_QBITS)
 typedef struct cpu_queue { /* single producer, many consumers, bounded ring */
     cpu_work *Slots;
+    cpu_pair *Pairs;                /* rows schedule: pair ring (CPU_PSIZE) */
     atomic_uint_fast64_t *Seq;      /* per slot: the ticket it is ready for */
     _Alignas(64) atomic_uint_fast64_t Head; /* next ticket to post */
     _Alignas(64) atomic_uint_fast64_t Tail; /* next ticket to take */
     _Alignas(64) atomic_int Done;
+    _Alignas(64) atomic_int Running;  /* rows schedule: tasks taken and not yet finished */
 } cpu_queue;
 
 typedef struct cpu_qctx {
@@ -306,9 +324,30 @@ static int cpu_take_one(cpu_queue *Q, or_ctx *X_)
                                                        memory_order_relaxed))
                 continue;
             cpu_work w = Q->Slots[i];
+            if (w.NPairs == 0) {
+                atomic_store_explicit(&Q->Seq[i], t + CPU_QSIZE, memory_order_release);
+                X_->TriIndex = w.TriIndex;
+                cpu_fill_line_avx2(X_, &w.L, &w.R, w.Row);
+                return 1;
+            }
+            /* FillLinesOptimized (629-1490): the row's pairs in order, each
+             * rebuilt as an edge pair from its end points (648-670).  The pair
+             * slots stay owned by this task until Running drops. */
+            atomic_fetch_add_explicit(&Q->Running, 1, memory_order_acq_rel);
             atomic_store_explicit(&Q->Seq[i], t + CPU_QSIZE, memory_order_release);
             X_->TriIndex = w.TriIndex;
-            cpu_fill_line_avx2(X_, &w.L, &w.R, w.Row);
+            for (int32_t k = 0; k < w.NPairs; ++k) {
+                const cpu_pair *p = &Q->Pairs[(uint32_t)(w.First + k) & (CPU_PSIZE - 1)];
+                or_edge L, R;
+                memset(&L, 0, sizeof L);
+                memset(&R, 0, sizeof R);
+                L.XMin = p->LX; R.XMin = p->RX; L.ZMin = p->LZ; R.ZMin = p->RZ;
+                L.OneOverZMin = p->LW; R.OneOverZMin = p->RW; L.UMin = p->LU; R.UMin = p->RU;
+                L.VMin = p->LV; R.VMin = p->RV;
+                for (int c = 0; c < 3; ++c) { L.MinNormal[c] = p->LN[c]; R.MinNormal[c] = p->RN[c]; }
+                cpu_fill_line_avx2(X_, &L, &R, w.Row);
+            }
+            atomic_fetch_sub_explicit(&Q->Running, 1, memory_order_acq_rel);
             return 1;
         }
         if (s < t + 1) return 0; /* empty */
@@ -316,21 +355,80 @@ static int cpu_take_one(cpu_queue *Q, or_ctx *X_)
     }
 }
 
-static void cpu_post_span(or_ctx *X_, const or_edge *L, const or_edge *R, int32_t Row)
+/* Claim the next ring slot (the producer runs queued tasks itself while the
+ * ring is full, so one thread, or slow workers, cannot deadlock it). */
+static cpu_work *cpu_claim(cpu_queue *Q, uint64_t *ticket)
 {
-    cpu_queue *Q = tl_post_q;
     uint64_t t = atomic_load_explicit(&Q->Head, memory_order_relaxed);
     size_t i = t & (CPU_QSIZE - 1);
-    /* Ring full: the producer runs queued spans itself until the slot frees
-     * (so one thread, or slow workers, cannot deadlock it). */
     while (atomic_load_explicit(&Q->Seq[i], memory_order_acquire) != t)
         if (!cpu_take_one(Q, tl_exec)) _mm_pause();
-    Q->Slots[i].L = *L;
-    Q->Slots[i].R = *R;
-    Q->Slots[i].Row = Row;
-    Q->Slots[i].TriIndex = X_->TriIndex;
-    atomic_store_explicit(&Q->Seq[i], t + 1, memory_order_release);
+    *ticket = t;
+    return &Q->Slots[i];
+}
+
+static void cpu_publish(cpu_queue *Q, uint64_t t)
+{
+    atomic_store_explicit(&Q->Seq[t & (CPU_QSIZE - 1)], t + 1, memory_order_release);
     atomic_store_explicit(&Q->Head, t + 1, memory_order_release);
+}
+
+static void cpu_post_span(or_ctx *X_, const or_edge *L, const or_edge *R, int32_t Row)
+{
+    uint64_t t;
+    cpu_work *w = cpu_claim(tl_post_q, &t);
+    w->L = *L;
+    w->R = *R;
+    w->Row = Row;
+    w->TriIndex = X_->TriIndex;
+    w->NPairs = 0;
+    cpu_publish(tl_post_q, t);
+}
+
+/* rows schedule producer: the AET walk hands over its spans one at a time, in
+ * row order; the spans of one row are gathered and posted as one task
+ * (3518-3609) when the row changes or the object ends. */
+typedef struct cpu_rowbuf {
+    int32_t Row, Tri, N, First;
+    uint32_t Next;       /* pair ring write position */
+    uint64_t TaskBase;   /* first ring ticket of the pending pair run */
+} cpu_rowbuf;
+static _Thread_local cpu_rowbuf tl_row;
+
+static void cpu_row_flush(void)
+{
+    if (tl_row.N == 0) return;
+    uint64_t t;
+    cpu_work *w = cpu_claim(tl_post_q, &t);
+    w->Row = tl_row.Row;
+    w->TriIndex = tl_row.Tri;
+    w->NPairs = tl_row.N;
+    w->First = tl_row.First;
+    cpu_publish(tl_post_q, t);
+    tl_row.N = 0;
+}
+
+static void cpu_post_row_pair(or_ctx *X_, const or_edge *L, const or_edge *R, int32_t Row)
+{
+    cpu_queue *Q = tl_post_q;
+    if (tl_row.N && (Row != tl_row.Row || tl_row.N >= 1000)) cpu_row_flush(); /* ThreadEdges[1000] */
+    /* The pair ring wraps only when no task holds pair slots: the producer
+     * helps drain the queue, then waits for the tasks still running. */
+    if (tl_row.Next + 1000u > CPU_PSIZE && tl_row.N == 0) {
+        while (atomic_load_explicit(&Q->Tail, memory_order_acquire) !=
+               atomic_load_explicit(&Q->Head, memory_order_acquire))
+            if (!cpu_take_one(Q, tl_exec)) _mm_pause();
+        while (atomic_load_explicit(&Q->Running, memory_order_acquire) != 0) _mm_pause();
+        tl_row.Next = 0;
+    }
+    if (tl_row.N == 0) { tl_row.Row = Row; tl_row.Tri = X_->TriIndex; tl_row.First = (int32_t)tl_row.Next; }
+    cpu_pair *p = &Q->Pairs[tl_row.Next & (CPU_PSIZE - 1)];
+    tl_row.Next++;
+    p->LX = L->XMin; p->RX = R->XMin; p->LZ = L->ZMin; p->RZ = R->ZMin;
+    p->LW = L->OneOverZMin; p->RW = R->OneOverZMin; p->LU = L->UMin; p->RU = R->UMin;
+    p->LV = L->VMin; p->RV = R->VMin;
+    for (int c = 0; c < 3; ++c) { p->LN[c] = L->MinNormal[c]; p->RN[c] = R->MinNormal[c]; }
+    tl_row.N++;
 }
 
 /* Take and run spans until the producer is done and the queue is empty. */
@@ -359,26 +457,27 @@ static void *cpu_worker(void *p)
     return NULL;
 }
 
-int cpu_avx_draw_queue(const or_draw_desc *D, const or_target *Tg, const prk_transform *T,
-                       const prk_light_data *Lights, int32_t threads, uint64_t *stats)
+static int cpu_avx_draw_tasks(const or_draw_desc *D, const or_target *Tg, const prk_transform *T,
+                              const prk_light_data *Lights, int32_t threads, uint64_t *stats, int rows)
 {
     if (!D || !Tg || !T || !Lights) return PRK_ERR_ARG;
     if (D->Semantics != PRK_SEM_AVX || !D->Bitmap || !D->Phong || (Tg->Width % 8)) return PRK_ERR_UNSUPPORTED;
     if (Lights->LightCount > PRK_MAX_LIGHTS) return PRK_ERR_ARG;
     if (threads < 1) threads = 1;
-    if (threads > 256) threads = 256;
+    if (threads > 1024) threads = 1024;
     const int nworkers = threads - 1; /* the producer is the last thread */
     cpu_queue Q;
     memset(&Q, 0, sizeof Q);
     Q.Slots = (cpu_work *)malloc(sizeof(cpu_work) * CPU_QSIZE);
     Q.Seq = (atomic_uint_fast64_t *)malloc(sizeof(atomic_uint_fast64_t) * CPU_QSIZE);
+    Q.Pairs = rows ? (cpu_pair *)malloc(sizeof(cpu_pair) * CPU_PSIZE) : NULL;
     size_t nlock = ((size_t)Tg->Width * Tg->Height + 7) / 8;
     atomic_uchar *zm = (atomic_uchar *)calloc(nlock, 1);
     uint32_t per = D->TrisPerObject ? D->TrisPerObject : 1;
     or_edge *Edges = (or_edge *)malloc(sizeof(or_edge) * 3 * per);
     or_edge *Sort = (or_edge *)malloc(sizeof(or_edge) * 3 * per);
-    if (!Q.Slots || !Q.Seq || !zm || !Edges || !Sort) {
-        free(Q.Slots); free(Q.Seq); free(zm); free(Edges); free(Sort);
+    if (!Q.Slots || !Q.Seq || !zm || !Edges || !Sort || (rows && !Q.Pairs)) {
+        free(Q.Slots); free(Q.Seq); free(Q.Pairs); free(zm); free(Edges); free(Sort);
         return PRK_ERR_NOMEM;
     }
     for (size_t i = 0; i < CPU_QSIZE; ++i) atomic_init(&Q.Seq[i], i);
@@ -392,9 +491,14 @@ int cpu_avx_draw_queue(const or_draw_desc *D, const or_target *Tg, const prk_tra
     base.RowLo = 0; base.RowHi = Tg->Height; base.Phong = D->Phong; base.Filter = D->Filter;
     base.BandH = 1; base.BandMod = 1; base.BandRem = 0;
 
-    cpu_qctx ctx[256];
-    pthread_t th[256];
-    int started[256];
+    cpu_qctx *ctx = (cpu_qctx *)calloc((size_t)threads, sizeof(cpu_qctx));
+    pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+    int *started = (int *)calloc((size_t)threads, sizeof(int));
+    if (!ctx || !th || !started) {
+        free(ctx); free(th); free(started);
+        free(Q.Slots); free(Q.Seq); free(Q.Pairs); free(zm); free(Edges); free(Sort);
+        return PRK_ERR_NOMEM;
+    }
     for (int k = 0; k < threads; ++k) {
         memset(&ctx[k], 0, sizeof ctx[k]);
         ctx[k].Q = &Q; ctx[k].Base = base; ctx[k].Locks = &locks;
@@ -408,12 +512,14 @@ int cpu_avx_draw_queue(const or_draw_desc *D, const or_target *Tg, const prk_tra
     tl_post_q = &Q;
     tl_exec = &X_;
     tl_locks = &locks;
+    memset(&tl_row, 0, sizeof tl_row);
     for (uint32_t t0 = 0; t0 < D->TriCount; t0 += per) {
         uint32_t n = D->TriCount - t0 < per ? D->TriCount - t0 : per;
         uint32_t ec = or_fill_edge_table(D->Vertices, D->Colors, D->Normals, D->UVs, t0, n, D->P, 1, D->Phong,
                                          T, Lights, Edges, Sort);
         P.TriIndex = D->TriIndexBase + (int32_t)t0;
-        or_aet_walk(&P, Edges, ec, cpu_post_span);
+        or_aet_walk(&P, Edges, ec, rows ? cpu_post_row_pair : cpu_post_span);
+        if (rows) cpu_row_flush(); /* the object's last row (3609) */
     }
     tl_post_q = NULL;
     atomic_store_explicit(&Q.Done, 1, memory_order_release);
@@ -429,8 +535,21 @@ int cpu_avx_draw_queue(const or_draw_desc *D, const or_target *Tg, const prk_tra
     if (stats)
         for (int k = 0; k < threads; ++k)
             for (int j = 0; j < 3; ++j) stats[j] += ctx[k].stats[j];
-    free(Q.Slots); free(Q.Seq); free(zm); free(Edges); free(Sort);
+    free(Q.Slots); free(Q.Seq); free(Q.Pairs); free(zm); free(Edges); free(Sort);
+    free(ctx); free(th); free(started);
     return PRK_OK;
+}
+
+int cpu_avx_draw_queue(const or_draw_desc *D, const or_target *Tg, const prk_transform *T,
+                       const prk_light_data *Lights, int32_t threads, uint64_t *stats)
+{
+    return cpu_avx_draw_tasks(D, Tg, T, Lights, threads, stats, 0);
+}
+
+int cpu_avx_draw_rows(const or_draw_desc *D, const or_target *Tg, const prk_transform *T,
+                      const prk_light_data *Lights, int32_t threads, uint64_t *stats)
+{
+    return cpu_avx_draw_tasks(D, Tg, T, Lights, threads, stats, 1);
 }
 
 int cpu_avx_supported(void) { return __builtin_cpu_supports("avx2") ? 1 : 0; }

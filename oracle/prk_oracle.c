@@ -910,9 +910,10 @@ int oracle_draw_mt(const or_draw_desc *D, const or_target *Tg, const prk_transfo
 {
     if (!Tg) return PRK_ERR_ARG;
     if (threads < 1) threads = 1;
-    if (threads > 256) threads = 256;
-    or_job jobs[256];
-    pthread_t th[256];
+    if (threads > 1024) threads = 1024;
+    or_job *jobs = (or_job *)calloc((size_t)threads, sizeof(or_job));
+    pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+    if (!jobs || !th) { free(jobs); free(th); return PRK_ERR_NOMEM; }
     for (int t = 0; t < threads; ++t) {
         memset(&jobs[t], 0, sizeof jobs[t]);
         jobs[t].D = D; jobs[t].Tg = Tg; jobs[t].T = T; jobs[t].L = Lights;
@@ -926,6 +927,8 @@ int oracle_draw_mt(const or_draw_desc *D, const or_target *Tg, const prk_transfo
         if (jobs[t].rc != PRK_OK) rc = jobs[t].rc;
         if (stats) for (int k = 0; k < 3; ++k) stats[k] += jobs[t].stats[k];
     }
+    free(jobs);
+    free(th);
     return rc;
 }
 

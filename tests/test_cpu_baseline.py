@@ -24,7 +24,8 @@ def same(a, b):
             and a[3]["span_pixels"] == b[3]["span_pixels"])
 
 
-@pytest.mark.parametrize("cpu,threads", [("banded", 1), ("banded", 3), ("queue", 1), ("queue", 4)])
+@pytest.mark.parametrize("cpu,threads", [("banded", 1), ("banded", 3), ("queue", 1), ("queue", 4), ("rows", 1),
+                                         ("rows", 4)])
 @pytest.mark.parametrize("seed,R,lights", [(1, 16, 1), (2, 60, 2), (3, 6, 0)])
 def test_avx2_baseline_matches_oracle(cpu, threads, seed, R, lights):
     kw = {} if lights == 1 else dict(lights=scenes.LIGHTS_TWO[:lights], ambient=scenes.AMBIENT_TWO)
@@ -41,7 +42,7 @@ def test_avx2_baseline_clipping_and_prior_contents():
     col = rng.integers(0, 2**32, (96, 128), dtype=np.uint32)
     z = rng.uniform(-2, 2, (96, 128)).astype(np.float32)
     a = O.render(s, color=col, z=z)
-    for cpu, th in (("banded", 2), ("queue", 3)):
+    for cpu, th in (("banded", 2), ("queue", 3), ("rows", 3)):
         assert same(a, O.render(s, color=col, z=z, threads=th, cpu=cpu))
 
 
@@ -49,3 +50,13 @@ def test_avx2_baseline_bilinear():
     s = scenes.random_soup(1500, 128, 128, radius=20, seed=11, textured=True)
     s.texture.filter = abi.PRK_FILTER_BILINEAR
     assert same(O.render(s), O.render(s, threads=2, cpu="banded"))
+
+
+@pytest.mark.parametrize("cpu", ["queue", "rows"])
+def test_avx2_baseline_whole_objects(cpu):
+    """Objects of several triangles (one AET per object, edges of different
+    triangles paired into spans): the rows schedule's per-row tasks hold
+    several pairs."""
+    s = scenes.random_soup(1200, 160, 128, radius=18, seed=21, textured=True)
+    ref = O.render(s, tris_per_object=6)
+    assert same(ref, O.render(s, tris_per_object=6, threads=3, cpu=cpu))
