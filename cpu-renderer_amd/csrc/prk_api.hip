@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -115,7 +116,8 @@ struct prk_context {
     // flush's stream.
     struct BinSet {
         DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_tri_n, d_tri_off, d_pair_tri, d_keys_a, d_vals_a, d_keys_b,
-            d_bins, d_offs, d_temp, d_won, d_list, d_nwin, d_wtag, d_recs, d_trwon, d_wlist, d_seltemp;
+            d_bins, d_offs, d_temp, d_won, d_list, d_nwin, d_wtag, d_recs, d_trwon, d_wlist, d_seltemp, d_trec,
+            d_nrec;
         // bytes last uploaded into d_draws / d_texs and the buffer they went
         // to: an unchanged table (every frame of a static scene) is not sent again
         std::vector<uint8_t> h_draws, h_texs;
@@ -132,6 +134,9 @@ struct prk_context {
     hipEvent_t s_mark = nullptr;  // flush-stream point the bin stream waits for (prior target contents)
     uint32_t *h_total = nullptr;  // pinned
     int32_t tile_w = 256, tile_h = 8;  // measured best for C3b
+    // all-AVX frames: per-triangle setup records; the AVX k_vis / k_walk read
+    // them (prk_kernels.hip PRK_SETUP_REC), so they are not optional
+    bool setup_rec = true;
     bool debug = false;
     bool winners_valid = false;
     prk_stats stats{};
@@ -214,7 +219,8 @@ int prk_destroy(prk_context *c) {
     for (auto &B : c->bset) {
         DevBuf *bb[] = {&B.d_draws, &B.d_texs, &B.d_tri_draw, &B.d_ranges, &B.d_tri_n, &B.d_tri_off, &B.d_pair_tri,
                         &B.d_keys_a, &B.d_vals_a, &B.d_keys_b, &B.d_bins, &B.d_offs, &B.d_temp, &B.d_won,
-                        &B.d_list, &B.d_nwin, &B.d_wtag, &B.d_recs, &B.d_trwon, &B.d_wlist, &B.d_seltemp};
+                        &B.d_list, &B.d_nwin, &B.d_wtag, &B.d_recs, &B.d_trwon, &B.d_wlist, &B.d_seltemp,
+                        &B.d_trec, &B.d_nrec};
         for (DevBuf *b : bb) b->release();
         if (B.free_ev) (void)hipEventDestroy(B.free_ev);
         if (B.binned_ev) (void)hipEventDestroy(B.binned_ev);
@@ -686,6 +692,14 @@ int prk_flush(prk_context *c, void *stream) {
     PRK_TRY(bset_ensure(B.d_tri_n, (size_t)(T + 1) * 4));
     PRK_TRY(bset_ensure(B.d_tri_off, (size_t)(T + 1) * 4));
     PRK_TRY(bset_ensure(B.d_offs, (size_t)(ntiles + 1) * 4));
+    fp.trec = nullptr;
+    fp.nrec = nullptr;
+    if (modeset == prk::MODE_AVX && c->setup_rec) {
+        PRK_TRY(bset_ensure(B.d_trec, (size_t)T * sizeof(prk::TriRec)));
+        PRK_TRY(bset_ensure(B.d_nrec, (size_t)T * sizeof(prk::NrmRec)));
+        fp.trec = (prk::TriRec *)B.d_trec.p;
+        fp.nrec = (prk::NrmRec *)B.d_nrec.p;
+    }
     size_t scan_bytes = 0;
     PRK_TRY(prk_bin_phase1(&fp, nullptr, nullptr, nullptr, nullptr, &scan_bytes, bs));
     PRK_TRY(bset_ensure(B.d_temp, scan_bytes));

@@ -115,7 +115,42 @@ __global__ void k_bin_count(FrameParams fp, uint32_t *__restrict__ tri_n, TileRa
         tr.tx0 = 1; tr.tx1 = 0; tr.ty0 = 1; tr.ty1 = 0; tr.oty0 = 1; tr.oty1 = 0;
     }
     ranges[g] = tr;
-    tri_n[g] = range_entries(tr);
+    const uint32_t ne = range_entries(tr);
+    tri_n[g] = ne;
+    if (fp.trec && ne) {
+        // All-AVX frame: FillEdgeTable + MergeSort + the first row's AET
+        // insertions once per triangle (TriRec / NrmRec, prk_device.h).
+        const DrawRec *d;
+        uint32_t gt;
+        resolve_draw(fp, g, d, gt);
+        Edge s0, s1, s2;
+        TriRaw<MODE_AVX> raw;
+        load_tri<MODE_AVX>(*d, gt, raw);
+        const int n = setup_from_raw<MODE_AVX>(raw, *d, fp, s0, s1, s2);
+        uint32_t anom = 0;
+        Walker<MODE_AVX, true> w;
+        w.init(n, s0, s1, s2, fp.H, fp.H, anom);
+        TriRec r;
+        NrmRec q;
+        rec_edge_out(s0, r.e[0], r.ymin[0], r.ymax[0]);
+        rec_edge_out(s1, r.e[1], r.ymin[1], r.ymax[1]);
+        rec_edge_out(s2, r.e[2], r.ymin[2], r.ymax[2]);
+        r.head = (uint32_t)n | (w.ord << 4) | ((uint32_t)w.cnt << 12) | ((uint32_t)(w.pend + 1) << 16) |
+                 (min(anom, 15u) << 20);
+        r.pad[0] = r.pad[1] = r.pad[2] = 0;
+        nrm_edge_out(s0, q.n[0]);
+        nrm_edge_out(s1, q.n[1]);
+        nrm_edge_out(s2, q.n[2]);
+        q.pad[0] = q.pad[1] = 0.0f;
+        float4 *dr = reinterpret_cast<float4 *>(fp.trec + g);
+        const float4 *sr = reinterpret_cast<const float4 *>(&r);
+#pragma unroll
+        for (int k = 0; k < 10; ++k) dr[k] = sr[k];
+        float4 *dq = reinterpret_cast<float4 *>(fp.nrec + g);
+        const float4 *sq = reinterpret_cast<const float4 *>(&q);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) dq[k] = sq[k];
+    }
 }
 
 // Sort key = tile << kRowClassBits | row class: within a tile's bin the

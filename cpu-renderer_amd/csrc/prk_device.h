@@ -43,6 +43,27 @@ struct TexRec {
     int32_t filter;      // PRK_FILTER_* (bilinear: AVX semantics only, an extension)
 };
 
+// Per-triangle setup record of an AVX-semantics frame, written once per
+// frame by the binning pass (k_bin_count) and read by every bin entry of the
+// triangle in k_vis and by k_walk: FillEdgeTable (projekt.cpp:3882-4121) +
+// MergeSort (2-72) + the AET insertions of the triangle's first row
+// (3654-3713), so no raster kernel repeats the ~30 divisions of the setup.
+// TriRec holds what the visibility sweep reads (160 B), NrmRec the normals
+// only the shading walk reads (80 B).
+struct TriRec {
+    float e[3][10];      // sorted edge k: X, G, Z, ZG, W, WG, U, UG, V, VG
+    int32_t ymin[3];     // YMin | Left << 31 (YMin >= 0: Maximum(0, .), 3999)
+    int32_t ymax[3];
+    uint32_t head;       // n | ord << 4 | cnt << 12 | (pend + 1) << 16 | anomaly << 20
+    uint32_t pad[3];
+};
+static_assert(sizeof(TriRec) == 160, "TriRec is ten dwordx4");
+struct NrmRec {
+    float n[3][6];       // sorted edge k: N0, N1, N2, NG0, NG1, NG2
+    float pad[2];
+};
+static_assert(sizeof(NrmRec) == 80, "NrmRec is five dwordx4");
+
 struct FrameParams {
     // projective_transform
     float D, F, M2P, Cx, Cy, InvM2P;
@@ -77,6 +98,10 @@ struct FrameParams {
     // kernel arguments, i.e. wave-uniform scalar registers.
     DrawRec draw0;
     TexRec tex0;
+    // Setup records (all-AVX frames; nullptr otherwise): written by
+    // k_bin_count for every binned triangle, read by k_vis / k_walk.
+    TriRec *trec;
+    NrmRec *nrec;
 };
 
 // d / FocalLength of UnprojectVertex(_8x) (projekt.cpp:141-142, 157).  When
@@ -462,6 +487,31 @@ __device__ __forceinline__ int setup_triangle(const DrawRec &d, uint32_t gt, con
     return setup_from_raw<M>(r, d, fp, s0, s1, s2);
 }
 
+// ---- setup records ---------------------------------------------------------
+__device__ __forceinline__ void rec_edge_out(const Edge &E, float *f, int32_t &ymin, int32_t &ymax) {
+    f[0] = E.X; f[1] = E.G; f[2] = E.Z; f[3] = E.ZG; f[4] = E.W;
+    f[5] = E.WG; f[6] = E.U; f[7] = E.UG; f[8] = E.V; f[9] = E.VG;
+    ymin = (int32_t)((uint32_t)E.YMin | ((uint32_t)(E.Left != 0) << 31));
+    ymax = E.YMax;
+}
+__device__ __forceinline__ void nrm_edge_out(const Edge &E, float *f) {
+    f[0] = E.N0; f[1] = E.N1; f[2] = E.N2; f[3] = E.NG0; f[4] = E.NG1; f[5] = E.NG2;
+}
+__device__ __forceinline__ Edge rec_edge_in(const float *f, int32_t ymin, int32_t ymax) {
+    Edge E;
+    E.X = f[0]; E.G = f[1]; E.Z = f[2]; E.ZG = f[3]; E.W = f[4];
+    E.WG = f[5]; E.U = f[6]; E.UG = f[7]; E.V = f[8]; E.VG = f[9];
+    E.N0 = E.N1 = E.N2 = E.NG0 = E.NG1 = E.NG2 = 0.0f;
+    E.C0 = E.C1 = E.C2 = E.C3 = E.CG0 = E.CG1 = E.CG2 = E.CG3 = 0.0f;
+    E.YMin = (int32_t)((uint32_t)ymin & 0x7FFFFFFFu);
+    E.Left = (int32_t)((uint32_t)ymin >> 31);
+    E.YMax = ymax;
+    return E;
+}
+__device__ __forceinline__ void nrm_edge_in(Edge &E, const float *f) {
+    E.N0 = f[0]; E.N1 = f[1]; E.N2 = f[2]; E.NG0 = f[3]; E.NG1 = f[4]; E.NG2 = f[5];
+}
+
 // AET edge step (projekt.cpp:3811-3829), only the fields mode M reads
 // (normals only when NRM: the visibility sweep never reads them).
 template <int M, bool NRM>
@@ -569,6 +619,22 @@ struct Walker {
         }
     }
 
+    // The same state from a setup record: the insertions of FirstRow were
+    // replayed once per triangle by the binning pass (head word of TriRec).
+    __device__ __forceinline__ void init_rec(int n, const EdgeT &s0, const EdgeT &s1, const EdgeT &s2, int32_t H,
+                                             int32_t row_end, uint32_t head) {
+        E0 = s0; E1 = s1; E2 = s2;
+        FirstRow = s0.YMin;
+        int32_t MaxRow = s0.YMax;
+        if (n > 1 && MaxRow < s1.YMax) MaxRow = s1.YMax;
+        if (n > 2 && MaxRow < s2.YMax) MaxRow = s2.YMax;
+        MaxY = min(min(MaxRow, H), row_end);
+        Row = FirstRow;
+        ord = (head >> 4) & 0xFFu;
+        cnt = (int)((head >> 12) & 0xFu);
+        pend = (int)((head >> 16) & 0xFu) - 1;
+    }
+
     // Insertion + expiry of this->Row; true when a pair is emitted: the left
     // edge is slot(0), the right edge slot(1).
     __device__ __forceinline__ bool begin_row() {
@@ -629,6 +695,10 @@ struct Walker {
         }
         const int32_t stop = ystart;
         if (Row >= stop) return 0;
+#if defined(PRK_DIAG) && (PRK_DIAG & 32)
+        Row = stop;  // diagnostic builds only: no replay (wrong output, timing ablation)
+        return 0;
+#endif
         if (n < 2 || E1.YMin != FirstRow || cnt < 2 || Row != FirstRow) return -1;
         const int32_t h0 = min(E0.YMax, stop), h1 = min(E1.YMax, stop);
         const int32_t i2 = n > 2 ? E2.YMin : stop, h2 = n > 2 ? min(E2.YMax, stop) : stop;

@@ -52,6 +52,9 @@
 #ifndef PRK_PIX_SPLIT
 #define PRK_PIX_SPLIT 1  // k_pix workgroups per tile
 #endif
+#ifndef PRK_SETUP_REC
+#define PRK_SETUP_REC 1  // all-AVX frames: k_vis / k_walk read the binning pass's setup records
+#endif
 #ifndef PRK_SHADE_MIN_WAVES
 #define PRK_SHADE_MIN_WAVES 3  // waves per SIMD k_shade is register-budgeted for
 #endif
@@ -689,7 +692,7 @@ __device__ __forceinline__ int wave_incl_max(int v) {  // v >= 0
 
 // One sweep over the tile's bin for mode M.  SHADE=false: visibility keys;
 // SHADE=true: shade the winners.
-template <int M, bool SHADE, bool UNI>
+template <int M, bool SHADE, bool UNI, bool REC = false>
 __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
                                       std::conditional_t<SHADE, ShadeSlots, VisSlots> &ws,
                                       const uint2 *__restrict__ bins, uint32_t b0, uint32_t n,
@@ -744,7 +747,23 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
             }
             Edge s0, s1, s2;
             int ne;
-            if constexpr (kPre) {
+            uint32_t rhead = 0;
+            if constexpr (REC) {
+                // Setup record of the binning pass: no per-entry FillEdgeTable.
+                const uint32_t g = bins[b0 + e].x;
+                const float4 *q = reinterpret_cast<const float4 *>(fp.trec + g);
+                float4 v[10];
+#pragma unroll
+                for (int k = 0; k < 10; ++k) v[k] = q[k];
+                const float *f = reinterpret_cast<const float *>(v);
+                const int32_t *iw = reinterpret_cast<const int32_t *>(v);
+                s0 = rec_edge_in(f + 0, iw[30], iw[33]);
+                s1 = rec_edge_in(f + 10, iw[31], iw[34]);
+                s2 = rec_edge_in(f + 20, iw[32], iw[35]);
+                rhead = (uint32_t)iw[36];
+                ne = (int)(rhead & 0xFu);
+                anom = (rhead >> 20) & 0xFu;
+            } else if constexpr (kPre) {
                 ne = setup_from_raw<M>(craw, fp.draw0, fp, s0, s1, s2);
                 texi = fp.draw0.tex;
             } else if constexpr (UNI) {  // one draw: its record is uniform (kernel arguments)
@@ -764,7 +783,8 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
             active = ne >= 2;
             if (active) {
                 Walker<M, SHADE> w0;
-                w0.init(ne, s0, s1, s2, fp.H, tc.y1, anom);
+                if constexpr (REC) w0.init_rec(ne, s0, s1, s2, fp.H, tc.y1, rhead);
+                else w0.init(ne, s0, s1, s2, fp.H, tc.y1, anom);
                 // Replay the rows above the tile (edge DDA only); row by row
                 // only for irregular edge lists.
                 const int fr = w0.fast_replay(ystart, ne);
@@ -919,7 +939,9 @@ __global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
     }
     __syncthreads();
     if constexpr (MODESET >= 0) {
-        sweep<(MODESET >= 0 ? MODESET : 0), false, UNI>(fp, tc, ws, bins, b0, n, nullptr, anomaly);
+        // all-AVX frames read the binning pass's setup records (TriRec)
+        sweep<(MODESET >= 0 ? MODESET : 0), false, UNI, MODESET == MODE_AVX && PRK_SETUP_REC>(
+            fp, tc, ws, bins, b0, n, nullptr, anomaly);
     } else {
         sweep<MODE_AVX, false, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly);
         sweep<MODE_SC_GOURAUD, false, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly);
@@ -1145,7 +1167,35 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
     if (active) {
         Edge s0, s1, s2;
         int ne;
-        if constexpr (UNI) {
+        uint32_t rhead = 0;
+        if constexpr (PRK_SETUP_REC) {  // the binning pass's setup records (TriRec + NrmRec)
+            const float4 *q = reinterpret_cast<const float4 *>(fp.trec + g);
+            const float4 *qn = reinterpret_cast<const float4 *>(fp.nrec + g);
+            float4 v[10], vn[5];
+#pragma unroll
+            for (int k = 0; k < 10; ++k) v[k] = q[k];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) vn[k] = qn[k];
+            const float *f = reinterpret_cast<const float *>(v);
+            const int32_t *iw = reinterpret_cast<const int32_t *>(v);
+            const float *fn = reinterpret_cast<const float *>(vn);
+            s0 = rec_edge_in(f + 0, iw[30], iw[33]);
+            s1 = rec_edge_in(f + 10, iw[31], iw[34]);
+            s2 = rec_edge_in(f + 20, iw[32], iw[35]);
+            nrm_edge_in(s0, fn + 0);
+            nrm_edge_in(s1, fn + 6);
+            nrm_edge_in(s2, fn + 12);
+            rhead = (uint32_t)iw[36];
+            ne = (int)(rhead & 0xFu);
+            if constexpr (UNI) {
+                texi = fp.draw0.tex;
+            } else {
+                const DrawRec *d;
+                uint32_t gt;
+                resolve_draw(fp, g, d, gt);
+                texi = d->tex;
+            }
+        } else if constexpr (UNI) {
             ne = setup_triangle<M>(fp.draw0, fp.draw0.geom_tri0 + (g - fp.draw0.first_global), fp, s0, s1, s2);
             texi = fp.draw0.tex;
         } else {
@@ -1159,7 +1209,8 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
         if (active) {
             uint32_t anom = 0;
             Walker<M, true> w0;
-            w0.init(ne, s0, s1, s2, fp.H, fp.row1, anom);
+            if constexpr (PRK_SETUP_REC) w0.init_rec(ne, s0, s1, s2, fp.H, fp.row1, rhead);
+            else w0.init(ne, s0, s1, s2, fp.H, fp.row1, anom);
             const int fr = w0.fast_replay(fp.row0, ne);  // band above row0 (row bands only)
             wk.from(w0);
             if (fr < 0)
