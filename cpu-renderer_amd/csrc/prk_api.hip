@@ -449,11 +449,14 @@ int prk_draw(prk_context *c, int32_t geometry, uint32_t first_tri, uint32_t tri_
     if (texture >= (int32_t)c->texs.size()) return PRK_ERR_ARG;
     const bool tex = texture >= 0;
     int mode;
-    if (semantics == PRK_SEM_AVX) {
+    uint32_t flags = 0;
+    if (semantics == PRK_SEM_AVX || semantics == PRK_SEM_AVX_ST) {
         // FillLineOptimized dereferences Bitmap at entry (projekt.cpp:1506) and
         // its non-Phong branch stores garbage (2285-2316): undefined -> rejected.
+        // The single-thread overload (2350-3358) shares both (2494, 3262-3290).
         if (!tex || !phong) return PRK_ERR_UNSUPPORTED;
         mode = prk::MODE_AVX;
+        if (semantics == PRK_SEM_AVX_ST) flags = prk::DRAW_ST;
     } else if (semantics == PRK_SEM_SCALAR) {
         mode = phong ? (tex ? prk::MODE_SC_PHONG_TEX : prk::MODE_SC_PHONG)
                      : (tex ? prk::MODE_SC_GOURAUD_TEX : prk::MODE_SC_GOURAUD);
@@ -478,6 +481,7 @@ int prk_draw(prk_context *c, int32_t geometry, uint32_t first_tri, uint32_t tri_
     d.P[0] = P ? P[0] : 0.0f;
     d.P[1] = P ? P[1] : 0.0f;
     d.P[2] = P ? P[2] : 0.0f;
+    d.flags = flags;
     c->draws.push_back(d);
     c->pending_tris += tri_count;
     return PRK_OK;
@@ -713,6 +717,7 @@ int prk_flush(prk_context *c, void *stream) {
     PRK_TRY(hipStreamSynchronize(bs));
     const uint32_t total = *c->h_total;
     c->stats.bin_entries = total;
+    if (total >= prk::kMaxPairs) return PRK_ERR_UNSUPPORTED;  // visibility tags hold a 31-bit pair index
     const size_t ne = (size_t)std::max<uint32_t>(total, 1);
     PRK_TRY(bset_ensure(B.d_pair_tri, ne * 4));
     PRK_TRY(bset_ensure(B.d_bins, ne * 8));  // (triangle, pair) per bin slot

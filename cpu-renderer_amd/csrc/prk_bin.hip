@@ -136,7 +136,7 @@ __global__ void k_bin_count(FrameParams fp, uint32_t *__restrict__ tri_n, TileRa
         rec_edge_out(s1, r.e[1], r.ymin[1], r.ymax[1]);
         rec_edge_out(s2, r.e[2], r.ymin[2], r.ymax[2]);
         r.head = (uint32_t)n | (w.ord << 4) | ((uint32_t)w.cnt << 12) | ((uint32_t)(w.pend + 1) << 16) |
-                 (min(anom, 15u) << 20);
+                 (min(anom, 15u) << 20) | ((d->flags & DRAW_ST) ? (1u << 24) : 0u);
         r.pad[0] = r.pad[1] = r.pad[2] = 0;
         nrm_edge_out(s0, q.n[0]);
         nrm_edge_out(s1, q.n[1]);

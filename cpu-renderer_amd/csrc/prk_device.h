@@ -35,7 +35,33 @@ struct DrawRec {
     int32_t mode;                 // Mode
     int32_t tex;                  // texture index or -1
     float P[3];                   // object offset (render_entry_3d_object::P)
+    uint32_t flags;               // DRAW_ST: single-thread DrawModelOptimized(Buffer,...) quirks
 };
+
+// Draw flags.  DRAW_ST: the single-thread overload DrawModelOptimized(Buffer,
+// ...) (projekt.cpp:2350-3358), whose span body differs from FillLineOptimized
+// in exactly two places: a left-clipped span sets XOffset = -XOffset (= -0.0f,
+// 2508) instead of -L.X, and the z-test is predicate 29, GE_OQ (3205):
+// z >= zbuf, so among equal z the LATEST fragment wins (and it beats an equal
+// prior z).
+enum : uint32_t { DRAW_ST = 1u };
+
+// Visibility key low words.  Keys are max-reduced: a
+// fragment's key is (ordered z << 32) | tag.  Queue-semantics pairs (strict
+// '>', earliest wins on equal z) take 0x7FFFFFFE - j, the prior z-buffer
+// 0x7FFFFFFF, single-thread pairs (>=, latest wins and beats the prior)
+// 0x80000000 + j, where j is the pair's submission-order index: this ordering
+// reproduces any interleaving of the two tie rules in one frame.
+constexpr uint32_t kTagPrior = 0x7FFFFFFFu;
+constexpr uint32_t kMaxPairs = 0x7FFFFFFFu;  // j < kMaxPairs
+__device__ __forceinline__ uint32_t pair_tag(uint32_t j, bool ge) { return ge ? 0x80000000u + j : 0x7FFFFFFEu - j; }
+// The winning pair of a key low word; false for the prior z (0x7FFFFFFF) and
+// for a NaN prior z, whose key is all ones and blocks the pixel.
+__device__ __forceinline__ bool tag_pair(uint32_t low, uint32_t &j) {
+    if (low == kTagPrior || low == 0xFFFFFFFFu) return false;
+    j = low < kTagPrior ? 0x7FFFFFFEu - low : low - 0x80000000u;
+    return true;
+}
 
 struct TexRec {
     const uint8_t *mem;  // (h+1) rows, last one the zeroed guard row
@@ -54,7 +80,7 @@ struct TriRec {
     float e[3][10];      // sorted edge k: X, G, Z, ZG, W, WG, U, UG, V, VG
     int32_t ymin[3];     // YMin | Left << 31 (YMin >= 0: Maximum(0, .), 3999)
     int32_t ymax[3];
-    uint32_t head;       // n | ord << 4 | cnt << 12 | (pend + 1) << 16 | anomaly << 20
+    uint32_t head;       // n | ord << 4 | cnt << 12 | (pend + 1) << 16 | anomaly << 20 | st << 24
     uint32_t pad[3];
 };
 static_assert(sizeof(TriRec) == 160, "TriRec is ten dwordx4");

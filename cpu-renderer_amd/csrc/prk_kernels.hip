@@ -9,7 +9,7 @@
 //                reference's exact span arithmetic (FillLineOptimized
 //                1492-2320 or DrawModel 298-538).
 //                Sweep 1 resolves visibility with 64-bit LDS atomicMax on
-//                key = (ordered z << 32) | (0xFFFFFFFE - bin entry): the
+//                key = (ordered z << 32) | tag(pair) (prk_device.h pair_tag): the
 //                reference's strict z '>' in submission order keeps exactly
 //                the EARLIEST fragment of maximal z, which is that max (bin
 //                entries are in submission order).  The triangles that won a
@@ -167,12 +167,12 @@ __device__ __forceinline__ void put_winner(const FrameParams &fp, int32_t x, int
 template <bool SHADE, class WS>
 __device__ __forceinline__ int span_setup_avx(const FrameParams &fp, const TileCtx &tc, WS &ws, int lane,
                                               uint32_t tag, int32_t texi, const Edge &L, const Edge &R,
-                                              int32_t Row) {
+                                              int32_t Row, bool st) {
     if (Row < tc.y0) return 0;
     const int32_t W = fp.W;
     float XOffset = 0.0f;
     float LeftX = L.X;  // 1545-1565
-    if (LeftX < 0) { XOffset = -L.X; LeftX = 0; }
+    if (LeftX < 0) { XOffset = st ? -XOffset : -L.X; LeftX = 0; }  // single-thread: -XOffset (2508)
     else if (LeftX >= W) LeftX = (float)W - 1;
     float RightX = R.X;
     if (RightX < 0) RightX = 0;
@@ -724,6 +724,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
         const uint32_t i = base + lane;
         bool active = i < n;
         uint32_t e = 0, j = 0;  // bin entry, its pair index (the tie-break order)
+        uint32_t st = 0;        // DRAW_ST: single-thread DrawModelOptimized(Buffer,...) semantics
         int32_t texi = 0;
         RowWalker<M, SHADE> wk;
         uint32_t anom = 0;
@@ -763,14 +764,17 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
                 rhead = (uint32_t)iw[36];
                 ne = (int)(rhead & 0xFu);
                 anom = (rhead >> 20) & 0xFu;
+                st = (rhead >> 24) & 1u;
             } else if constexpr (kPre) {
                 ne = setup_from_raw<M>(craw, fp.draw0, fp, s0, s1, s2);
                 texi = fp.draw0.tex;
+                st = fp.draw0.flags & DRAW_ST;
             } else if constexpr (UNI) {  // one draw: its record is uniform (kernel arguments)
                 const uint32_t g = bins[b0 + e].x;
                 const uint32_t gt = fp.draw0.geom_tri0 + (g - fp.draw0.first_global);
                 ne = setup_triangle<M>(fp.draw0, gt, fp, s0, s1, s2);
                 texi = fp.draw0.tex;
+                st = fp.draw0.flags & DRAW_ST;
             } else {
                 const uint32_t g = bins[b0 + e].x;
                 const DrawRec *d;
@@ -779,6 +783,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
                 // (mixed frames sweep the bin once per mode)
                 ne = d->mode == M ? setup_triangle<M>(*d, gt, fp, s0, s1, s2) : 0;
                 texi = d->tex;
+                st = d->flags & DRAW_ST;
             }
             active = ne >= 2;
             if (active) {
@@ -803,7 +808,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
         // Visibility tag: the pair index orders fragments of equal z exactly as
         // submission order does (pairs are numbered in triangle order, one per
         // triangle and tile), whatever order the bin lists them in.
-        const uint32_t tag = 0xFFFFFFFEu - j;
+        const uint32_t tag = pair_tag(j, st != 0);
         if (PRK_DIAG & 4) active = false;
         if (PRK_PROF) { const unsigned long long t1 = PRK_T(); pt[0] += t1 - t0; t0 = t1; }
         // PRK_LANE_ROWS: every lane walks its own next row each iteration (the
@@ -816,7 +821,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
                 const bool paired = wk.begin_row();
                 if (paired) {
                     const Edge &L = wk.S0, &R = wk.S1;
-                    if (M == MODE_AVX) items = span_setup_avx<SHADE>(fp, tc, ws, lane, tag, texi, L, R, row);
+                    if (M == MODE_AVX) items = span_setup_avx<SHADE>(fp, tc, ws, lane, tag, texi, L, R, row, st != 0);
                     else items = span_setup_scalar<M, SHADE>(fp, tc, ws, lane, tag, texi, L, R, row);
                     ws.i[SI_ROW][lane] = row;
                 }
@@ -933,7 +938,7 @@ __global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
         unsigned long long k = ~0ull;
         if (x < tc.x1 && y < tc.y1) {
             const float z = fp.clear_fused ? fp.clear_z : fp.zbuf[(size_t)(y - fp.row0) * fp.W + x];
-            k = (z != z) ? ~0ull : (((unsigned long long)zkey(z) << 32) | 0xFFFFFFFFull);
+            k = (z != z) ? ~0ull : (((unsigned long long)zkey(z) << 32) | kTagPrior);
         }
         tc.key[p] = k;
     }
@@ -956,8 +961,8 @@ __global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
     for (int p = threadIdx.x; p < npx; p += blockDim.x) {
         const uint32_t low = (uint32_t)tc.key[p];
         tags_out[p] = low;
-        if (low == 0xFFFFFFFFu) continue;
-        const uint32_t j = 0xFFFFFFFEu - low;  // the winning pair
+        uint32_t j;  // the winning pair
+        if (!tag_pair(low, j)) continue;
         if constexpr (kRec) {  // the winner's (pair, row) and triangle (benign same-value races)
             anyw = 1;
             won[(size_t)j * fp.tile_h + (p >> fp.tile_w_log2)] = 1;
@@ -971,9 +976,9 @@ __global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
         for (int p = threadIdx.x; p < npx; p += blockDim.x) {
             const int x = tc.x0 + (p & (fp.tile_w - 1)), y = tc.y0 + (p >> fp.tile_w_log2);
             if (x >= tc.x1 || y >= tc.y1) continue;
-            const uint32_t low = (uint32_t)tc.key[p];
+            uint32_t j;
             fp.winners[(size_t)(y - fp.row0) * fp.W + x] =
-                low != 0xFFFFFFFFu ? (int32_t)pair_tri[0xFFFFFFFEu - low] : -1;
+                tag_pair((uint32_t)tc.key[p], j) ? (int32_t)pair_tri[j] : -1;
         }
     }
     if constexpr (kRec) {
@@ -1056,12 +1061,12 @@ static_assert(sizeof(SpanRec) == 64, "span record is four dwordx4");
 // in k_vis, write the span's record at recs[pair * tile_h + row-in-tile].
 __device__ __forceinline__ void walk_record(const FrameParams &fp, const Edge &L, const Edge &R, int32_t Row,
                                             int32_t texi, const TileRange &tr, uint32_t jb, int ntx,
-                                            const uint8_t *__restrict__ won, SpanRec *__restrict__ recs) {
+                                            const uint8_t *__restrict__ won, SpanRec *__restrict__ recs, bool st) {
     if (Row < fp.row0) return;
     const int32_t W = fp.W;
     float XOffset = 0.0f;
     float LeftX = L.X;  // 1545-1565
-    if (LeftX < 0) { XOffset = -L.X; LeftX = 0; }
+    if (LeftX < 0) { XOffset = st ? -XOffset : -L.X; LeftX = 0; }  // single-thread: -XOffset (2508)
     else if (LeftX >= W) LeftX = (float)W - 1;
     float RightX = R.X;
     if (RightX < 0) RightX = 0;
@@ -1129,7 +1134,8 @@ __device__ __forceinline__ void walk_flush(const FrameParams &fp, const WalkQueu
     TileRange tr;
     tr.tx0 = (uint16_t)(t0 & 0xFFFF); tr.ty0 = (uint16_t)(t0 >> 16);
     tr.tx1 = (uint16_t)(t1 & 0xFFFF); tr.ty1 = (uint16_t)(t1 >> 16);
-    walk_record(fp, L, R, rt & 0xFFFF, rt >> 16, tr, jb, (int)tr.tx1 - (int)tr.tx0 + 1, won, recs);
+    walk_record(fp, L, R, rt & 0xFFFF, (rt >> 16) & 0x7FFF, tr, jb, (int)tr.tx1 - (int)tr.tx0 + 1, won, recs,
+                (rt >> 31) != 0);
 }
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -1159,6 +1165,7 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
     const uint32_t g = active ? wlist[i] : 0u;  // the triangles that won a pixel (compacted)
     RowWalker<M, true> wk;
     int32_t texi = 0;
+    uint32_t st = 0;  // DRAW_ST
     TileRange tr{};
     uint32_t jb = 0;
     uint64_t rows = ~0ull;
@@ -1187,6 +1194,7 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
             nrm_edge_in(s2, fn + 12);
             rhead = (uint32_t)iw[36];
             ne = (int)(rhead & 0xFu);
+            st = (rhead >> 24) & 1u;
             if constexpr (UNI) {
                 texi = fp.draw0.tex;
             } else {
@@ -1198,12 +1206,14 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
         } else if constexpr (UNI) {
             ne = setup_triangle<M>(fp.draw0, fp.draw0.geom_tri0 + (g - fp.draw0.first_global), fp, s0, s1, s2);
             texi = fp.draw0.tex;
+            st = fp.draw0.flags & DRAW_ST;
         } else {
             const DrawRec *d;
             uint32_t gt;
             resolve_draw(fp, g, d, gt);
             ne = setup_triangle<M>(*d, gt, fp, s0, s1, s2);
             texi = d->tex;
+            st = d->flags & DRAW_ST;
         }
         active = ne >= 2;
         if (active) {
@@ -1261,7 +1271,7 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
             q.f[5][slot] = L.N0; q.f[6][slot] = L.N1; q.f[7][slot] = L.N2;
             q.f[8][slot] = R.X; q.f[9][slot] = R.W; q.f[10][slot] = R.U; q.f[11][slot] = R.V; q.f[12][slot] = R.Z;
             q.f[13][slot] = R.N0; q.f[14][slot] = R.N1; q.f[15][slot] = R.N2;
-            q.i[0][slot] = (Row & 0xFFFF) | (texi << 16);
+            q.i[0][slot] = (int32_t)((uint32_t)(Row & 0xFFFF) | ((uint32_t)texi << 16) | (st << 31));
             q.i[1][slot] = (int32_t)jb;
             q.i[2][slot] = t0;
             q.i[3][slot] = t1;
@@ -1298,14 +1308,14 @@ __global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__r
     const uint32_t *tags = wtag + (size_t)t * npx;
     const int pend = (int)(((long long)npx * (part + 1)) / PRK_PIX_SPLIT);
     for (int p = (int)(((long long)npx * part) / PRK_PIX_SPLIT) + threadIdx.x; p < pend; p += blockDim.x) {
-        const uint32_t tag = any ? tags[p] : 0xFFFFFFFFu;
+        const uint32_t tag = any ? tags[p] : kTagPrior;
         const int ly = p >> fp.tile_w_log2;
         const int32_t x = tc.x0 + (p & (fp.tile_w - 1)), Row = tc.y0 + ly;
-        if (tag == 0xFFFFFFFFu) {  // no fragment beat the prior z
+        uint32_t j;  // the winning pair
+        if (!tag_pair(tag, j)) {  // no fragment beat the prior z
             if (fp.clear_fused && x < tc.x1 && Row < tc.y1) put_winner(fp, x, Row, fp.clear_z, fp.clear_color);
             continue;
         }
-        const uint32_t j = 0xFFFFFFFEu - tag;  // the winning pair
         const float4 *q = reinterpret_cast<const float4 *>(recs + (size_t)j * fp.tile_h + ly);
         const float4 r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];
         const int32_t lt = __float_as_int(r0.x);

@@ -20,7 +20,8 @@ import os
 import numpy as np
 
 from . import abi
-from .abi import PRK_SEM_AVX, PRK_SEM_SCALAR  # noqa: F401
+from . import scenes as scenes_mod
+from .abi import PRK_SEM_AVX, PRK_SEM_AVX_ST, PRK_SEM_SCALAR  # noqa: F401
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PRK_LIB") or os.path.join(os.path.dirname(_HERE), "libprk_hip.so")
@@ -240,6 +241,16 @@ class Renderer:
         """DrawModel (projekt.cpp:162-601) scalar semantics."""
         self._draw(geom, first_tri, tri_count, P, abi.PRK_SEM_SCALAR, phong, bitmap)
 
+    def draw_model_optimized_st(self, geom, tri_count, first_tri=0, P=None, bitmap=None, phong=True):
+        """The single-thread overload DrawModelOptimized(Buffer, ...)
+        (projekt.cpp:2350-3358): FillLineOptimized's math with its left-clip
+        XOffset quirk (2508) and the >= z-test (3205).  Needs bitmap + phong."""
+        self._draw(geom, first_tri, tri_count, P, abi.PRK_SEM_AVX_ST, phong, bitmap)
+
+    def draw(self, semantics, geom, tri_count, first_tri=0, P=None, bitmap=None, phong=True):
+        """Any PRK_SEM_* draw."""
+        self._draw(geom, first_tri, tri_count, P, semantics, phong, bitmap)
+
     def complete_all_work(self, stream=None):
         """Platform.CompleteAllWork: run every recorded draw (asynchronous)."""
         _check("prk_flush", self._L.prk_flush(self._h, None if stream is None else C.c_void_p(stream)))
@@ -289,16 +300,14 @@ def render_scene(scene, semantics=abi.PRK_SEM_AVX, phong=True, device=0, tile=No
         g = r.geometry(scene.vertices, scene.colors, scene.normals, scene.uvs)
         draws = scene.draws if scene.draws is not None else [(0, scene.tri_count, scene.texture)]
         handles = {}
-        for first, count, texture in draws:
+        for d in draws:
+            first, count, texture, sem = scenes_mod.draw_spec(d, semantics)
             tex = None
             if texture is not None:
                 if id(texture) not in handles:
                     handles[id(texture)] = r.texture(texture)
                 tex = handles[id(texture)]
-            if semantics == abi.PRK_SEM_AVX:
-                r.draw_model_optimized(g, count, first_tri=first, P=scene.P, bitmap=tex, phong=phong)
-            else:
-                r.draw_model(g, count, first_tri=first, P=scene.P, bitmap=tex, phong=phong)
+            r.draw(sem, g, count, first_tri=first, P=scene.P, bitmap=tex, phong=phong)
         r.complete_all_work()
         r.synchronize()
         col, zb = r.download()

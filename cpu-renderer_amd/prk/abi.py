@@ -18,6 +18,7 @@ PRK_ERR_NO_TARGET = -5
 
 PRK_SEM_SCALAR = 0  # DrawModel            projekt.cpp:162-601
 PRK_SEM_AVX = 1     # FillLineOptimized    projekt.cpp:1492-2320
+PRK_SEM_AVX_ST = 2  # DrawModelOptimized(Buffer,...) single-thread overload, projekt.cpp:2350-3358
 
 PRK_FILTER_NEAREST = 0   # the reference's sampling (projekt.cpp:1881-2032)
 PRK_FILTER_BILINEAR = 1  # extension (AVX semantics)

@@ -52,9 +52,10 @@ class Scene:
     P: tuple = (0.0, 0.0, 0.0)
     name: str = "scene"
     meta: dict = field(default_factory=dict)
-    # Multi-draw scenes: [(first_tri, tri_count, Texture or None), ...] drawn
-    # in order into one frame (one DrawModel* call each); None = one draw of
-    # every triangle with `texture`.
+    # Multi-draw scenes: [(first_tri, tri_count, Texture or None[, semantics]),
+    # ...] drawn in order into one frame (one DrawModel* call each; semantics
+    # PRK_SEM_* overrides the frame's); None = one draw of every triangle with
+    # `texture`.
     draws: Optional[list] = None
 
     @property
@@ -392,3 +393,36 @@ def sponza_like(width=3840, height=2160, seed=0, detail=1.56, tex_size=1024, fil
     return Scene(width, height, V, C, N, UV, cam, lights, (0.25, 0.25, 0.25, 1.0), None,
                  name="sponza_like%d_%dx%d" % (V.shape[0] // 3, width, height),
                  meta=dict(kind="sponza_like", seed=seed), draws=draws)
+
+
+def draw_spec(d, semantics):
+    """(first, count, texture, semantics) of a Scene.draws entry."""
+    return (d[0], d[1], d[2], d[3] if len(d) > 3 and d[3] is not None else semantics)
+
+
+def with_ties(scene, frac=0.5, seed=0):
+    """The scene plus exact positional duplicates of a random `frac` of its
+    triangles (new normals, uvs and colours, so the tie's two fragments shade
+    differently), each inserted at a random later position: equal-z
+    fragments decide the z-test's tie rule (projekt.cpp:2219 strict '>' vs
+    3205 '>=')."""
+    rng = np.random.default_rng(seed)
+    T = scene.tri_count
+    pick = np.sort(rng.choice(T, int(T * frac), replace=False))
+    order = list(range(T))
+    for k in pick[::-1]:
+        order.insert(int(rng.integers(k + 1, len(order) + 1)), T + int(np.searchsorted(pick, k)))
+    V = scene.vertices.reshape(T, 3, 3)
+    Vd = np.concatenate([V, V[pick]])
+    def fresh(a, lo, hi):
+        a = a.reshape(T, 3, -1)
+        b = rng.uniform(lo, hi, a[pick].shape).astype(np.float32)
+        return np.concatenate([a, b])
+    N = fresh(scene.normals, -1.0, 1.0)
+    N /= np.linalg.norm(N, axis=-1, keepdims=True)
+    UV = fresh(scene.uvs, 0.0, 1.0)
+    C = fresh(scene.colors, 0.0, 1.0)
+    o = np.array(order)
+    return Scene(scene.width, scene.height, Vd[o].reshape(-1, 3).copy(), C[o].reshape(-1, 4).copy(),
+                 N[o].reshape(-1, 3).astype(np.float32).copy(), UV[o].reshape(-1, 2).copy(), scene.transform,
+                 scene.lights, scene.ambient, scene.texture, scene.P, scene.name + "+ties", dict(scene.meta))

@@ -47,8 +47,15 @@ enum prk_status {
 /* Which of the reference's span kernels a draw reproduces. */
 enum prk_semantics {
     PRK_SEM_SCALAR = 0,  /* DrawModel            projekt.cpp:162-601   */
-    PRK_SEM_AVX = 1      /* FillLineOptimized    projekt.cpp:1492-2320, driven by
-                            DrawModelOptimized(RenderQueue,...) 3615-3871 */
+    PRK_SEM_AVX = 1,     /* FillLineOptimized    projekt.cpp:1492-2320, driven by
+                            DrawModelOptimized(RenderQueue,...) 3615-3871, or by
+                            DrawModelOptimizedLines 3362-3613 (FillLinesOptimized
+                            629-1490 has the same block math) */
+    PRK_SEM_AVX_ST = 2   /* the single-thread overload DrawModelOptimized(Buffer,...)
+                            2350-3358: FillLineOptimized's math with two quirks:
+                            a left-clipped span keeps XOffset = -0.0f (2508) and the
+                            z-test is z >= zbuf (predicate 29, 3205): among equal z
+                            the latest fragment wins */
 };
 
 /* Texture sampling of a texture handle (prk_texture_set_filter).  The

@@ -113,11 +113,13 @@ def render(scene, semantics=abi.PRK_SEM_AVX, phong=True, tris_per_object=1, thre
     zb = np.full((H, W), CLEAR_Z, np.float32) if z is None else np.array(z, np.float32)
     win = np.full((H, W), -1, np.int32) if winners else None
     if scene.draws is not None:  # multi-draw scene: the draws in order, one target
+        from prk.scenes import draw_spec
         tot = [0, 0, 0]
-        for first, count, texture in scene.draws:
+        for d in scene.draws:
+            first, count, texture, sem = draw_spec(d, semantics)
             sub = scene.subset(first, first + count)
             sub.texture, sub.draws = texture, None
-            _, _, _, st = _render_one(sub, semantics, phong, tris_per_object, threads, col, zb, win, rows,
+            _, _, _, st = _render_one(sub, sem, phong, tris_per_object, threads, col, zb, win, rows,
                                       tri_base=first, cpu=cpu)
             tot = [tot[0] + st["spans"], tot[1] + st["span_pixels"], tot[2] + st["writes"]]
         return col, zb, win, dict(spans=tot[0], span_pixels=tot[1], writes=tot[2])

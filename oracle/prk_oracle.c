@@ -133,6 +133,7 @@ typedef struct or_ctx {
     int32_t BandH, BandMod, BandRem; /* interleaved bands: draw row r iff (r/BandH)%BandMod==BandRem */
     int Phong;
     int Filter;                /* PRK_FILTER_*: texture sampling of the AVX span */
+    int St;                    /* the single-thread overload DrawModelOptimized(Buffer,...) */
     uint64_t Spans, SpanPixels, Writes;
 } or_ctx;
 
@@ -367,6 +368,11 @@ static void or_bilinear(const prk_bitmap *B, float FU, float FV, float *CA, floa
 /* ------------------------------------------------------------------ */
 /* FillLineOptimized (projekt.cpp:1492-2320), one lane at a time.      */
 /* The non-Phong branch (2285-2316) is out of scope (prk rejects it).  */
+/* X_->St: the span body of the single-thread overload                */
+/* DrawModelOptimized(Buffer,...) (2350-3358), identical but for the   */
+/* left-clip XOffset = -XOffset (2508, i.e. -0.0f) and the GE_OQ z-test */
+/* (predicate 29, 3205); its unlocked aligned stores (3235-3236) store  */
+/* the same values.                                                     */
 /* ------------------------------------------------------------------ */
 static void or_fill_line_optimized(or_ctx *X_, const or_edge *L, const or_edge *R, int32_t Row)
 {
@@ -378,7 +384,7 @@ static void or_fill_line_optimized(or_ctx *X_, const or_edge *L, const or_edge *
     if (Row < 0) return;
 
     float LeftX = L->XMin; /* 1545-1565 */
-    if (LeftX < 0) { XOffset = -L->XMin; LeftX = 0; }
+    if (LeftX < 0) { XOffset = X_->St ? -XOffset /* 2508 */ : -L->XMin; LeftX = 0; }
     else if (LeftX >= W) LeftX = (float)W - 1;
     float RightX = R->XMin;
     if (RightX < 0) RightX = 0;
@@ -499,8 +505,9 @@ static void or_fill_line_optimized(or_ctx *X_, const or_edge *L, const or_edge *
                               ((uint32_t)or_cvt_rne_s32(Fg * 255.0f) << 8) |
                               ((uint32_t)or_cvt_rne_s32(Fb * 255.0f) << 0) |
                               ((uint32_t)or_cvt_rne_s32(Fa * 255.0f) << 24);
-            /* z-test, predicate 30 = GT_OQ (2217-2233). */
-            if (Zl[i] > zb) {
+            /* z-test, predicate 30 = GT_OQ (2217-2233); single-thread
+             * overload: predicate 29 = GE_OQ (3205). */
+            if (X_->St ? (Zl[i] >= zb) : (Zl[i] > zb)) {
                 size_t px = (size_t)Row * W + X + i;
                 X_->Z[px] = Zl[i];
                 uint32_t *row = (uint32_t *)((uint8_t *)X_->Color + (size_t)Row * X_->Pitch);
@@ -826,8 +833,9 @@ static int or_draw_filtered(const or_draw_desc *D, const or_target *Tg, const pr
                             int32_t band_h, int32_t band_mod, int32_t band_rem, uint64_t *stats)
 {
     if (!D || !Tg || !T || !Lights) return PRK_ERR_ARG;
-    if (D->Semantics == PRK_SEM_AVX && (!D->Bitmap || !D->Phong)) return PRK_ERR_UNSUPPORTED;
-    if (D->Semantics == PRK_SEM_AVX && (Tg->Width % 8)) return PRK_ERR_UNSUPPORTED;
+    const int avx = D->Semantics == PRK_SEM_AVX || D->Semantics == PRK_SEM_AVX_ST;
+    if (avx && (!D->Bitmap || !D->Phong)) return PRK_ERR_UNSUPPORTED;
+    if (avx && (Tg->Width % 8)) return PRK_ERR_UNSUPPORTED;
     if (Lights->LightCount > PRK_MAX_LIGHTS) return PRK_ERR_ARG;
     uint32_t per = D->TrisPerObject ? D->TrisPerObject : 1;
     or_edge *Edges = (or_edge *)malloc(sizeof(or_edge) * 3 * per);
@@ -840,9 +848,11 @@ static int or_draw_filtered(const or_draw_desc *D, const or_target *Tg, const pr
     X_.Width = Tg->Width; X_.Height = Tg->Height; X_.Winners = Tg->Winners;
     X_.RowLo = row_lo; X_.RowHi = row_hi; X_.Phong = D->Phong; X_.Filter = D->Filter;
     X_.BandH = band_h; X_.BandMod = band_mod; X_.BandRem = band_rem;
+    X_.St = D->Semantics == PRK_SEM_AVX_ST;
     /* OR_AVX_SPAN: the AVX2 CPU baseline (prk_cpu_avx.c) substitutes its
      * 8-wide span here; this file alone always uses the scalar restatement. */
-    or_span_fn Span = D->Semantics == PRK_SEM_AVX ? OR_AVX_SPAN : or_fill_line_scalar;
+    or_span_fn Span = D->Semantics == PRK_SEM_AVX ? OR_AVX_SPAN
+                      : (D->Semantics == PRK_SEM_AVX_ST ? or_fill_line_optimized : or_fill_line_scalar);
     for (uint32_t t0 = 0; t0 < D->TriCount; t0 += per) {
         uint32_t n = D->TriCount - t0 < per ? D->TriCount - t0 : per;
         if (band_mod > 1 || row_lo > 0 || row_hi < Tg->Height) {

@@ -118,7 +118,8 @@ class Ctx:
         self.D, self.F, self.M2P, self.cx, self.cy = D, F, M2P, cx, cy
         self.lights = [([f32(c) for c in p], [f32(c) for c in i]) for p, i in scene.lights]
         self.amb = [f32(c) for c in scene.ambient]
-        self.avx = semantics == 1
+        self.avx = semantics in (1, 2)
+        self.st = semantics == 2  # DrawModelOptimized(Buffer,...) projekt.cpp:2350-3358
         self.phong = phong
         self.tex = scene.texture
         self.color = np.full((self.H, self.W), 0xFF000000, np.uint32) if color is None else color
@@ -299,7 +300,7 @@ def span_avx(ctx, t, L, R, row):
     xoff = f32(0)
     lx = L["X"]
     if lx < 0:
-        xoff, lx = -L["X"], f32(0)
+        xoff, lx = (-xoff if ctx.st else -L["X"]), f32(0)  # single-thread: XOffset = -XOffset (2508)
     elif lx >= W:
         lx = f32(W) - f32(1)
     rx = R["X"]
@@ -337,7 +338,7 @@ def span_avx(ctx, t, L, R, row):
             if not (fu >= 0 and fu <= 1 and fv >= 0 and fv <= 1):
                 continue
             z = v["Z"]
-            if not z > ctx.z[row, x]:
+            if not (z >= ctx.z[row, x] if ctx.st else z > ctx.z[row, x]):  # GE_OQ (3205) / GT_OQ (2219)
                 continue
             tx = ctx.tex
             fx = (cvtt(f32(tx.width) * fu) << 2) & 0xFFFFFFFF

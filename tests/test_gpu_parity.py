@@ -263,6 +263,43 @@ def test_mixed_semantics_one_frame(gpu):
     assert (gw == ow).all()
 
 
+@pytest.mark.parametrize("sem", [abi.PRK_SEM_AVX, abi.PRK_SEM_AVX_ST])
+def test_tie_rules(gpu, sem):
+    """Exact positional duplicates (equal z at every shared pixel): strict
+    '>' keeps the EARLIER fragment (projekt.cpp:2219), the single-thread
+    overload's '>=' the LATER one (3205)."""
+    s = scenes.with_ties(scenes.random_soup(4000, 256, 256, radius=20, seed=12), seed=5)
+    run_both(s, semantics=sem)
+
+
+def test_single_thread_overload_clipping(gpu):
+    """DrawModelOptimized(Buffer,...) (2350-3358) with spans over every
+    border: its left-clip XOffset quirk (2508) on every left-clipped span."""
+    run_both(scenes.random_soup(3000, 512, 512, radius=200, seed=6, centroid_margin=150),
+             semantics=abi.PRK_SEM_AVX_ST)
+
+
+def test_mixed_tie_rules_one_frame(gpu):
+    """Queue and single-thread draws alternating in one frame over tie-heavy
+    geometry: each pair's tie rule holds against every earlier fragment."""
+    s = scenes.with_ties(scenes.random_soup(6000, 256, 256, radius=20, seed=13), seed=6)
+    T = s.tri_count
+    cut = [0, T // 5, 2 * T // 5, 3 * T // 5, T]
+    s.draws = [(cut[k], cut[k + 1] - cut[k], s.texture, abi.PRK_SEM_AVX if k % 2 == 0 else abi.PRK_SEM_AVX_ST)
+               for k in range(4)]
+    run_both(s)
+
+
+def test_mixed_tie_rules_with_scalar(gpu):
+    """Single-thread, queue and scalar draws in one frame (the mixed-mode
+    sweep path, not the all-AVX one)."""
+    s = scenes.with_ties(scenes.random_soup(3000, 256, 256, radius=20, seed=14), seed=7)
+    T = s.tri_count
+    s.draws = [(0, T // 3, s.texture, abi.PRK_SEM_AVX_ST), (T // 3, T // 3, None, abi.PRK_SEM_SCALAR),
+               (2 * T // 3, T - 2 * (T // 3), s.texture, abi.PRK_SEM_AVX)]
+    run_both(s, exact_color=True)
+
+
 def test_unsupported_combinations(gpu):
     s = scenes.random_soup(10, 64, 64, seed=0)
     r = prk.Renderer()

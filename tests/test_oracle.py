@@ -21,7 +21,7 @@ from prk import abi, scenes
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MODES = [(abi.PRK_SEM_AVX, True, True), (abi.PRK_SEM_SCALAR, False, False), (abi.PRK_SEM_SCALAR, True, False),
-         (abi.PRK_SEM_SCALAR, False, True), (abi.PRK_SEM_SCALAR, True, True)]
+         (abi.PRK_SEM_SCALAR, False, True), (abi.PRK_SEM_SCALAR, True, True), (abi.PRK_SEM_AVX_ST, True, True)]
 
 
 def same(a, b):
@@ -39,7 +39,7 @@ def test_two_restatements_agree(sem, phong, tex, seed):
     assert same(o, p)
 
 
-@pytest.mark.parametrize("sem,phong,tex", [MODES[0], MODES[1], MODES[4]])
+@pytest.mark.parametrize("sem,phong,tex", [MODES[0], MODES[1], MODES[4], MODES[5]])
 def test_two_restatements_agree_clipping(sem, phong, tex):
     """Big triangles hanging over every screen edge (top clip, left XOffset,
     right clamp, offscreen triangles, row-overflow store)."""
@@ -238,3 +238,29 @@ def test_sponza_like_multi_draw_oracle():
     c, z, w, _ = O.render(s, threads=4)
     assert (w >= 0).mean() > 0.9
     assert len(np.unique(w[w >= 0])) > 1000
+
+
+def test_single_thread_overload_ties_and_left_clip():
+    """DrawModelOptimized(Buffer,...) (projekt.cpp:2350-3358) against
+    FillLineOptimized: equal z goes to the LATER fragment (GE_OQ, 3205 vs
+    GT_OQ, 2219), and a left-clipped span starts its lane interpolation at
+    the left edge's values (XOffset = -XOffset = -0.0f, 2508, instead of
+    -L.X).  Everywhere else the two agree bit for bit; both restatements
+    agree on both."""
+    s = scenes.with_ties(scenes.random_soup(300, 128, 96, radius=24, seed=31, textured=True,
+                                            centroid_margin=-26), seed=3)  # no clipped span
+    a = O.render(s, semantics=abi.PRK_SEM_AVX)
+    st = O.render(s, semantics=abi.PRK_SEM_AVX_ST)
+    assert same(st, pyref.render(s, abi.PRK_SEM_AVX_ST, True))
+    # ties: some pixel's winner flips from a triangle to its later duplicate
+    diff = a[2] != st[2]
+    assert diff.any()
+    assert (a[1].view(np.uint32)[diff] == st[1].view(np.uint32)[diff]).all()  # same z, other winner
+    # left clip: XOffset differs only for spans whose left edge is at x < 0
+    c = scenes.random_soup(40, 64, 48, radius=40, seed=8, textured=True, centroid_margin=10)
+    c.vertices[:, 0] -= np.float32(0.35)  # push everything over the left border
+    ca = O.render(c, semantics=abi.PRK_SEM_AVX)
+    cs = O.render(c, semantics=abi.PRK_SEM_AVX_ST)
+    assert same(cs, pyref.render(c, abi.PRK_SEM_AVX_ST, True))
+    zd = ca[1].view(np.uint32) != cs[1].view(np.uint32)
+    assert zd.any() and zd[:, 0].any()  # the clipped column differs
