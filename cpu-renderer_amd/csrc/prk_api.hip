@@ -31,7 +31,21 @@ hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, co
                              uint32_t *, uint32_t *, uint32_t *, void *, uint32_t *, hipEvent_t, hipEvent_t,
                              hipStream_t, hipStream_t);
 hipError_t prk_walk_select_bytes(uint32_t, size_t *);
+hipError_t prk_obj_walk(const prk::FrameParams *, const void *, uint32_t, void *, uint32_t *, uint32_t *, int,
+                        uint32_t *, const uint32_t *, void *, void *, uint32_t *, const void *, const void *,
+                        hipStream_t);
+hipError_t prk_scan_u32(const uint32_t *, uint32_t *, uint32_t, void *, size_t *, hipStream_t);
+hipError_t prk_span_count(const prk::FrameParams *, const void *, uint32_t, uint32_t *, hipStream_t);
+hipError_t prk_span_bin(const prk::FrameParams *, const void *, uint32_t, const uint32_t *, uint32_t, uint32_t *,
+                        uint32_t *, uint32_t *, uint32_t *, uint32_t *, void *, size_t *, hipStream_t);
+hipError_t prk_launch_spans(const prk::FrameParams *, const uint32_t *, const uint32_t *, const void *,
+                            const void *, const uint32_t *, uint32_t *, uint32_t *, hipStream_t);
 }
+
+// prk_spans.hip's object descriptor.
+struct ObjDesc {
+    uint32_t draw, g0, tris, edge_off, kind, src, nsrc, pad;
+};
 
 // AVX frames shade through span records (k_walk + k_pix); must match
 // PRK_SPAN_RECORDS of prk_kernels.hip.
@@ -111,6 +125,8 @@ struct prk_context {
     std::vector<Texture> texs;
     std::vector<prk::DrawRec> draws;
     uint32_t pending_tris = 0;
+    std::vector<prk_edge> pend_edges;  // prk_draw_edges input of the pending frame
+    std::vector<prk_span> pend_spans;  // prk_draw_spans input of the pending frame
     // Per-frame scratch, two sets: frame k bins (and, on span-record frames,
     // runs k_vis) into set k % 2 on bin_stream while frame k-1 shades on the
     // flush's stream.
@@ -149,6 +165,12 @@ struct prk_context {
     bool split_span[kRing] = {};  // the slot's flush ran k_walk + k_pix
     uint32_t frame = 0;
     int last_slot = -1;
+    int last_set = -1;  // scratch set of the last per-triangle pass
+    // Span path (whole-object AETs) scratch, reused frame to frame.
+    struct SpanScratch {
+        DevBuf d_draws, d_texs, d_objs, d_edges, d_ord, d_tmp, d_cnt, d_off, d_temp, d_recs, d_pos, d_span_tri,
+            d_scnt, d_soff, d_keys_a, d_vals_a, d_keys_b, d_vals_b, d_offs, d_nwin, d_wtag, d_edges_in, d_spans_in;
+    } spans;
 };
 
 #define PRK_TRY(expr)                              \
@@ -227,6 +249,14 @@ int prk_destroy(prk_context *c) {
     }
     DevBuf *bufs[] = {&c->d_winners, &c->d_anomaly, &c->d_prof};
     for (DevBuf *b : bufs) b->release();
+    {
+        auto &S = c->spans;
+        DevBuf *sb[] = {&S.d_draws, &S.d_texs, &S.d_objs, &S.d_edges, &S.d_ord, &S.d_tmp, &S.d_cnt, &S.d_off,
+                        &S.d_temp, &S.d_recs, &S.d_pos, &S.d_span_tri, &S.d_scnt, &S.d_soff, &S.d_keys_a,
+                        &S.d_vals_a, &S.d_keys_b, &S.d_vals_b, &S.d_offs, &S.d_nwin, &S.d_wtag, &S.d_edges_in,
+                        &S.d_spans_in};
+        for (DevBuf *b : sb) b->release();
+    }
     if (c->s_mark) (void)hipEventDestroy(c->s_mark);
     if (c->h_total) (void)hipHostFree(c->h_total);
     for (auto &slot : c->ev)
@@ -443,7 +473,12 @@ int prk_geometry_wrap_device(prk_context *c, const float *v, const float *col, c
 
 int prk_draw(prk_context *c, int32_t geometry, uint32_t first_tri, uint32_t tri_count, const float P[3],
              int32_t semantics, int32_t phong, int32_t texture) {
-    if (!c || geometry < 0 || geometry >= (int32_t)c->geoms.size()) return PRK_ERR_ARG;
+    return prk_draw_objects(c, geometry, first_tri, tri_count, 1, P, semantics, phong, texture);
+}
+
+int prk_draw_objects(prk_context *c, int32_t geometry, uint32_t first_tri, uint32_t tri_count,
+                     uint32_t tris_per_object, const float P[3], int32_t semantics, int32_t phong, int32_t texture) {
+    if (!c || geometry < 0 || geometry >= (int32_t)c->geoms.size() || tris_per_object == 0) return PRK_ERR_ARG;
     const Geometry &g = c->geoms[geometry];
     if ((uint64_t)first_tri + tri_count > g.vertex_count / 3) return PRK_ERR_ARG;
     if (texture >= (int32_t)c->texs.size()) return PRK_ERR_ARG;
@@ -466,6 +501,9 @@ int prk_draw(prk_context *c, int32_t geometry, uint32_t first_tri, uint32_t tri_
     if ((phong || !tex) && !g.N) return PRK_ERR_ARG;
     if (tex && !g.UV) return PRK_ERR_ARG;
     if ((mode == prk::MODE_SC_GOURAUD || mode == prk::MODE_SC_PHONG) && !g.C) return PRK_ERR_ARG;
+    // Whole-object AETs are emulated for the AVX semantics (the reference of
+    // record and the single-thread overload); DrawModel's (scalar) are not.
+    if (tris_per_object > 1 && mode != prk::MODE_AVX) return PRK_ERR_UNSUPPORTED;
     if (tri_count == 0) return PRK_OK;
     if ((uint64_t)c->pending_tris + tri_count >= 0xFFFFFFF0ull) return PRK_ERR_ARG;
     prk::DrawRec d{};
@@ -482,15 +520,63 @@ int prk_draw(prk_context *c, int32_t geometry, uint32_t first_tri, uint32_t tri_
     d.P[1] = P ? P[1] : 0.0f;
     d.P[2] = P ? P[2] : 0.0f;
     d.flags = flags;
+    d.obj_tris = tris_per_object;
     c->draws.push_back(d);
     c->pending_tris += tri_count;
     return PRK_OK;
+}
+
+// A draw of caller edges or spans (span path): semantics / texture checks as
+// prk_draw; it takes `ids` triangle ids of the frame's numbering.
+static int draw_src(prk_context *c, uint32_t kind, uint32_t off, uint32_t n, uint32_t ids, int32_t semantics,
+                    int32_t phong, int32_t texture) {
+    if (texture >= (int32_t)c->texs.size()) return PRK_ERR_ARG;
+    if (semantics != PRK_SEM_AVX && semantics != PRK_SEM_AVX_ST) {
+        return semantics == PRK_SEM_SCALAR ? PRK_ERR_UNSUPPORTED : PRK_ERR_ARG;
+    }
+    if (texture < 0 || !phong) return PRK_ERR_UNSUPPORTED;  // projekt.cpp:1506, 2285-2316
+    if ((uint64_t)c->pending_tris + ids >= 0xFFFFFFF0ull) return PRK_ERR_ARG;
+    prk::DrawRec d{};
+    d.first_global = c->pending_tris;
+    d.tri_count = ids;
+    d.mode = prk::MODE_AVX;
+    d.tex = texture;
+    d.flags = semantics == PRK_SEM_AVX_ST ? prk::DRAW_ST : 0u;
+    d.obj_tris = 1;
+    d.src_kind = kind;
+    d.src_off = off;
+    d.src_n = n;
+    c->draws.push_back(d);
+    c->pending_tris += ids;
+    return PRK_OK;
+}
+
+int prk_draw_edges(prk_context *c, const prk_edge *edges, uint32_t edge_count, int32_t semantics, int32_t phong,
+                   int32_t texture) {
+    if (!c || (!edges && edge_count)) return PRK_ERR_ARG;
+    if (edge_count == 0) return PRK_OK;  // 0 edges: nothing to draw (P1)
+    const uint32_t off = (uint32_t)c->pend_edges.size();
+    const int rc = draw_src(c, 1, off, edge_count, 1, semantics, phong, texture);
+    if (rc == PRK_OK) c->pend_edges.insert(c->pend_edges.end(), edges, edges + edge_count);
+    return rc;
+}
+
+int prk_draw_spans(prk_context *c, const prk_span *spans, uint32_t count, int32_t semantics, int32_t phong,
+                   int32_t texture) {
+    if (!c || (!spans && count)) return PRK_ERR_ARG;
+    if (count == 0) return PRK_OK;
+    const uint32_t off = (uint32_t)c->pend_spans.size();
+    const int rc = draw_src(c, 2, off, count, count, semantics, phong, texture);
+    if (rc == PRK_OK) c->pend_spans.insert(c->pend_spans.end(), spans, spans + count);
+    return rc;
 }
 
 int prk_reset_draws(prk_context *c) {
     if (!c) return PRK_ERR_ARG;
     c->draws.clear();
     c->pending_tris = 0;
+    c->pend_edges.clear();
+    c->pend_spans.clear();
     return PRK_OK;
 }
 
@@ -547,25 +633,9 @@ int prk_debug_counters(prk_context *c, uint64_t *out, int32_t n) {
     return PRK_OK;
 }
 
-int prk_flush(prk_context *c, void *stream) {
-    if (!c) return PRK_ERR_ARG;
-    if (!c->color) return PRK_ERR_NO_TARGET;
-    if (!c->have_camera) return PRK_ERR_ARG;
-    PRK_TRY(hipSetDevice(c->device));
-    hipStream_t s = stream ? (hipStream_t)stream : c->own_stream;
-    const uint32_t T = c->pending_tris;
-    bool any_avx = false;
-    int modeset = -2;
-    for (const auto &d : c->draws) {
-        any_avx |= d.mode == prk::MODE_AVX;
-        if (modeset == -2) modeset = d.mode;
-        else if (modeset != d.mode) modeset = -1;
-    }
-    if (any_avx && (c->W % 8)) return PRK_ERR_UNSUPPORTED;  // aligned 8-wide z load, projekt.cpp:2218
-    if (modeset != prk::MODE_AVX && modeset != prk::MODE_SC_GOURAUD && modeset != prk::MODE_SC_PHONG)
-        modeset = -1;
-
-    prk::FrameParams fp{};
+// The frame parameters every pass of a flush shares (camera, lights, target, tiling).
+static void frame_params(const prk_context *c, prk::FrameParams &fp) {
+    fp = prk::FrameParams{};
     fp.D = c->transform.DistanceAboveTarget;
     fp.F = c->transform.FocalLength;
     fp.M2P = c->transform.MetersToPixels;
@@ -597,54 +667,76 @@ int prk_flush(prk_context *c, void *stream) {
     while ((1 << fp.tile_w_log2) < c->tile_w) ++fp.tile_w_log2;
     fp.tiles_x = (c->W + c->tile_w - 1) / c->tile_w;
     fp.tiles_y = (c->row1 - c->row0 + c->tile_h - 1) / c->tile_h;
+    fp.prof = (unsigned long long *)c->d_prof.p;
+    fp.winners = c->debug ? (int32_t *)c->d_winners.p : nullptr;
+    fp.clear_color = c->clear_color;
+    fp.clear_z = c->clear_z;
+}
+
+// A pending clear that the pass cannot fuse into its kernels: fill first.
+static int fill_pending_clear(prk_context *c, hipStream_t s) {
+    if (!c->clear_pending) return PRK_OK;
+    c->clear_pending = false;
+    const size_t n = (size_t)c->W * (c->row1 - c->row0);
+    if (n) {
+        hipLaunchKernelGGL(k_fill_target, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (uint32_t *)c->color,
+                           c->pitch, c->zbuf, c->W, c->row1 - c->row0, c->clear_color, c->clear_z);
+        PRK_TRY(hipGetLastError());
+    }
+    return PRK_OK;
+}
+
+// One pass of per-triangle AETs (draws of one triangle per object): bin +
+// raster into the target.  `draws` number their triangles from 0; winner ids
+// are win_base + that index.
+static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::DrawRec> &draws, uint32_t T,
+                      uint32_t win_base) {
+    int modeset = -2;
+    for (const auto &d : draws) {
+        if (modeset == -2) modeset = d.mode;
+        else if (modeset != d.mode) modeset = -1;
+    }
+    if (modeset != prk::MODE_AVX && modeset != prk::MODE_SC_GOURAUD && modeset != prk::MODE_SC_PHONG)
+        modeset = -1;
+    prk::FrameParams fp;
+    frame_params(c, fp);
     fp.tri_count = T;
-    fp.ndraws = (uint32_t)c->draws.size();
+    fp.ndraws = (uint32_t)draws.size();
+    fp.win_base = win_base;
     const uint32_t ntiles = (uint32_t)(fp.tiles_x * fp.tiles_y);
-    if (fp.tiles_x > 65535 || fp.tiles_y > 65535) return PRK_ERR_UNSUPPORTED;
 
     c->stats.triangles = T;
     c->stats.tiles = ntiles;
     c->stats.bin_entries = 0;
     const int slot = (int)(c->frame % prk_context::kRing);
     harvest(c, slot);  // a flush kRing frames old: long finished
-    if (!c->d_prof.p) {
-        PRK_TRY(c->d_prof.ensure(16 * sizeof(uint64_t)));
-        PRK_TRY(hipMemsetAsync(c->d_prof.p, 0, 16 * sizeof(uint64_t), s));
-    }
-    fp.prof = (unsigned long long *)c->d_prof.p;
-    if (c->debug) {
-        PRK_TRY(c->d_winners.ensure((size_t)c->W * (c->row1 - c->row0) * 4));
-        PRK_TRY(hipMemsetAsync(c->d_winners.p, 0xFF, (size_t)c->W * (c->row1 - c->row0) * 4, s));
-        fp.winners = (int32_t *)c->d_winners.p;
-        c->winners_valid = true;
-    }
     // A pending fused clear: the span-record kernels (AVX frames) fold it in;
     // every other frame fills the target first, on this stream.
     const bool fuse = c->clear_pending && T > 0 && modeset == prk::MODE_AVX && PRK_SPAN_RECORDS_HOST;
-    if (c->clear_pending && !fuse) {
-        size_t n = (size_t)c->W * (c->row1 - c->row0);
-        if (n) {
-            hipLaunchKernelGGL(k_fill_target, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                               (uint32_t *)c->color, c->pitch, c->zbuf, c->W, c->row1 - c->row0, c->clear_color,
-                               c->clear_z);
-            PRK_TRY(hipGetLastError());
-        }
+    if (!fuse) {
+        const int rc = fill_pending_clear(c, s);
+        if (rc != PRK_OK) return rc;
     }
     c->clear_pending = false;
     fp.clear_fused = fuse ? 1 : 0;
-    fp.clear_color = c->clear_color;
-    fp.clear_z = c->clear_z;
-    if (T == 0) {
-        c->draws.clear();
-        c->pending_tris = 0;
-        return PRK_OK;
-    }
-    // Binning runs on bin_stream into scratch set k % 2, so it overlaps the
-    // previous frame's raster on the flush stream; the raster waits for it.
-    // (any set may follow any: a set's reuse waits for its own last reader)
+    if (T == 0) return PRK_OK;
+    // Binning runs on bin_stream into one of the scratch sets, so it overlaps
+    // the previous frame's raster on the flush stream; the raster waits for
+    // it.  Consecutive frames take consecutive sets (nsets of them), and a
+    // set's reuse waits for its own last reader.
     const int nsets = (size_t)c->W * (size_t)(c->row1 - c->row0) <= kSmallBandPx ? prk_context::kSets
                                                                                 : std::min(prk_context::kSets, 2);
-    prk_context::BinSet &B = c->bset[c->frame % nsets];
+    const int si = (c->last_set + 1) % nsets;
+    c->last_set = si;
+    prk_context::BinSet &B = c->bset[si];
+    // Any error below leaves the set's table mirrors unknown: forget them.
+    struct MirrorGuard {
+        prk_context::BinSet &b;
+        bool ok = false;
+        ~MirrorGuard() {
+            if (!ok) b.h_draws_at = b.h_texs_at = nullptr;
+        }
+    } guard{B};
     hipStream_t bs = c->bin_stream;
     if (B.used) PRK_TRY(hipStreamWaitEvent(bs, B.free_ev, 0));  // the raster of frame k-2 read this set
     // A set buffer that must grow is freed by the host: wait for its reader.
@@ -671,19 +763,20 @@ int prk_flush(prk_context *c, void *stream) {
         hipError_t e = bset_ensure(d, bytes);
         if (e != hipSuccess) return e;
         if (at == d.p && mirror.size() == bytes && std::memcmp(mirror.data(), src, bytes) == 0) return hipSuccess;
+        at = nullptr;  // unknown until the copy is queued
         mirror.assign((const uint8_t *)src, (const uint8_t *)src + bytes);
-        at = d.p;
-        // from the mirror: it outlives this call (the next frame's host sync
-        // on the bin stream precedes its next reassignment)
-        return hipMemcpyAsync(d.p, mirror.data(), bytes, hipMemcpyHostToDevice, bs);
+        // from the mirror: it outlives this call (the set's next use waits for
+        // this frame's raster, which follows the copy on the bin stream)
+        e = hipMemcpyAsync(d.p, mirror.data(), bytes, hipMemcpyHostToDevice, bs);
+        if (e == hipSuccess) at = d.p;
+        return e;
     };
-    PRK_TRY(upload_table(B.d_draws, B.h_draws, B.h_draws_at, c->draws.data(),
-                         c->draws.size() * sizeof(prk::DrawRec)));
+    PRK_TRY(upload_table(B.d_draws, B.h_draws, B.h_draws_at, draws.data(), draws.size() * sizeof(prk::DrawRec)));
     if (!texs.empty())
         PRK_TRY(upload_table(B.d_texs, B.h_texs, B.h_texs_at, texs.data(), texs.size() * sizeof(prk::TexRec)));
     fp.draws = (const prk::DrawRec *)B.d_draws.p;
     fp.texs = (const prk::TexRec *)B.d_texs.p;
-    fp.draw0 = c->draws[0];
+    fp.draw0 = draws[0];
     fp.tex0 = prk::TexRec{};
     if (fp.draw0.tex >= 0 && (size_t)fp.draw0.tex < texs.size()) fp.tex0 = texs[fp.draw0.tex];
     fp.tri_draw = nullptr;
@@ -791,10 +884,189 @@ int prk_flush(prk_context *c, void *stream) {
     c->split_span[slot] = modeset == prk::MODE_AVX;
     c->last_slot = slot;
     c->frame++;
-    c->draws.clear();
-    c->pending_tris = 0;
+    guard.ok = true;
     return PRK_OK;
 }
+
+// One pass of whole-object AETs (prk_spans.hip): walk every object's AET
+// into span records (count pass, scan, emit pass), bin the spans to tiles,
+// then visibility + shading.  Synchronous with respect to the host at the
+// two counts it reads back.
+static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::DrawRec> &draws, uint32_t T,
+                       uint32_t win_base) {
+    prk::FrameParams fp;
+    frame_params(c, fp);
+    fp.tri_count = T;
+    fp.ndraws = (uint32_t)draws.size();
+    fp.win_base = win_base;
+    const uint32_t ntiles = (uint32_t)(fp.tiles_x * fp.tiles_y);
+    const bool fuse = c->clear_pending && T > 0;
+    c->clear_pending = false;
+    fp.clear_fused = fuse ? 1 : 0;
+    if (T == 0) return PRK_OK;
+    prk_context::SpanScratch &S = c->spans;
+    // Objects in submission order (ObjDesc kinds: prk_spans.hip).
+    std::vector<ObjDesc> objs;
+    uint64_t eslots = 0;
+    for (uint32_t di = 0; di < draws.size(); ++di) {
+        const prk::DrawRec &d = draws[di];
+        if (d.src_kind == 1) {
+            objs.push_back(ObjDesc{di, d.first_global, 0u, (uint32_t)eslots, 1u, d.src_off, d.src_n, 0u});
+            eslots += d.src_n;
+        } else if (d.src_kind == 2) {
+            for (uint32_t k = 0; k < d.src_n; ++k)
+                objs.push_back(ObjDesc{di, d.first_global + k, 0u, 0u, 2u, d.src_off + k, 1u, 0u});
+        } else {
+            const uint32_t per = std::max<uint32_t>(1u, d.obj_tris);
+            for (uint32_t t = 0; t < d.tri_count; t += per) {
+                const uint32_t n = std::min(per, d.tri_count - t);
+                objs.push_back(ObjDesc{di, d.first_global + t, n, (uint32_t)eslots, 0u, 0u, 0u, 0u});
+                eslots += 3ull * n;
+            }
+        }
+    }
+    if (eslots >= 0xFFFFFFFFull) return PRK_ERR_UNSUPPORTED;
+    const uint32_t nobj = (uint32_t)objs.size();
+    std::vector<prk::TexRec> texs(c->texs.size());
+    for (size_t i = 0; i < texs.size(); ++i)
+        texs[i] = prk::TexRec{c->texs[i].mem, c->texs[i].w, c->texs[i].h, c->texs[i].pitch, c->texs[i].filter};
+    PRK_TRY(hipDeviceSynchronize());  // the scratch below is reused frame to frame
+    PRK_TRY(S.d_draws.ensure(draws.size() * sizeof(prk::DrawRec)));
+    PRK_TRY(hipMemcpy(S.d_draws.p, draws.data(), draws.size() * sizeof(prk::DrawRec), hipMemcpyHostToDevice));
+    if (!texs.empty()) {
+        PRK_TRY(S.d_texs.ensure(texs.size() * sizeof(prk::TexRec)));
+        PRK_TRY(hipMemcpy(S.d_texs.p, texs.data(), texs.size() * sizeof(prk::TexRec), hipMemcpyHostToDevice));
+    }
+    fp.draws = (const prk::DrawRec *)S.d_draws.p;
+    fp.texs = (const prk::TexRec *)S.d_texs.p;
+    fp.draw0 = draws[0];
+    fp.tex0 = prk::TexRec{};
+    if (fp.draw0.tex >= 0 && (size_t)fp.draw0.tex < texs.size()) fp.tex0 = texs[fp.draw0.tex];
+    PRK_TRY(S.d_objs.ensure(objs.size() * sizeof(ObjDesc)));
+    PRK_TRY(hipMemcpy(S.d_objs.p, objs.data(), objs.size() * sizeof(ObjDesc), hipMemcpyHostToDevice));
+    const size_t es = std::max<size_t>((size_t)eslots, 1);
+    PRK_TRY(S.d_edges.ensure(es * 80));
+    PRK_TRY(S.d_ord.ensure(es * 4));
+    PRK_TRY(S.d_tmp.ensure(es * 4));
+    if (!c->pend_edges.empty()) {
+        PRK_TRY(S.d_edges_in.ensure(c->pend_edges.size() * sizeof(prk_edge)));
+        PRK_TRY(hipMemcpy(S.d_edges_in.p, c->pend_edges.data(), c->pend_edges.size() * sizeof(prk_edge),
+                          hipMemcpyHostToDevice));
+    }
+    if (!c->pend_spans.empty()) {
+        PRK_TRY(S.d_spans_in.ensure(c->pend_spans.size() * sizeof(prk_span)));
+        PRK_TRY(hipMemcpy(S.d_spans_in.p, c->pend_spans.data(), c->pend_spans.size() * sizeof(prk_span),
+                          hipMemcpyHostToDevice));
+    }
+    PRK_TRY(S.d_cnt.ensure(((size_t)nobj + 1) * 4));
+    PRK_TRY(S.d_off.ensure(((size_t)nobj + 1) * 4));
+    uint32_t *cnt = (uint32_t *)S.d_cnt.p, *off = (uint32_t *)S.d_off.p;
+    PRK_TRY(hipMemsetAsync(cnt, 0, ((size_t)nobj + 1) * 4, s));
+    PRK_TRY(prk_obj_walk(&fp, S.d_objs.p, nobj, S.d_edges.p, (uint32_t *)S.d_ord.p, (uint32_t *)S.d_tmp.p, 0, cnt,
+                         nullptr, nullptr, nullptr, nullptr, S.d_edges_in.p, S.d_spans_in.p, s));
+    size_t tb = 0;
+    PRK_TRY(prk_scan_u32(cnt, off, nobj + 1, nullptr, &tb, s));
+    PRK_TRY(S.d_temp.ensure(std::max<size_t>(tb, 16)));
+    PRK_TRY(prk_scan_u32(cnt, off, nobj + 1, S.d_temp.p, &tb, s));
+    uint32_t nspan = 0;
+    PRK_TRY(hipMemcpyAsync(&nspan, off + nobj, 4, hipMemcpyDeviceToHost, s));
+    PRK_TRY(hipStreamSynchronize(s));
+    if (nspan >= prk::kMaxPairs) return PRK_ERR_UNSUPPORTED;  // 31-bit span tags
+    const size_t ns = std::max<uint32_t>(nspan, 1);
+    PRK_TRY(S.d_recs.ensure(ns * 64));
+    PRK_TRY(S.d_pos.ensure(ns * 16));
+    PRK_TRY(S.d_span_tri.ensure(ns * 4));
+    PRK_TRY(prk_obj_walk(&fp, S.d_objs.p, nobj, S.d_edges.p, (uint32_t *)S.d_ord.p, (uint32_t *)S.d_tmp.p, 1, cnt,
+                         off, S.d_recs.p, S.d_pos.p, (uint32_t *)S.d_span_tri.p, S.d_edges_in.p, S.d_spans_in.p,
+                         s));
+    PRK_TRY(S.d_scnt.ensure(((size_t)nspan + 1) * 4));
+    PRK_TRY(S.d_soff.ensure(((size_t)nspan + 1) * 4));
+    uint32_t *scnt = (uint32_t *)S.d_scnt.p, *soff = (uint32_t *)S.d_soff.p;
+    PRK_TRY(prk_span_count(&fp, S.d_pos.p, nspan, scnt, s));
+    PRK_TRY(prk_scan_u32(scnt, soff, nspan + 1, nullptr, &tb, s));
+    PRK_TRY(S.d_temp.ensure(std::max<size_t>(tb, 16)));
+    PRK_TRY(prk_scan_u32(scnt, soff, nspan + 1, S.d_temp.p, &tb, s));
+    uint32_t total = 0;
+    PRK_TRY(hipMemcpyAsync(&total, soff + nspan, 4, hipMemcpyDeviceToHost, s));
+    PRK_TRY(hipStreamSynchronize(s));
+    c->stats.triangles = T;
+    c->stats.tiles = ntiles;
+    c->stats.bin_entries = total;
+    const size_t ne = std::max<uint32_t>(total, 1);
+    PRK_TRY(S.d_keys_a.ensure(ne * 4));
+    PRK_TRY(S.d_vals_a.ensure(ne * 4));
+    PRK_TRY(S.d_keys_b.ensure(ne * 4));
+    PRK_TRY(S.d_vals_b.ensure(ne * 4));
+    PRK_TRY(S.d_offs.ensure(((size_t)ntiles + 1) * 4));
+    size_t sb = 0;
+    PRK_TRY(prk_span_bin(&fp, S.d_pos.p, nspan, soff, total, (uint32_t *)S.d_keys_a.p, (uint32_t *)S.d_vals_a.p,
+                         (uint32_t *)S.d_keys_b.p, (uint32_t *)S.d_vals_b.p, (uint32_t *)S.d_offs.p, nullptr, &sb, s));
+    PRK_TRY(S.d_temp.ensure(std::max<size_t>(sb, 16)));
+    PRK_TRY(prk_span_bin(&fp, S.d_pos.p, nspan, soff, total, (uint32_t *)S.d_keys_a.p, (uint32_t *)S.d_vals_a.p,
+                         (uint32_t *)S.d_keys_b.p, (uint32_t *)S.d_vals_b.p, (uint32_t *)S.d_offs.p, S.d_temp.p, &sb,
+                         s));
+    PRK_TRY(S.d_nwin.ensure((size_t)ntiles * 4));
+    PRK_TRY(S.d_wtag.ensure((size_t)ntiles * c->tile_w * c->tile_h * 4));
+    PRK_TRY(prk_launch_spans(&fp, (const uint32_t *)S.d_offs.p, (const uint32_t *)S.d_vals_b.p, S.d_pos.p,
+                             S.d_recs.p, (const uint32_t *)S.d_span_tri.p, (uint32_t *)S.d_nwin.p,
+                             (uint32_t *)S.d_wtag.p, s));
+    return PRK_OK;
+}
+
+int prk_flush(prk_context *c, void *stream) {
+    if (!c) return PRK_ERR_ARG;
+    if (!c->color) return PRK_ERR_NO_TARGET;
+    if (!c->have_camera) return PRK_ERR_ARG;
+    PRK_TRY(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->own_stream;
+    bool any_avx = false;
+    for (const auto &d : c->draws) any_avx |= d.mode == prk::MODE_AVX;
+    if (any_avx && (c->W % 8)) return PRK_ERR_UNSUPPORTED;  // aligned 8-wide z load, projekt.cpp:2218
+    prk::FrameParams probe;
+    frame_params(c, probe);
+    if (probe.tiles_x > 65535 || probe.tiles_y > 65535) return PRK_ERR_UNSUPPORTED;
+    if (!c->d_prof.p) {
+        PRK_TRY(c->d_prof.ensure(16 * sizeof(uint64_t)));
+        PRK_TRY(hipMemsetAsync(c->d_prof.p, 0, 16 * sizeof(uint64_t), s));
+    }
+    if (c->debug) {
+        PRK_TRY(c->d_winners.ensure((size_t)c->W * (c->row1 - c->row0) * 4));
+        PRK_TRY(hipMemsetAsync(c->d_winners.p, 0xFF, (size_t)c->W * (c->row1 - c->row0) * 4, s));
+        c->winners_valid = true;
+    }
+    // Passes: maximal runs of draws of one kind (per-triangle AETs, or
+    // whole-object AETs); each pass z-tests against the target as the
+    // previous one left it, which is the reference's sequential order.
+    std::vector<prk::DrawRec> dr = std::move(c->draws);
+    c->draws.clear();
+    c->pending_tris = 0;
+    struct Clear {  // the frame's edge / span input goes with its draws
+        prk_context *c;
+        ~Clear() { c->pend_edges.clear(); c->pend_spans.clear(); }
+    } clear_src{c};
+    if (dr.empty()) return c->clear_pending ? fill_pending_clear(c, s) : PRK_OK;
+    auto span_path = [](const prk::DrawRec &d) { return d.obj_tris > 1 || d.src_kind != 0; };
+    size_t i = 0;
+    int rc = PRK_OK;
+    while (i < dr.size() && rc == PRK_OK) {
+        const bool obj = span_path(dr[i]);
+        size_t j = i;
+        std::vector<prk::DrawRec> seg;
+        uint32_t T = 0;
+        const uint32_t base = dr[i].first_global;
+        while (j < dr.size() && span_path(dr[j]) == obj) {
+            prk::DrawRec d = dr[j];
+            d.first_global -= base;
+            T += d.tri_count;
+            seg.push_back(d);
+            ++j;
+        }
+        rc = obj ? flush_spans(c, s, seg, T, base) : flush_tris(c, s, seg, T, base);
+        i = j;
+    }
+    return rc;
+}
+
 
 int prk_synchronize(prk_context *c) {
     if (!c) return PRK_ERR_ARG;

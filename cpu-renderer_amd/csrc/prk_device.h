@@ -36,6 +36,10 @@ struct DrawRec {
     int32_t tex;                  // texture index or -1
     float P[3];                   // object offset (render_entry_3d_object::P)
     uint32_t flags;               // DRAW_ST: single-thread DrawModelOptimized(Buffer,...) quirks
+    uint32_t obj_tris;            // triangles per render_entry_3d_object (1: per-triangle AETs;
+                                  // > 1: one AET per object, drawn through the span path)
+    uint32_t src_kind;            // 0: geometry; 1: a caller's edge list; 2: caller spans (span path)
+    uint32_t src_off, src_n;      // kind 1/2: range of the flush's edge / span input
 };
 
 // Draw flags.  DRAW_ST: the single-thread overload DrawModelOptimized(Buffer,
@@ -106,6 +110,7 @@ struct FrameParams {
     uint32_t *color; // points at frame row row0
     float *zbuf;     // points at frame row row0 (row stride W floats)
     int32_t *winners;// optional (debug): per pixel winning triangle, -1 none
+    uint32_t win_base; // winner ids of this pass start here (frames drawn in several passes)
     // fused clear (prk_target_clear_on_flush): prior contents are (clear_color, clear_z)
     int32_t clear_fused;
     uint32_t clear_color;
@@ -350,11 +355,11 @@ __device__ __forceinline__ void load_tri(const DrawRec &d, uint32_t gt, TriRaw<M
 }
 
 // FillEdgeTable (projekt.cpp:3882-4121) for ONE binned (front-facing)
-// triangle followed by MergeSort (2-72) of its <= 3 visible edges.  Returns
-// the edge count.
+// triangle: its three edges {0,1},{1,2},{2,0} and which of them are visible
+// (3968, 4066), in edge order, unsorted.
 template <int M>
-__device__ __forceinline__ int setup_from_raw(const TriRaw<M> &r, const DrawRec &d, const FrameParams &fp,
-                                              Edge &s0, Edge &s1, Edge &s2) {
+__device__ __forceinline__ void tri_edges(const TriRaw<M> &r, const DrawRec &d, const FrameParams &fp, Edge &e0,
+                                          Edge &e1, Edge &e2, bool *vis) {
     using TR = ModeTraits<M>;
     constexpr bool kTex = TR::tex;
     constexpr bool kPhong = TR::phong;
@@ -379,8 +384,6 @@ __device__ __forceinline__ int setup_from_raw(const TriRaw<M> &r, const DrawRec 
         uv[k][0] = r.uv[2 * k + 0]; uv[k][1] = r.uv[2 * k + 1];
     }
 
-    Edge e0, e1, e2;
-    bool vis[3];
 #pragma unroll
     for (int ei = 0; ei < 3; ++ei) {
         const int i0 = ei, i1 = (ei + 1) % 3;  // Indices {0,1},{1,2},{2,0}
@@ -481,6 +484,16 @@ __device__ __forceinline__ int setup_from_raw(const TriRaw<M> &r, const DrawRec 
         E.Left = (E.YMin == round_s32(proj[i0].y)) ? 1 : 0;  // 4093
         if (ei == 0) e0 = E; else if (ei == 1) e1 = E; else e2 = E;
     }
+}
+
+// FillEdgeTable for ONE triangle followed by MergeSort (2-72) of its <= 3
+// visible edges (the per-triangle AET).  Returns the edge count.
+template <int M>
+__device__ __forceinline__ int setup_from_raw(const TriRaw<M> &r, const DrawRec &d, const FrameParams &fp,
+                                              Edge &s0, Edge &s1, Edge &s2) {
+    Edge e0, e1, e2;
+    bool vis[3];
+    tri_edges<M>(r, d, fp, e0, e1, e2, vis);
     // Compact visible edges in edge order, then MergeSort (projekt.cpp:2-72).
     const int n = (int)vis[0] + (int)vis[1] + (int)vis[2];
     const Edge a0 = sel(vis[0], e0, sel(vis[1], e1, e2));

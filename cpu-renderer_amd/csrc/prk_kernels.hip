@@ -976,9 +976,9 @@ __global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
         for (int p = threadIdx.x; p < npx; p += blockDim.x) {
             const int x = tc.x0 + (p & (fp.tile_w - 1)), y = tc.y0 + (p >> fp.tile_w_log2);
             if (x >= tc.x1 || y >= tc.y1) continue;
-            uint32_t j;
-            fp.winners[(size_t)(y - fp.row0) * fp.W + x] =
-                tag_pair((uint32_t)tc.key[p], j) ? (int32_t)pair_tri[j] : -1;
+            uint32_t j;  // (the prior contents keep their winner: an earlier pass's, or -1)
+            if (tag_pair((uint32_t)tc.key[p], j))
+                fp.winners[(size_t)(y - fp.row0) * fp.W + x] = (int32_t)(fp.win_base + pair_tri[j]);
         }
     }
     if constexpr (kRec) {
@@ -1293,8 +1293,9 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
     if ((uint32_t)lane < cnt) walk_flush(fp, q, (int)((head + lane) & (kWalkQ - 1)), won, recs);
 }
 
-// k_pix: shade the won pixels of one tile from their span records.
-template <bool UNI>
+// k_pix: shade the won pixels of one tile from their span records (SPAN:
+// records indexed by span, the whole-object path; else by (pair, row in tile)).
+template <bool UNI, bool SPAN = false>
 __global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__restrict__ nwin_in,
                                              const uint32_t *__restrict__ wtag, const SpanRec *__restrict__ recs) {
     // PRK_PIX_SPLIT workgroups per tile, each a contiguous share of its pixels
@@ -1316,7 +1317,7 @@ __global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__r
             if (fp.clear_fused && x < tc.x1 && Row < tc.y1) put_winner(fp, x, Row, fp.clear_z, fp.clear_color);
             continue;
         }
-        const float4 *q = reinterpret_cast<const float4 *>(recs + (size_t)j * fp.tile_h + ly);
+        const float4 *q = reinterpret_cast<const float4 *>(recs + (SPAN ? (size_t)j : (size_t)j * fp.tile_h + ly));
         const float4 r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];
         const int32_t lt = __float_as_int(r0.x);
         const int32_t LeftXa = (int32_t)(int16_t)(lt & 0xFFFF);
@@ -1348,6 +1349,116 @@ __global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__r
     }
 }
 
+// ---------------------------------------------------------------------------
+// Span path (whole-object AETs, prk_spans.hip): visibility over a tile's bin
+// of spans.  Every span is one pair of one row, given by its lane-init record
+// (SpanRec) and pixel range; its tag is its submission-order index.  The
+// items are the triangle path's visibility items (item_vis_group).
+// ---------------------------------------------------------------------------
+struct SpanPosK { int32_t row, minx, maxx; uint32_t flags; };  // == prk_spans.hip SpanPos
+
+__global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
+    k_span_vis(FrameParams fp, const uint32_t *__restrict__ offs, const uint32_t *__restrict__ bins,
+               const SpanPosK *__restrict__ pos, const SpanRec *__restrict__ recs,
+               const uint32_t *__restrict__ span_tri, uint32_t *__restrict__ nwin_out, uint32_t *__restrict__ wtag) {
+    extern __shared__ unsigned long long lds[];
+    const int ntile = fp.tiles_x * fp.tiles_y;
+    const int t = blockIdx.x;
+    if (t >= ntile) return;
+    const uint32_t b0 = offs[t], b1 = offs[t + 1];
+    if (b0 == b1) {
+        if (threadIdx.x == 0) nwin_out[t] = 0;
+        return;
+    }
+    const uint32_t n = b1 - b0;
+    TileCtx tc = tile_ctx(fp, t);
+    const int npx = fp.tile_w * fp.tile_h;
+    tc.key = lds;
+    VisSlots *slots = reinterpret_cast<VisSlots *>(lds + npx);
+    VisSlots &ws = slots[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int p = threadIdx.x; p < npx; p += blockDim.x) {  // prior z (as k_vis)
+        const int lx = p & (fp.tile_w - 1), ly = p >> fp.tile_w_log2;
+        const int x = tc.x0 + lx, y = tc.y0 + ly;
+        unsigned long long k = ~0ull;
+        if (x < tc.x1 && y < tc.y1) {
+            const float z = fp.clear_fused ? fp.clear_z : fp.zbuf[(size_t)(y - fp.row0) * fp.W + x];
+            k = (z != z) ? ~0ull : (((unsigned long long)zkey(z) << 32) | kTagPrior);
+        }
+        tc.key[p] = k;
+    }
+    __syncthreads();
+    constexpr int G = PRK_VIS_GROUP > 0 ? PRK_VIS_GROUP : 1;
+    const uint32_t nwaves = blockDim.x >> 6;
+    for (uint32_t base = wave * 64; base < n; base += 64 * nwaves) {
+        const uint32_t i = base + lane;
+        int items = 0;
+        if (i < n) {
+            const uint32_t sidx = bins[b0 + i];
+            const SpanPosK sp = pos[sidx];
+            if (sp.row >= tc.y0 && sp.row < tc.y1) {
+                const int32_t xa = max(sp.minx, tc.x0), xb = min(sp.maxx, tc.x1);
+                if (xa < xb) {
+                    const float4 *q = reinterpret_cast<const float4 *>(recs + sidx);
+                    const float4 r0 = q[0], r1 = q[1], r2 = q[2];
+                    ws.i[SI_XA][lane] = xa;
+                    ws.i[SI_XB][lane] = xb;
+                    ws.i[SI_LEFT][lane] = (int32_t)(int16_t)(__float_as_int(r0.x) & 0xFFFF);
+                    ws.i[SI_TAG][lane] = (int32_t)pair_tag(sidx, (sp.flags & DRAW_ST) != 0);
+                    ws.i[SI_ROW][lane] = sp.row;
+                    ws.f[SF_XOFF][lane] = r0.y;
+                    ws.f[SF_LW][lane] = r0.z; ws.f[SF_LU][lane] = r0.w; ws.f[SF_LV][lane] = r1.x;
+                    ws.f[SF_LZ][lane] = r1.y;
+                    ws.f[SF_IW][lane] = r1.z; ws.f[SF_IU][lane] = r1.w; ws.f[SF_IV][lane] = r2.x;
+                    ws.f[SF_IZ][lane] = r2.y;
+                    items = (xb - xa + G - 1) / G;
+                }
+            }
+        }
+        const int incl = wave_incl_scan(items, lane);
+        const int total = __builtin_amdgcn_readlane(incl, 63);
+        const int excl = incl - items;
+        ws.i[SI_PRE][lane] = excl;
+        int carry = 0;
+        for (int it0 = 0; it0 < total; it0 += 64) {
+            ws.i[SI_MARK][lane] = 0;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (items > 0 && excl >= it0 && excl < it0 + 64) ws.i[SI_MARK][excl - it0] = lane + 1;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const int m = max(wave_incl_max(ws.i[SI_MARK][lane]), carry);
+            carry = __builtin_amdgcn_readlane(m, 63);
+            const int it = it0 + lane;
+            if (it < total) {
+                const int sl = m - 1, j = it - ws.i[SI_PRE][sl];
+                item_vis_group(tc, ws, sl, j, ws.i[SI_ROW][sl]);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    __syncthreads();
+    uint32_t *tags_out = wtag + (size_t)t * npx;
+    int anyw = 0;
+    for (int p = threadIdx.x; p < npx; p += blockDim.x) {
+        const uint32_t low = (uint32_t)tc.key[p];
+        tags_out[p] = low;
+        uint32_t j;
+        if (tag_pair(low, j)) anyw = 1;
+        if (fp.winners) {
+            const int x = tc.x0 + (p & (fp.tile_w - 1)), y = tc.y0 + (p >> fp.tile_w_log2);
+            if (x < tc.x1 && y < tc.y1 && tag_pair(low, j))
+                fp.winners[(size_t)(y - fp.row0) * fp.W + x] = (int32_t)(fp.win_base + span_tri[j]);
+        }
+    }
+    anyw = __syncthreads_or(anyw);
+    if (threadIdx.x == 0) nwin_out[t] = (uint32_t)anyw;
+}
+
 // Explicit instantiations used by the host.
 #define PRK_VIS_ARGS FrameParams, const uint32_t *, const uint2 *, uint8_t *, uint32_t *, uint32_t *, uint32_t *, \
                      const uint32_t *, uint8_t *, uint32_t *
@@ -1363,6 +1474,7 @@ template __global__ void k_walk<false>(PRK_WALK_ARGS);
 template __global__ void k_walk<true>(PRK_WALK_ARGS);
 template __global__ void k_pix<false>(PRK_PIX_ARGS);
 template __global__ void k_pix<true>(PRK_PIX_ARGS);
+template __global__ void k_pix<false, true>(PRK_PIX_ARGS);
 PRK_INST(-1, false)
 PRK_INST(MODE_AVX, false)
 PRK_INST(MODE_AVX, true)
@@ -1476,6 +1588,21 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
 #undef PRK_VIS
 #undef PRK_SHADE
 #undef PRK_SPANPIX
+    return hipGetLastError();
+}
+
+// Span path: visibility then shading of the pass's spans.
+hipError_t prk_launch_spans(const prk::FrameParams *fp, const uint32_t *offs, const uint32_t *bins, const void *pos,
+                            const void *recs, const uint32_t *span_tri, uint32_t *nwin, uint32_t *wtag,
+                            hipStream_t s) {
+    const uint32_t ntile = (uint32_t)(fp->tiles_x * fp->tiles_y);
+    if (ntile == 0) return hipSuccess;
+    const size_t lv = vis_lds(fp);
+    hipLaunchKernelGGL(prk::k_span_vis, dim3(ntile), dim3(64 * prk::kVisWaves), lv, s, *fp, offs, bins,
+                       reinterpret_cast<const prk::SpanPosK *>(pos), reinterpret_cast<const prk::SpanRec *>(recs),
+                       span_tri, nwin, wtag);
+    hipLaunchKernelGGL((prk::k_pix<false, true>), dim3(ntile * PRK_PIX_SPLIT), dim3(256), 0, s, *fp, nwin, wtag,
+                       reinterpret_cast<const prk::SpanRec *>(recs));
     return hipGetLastError();
 }
 

@@ -58,6 +58,10 @@ _SIGS = {
                                            C.c_uint32, C.POINTER(C.c_int32)]),
     "prk_draw": (C.c_int, [C.c_void_p, C.c_int32, C.c_uint32, C.c_uint32, C.POINTER(C.c_float),
                            C.c_int32, C.c_int32, C.c_int32]),
+    "prk_draw_objects": (C.c_int, [C.c_void_p, C.c_int32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                   C.POINTER(C.c_float), C.c_int32, C.c_int32, C.c_int32]),
+    "prk_draw_edges": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int32, C.c_int32, C.c_int32]),
+    "prk_draw_spans": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int32, C.c_int32, C.c_int32]),
     "prk_flush": (C.c_int, [C.c_void_p, C.c_void_p]),
     "prk_reset_draws": (C.c_int, [C.c_void_p]),
     "prk_synchronize": (C.c_int, [C.c_void_p]),
@@ -227,10 +231,11 @@ class Renderer:
         _check("prk_set_debug", self._L.prk_set_debug(self._h, int(bool(on))))
 
     # ---- draws (the reference's entry points) -----------------------------
-    def _draw(self, geom, first_tri, tri_count, P, semantics, phong, texture):
+    def _draw(self, geom, first_tri, tri_count, P, semantics, phong, texture, tris_per_object=1):
         Pc = (C.c_float * 3)(*(P or (0.0, 0.0, 0.0)))
-        _check("prk_draw", self._L.prk_draw(self._h, geom, first_tri, tri_count, Pc, semantics,
-                                            int(bool(phong)), -1 if texture is None else texture))
+        _check("prk_draw_objects", self._L.prk_draw_objects(self._h, geom, first_tri, tri_count, tris_per_object,
+                                                            Pc, semantics, int(bool(phong)),
+                                                            -1 if texture is None else texture))
 
     def draw_model_optimized(self, geom, tri_count, first_tri=0, P=None, bitmap=None, phong=True):
         """DrawModelOptimized(RenderQueue, ...) -> FillLineOptimized semantics
@@ -247,9 +252,26 @@ class Renderer:
         XOffset quirk (2508) and the >= z-test (3205).  Needs bitmap + phong."""
         self._draw(geom, first_tri, tri_count, P, abi.PRK_SEM_AVX_ST, phong, bitmap)
 
-    def draw(self, semantics, geom, tri_count, first_tri=0, P=None, bitmap=None, phong=True):
-        """Any PRK_SEM_* draw."""
-        self._draw(geom, first_tri, tri_count, P, semantics, phong, bitmap)
+    def draw(self, semantics, geom, tri_count, first_tri=0, P=None, bitmap=None, phong=True, tris_per_object=1):
+        """Any PRK_SEM_* draw; tris_per_object > 1: consecutive objects of that
+        many triangles, one active edge table each (prk_draw_objects)."""
+        self._draw(geom, first_tri, tri_count, P, semantics, phong, bitmap, tris_per_object)
+
+    def draw_edges(self, edge_words, semantics=abi.PRK_SEM_AVX, bitmap=None, phong=True):
+        """DrawModelOptimized* on a ready edge_info list: uint32 [n, 27] in
+        prk_edge layout (prk.h), sorted by YMin as FillEdgeTable leaves it."""
+        w = np.ascontiguousarray(edge_words, np.uint32)
+        self._keep.append(w)
+        _check("prk_draw_edges", self._L.prk_draw_edges(self._h, _ptr(w), w.shape[0], semantics, int(bool(phong)),
+                                                        -1 if bitmap is None else bitmap))
+
+    def draw_spans(self, span_words, semantics=abi.PRK_SEM_AVX, bitmap=None, phong=True):
+        """Caller spans (the work records of DoLineRenderWork): uint32 [n, 25]
+        in prk_span layout (prk.h)."""
+        w = np.ascontiguousarray(span_words, np.uint32)
+        self._keep.append(w)
+        _check("prk_draw_spans", self._L.prk_draw_spans(self._h, _ptr(w), w.shape[0], semantics, int(bool(phong)),
+                                                        -1 if bitmap is None else bitmap))
 
     def complete_all_work(self, stream=None):
         """Platform.CompleteAllWork: run every recorded draw (asynchronous)."""
@@ -278,7 +300,7 @@ class Renderer:
 
 
 def render_scene(scene, semantics=abi.PRK_SEM_AVX, phong=True, device=0, tile=None, debug=True,
-                 color=None, z=None, rows=None, fused_clear=False):
+                 color=None, z=None, rows=None, fused_clear=False, tris_per_object=1):
     """Convenience: draw a whole scenes.Scene (per-triangle submission) and
     return (color, z, winners or None, stats).  fused_clear: upload
     color / z, then clear through prk_target_clear_on_flush (the frame must
@@ -301,13 +323,13 @@ def render_scene(scene, semantics=abi.PRK_SEM_AVX, phong=True, device=0, tile=No
         draws = scene.draws if scene.draws is not None else [(0, scene.tri_count, scene.texture)]
         handles = {}
         for d in draws:
-            first, count, texture, sem = scenes_mod.draw_spec(d, semantics)
+            first, count, texture, sem, tpo = scenes_mod.draw_spec(d, semantics, tris_per_object)
             tex = None
             if texture is not None:
                 if id(texture) not in handles:
                     handles[id(texture)] = r.texture(texture)
                 tex = handles[id(texture)]
-            r.draw(sem, g, count, first_tri=first, P=scene.P, bitmap=tex, phong=phong)
+            r.draw(sem, g, count, first_tri=first, P=scene.P, bitmap=tex, phong=phong, tris_per_object=tpo)
         r.complete_all_work()
         r.synchronize()
         col, zb = r.download()

@@ -52,10 +52,10 @@ class Scene:
     P: tuple = (0.0, 0.0, 0.0)
     name: str = "scene"
     meta: dict = field(default_factory=dict)
-    # Multi-draw scenes: [(first_tri, tri_count, Texture or None[, semantics]),
-    # ...] drawn in order into one frame (one DrawModel* call each; semantics
-    # PRK_SEM_* overrides the frame's); None = one draw of every triangle with
-    # `texture`.
+    # Multi-draw scenes: [(first_tri, tri_count, Texture or None[, semantics
+    # [, tris_per_object]]), ...] drawn in order into one frame (one DrawModel*
+    # call each; semantics PRK_SEM_* / tris_per_object override the frame's);
+    # None = one draw of every triangle with `texture`.
     draws: Optional[list] = None
 
     @property
@@ -395,9 +395,11 @@ def sponza_like(width=3840, height=2160, seed=0, detail=1.56, tex_size=1024, fil
                  meta=dict(kind="sponza_like", seed=seed), draws=draws)
 
 
-def draw_spec(d, semantics):
-    """(first, count, texture, semantics) of a Scene.draws entry."""
-    return (d[0], d[1], d[2], d[3] if len(d) > 3 and d[3] is not None else semantics)
+def draw_spec(d, semantics, tris_per_object=1):
+    """(first, count, texture, semantics, tris_per_object) of a Scene.draws
+    entry (first, count, texture[, semantics[, tris_per_object]])."""
+    return (d[0], d[1], d[2], d[3] if len(d) > 3 and d[3] is not None else semantics,
+            d[4] if len(d) > 4 and d[4] is not None else tris_per_object)
 
 
 def with_ties(scene, frac=0.5, seed=0):

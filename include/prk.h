@@ -188,6 +188,52 @@ int prk_geometry_wrap_device(prk_context *ctx, const float *vertices, const floa
  * branch writes garbage (projekt.cpp:2285-2316). */
 int prk_draw(prk_context *ctx, int32_t geometry, uint32_t first_tri, uint32_t tri_count,
              const float P[3], int32_t semantics, int32_t phong, int32_t texture);
+/* The same draw as consecutive render_entry_3d_objects of `tris_per_object`
+ * triangles each (the last one may be smaller): every object is ONE active
+ * edge table, as FillEdgeTable + DrawModelOptimized(RenderQueue,...) build it
+ * (projekt.cpp:3894-4117, 3654-3869), so spans pair edges of different
+ * triangles of the object.  tris_per_object == 1 is prk_draw.  Objects of
+ * more than one triangle are supported for PRK_SEM_AVX / PRK_SEM_AVX_ST
+ * (PRK_ERR_UNSUPPORTED for PRK_SEM_SCALAR). */
+int prk_draw_objects(prk_context *ctx, int32_t geometry, uint32_t first_tri, uint32_t tri_count,
+                     uint32_t tris_per_object, const float P[3], int32_t semantics, int32_t phong,
+                     int32_t texture);
+
+/* edge_info (projekt.h:17-37) without its list pointer: what the reference's
+ * FillEdgeTable leaves in EdgeMemory and DrawModel* walk.  prk_draw_edges
+ * draws one object from such a list, already sorted by YMin as FillEdgeTable
+ * leaves it, exactly as DrawModelOptimized(RenderQueue,...) (3615-3871) or
+ * the single-thread overload (2350-3358) walks it.  Supported for
+ * PRK_SEM_AVX / PRK_SEM_AVX_ST; the winner id of its pixels is the draw's
+ * position in the frame's triangle numbering (it counts as one). */
+typedef struct prk_edge {
+    int32_t YMax;
+    float XMin, ZMin, OneOverZMin, Gradient, ZGradient, OneOverZGradient;
+    int32_t YMin;
+    float UMin, VMin, UGradient, VGradient;
+    int32_t Left;
+    float MinColor[4], ColorGradient[4], MinNormal[3], NormalGradient[3];
+} prk_edge;
+int prk_draw_edges(prk_context *ctx, const prk_edge *edges, uint32_t edge_count, int32_t semantics, int32_t phong,
+                   int32_t texture);
+
+/* One span end as line_render_work carries it by value (projekt.h:65-74) or
+ * thread_edge_info holds it (39-63): what FillLineOptimized /
+ * FillLinesOptimized read of an edge (1543-1835; 648-670). */
+typedef struct prk_span_end {
+    float XMin, ZMin, OneOverZMin, UMin, VMin;
+    float MinColor[4];
+    float MinNormal[3];
+} prk_span_end;
+typedef struct prk_span {
+    prk_span_end Left, Right;
+    int32_t Row;
+} prk_span;
+/* Draw caller-built spans (the work records DoLineRenderWork /
+ * DoBufferLineRenderWork run, 2336-2348), in order, each with
+ * FillLineOptimized's span body.  Each span counts as one triangle id. */
+int prk_draw_spans(prk_context *ctx, const prk_span *spans, uint32_t count, int32_t semantics, int32_t phong,
+                   int32_t texture);
 
 /* Execute every recorded draw, in submission order, into the bound target
  * (the reference's Platform.CompleteAllWork).  `stream` is a hipStream_t or

@@ -46,7 +46,7 @@ def lib():
             build()
         _LIB = C.CDLL(path)
         for fn in ("oracle_draw", "oracle_draw_band", "oracle_draw_mt",
-                   "oracle_fill_edge_table"):
+                   "oracle_fill_edge_table", "oracle_draw_edges", "oracle_draw_spans"):
             getattr(_LIB, fn).restype = C.c_int
     return _LIB
 
@@ -116,10 +116,10 @@ def render(scene, semantics=abi.PRK_SEM_AVX, phong=True, tris_per_object=1, thre
         from prk.scenes import draw_spec
         tot = [0, 0, 0]
         for d in scene.draws:
-            first, count, texture, sem = draw_spec(d, semantics)
+            first, count, texture, sem, tpo = draw_spec(d, semantics, tris_per_object)
             sub = scene.subset(first, first + count)
             sub.texture, sub.draws = texture, None
-            _, _, _, st = _render_one(sub, sem, phong, tris_per_object, threads, col, zb, win, rows,
+            _, _, _, st = _render_one(sub, sem, phong, tpo, threads, col, zb, win, rows,
                                       tri_base=first, cpu=cpu)
             tot = [tot[0] + st["spans"], tot[1] + st["span_pixels"], tot[2] + st["writes"]]
         return col, zb, win, dict(spans=tot[0], span_pixels=tot[1], writes=tot[2])
@@ -183,3 +183,44 @@ def fill_edge_table(scene, tri0=0, n=1, phong=True, semantics=abi.PRK_SEM_AVX):
                         ColorGradient=f[r, 17:21].copy(), MinNormal=f[r, 21:24].copy(),
                         NormalGradient=f[r, 24:27].copy()))
     return out
+
+
+def fill_edge_table_words(scene, tri0=0, n=1, phong=True, semantics=abi.PRK_SEM_AVX):
+    """FillEdgeTable (projekt.cpp:3882-4121) on triangles [tri0, tri0+n) as one
+    object: the sorted edges as uint32 words [count, 27] in prk_edge layout."""
+    k = _Keep(scene, semantics, phong, n)
+    words = np.zeros(27 * 3 * n + 27, np.uint32)
+    cnt = C.c_uint32(0)
+    rc = lib().oracle_fill_edge_table(C.byref(k.desc), C.c_uint32(tri0), C.c_uint32(n),
+                                      C.byref(k.transform), C.byref(k.lights), _ptr(words), C.byref(cnt))
+    if rc != 0:
+        raise RuntimeError("oracle_fill_edge_table failed: %d" % rc)
+    return words.reshape(-1, 27)[: cnt.value].copy()
+
+
+def _src_render(fn, scene, items, semantics, color, z, tri_index):
+    W, H = scene.width, scene.height
+    col = np.full((H, W), CLEAR_COLOR, np.uint32) if color is None else color
+    zb = np.full((H, W), CLEAR_Z, np.float32) if z is None else z
+    win = np.full((H, W), -1, np.int32)
+    k = _Keep(scene, semantics, True, 1)
+    tg = OrTarget(_ptr(col), W * 4, _ptr(zb), W, H, _ptr(win))
+    stats = (C.c_uint64 * 3)()
+    items = np.ascontiguousarray(items, np.uint32)
+    rc = fn(_ptr(items), C.c_uint32(items.shape[0]), C.c_int32(semantics), C.pointer(k.bitmap), C.c_int32(1),
+            C.c_int32(k.desc.Filter), C.c_int32(tri_index), C.byref(tg), C.byref(k.transform), C.byref(k.lights),
+            stats)
+    if rc != 0:
+        raise RuntimeError("oracle draw failed: %d" % rc)
+    return col, zb, win, dict(spans=stats[0], span_pixels=stats[1], writes=stats[2])
+
+
+def render_edges(scene, edge_words, semantics=abi.PRK_SEM_AVX, color=None, z=None, tri_index=0):
+    """DrawModelOptimized* of one ready edge list ([n, 27] prk_edge words)
+    with the scene's camera, lights and texture."""
+    return _src_render(lib().oracle_draw_edges, scene, edge_words, semantics, color, z, tri_index)
+
+
+def render_spans(scene, span_words, semantics=abi.PRK_SEM_AVX, color=None, z=None, tri_index=0):
+    """FillLineOptimized on caller spans ([n, 25] prk_span words)."""
+    return _src_render(lib().oracle_draw_spans, scene, span_words, semantics, color, z, tri_index)

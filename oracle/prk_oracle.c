@@ -976,3 +976,73 @@ int oracle_fill_edge_table(const or_draw_desc *D, uint32_t tri0, uint32_t n,
 }
 
 uint32_t oracle_edge_words(void) { return 27u; }
+
+/* ------------------------------------------------------------------ */
+/* Draws from a caller's edge list / span list (prk_draw_edges /       */
+/* prk_draw_spans): DrawModelOptimized* on a ready edge_info list      */
+/* (3615-3871: no sort, the insertion scan over every edge each row)   */
+/* and the work records of DoLineRenderWork / DoBufferLineRenderWork   */
+/* (2336-2348: FillLineOptimized / FillLinesOptimized on a pair).      */
+/* ------------------------------------------------------------------ */
+static void or_ctx_for(or_ctx *X_, int32_t semantics, const prk_bitmap *Bm, int32_t phong, int32_t filter,
+                       const or_target *Tg, const prk_transform *T, const prk_light_data *L)
+{
+    memset(X_, 0, sizeof *X_);
+    X_->T = T; X_->Lights = L; X_->Bitmap = Bm;
+    X_->Color = Tg->Color; X_->Pitch = Tg->Pitch; X_->Z = Tg->Z;
+    X_->Width = Tg->Width; X_->Height = Tg->Height; X_->Winners = Tg->Winners;
+    X_->RowLo = 0; X_->RowHi = Tg->Height; X_->Phong = phong; X_->Filter = filter;
+    X_->BandH = 1; X_->BandMod = 1; X_->BandRem = 0;
+    X_->St = semantics == PRK_SEM_AVX_ST;
+}
+
+int oracle_draw_edges(const prk_edge *E, uint32_t n, int32_t semantics, const prk_bitmap *Bm, int32_t phong,
+                      int32_t filter, int32_t tri_index, const or_target *Tg, const prk_transform *T,
+                      const prk_light_data *L, uint64_t *stats)
+{
+    if (semantics != PRK_SEM_AVX && semantics != PRK_SEM_AVX_ST) return PRK_ERR_UNSUPPORTED;
+    if (!Bm || !phong || (Tg->Width % 8)) return PRK_ERR_UNSUPPORTED;
+    or_edge *Edges = (or_edge *)calloc((size_t)n + 1, sizeof(or_edge));
+    if (!Edges) return PRK_ERR_NOMEM;
+    for (uint32_t i = 0; i < n; ++i) {
+        or_edge *o = Edges + i;
+        o->YMax = E[i].YMax; o->XMin = E[i].XMin; o->ZMin = E[i].ZMin; o->OneOverZMin = E[i].OneOverZMin;
+        o->Gradient = E[i].Gradient; o->ZGradient = E[i].ZGradient; o->OneOverZGradient = E[i].OneOverZGradient;
+        o->YMin = E[i].YMin; o->UMin = E[i].UMin; o->VMin = E[i].VMin; o->UGradient = E[i].UGradient;
+        o->VGradient = E[i].VGradient; o->Left = E[i].Left;
+        memcpy(o->MinColor, E[i].MinColor, 16); memcpy(o->ColorGradient, E[i].ColorGradient, 16);
+        memcpy(o->MinNormal, E[i].MinNormal, 12); memcpy(o->NormalGradient, E[i].NormalGradient, 12);
+        o->Next = NULL;
+    }
+    or_ctx X_;
+    or_ctx_for(&X_, semantics, Bm, phong, filter, Tg, T, L);
+    X_.TriIndex = tri_index;
+    or_aet_walk(&X_, Edges, n, or_fill_line_optimized);
+    free(Edges);
+    if (stats) { stats[0] += X_.Spans; stats[1] += X_.SpanPixels; stats[2] += X_.Writes; }
+    return PRK_OK;
+}
+
+int oracle_draw_spans(const prk_span *S, uint32_t n, int32_t semantics, const prk_bitmap *Bm, int32_t phong,
+                      int32_t filter, int32_t tri_index_base, const or_target *Tg, const prk_transform *T,
+                      const prk_light_data *L, uint64_t *stats)
+{
+    if (semantics != PRK_SEM_AVX && semantics != PRK_SEM_AVX_ST) return PRK_ERR_UNSUPPORTED;
+    if (!Bm || !phong || (Tg->Width % 8)) return PRK_ERR_UNSUPPORTED;
+    or_ctx X_;
+    or_ctx_for(&X_, semantics, Bm, phong, filter, Tg, T, L);
+    for (uint32_t k = 0; k < n; ++k) {
+        or_edge Le, Re; /* FillLinesOptimized 648-670: the pair's end points only */
+        memset(&Le, 0, sizeof Le);
+        memset(&Re, 0, sizeof Re);
+        const prk_span_end *a = &S[k].Left, *b = &S[k].Right;
+        Le.XMin = a->XMin; Le.ZMin = a->ZMin; Le.OneOverZMin = a->OneOverZMin; Le.UMin = a->UMin; Le.VMin = a->VMin;
+        memcpy(Le.MinColor, a->MinColor, 16); memcpy(Le.MinNormal, a->MinNormal, 12);
+        Re.XMin = b->XMin; Re.ZMin = b->ZMin; Re.OneOverZMin = b->OneOverZMin; Re.UMin = b->UMin; Re.VMin = b->VMin;
+        memcpy(Re.MinColor, b->MinColor, 16); memcpy(Re.MinNormal, b->MinNormal, 12);
+        X_.TriIndex = tri_index_base + (int32_t)k;
+        if (S[k].Row < Tg->Height) or_fill_line_optimized(&X_, &Le, &Re, S[k].Row);
+    }
+    if (stats) { stats[0] += X_.Spans; stats[1] += X_.SpanPixels; stats[2] += X_.Writes; }
+    return PRK_OK;
+}

@@ -44,9 +44,10 @@ def compare(g, o, exact_color=True, label=""):
 
 
 def run_both(scene, semantics=abi.PRK_SEM_AVX, phong=True, tile=None, threads=8, exact_color=True,
-             label=""):
-    o = O.render(scene, semantics=semantics, phong=phong, threads=threads)
-    g = prk.render_scene(scene, semantics=semantics, phong=phong, tile=tile)
+             label="", tris_per_object=1):
+    o = O.render(scene, semantics=semantics, phong=phong, threads=threads if tris_per_object == 1 else 1,
+                 tris_per_object=tris_per_object)
+    g = prk.render_scene(scene, semantics=semantics, phong=phong, tile=tile, tris_per_object=tris_per_object)
     compare(g, o, exact_color=exact_color, label=label or scene.name)
     return g, o
 
@@ -298,6 +299,112 @@ def test_mixed_tie_rules_with_scalar(gpu):
     s.draws = [(0, T // 3, s.texture, abi.PRK_SEM_AVX_ST), (T // 3, T // 3, None, abi.PRK_SEM_SCALAR),
                (2 * T // 3, T - 2 * (T // 3), s.texture, abi.PRK_SEM_AVX)]
     run_both(s, exact_color=True)
+
+
+def _sphere_scene(W=512, H=512):
+    V, Cc, N, UV = prk.construct_sphere()
+    base = scenes.random_soup(1, W, H, seed=0)
+    return scenes.Scene(W, H, V, Cc, N, UV, base.transform, scenes.LIGHTS_ONE, scenes.AMBIENT_ONE,
+                        base.texture, P=(0.0, 0.0, 2.0), name="sphere")
+
+
+@pytest.mark.parametrize("sem", [abi.PRK_SEM_AVX, abi.PRK_SEM_AVX_ST])
+def test_whole_object_construct_sphere(gpu, sem):
+    """ConstructSphere (projekt.cpp:4123-4289) submitted as ONE
+    render_entry_3d_object: one active edge table for all 2208 triangles, so
+    spans pair edges of different triangles (3654-3869), against the oracle's
+    whole-object walk.  Differs from the per-triangle image."""
+    s = _sphere_scene()
+    g, o = run_both(s, semantics=sem, tris_per_object=s.tri_count, threads=1)
+    per_tri = O.render(s, semantics=sem)
+    assert (g[1].view(np.uint32) != per_tri[1].view(np.uint32)).any()  # whole-object is really different
+    assert (g[2] >= 0).sum() > 10000
+
+
+@pytest.mark.parametrize("tpo,seed", [(2, 1), (5, 2), (16, 3)])
+def test_whole_object_random_objects(gpu, tpo, seed):
+    """Random objects of several triangles, clipped on every side, with ties:
+    spans across unrelated triangles, crossing swaps, expiry mid-list."""
+    s = scenes.with_ties(scenes.random_soup(3000, 256, 256, radius=30, seed=seed, centroid_margin=30), seed=seed)
+    run_both(s, tris_per_object=tpo)
+
+
+def test_whole_object_mixed_passes(gpu):
+    """Per-triangle and whole-object draws, queue and single-thread, in one
+    frame: the passes z-test against each other in submission order."""
+    s = scenes.with_ties(scenes.random_soup(4000, 256, 256, radius=20, seed=17), seed=8)
+    T = s.tri_count
+    q = T // 4
+    s.draws = [(0, q, s.texture, abi.PRK_SEM_AVX, 1), (q, q, s.texture, abi.PRK_SEM_AVX, 6),
+               (2 * q, q, s.texture, abi.PRK_SEM_AVX_ST, 1), (3 * q, T - 3 * q, s.texture, abi.PRK_SEM_AVX_ST, 3)]
+    run_both(s)
+
+
+def _render_src(scene, kind, words, semantics):
+    r = prk.Renderer()
+    try:
+        r.target_alloc(scene.width, scene.height)
+        r.clear()
+        r.set_debug(True)
+        r.set_camera(scene.prk_transform(), scene.prk_lights())
+        tex = r.texture(scene.texture)
+        (r.draw_edges if kind == "edges" else r.draw_spans)(words, semantics=semantics, bitmap=tex)
+        r.complete_all_work()
+        c, z = r.download()
+        return c, z, r.winners(), r.stats()
+    finally:
+        r.close()
+
+
+@pytest.mark.parametrize("sem", [abi.PRK_SEM_AVX, abi.PRK_SEM_AVX_ST])
+def test_draw_caller_edge_list(gpu, sem):
+    """DrawModelOptimized* on a ready edge_info list (prk_draw_edges): the
+    oracle's FillEdgeTable output of a 60-triangle object, drawn by the GPU's
+    AET walk, equals the oracle's walk of the same list."""
+    s = scenes.random_soup(60, 256, 256, radius=60, seed=43, textured=True, centroid_margin=40)
+    words = O.fill_edge_table_words(s, 0, 60)
+    compare(_render_src(s, "edges", words, sem), O.render_edges(s, words, semantics=sem), label="edges")
+
+
+@pytest.mark.parametrize("sem", [abi.PRK_SEM_AVX, abi.PRK_SEM_AVX_ST])
+def test_draw_caller_spans(gpu, sem):
+    """Caller-built spans (DoLineRenderWork / DoBufferLineRenderWork work
+    records, prk_draw_spans): random end points over every border, random
+    rows, overlapping spans with equal z."""
+    rng = np.random.default_rng(5)
+    s = scenes.random_soup(1, 256, 192, seed=0, textured=True)
+    n = 3000
+    w = np.zeros((n, 25), np.uint32)
+    f = w.view(np.float32)
+    x0 = rng.uniform(-40, 260, n)
+    x1 = x0 + rng.uniform(-5, 120, n)
+    for k, x in ((0, x0), (12, x1)):
+        zc = rng.uniform(-1, 1, n)
+        iz = 1.0 / (4.0 - zc)
+        f[:, k + 0] = x
+        f[:, k + 1] = zc
+        f[:, k + 2] = iz
+        f[:, k + 3] = rng.uniform(-0.1, 1.1, n) * iz
+        f[:, k + 4] = rng.uniform(-0.1, 1.1, n) * iz
+        f[:, k + 5:k + 9] = rng.uniform(0, 1, (n, 4))
+        nv = rng.normal(size=(n, 3))
+        f[:, k + 9:k + 12] = nv / np.linalg.norm(nv, axis=1, keepdims=True)
+    f[n // 2:, 1] = f[: n - n // 2, 1]  # repeat z: ties between spans
+    f[n // 2:, 13] = f[: n - n // 2, 13]
+    w[:, 24] = rng.integers(0, 192, n).astype(np.uint32)
+    compare(_render_src(s, "spans", w, sem), O.render_spans(s, w, semantics=sem), label="spans")
+
+
+def test_whole_object_scalar_unsupported(gpu):
+    s = scenes.random_soup(10, 64, 64, seed=0)
+    r = prk.Renderer()
+    try:
+        g = r.geometry(s.vertices, s.colors, s.normals, s.uvs)
+        with pytest.raises(prk.PrkError) as e:
+            r.draw(abi.PRK_SEM_SCALAR, g, 10, phong=False, tris_per_object=5)
+        assert e.value.code == abi.PRK_ERR_UNSUPPORTED
+    finally:
+        r.close()
 
 
 def test_unsupported_combinations(gpu):

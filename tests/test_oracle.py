@@ -264,3 +264,62 @@ def test_single_thread_overload_ties_and_left_clip():
     assert same(cs, pyref.render(c, abi.PRK_SEM_AVX_ST, True))
     zd = ca[1].view(np.uint32) != cs[1].view(np.uint32)
     assert zd.any() and zd[:, 0].any()  # the clipped column differs
+
+
+def test_edge_list_draw_equals_object_draw():
+    """FillEdgeTable + DrawModelOptimized composed: drawing an object's
+    exported edge list (oracle_draw_edges, the prk_draw_edges checker) gives
+    the object draw's frame exactly (whole-object AET)."""
+    s = scenes.random_soup(24, 96, 64, radius=30, seed=41, textured=True)
+    for sem in (abi.PRK_SEM_AVX, abi.PRK_SEM_AVX_ST):
+        ref = O.render(s, semantics=sem, tris_per_object=24)
+        words = O.fill_edge_table_words(s, 0, 24)
+        assert words.shape[0] > 30
+        got = O.render_edges(s, words, semantics=sem)
+        assert same(ref, got)
+
+
+def test_span_list_draw_equals_per_triangle_spans():
+    """A one-triangle draw is the spans its AET emits: the span list from the
+    walk (left/right end points per row, thread_edge_info, projekt.h:39-63)
+    drawn through oracle_draw_spans gives the same frame."""
+    s = scenes.random_soup(1, 64, 48, radius=18, seed=3, textured=True, centroid_margin=-20)
+    ref = O.render(s)
+    E = [dict(e) for e in O.fill_edge_table(s, 0, 1)]
+    spans = []
+    row, lst = E[0]["YMin"], []
+    def step(e):
+        e["XMin"] = np.float32(e["XMin"] + e["Gradient"]); e["ZMin"] = np.float32(e["ZMin"] + e["ZGradient"])
+        n = np.array(e["MinNormal"], np.float32) + np.array(e["NormalGradient"], np.float32)
+        inv = np.float32(1) / np.sqrt(np.float32((n[0] * n[0] + n[1] * n[1]) + n[2] * n[2]))
+        e["MinNormal"] = (inv * n).astype(np.float32)
+        e["UMin"] = np.float32(e["UMin"] + e["UGradient"]); e["VMin"] = np.float32(e["VMin"] + e["VGradient"])
+        e["OneOverZMin"] = np.float32(e["OneOverZMin"] + e["OneOverZGradient"])
+    maxy = min(max(e["YMax"] for e in E), s.height)
+    while row < maxy:
+        for e in E:
+            if e["YMin"] == row:
+                pos = len(lst)
+                for j, o in enumerate(lst):
+                    if (e["XMin"], e["Gradient"], e["Left"]) < (o["XMin"], o["Gradient"], o["Left"]):
+                        pos = j
+                        break
+                lst.insert(pos, e)
+        lst = [e for e in lst if not e["YMax"] <= row]
+        if len(lst) >= 2:
+            L, R = lst[0], lst[1]
+            w = np.zeros(25, np.uint32)
+            f = w.view(np.float32)
+            for k, ee in enumerate((L, R)):
+                o = 12 * k
+                f[o:o + 5] = [ee["XMin"], ee["ZMin"], ee["OneOverZMin"], ee["UMin"], ee["VMin"]]
+                f[o + 5:o + 9] = ee["MinColor"]
+                f[o + 9:o + 12] = ee["MinNormal"]
+            w[24] = row
+            spans.append(w)
+            step(L); step(R)
+            if L["XMin"] > R["XMin"]:
+                lst[0], lst[1] = R, L
+        row += 1
+    got = O.render_spans(s, np.stack(spans))
+    assert (got[1].view(np.uint32) == ref[1].view(np.uint32)).all() and (got[0] == ref[0]).all()
