@@ -87,6 +87,7 @@ struct DevBuf {
 struct Geometry {
     const float *V = nullptr, *C = nullptr, *N = nullptr, *UV = nullptr;
     uint32_t vertex_count = 0;
+    uint32_t cap_vertices = 0;  // owned buffers hold this many vertices
     bool owned = false;
 };
 
@@ -391,24 +392,82 @@ int prk_set_camera(prk_context *c, const prk_transform *t, const prk_light_data 
     return PRK_OK;
 }
 
+static bool bitmap_ok(const prk_bitmap *b) {
+    return b && b->Memory && b->Width > 0 && b->Height > 0 && b->Pitch >= 4 * b->Width && !(b->Pitch & 3);
+}
+
+// Copy the caller's Height rows (Pitch bytes each) into a texture holding
+// Height + 1 rows, the last one the zeroed guard row that the u == 1 / v == 1
+// over-read lands on: the caller's loaded_bitmap is read
+// exactly as the reference reads it (Memory, Width, Height, Pitch,
+// projekt.cpp:1506, 1881-1935) and never past its last row.
+static hipError_t texture_fill(const Texture &t, const prk_bitmap *b) {
+    hipError_t e = hipMemcpy(t.mem, b->Memory, (size_t)b->Pitch * b->Height, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(t.mem + (size_t)b->Pitch * b->Height, 0, (size_t)b->Pitch);
+    return e;
+}
+
 int prk_texture_create(prk_context *c, const prk_bitmap *b, int32_t *handle_out) {
-    if (!c || !b || !b->Memory || !handle_out || b->Width <= 0 || b->Height <= 0 || b->Pitch < 4 * b->Width ||
-        (b->Pitch & 3))
-        return PRK_ERR_ARG;
+    if (!c || !bitmap_ok(b) || !handle_out) return PRK_ERR_ARG;
     PRK_TRY(hipSetDevice(c->device));
     Texture t;
     t.w = b->Width;
     t.h = b->Height;
     t.pitch = b->Pitch;
-    size_t bytes = (size_t)b->Pitch * (b->Height + 1);
-    PRK_TRY(hipMalloc((void **)&t.mem, bytes));
-    hipError_t e = hipMemcpy(t.mem, b->Memory, bytes, hipMemcpyHostToDevice);
+    PRK_TRY(hipMalloc((void **)&t.mem, (size_t)b->Pitch * (b->Height + 1)));
+    hipError_t e = texture_fill(t, b);
     if (e != hipSuccess) {
         (void)hipFree(t.mem);
         return status_of(e);
     }
     *handle_out = (int32_t)c->texs.size();
     c->texs.push_back(t);
+    return PRK_OK;
+}
+
+int prk_texture_update(prk_context *c, int32_t handle, const prk_bitmap *b) {
+    if (!c || handle < 0 || (size_t)handle >= c->texs.size() || !bitmap_ok(b)) return PRK_ERR_ARG;
+    PRK_TRY(hipSetDevice(c->device));
+    Texture &t = c->texs[handle];
+    PRK_TRY(hipDeviceSynchronize());  // frames in flight may still sample it
+    if (t.w != b->Width || t.h != b->Height || t.pitch != b->Pitch) {
+        uint8_t *m = nullptr;
+        PRK_TRY(hipMalloc((void **)&m, (size_t)b->Pitch * (b->Height + 1)));
+        (void)hipFree(t.mem);
+        t.mem = m;
+        t.w = b->Width;
+        t.h = b->Height;
+        t.pitch = b->Pitch;
+    }
+    PRK_TRY(texture_fill(t, b));
+    return PRK_OK;
+}
+
+int prk_host_alloc(prk_context *c, size_t bytes, void **out) {
+    if (!c || !out) return PRK_ERR_ARG;
+    *out = nullptr;
+    PRK_TRY(hipSetDevice(c->device));
+    PRK_TRY(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+    return PRK_OK;
+}
+
+int prk_host_free(prk_context *c, void *p) {
+    if (!c) return PRK_ERR_ARG;
+    if (p) PRK_TRY(hipHostFree(p));
+    return PRK_OK;
+}
+
+int prk_host_register(prk_context *c, void *p, size_t bytes) {
+    if (!c || !p || !bytes) return PRK_ERR_ARG;
+    PRK_TRY(hipSetDevice(c->device));
+    PRK_TRY(hipHostRegister(p, bytes, hipHostRegisterDefault));
+    return PRK_OK;
+}
+
+int prk_host_unregister(prk_context *c, void *p) {
+    if (!c || !p) return PRK_ERR_ARG;
+    PRK_TRY(hipSetDevice(c->device));
+    PRK_TRY(hipHostUnregister(p));
     return PRK_OK;
 }
 
@@ -439,6 +498,7 @@ int prk_geometry_create(prk_context *c, const float *v, const float *col, const 
     PRK_TRY(hipSetDevice(c->device));
     Geometry g;
     g.vertex_count = vertex_count;
+    g.cap_vertices = vertex_count;
     g.owned = true;
     int rc = upload_array(v, (size_t)vertex_count * 3, &g.V);
     if (rc == PRK_OK) rc = upload_array(col, (size_t)vertex_count * 4, &g.C);
@@ -453,6 +513,41 @@ int prk_geometry_create(prk_context *c, const float *v, const float *col, const 
     }
     *handle_out = (int32_t)c->geoms.size();
     c->geoms.push_back(g);
+    return PRK_OK;
+}
+
+// Replace a library-owned geometry's contents (the reference re-reads
+// VertexData at every FillEdgeTable, projekt.cpp:3898-3925).  Buffers are kept
+// when large enough; frames in flight finish first.  Draws recorded before
+// the update read the new contents.
+int prk_geometry_update(prk_context *c, int32_t handle, const float *v, const float *col, const float *n,
+                        const float *uv, uint32_t vertex_count) {
+    if (!c || handle < 0 || (size_t)handle >= c->geoms.size() || !v || vertex_count % 3) return PRK_ERR_ARG;
+    Geometry &g = c->geoms[handle];
+    if (!g.owned) return PRK_ERR_ARG;
+    PRK_TRY(hipSetDevice(c->device));
+    PRK_TRY(hipDeviceSynchronize());
+    const float *src[4] = {v, col, n, uv};
+    const float **dst[4] = {&g.V, &g.C, &g.N, &g.UV};
+    const size_t comp[4] = {3, 4, 3, 2};
+    for (int k = 0; k < 4; ++k) {
+        const size_t bytes = (size_t)vertex_count * comp[k] * sizeof(float);
+        if (!src[k]) continue;
+        if (!*dst[k] || vertex_count > g.cap_vertices) {
+            float *d = nullptr;
+            PRK_TRY(hipMalloc((void **)&d, bytes ? bytes : 4));
+            (void)hipFree((void *)*dst[k]);
+            *dst[k] = d;
+        }
+        PRK_TRY(hipMemcpy((void *)*dst[k], src[k], bytes, hipMemcpyHostToDevice));
+    }
+    g.vertex_count = vertex_count;
+    g.cap_vertices = std::max(g.cap_vertices, vertex_count);
+    // recorded draws carry the geometry's device pointers: refresh them
+    for (auto &d : c->draws)
+        if (d.src_kind == 0 && d.geom == handle) {
+            d.V = g.V; d.C = g.C; d.N = g.N; d.UV = g.UV;
+        }
     return PRK_OK;
 }
 
@@ -506,11 +601,31 @@ int prk_draw_objects(prk_context *c, int32_t geometry, uint32_t first_tri, uint3
     if (tris_per_object > 1 && mode != prk::MODE_AVX) return PRK_ERR_UNSUPPORTED;
     if (tri_count == 0) return PRK_OK;
     if ((uint64_t)c->pending_tris + tri_count >= 0xFFFFFFF0ull) return PRK_ERR_ARG;
+    // A draw that continues the previous one (same geometry, the next
+    // triangles, same object offset, semantics, texture and object size, the
+    // previous one ending on an object boundary) extends it: per-object AETs
+    // in submission order are unchanged, and a caller submitting one object
+    // per call (the reference's render_entry_3d_object pattern) yields a few
+    // draws per frame instead of one per triangle.
+    if (!c->draws.empty()) {
+        prk::DrawRec &b = c->draws.back();
+        const float p0 = P ? P[0] : 0.0f, p1 = P ? P[1] : 0.0f, p2 = P ? P[2] : 0.0f;
+        if (b.src_kind == 0 && b.geom == geometry && b.geom_tri0 + b.tri_count == first_tri && b.mode == mode &&
+            b.flags == flags && b.tex == texture && b.obj_tris == tris_per_object &&
+            b.tri_count % tris_per_object == 0 && b.P[0] == p0 && b.P[1] == p1 && b.P[2] == p2 &&
+            std::signbit(b.P[0]) == std::signbit(p0) && std::signbit(b.P[1]) == std::signbit(p1) &&
+            std::signbit(b.P[2]) == std::signbit(p2)) {
+            b.tri_count += tri_count;
+            c->pending_tris += tri_count;
+            return PRK_OK;
+        }
+    }
     prk::DrawRec d{};
     d.V = g.V;
     d.C = g.C;
     d.N = g.N;
     d.UV = g.UV;
+    d.geom = geometry;
     d.geom_tri0 = first_tri;
     d.first_global = c->pending_tris;
     d.tri_count = tri_count;

@@ -40,6 +40,7 @@ struct DrawRec {
                                   // > 1: one AET per object, drawn through the span path)
     uint32_t src_kind;            // 0: geometry; 1: a caller's edge list; 2: caller spans (span path)
     uint32_t src_off, src_n;      // kind 1/2: range of the flush's edge / span input
+    int32_t geom;                 // host: the geometry handle (draw coalescing, geometry updates)
 };
 
 // Draw flags.  DRAW_ST: the single-thread overload DrawModelOptimized(Buffer,

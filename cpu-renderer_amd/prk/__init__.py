@@ -52,6 +52,13 @@ _SIGS = {
     "prk_set_camera": (C.c_int, [C.c_void_p, C.POINTER(abi.PrkTransform), C.POINTER(abi.PrkLightData)]),
     "prk_texture_create": (C.c_int, [C.c_void_p, C.POINTER(abi.PrkBitmap), C.POINTER(C.c_int32)]),
     "prk_texture_set_filter": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+    "prk_texture_update": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(abi.PrkBitmap)]),
+    "prk_geometry_update": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_uint32]),
+    "prk_host_alloc": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
+    "prk_host_free": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "prk_host_register": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    "prk_host_unregister": (C.c_int, [C.c_void_p, C.c_void_p]),
     "prk_geometry_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_uint32, C.POINTER(C.c_int32)]),
     "prk_geometry_wrap_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -202,6 +209,18 @@ class Renderer:
         if getattr(tex, "filter", abi.PRK_FILTER_NEAREST) != abi.PRK_FILTER_NEAREST:
             self.set_filter(h.value, tex.filter)
         return h.value
+
+    def texture_update(self, handle, tex):
+        """Re-read a texture's bitmap into `handle` (prk_texture_update)."""
+        texels = np.ascontiguousarray(tex.texels, np.uint32)
+        bm = abi.PrkBitmap(texels.ctypes.data, tex.width, tex.height, texels.shape[1] * 4)
+        _check("prk_texture_update", self._L.prk_texture_update(self._h, handle, C.byref(bm)))
+
+    def geometry_update(self, handle, vertices, colors=None, normals=None, uvs=None):
+        arrs = [None if a is None else np.ascontiguousarray(a, np.float32)
+                for a in (vertices, colors, normals, uvs)]
+        _check("prk_geometry_update", self._L.prk_geometry_update(self._h, handle, *[_ptr(a) for a in arrs],
+                                                                  arrs[0].shape[0]))
 
     def set_filter(self, texture, filt):
         """Texture sampling: PRK_FILTER_NEAREST (the reference's) or

@@ -27,6 +27,7 @@
 #ifndef PRK_H
 #define PRK_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -160,13 +161,26 @@ int prk_target_download(prk_context *ctx, uint32_t *color_host, int32_t host_pit
 int prk_target_upload(prk_context *ctx, const uint32_t *color_host, int32_t host_pitch_bytes,
                       const float *z_host);
 
+/* Pinned host memory for staging (prk_host_alloc / prk_host_free), and
+ * page-locking of caller memory (a framebuffer, a z-buffer) so uploads and
+ * downloads run as DMA at full PCIe rate. */
+int prk_host_alloc(prk_context *ctx, size_t bytes, void **out);
+int prk_host_free(prk_context *ctx, void *p);
+int prk_host_register(prk_context *ctx, void *p, size_t bytes);
+int prk_host_unregister(prk_context *ctx, void *p);
+
 /* Camera and lights (game_render_commands::Transform / LightData). */
 int prk_set_camera(prk_context *ctx, const prk_transform *transform,
                    const prk_light_data *lights);
 
-/* Textures.  `bitmap->Memory` is host memory of (Height+1)*Pitch bytes, the
- * last row being the guard row (zero it).  Returns a handle >= 0. */
+/* Textures.  `bitmap->Memory` is host memory of Height rows of Pitch bytes
+ * (loaded_bitmap as the reference reads it, projekt.cpp:1506, 1881-1935); the
+ * library appends the zeroed guard row the u == 1 / v == 1 over-read lands
+ * on and never reads past the caller's last row.
+ * Returns a handle >= 0.  prk_texture_update re-reads a bitmap into a handle
+ * (the drop-in refreshes every texture once per frame). */
 int prk_texture_create(prk_context *ctx, const prk_bitmap *bitmap, int32_t *handle_out);
+int prk_texture_update(prk_context *ctx, int32_t handle, const prk_bitmap *bitmap);
 int prk_texture_set_filter(prk_context *ctx, int32_t handle, int32_t filter);  /* PRK_FILTER_* */
 
 /* Geometry: non-indexed SoA vertex arrays exactly as render_entry_3d_object
@@ -175,7 +189,12 @@ int prk_texture_set_filter(prk_context *ctx, int32_t handle, int32_t filter);  /
 int prk_geometry_create(prk_context *ctx, const float *vertices, const float *colors,
                         const float *normals, const float *uvs, uint32_t vertex_count,
                         int32_t *handle_out);
-/* Same, but from device pointers the caller keeps alive (no copy). */
+/* New contents for a library-owned geometry (grows its buffers if needed);
+ * draws already recorded read the new contents. */
+int prk_geometry_update(prk_context *ctx, int32_t handle, const float *vertices, const float *colors,
+                        const float *normals, const float *uvs, uint32_t vertex_count);
+/* Same as prk_geometry_create, but from device pointers the caller keeps
+ * alive (no copy). */
 int prk_geometry_wrap_device(prk_context *ctx, const float *vertices, const float *colors,
                              const float *normals, const float *uvs, uint32_t vertex_count,
                              int32_t *handle_out);

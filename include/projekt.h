@@ -4,28 +4,47 @@
 //
 // A caller of the reference keeps its code:
 //
-//     u32 EdgeCount = FillEdgeTable(Object, Commands, Phong);          // projekt.cpp:3882
+//     u32 EdgeCount = FillEdgeTable(Object, Commands, Phong);                  // projekt.cpp:3882
 //     DrawModelOptimized(RenderQueue, Buffer, (edge_info *)Object->EdgeMemory,
-//                        EdgeCount, Commands, Bitmap, Phong);          // projekt.cpp:3615
-//     ... or DrawModel(Buffer, Edges, EdgeCount, Commands, Bitmap, Phong);   // 162
+//                        EdgeCount, Commands, Bitmap, Phong);                  // 3615
+//     ... or DrawModelOptimizedLines(RenderQueue, Buffer, Edges, ...)         // 3362
+//     ... or DrawModelOptimized(Buffer, Edges, EdgeCount, Commands, ...)      // 2350 (single thread)
+//     ... or DrawModel(Buffer, Edges, EdgeCount, Commands, Bitmap, Phong)     // 162
+//     ... work records run through DoLineRenderWork / DoBufferLineRenderWork /
+//         DoModelRenderWork (2336, 2343, 3873)
 //     Platform.CompleteAllWork(RenderQueue)  ->  PRK_CompleteAllWork(Buffer, Commands)
 //
-// and links libprk_hip.so.  Differences from the reference, all deliberate:
-//  * FillEdgeTable does not build a CPU edge list: it registers the object
-//    (geometry is uploaded to HBM once per VertexData pointer) and leaves a
-//    token in Object->EdgeMemory that DrawModel* reads back.  It returns the
-//    reference's upper bound 3*T (a non-zero EdgeCount).
-//  * Every triangle is its own active edge table ("per-triangle
-//    submission").  For objects of one triangle this is exactly
-//    the reference; for multi-triangle objects the reference pairs edges of
-//    different triangles into one AET, which DESIGN.md §2 lists as not yet
-//    emulated.
-//  * Work runs on the GPU at PRK_CompleteAllWork (the reference's
-//    CompleteAllWork point), which downloads colour and z into Buffer->Memory
-//    and Commands->ZBuffer.  The prior contents of both are uploaded at the
-//    first draw of a frame, so draws still z-test against them.
+// and links libprk_hip.so.  What each entry point does here:
+//  * FillEdgeTable copies the object's VertexData / ColorData / NormalData /
+//    UVData as they are at the call (the reference reads them there,
+//    3898-3925) into the frame's pinned staging arena, and leaves a token in
+//    Object->EdgeMemory that DrawModel* read back; the setup itself
+//    (projection, cull, edges, MergeSort) runs on the GPU at
+//    PRK_CompleteAllWork.  It returns 3*T, the reference's upper bound on the
+//    edge count (non-zero for any object with a triangle).
+//  * DrawModelOptimized(RenderQueue, ...) and DrawModelOptimizedLines draw
+//    the object with FillLineOptimized semantics (FillLinesOptimized has the
+//    same block math); DrawModelOptimized(Buffer, ...) with the
+//    single-thread overload's quirks (PRK_SEM_AVX_ST); DrawModel with the
+//    scalar semantics.  An object of several triangles is ONE active edge
+//    table, as in the reference (prk_draw_objects); DrawModel's scalar
+//    whole-object AET is not emulated and is drawn per triangle.
+//  * DrawModel* given edges that are NOT a FillEdgeTable token (a caller's
+//    own edge_info list, e.g. built by the reference's FillEdgeTable) draw
+//    that list as is (prk_draw_edges).  The work-queue callbacks draw the
+//    spans of their work records (prk_draw_spans) or, for DoModelRenderWork,
+//    the object (single-thread overload).
+//  * PRK_CompleteAllWork (the absent platform's CompleteAllWork) uploads the
+//    frame's geometry, runs every recorded draw in order on the GPU and copies
+//    colour and z back into Buffer->Memory and Commands->ZBuffer.  The device
+//    target is allocated once per size; the caller's framebuffer and z-buffer
+//    are page-locked once, so the prior contents go up (draws z-test against
+//    them) and the result comes down as DMA.  PRK_ClearNextFrame(color, z)
+//    replaces that upload by a clear fused into the frame's kernels.
+//  * Textures (loaded_bitmap) are read at their first use in each frame.
+//  * One camera and light set per frame (the last draw's Commands).
 //  * Inputs the reference crashes on are rejected or pinned, see
-//    prk.h.
+//    prk.h; PRK_LastStatus() reports the last library status.
 //
 // The caller-owned types of the reference live in its absent platform and
 // math headers.  If the caller has them, define PRK_CALLER_TYPES before
@@ -38,7 +57,8 @@
 #include <string.h>
 
 #include <map>
-#include <utility>
+#include <set>
+#include <vector>
 
 #include "prk.h"
 
@@ -84,7 +104,11 @@ struct game_render_commands { // fields as used at projekt.cpp:170-171, 452-458,
 struct platform_work_queue;
 #endif  // PRK_CALLER_TYPES
 
-// The reference's own structs (projekt.h:2-37), field for field.
+#ifndef PLATFORM_WORK_QUEUE_CALLBACK
+#define PLATFORM_WORK_QUEUE_CALLBACK(name) void name(platform_work_queue *Queue, void *Data)
+#endif
+
+// The reference's own structs (projekt.h:2-98), field for field.
 struct render_entry_3d_object {
     v3 P;
     u32 VertexCount;
@@ -109,43 +133,156 @@ struct edge_info {
     edge_info *Next;
 };
 
+struct thread_edge_info {
+    r32 LeftXMin, RightXMin;
+    r32 LeftZMin, RightZMin;
+    r32 LeftOneOverZMin, RightOneOverZMin;
+    r32 LeftUMin, RightUMin;
+    r32 LeftVMin, RightVMin;
+    v4 LeftMinColor, RightMinColor;
+    v3 LeftMinNormal, RightMinNormal;
+};
+
+struct line_render_work {
+    game_render_commands *Commands;
+    loaded_bitmap *OutputTarget;
+    loaded_bitmap *Bitmap;
+    edge_info CurrentEdgeInList;
+    edge_info NextEdgeInList;
+    s32 RowIndex;
+    b32 PhongShading;
+};
+
+struct buffer_line_render_work {
+    game_render_commands *Commands;
+    loaded_bitmap *OutputTarget;
+    loaded_bitmap *Bitmap;
+    s32 RowIndex;
+    b32 PhongShading;
+    u32 EdgeCount;
+    u32 Pad;
+    thread_edge_info Edges;  // the first of EdgeCount (3604-3607)
+};
+
+struct model_render_work {
+    game_render_commands *Commands;
+    loaded_bitmap *OutputTarget;
+    loaded_bitmap *Bitmap;
+    edge_info *EdgeMemory;
+    u32 EdgeCount;
+    b32 PhongShading;
+};
+
 namespace prk_dropin {
 
 // Token FillEdgeTable leaves in Object->EdgeMemory for DrawModel*.
 struct object_token {
     uint32_t Magic;
-    int32_t Geometry;
+    uint32_t Frame;    // frame serial the object was filled in
+    uint32_t Object;   // index into the frame's object table
     uint32_t TriCount;
-    int32_t Phong;
-    float P[3];
-    int32_t Texture;
 };
 static_assert(sizeof(object_token) <= sizeof(edge_info), "token must fit one edge_info");
-static const uint32_t kMagic = 0x4B525031u;  // "PRK1"
+static const uint32_t kMagic = 0x4B525032u;  // "PRK2"
+
+struct frame_object {
+    uint32_t FirstTri, Tris;
+    float P[3];
+};
+
+enum { DRAW_OBJECT = 0, DRAW_EDGES = 1, DRAW_SPANS = 2 };
+struct pending_draw {
+    int Kind;
+    uint32_t First, Count;  // object index / range of Edges / range of Spans
+    int32_t Semantics, Phong, Texture;
+};
 
 struct state {
     prk_context *Ctx = nullptr;
     int LastStatus = PRK_OK;
-    std::map<const void *, std::pair<int32_t, uint32_t>> Geometry;  // VertexData -> (handle, vertices)
-    std::map<const void *, int32_t> Textures;                       // Bitmap->Memory -> handle
+    // frame geometry: pinned staging arena (vertices), uploaded at CompleteAllWork
+    float *AV = nullptr, *AC = nullptr, *AN = nullptr, *AUV = nullptr;
+    uint32_t ArenaCap = 0, ArenaUsed = 0;  // vertices
+    int32_t Geom = -1;
+    std::vector<frame_object> Objects;
+    std::vector<pending_draw> Draws;
+    std::vector<prk_edge> Edges;
+    std::vector<prk_span> Spans;
+    std::map<const void *, int32_t> Textures;  // Bitmap->Memory -> handle
+    std::set<int32_t> TexFresh;                // handles re-read this frame
+    std::map<void *, size_t> Registered;       // page-locked caller buffers
     loaded_bitmap *Target = nullptr;
     game_render_commands *Commands = nullptr;
+    int32_t TW = 0, TH = 0;                    // device target size
     bool FrameOpen = false;
+    uint32_t Frame = 1;
+    bool ClearNext = false;
+    uint32_t ClearColor = 0;
+    float ClearZ = 0.0f;
 };
 inline state &S() {
     static state s;
     return s;
 }
 
+inline bool ok(int rc) {
+    S().LastStatus = rc;
+    return rc == PRK_OK;
+}
+
+inline void free_arena(state &st) {
+    prk_host_free(st.Ctx, st.AV);
+    prk_host_free(st.Ctx, st.AC);
+    prk_host_free(st.Ctx, st.AN);
+    prk_host_free(st.Ctx, st.AUV);
+    st.AV = st.AC = st.AN = st.AUV = nullptr;
+    st.ArenaCap = 0;
+}
+
+// Room for `more` vertices in the pinned arena (grows by doubling).
+inline bool arena_reserve(state &st, uint32_t more) {
+    const uint64_t need = (uint64_t)st.ArenaUsed + more;
+    if (need <= st.ArenaCap) return true;
+    if (need > 0xFFFFFFF0ull) return ok(PRK_ERR_ARG);
+    uint64_t cap = st.ArenaCap ? st.ArenaCap : 3u * 4096u;
+    while (cap < need) cap *= 2;
+    if (cap > 0xFFFFFFF0ull) cap = need;
+    void *p[4] = {nullptr, nullptr, nullptr, nullptr};
+    const size_t comp[4] = {3, 4, 3, 2};
+    for (int k = 0; k < 4; ++k)
+        if (!ok(prk_host_alloc(st.Ctx, (size_t)cap * comp[k] * sizeof(float), &p[k]))) {
+            for (int j = 0; j < k; ++j) prk_host_free(st.Ctx, p[j]);
+            return false;
+        }
+    float *old[4] = {st.AV, st.AC, st.AN, st.AUV};
+    for (int k = 0; k < 4; ++k)
+        if (old[k]) memcpy(p[k], old[k], (size_t)st.ArenaUsed * comp[k] * sizeof(float));
+    free_arena(st);
+    st.AV = (float *)p[0];
+    st.AC = (float *)p[1];
+    st.AN = (float *)p[2];
+    st.AUV = (float *)p[3];
+    st.ArenaCap = (uint32_t)cap;
+    return true;
+}
+
+// The bitmap as it is now: created on first use, re-read once per frame.
 inline int32_t texture_for(loaded_bitmap *Bitmap) {
     if (!Bitmap || !Bitmap->Memory) return -1;
     state &st = S();
-    auto it = st.Textures.find(Bitmap->Memory);
-    if (it != st.Textures.end()) return it->second;
     prk_bitmap b = {Bitmap->Memory, Bitmap->Width, Bitmap->Height, Bitmap->Pitch};
+    auto it = st.Textures.find(Bitmap->Memory);
+    if (it != st.Textures.end()) {
+        if (!st.TexFresh.count(it->second)) {
+            if (!ok(prk_texture_update(st.Ctx, it->second, &b))) return -1;
+            st.TexFresh.insert(it->second);
+        }
+        return it->second;
+    }
     int32_t h = -1;
-    st.LastStatus = prk_texture_create(st.Ctx, &b, &h);  // needs the zeroed guard row (prk.h)
-    if (st.LastStatus == PRK_OK) st.Textures[Bitmap->Memory] = h;
+    if (!ok(prk_texture_create(st.Ctx, &b, &h))) return -1;
+    st.Textures[Bitmap->Memory] = h;
+    st.TexFresh.insert(h);
     return h;
 }
 
@@ -164,35 +301,147 @@ inline void set_camera(game_render_commands *Commands) {
         for (int c = 0; c < 3; ++c) l.Lights[i].P[c] = Commands->LightData.Lights[i].P.E[c];
         for (int c = 0; c < 4; ++c) l.Lights[i].Intensity[c] = Commands->LightData.Lights[i].Intensity.E[c];
     }
-    S().LastStatus = prk_set_camera(S().Ctx, &t, &l);
+    ok(prk_set_camera(S().Ctx, &t, &l));
 }
 
-// First draw of a frame: bind a device target of the Buffer's size and upload
-// the caller's current colour and z (draws z-test against them).
+inline void register_host(state &st, void *p, size_t bytes) {
+    auto it = st.Registered.find(p);
+    if (it != st.Registered.end()) {
+        if (it->second >= bytes) return;
+        prk_host_unregister(st.Ctx, p);
+        st.Registered.erase(it);
+    }
+    // best effort: unregistered memory still works, through staging copies
+    if (prk_host_register(st.Ctx, p, bytes) == PRK_OK) st.Registered[p] = bytes;
+}
+
+// First draw of a frame: the device target (reallocated only when the size
+// changes) takes the caller's current colour and z, so draws z-test against
+// them; PRK_ClearNextFrame replaces that upload by a fused clear.
 inline bool open_frame(loaded_bitmap *Buffer, game_render_commands *Commands) {
     state &st = S();
-    if (st.FrameOpen && st.Target == Buffer && st.Commands == Commands) return true;
-    st.LastStatus = prk_target_alloc(st.Ctx, Buffer->Width, Buffer->Height, 0, Buffer->Height, nullptr, nullptr);
-    if (st.LastStatus != PRK_OK) return false;
-    st.LastStatus = prk_target_upload(st.Ctx, (const uint32_t *)Buffer->Memory, Buffer->Pitch, Commands->ZBuffer);
-    if (st.LastStatus != PRK_OK) return false;
+    if (st.FrameOpen) {
+        if (st.Target == Buffer && st.Commands == Commands) return true;
+        return ok(PRK_ERR_ARG);  // one target per frame: CompleteAllWork first
+    }
+    if (!Buffer || !Commands || !Buffer->Memory || Buffer->Width <= 0 || Buffer->Height <= 0 ||
+        (Commands->Width != (u32)Buffer->Width))  // z rows are Commands->Width floats (170, 1511)
+        return ok(PRK_ERR_ARG);
+    if (Buffer->Width != st.TW || Buffer->Height != st.TH) {
+        if (!ok(prk_target_alloc(st.Ctx, Buffer->Width, Buffer->Height, 0, Buffer->Height, nullptr, nullptr)))
+            return false;
+        st.TW = Buffer->Width;
+        st.TH = Buffer->Height;
+    }
+    register_host(st, Buffer->Memory, (size_t)Buffer->Pitch * Buffer->Height);
+    if (Commands->ZBuffer) register_host(st, Commands->ZBuffer, (size_t)Buffer->Width * Buffer->Height * 4);
+    if (st.ClearNext) {
+        if (!ok(prk_target_clear_on_flush(st.Ctx, st.ClearColor, st.ClearZ))) return false;
+        st.ClearNext = false;
+    } else if (!ok(prk_target_upload(st.Ctx, (const uint32_t *)Buffer->Memory, Buffer->Pitch, Commands->ZBuffer))) {
+        return false;
+    }
     st.Target = Buffer;
     st.Commands = Commands;
     st.FrameOpen = true;
     return true;
 }
 
+inline void edge_in(prk_edge &o, const edge_info &e) {
+    o.YMax = e.YMax; o.XMin = e.XMin; o.ZMin = e.ZMin; o.OneOverZMin = e.OneOverZMin; o.Gradient = e.Gradient;
+    o.ZGradient = e.ZGradient; o.OneOverZGradient = e.OneOverZGradient; o.YMin = e.YMin; o.UMin = e.UMin;
+    o.VMin = e.VMin; o.UGradient = e.UGradient; o.VGradient = e.VGradient; o.Left = e.Left;
+    for (int c = 0; c < 4; ++c) { o.MinColor[c] = e.MinColor.E[c]; o.ColorGradient[c] = e.ColorGradient.E[c]; }
+    for (int c = 0; c < 3; ++c) { o.MinNormal[c] = e.MinNormal.E[c]; o.NormalGradient[c] = e.NormalGradient.E[c]; }
+}
+
+inline void span_end(prk_span_end &o, const edge_info &e) {  // line_render_work's edges by value
+    o.XMin = e.XMin; o.ZMin = e.ZMin; o.OneOverZMin = e.OneOverZMin; o.UMin = e.UMin; o.VMin = e.VMin;
+    for (int c = 0; c < 4; ++c) o.MinColor[c] = e.MinColor.E[c];
+    for (int c = 0; c < 3; ++c) o.MinNormal[c] = e.MinNormal.E[c];
+}
+
 inline void draw(loaded_bitmap *Buffer, edge_info *Edges, u32 EdgeCount, game_render_commands *Commands,
                  loaded_bitmap *Bitmap, b32 PhongShading, int32_t semantics) {
     state &st = S();
     if (!st.Ctx || !Edges || EdgeCount == 0) return;  // 0 edges: nothing to draw (P1)
-    object_token tok;
-    memcpy(&tok, Edges, sizeof tok);
-    if (tok.Magic != kMagic) { st.LastStatus = PRK_ERR_ARG; return; }
     if (!open_frame(Buffer, Commands)) return;
     set_camera(Commands);
-    int32_t tex = Bitmap ? texture_for(Bitmap) : -1;
-    st.LastStatus = prk_draw(st.Ctx, tok.Geometry, 0, tok.TriCount, tok.P, semantics, PhongShading ? 1 : 0, tex);
+    const int32_t tex = Bitmap ? texture_for(Bitmap) : -1;
+    object_token tok;
+    memcpy(&tok, Edges, sizeof tok);
+    pending_draw d;
+    d.Semantics = semantics;
+    d.Phong = PhongShading ? 1 : 0;
+    d.Texture = tex;
+    if (tok.Magic == kMagic && tok.Frame == st.Frame && tok.Object < st.Objects.size()) {
+        d.Kind = DRAW_OBJECT;
+        d.First = tok.Object;
+        d.Count = 1;
+    } else {  // a caller's own edge_info list, drawn as given
+        d.Kind = DRAW_EDGES;
+        d.First = (uint32_t)st.Edges.size();
+        d.Count = EdgeCount;
+        st.Edges.resize(st.Edges.size() + EdgeCount);
+        for (u32 i = 0; i < EdgeCount; ++i) edge_in(st.Edges[d.First + i], Edges[i]);
+    }
+    st.Draws.push_back(d);
+    st.LastStatus = PRK_OK;
+}
+
+inline void draw_spans(loaded_bitmap *Buffer, game_render_commands *Commands, loaded_bitmap *Bitmap,
+                       b32 PhongShading, const prk_span *spans, uint32_t n) {
+    state &st = S();
+    if (!st.Ctx || n == 0) return;
+    if (!open_frame(Buffer, Commands)) return;
+    set_camera(Commands);
+    pending_draw d;
+    d.Kind = DRAW_SPANS;
+    d.First = (uint32_t)st.Spans.size();
+    d.Count = n;
+    d.Semantics = PRK_SEM_AVX;
+    d.Phong = PhongShading ? 1 : 0;
+    d.Texture = Bitmap ? texture_for(Bitmap) : -1;
+    st.Spans.insert(st.Spans.end(), spans, spans + n);
+    st.Draws.push_back(d);
+}
+
+// Records the frame's draws with the library, in order.
+inline int issue(state &st) {
+    int rc = PRK_OK;
+    if (st.ArenaUsed) {
+        rc = st.Geom < 0 ? prk_geometry_create(st.Ctx, st.AV, st.AC, st.AN, st.AUV, st.ArenaUsed, &st.Geom)
+                         : prk_geometry_update(st.Ctx, st.Geom, st.AV, st.AC, st.AN, st.AUV, st.ArenaUsed);
+        if (rc != PRK_OK) return rc;
+    }
+    for (const pending_draw &d : st.Draws) {
+        if (d.Kind == DRAW_OBJECT) {
+            const frame_object &o = st.Objects[d.First];
+            rc = prk_draw_objects(st.Ctx, st.Geom, o.FirstTri, o.Tris, o.Tris, o.P, d.Semantics, d.Phong, d.Texture);
+            if (rc == PRK_ERR_UNSUPPORTED && d.Semantics == PRK_SEM_SCALAR && o.Tris > 1)
+                // DrawModel's scalar whole-object AET is not emulated: per triangle
+                rc = prk_draw_objects(st.Ctx, st.Geom, o.FirstTri, o.Tris, 1, o.P, d.Semantics, d.Phong, d.Texture);
+        } else if (d.Kind == DRAW_EDGES) {
+            rc = prk_draw_edges(st.Ctx, st.Edges.data() + d.First, d.Count, d.Semantics, d.Phong, d.Texture);
+        } else {
+            rc = prk_draw_spans(st.Ctx, st.Spans.data() + d.First, d.Count, d.Semantics, d.Phong, d.Texture);
+        }
+        if (rc != PRK_OK) return rc;
+    }
+    return rc;
+}
+
+inline void end_frame(state &st) {
+    st.ArenaUsed = 0;
+    st.Objects.clear();
+    st.Draws.clear();
+    st.Edges.clear();
+    st.Spans.clear();
+    st.TexFresh.clear();
+    st.FrameOpen = false;
+    st.Target = nullptr;
+    st.Commands = nullptr;
+    ++st.Frame;
 }
 
 }  // namespace prk_dropin
@@ -207,17 +456,32 @@ inline int PRK_Init(int device) {
 inline int PRK_LastStatus() { return prk_dropin::S().LastStatus; }
 inline void PRK_Shutdown() {
     prk_dropin::state &st = prk_dropin::S();
-    if (st.Ctx) prk_destroy(st.Ctx);
+    if (st.Ctx) {
+        prk_synchronize(st.Ctx);
+        for (auto &r : st.Registered) prk_host_unregister(st.Ctx, r.first);
+        prk_dropin::free_arena(st);
+        prk_destroy(st.Ctx);
+    }
     st = prk_dropin::state();
+}
+// Extension: the next frame starts from (color, z) instead of the caller's
+// buffers (no upload; the clear is fused into the frame's kernels).
+inline void PRK_ClearNextFrame(uint32_t color, float z) {
+    prk_dropin::state &st = prk_dropin::S();
+    st.ClearNext = true;
+    st.ClearColor = color;
+    st.ClearZ = z;
 }
 // Platform.CompleteAllWork equivalent: run the frame, copy colour and z back.
 inline int PRK_CompleteAllWork(loaded_bitmap *Buffer, game_render_commands *Commands) {
     prk_dropin::state &st = prk_dropin::S();
     if (!st.Ctx || !st.FrameOpen) return PRK_OK;
-    int rc = prk_flush(st.Ctx, nullptr);
+    int rc = prk_dropin::issue(st);
+    if (rc == PRK_OK) rc = prk_flush(st.Ctx, nullptr);
+    else prk_reset_draws(st.Ctx);
     if (rc == PRK_OK)
         rc = prk_target_download(st.Ctx, (uint32_t *)Buffer->Memory, Buffer->Pitch, Commands->ZBuffer);
-    st.FrameOpen = false;
+    prk_dropin::end_frame(st);
     st.LastStatus = rc;
     return rc;
 }
@@ -226,29 +490,32 @@ inline int PRK_CompleteAllWork(loaded_bitmap *Buffer, game_render_commands *Comm
 // projekt.cpp:3882-4121
 inline u32 FillEdgeTable(render_entry_3d_object *Object, game_render_commands *Commands, b32 PhongShading = 0) {
     (void)Commands;
+    (void)PhongShading;  // the semantics travel with the DrawModel* call
     prk_dropin::state &st = prk_dropin::S();
-    if (!st.Ctx || !Object || !Object->EdgeMemory || Object->VertexCount < 3) return 0;
-    const u32 T = Object->VertexCount / 3;
-    auto it = st.Geometry.find(Object->VertexData);
-    int32_t g = -1;
-    if (it != st.Geometry.end() && it->second.second == Object->VertexCount) {
-        g = it->second.first;
-    } else {
-        st.LastStatus = prk_geometry_create(st.Ctx, (const float *)Object->VertexData,
-                                            (const float *)Object->ColorData, (const float *)Object->NormalData,
-                                            (const float *)Object->UVData, T * 3, &g);
-        if (st.LastStatus != PRK_OK) return 0;
-        st.Geometry[Object->VertexData] = std::make_pair(g, Object->VertexCount);
-    }
+    if (!st.Ctx || !Object || !Object->EdgeMemory || !Object->VertexData || Object->VertexCount < 3) return 0;
+    const u32 T = Object->VertexCount / 3, nv = 3 * T;
+    if (!prk_dropin::arena_reserve(st, nv)) return 0;
+    const uint32_t v0 = st.ArenaUsed;
+    memcpy(st.AV + 3 * (size_t)v0, Object->VertexData, (size_t)nv * 12);
+    if (Object->ColorData) memcpy(st.AC + 4 * (size_t)v0, Object->ColorData, (size_t)nv * 16);
+    else memset(st.AC + 4 * (size_t)v0, 0, (size_t)nv * 16);
+    if (Object->NormalData) memcpy(st.AN + 3 * (size_t)v0, Object->NormalData, (size_t)nv * 12);
+    else memset(st.AN + 3 * (size_t)v0, 0, (size_t)nv * 12);
+    if (Object->UVData) memcpy(st.AUV + 2 * (size_t)v0, Object->UVData, (size_t)nv * 8);
+    else memset(st.AUV + 2 * (size_t)v0, 0, (size_t)nv * 8);
+    st.ArenaUsed += nv;
+    prk_dropin::frame_object o;
+    o.FirstTri = v0 / 3;
+    o.Tris = T;
+    o.P[0] = Object->P.x;
+    o.P[1] = Object->P.y;
+    o.P[2] = Object->P.z;
     prk_dropin::object_token tok;
     tok.Magic = prk_dropin::kMagic;
-    tok.Geometry = g;
+    tok.Frame = st.Frame;
+    tok.Object = (uint32_t)st.Objects.size();
     tok.TriCount = T;
-    tok.Phong = PhongShading ? 1 : 0;
-    tok.P[0] = Object->P.x;
-    tok.P[1] = Object->P.y;
-    tok.P[2] = Object->P.z;
-    tok.Texture = -1;
+    st.Objects.push_back(o);
     memcpy(Object->EdgeMemory, &tok, sizeof tok);
     return 3 * T;
 }
@@ -261,10 +528,64 @@ inline void DrawModelOptimized(platform_work_queue *RenderQueue, loaded_bitmap *
     prk_dropin::draw(Buffer, Edges, EdgeCount, Commands, Bitmap, PhongShading, PRK_SEM_AVX);
 }
 
+// projekt.cpp:3362-3613 (+ FillLinesOptimized 629-1490: FillLineOptimized's block math)
+inline void DrawModelOptimizedLines(platform_work_queue *RenderQueue, loaded_bitmap *Buffer, edge_info *Edges,
+                                    u32 EdgeCount, game_render_commands *Commands, loaded_bitmap *Bitmap = 0,
+                                    b32 PhongShading = 0) {
+    (void)RenderQueue;
+    prk_dropin::draw(Buffer, Edges, EdgeCount, Commands, Bitmap, PhongShading, PRK_SEM_AVX);
+}
+
+// projekt.cpp:2350-3358, the single-thread overload
+inline void DrawModelOptimized(loaded_bitmap *Buffer, edge_info *Edges, u32 EdgeCount, game_render_commands *Commands,
+                               loaded_bitmap *Bitmap = 0, b32 PhongShading = 0) {
+    prk_dropin::draw(Buffer, Edges, EdgeCount, Commands, Bitmap, PhongShading, PRK_SEM_AVX_ST);
+}
+
 // projekt.cpp:162-601
 inline void DrawModel(loaded_bitmap *Buffer, edge_info *Edges, u32 EdgeCount, game_render_commands *Commands,
                       loaded_bitmap *Bitmap = 0, b32 PhongShading = 0) {
     prk_dropin::draw(Buffer, Edges, EdgeCount, Commands, Bitmap, PhongShading, PRK_SEM_SCALAR);
+}
+
+// projekt.cpp:2336-2341: one span of a line_render_work
+inline PLATFORM_WORK_QUEUE_CALLBACK(DoLineRenderWork) {
+    (void)Queue;
+    line_render_work *Work = (line_render_work *)Data;
+    prk_span sp;
+    prk_dropin::span_end(sp.Left, Work->CurrentEdgeInList);
+    prk_dropin::span_end(sp.Right, Work->NextEdgeInList);
+    sp.Row = Work->RowIndex;
+    prk_dropin::draw_spans(Work->OutputTarget, Work->Commands, Work->Bitmap, Work->PhongShading, &sp, 1);
+}
+
+// projekt.cpp:2343-2348: the spans of one row (FillLinesOptimized 629-1490)
+inline PLATFORM_WORK_QUEUE_CALLBACK(DoBufferLineRenderWork) {
+    (void)Queue;
+    buffer_line_render_work *Work = (buffer_line_render_work *)Data;
+    const thread_edge_info *E = &Work->Edges;
+    std::vector<prk_span> sp(Work->EdgeCount);
+    for (u32 k = 0; k < Work->EdgeCount; ++k) {  // 648-670
+        prk_span &s = sp[k];
+        s.Left.XMin = E[k].LeftXMin; s.Right.XMin = E[k].RightXMin;
+        s.Left.ZMin = E[k].LeftZMin; s.Right.ZMin = E[k].RightZMin;
+        s.Left.OneOverZMin = E[k].LeftOneOverZMin; s.Right.OneOverZMin = E[k].RightOneOverZMin;
+        s.Left.UMin = E[k].LeftUMin; s.Right.UMin = E[k].RightUMin;
+        s.Left.VMin = E[k].LeftVMin; s.Right.VMin = E[k].RightVMin;
+        for (int c = 0; c < 4; ++c) { s.Left.MinColor[c] = E[k].LeftMinColor.E[c]; s.Right.MinColor[c] = E[k].RightMinColor.E[c]; }
+        for (int c = 0; c < 3; ++c) { s.Left.MinNormal[c] = E[k].LeftMinNormal.E[c]; s.Right.MinNormal[c] = E[k].RightMinNormal.E[c]; }
+        s.Row = Work->RowIndex;
+    }
+    prk_dropin::draw_spans(Work->OutputTarget, Work->Commands, Work->Bitmap, Work->PhongShading, sp.data(),
+                           (uint32_t)sp.size());
+}
+
+// projekt.cpp:3873-3878: a whole object through the single-thread overload
+inline PLATFORM_WORK_QUEUE_CALLBACK(DoModelRenderWork) {
+    (void)Queue;
+    model_render_work *Work = (model_render_work *)Data;
+    DrawModelOptimized(Work->OutputTarget, Work->EdgeMemory, Work->EdgeCount, Work->Commands, Work->Bitmap,
+                       Work->PhongShading);
 }
 
 // The reference's test mesh (projekt.cpp:4123-4289).

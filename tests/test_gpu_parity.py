@@ -453,11 +453,26 @@ def test_gpu_matches_golden_fixtures(gpu, path):
             label=os.path.basename(path))
 
 
-@pytest.mark.parametrize("scalar", [False, True])
-def test_dropin_demo_matches_oracle(gpu, tmp_path, scalar):
+def _dropin_scene(textured=True, salt=0):
+    V, Cc, N, UV = prk.construct_sphere()
+    tex = np.zeros((65, 64), np.uint32)
+    y, x = np.mgrid[0:64, 0:64]
+    tex[:64] = np.where(((x ^ y) & 8) != 0, 0xFFE0C080, 0xFF4060A0).astype(np.uint32) ^ np.uint32(salt * 0x00102030)
+    return scenes.Scene(256, 256, V.copy(), Cc, N.copy(), UV, scenes.default_camera(256, 256), scenes.LIGHTS_ONE,
+                        scenes.AMBIENT_ONE, scenes.Texture(tex, 64, 64) if textured else None, P=(0.0, 0.0, 2.0))
+
+
+DROPIN_MODES = ["queue", "lines", "st", "scalar", "object", "mutate", "edges", "work"]
+
+
+@pytest.mark.parametrize("mode", DROPIN_MODES)
+def test_dropin_demo_matches_oracle(gpu, tmp_path, mode):
     """examples/dropin_demo.cpp drives the reference's own entry points
-    (FillEdgeTable / DrawModelOptimized / DrawModel through include/projekt.h)
-    on ConstructSphere; its framebuffer must equal the oracle's."""
+    through include/projekt.h (FillEdgeTable, DrawModelOptimized(RenderQueue),
+    DrawModelOptimizedLines, the single-thread DrawModelOptimized, DrawModel,
+    the three work-queue callbacks, a caller-built edge list, vertices and a
+    texture rewritten in place between frames; its texture ends at an
+    inaccessible page).  Its framebuffer must equal the oracle's."""
     import os
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -468,22 +483,60 @@ def test_dropin_demo_matches_oracle(gpu, tmp_path, scalar):
                         "-Wl,-rpath," + os.path.join(root, "cpu-renderer_amd"), "-o", str(exe)],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
-    args = [str(exe), str(tmp_path / "c.u32"), str(tmp_path / "z.f32")] + (["scalar"] if scalar else [])
+    s = _dropin_scene(textured=mode != "scalar")
+    T = s.tri_count
+    extra = []
+    if mode == "edges":
+        words = O.fill_edge_table_words(s, 0, T)
+        words.tofile(tmp_path / "edges.u32")
+        extra = [str(tmp_path / "edges.u32")]
+    if mode == "work":
+        rng = np.random.default_rng(2)
+        n = 400
+        w = np.zeros((n, 25), np.uint32)
+        f = w.view(np.float32)
+        x0 = rng.uniform(-20, 250, n)
+        for k, x in ((0, x0), (12, x0 + rng.uniform(0, 60, n))):
+            zc = rng.uniform(-1, 1, n)
+            f[:, k] = x
+            f[:, k + 1] = zc
+            f[:, k + 2] = 1.0 / (4.0 - zc)
+            f[:, k + 3] = rng.uniform(0, 1, n) * f[:, k + 2]
+            f[:, k + 4] = rng.uniform(0, 1, n) * f[:, k + 2]
+            f[:, k + 5:k + 9] = rng.uniform(0, 1, (n, 4))
+            nv = rng.normal(size=(n, 3))
+            f[:, k + 9:k + 12] = nv / np.linalg.norm(nv, axis=1, keepdims=True)
+        w[:, 24] = np.sort(rng.integers(0, 256, n)).astype(np.uint32)
+        w.tofile(tmp_path / "spans.u32")
+        extra = [str(tmp_path / "spans.u32")]
+    args = [str(exe), str(tmp_path / "c.u32"), str(tmp_path / "z.f32"), mode] + extra
     run = subprocess.run(args, capture_output=True, text=True, timeout=120)
     assert run.returncode == 0, run.stderr
     gc = np.fromfile(tmp_path / "c.u32", np.uint32).reshape(256, 256)
     gz = np.fromfile(tmp_path / "z.f32", np.float32).reshape(256, 256)
-    V, Cc, N, UV = prk.construct_sphere()
-    tex = np.zeros((65, 64), np.uint32)
-    y, x = np.mgrid[0:64, 0:64]
-    tex[:64] = np.where(((x ^ y) & 8) != 0, 0xFFE0C080, 0xFF4060A0).astype(np.uint32)
-    s = scenes.Scene(256, 256, V, Cc, N, UV, scenes.default_camera(256, 256), scenes.LIGHTS_ONE,
-                     scenes.AMBIENT_ONE, None if scalar else scenes.Texture(tex, 64, 64), P=(0.0, 0.0, 2.0))
-    sem = abi.PRK_SEM_SCALAR if scalar else abi.PRK_SEM_AVX
-    oc, oz, ow, _ = O.render(s, semantics=sem, phong=not scalar)
-    assert (gz.view(np.uint32) == oz.view(np.uint32)).all()
-    assert (gc == oc).all()
-    assert (ow >= 0).sum() > 2000
+    if mode in ("queue", "lines"):
+        oc, oz, _, _ = O.render(s)
+    elif mode == "st":
+        oc, oz, _, _ = O.render(s, semantics=abi.PRK_SEM_AVX_ST)
+    elif mode == "scalar":
+        oc, oz, _, _ = O.render(s, semantics=abi.PRK_SEM_SCALAR, phong=False)
+    elif mode == "object":
+        oc, oz, _, _ = O.render(s, tris_per_object=T)
+    elif mode == "mutate":
+        m = _dropin_scene(salt=1)
+        m.vertices[:, 0] = m.vertices[:, 0] * np.float32(0.75) + np.float32(0.125)
+        m.vertices[:, 1] = m.vertices[:, 1] * np.float32(1.25) - np.float32(0.0625)
+        m.normals[:, 2] = -m.normals[:, 2]
+        oc, oz, _, _ = O.render(m)
+    elif mode == "edges":
+        oc, oz, _, _ = O.render_edges(s, words)
+    else:  # work
+        oc, oz, _, _ = O.render_spans(s, w[: n // 2])
+        oc, oz, _, _ = O.render_spans(s, w[n // 2:], color=oc, z=oz)
+        oc, oz, _, _ = O.render(s, semantics=abi.PRK_SEM_AVX_ST, tris_per_object=T, color=oc, z=oz)
+    assert (gz.view(np.uint32) == oz.view(np.uint32)).all(), mode
+    assert (gc == oc).all(), mode
+    assert (gz > -3e38).sum() > 2000
 
 
 @pytest.mark.parametrize("semantics,phong,textured", [(abi.PRK_SEM_SCALAR, False, False),
