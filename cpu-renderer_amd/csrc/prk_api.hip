@@ -87,7 +87,7 @@ struct DevBuf {
 struct Geometry {
     const float *V = nullptr, *C = nullptr, *N = nullptr, *UV = nullptr;
     uint32_t vertex_count = 0;
-    uint32_t cap_vertices = 0;  // owned buffers hold this many vertices
+    uint32_t cap[4] = {0, 0, 0, 0};  // owned V / C / N / UV buffers hold this many vertices
     bool owned = false;
 };
 
@@ -498,7 +498,7 @@ int prk_geometry_create(prk_context *c, const float *v, const float *col, const 
     PRK_TRY(hipSetDevice(c->device));
     Geometry g;
     g.vertex_count = vertex_count;
-    g.cap_vertices = vertex_count;
+    for (int k = 0; k < 4; ++k) g.cap[k] = vertex_count;
     g.owned = true;
     int rc = upload_array(v, (size_t)vertex_count * 3, &g.V);
     if (rc == PRK_OK) rc = upload_array(col, (size_t)vertex_count * 4, &g.C);
@@ -530,19 +530,19 @@ int prk_geometry_update(prk_context *c, int32_t handle, const float *v, const fl
     const float *src[4] = {v, col, n, uv};
     const float **dst[4] = {&g.V, &g.C, &g.N, &g.UV};
     const size_t comp[4] = {3, 4, 3, 2};
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 4; ++k) {  // an array passed as null keeps its previous contents
         const size_t bytes = (size_t)vertex_count * comp[k] * sizeof(float);
         if (!src[k]) continue;
-        if (!*dst[k] || vertex_count > g.cap_vertices) {
+        if (!*dst[k] || vertex_count > g.cap[k]) {
             float *d = nullptr;
             PRK_TRY(hipMalloc((void **)&d, bytes ? bytes : 4));
             (void)hipFree((void *)*dst[k]);
             *dst[k] = d;
+            g.cap[k] = vertex_count;
         }
         PRK_TRY(hipMemcpy((void *)*dst[k], src[k], bytes, hipMemcpyHostToDevice));
     }
     g.vertex_count = vertex_count;
-    g.cap_vertices = std::max(g.cap_vertices, vertex_count);
     // recorded draws carry the geometry's device pointers: refresh them
     for (auto &d : c->draws)
         if (d.src_kind == 0 && d.geom == handle) {

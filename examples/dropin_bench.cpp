@@ -1,0 +1,140 @@
+// dropin_bench.cpp — the headline workload (C3b: 4096 x 4096, 1M random
+// triangles with offsets of +-16 px, Phong + 256^2 texture, one light) driven
+// the way a reference caller drives it: every triangle its own
+// render_entry_3d_object through FillEdgeTable + DrawModelOptimized(RenderQueue,
+// ...) of include/projekt.h, then PRK_CompleteAllWork, frame after frame.
+//
+// Per frame it reports the host time of the 1M FillEdgeTable + DrawModel
+// calls (vertex snapshot into the pinned arena), the time of
+// PRK_CompleteAllWork (geometry upload over PCIe, the GPU frame, colour + z
+// download into the caller's buffers), and the GPU kernels' own time.  Two
+// modes: "upload" (the generic drop-in: the caller's framebuffer and z-buffer
+// go up as the frame's prior contents) and "clear" (PRK_ClearNextFrame: the
+// caller clears, the clear is fused into the GPU frame instead of uploaded).
+// The scene is generated here with std::mt19937 (same distribution as
+// prk.scenes.random_soup, not the same numbers).
+//
+// usage: dropin_bench [frames] [triangles] [width]
+#include <chrono>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "projekt.h"
+
+using clk = std::chrono::steady_clock;
+static double ms_since(clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); }
+
+int main(int argc, char **argv) {
+    const int frames = argc > 1 ? std::atoi(argv[1]) : 5;
+    const u32 T = argc > 2 ? (u32)std::atoi(argv[2]) : 1000000u;
+    const s32 W = argc > 3 ? std::atoi(argv[3]) : 4096, H = W;
+    if (PRK_Init(0) != PRK_OK) {
+        std::fprintf(stderr, "dropin_bench: no HIP device (status %d)\n", PRK_LastStatus());
+        return 2;
+    }
+    // camera of prk.scenes: D = 4, F = 1, M2P = W/2, C = (W/2, H/2)
+    const float D = 4.0f, M2P = W / 2.0f, cx = W / 2.0f, cy = H / 2.0f, R = 16.0f;
+    std::mt19937 rng(2024);
+    std::uniform_real_distribution<float> U01(0.0f, 1.0f);
+    std::vector<v3> V(3 * (size_t)T), N(3 * (size_t)T);
+    std::vector<v4> C(3 * (size_t)T);
+    std::vector<v2> UV(3 * (size_t)T);
+    for (u32 t = 0; t < T; ++t) {
+        const float ccx = -R + (W + 2 * R) * U01(rng), ccy = -R + (H + 2 * R) * U01(rng);
+        float sx[3], sy[3];
+        for (int k = 0; k < 3; ++k) {
+            sx[k] = ccx + (2 * U01(rng) - 1) * R;
+            sy[k] = ccy + (2 * U01(rng) - 1) * R;
+        }
+        if ((sx[1] - sx[0]) * (sy[2] - sy[0]) - (sy[1] - sy[0]) * (sx[2] - sx[0]) > 0) {  // front-facing winding
+            std::swap(sx[1], sx[2]);
+            std::swap(sy[1], sy[2]);
+        }
+        const float z0 = 2 * U01(rng) - 1;
+        for (int k = 0; k < 3; ++k) {
+            const float z = z0 + (2 * U01(rng) - 1) * 0.15f;
+            const size_t i = 3 * (size_t)t + k;
+            V[i] = {{(sx[k] - cx) * (D - z) / M2P, (sy[k] - cy) * (D - z) / M2P, z}};
+            float nx = 2 * U01(rng) - 1, ny = 2 * U01(rng) - 1, nz = 2 * U01(rng) - 1;
+            const float l = std::sqrt(nx * nx + ny * ny + nz * nz) + 1e-6f;
+            N[i] = {{nx / l, ny / l, nz / l}};
+            C[i] = {{U01(rng), U01(rng), U01(rng), 1.0f}};
+            UV[i] = {{U01(rng), U01(rng)}};
+        }
+    }
+    std::vector<u32> texels(256 * 256);
+    for (auto &x : texels) x = (u32)rng();
+    loaded_bitmap Texture = {texels.data(), 256, 256, 256 * 4};
+    std::vector<u32> pixels((size_t)W * H);
+    std::vector<r32> zbuf((size_t)W * H);
+    loaded_bitmap Buffer = {pixels.data(), W, H, W * 4};
+    game_render_commands Commands = {};
+    Commands.ZBuffer = zbuf.data();
+    Commands.Width = (u32)W;
+    Commands.Transform.DistanceAboveTarget = D;
+    Commands.Transform.FocalLength = 1.0f;
+    Commands.Transform.MetersToPixels = M2P;
+    Commands.Transform.ScreenCenter.x = cx;
+    Commands.Transform.ScreenCenter.y = cy;
+    Commands.LightData.LightCount = 1;
+    Commands.LightData.Lights[0].P = {{1.0f, 1.0f, 3.0f}};
+    Commands.LightData.Lights[0].Intensity = {{0.8f, 0.8f, 0.8f, 1.0f}};
+    Commands.LightData.AmbientIntensity = {{0.2f, 0.2f, 0.2f, 1.0f}};
+    std::vector<edge_info> EdgeMemory(3);
+
+    std::printf("{\"workload\": \"C3b through include/projekt.h: %u per-triangle objects, %dx%d\", \"modes\": {", T, W, H);
+    for (int m = 0; m < 2; ++m) {
+        const bool clear = m == 1;
+        double calls = 0, complete = 0, total = 0, gpu = 0;
+        int timed = 0;
+        for (int f = 0; f < frames + 1; ++f) {
+            // the caller's own clear of its buffers (both modes: the reference caller does it)
+            const auto t0 = clk::now();
+            std::fill(pixels.begin(), pixels.end(), 0xFF000000u);
+            std::fill(zbuf.begin(), zbuf.end(), -FLT_MAX);
+            if (clear) PRK_ClearNextFrame(0xFF000000u, -FLT_MAX);
+            prk_timing_reset(prk_dropin::S().Ctx);
+            const auto t1 = clk::now();
+            for (u32 t = 0; t < T; ++t) {
+                render_entry_3d_object Object = {};
+                Object.VertexCount = 3;
+                Object.PhongShading = 1;
+                Object.VertexData = &V[3 * (size_t)t];
+                Object.ColorData = &C[3 * (size_t)t];
+                Object.NormalData = &N[3 * (size_t)t];
+                Object.UVData = &UV[3 * (size_t)t];
+                Object.EdgeMemory = EdgeMemory.data();
+                Object.Bitmap = &Texture;
+                const u32 n = FillEdgeTable(&Object, &Commands, 1);
+                DrawModelOptimized(nullptr, &Buffer, EdgeMemory.data(), n, &Commands, &Texture, 1);
+            }
+            const double tc = ms_since(t1);
+            const auto t2 = clk::now();
+            if (PRK_CompleteAllWork(&Buffer, &Commands) != PRK_OK) {
+                std::fprintf(stderr, "dropin_bench: CompleteAllWork failed (status %d)\n", PRK_LastStatus());
+                return 2;
+            }
+            const double tw = ms_since(t2), tt = ms_since(t0);
+            prk_stats st;
+            prk_get_stats(prk_dropin::S().Ctx, &st);
+            if (f > 0) {  // frame 0 warms up (allocations, page locking)
+                calls += tc;
+                complete += tw;
+                total += tt;
+                gpu += st.frames_timed ? (st.sum_ms_raster + st.sum_ms_bin) / st.frames_timed : 0.0;
+                ++timed;
+            }
+        }
+        std::printf("%s\"%s\": {\"frame_ms\": %.3f, \"host_calls_ms\": %.3f, \"complete_all_work_ms\": %.3f, "
+                    "\"gpu_bin_plus_raster_ms\": %.3f, \"mpixels_s\": %.1f}",
+                    m ? ", " : "", clear ? "clear" : "upload", total / timed, calls / timed, complete / timed,
+                    gpu / timed, (double)W * H / (total / timed * 1e-3) / 1e6);
+    }
+    std::printf("}, \"frames\": %d}\n", frames);
+    PRK_Shutdown();
+    return 0;
+}

@@ -190,7 +190,8 @@ int prk_geometry_create(prk_context *ctx, const float *vertices, const float *co
                         const float *normals, const float *uvs, uint32_t vertex_count,
                         int32_t *handle_out);
 /* New contents for a library-owned geometry (grows its buffers if needed);
- * draws already recorded read the new contents. */
+ * an array passed as NULL keeps its previous contents (and must not be read
+ * past them); draws already recorded read the new contents. */
 int prk_geometry_update(prk_context *ctx, int32_t handle, const float *vertices, const float *colors,
                         const float *normals, const float *uvs, uint32_t vertex_count);
 /* Same as prk_geometry_create, but from device pointers the caller keeps

@@ -42,7 +42,8 @@
 //    them) and the result comes down as DMA.  PRK_ClearNextFrame(color, z)
 //    replaces that upload by a clear fused into the frame's kernels.
 //  * Textures (loaded_bitmap) are read at their first use in each frame.
-//  * One camera and light set per frame (the last draw's Commands).
+//  * One camera and light set per frame: the Commands of the frame's draws as
+//    they are at PRK_CompleteAllWork.
 //  * Inputs the reference crashes on are rejected or pinned, see
 //    prk.h; PRK_LastStatus() reports the last library status.
 //
@@ -219,6 +220,9 @@ struct state {
     bool ClearNext = false;
     uint32_t ClearColor = 0;
     float ClearZ = 0.0f;
+    loaded_bitmap *LastBitmap = nullptr;        // texture of the previous draw this frame
+    void *LastBitmapMemory = nullptr;
+    int32_t LastTexture = -1;
 };
 inline state &S() {
     static state s;
@@ -366,8 +370,16 @@ inline void draw(loaded_bitmap *Buffer, edge_info *Edges, u32 EdgeCount, game_re
     state &st = S();
     if (!st.Ctx || !Edges || EdgeCount == 0) return;  // 0 edges: nothing to draw (P1)
     if (!open_frame(Buffer, Commands)) return;
-    set_camera(Commands);
-    const int32_t tex = Bitmap ? texture_for(Bitmap) : -1;
+    int32_t tex = -1;
+    if (Bitmap) {  // the same bitmap as the previous draw: its handle, already fresh this frame
+        if (Bitmap == st.LastBitmap && Bitmap->Memory == st.LastBitmapMemory) tex = st.LastTexture;
+        else {
+            tex = texture_for(Bitmap);
+            st.LastBitmap = Bitmap;
+            st.LastBitmapMemory = Bitmap->Memory;
+            st.LastTexture = tex;
+        }
+    }
     object_token tok;
     memcpy(&tok, Edges, sizeof tok);
     pending_draw d;
@@ -394,7 +406,6 @@ inline void draw_spans(loaded_bitmap *Buffer, game_render_commands *Commands, lo
     state &st = S();
     if (!st.Ctx || n == 0) return;
     if (!open_frame(Buffer, Commands)) return;
-    set_camera(Commands);
     pending_draw d;
     d.Kind = DRAW_SPANS;
     d.First = (uint32_t)st.Spans.size();
@@ -406,12 +417,20 @@ inline void draw_spans(loaded_bitmap *Buffer, game_render_commands *Commands, lo
     st.Draws.push_back(d);
 }
 
-// Records the frame's draws with the library, in order.
+// Records the frame's draws with the library, in order, with the frame's
+// camera and lights (the Commands of its draws).
 inline int issue(state &st) {
     int rc = PRK_OK;
+    set_camera(st.Commands);
+    if (st.LastStatus != PRK_OK) return st.LastStatus;
     if (st.ArenaUsed) {
+        // vertex colours reach the output only through DrawModel (scalar); the
+        // FillLineOptimized paths replace them by the texel (2029-2032)
+        bool colors = st.Geom < 0;
+        for (const pending_draw &d : st.Draws) colors |= d.Kind == DRAW_OBJECT && d.Semantics == PRK_SEM_SCALAR;
         rc = st.Geom < 0 ? prk_geometry_create(st.Ctx, st.AV, st.AC, st.AN, st.AUV, st.ArenaUsed, &st.Geom)
-                         : prk_geometry_update(st.Ctx, st.Geom, st.AV, st.AC, st.AN, st.AUV, st.ArenaUsed);
+                         : prk_geometry_update(st.Ctx, st.Geom, st.AV, colors ? st.AC : nullptr, st.AN, st.AUV,
+                                               st.ArenaUsed);
         if (rc != PRK_OK) return rc;
     }
     for (const pending_draw &d : st.Draws) {
@@ -432,6 +451,9 @@ inline int issue(state &st) {
 }
 
 inline void end_frame(state &st) {
+    st.LastBitmap = nullptr;
+    st.LastBitmapMemory = nullptr;
+    st.LastTexture = -1;
     st.ArenaUsed = 0;
     st.Objects.clear();
     st.Draws.clear();
