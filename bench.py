@@ -111,8 +111,8 @@ def cpu_topology():
 def cpu_baseline(scene, threads, max_tris, frames=3, scan=(16, 64)):
     """The CPU path on the same scene, on the host cores (SURVEY §8(d) "CPU
     path timing"): the AVX2 restatement (oracle/prk_cpu_avx.c, bit-exact to
-    the scalar oracle) on `threads` = every CPU of this process's affinity
-    mask, under three schedules:
+    the scalar oracle), scanned up to `threads` = every CPU of this process's
+    affinity mask, under three schedules:
       banded  row bands per thread, no locks (median of `frames` full frames
               after one warm-up);
       queue   the reference's DrawModelOptimized(RenderQueue,...): a producer
@@ -121,8 +121,10 @@ def cpu_baseline(scene, threads, max_tris, frames=3, scan=(16, 64)):
       rows    DrawModelOptimizedLines + FillLinesOptimized: one task per row
               of an object (projekt.cpp:3362-3613, 629-1490).
     queue / rows are timed on a bounded sample (the scene's first triangles)
-    and scaled to the scene.  `value` is the fastest schedule at `threads`;
-    `scan` has the banded schedule at fewer threads for context."""
+    and scaled to the scene.  The banded schedule runs at every count of
+    `scan`, the cgroup CPU quota and `threads`; `value` is the fastest
+    schedule at the fastest count (on the GPU box the cgroup quota is 16 CPUs
+    of 256, and 256 threads run slower than 64)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from prk import abi
@@ -151,30 +153,37 @@ def cpu_baseline(scene, threads, max_tris, frames=3, scan=(16, 64)):
 
     n = min(T, max_tris)
     sub = scene if n == T else scene.subset(0, n)
-    fb, st = timed(sub, "banded", threads, frames)
-    fb *= T / n
-    variants = {"banded": {"threads": threads, "frame_ms": fb * 1e3, "mpixels_s": px / fb / 1e6,
+    # banded thread scan: 16, 64, the cgroup CPU quota (the box's share of
+    # the host), every CPU of the affinity mask; the fastest count is the
+    # one the other schedules run at and the one `cores` reports.
+    counts = sorted({th for th in scan if th < threads} | {threads} |
+                    ({int(topo["cgroup_cpu_quota"])} if topo.get("cgroup_cpu_quota") and
+                     1 <= topo["cgroup_cpu_quota"] < threads else set()))
+    scan_out, st = {}, None
+    for th in counts:
+        f, s_ = timed(sub, "banded", th, frames)
+        st = st or s_
+        f *= T / n
+        scan_out[str(th)] = {"frame_ms": f * 1e3, "mpixels_s": px / f / 1e6}
+    tbest = int(min(scan_out, key=lambda k: scan_out[k]["frame_ms"]))
+    fb = scan_out[str(tbest)]["frame_ms"] * 1e-3
+    variants = {"banded": {"threads": tbest, "frame_ms": fb * 1e3, "mpixels_s": px / fb / 1e6,
                            "sample": "%d of %d triangles, median of %d frames" % (n, T, frames)}}
     nq = min(n, 20_000)
     subq = scene.subset(0, nq) if nq < T else scene
     for sched in ("queue", "rows"):
-        fq, _ = timed(subq, sched, threads, 2)
+        fq, _ = timed(subq, sched, tbest, 2)
         fq *= T / nq
-        variants[sched] = {"threads": threads, "frame_ms": fq * 1e3, "mpixels_s": px / fq / 1e6,
+        variants[sched] = {"threads": tbest, "frame_ms": fq * 1e3, "mpixels_s": px / fq / 1e6,
                            "sample": "first %d triangles, median of 2 frames, scaled to T" % nq}
-    scan_out = {}
-    for th in scan:
-        if th < threads:
-            f, _ = timed(sub, "banded", th, frames)
-            f *= T / n
-            scan_out[str(th)] = {"frame_ms": f * 1e3, "mpixels_s": px / f / 1e6}
-    scan_out[str(threads)] = {"frame_ms": fb * 1e3, "mpixels_s": px / fb / 1e6}
     best = min(variants, key=lambda k: variants[k]["frame_ms"])
     frame = variants[best]["frame_ms"] * 1e-3
-    return dict(value=px / frame / 1e6, unit="Mpixels/s", cores=threads, kind="port",
-                sample="AVX2 restatement of FillLineOptimized (oracle/prk_cpu_avx.c) on all %d CPUs of the "
-                       "affinity mask; value = fastest schedule (%s); banded: %s; queue/rows: %s"
-                       % (threads, best, variants["banded"]["sample"], variants["queue"]["sample"]),
+    return dict(value=px / frame / 1e6, unit="Mpixels/s", cores=tbest, kind="port",
+                sample="AVX2 restatement of FillLineOptimized (oracle/prk_cpu_avx.c); banded schedule scanned "
+                       "over %s threads (%d = every CPU of the affinity mask), value = fastest schedule (%s) at "
+                       "the fastest count (%d threads); banded: %s; queue/rows: %s"
+                       % ("/".join(map(str, counts)), threads, best, tbest, variants["banded"]["sample"],
+                          variants["queue"]["sample"]),
                 variants=variants, banded_thread_scan=scan_out, frame_s=frame,
                 span_pixels=st["span_pixels"] if n == T else None, **topo)
 

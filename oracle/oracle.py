@@ -14,6 +14,14 @@ import sys
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+# PRK_ORACLE_LIBDIR: load the libraries from another directory (the
+# sanitizer builds of `make -C oracle san`, tests/test_sanitizers.py).
+_LIBDIR = os.environ.get("PRK_ORACLE_LIBDIR") or _HERE
+
+
+def _libpath(name):
+    p = os.path.join(_LIBDIR, name)
+    return p if os.path.exists(p) else os.path.join(_HERE, name)
 sys.path.insert(0, os.path.join(os.path.dirname(_HERE), "cpu-renderer_amd"))
 from prk import abi  # noqa: E402
 from prk.scenes import CLEAR_COLOR, CLEAR_Z  # noqa: E402
@@ -41,7 +49,7 @@ def build():
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(_HERE, "liboracle.so")
+        path = _libpath("liboracle.so")
         if not os.path.exists(path):
             build()
         _LIB = C.CDLL(path)
@@ -56,7 +64,7 @@ def cpu_lib():
     host has no AVX2."""
     global _CPU
     if _CPU is None:
-        path = os.path.join(_HERE, "liborcpu.so")
+        path = _libpath("liborcpu.so")
         if not os.path.exists(path):
             build()
         _CPU = C.CDLL(path)

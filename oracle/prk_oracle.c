@@ -904,7 +904,7 @@ int oracle_draw(const or_draw_desc *D, const or_target *Tg, const prk_transform 
 #define OR_BAND_H 32
 typedef struct or_job {
     const or_draw_desc *D; const or_target *Tg; const prk_transform *T;
-    const prk_light_data *L; int32_t mod, rem; uint64_t stats[3]; int rc;
+    const prk_light_data *L; int32_t mod, rem; uint64_t stats[3]; int rc, spawned;
 } or_job;
 
 static void *or_job_run(void *p)
@@ -928,11 +928,13 @@ int oracle_draw_mt(const or_draw_desc *D, const or_target *Tg, const prk_transfo
         memset(&jobs[t], 0, sizeof jobs[t]);
         jobs[t].D = D; jobs[t].Tg = Tg; jobs[t].T = T; jobs[t].L = Lights;
         jobs[t].mod = threads; jobs[t].rem = t;
-        if (pthread_create(&th[t], NULL, or_job_run, &jobs[t]) != 0) { jobs[t].rc = -100; }
+        jobs[t].spawned = pthread_create(&th[t], NULL, or_job_run, &jobs[t]) == 0;
     }
     int rc = PRK_OK;
     for (int t = 0; t < threads; ++t) {
-        if (jobs[t].rc != -100) pthread_join(th[t], NULL);
+        /* `spawned` is written before the thread exists; `rc` belongs to the
+         * thread until the join (reading it earlier raced, found by TSan). */
+        if (jobs[t].spawned) pthread_join(th[t], NULL);
         else or_job_run(&jobs[t]); /* could not spawn: run inline */
         if (jobs[t].rc != PRK_OK) rc = jobs[t].rc;
         if (stats) for (int k = 0; k < 3; ++k) stats[k] += jobs[t].stats[k];
