@@ -23,6 +23,13 @@
 extern "C" {
 hipError_t prk_launch_tri_draw(const prk::DrawRec *, uint32_t, uint32_t *, uint32_t, hipStream_t);
 hipError_t prk_bin_phase1(const prk::FrameParams *, uint32_t *, uint32_t *, void *, void *, size_t *, hipStream_t);
+hipError_t prk_bin_count(const prk::FrameParams *, uint32_t *, void *, hipStream_t);
+uint32_t prk_cs_chunks(uint32_t);
+uint32_t prk_cs_max_tiles(void);
+uint32_t prk_cs_max_pairs(void);
+hipError_t prk_bin_cs(const prk::FrameParams *, const void *, const uint32_t *, uint32_t *, uint32_t *, uint32_t *,
+                      uint32_t *, uint32_t *, uint32_t, uint32_t *, uint32_t *, void *, uint32_t *, uint8_t *, uint32_t,
+                      uint8_t *, hipStream_t);
 hipError_t prk_bin_phase2(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, uint32_t *, void *,
                           uint32_t *, void *, uint32_t *, uint32_t *, uint8_t *, uint32_t, uint8_t *, void *, size_t *,
                           hipStream_t);
@@ -134,7 +141,9 @@ struct prk_context {
     struct BinSet {
         DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_tri_n, d_tri_off, d_pair_tri, d_keys_a, d_vals_a, d_keys_b,
             d_bins, d_offs, d_temp, d_won, d_list, d_nwin, d_wtag, d_recs, d_trwon, d_wlist, d_seltemp, d_trec,
-            d_nrec;
+            d_nrec, d_ghist, d_tile_tot, d_chunk, d_info;
+        uint32_t *h_info = nullptr;       // pinned: [entry count, overflow] of the set's last binning
+        hipEvent_t counted_ev = nullptr;  // h_info of this set's binning has landed
         // bytes last uploaded into d_draws / d_texs and the buffer they went
         // to: an unchanged table (every frame of a static scene) is not sent again
         std::vector<uint8_t> h_draws, h_texs;
@@ -150,6 +159,8 @@ struct prk_context {
     DevBuf d_winners, d_anomaly, d_prof;
     hipEvent_t s_mark = nullptr;  // flush-stream point the bin stream waits for (prior target contents)
     uint32_t *h_total = nullptr;  // pinned
+    uint32_t pair_hint = 0;       // entry count of the last frame (counting-sort capacity)
+    bool legacy_bin = false;      // PRK_BIN_LEGACY=1: radix-sort binning with the count read back first
     int32_t tile_w = 256, tile_h = 8;  // measured best for C3b
     // all-AVX frames: per-triangle setup records; the AVX k_vis / k_walk read
     // them (prk_kernels.hip PRK_SETUP_REC), so they are not optional
@@ -210,6 +221,12 @@ int prk_create(int device, prk_context **out) {
     for (int i = 0; i < prk_context::kSets && e == hipSuccess; ++i) {
         e = hipEventCreateWithFlags(&c->bset[i].free_ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->bset[i].binned_ev, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->bset[i].counted_ev, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipHostMalloc((void **)&c->bset[i].h_info, 2 * sizeof(uint32_t), hipHostMallocDefault);
+    }
+    {
+        const char *lb = std::getenv("PRK_BIN_LEGACY");
+        c->legacy_bin = lb && lb[0] == '1';
     }
     for (int i = 0; i < prk_context::kRing && e == hipSuccess; ++i)
         for (int k = 0; k < 6 && e == hipSuccess; ++k) e = hipEventCreate(&c->ev[i][k]);
@@ -243,10 +260,12 @@ int prk_destroy(prk_context *c) {
         DevBuf *bb[] = {&B.d_draws, &B.d_texs, &B.d_tri_draw, &B.d_ranges, &B.d_tri_n, &B.d_tri_off, &B.d_pair_tri,
                         &B.d_keys_a, &B.d_vals_a, &B.d_keys_b, &B.d_bins, &B.d_offs, &B.d_temp, &B.d_won,
                         &B.d_list, &B.d_nwin, &B.d_wtag, &B.d_recs, &B.d_trwon, &B.d_wlist, &B.d_seltemp,
-                        &B.d_trec, &B.d_nrec};
+                        &B.d_trec, &B.d_nrec, &B.d_ghist, &B.d_tile_tot, &B.d_chunk, &B.d_info};
         for (DevBuf *b : bb) b->release();
         if (B.free_ev) (void)hipEventDestroy(B.free_ev);
         if (B.binned_ev) (void)hipEventDestroy(B.binned_ev);
+        if (B.counted_ev) (void)hipEventDestroy(B.counted_ev);
+        if (B.h_info) (void)hipHostFree(B.h_info);
     }
     DevBuf *bufs[] = {&c->d_winners, &c->d_anomaly, &c->d_prof};
     for (DevBuf *b : bufs) b->release();
@@ -912,53 +931,98 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
         fp.trec = (prk::TriRec *)B.d_trec.p;
         fp.nrec = (prk::NrmRec *)B.d_nrec.p;
     }
-    size_t scan_bytes = 0;
-    PRK_TRY(prk_bin_phase1(&fp, nullptr, nullptr, nullptr, nullptr, &scan_bytes, bs));
-    PRK_TRY(bset_ensure(B.d_temp, scan_bytes));
-    PRK_TRY(hipEventRecord(c->ev[slot][0], bs));
-    PRK_TRY(prk_bin_phase1(&fp, (uint32_t *)B.d_tri_n.p, (uint32_t *)B.d_tri_off.p, B.d_ranges.p, B.d_temp.p,
-                           &scan_bytes, bs));
-    // The bin array size is data dependent: read the total back (one small
-    // D2H copy per frame; the host waits for the binning only, not for the
-    // previous frame's raster) and grow the buffers if needed.
-    PRK_TRY(hipMemcpyAsync(c->h_total, (uint32_t *)B.d_tri_off.p + T, 4, hipMemcpyDeviceToHost, bs));
-    PRK_TRY(hipStreamSynchronize(bs));
-    const uint32_t total = *c->h_total;
-    c->stats.bin_entries = total;
-    if (total >= prk::kMaxPairs) return PRK_ERR_UNSUPPORTED;  // visibility tags hold a 31-bit pair index
-    const size_t ne = (size_t)std::max<uint32_t>(total, 1);
-    PRK_TRY(bset_ensure(B.d_pair_tri, ne * 4));
-    PRK_TRY(bset_ensure(B.d_bins, ne * 8));  // (triangle, pair) per bin slot
-    PRK_TRY(bset_ensure(B.d_keys_a, ne * 4));
-    PRK_TRY(bset_ensure(B.d_vals_a, ne * 8));
-    PRK_TRY(bset_ensure(B.d_keys_b, ne * 4));
-    // won flags: per (pair, row in tile) for span-record (AVX) frames, per
-    // pair otherwise; k_bin_emit clears them (and trwon) for every pair.
     const bool span_rec = modeset == prk::MODE_AVX;
+    // won flags: per (pair, row in tile) for span-record (AVX) frames, per
+    // pair otherwise; the binning clears them (and trwon) for every pair.
     const uint32_t won_stride = span_rec ? (uint32_t)c->tile_h : 1u;
-    const size_t won_bytes = ne * won_stride;
     size_t sel_bytes = 0;
     if (span_rec) PRK_TRY(prk_walk_select_bytes(T, &sel_bytes));
-    PRK_TRY(bset_ensure(B.d_list, ne * 4));
-    PRK_TRY(bset_ensure(B.d_won, won_bytes));
+    // Every per-pair array of the set, for `np` pairs.
+    auto ensure_pairs = [&](size_t np, bool sort_keys) -> hipError_t {
+        const size_t ne = std::max<size_t>(np, 1);
+        hipError_t e = hipSuccess;
+        if (e == hipSuccess) e = bset_ensure(B.d_pair_tri, ne * 4);
+        if (e == hipSuccess) e = bset_ensure(B.d_bins, ne * 8);  // (triangle, pair) per bin slot
+        if (e == hipSuccess && sort_keys) e = bset_ensure(B.d_keys_a, ne * 4);
+        if (e == hipSuccess && sort_keys) e = bset_ensure(B.d_vals_a, ne * 8);
+        if (e == hipSuccess && sort_keys) e = bset_ensure(B.d_keys_b, ne * 4);
+        if (e == hipSuccess) e = bset_ensure(B.d_list, ne * 4);
+        if (e == hipSuccess) e = bset_ensure(B.d_won, ne * won_stride);
+        // span records: 64 B per (pair, row in tile); only won ones are written
+        if (e == hipSuccess && span_rec) e = bset_ensure(B.d_recs, ne * won_stride * 64);
+        return e;
+    };
     PRK_TRY(bset_ensure(B.d_nwin, (size_t)ntiles * 4));
     PRK_TRY(bset_ensure(B.d_wtag, (size_t)ntiles * c->tile_w * c->tile_h * 4));
     if (span_rec) {
         PRK_TRY(bset_ensure(B.d_trwon, T));
         PRK_TRY(bset_ensure(B.d_wlist, ((size_t)T + 1) * 4));  // won triangles + their count
         PRK_TRY(bset_ensure(B.d_seltemp, std::max<size_t>(sel_bytes, 16)));
-        // span records: 64 B per (pair, row in tile); only won ones are written
-        PRK_TRY(bset_ensure(B.d_recs, won_bytes * 64));
     }
-    uint8_t *won = (uint8_t *)B.d_won.p, *trwon = span_rec ? (uint8_t *)B.d_trwon.p : nullptr;
-    size_t sort_bytes = 0;
-    PRK_TRY(prk_bin_phase2(&fp, B.d_ranges.p, (const uint32_t *)B.d_tri_off.p, total, (uint32_t *)B.d_keys_a.p,
-                           B.d_vals_a.p, (uint32_t *)B.d_keys_b.p, B.d_bins.p, (uint32_t *)B.d_pair_tri.p,
-                           (uint32_t *)B.d_offs.p, won, won_stride, trwon, nullptr, &sort_bytes, bs));
-    PRK_TRY(bset_ensure(B.d_temp, std::max(sort_bytes, scan_bytes)));
-    PRK_TRY(prk_bin_phase2(&fp, B.d_ranges.p, (const uint32_t *)B.d_tri_off.p, total, (uint32_t *)B.d_keys_a.p,
-                           B.d_vals_a.p, (uint32_t *)B.d_keys_b.p, B.d_bins.p, (uint32_t *)B.d_pair_tri.p,
-                           (uint32_t *)B.d_offs.p, won, won_stride, trwon, B.d_temp.p, &sort_bytes, bs));
+    uint8_t *won, *trwon;
+    const bool cs = !c->legacy_bin && ntiles <= prk_cs_max_tiles();
+    uint32_t total = 0;
+    if (cs) {
+        // Counting-sort binning (prk_bin.hip k_cs_*): all sizes stay on the
+        // device.  The per-pair arrays hold `cap` pairs (the last frame's
+        // count plus room; a first frame guesses 4 per triangle); a frame with
+        // more entries leaves its bins empty and is re-run below, once the
+        // count is known.
+        const uint32_t nch = prk_cs_chunks(T);
+        const uint64_t want64 = c->pair_hint ? (uint64_t)c->pair_hint + c->pair_hint / 8 + 4096
+                                             : std::max<uint64_t>(4ull * T, 1u << 16);
+        const uint32_t want = (uint32_t)std::min<uint64_t>(want64, prk_cs_max_pairs());
+        // pairs the set's per-pair arrays hold now (they never shrink)
+        auto pairs_held = [&]() -> size_t {
+            size_t m = std::min(B.d_pair_tri.cap / 4, B.d_bins.cap / 8);
+            m = std::min(m, B.d_list.cap / 4);
+            m = std::min(m, B.d_won.cap / won_stride);
+            if (span_rec) m = std::min(m, B.d_recs.cap / ((size_t)won_stride * 64));
+            return m;
+        };
+        if (pairs_held() < want) PRK_TRY(ensure_pairs(want, false));
+        const uint32_t cap = (uint32_t)std::min<size_t>(pairs_held(), prk_cs_max_pairs());
+        PRK_TRY(bset_ensure(B.d_ghist, std::max<size_t>((size_t)nch * ntiles * 4, 4)));
+        PRK_TRY(bset_ensure(B.d_tile_tot, (size_t)ntiles * 4));
+        PRK_TRY(bset_ensure(B.d_chunk, std::max<size_t>((size_t)nch * 8, 8)));
+        PRK_TRY(bset_ensure(B.d_info, 8));
+        won = (uint8_t *)B.d_won.p;
+        trwon = span_rec ? (uint8_t *)B.d_trwon.p : nullptr;
+        PRK_TRY(hipEventRecord(c->ev[slot][0], bs));
+        PRK_TRY(prk_bin_count(&fp, (uint32_t *)B.d_tri_n.p, B.d_ranges.p, bs));
+        uint32_t *chunk = (uint32_t *)B.d_chunk.p;
+        PRK_TRY(prk_bin_cs(&fp, B.d_ranges.p, (const uint32_t *)B.d_tri_n.p, (uint32_t *)B.d_ghist.p,
+                           (uint32_t *)B.d_tile_tot.p, chunk, chunk + nch, (uint32_t *)B.d_offs.p, cap,
+                           (uint32_t *)B.d_info.p, (uint32_t *)B.d_tri_off.p, B.d_bins.p, (uint32_t *)B.d_pair_tri.p,
+                           won, won_stride, trwon, bs));
+        PRK_TRY(hipMemcpyAsync(B.h_info, B.d_info.p, 8, hipMemcpyDeviceToHost, bs));
+        PRK_TRY(hipEventRecord(B.counted_ev, bs));
+    } else {
+        // Radix-sort binning: the bin array size is read back first (one
+        // small D2H copy per frame; the host waits for the binning only).
+        size_t scan_bytes = 0;
+        PRK_TRY(prk_bin_phase1(&fp, nullptr, nullptr, nullptr, nullptr, &scan_bytes, bs));
+        PRK_TRY(bset_ensure(B.d_temp, scan_bytes));
+        PRK_TRY(hipEventRecord(c->ev[slot][0], bs));
+        PRK_TRY(prk_bin_phase1(&fp, (uint32_t *)B.d_tri_n.p, (uint32_t *)B.d_tri_off.p, B.d_ranges.p, B.d_temp.p,
+                               &scan_bytes, bs));
+        PRK_TRY(hipMemcpyAsync(c->h_total, (uint32_t *)B.d_tri_off.p + T, 4, hipMemcpyDeviceToHost, bs));
+        PRK_TRY(hipStreamSynchronize(bs));
+        total = *c->h_total;
+        c->stats.bin_entries = total;
+        if (total >= prk::kMaxPairs) return PRK_ERR_UNSUPPORTED;  // visibility tags hold a 31-bit pair index
+        PRK_TRY(ensure_pairs(total, true));
+        won = (uint8_t *)B.d_won.p;
+        trwon = span_rec ? (uint8_t *)B.d_trwon.p : nullptr;
+        size_t sort_bytes = 0;
+        PRK_TRY(prk_bin_phase2(&fp, B.d_ranges.p, (const uint32_t *)B.d_tri_off.p, total, (uint32_t *)B.d_keys_a.p,
+                               B.d_vals_a.p, (uint32_t *)B.d_keys_b.p, B.d_bins.p, (uint32_t *)B.d_pair_tri.p,
+                               (uint32_t *)B.d_offs.p, won, won_stride, trwon, nullptr, &sort_bytes, bs));
+        PRK_TRY(bset_ensure(B.d_temp, std::max(sort_bytes, scan_bytes)));
+        PRK_TRY(prk_bin_phase2(&fp, B.d_ranges.p, (const uint32_t *)B.d_tri_off.p, total, (uint32_t *)B.d_keys_a.p,
+                               B.d_vals_a.p, (uint32_t *)B.d_keys_b.p, B.d_bins.p, (uint32_t *)B.d_pair_tri.p,
+                               (uint32_t *)B.d_offs.p, won, won_stride, trwon, B.d_temp.p, &sort_bytes, bs));
+    }
     PRK_TRY(hipEventRecord(c->ev[slot][1], bs));
     PRK_TRY(hipEventRecord(B.binned_ev, bs));
 
@@ -1000,6 +1064,22 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
     c->last_slot = slot;
     c->frame++;
     guard.ok = true;
+    if (cs) {
+        // The whole frame is queued; now the entry count (the binning's first
+        // few kernels) decides whether it fitted.  An over-capacity frame drew
+        // nothing (empty bins; with a fused clear its k_pix wrote the clear
+        // values, which the re-run writes again): re-run it with room for
+        // every entry.
+        PRK_TRY(hipEventSynchronize(B.counted_ev));
+        total = B.h_info[0];
+        c->stats.bin_entries = total;
+        c->pair_hint = total;
+        if (B.h_info[1]) {
+            if (total > prk_cs_max_pairs()) return PRK_ERR_UNSUPPORTED;  // 29-bit pair index in the bins
+            c->clear_pending = fuse;
+            return flush_tris(c, s, draws, T, win_base);
+        }
+    }
     return PRK_OK;
 }
 

@@ -101,56 +101,87 @@ __device__ __forceinline__ uint32_t range_entries(const TileRange &tr) {
     return n;
 }
 
+#ifndef PRK_ROWCLASS
+#define PRK_ROWCLASS 1
+#endif
 constexpr int kRowClassBits = 3;
 
-__global__ void k_bin_count(FrameParams fp, uint32_t *__restrict__ tri_n, TileRange *__restrict__ ranges) {
+// Records leave through LDS: a wave's 64 records are written out as
+// consecutive 16-byte chunks (one coalesced store per 64 chunks) instead of
+// ten 160-byte-strided stores per lane.
+constexpr int kCountThreads = 256;
+__global__ void __launch_bounds__(kCountThreads) k_bin_count(FrameParams fp, uint32_t *__restrict__ tri_n,
+                                                              TileRange *__restrict__ ranges) {
+    __shared__ float4 stage[kCountThreads / 64][64 * 10];
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g > fp.tri_count) return;
-    if (g == fp.tri_count) {  // sentinel: the scan's last element is the total
-        tri_n[g] = 0;
-        return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    bool rec = false;
+    TriRec r;
+    NrmRec q;
+    if (g < fp.tri_count) {
+        TileRange tr;
+        if (!tri_tile_range(fp, g, tr)) {
+            tr.tx0 = 1; tr.tx1 = 0; tr.ty0 = 1; tr.ty1 = 0; tr.oty0 = 1; tr.oty1 = 0;
+        }
+        ranges[g] = tr;
+        const uint32_t ne = range_entries(tr);
+        tri_n[g] = ne;
+        if (fp.trec && ne) {
+            // All-AVX frame: FillEdgeTable + MergeSort + the first row's AET
+            // insertions once per triangle (TriRec / NrmRec, prk_device.h).
+            const DrawRec *d;
+            uint32_t gt;
+            resolve_draw(fp, g, d, gt);
+            Edge s0, s1, s2;
+            TriRaw<MODE_AVX> raw;
+            load_tri<MODE_AVX>(*d, gt, raw);
+            const int n = setup_from_raw<MODE_AVX>(raw, *d, fp, s0, s1, s2);
+            uint32_t anom = 0;
+            Walker<MODE_AVX, true> w;
+            w.init(n, s0, s1, s2, fp.H, fp.H, anom);
+            rec_edge_out(s0, r.e[0], r.ymin[0], r.ymax[0]);
+            rec_edge_out(s1, r.e[1], r.ymin[1], r.ymax[1]);
+            rec_edge_out(s2, r.e[2], r.ymin[2], r.ymax[2]);
+            r.head = (uint32_t)n | (w.ord << 4) | ((uint32_t)w.cnt << 12) | ((uint32_t)(w.pend + 1) << 16) |
+                     (min(anom, 15u) << 20) | ((d->flags & DRAW_ST) ? (1u << 24) : 0u);
+            r.pad[0] = r.pad[1] = r.pad[2] = 0;
+            nrm_edge_out(s0, q.n[0]);
+            nrm_edge_out(s1, q.n[1]);
+            nrm_edge_out(s2, q.n[2]);
+            q.pad[0] = q.pad[1] = 0.0f;
+            rec = true;
+        }
+    } else if (g == fp.tri_count) {
+        tri_n[g] = 0;  // sentinel: a scan's last element is the total
     }
-    TileRange tr;
-    if (!tri_tile_range(fp, g, tr)) {
-        tr.tx0 = 1; tr.tx1 = 0; tr.ty0 = 1; tr.ty1 = 0; tr.oty0 = 1; tr.oty1 = 0;
-    }
-    ranges[g] = tr;
-    const uint32_t ne = range_entries(tr);
-    tri_n[g] = ne;
-    if (fp.trec && ne) {
-        // All-AVX frame: FillEdgeTable + MergeSort + the first row's AET
-        // insertions once per triangle (TriRec / NrmRec, prk_device.h).
-        const DrawRec *d;
-        uint32_t gt;
-        resolve_draw(fp, g, d, gt);
-        Edge s0, s1, s2;
-        TriRaw<MODE_AVX> raw;
-        load_tri<MODE_AVX>(*d, gt, raw);
-        const int n = setup_from_raw<MODE_AVX>(raw, *d, fp, s0, s1, s2);
-        uint32_t anom = 0;
-        Walker<MODE_AVX, true> w;
-        w.init(n, s0, s1, s2, fp.H, fp.H, anom);
-        TriRec r;
-        NrmRec q;
-        rec_edge_out(s0, r.e[0], r.ymin[0], r.ymax[0]);
-        rec_edge_out(s1, r.e[1], r.ymin[1], r.ymax[1]);
-        rec_edge_out(s2, r.e[2], r.ymin[2], r.ymax[2]);
-        r.head = (uint32_t)n | (w.ord << 4) | ((uint32_t)w.cnt << 12) | ((uint32_t)(w.pend + 1) << 16) |
-                 (min(anom, 15u) << 20) | ((d->flags & DRAW_ST) ? (1u << 24) : 0u);
-        r.pad[0] = r.pad[1] = r.pad[2] = 0;
-        nrm_edge_out(s0, q.n[0]);
-        nrm_edge_out(s1, q.n[1]);
-        nrm_edge_out(s2, q.n[2]);
-        q.pad[0] = q.pad[1] = 0.0f;
-        float4 *dr = reinterpret_cast<float4 *>(fp.trec + g);
+    const uint64_t mask = __ballot(rec);
+    if (mask == 0) return;
+    const uint32_t gw = g - (uint32_t)lane;  // the wave's first triangle
+    float4 *st = stage[wv];
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    if (rec) {
         const float4 *sr = reinterpret_cast<const float4 *>(&r);
 #pragma unroll
-        for (int k = 0; k < 10; ++k) dr[k] = sr[k];
-        float4 *dq = reinterpret_cast<float4 *>(fp.nrec + g);
+        for (int k = 0; k < 10; ++k) st[lane * 10 + k] = sr[k];
+    }
+    wave_sync();
+    float4 *dr = reinterpret_cast<float4 *>(fp.trec + gw);
+    for (int c = lane; c < 64 * 10; c += 64)
+        if ((mask >> (c / 10)) & 1) dr[c] = st[c];
+    wave_sync();
+    if (rec) {
         const float4 *sq = reinterpret_cast<const float4 *>(&q);
 #pragma unroll
-        for (int k = 0; k < 5; ++k) dq[k] = sq[k];
+        for (int k = 0; k < 5; ++k) st[lane * 5 + k] = sq[k];
     }
+    wave_sync();
+    float4 *dq = reinterpret_cast<float4 *>(fp.nrec + gw);
+    for (int c = lane; c < 64 * 5; c += 64)
+        if ((mask >> (c / 5)) & 1) dq[c] = st[c];
 }
 
 // Sort key = tile << kRowClassBits | row class: within a tile's bin the
@@ -178,7 +209,7 @@ __global__ void k_bin_emit(FrameParams fp, const TileRange *__restrict__ ranges,
         for (int ty = tr.ty0; ty <= tr.ty1; ++ty) {
             const int y0 = ty * fp.tile_h;
             const int rows = min((int)tr.pad1, y0 + fp.tile_h) - max((int)tr.pad0, y0);
-            const uint32_t cls = (uint32_t)min(kMaxClass, max(0, fp.tile_h - rows));
+            const uint32_t cls = PRK_ROWCLASS ? (uint32_t)min(kMaxClass, max(0, fp.tile_h - rows)) : 0u;
             for (int tx = tr.tx0; tx <= tr.tx1; ++tx) {
                 keys[o] = ((uint32_t)(ty * fp.tiles_x + tx) << kRowClassBits) | cls;
                 vals[o] = make_uint2(g, o);
@@ -189,7 +220,7 @@ __global__ void k_bin_emit(FrameParams fp, const TileRange *__restrict__ ranges,
         }
     for (int ty = tr.oty0; ty <= tr.oty1; ++ty)
         if (!(tr.tx0 == 0 && tr.tx0 <= tr.tx1 && ty >= tr.ty0 && ty <= tr.ty1)) {
-            keys[o] = ((uint32_t)(ty * fp.tiles_x) << kRowClassBits) | (uint32_t)kMaxClass;
+            keys[o] = ((uint32_t)(ty * fp.tiles_x) << kRowClassBits) | (PRK_ROWCLASS ? (uint32_t)kMaxClass : 0u);
             vals[o] = make_uint2(g, o);
             pair_tri[o] = g;
             clear_won(won, won_stride, o);
@@ -211,6 +242,277 @@ __global__ void k_tile_offsets(const uint32_t *__restrict__ keys, uint32_t total
     offs[t] = lo;
 }
 
+// ---------------------------------------------------------------------------
+// Counting-sort binning (the default when the frame has at most kCsMaxTiles
+// tiles): no radix sort, no host round trip before the bin kernels.
+//
+//   k_bin_count   as above (ranges, per-triangle counts, setup records)
+//   k_cs_hist     one workgroup per chunk of kCsChunk triangles: LDS histogram
+//                 of the chunk's entries per tile -> ghist[chunk][tile], and
+//                 the chunk's entry total
+//   k_cs_colscan  per tile, exclusive prefix over the chunks (in place) and
+//                 the tile's total
+//   k_cs_scan     one workgroup: tile offsets (bin starts), chunk pair bases,
+//                 the frame's entry count; an entry count above the scratch
+//                 capacity empties every bin (the host re-runs the frame)
+//   k_cs_emit     one workgroup per chunk: pair offsets of its triangles in
+//                 triangle order (pair j = the tie-break key), and each entry
+//                 scattered into its tile's bin through an LDS cursor
+//   k_cs_class    one workgroup per tile: the bin grouped by row class (how
+//                 many of the tile's rows the triangle can cover), so the 64
+//                 triangles a k_vis wave walks together cover similar row
+//                 counts (k_vis -13 % against no grouping, measured)
+//
+// The order inside a bin is free (the pair index, not the bin position,
+// orders equal-z fragments), so the LDS cursors need no ordering.
+// ---------------------------------------------------------------------------
+constexpr int kCsThreads = 1024;
+constexpr uint32_t kCsTrisPerThread = 4;
+constexpr uint32_t kCsChunk = kCsThreads * kCsTrisPerThread;
+constexpr uint32_t kCsMaxTiles = 32768;  // LDS: one u32 per tile (128 KiB)
+constexpr uint32_t kCsClassShift = 29;   // row class in bits 29-31 of the emitted pair index
+constexpr uint32_t kCsPairMask = (1u << kCsClassShift) - 1u;
+constexpr int kCsClassWindow = 2048;     // k_cs_class: entries grouped per pass
+
+__device__ __forceinline__ uint32_t cs_wave_incl_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false); // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false); // row_bcast:31
+    return v;
+}
+
+// Exclusive scan over the workgroup (one value per thread); `total` = sum.
+// scratch: one u32 per wave.
+__device__ __forceinline__ uint32_t cs_block_excl_scan(uint32_t v, uint32_t *scratch, uint32_t &total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const uint32_t incl = cs_wave_incl_scan(v);
+    if (lane == 63) scratch[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    total = 0;
+    for (int w = 0; w < nw; ++w) {
+        const uint32_t x = scratch[w];
+        before += w < wave ? x : 0u;
+        total += x;
+    }
+    __syncthreads();
+    return before + incl - v;
+}
+
+// The (tile, row class) of every entry of a range, in pair order: the
+// rectangle row-major, then the column-0 overflow tiles not in it.
+template <class F>
+__device__ __forceinline__ void for_each_entry(const FrameParams &fp, const TileRange &tr, F &&f) {
+    constexpr int kMaxClass = (1 << kRowClassBits) - 1;
+    if (tr.tx0 <= tr.tx1 && tr.ty0 <= tr.ty1)
+        for (int ty = tr.ty0; ty <= tr.ty1; ++ty) {
+            const int y0 = ty * fp.tile_h;
+            const int rows = min((int)tr.pad1, y0 + fp.tile_h) - max((int)tr.pad0, y0);
+            const uint32_t cls = PRK_ROWCLASS ? (uint32_t)min(kMaxClass, max(0, fp.tile_h - rows)) : 0u;
+            for (int tx = tr.tx0; tx <= tr.tx1; ++tx) f((uint32_t)(ty * fp.tiles_x + tx), cls);
+        }
+    for (int ty = tr.oty0; ty <= tr.oty1; ++ty)
+        if (!(tr.tx0 == 0 && tr.tx0 <= tr.tx1 && ty >= tr.ty0 && ty <= tr.ty1))
+            f((uint32_t)(ty * fp.tiles_x), PRK_ROWCLASS ? (uint32_t)kMaxClass : 0u);
+}
+
+__global__ void __launch_bounds__(kCsThreads) k_cs_hist(FrameParams fp, const TileRange *__restrict__ ranges,
+                                                         const uint32_t *__restrict__ tri_n,
+                                                         uint32_t *__restrict__ ghist,
+                                                         uint32_t *__restrict__ chunk_tot, uint32_t ntiles) {
+    extern __shared__ uint32_t h[];
+    __shared__ uint32_t scratch[kCsThreads / 64];
+    for (uint32_t i = threadIdx.x; i < ntiles; i += kCsThreads) h[i] = 0;
+    __syncthreads();
+    const uint32_t c = blockIdx.x;
+    uint32_t sum = 0;
+    for (uint32_t r = 0; r < kCsTrisPerThread; ++r) {
+        const uint32_t g = c * kCsChunk + r * kCsThreads + threadIdx.x;
+        if (g >= fp.tri_count) break;
+        const uint32_t n = tri_n[g];
+        if (!n) continue;
+        sum += n;
+        const TileRange tr = ranges[g];
+        for_each_entry(fp, tr, [&](uint32_t tile, uint32_t) { atomicAdd(&h[tile], 1u); });
+    }
+    uint32_t tot;
+    (void)cs_block_excl_scan(sum, scratch, tot);  // (its barriers also order the LDS histogram)
+    if (threadIdx.x == 0) chunk_tot[c] = tot;
+    uint32_t *out = ghist + (size_t)c * ntiles;
+    for (uint32_t i = threadIdx.x; i < ntiles; i += kCsThreads) out[i] = h[i];
+}
+
+// 1024 threads = 64 tiles x 16 chunk segments; lane = tile, wave = segment.
+constexpr int kColSegs = 16;
+__global__ void __launch_bounds__(64 * kColSegs) k_cs_colscan(uint32_t *__restrict__ ghist, uint32_t nchunks,
+                                                               uint32_t ntiles, uint32_t *__restrict__ tile_tot) {
+    __shared__ uint32_t seg[kColSegs][64];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t t = blockIdx.x * 64 + lane;
+    const uint32_t per = (nchunks + kColSegs - 1) / kColSegs, c0 = min(nchunks, w * per), c1 = min(nchunks, c0 + per);
+    uint32_t s = 0;
+    if (t < ntiles)
+        for (uint32_t c = c0; c < c1; ++c) s += ghist[(size_t)c * ntiles + t];
+    seg[w][lane] = s;
+    __syncthreads();
+    uint32_t run = 0;
+    for (uint32_t k = 0; k < w; ++k) run += seg[k][lane];
+    if (t < ntiles) {
+        for (uint32_t c = c0; c < c1; ++c) {
+            const size_t i = (size_t)c * ntiles + t;
+            const uint32_t v = ghist[i];
+            ghist[i] = run;
+            run += v;
+        }
+        if (w == kColSegs - 1) tile_tot[t] = run;
+    }
+}
+
+// One workgroup.  offs[0..ntiles] = exclusive scan of the tile totals (bin
+// starts; offs[ntiles] = the frame's entry count), chunk_base = exclusive scan
+// of the chunk totals; info[0] = entry count, info[1] = 1 if it exceeds `cap`
+// (then every bin is left empty and k_cs_emit writes no pair).
+// Exclusive scan of n values (n <= kCsThreads * kScanPer) by one workgroup:
+// each thread loads kScanPer consecutive values first, so the whole scan is
+// one round of loads and one workgroup scan.
+constexpr uint32_t kScanPer = kCsMaxTiles / kCsThreads;
+__device__ __forceinline__ uint32_t cs_scan_small(const uint32_t *__restrict__ in, uint32_t n,
+                                                  uint32_t *__restrict__ out, uint32_t *scratch, uint32_t base) {
+    uint32_t v[kScanPer];
+    const uint32_t i0 = threadIdx.x * kScanPer;
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k) {
+        v[k] = i0 + k < n ? in[i0 + k] : 0u;
+        sum += v[k];
+    }
+    uint32_t tot;
+    uint32_t run = base + cs_block_excl_scan(sum, scratch, tot);
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k) {
+        if (i0 + k < n) out[i0 + k] = run;
+        run += v[k];
+    }
+    return tot;
+}
+
+// One workgroup.  offs[0..ntiles] = exclusive scan of the tile totals (bin
+// starts; offs[ntiles] = the frame's entry count), chunk_base = exclusive scan
+// of the chunk totals; info[0] = entry count, info[1] = 1 if it exceeds `cap`
+// (then every bin is left empty and k_cs_emit writes no pair).
+__global__ void __launch_bounds__(kCsThreads) k_cs_scan(const uint32_t *__restrict__ tile_tot, uint32_t ntiles,
+                                                         const uint32_t *__restrict__ chunk_tot, uint32_t nchunks,
+                                                         uint32_t *__restrict__ offs,
+                                                         uint32_t *__restrict__ chunk_base, uint32_t cap,
+                                                         uint32_t *__restrict__ info) {
+    __shared__ uint32_t scratch[kCsThreads / 64];
+    const uint32_t total = cs_scan_small(tile_tot, ntiles, offs, scratch, 0u);
+    const bool over = total > cap;
+    uint32_t run = 0;  // chunk bases (more than one round past 128 M triangles)
+    for (uint32_t b = 0; b < nchunks; b += kCsThreads * kScanPer)
+        run += cs_scan_small(chunk_tot + b, min(nchunks - b, kCsThreads * kScanPer), chunk_base + b, scratch, run);
+    if (over) {  // empty bins: the frame's raster draws nothing
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i <= ntiles; i += kCsThreads) offs[i] = 0;
+    } else if (threadIdx.x == 0) {
+        offs[ntiles] = total;
+    }
+    if (threadIdx.x == 0) {
+        info[0] = total;
+        info[1] = over ? 1u : 0u;
+    }
+}
+
+__global__ void __launch_bounds__(kCsThreads) k_cs_emit(FrameParams fp, const TileRange *__restrict__ ranges,
+                                                         const uint32_t *__restrict__ tri_n,
+                                                         const uint32_t *__restrict__ ghist,
+                                                         const uint32_t *__restrict__ offs,
+                                                         const uint32_t *__restrict__ chunk_base,
+                                                         const uint32_t *__restrict__ info, uint32_t ntiles,
+                                                         uint32_t *__restrict__ tri_off, uint2 *__restrict__ bins,
+                                                         uint32_t *__restrict__ pair_tri, uint8_t *__restrict__ won,
+                                                         uint32_t won_stride, uint8_t *__restrict__ trwon) {
+    extern __shared__ uint32_t cur[];
+    __shared__ uint32_t scratch[kCsThreads / 64];
+    const uint32_t c = blockIdx.x;
+    const bool over = info[1] != 0;
+    if (!over) {
+        const uint32_t *gh = ghist + (size_t)c * ntiles;
+        for (uint32_t i = threadIdx.x; i < ntiles; i += kCsThreads) cur[i] = offs[i] + gh[i];
+    }
+    uint32_t base = chunk_base[c];
+    for (uint32_t r = 0; r < kCsTrisPerThread; ++r) {
+        const uint32_t g = c * kCsChunk + r * kCsThreads + threadIdx.x;
+        const bool in = g < fp.tri_count;
+        const uint32_t n = in ? tri_n[g] : 0u;
+        uint32_t tot;
+        const uint32_t j0 = base + cs_block_excl_scan(n, scratch, tot);  // (also orders the cursor loads)
+        base += tot;
+        if (!in) continue;
+        if (trwon) trwon[g] = 0;
+        if (over) continue;
+        tri_off[g] = j0;
+        if (!n) continue;
+        const TileRange tr = ranges[g];
+        uint32_t j = j0;
+        for_each_entry(fp, tr, [&](uint32_t tile, uint32_t cls) {
+            const uint32_t pos = atomicAdd(&cur[tile], 1u);
+            bins[pos] = make_uint2(g, j | (cls << kCsClassShift));
+            pair_tri[j] = g;
+            clear_won(won, won_stride, j);
+            ++j;
+        });
+    }
+    if (!over && c == gridDim.x - 1 && threadIdx.x == 0) tri_off[fp.tri_count] = info[0];
+}
+
+// Group every bin by row class (windows of kCsClassWindow entries) and strip
+// the class bits from the pair index.
+__global__ void __launch_bounds__(256) k_cs_class(const uint32_t *__restrict__ offs, uint2 *__restrict__ bins) {
+    constexpr int kPer = kCsClassWindow / 256;
+    constexpr int kClasses = 1 << kRowClassBits;
+    __shared__ uint32_t cnt[kClasses];
+    const uint32_t t = blockIdx.x;
+    const uint32_t b0 = offs[t], n = offs[t + 1] - b0;
+    if (n == 0) return;
+    for (uint32_t w0 = 0; w0 < n; w0 += kCsClassWindow) {
+        const uint32_t m = min((uint32_t)kCsClassWindow, n - w0);
+        uint2 e[kPer];
+        if (threadIdx.x < kClasses) cnt[threadIdx.x] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const uint32_t i = threadIdx.x + 256u * k;
+            if (i < m) {
+                e[k] = bins[b0 + w0 + i];
+                atomicAdd(&cnt[e[k].y >> kCsClassShift], 1u);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t run = 0;
+            for (int k = 0; k < kClasses; ++k) {
+                const uint32_t v = cnt[k];
+                cnt[k] = run;
+                run += v;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const uint32_t i = threadIdx.x + 256u * k;
+            if (i < m) {
+                const uint32_t pos = atomicAdd(&cnt[e[k].y >> kCsClassShift], 1u);
+                bins[b0 + w0 + pos] = make_uint2(e[k].x, e[k].y & kCsPairMask);
+            }
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace prk
 
 // Bin sort: onesweep radix at every size above one block.  rocprim's
@@ -229,8 +531,8 @@ hipError_t prk_bin_phase1(const prk::FrameParams *fp, uint32_t *tri_n, uint32_t 
                           void *temp, size_t *temp_bytes, hipStream_t s) {
     const uint32_t n = fp->tri_count + 1;
     if (!temp) return hipcub::DeviceScan::ExclusiveSum(nullptr, *temp_bytes, tri_n, scan_out, n, s);
-    hipLaunchKernelGGL(prk::k_bin_count, dim3((n + 255) / 256), dim3(256), 0, s, *fp, tri_n,
-                       reinterpret_cast<prk::TileRange *>(ranges));
+    hipLaunchKernelGGL(prk::k_bin_count, dim3((n + prk::kCountThreads - 1) / prk::kCountThreads),
+                       dim3(prk::kCountThreads), 0, s, *fp, tri_n, reinterpret_cast<prk::TileRange *>(ranges));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, tri_n, scan_out, n, s);
@@ -266,6 +568,62 @@ hipError_t prk_bin_phase2(const prk::FrameParams *fp, const void *ranges, const 
     }
     hipLaunchKernelGGL(prk::k_tile_offsets, dim3((ntiles + 1 + 255) / 256), dim3(256), 0, s, keys_b, total, ntiles,
                        offs);
+    return hipGetLastError();
+}
+
+
+// Counting-sort binning (k_cs_*), after prk_bin_phase1's k_bin_count (scan
+// not needed: pass scan_out == nullptr there).  Every size is device-side:
+// info[0] = entry count, info[1] = overflow (count > cap: bins left empty,
+// no pair written; the caller re-runs the frame with more room).
+// ghist: nchunks * ntiles u32; tile_tot: ntiles; chunk_tot / chunk_base: nchunks.
+hipError_t prk_bin_count(const prk::FrameParams *fp, uint32_t *tri_n, void *ranges, hipStream_t s) {
+    const uint32_t n = fp->tri_count + 1;
+    hipLaunchKernelGGL(prk::k_bin_count, dim3((n + prk::kCountThreads - 1) / prk::kCountThreads),
+                       dim3(prk::kCountThreads), 0, s, *fp, tri_n, reinterpret_cast<prk::TileRange *>(ranges));
+    return hipGetLastError();
+}
+
+uint32_t prk_cs_chunks(uint32_t tri_count) { return (tri_count + prk::kCsChunk - 1) / prk::kCsChunk; }
+uint32_t prk_cs_max_tiles(void) { return prk::kCsMaxTiles; }
+uint32_t prk_cs_max_pairs(void) { return prk::kCsPairMask; }
+
+hipError_t prk_bin_cs(const prk::FrameParams *fp, const void *ranges, const uint32_t *tri_n, uint32_t *ghist,
+                      uint32_t *tile_tot, uint32_t *chunk_tot, uint32_t *chunk_base, uint32_t *offs, uint32_t cap,
+                      uint32_t *info, uint32_t *tri_off, void *bins, uint32_t *pair_tri, uint8_t *won,
+                      uint32_t won_stride, uint8_t *trwon, hipStream_t s) {
+    const uint32_t ntiles = (uint32_t)(fp->tiles_x * fp->tiles_y);
+    if (ntiles > prk::kCsMaxTiles || ntiles == 0) return hipErrorInvalidValue;
+    const uint32_t nch = prk_cs_chunks(fp->tri_count);
+    const prk::TileRange *tr = reinterpret_cast<const prk::TileRange *>(ranges);
+    const size_t lds = (size_t)ntiles * 4;
+    static bool attr = false;  // dynamic LDS above 64 KiB (up to kCsMaxTiles tiles)
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&prk::k_cs_hist),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, prk::kCsMaxTiles * 4);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(reinterpret_cast<const void *>(&prk::k_cs_emit),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, prk::kCsMaxTiles * 4);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    if (nch) {
+        hipLaunchKernelGGL(prk::k_cs_hist, dim3(nch), dim3(prk::kCsThreads), lds, s, *fp, tr, tri_n, ghist, chunk_tot,
+                           ntiles);
+        hipLaunchKernelGGL(prk::k_cs_colscan, dim3((ntiles + 63) / 64), dim3(64 * prk::kColSegs), 0, s, ghist, nch,
+                           ntiles, tile_tot);
+    } else {
+        hipError_t e = hipMemsetAsync(tile_tot, 0, (size_t)ntiles * 4, s);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(prk::k_cs_scan, dim3(1), dim3(prk::kCsThreads), 0, s, tile_tot, ntiles, chunk_tot, nch, offs,
+                       chunk_base, std::min(cap, prk::kCsPairMask), info);
+    if (nch)
+        hipLaunchKernelGGL(prk::k_cs_emit, dim3(nch), dim3(prk::kCsThreads), lds, s, *fp, tr, tri_n, ghist, offs,
+                           chunk_base, info, ntiles, tri_off, reinterpret_cast<uint2 *>(bins), pair_tri, won,
+                           won_stride, trwon);
+    if (PRK_ROWCLASS)
+        hipLaunchKernelGGL(prk::k_cs_class, dim3(ntiles), dim3(256), 0, s, offs, reinterpret_cast<uint2 *>(bins));
     return hipGetLastError();
 }
 

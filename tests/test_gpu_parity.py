@@ -194,6 +194,71 @@ def test_pipelined_frames_one_target(gpu):
     assert (gc == oc).all()
 
 
+def test_bin_capacity_rerun(gpu):
+    """Counting-sort binning sizes its per-pair arrays from the previous
+    frame's entry count; a frame with more entries leaves its bins empty and
+    is re-run.  Frames queued without a host sync: a small frame, an
+    over-capacity frame drawn over it, an over-capacity frame with a fused
+    clear, and a small frame over that."""
+    small = scenes.random_soup(3000, 512, 384, radius=16, seed=71)
+    big = scenes.random_soup(3000, 512, 384, radius=220, seed=72)
+    bigger = scenes.random_soup(6000, 512, 384, radius=300, seed=73)
+    small2 = scenes.random_soup(2000, 512, 384, radius=24, seed=74)
+    plan = [(small, True), (big, False), (bigger, True), (small2, False)]
+    r = prk.Renderer(0)
+    entries = []
+    try:
+        r.target_alloc(512, 384)
+        r.set_camera(small.prk_transform(), small.prk_lights())
+        tex = r.texture(small.texture)
+        geos = [r.geometry(s.vertices, s.colors, s.normals, s.uvs) for s, _ in plan]
+        for (s, clear), g in zip(plan, geos):
+            if clear:
+                r.clear_on_flush()
+            r.draw_model_optimized(g, s.tri_count, P=s.P, bitmap=tex, phong=True)
+            r.complete_all_work()
+            entries.append(r.stats()["bin_entries"])
+        r.synchronize()
+        gc, gz = r.download()
+    finally:
+        r.close()
+    assert entries[1] > 4 * entries[0] and entries[2] > entries[1], entries
+    for s, _ in plan:
+        s.texture = small.texture
+    oc, oz, _, _ = O.render(bigger)
+    oc, oz, _, _ = O.render(small2, color=oc, z=oz)
+    assert (gz.view(np.uint32) == oz.view(np.uint32)).all()
+    assert (gc == oc).all()
+
+
+def test_pipelined_identical_frames_and_band_rebind(gpu):
+    """Identical fused-clear frames queued back to back (every scratch set in
+    turn) end as the one frame; then the target is re-bound from a full frame
+    (two scratch sets) to a band small enough for three and back, frames
+    queued across each re-bind."""
+    s = scenes.random_soup(16000, 4096, 2048, radius=16, seed=81)
+    oc, oz, _, _ = O.render(s)
+    r = prk.Renderer(0)
+    try:
+        r.set_camera(s.prk_transform(), s.prk_lights())
+        g = r.geometry(s.vertices, s.colors, s.normals, s.uvs)
+        tex = r.texture(s.texture)
+        got = []
+        for rows in [(0, 2048), (0, 2048), (512, 1024), (0, 2048)]:  # 8 Mpx -> 2 sets, 2 Mpx -> 3 sets
+            r.target_alloc(4096, 2048, *rows)
+            for _ in range(5):
+                r.clear_on_flush()
+                r.draw_model_optimized(g, s.tri_count, P=s.P, bitmap=tex, phong=True)
+                r.complete_all_work()
+            r.synchronize()
+            got.append((rows, r.download()))
+    finally:
+        r.close()
+    for (r0, r1), (gc, gz) in got:
+        assert (gz.view(np.uint32) == oz[r0:r1].view(np.uint32)).all(), (r0, r1)
+        assert (gc == oc[r0:r1]).all(), (r0, r1)
+
+
 def test_draw_tables_change_between_frames(gpu):
     """Each scratch set re-sends its draw / texture tables only when their
     bytes change: frames that alternate geometry and texture on the same set
