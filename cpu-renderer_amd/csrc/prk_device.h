@@ -746,8 +746,11 @@ struct Walker {
         const bool three = n > 2 && i2 < min(min(h0, h1), h2);
         if (three || l0 + l1 + l2 != 2 * (stop - FirstRow)) return -1;
         const float ox0 = E0.X, ox1 = E1.X, ox2 = E2.X;
+#pragma unroll 4
         for (int32_t k = 0; k < l0; ++k) step_edge<M, NRM>(E0);
+#pragma unroll 4
         for (int32_t k = 0; k < l1; ++k) step_edge<M, NRM>(E1);
+#pragma unroll 4
         for (int32_t k = 0; k < l2; ++k) step_edge<M, NRM>(E2);
         // The pair of row stop-1 (exactly two of these hold).
         const bool act0 = E0.YMax >= stop, act1 = E1.YMax >= stop;

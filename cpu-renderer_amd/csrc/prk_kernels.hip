@@ -101,6 +101,12 @@ __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
 #ifndef PRK_LANE_ROWS
 #define PRK_LANE_ROWS 1  // sweeps: each lane walks its own rows (no row lock step across the wave)
 #endif
+#ifndef PRK_MULTI_ROWS
+#define PRK_MULTI_ROWS 1  // sweeps: lanes emit up to 8 rows per iteration when few lanes hold rows
+#endif
+#ifndef PRK_MULTI_ROWS_AVX
+#define PRK_MULTI_ROWS_AVX 4  // AVX sweeps: multi-row iterations only with at most this many active lanes
+#endif
 #ifndef PRK_VIS_GROUP
 #define PRK_VIS_GROUP 2  // visibility items: G consecutive pixels each (0: one lane chain each)
 #endif
@@ -246,7 +252,21 @@ __device__ __forceinline__ int span_setup_avx(const FrameParams &fp, const TileC
     return min(8, xb - xa);
 }
 
-// DrawModel span setup (projekt.cpp:298-412).  One item per span.
+// DrawModel spans are split into chunks of kScChunk pixels, one work item
+// each.  The span's recurrence is sequential per pixel (423-538: Current* +=
+// Increment after every pixel), so a chunk replays the adds (and, Phong, the
+// renormalisations) from MinX to its first pixel, then does the per-pixel work
+// of its own pixels only: a 200-px span costs its lanes one 200-step add chain
+// instead of one lane 200 z-tests / shades in sequence.
+template <bool SHADE>
+constexpr int kScChunk = SHADE ? 8 : 16;
+template <bool SHADE>
+__device__ __forceinline__ int scalar_chunks(int32_t xa, int32_t xb) {
+    return xa < xb ? (xb - xa + kScChunk<SHADE> - 1) / kScChunk<SHADE> : 0;
+}
+
+// DrawModel span setup (projekt.cpp:298-412).  Items: the span's chunks of
+// [xa, xb), plus one for the one-past-the-row pixel (SI_OVF).
 template <int M, bool SHADE, class WS>
 __device__ __forceinline__ int span_setup_scalar(const FrameParams &fp, const TileCtx &tc, WS &ws, int lane,
                                                  uint32_t tag, int32_t texi, const Edge &L, const Edge &R,
@@ -293,6 +313,7 @@ __device__ __forceinline__ int span_setup_scalar(const FrameParams &fp, const Ti
     const int32_t xb = in_rows ? min(MaxX + 1, tc.x1) : 0;
     const bool ovf = tc.x0 == 0 && MaxX >= W && Row + 1 >= tc.y0 && Row + 1 < tc.y1;
     if (xa >= xb && !ovf) return 0;
+    const int items = scalar_chunks<SHADE>(xa, xb) + (ovf ? 1 : 0);
     ws.i[SI_XA][lane] = xa;
     ws.i[SI_XB][lane] = xb;
     ws.i[SI_LEFT][lane] = MinX;
@@ -319,7 +340,7 @@ __device__ __forceinline__ int span_setup_scalar(const FrameParams &fp, const Ti
             ws.f[SS_C3][lane] = L.C3 + XOffset * IC3; ws.f[SS_IC3][lane] = IC3;
         }
     }
-    return 1;
+    return items;
 }
 
 // ----- work items ----------------------------------------------------------
@@ -566,20 +587,25 @@ __device__ __forceinline__ void item_avx_pixel(const FrameParams &fp, const Tile
                                                : shade_avx_texel(fp, t, z, n0, n1, n2, x, i, Row));
 }
 
-// A whole DrawModel span (projekt.cpp:423-538) restricted to the tile.
+// Chunk j of a DrawModel span (projekt.cpp:423-538) restricted to the tile:
+// pixels [xa + j*K, min(xa + (j+1)*K, xb)), or (j past the last chunk) the
+// one-past-the-row pixel x == W stored at (Row + 1, 0).
 template <int M, bool SHADE, bool UNI, class WS>
 __device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx &tc, const WS &ws, int s,
-                                            int32_t Row) {
+                                            int j, int32_t Row) {
     using TR = ModeTraits<M>;
+    constexpr int K = kScChunk<SHADE>;
     const int32_t W = fp.W;
     const int32_t xa = ws.i[SI_XA][s], xb = ws.i[SI_XB][s], MinX = ws.i[SI_LEFT][s];
     const uint32_t tag = (uint32_t)ws.i[SI_TAG][s];
     const int povf = ws.i[SI_OVF][s];
     const int rowoff = (Row - tc.y0) * tc.tw - tc.x0;
-    const int32_t xend = povf >= 0 ? W + 1 : xb;
+    const bool reg = j < scalar_chunks<SHADE>(xa, xb);
+    const int32_t cx0 = reg ? xa + j * K : W;
+    const int32_t cx1 = reg ? min(cx0 + K, xb) : W + 1;
     if (SHADE) {
-        bool any = povf >= 0 && is_winner(tc, povf, tag);
-        for (int32_t x = xa; x < xb; ++x) any |= is_winner(tc, rowoff + x, tag);
+        bool any = false;
+        for (int32_t x = cx0; x < cx1; ++x) any |= is_winner(tc, x == W ? povf : rowoff + x, tag);
         if (!any) return;
     }
     TexRec tex;
@@ -603,8 +629,23 @@ __device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx
             IC0 = ws.f[SS_IC0][s]; IC1 = ws.f[SS_IC1][s]; IC2 = ws.f[SS_IC2][s]; IC3 = ws.f[SS_IC3][s];
         }
     }
-    for (int32_t x = MinX; x < xend; ++x) {  // 423: sequential per-pixel stepping
-        if ((x >= xa && x < xb) || x == W) {
+    // The per-pixel steps of pixels [MinX, cx0) (504-510 / 530-535): the
+    // same adds in the same order as the reference's loop, nothing else.
+#pragma unroll 4
+    for (int32_t x = MinX; x < cx0; ++x) {
+        if (SHADE) {
+            if (TR::phong) {
+                float a = n0 + IN0, b = n1 + IN1, c = n2 + IN2;
+                normalize_rcp(a, b, c);
+                n0 = a; n1 = b; n2 = c;
+            }
+            if (TR::color) { c0 = c0 + IC0; c1 = c1 + IC1; c2 = c2 + IC2; c3 = c3 + IC3; }
+            if (TR::tex) { w += IW; u += IU; v += IV; }
+        }
+        z += IZ;
+    }
+    for (int32_t x = cx0; x < cx1; ++x) {  // 423: sequential per-pixel stepping
+        {
             const int p = x == W ? povf : rowoff + x;
             if (!SHADE) {
                 if (z == z) atomicMax(&tc.key[p], make_key(z, tag));
@@ -688,6 +729,13 @@ __device__ __forceinline__ int wave_incl_max(int v) {  // v >= 0
     v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));
     v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));
     return v;
+}
+
+// The wave's LDS writes are visible to all its lanes (no workgroup barrier).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // One sweep over the tile's bin for mode M.  SHADE=false: visibility keys;
@@ -815,18 +863,46 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
         // span's row travels in its slot); else all lanes step row r together.
         if (PRK_LANE_ROWS && active) active = wk.Row < tc.y1;
         for (int32_t r = ystart; PRK_LANE_ROWS || r < tc.y1; ++r) {
+            // Rows per lane this iteration: when few lanes still hold rows, each
+            // emits up to 8 of its next rows into the wave's 64 span slots
+            // (slot = rank among the active lanes * k + q), so the items of
+            // several rows share one window and the rows' per-pixel recurrences
+            // run side by side instead of one row after another.
+            int k = 1, rank = 0;
+            if (PRK_LANE_ROWS && PRK_MULTI_ROWS) {
+                const unsigned long long am = __ballot(active);
+                const int A = __popcll(am);
+                if (M != MODE_AVX) k = A <= 8 ? 8 : (A <= 16 ? 4 : (A <= 32 ? 2 : 1));
+                else k = A <= PRK_MULTI_ROWS_AVX ? 8 : 1;  // (AVX: only near-idle waves; C3b measured 2 % slower otherwise)
+                rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
+            }
+            const bool multi = k > 1;
             int items = 0;
-            if (active && (PRK_LANE_ROWS || wk.Row == r)) {
-                const int32_t row = wk.Row;
-                const bool paired = wk.begin_row();
-                if (paired) {
-                    const Edge &L = wk.S0, &R = wk.S1;
-                    if (M == MODE_AVX) items = span_setup_avx<SHADE>(fp, tc, ws, lane, tag, texi, L, R, row, st != 0);
-                    else items = span_setup_scalar<M, SHADE>(fp, tc, ws, lane, tag, texi, L, R, row);
-                    ws.i[SI_ROW][lane] = row;
+            if (multi) {  // per-slot item counts go through SI_PRE (rewritten after the scan)
+                ws.i[SI_PRE][lane] = 0;
+                wave_lds_sync();
+            }
+            for (int q = 0; q < k; ++q) {
+                if (active && (PRK_LANE_ROWS || wk.Row == r)) {
+                    const int slot = multi ? rank * k + q : lane;
+                    const int32_t row = wk.Row;
+                    const bool paired = wk.begin_row();
+                    if (paired) {
+                        const Edge &L = wk.S0, &R = wk.S1;
+                        int ni;
+                        if (M == MODE_AVX) ni = span_setup_avx<SHADE>(fp, tc, ws, slot, tag, texi, L, R, row, st != 0);
+                        else ni = span_setup_scalar<M, SHADE>(fp, tc, ws, slot, tag, texi, L, R, row);
+                        ws.i[SI_ROW][slot] = row;
+                        if (multi) ws.i[SI_PRE][slot] = ni;
+                        else items = ni;
+                    }
+                    wk.end_row(paired);
+                    active = wk.Row < wk.MaxY && (!PRK_LANE_ROWS || wk.Row < tc.y1);
                 }
-                wk.end_row(paired);
-                active = wk.Row < wk.MaxY && (!PRK_LANE_ROWS || wk.Row < tc.y1);
+            }
+            if (multi) {
+                wave_lds_sync();
+                items = ws.i[SI_PRE][lane];
             }
             if (PRK_PROF) { const unsigned long long t1 = PRK_T(); pt[1] += t1 - t0; t0 = t1; }
             const int incl = wave_incl_scan(items, lane);
@@ -857,7 +933,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
                     if constexpr (M == MODE_AVX && SHADE && PRK_PIXEL_ITEMS) item_avx_pixel<UNI>(fp, tc, ws, s, j, srow);
                     else if constexpr (M == MODE_AVX && !SHADE && PRK_VIS_GROUP > 0) item_vis_group(tc, ws, s, j, srow);
                     else if constexpr (M == MODE_AVX) item_avx<SHADE, UNI>(fp, tc, ws, s, j, srow);
-                    else item_scalar<M, SHADE, UNI>(fp, tc, ws, s, srow);
+                    else item_scalar<M, SHADE, UNI>(fp, tc, ws, s, j, srow);
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1138,11 +1214,6 @@ __device__ __forceinline__ void walk_flush(const FrameParams &fp, const WalkQueu
                 (rt >> 31) != 0);
 }
 
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // k_walk: one thread per triangle that won a pixel.  FillEdgeTable +
 // MergeSort once, then the triangle's whole AET walk (projekt.cpp:3615-3871,
