@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--cpu-max-tris", type=int, default=1_000_000,
                     help="bound on the CPU sample (triangles of the same scene)")
     ap.add_argument("--check", type=int, default=0, help="compare the frame with the oracle")
+    ap.add_argument("--comm", choices=("torch", "prk"), default="torch",
+                    help="N > 1 strip gather: torch.distributed P2P (RCCL) or the C-ABI's prk_gather_frame "
+                         "(RCCL from libprk_hip.so)")
     return ap.parse_args()
 
 
@@ -245,6 +248,13 @@ def main():
 
     pending = [[] for _ in range(nbuf)]
     nstep = [0]
+    comm = comm_stream = None
+    if a.comm == "prk":  # the C-ABI's RCCL gather (prk_comm_init / prk_gather_frame)
+        uid = [prk.comm_unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        comm = prk.Comm.init(r, uid[0], world, rank)
+        comm_stream = torch.cuda.Stream()
 
     def step():
         b = nstep[0] % nbuf
@@ -259,7 +269,16 @@ def main():
         r.clear_on_flush(0xFF000000, zmin)
         r.draw_model_optimized(geom, scene.tri_count, bitmap=tex, phong=True)
         r.complete_all_work(stream)
-        if world > 1:  # RCCL over xGMI: strips -> rank 0's frame
+        if world > 1 and comm is not None:  # prk_gather_frame on its own stream
+            ev = torch.cuda.Event()
+            ev.record()
+            comm_stream.wait_event(ev)
+            comm.gather(r, frames[b].data_ptr() if rank == 0 else None, None, with_z=False,
+                        stream=comm_stream.cuda_stream)
+            done = torch.cuda.Event()
+            done.record(comm_stream)
+            pending[b] = [done]  # Event.wait(): the render stream waits for it
+        elif world > 1:  # RCCL over xGMI: strips -> rank 0's frame
             _, pending[b] = pdist.gather_strips_start(dist, colors[b], rank, world, H, out=frames[b])
 
     def drain():
@@ -335,6 +354,8 @@ def main():
                      color_mismatch=int((gc != oc).sum()))
 
     if rank != 0:
+        if comm is not None:
+            comm.close()
         if dist is not None:
             dist.destroy_process_group()
         return
@@ -364,7 +385,9 @@ def main():
                                % (W, H, T, a.radius),
                    "width": W, "height": H, "triangles": T, "radius_px": a.radius,
                    "lights": len(scene.lights), "texture": "256x256",
-                   "parallelism": "row bands x%d + RCCL gather" % world if world > 1 else "1 GPU",
+                   "parallelism": ("row bands x%d + RCCL gather (%s)" % (world, "prk_gather_frame" if comm
+                                                                          else "torch.distributed")
+                                   if world > 1 else "1 GPU"),
                    "tile": a.tile or "256x8"},
         "mtri_per_s": T / (ms * 1e-3) / 1e6,
         # binning runs on its own stream, overlapping the previous frame's
@@ -405,6 +428,8 @@ def main():
     else:
         out["cpu_baseline"] = None
     print(json.dumps(out))
+    if comm is not None:
+        comm.close()
     r.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -1263,6 +1263,27 @@ int prk_flush(prk_context *c, void *stream) {
 }
 
 
+int prk_get_target(prk_context *c, void **color, int32_t *pitch_bytes, float **zbuf, int32_t *width,
+                   int32_t *height, int32_t *row0, int32_t *row1) {
+    if (!c) return PRK_ERR_ARG;
+    if (!c->color) return PRK_ERR_NO_TARGET;
+    if (color) *color = c->color;
+    if (pitch_bytes) *pitch_bytes = c->pitch;
+    if (zbuf) *zbuf = c->zbuf;
+    if (width) *width = c->W;
+    if (height) *height = c->H;
+    if (row0) *row0 = c->row0;
+    if (row1) *row1 = c->row1;
+    return PRK_OK;
+}
+
+int prk_get_device(prk_context *c, int32_t *device, void **stream) {
+    if (!c) return PRK_ERR_ARG;
+    if (device) *device = c->device;
+    if (stream) *stream = (void *)c->own_stream;
+    return PRK_OK;
+}
+
 int prk_synchronize(prk_context *c) {
     if (!c) return PRK_ERR_ARG;
     PRK_TRY(hipSetDevice(c->device));

@@ -80,7 +80,25 @@ _SIGS = {
     "prk_set_tile": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     "prk_construct_sphere": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.POINTER(C.c_uint32)]),
+    "prk_get_target": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int32), C.POINTER(C.c_void_p),
+                                 C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                 C.POINTER(C.c_int32)]),
+    "prk_get_device": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_void_p)]),
+    "prk_band_rows": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "prk_comm_available": (C.c_int, []),
+    "prk_comm_unique_id": (C.c_int, [C.c_void_p]),
+    "prk_comm_init": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    "prk_comm_init_all": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.POINTER(C.c_void_p)]),
+    "prk_comm_destroy": (C.c_int, [C.c_void_p]),
+    "prk_gather_frame": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p,
+                                   C.c_void_p]),
+    "prk_gather_frame_all": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_int32, C.c_int32,
+                                       C.c_void_p, C.c_int32, C.c_void_p]),
+    "prk_gather_frame_local": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.c_int32, C.c_void_p, C.c_int32,
+                                         C.c_void_p]),
 }
+
+COMM_ID_BYTES = 128  # PRK_COMM_ID_BYTES
 
 
 def exported_symbols():
@@ -128,6 +146,82 @@ def construct_sphere():
     _check("prk_construct_sphere", lib().prk_construct_sphere(_ptr(V), _ptr(Cc), _ptr(N), _ptr(UV),
                                                                C.byref(n)))
     return V[: n.value], Cc[: n.value], N[: n.value], UV[: n.value]
+
+
+def band_rows(height, rank, nranks):
+    """prk_band_rows: frame rows [row0, row1) of rank `rank` of `nranks`."""
+    a, b = C.c_int32(0), C.c_int32(0)
+    _check("prk_band_rows", lib().prk_band_rows(height, rank, nranks, C.byref(a), C.byref(b)))
+    return a.value, b.value
+
+
+def comm_available():
+    """True when librccl can be loaded (prk_comm_*)."""
+    return bool(lib().prk_comm_available())
+
+
+def comm_unique_id():
+    """prk_comm_unique_id (rank 0): the RCCL unique id as bytes."""
+    buf = (C.c_uint8 * COMM_ID_BYTES)()
+    _check("prk_comm_unique_id", lib().prk_comm_unique_id(buf))
+    return bytes(buf)
+
+
+class Comm:
+    """An RCCL communicator of one rank (prk_comm_init) or of one context of
+    a single-process group (Comm.init_all)."""
+
+    def __init__(self, handle, rank, nranks):
+        self._h, self.rank, self.nranks = handle, rank, nranks
+
+    @classmethod
+    def init(cls, renderer, uid, nranks, rank):
+        buf = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        _check("prk_comm_init", lib().prk_comm_init(renderer._h, buf, nranks, rank, C.byref(h)))
+        return cls(h, rank, nranks)
+
+    @classmethod
+    def init_all(cls, renderers):
+        n = len(renderers)
+        ctxs = (C.c_void_p * n)(*[r._h.value for r in renderers])
+        out = (C.c_void_p * n)()
+        _check("prk_comm_init_all", lib().prk_comm_init_all(ctxs, n, out))
+        return [cls(C.c_void_p(out[i]), i, n) for i in range(n)]
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().prk_comm_destroy(self._h)
+            self._h = None
+
+    def gather(self, renderer, frame_color_ptr=None, frame_z_ptr=None, with_z=False, stream=None):
+        """prk_gather_frame: rank 0 passes its device frame (packed rows),
+        the other ranks nothing."""
+        pitch = renderer.width * 4
+        _check("prk_gather_frame", lib().prk_gather_frame(
+            renderer._h, self._h, int(bool(with_z)), C.c_void_p(frame_color_ptr) if frame_color_ptr else None,
+            pitch, C.c_void_p(frame_z_ptr) if frame_z_ptr else None,
+            None if stream is None else C.c_void_p(stream)))
+
+
+def gather_frame_all(renderers, comms, frame_color_ptr, frame_z_ptr=None, with_z=False):
+    """prk_gather_frame_all: one process, N contexts, one RCCL group."""
+    n = len(renderers)
+    ctxs = (C.c_void_p * n)(*[r._h.value for r in renderers])
+    cms = (C.c_void_p * n)(*[c._h.value for c in comms])
+    _check("prk_gather_frame_all", lib().prk_gather_frame_all(
+        ctxs, cms, n, int(bool(with_z)), C.c_void_p(frame_color_ptr), renderers[0].width * 4,
+        C.c_void_p(frame_z_ptr) if frame_z_ptr else None))
+
+
+def gather_frame_local(renderers, frame_color_ptr, frame_pitch, frame_z_ptr=None, with_z=False):
+    """prk_gather_frame_local: every band's device copies its strip into
+    renderers[0]'s device frame (peer copies, no RCCL)."""
+    n = len(renderers)
+    ctxs = (C.c_void_p * n)(*[r._h.value for r in renderers])
+    _check("prk_gather_frame_local", lib().prk_gather_frame_local(
+        ctxs, n, int(bool(with_z)), C.c_void_p(frame_color_ptr), frame_pitch,
+        C.c_void_p(frame_z_ptr) if frame_z_ptr else None))
 
 
 class Renderer:
@@ -242,6 +336,20 @@ class Renderer:
         _check("prk_geometry_wrap_device", self._L.prk_geometry_wrap_device(self._h, *ptrs, vertex_count,
                                                                             C.byref(h)))
         return h.value
+
+    def target(self):
+        """prk_get_target: (color_ptr, pitch, z_ptr, W, H, row0, row1)."""
+        cp, zp = C.c_void_p(), C.c_void_p()
+        v = [C.c_int32(0) for _ in range(5)]
+        _check("prk_get_target", self._L.prk_get_target(self._h, C.byref(cp), C.byref(v[0]), C.byref(zp),
+                                                        *[C.byref(x) for x in v[1:]]))
+        return cp.value, v[0].value, zp.value, v[1].value, v[2].value, v[3].value, v[4].value
+
+    def device_stream(self):
+        """prk_get_device: (device, own stream as an int)."""
+        d, s = C.c_int32(0), C.c_void_p()
+        _check("prk_get_device", self._L.prk_get_device(self._h, C.byref(d), C.byref(s)))
+        return d.value, s.value or 0
 
     def set_tile(self, tw, th):
         _check("prk_set_tile", self._L.prk_set_tile(self._h, tw, th))

@@ -9,7 +9,10 @@ in submission order), so the only exchange is the final gather of the colour
 
 
 def band_rows(rank, world, height):
-    return height * rank // world, height * (rank + 1) // world
+    """Rank `rank`'s rows: the C-ABI's prk_band_rows, the same split the C++
+    drop-in (PRK_InitDevices) and prk_gather_frame use."""
+    from . import band_rows as c_band_rows
+    return c_band_rows(height, rank, world)
 
 
 def max_band_rows(world, height):

@@ -21,7 +21,7 @@
 // The texture is a loaded_bitmap of exactly Height rows whose last byte is
 // followed by an inaccessible page: a read past it faults.
 //
-// usage: dropin_demo <out_color.u32> <out_z.f32> [mode [file]]
+// usage: [PRK_DEMO_BANDS=n] dropin_demo <out_color.u32> <out_z.f32> [mode [file]]
 // exit: 0 ok, 1 usage, 2 no GPU / library error
 #include <sys/mman.h>
 #include <unistd.h>
@@ -68,7 +68,15 @@ int main(int argc, char **argv) {
         return 1;
     }
     const std::string mode = argc > 3 ? argv[3] : "queue";
-    if (PRK_Init(0) != PRK_OK) {
+    // PRK_DEMO_BANDS=n: the frame split into n row bands, one context each,
+    // on the visible GPUs round robin (several bands may share one GPU).
+    const char *nb = std::getenv("PRK_DEMO_BANDS");
+    const int bands = nb ? std::atoi(nb) : 1;
+    int ndev = 0;
+    prk_device_count(&ndev);
+    std::vector<int> devs(bands > 0 ? bands : 1);
+    for (size_t r = 0; r < devs.size(); ++r) devs[r] = ndev > 0 ? (int)r % ndev : 0;
+    if (PRK_InitDevices(devs.data(), (int)devs.size()) != PRK_OK) {
         std::fprintf(stderr, "dropin_demo: no HIP device (status %d)\n", PRK_LastStatus());
         return 2;
     }

@@ -273,6 +273,53 @@ int prk_download_winners(prk_context *ctx, int32_t *winners_host);
  * with -DPRK_PROF; zeroed by prk_timing_reset), n <= 16. */
 int prk_debug_counters(prk_context *ctx, uint64_t *out, int32_t n);
 
+/* The bound target (any pointer may be NULL) and the context's device and
+ * own stream (a hipStream_t; prk_flush(ctx, NULL) runs on it). */
+int prk_get_target(prk_context *ctx, void **color, int32_t *pitch_bytes, float **zbuf, int32_t *width,
+                   int32_t *height, int32_t *row0, int32_t *row1);
+int prk_get_device(prk_context *ctx, int32_t *device, void **stream);
+
+/* ---- Multi-GPU: row bands and the frame gather ------------
+ * The reference has no distribution; this is the build's.  Rank r of N binds
+ * (or allocates) a target for frame rows prk_band_rows(H, r, N) and records
+ * the same draws as every other rank: each rank bins all triangles against
+ * its band, so every pixel has one owner and submission order holds.  The
+ * only exchange is the gather of the band strips into one frame on rank 0
+ * (colour, and z when with_z).  A caller that wants the frame in host memory
+ * needs no gather: each rank downloads its band into its rows.
+ *
+ * One process per GPU: RCCL over xGMI.  Rank 0 makes a unique id
+ * (PRK_COMM_ID_BYTES bytes), the caller hands it to every rank (its own
+ * channel: MPI, a socket, torch.distributed ...), and every rank creates its
+ * communicator with prk_comm_init.  librccl is loaded on first use;
+ * PRK_ERR_UNSUPPORTED when it is absent (prk_comm_available() == 0). */
+#define PRK_COMM_ID_BYTES 128
+typedef struct prk_comm prk_comm;
+int prk_band_rows(int32_t height, int32_t rank, int32_t nranks, int32_t *row0, int32_t *row1);
+int prk_comm_available(void);
+int prk_comm_unique_id(void *id);
+int prk_comm_init(prk_context *ctx, const void *id, int32_t nranks, int32_t rank, prk_comm **out);
+/* One process driving N GPUs: one communicator per context (ncclCommInitAll). */
+int prk_comm_init_all(prk_context *const *ctxs, int32_t n, prk_comm **comms_out);
+int prk_comm_destroy(prk_comm *comm);
+/* Every rank's band into rank 0's device frame (W x H; colour rows of
+ * frame_pitch == 4*W bytes, z rows of W floats).  Rank 0 passes the frame,
+ * other ranks pass NULL (their bands must be packed: pitch 4*W).  Enqueued on
+ * `stream` (NULL: the context's own stream) after the work already there;
+ * rank 0's own band is copied unless its target is the frame's slice. */
+int prk_gather_frame(prk_context *ctx, prk_comm *comm, int32_t with_z, void *frame_color, int32_t frame_pitch,
+                     float *frame_z, void *stream);
+/* The same for N contexts of one process, as one RCCL group (ctxs[r] and
+ * comms[r] are rank r; each rank's ops go on its context's own stream). */
+int prk_gather_frame_all(prk_context *const *ctxs, prk_comm *const *comms, int32_t n, int32_t with_z,
+                         void *frame_color, int32_t frame_pitch, float *frame_z);
+/* One process driving N GPUs without RCCL: each band's device copies its
+ * strip into ctxs[0]'s frame over xGMI (peer access), after the work on its
+ * own stream; ctxs[0]'s own stream waits for every copy (prk_synchronize on
+ * ctxs[0] waits for the whole frame).  Contexts may share a device. */
+int prk_gather_frame_local(prk_context *const *ctxs, int32_t n, int32_t with_z, void *frame_color,
+                           int32_t frame_pitch, float *frame_z);
+
 /* Tunables (testing / benchmarking). tile_w must be a power of two >= 8,
  * 64 <= tile_w * tile_h <= 8192. */
 int prk_set_tile(prk_context *ctx, int32_t tile_w, int32_t tile_h);

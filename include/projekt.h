@@ -199,7 +199,8 @@ struct pending_draw {
 };
 
 struct state {
-    prk_context *Ctx = nullptr;
+    prk_context *Ctx = nullptr;         // band 0's context (and the one of a 1-GPU drop-in)
+    std::vector<prk_context *> Ctxs;    // one per GPU: context r renders rows prk_band_rows(H, r, N)
     int LastStatus = PRK_OK;
     // frame geometry: pinned staging arena (vertices), uploaded at CompleteAllWork
     float *AV = nullptr, *AC = nullptr, *AN = nullptr, *AUV = nullptr;
@@ -270,6 +271,32 @@ inline bool arena_reserve(state &st, uint32_t more) {
     return true;
 }
 
+// f(ctx) on every band's context in rank order; the first failing status.
+template <class F>
+inline int each(F &&f) {
+    for (prk_context *c : S().Ctxs) {
+        const int rc = f(c);
+        if (rc != PRK_OK) return rc;
+    }
+    return PRK_OK;
+}
+
+// f(ctx, first colour byte, first z float) of every band's rows of the
+// caller's buffers.
+template <class F>
+inline int each_band(loaded_bitmap *Buffer, game_render_commands *Commands, F &&f) {
+    const int n = (int)S().Ctxs.size();
+    for (int r = 0; r < n; ++r) {
+        int32_t a = 0, b = 0;
+        int rc = prk_band_rows(Buffer->Height, r, n, &a, &b);
+        if (rc == PRK_OK)
+            rc = f(S().Ctxs[r], (uint8_t *)Buffer->Memory + (size_t)a * Buffer->Pitch,
+                   Commands->ZBuffer ? Commands->ZBuffer + (size_t)a * Buffer->Width : nullptr);
+        if (rc != PRK_OK) return rc;
+    }
+    return PRK_OK;
+}
+
 // The bitmap as it is now: created on first use, re-read once per frame.
 inline int32_t texture_for(loaded_bitmap *Bitmap) {
     if (!Bitmap || !Bitmap->Memory) return -1;
@@ -278,13 +305,21 @@ inline int32_t texture_for(loaded_bitmap *Bitmap) {
     auto it = st.Textures.find(Bitmap->Memory);
     if (it != st.Textures.end()) {
         if (!st.TexFresh.count(it->second)) {
-            if (!ok(prk_texture_update(st.Ctx, it->second, &b))) return -1;
+            if (!ok(each([&](prk_context *c) { return prk_texture_update(c, it->second, &b); }))) return -1;
             st.TexFresh.insert(it->second);
         }
         return it->second;
     }
     int32_t h = -1;
-    if (!ok(prk_texture_create(st.Ctx, &b, &h))) return -1;
+    // every context creates its textures in the same order: same handles
+    if (!ok(each([&](prk_context *c) {
+            int32_t hc = -1;
+            const int rc = prk_texture_create(c, &b, &hc);
+            if (rc == PRK_OK && h >= 0 && hc != h) return (int)PRK_ERR_ARG;
+            h = hc;
+            return rc;
+        })))
+        return -1;
     st.Textures[Bitmap->Memory] = h;
     st.TexFresh.insert(h);
     return h;
@@ -305,7 +340,7 @@ inline void set_camera(game_render_commands *Commands) {
         for (int c = 0; c < 3; ++c) l.Lights[i].P[c] = Commands->LightData.Lights[i].P.E[c];
         for (int c = 0; c < 4; ++c) l.Lights[i].Intensity[c] = Commands->LightData.Lights[i].Intensity.E[c];
     }
-    ok(prk_set_camera(S().Ctx, &t, &l));
+    ok(each([&](prk_context *c) { return prk_set_camera(c, &t, &l); }));
 }
 
 inline void register_host(state &st, void *p, size_t bytes) {
@@ -332,17 +367,25 @@ inline bool open_frame(loaded_bitmap *Buffer, game_render_commands *Commands) {
         (Commands->Width != (u32)Buffer->Width))  // z rows are Commands->Width floats (170, 1511)
         return ok(PRK_ERR_ARG);
     if (Buffer->Width != st.TW || Buffer->Height != st.TH) {
-        if (!ok(prk_target_alloc(st.Ctx, Buffer->Width, Buffer->Height, 0, Buffer->Height, nullptr, nullptr)))
-            return false;
+        const int n = (int)st.Ctxs.size();
+        for (int r = 0; r < n; ++r) {
+            int32_t a = 0, b = 0;
+            if (!ok(prk_band_rows(Buffer->Height, r, n, &a, &b))) return false;
+            if (!ok(prk_target_alloc(st.Ctxs[r], Buffer->Width, Buffer->Height, a, b, nullptr, nullptr)))
+                return false;
+        }
         st.TW = Buffer->Width;
         st.TH = Buffer->Height;
     }
     register_host(st, Buffer->Memory, (size_t)Buffer->Pitch * Buffer->Height);
     if (Commands->ZBuffer) register_host(st, Commands->ZBuffer, (size_t)Buffer->Width * Buffer->Height * 4);
     if (st.ClearNext) {
-        if (!ok(prk_target_clear_on_flush(st.Ctx, st.ClearColor, st.ClearZ))) return false;
+        if (!ok(each([&](prk_context *c) { return prk_target_clear_on_flush(c, st.ClearColor, st.ClearZ); })))
+            return false;
         st.ClearNext = false;
-    } else if (!ok(prk_target_upload(st.Ctx, (const uint32_t *)Buffer->Memory, Buffer->Pitch, Commands->ZBuffer))) {
+    } else if (!ok(each_band(Buffer, Commands, [&](prk_context *c, uint8_t *col, float *z) {
+                   return prk_target_upload(c, (const uint32_t *)col, Buffer->Pitch, z);
+               }))) {
         return false;
     }
     st.Target = Buffer;
@@ -428,26 +471,39 @@ inline int issue(state &st) {
         // FillLineOptimized paths replace them by the texel (2029-2032)
         bool colors = st.Geom < 0;
         for (const pending_draw &d : st.Draws) colors |= d.Kind == DRAW_OBJECT && d.Semantics == PRK_SEM_SCALAR;
-        rc = st.Geom < 0 ? prk_geometry_create(st.Ctx, st.AV, st.AC, st.AN, st.AUV, st.ArenaUsed, &st.Geom)
-                         : prk_geometry_update(st.Ctx, st.Geom, st.AV, colors ? st.AC : nullptr, st.AN, st.AUV,
-                                               st.ArenaUsed);
+        const bool create = st.Geom < 0;
+        int32_t g = -1;
+        rc = each([&](prk_context *c) {
+            if (!create)
+                return prk_geometry_update(c, st.Geom, st.AV, colors ? st.AC : nullptr, st.AN, st.AUV, st.ArenaUsed);
+            int32_t gc = -1;
+            const int r = prk_geometry_create(c, st.AV, st.AC, st.AN, st.AUV, st.ArenaUsed, &gc);
+            if (r == PRK_OK && g >= 0 && gc != g) return (int)PRK_ERR_ARG;
+            g = gc;
+            return r;
+        });
         if (rc != PRK_OK) return rc;
+        if (create) st.Geom = g;
     }
-    for (const pending_draw &d : st.Draws) {
-        if (d.Kind == DRAW_OBJECT) {
-            const frame_object &o = st.Objects[d.First];
-            rc = prk_draw_objects(st.Ctx, st.Geom, o.FirstTri, o.Tris, o.Tris, o.P, d.Semantics, d.Phong, d.Texture);
-            if (rc == PRK_ERR_UNSUPPORTED && d.Semantics == PRK_SEM_SCALAR && o.Tris > 1)
-                // DrawModel's scalar whole-object AET is not emulated: per triangle
-                rc = prk_draw_objects(st.Ctx, st.Geom, o.FirstTri, o.Tris, 1, o.P, d.Semantics, d.Phong, d.Texture);
-        } else if (d.Kind == DRAW_EDGES) {
-            rc = prk_draw_edges(st.Ctx, st.Edges.data() + d.First, d.Count, d.Semantics, d.Phong, d.Texture);
-        } else {
-            rc = prk_draw_spans(st.Ctx, st.Spans.data() + d.First, d.Count, d.Semantics, d.Phong, d.Texture);
+    // every band records every draw (each bins all triangles against its rows)
+    return each([&](prk_context *c) {
+        int r = PRK_OK;
+        for (const pending_draw &d : st.Draws) {
+            if (d.Kind == DRAW_OBJECT) {
+                const frame_object &o = st.Objects[d.First];
+                r = prk_draw_objects(c, st.Geom, o.FirstTri, o.Tris, o.Tris, o.P, d.Semantics, d.Phong, d.Texture);
+                if (r == PRK_ERR_UNSUPPORTED && d.Semantics == PRK_SEM_SCALAR && o.Tris > 1)
+                    // DrawModel's scalar whole-object AET is not emulated: per triangle
+                    r = prk_draw_objects(c, st.Geom, o.FirstTri, o.Tris, 1, o.P, d.Semantics, d.Phong, d.Texture);
+            } else if (d.Kind == DRAW_EDGES) {
+                r = prk_draw_edges(c, st.Edges.data() + d.First, d.Count, d.Semantics, d.Phong, d.Texture);
+            } else {
+                r = prk_draw_spans(c, st.Spans.data() + d.First, d.Count, d.Semantics, d.Phong, d.Texture);
+            }
+            if (r != PRK_OK) return r;
         }
-        if (rc != PRK_OK) return rc;
-    }
-    return rc;
+        return r;
+    });
 }
 
 inline void end_frame(state &st) {
@@ -469,20 +525,35 @@ inline void end_frame(state &st) {
 }  // namespace prk_dropin
 
 // ---- platform hooks --------------------------------------------------------
-inline int PRK_Init(int device) {
+// Extension: the frame split into n row bands, band r rendered by GPU
+// devices[r] (a device may appear more than once); every band's colour and z
+// come back into the caller's buffers over that GPU's own link.
+inline int PRK_InitDevices(const int *devices, int n) {
     prk_dropin::state &st = prk_dropin::S();
     if (st.Ctx) return PRK_OK;
-    st.LastStatus = prk_create(device, &st.Ctx);
+    if (!devices || n <= 0) return st.LastStatus = PRK_ERR_ARG;
+    for (int r = 0; r < n; ++r) {
+        prk_context *c = nullptr;
+        st.LastStatus = prk_create(devices[r], &c);
+        if (st.LastStatus != PRK_OK) {
+            for (prk_context *k : st.Ctxs) prk_destroy(k);
+            st.Ctxs.clear();
+            return st.LastStatus;
+        }
+        st.Ctxs.push_back(c);
+    }
+    st.Ctx = st.Ctxs[0];
     return st.LastStatus;
 }
+inline int PRK_Init(int device) { return PRK_InitDevices(&device, 1); }
 inline int PRK_LastStatus() { return prk_dropin::S().LastStatus; }
 inline void PRK_Shutdown() {
     prk_dropin::state &st = prk_dropin::S();
     if (st.Ctx) {
-        prk_synchronize(st.Ctx);
+        for (prk_context *c : st.Ctxs) prk_synchronize(c);
         for (auto &r : st.Registered) prk_host_unregister(st.Ctx, r.first);
         prk_dropin::free_arena(st);
-        prk_destroy(st.Ctx);
+        for (prk_context *c : st.Ctxs) prk_destroy(c);
     }
     st = prk_dropin::state();
 }
@@ -499,10 +570,13 @@ inline int PRK_CompleteAllWork(loaded_bitmap *Buffer, game_render_commands *Comm
     prk_dropin::state &st = prk_dropin::S();
     if (!st.Ctx || !st.FrameOpen) return PRK_OK;
     int rc = prk_dropin::issue(st);
-    if (rc == PRK_OK) rc = prk_flush(st.Ctx, nullptr);
-    else prk_reset_draws(st.Ctx);
+    // all bands' frames are queued before the first download waits
+    if (rc == PRK_OK) rc = prk_dropin::each([](prk_context *c) { return prk_flush(c, nullptr); });
+    else prk_dropin::each([](prk_context *c) { return prk_reset_draws(c); });
     if (rc == PRK_OK)
-        rc = prk_target_download(st.Ctx, (uint32_t *)Buffer->Memory, Buffer->Pitch, Commands->ZBuffer);
+        rc = prk_dropin::each_band(Buffer, Commands, [&](prk_context *c, uint8_t *col, float *z) {
+            return prk_target_download(c, (uint32_t *)col, Buffer->Pitch, z);
+        });
     prk_dropin::end_frame(st);
     st.LastStatus = rc;
     return rc;

@@ -23,6 +23,19 @@ def free_port():
     return p
 
 
+def test_band_rows_c_abi():
+    """prk_band_rows (C-ABI) is the split r*H/N in 64-bit arithmetic and
+    rejects bad arguments."""
+    import prk
+    for world in (1, 2, 3, 5, 8):
+        for H in (1, 7, 150, 4096, 4097, 8192, 2**31 - 1):
+            for r in range(world):
+                assert prk.band_rows(H, r, world) == (H * r // world, H * (r + 1) // world)
+    for bad in ((0, 0, 1), (16, 2, 2), (16, -1, 2), (16, 0, 0)):
+        with pytest.raises(prk.PrkError):
+            prk.band_rows(*bad)
+
+
 def test_band_rows_partition():
     for world in (1, 2, 3, 8):
         for H in (150, 4096, 4097):

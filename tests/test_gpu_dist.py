@@ -1,0 +1,100 @@
+"""GPU: the C-ABI's multi-GPU path on one MI355X.
+
+Row bands rendered by separate contexts and gathered into one device frame
+must equal the single-context frame bit for bit:
+  * prk_gather_frame_local (peer copies; here every band's context shares
+    device 0, on a node each band is its own GPU),
+  * prk_gather_frame / prk_gather_frame_all over RCCL with one rank (a one-GPU
+    box cannot host two RCCL ranks: RCCL rejects two ranks on one device), so
+    the communicator set-up, the group and rank 0's own-band copy run; the
+    peer sends and receives run only on the 8-GPU node.
+"""
+import numpy as np
+import pytest
+
+import prk
+from prk import abi, scenes
+
+pytestmark = pytest.mark.gpu
+
+
+def _band_renderers(s, n, devices=None):
+    rs = []
+    for r in range(n):
+        R = prk.Renderer(0 if devices is None else devices[r])
+        a, b = prk.band_rows(s.height, r, n)
+        R.target_alloc(s.width, s.height, a, b)
+        R.clear_on_flush()
+        R.set_camera(s.prk_transform(), s.prk_lights())
+        g = R.geometry(s.vertices, s.colors, s.normals, s.uvs)
+        t = R.texture(s.texture)
+        R.draw_model_optimized(g, s.tri_count, bitmap=t)
+        R.complete_all_work()
+        rs.append(R)
+    return rs
+
+
+def _frame(s):
+    F = prk.Renderer(0)
+    F.target_alloc(s.width, s.height)
+    return F
+
+
+@pytest.fixture(scope="module")
+def scene_ref():
+    s = scenes.random_soup(20000, 512, 384, radius=24, seed=41)
+    col, z, _, _ = prk.render_scene(s, debug=False, fused_clear=True)
+    return s, col, z
+
+
+@pytest.mark.parametrize("n", [2, 3, 5])
+def test_gather_frame_local(gpu, scene_ref, n):
+    s, col, z = scene_ref
+    rs = _band_renderers(s, n)
+    F = _frame(s)
+    cp, pitch, zp, *_ = F.target()
+    prk.gather_frame_local(rs, cp, pitch, zp, with_z=True)
+    rs[0].synchronize()
+    gc, gz = F.download()
+    assert (gc == col).all() and (gz.view(np.uint32) == z.view(np.uint32)).all()
+    for R in rs + [F]:
+        R.close()
+
+
+def test_gather_frame_rccl_one_rank(gpu, scene_ref):
+    if not prk.comm_available():
+        pytest.fail("librccl did not load")
+    s, col, z = scene_ref
+    (R,) = _band_renderers(s, 1)
+    F = _frame(s)
+    cp, _, zp, *_ = F.target()
+    c = prk.Comm.init(R, prk.comm_unique_id(), 1, 0)
+    c.gather(R, cp, zp, with_z=True)
+    R.synchronize()
+    gc, gz = F.download()
+    assert (gc == col).all() and (gz.view(np.uint32) == z.view(np.uint32)).all()
+    c.close()
+    # the single-process group form (ncclCommInitAll)
+    (c1,) = prk.Comm.init_all([R])
+    F2 = _frame(s)
+    cp2, _, zp2, *_ = F2.target()
+    prk.gather_frame_all([R], [c1], cp2, zp2, with_z=True)
+    R.synchronize()
+    gc2, gz2 = F2.download()
+    assert (gc2 == col).all() and (gz2.view(np.uint32) == z.view(np.uint32)).all()
+    c1.close()
+    for x in (R, F, F2):
+        x.close()
+
+
+def test_gather_rejects_wrong_band(gpu, scene_ref):
+    s, _, _ = scene_ref
+    rs = _band_renderers(s, 2)
+    F = _frame(s)
+    cp, pitch, zp, *_ = F.target()
+    with pytest.raises(prk.PrkError):  # bands in the wrong order
+        prk.gather_frame_local([rs[1], rs[0]], cp, pitch, zp, with_z=True)
+    with pytest.raises(prk.PrkError):  # z asked for, no z frame
+        prk.gather_frame_local(rs, cp, pitch, None, with_z=True)
+    for R in rs + [F]:
+        R.close()

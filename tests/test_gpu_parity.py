@@ -530,14 +530,18 @@ def _dropin_scene(textured=True, salt=0):
 DROPIN_MODES = ["queue", "lines", "st", "scalar", "object", "mutate", "edges", "work"]
 
 
-@pytest.mark.parametrize("mode", DROPIN_MODES)
-def test_dropin_demo_matches_oracle(gpu, tmp_path, mode):
+@pytest.mark.parametrize("mode,bands", [(m, 1) for m in DROPIN_MODES] +
+                         [("queue", 3), ("object", 2), ("mutate", 3), ("scalar", 3), ("work", 2)])
+def test_dropin_demo_matches_oracle(gpu, tmp_path, mode, bands):
     """examples/dropin_demo.cpp drives the reference's own entry points
     through include/projekt.h (FillEdgeTable, DrawModelOptimized(RenderQueue),
     DrawModelOptimizedLines, the single-thread DrawModelOptimized, DrawModel,
     the three work-queue callbacks, a caller-built edge list, vertices and a
     texture rewritten in place between frames; its texture ends at an
-    inaccessible page).  Its framebuffer must equal the oracle's."""
+    inaccessible page).  Its framebuffer must equal the oracle's.  bands > 1:
+    the drop-in splits the frame into row bands, one context each
+    (PRK_InitDevices; on a one-GPU box they share the GPU), every band
+    downloaded into its rows of the caller's buffers."""
     import os
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -575,7 +579,8 @@ def test_dropin_demo_matches_oracle(gpu, tmp_path, mode):
         w.tofile(tmp_path / "spans.u32")
         extra = [str(tmp_path / "spans.u32")]
     args = [str(exe), str(tmp_path / "c.u32"), str(tmp_path / "z.f32"), mode] + extra
-    run = subprocess.run(args, capture_output=True, text=True, timeout=120)
+    env = dict(os.environ, PRK_DEMO_BANDS=str(bands))
+    run = subprocess.run(args, capture_output=True, text=True, timeout=120, env=env)
     assert run.returncode == 0, run.stderr
     gc = np.fromfile(tmp_path / "c.u32", np.uint32).reshape(256, 256)
     gz = np.fromfile(tmp_path / "z.f32", np.float32).reshape(256, 256)
