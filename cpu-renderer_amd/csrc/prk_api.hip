@@ -58,8 +58,8 @@ struct ObjDesc {
 // PRK_SPAN_RECORDS of prk_kernels.hip.
 #define PRK_SPAN_RECORDS_HOST 1
 // Per-frame scratch sets in flight: a frame whose target band has at most
-// kSmallBandPx pixels cycles PRK_FRAME_SETS sets (frame k: set k % 3),
-// larger ones 2: with three, frame k+1's binning need not wait for
+// kSmallBandPx pixels cycles PRK_FRAME_SETS sets, larger ones 2 (the set
+// count nsets; consecutive frames take consecutive sets): with three, frame k+1's binning need not wait for
 // frame k-1's raster, which pays when binning is a large share of the frame
 // (band of 512 x 4096 px, one rank of 8: 0.284 -> 0.247 ms; 1024 rows:
 // 0.405 -> 0.378) and costs ~1-3 % on bigger frames, where the extra
@@ -135,8 +135,9 @@ struct prk_context {
     uint32_t pending_tris = 0;
     std::vector<prk_edge> pend_edges;  // prk_draw_edges input of the pending frame
     std::vector<prk_span> pend_spans;  // prk_draw_spans input of the pending frame
-    // Per-frame scratch, two sets: frame k bins (and, on span-record frames,
-    // runs k_vis) into set k % 2 on bin_stream while frame k-1 shades on the
+    // Per-frame scratch, nsets of them in use (2, or PRK_FRAME_SETS for small
+    // bands): frame k bins (and, on span-record frames, runs k_vis) into the
+    // set after frame k-1's on bin_stream while frame k-1 shades on the
     // flush's stream.
     struct BinSet {
         DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_tri_n, d_tri_off, d_pair_tri, d_keys_a, d_vals_a, d_keys_b,
@@ -872,7 +873,7 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
         }
     } guard{B};
     hipStream_t bs = c->bin_stream;
-    if (B.used) PRK_TRY(hipStreamWaitEvent(bs, B.free_ev, 0));  // the raster of frame k-2 read this set
+    if (B.used) PRK_TRY(hipStreamWaitEvent(bs, B.free_ev, 0));  // the raster of frame k-nsets read this set
     // A set buffer that must grow is freed by the host: wait for its reader.
     auto bset_ensure = [&](DevBuf &d, size_t n) -> hipError_t {
         if (d.cap < n && B.used) {
@@ -891,7 +892,7 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
         texs[i].filter = c->texs[i].filter;
     }
     // Upload a table into this set unless the set already holds the same
-    // bytes (the set's previous reader, frame k-2's raster, is waited for above).
+    // bytes (the set's previous reader, frame k-nsets's raster, is waited for above).
     auto upload_table = [&](DevBuf &d, std::vector<uint8_t> &mirror, const void *&at, const void *src,
                             size_t bytes) -> hipError_t {
         hipError_t e = bset_ensure(d, bytes);
