@@ -142,7 +142,7 @@ struct prk_context {
     struct BinSet {
         DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_tri_n, d_tri_off, d_pair_tri, d_keys_a, d_vals_a, d_keys_b,
             d_bins, d_offs, d_temp, d_won, d_list, d_nwin, d_wtag, d_recs, d_trwon, d_wlist, d_seltemp, d_trec,
-            d_nrec, d_ghist, d_tile_tot, d_chunk, d_info;
+            d_ghist, d_tile_tot, d_chunk, d_info;
         uint32_t *h_info = nullptr;       // pinned: [entry count, overflow] of the set's last binning
         hipEvent_t counted_ev = nullptr;  // h_info of this set's binning has landed
         // bytes last uploaded into d_draws / d_texs and the buffer they went
@@ -261,7 +261,7 @@ int prk_destroy(prk_context *c) {
         DevBuf *bb[] = {&B.d_draws, &B.d_texs, &B.d_tri_draw, &B.d_ranges, &B.d_tri_n, &B.d_tri_off, &B.d_pair_tri,
                         &B.d_keys_a, &B.d_vals_a, &B.d_keys_b, &B.d_bins, &B.d_offs, &B.d_temp, &B.d_won,
                         &B.d_list, &B.d_nwin, &B.d_wtag, &B.d_recs, &B.d_trwon, &B.d_wlist, &B.d_seltemp,
-                        &B.d_trec, &B.d_nrec, &B.d_ghist, &B.d_tile_tot, &B.d_chunk, &B.d_info};
+                        &B.d_trec, &B.d_ghist, &B.d_tile_tot, &B.d_chunk, &B.d_info};
         for (DevBuf *b : bb) b->release();
         if (B.free_ev) (void)hipEventDestroy(B.free_ev);
         if (B.binned_ev) (void)hipEventDestroy(B.binned_ev);
@@ -925,12 +925,9 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
     PRK_TRY(bset_ensure(B.d_tri_off, (size_t)(T + 1) * 4));
     PRK_TRY(bset_ensure(B.d_offs, (size_t)(ntiles + 1) * 4));
     fp.trec = nullptr;
-    fp.nrec = nullptr;
     if (modeset == prk::MODE_AVX && c->setup_rec) {
         PRK_TRY(bset_ensure(B.d_trec, (size_t)T * sizeof(prk::TriRec)));
-        PRK_TRY(bset_ensure(B.d_nrec, (size_t)T * sizeof(prk::NrmRec)));
         fp.trec = (prk::TriRec *)B.d_trec.p;
-        fp.nrec = (prk::NrmRec *)B.d_nrec.p;
     }
     const bool span_rec = modeset == prk::MODE_AVX;
     // won flags: per (pair, row in tile) for span-record (AVX) frames, per

@@ -117,7 +117,6 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_count(FrameParams fp, uin
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     bool rec = false;
     TriRec r;
-    NrmRec q;
     if (g < fp.tri_count) {
         TileRange tr;
         if (!tri_tile_range(fp, g, tr)) {
@@ -128,7 +127,7 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_count(FrameParams fp, uin
         tri_n[g] = ne;
         if (fp.trec && ne) {
             // All-AVX frame: FillEdgeTable + MergeSort + the first row's AET
-            // insertions once per triangle (TriRec / NrmRec, prk_device.h).
+            // insertions once per triangle (TriRec, prk_device.h).
             const DrawRec *d;
             uint32_t gt;
             resolve_draw(fp, g, d, gt);
@@ -144,11 +143,8 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_count(FrameParams fp, uin
             rec_edge_out(s2, r.e[2], r.ymin[2], r.ymax[2]);
             r.head = (uint32_t)n | (w.ord << 4) | ((uint32_t)w.cnt << 12) | ((uint32_t)(w.pend + 1) << 16) |
                      (min(anom, 15u) << 20) | ((d->flags & DRAW_ST) ? (1u << 24) : 0u);
-            r.pad[0] = r.pad[1] = r.pad[2] = 0;
-            nrm_edge_out(s0, q.n[0]);
-            nrm_edge_out(s1, q.n[1]);
-            nrm_edge_out(s2, q.n[2]);
-            q.pad[0] = q.pad[1] = 0.0f;
+            r.vtx = (uint32_t)s0.Vtx | ((uint32_t)s1.Vtx << 4) | ((uint32_t)s2.Vtx << 8);
+            r.pad[0] = r.pad[1] = 0;
             rec = true;
         }
     } else if (g == fp.tri_count) {
@@ -172,16 +168,6 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_count(FrameParams fp, uin
     float4 *dr = reinterpret_cast<float4 *>(fp.trec + gw);
     for (int c = lane; c < 64 * 10; c += 64)
         if ((mask >> (c / 10)) & 1) dr[c] = st[c];
-    wave_sync();
-    if (rec) {
-        const float4 *sq = reinterpret_cast<const float4 *>(&q);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) st[lane * 5 + k] = sq[k];
-    }
-    wave_sync();
-    float4 *dq = reinterpret_cast<float4 *>(fp.nrec + gw);
-    for (int c = lane; c < 64 * 5; c += 64)
-        if ((mask >> (c / 5)) & 1) dq[c] = st[c];
 }
 
 // Sort key = tile << kRowClassBits | row class: within a tile's bin the

@@ -79,21 +79,19 @@ struct TexRec {
 // triangle in k_vis and by k_walk: FillEdgeTable (projekt.cpp:3882-4121) +
 // MergeSort (2-72) + the AET insertions of the triangle's first row
 // (3654-3713), so no raster kernel repeats the ~30 divisions of the setup.
-// TriRec holds what the visibility sweep reads (160 B), NrmRec the normals
-// only the shading walk reads (80 B).
+// TriRec holds what the visibility sweep reads (160 B) plus, for the shading
+// walk, which vertices each sorted edge joins: k_walk rebuilds the edges'
+// normals (4014-4019, 4103-4108: no top clip) from the triangle's three vertex
+// normals, which costs it a 36-B read instead of an 80-B record per triangle.
 struct TriRec {
     float e[3][10];      // sorted edge k: X, G, Z, ZG, W, WG, U, UG, V, VG
     int32_t ymin[3];     // YMin | Left << 31 (YMin >= 0: Maximum(0, .), 3999)
     int32_t ymax[3];
     uint32_t head;       // n | ord << 4 | cnt << 12 | (pend + 1) << 16 | anomaly << 20 | st << 24
-    uint32_t pad[3];
+    uint32_t vtx;        // sorted edge k's Vtx (mi | ma << 2) at bits 4k
+    uint32_t pad[2];
 };
 static_assert(sizeof(TriRec) == 160, "TriRec is ten dwordx4");
-struct NrmRec {
-    float n[3][6];       // sorted edge k: N0, N1, N2, NG0, NG1, NG2
-    float pad[2];
-};
-static_assert(sizeof(NrmRec) == 80, "NrmRec is five dwordx4");
 
 struct FrameParams {
     // projective_transform
@@ -133,7 +131,6 @@ struct FrameParams {
     // Setup records (all-AVX frames; nullptr otherwise): written by
     // k_bin_count for every binned triangle, read by k_vis / k_walk.
     TriRec *trec;
-    NrmRec *nrec;
 };
 
 // d / FocalLength of UnprojectVertex(_8x) (projekt.cpp:141-142, 157).  When
@@ -237,6 +234,7 @@ struct Edge {
     float N0, N1, N2, NG0, NG1, NG2;
     float C0, C1, C2, C3, CG0, CG1, CG2, CG3;
     int32_t YMin, YMax, Left;
+    int32_t Vtx;  // the edge's (Min, Max) vertex of its triangle: mi | ma << 2 (setup records)
 };
 
 __device__ __forceinline__ Edge sel(bool c, const Edge &a, const Edge &b) {
@@ -250,6 +248,7 @@ __device__ __forceinline__ Edge sel(bool c, const Edge &a, const Edge &b) {
     r.CG0 = c ? a.CG0 : b.CG0; r.CG1 = c ? a.CG1 : b.CG1; r.CG2 = c ? a.CG2 : b.CG2;
     r.CG3 = c ? a.CG3 : b.CG3;
     r.YMin = c ? a.YMin : b.YMin; r.YMax = c ? a.YMax : b.YMax; r.Left = c ? a.Left : b.Left;
+    r.Vtx = c ? a.Vtx : b.Vtx;
     return r;
 }
 
@@ -483,6 +482,7 @@ __device__ __forceinline__ void tri_edges(const TriRaw<M> &r, const DrawRec &d, 
             E.NG2 = (MaxN[2] - E.N2) / YDiff;
         }
         E.Left = (E.YMin == round_s32(proj[i0].y)) ? 1 : 0;  // 4093
+        E.Vtx = mi | (ma << 2);
         if (ei == 0) e0 = E; else if (ei == 1) e1 = E; else e2 = E;
     }
 }
@@ -534,9 +534,6 @@ __device__ __forceinline__ void rec_edge_out(const Edge &E, float *f, int32_t &y
     ymin = (int32_t)((uint32_t)E.YMin | ((uint32_t)(E.Left != 0) << 31));
     ymax = E.YMax;
 }
-__device__ __forceinline__ void nrm_edge_out(const Edge &E, float *f) {
-    f[0] = E.N0; f[1] = E.N1; f[2] = E.N2; f[3] = E.NG0; f[4] = E.NG1; f[5] = E.NG2;
-}
 __device__ __forceinline__ Edge rec_edge_in(const float *f, int32_t ymin, int32_t ymax) {
     Edge E;
     E.X = f[0]; E.G = f[1]; E.Z = f[2]; E.ZG = f[3]; E.W = f[4];
@@ -548,8 +545,16 @@ __device__ __forceinline__ Edge rec_edge_in(const float *f, int32_t ymin, int32_
     E.YMax = ymax;
     return E;
 }
-__device__ __forceinline__ void nrm_edge_in(Edge &E, const float *f) {
-    E.N0 = f[0]; E.N1 = f[1]; E.N2 = f[2]; E.NG0 = f[3]; E.NG1 = f[4]; E.NG2 = f[5];
+// The normals of a sorted edge from its triangle's vertex normals n[9]
+// (FillEdgeTable 4014-4019, 4103-4108: MinNormal = the Min vertex's normal,
+// no top clip; NormalGradient = (MaxNormal - MinNormal) / YDiff).
+__device__ __forceinline__ void nrm_edge_from(Edge &E, uint32_t vtx, const float *n) {
+    const int mi = (int)(vtx & 3u), ma = (int)((vtx >> 2) & 3u);
+    const float YDiff = (float)E.YMax - (float)E.YMin;
+    E.N0 = n[3 * mi + 0]; E.N1 = n[3 * mi + 1]; E.N2 = n[3 * mi + 2];
+    E.NG0 = (n[3 * ma + 0] - E.N0) / YDiff;
+    E.NG1 = (n[3 * ma + 1] - E.N1) / YDiff;
+    E.NG2 = (n[3 * ma + 2] - E.N2) / YDiff;
 }
 
 // AET edge step (projekt.cpp:3811-3829), only the fields mode M reads

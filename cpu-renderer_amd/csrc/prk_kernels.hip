@@ -682,7 +682,14 @@ __device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx
                         float Hx = Lx + Vx, Hy = Ly + Vy, Hz = Lz + Vz;
                         normalize_rcp(Hx, Hy, Hz);
                         float Ph = clamp01((n0 * Hx + n1 * Hy) + n2 * Hz);
-                        Ph = (float)pow((double)Ph, 16.0);
+                        // pow((double)Ph, 16.0) (473) as four exact-range
+                        // double squarings: within 2 ulp(double) of any libm's
+                        // pow, the same float after the cast except within
+                        // ~2^-50 of a float rounding boundary (the ±1 LSB of
+                        // the scalar Phong contract); no f64 log/exp.
+                        double ph = (double)Ph;
+                        ph = ph * ph; ph = ph * ph; ph = ph * ph; ph = ph * ph;
+                        Ph = (float)ph;
                         for (int c = 0; c < 4; ++c)
                             F[c] = F[c] + ((Cos * (C[c] * fp.li[li][c])) + (Ph * (1.0f * fp.li[li][c])));
                     }
@@ -1246,34 +1253,32 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
         Edge s0, s1, s2;
         int ne;
         uint32_t rhead = 0;
-        if constexpr (PRK_SETUP_REC) {  // the binning pass's setup records (TriRec + NrmRec)
+        if constexpr (PRK_SETUP_REC) {  // the binning pass's setup record + the vertex normals
             const float4 *q = reinterpret_cast<const float4 *>(fp.trec + g);
-            const float4 *qn = reinterpret_cast<const float4 *>(fp.nrec + g);
-            float4 v[10], vn[5];
+            float4 v[10];
 #pragma unroll
             for (int k = 0; k < 10; ++k) v[k] = q[k];
+            const DrawRec *d = &fp.draw0;
+            uint32_t gt;
+            if constexpr (UNI) gt = fp.draw0.geom_tri0 + (g - fp.draw0.first_global);
+            else resolve_draw(fp, g, d, gt);
+            texi = d->tex;
+            const float *nv = d->N + 9 * (size_t)gt;
+            float n[9];
 #pragma unroll
-            for (int k = 0; k < 5; ++k) vn[k] = qn[k];
+            for (int k = 0; k < 9; ++k) n[k] = nv[k];
             const float *f = reinterpret_cast<const float *>(v);
             const int32_t *iw = reinterpret_cast<const int32_t *>(v);
-            const float *fn = reinterpret_cast<const float *>(vn);
             s0 = rec_edge_in(f + 0, iw[30], iw[33]);
             s1 = rec_edge_in(f + 10, iw[31], iw[34]);
             s2 = rec_edge_in(f + 20, iw[32], iw[35]);
-            nrm_edge_in(s0, fn + 0);
-            nrm_edge_in(s1, fn + 6);
-            nrm_edge_in(s2, fn + 12);
+            const uint32_t vtx = (uint32_t)iw[37];
+            nrm_edge_from(s0, vtx, n);
+            nrm_edge_from(s1, vtx >> 4, n);
+            nrm_edge_from(s2, vtx >> 8, n);
             rhead = (uint32_t)iw[36];
             ne = (int)(rhead & 0xFu);
             st = (rhead >> 24) & 1u;
-            if constexpr (UNI) {
-                texi = fp.draw0.tex;
-            } else {
-                const DrawRec *d;
-                uint32_t gt;
-                resolve_draw(fp, g, d, gt);
-                texi = d->tex;
-            }
         } else if constexpr (UNI) {
             ne = setup_triangle<M>(fp.draw0, fp.draw0.geom_tri0 + (g - fp.draw0.first_global), fp, s0, s1, s2);
             texi = fp.draw0.tex;
