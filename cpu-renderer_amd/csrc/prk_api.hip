@@ -38,6 +38,7 @@ hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, co
                              uint32_t *, uint32_t *, uint32_t *, void *, uint32_t *, hipEvent_t, hipEvent_t,
                              hipStream_t, hipStream_t);
 hipError_t prk_walk_select_bytes(uint32_t, size_t *);
+hipError_t prk_selftest_div_launch(uint32_t n, uint64_t seed, unsigned long long *bad, hipStream_t s);
 hipError_t prk_obj_walk(const prk::FrameParams *, const void *, uint32_t, void *, uint32_t *, uint32_t *, int,
                         uint32_t *, const uint32_t *, void *, void *, uint32_t *, const void *, const void *,
                         hipStream_t);
@@ -202,6 +203,23 @@ int prk_device_count(int *out) {
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess) n = 0;
     *out = n;
+    return PRK_OK;
+}
+
+// Self-test of the shared-divisor quotients against the compiler's division
+// (prk.h).  Runs on `device`, synchronously.
+int prk_selftest_div(int32_t device, uint32_t n, uint64_t seed, uint64_t *mismatches) {
+    if (!mismatches || device < 0) return PRK_ERR_ARG;
+    PRK_TRY(hipSetDevice(device));
+    unsigned long long *d = nullptr;
+    PRK_TRY(hipMalloc(&d, sizeof(unsigned long long)));
+    hipError_t e = hipMemset(d, 0, sizeof(unsigned long long));
+    if (e == hipSuccess) e = prk_selftest_div_launch(n, seed, d, nullptr);
+    unsigned long long h = 0;
+    if (e == hipSuccess) e = hipMemcpy(&h, d, sizeof(h), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return status_of(e);
+    *mismatches = h;
     return PRK_OK;
 }
 

@@ -256,7 +256,13 @@ constexpr int kCsThreads = 1024;
 constexpr uint32_t kCsTrisPerThread = 4;
 constexpr uint32_t kCsChunk = kCsThreads * kCsTrisPerThread;
 constexpr uint32_t kCsMaxTiles = 32768;  // LDS: one u32 per tile (128 KiB)
-constexpr uint32_t kCsClassShift = 29;   // row class in bits 29-31 of the emitted pair index
+#ifndef PRK_REPCLASS
+#define PRK_REPCLASS 0  // 1: bins also grouped by how many tile rows of the triangle lie above the
+                        // tile (its replay length); measured k_vis +6 % on C3b (0.497 -> 0.528 ms)
+#endif
+constexpr int kRepClassBits = PRK_REPCLASS ? 2 : 0;
+constexpr int kClassBits = kRowClassBits + kRepClassBits;
+constexpr uint32_t kCsClassShift = 32 - kClassBits;  // (replay, row) class in the top bits of the emitted pair index
 constexpr uint32_t kCsPairMask = (1u << kCsClassShift) - 1u;
 constexpr int kCsClassWindow = 2048;     // k_cs_class: entries grouped per pass
 
@@ -288,21 +294,28 @@ __device__ __forceinline__ uint32_t cs_block_excl_scan(uint32_t v, uint32_t *scr
     return before + incl - v;
 }
 
-// The (tile, row class) of every entry of a range, in pair order: the
-// rectangle row-major, then the column-0 overflow tiles not in it.
+// The (tile, class) of every entry of a range, in pair order: the rectangle
+// row-major, then the column-0 overflow tiles not in it.  Class = the rows
+// of the tile the triangle can cover (k_vis's row walk) and, above it, how
+// many tile rows of the triangle lie above the tile (its replay of the rows
+// above: 0, 1, 2, 3+), so the 64 entries of a k_vis wave walk and replay
+// about as many rows each.
 template <class F>
 __device__ __forceinline__ void for_each_entry(const FrameParams &fp, const TileRange &tr, F &&f) {
     constexpr int kMaxClass = (1 << kRowClassBits) - 1;
+    constexpr int kMaxRep = (1 << kRepClassBits) - 1;
     if (tr.tx0 <= tr.tx1 && tr.ty0 <= tr.ty1)
         for (int ty = tr.ty0; ty <= tr.ty1; ++ty) {
             const int y0 = ty * fp.tile_h;
             const int rows = min((int)tr.pad1, y0 + fp.tile_h) - max((int)tr.pad0, y0);
-            const uint32_t cls = PRK_ROWCLASS ? (uint32_t)min(kMaxClass, max(0, fp.tile_h - rows)) : 0u;
+            uint32_t cls = PRK_ROWCLASS ? (uint32_t)min(kMaxClass, max(0, fp.tile_h - rows)) : 0u;
+            const int rep = max(0, y0 - (int)tr.pad0);
+            cls |= (uint32_t)min(kMaxRep, (rep + fp.tile_h - 1) / fp.tile_h) << kRowClassBits;
             for (int tx = tr.tx0; tx <= tr.tx1; ++tx) f((uint32_t)(ty * fp.tiles_x + tx), cls);
         }
     for (int ty = tr.oty0; ty <= tr.oty1; ++ty)
         if (!(tr.tx0 == 0 && tr.tx0 <= tr.tx1 && ty >= tr.ty0 && ty <= tr.ty1))
-            f((uint32_t)(ty * fp.tiles_x), PRK_ROWCLASS ? (uint32_t)kMaxClass : 0u);
+            f((uint32_t)(ty * fp.tiles_x), PRK_ROWCLASS ? (uint32_t)((kMaxRep << kRowClassBits) | kMaxClass) : 0u);
 }
 
 __global__ void __launch_bounds__(kCsThreads) k_cs_hist(FrameParams fp, const TileRange *__restrict__ ranges,
@@ -459,7 +472,7 @@ __global__ void __launch_bounds__(kCsThreads) k_cs_emit(FrameParams fp, const Ti
 // the class bits from the pair index.
 __global__ void __launch_bounds__(256) k_cs_class(const uint32_t *__restrict__ offs, uint2 *__restrict__ bins) {
     constexpr int kPer = kCsClassWindow / 256;
-    constexpr int kClasses = 1 << kRowClassBits;
+    constexpr int kClasses = 1 << kClassBits;
     __shared__ uint32_t cnt[kClasses];
     const uint32_t t = blockIdx.x;
     const uint32_t b0 = offs[t], n = offs[t + 1] - b0;

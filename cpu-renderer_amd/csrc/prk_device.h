@@ -137,10 +137,7 @@ struct FrameParams {
 // F is a power of two the quotient is the single rounding of d*2^-k, which
 // the multiply by the exact 1/F also produces.  (fp is uniform: a scalar
 // branch, no divergence.)
-__device__ __forceinline__ float div_focal(const FrameParams &fp, float d) {
-    if (fp.f_pow2) return d * fp.InvF;
-    return d / fp.F;
-}
+__device__ __forceinline__ float div_focal(const FrameParams &fp, float d);  // (below DivBy)
 
 // (float)k / 255.0f for an integer k in [0, 255], bit for bit: k * RN(1/255)
 // plus one FMA residual correction is the correctly rounded quotient for
@@ -188,12 +185,85 @@ __device__ __forceinline__ void normalize_rcp(float &x, float &y, float &z) {
     y = s * y;
     z = s * z;
 }
-// NormalizeVector_8x (projekt.cpp:603-620), one lane: division form.
+// ---- quotients sharing one divisor ------------------------------------------
+// `x / d` (f32, IEEE division, denormals on) compiles on gfx950 to: v_div_scale
+// of d and of x, v_rcp of the scaled d, two Newton FMAs refining the
+// reciprocal, the quotient, two residual FMAs, v_div_fmas and v_div_fixup.
+// When |d| lies in [2^-32, 2^32] and |x| in [2^-80, 2^32], v_div_scale returns
+// its operands unchanged (no extreme exponent gap, no denormal operand,
+// reciprocal or quotient) and v_div_fixup passes the finite quotient through,
+// so the sequence is exactly the FMA chain of div_fast — whose reciprocal half
+// (div_by) depends on d alone.  Several quotients over one d (a
+// normalisation, a span's or an edge's increments) share it: one v_rcp and
+// two FMAs instead of one v_rcp, two v_div_scale, v_div_fmas and v_div_fixup
+// per quotient.  div_all takes that path when every lane of the wave is in
+// range (a wave-uniform branch, so the quotients stay one straight-line,
+// interleaved block) and the plain divisions otherwise: every quotient is the
+// correctly rounded x / d, bit for bit (prk_selftest_div,
+// tests/test_gpu_parity.py::test_shared_divisor_exact).
+#ifndef PRK_SHARED_DIV
+#define PRK_SHARED_DIV 1
+#endif
+struct DivBy {
+    float nd, r;
+};
+__device__ __forceinline__ DivBy div_by(float d) {
+    DivBy s;
+    s.nd = -d;
+    const float r0 = __builtin_amdgcn_rcpf(d);
+    const float e = __builtin_fmaf(s.nd, r0, 1.0f);
+    s.r = __builtin_fmaf(e, r0, r0);
+    return s;
+}
+__device__ __forceinline__ float div_fast(const DivBy &s, float x) {
+    const float m = x * s.r;
+    const float f2 = __builtin_fmaf(s.nd, m, x);
+    const float m1 = __builtin_fmaf(f2, s.r, m);
+    const float f4 = __builtin_fmaf(s.nd, m1, x);
+    return __builtin_fmaf(f4, s.r, m1);
+}
+// x[k] / d for every k.
+template <int K>
+__device__ __forceinline__ void div_all(float d, float (&x)[K]) {
+    if (PRK_SHARED_DIV) {
+        // NaN / inf / large numerators fail the sum, zero and tiny ones the min
+        float sum = fabsf(x[0]), mn = fabsf(x[0]);
+#pragma unroll
+        for (int k = 1; k < K; ++k) {
+            sum = sum + fabsf(x[k]);
+            mn = fminf(mn, fabsf(x[k]));
+        }
+        const float ad = fabsf(d);
+        const bool ok = ad >= 0x1p-32f && ad <= 0x1p32f && sum <= 0x1p32f && mn >= 0x1p-80f;
+        if (__builtin_expect(__all(ok), 1)) {
+            const DivBy s = div_by(d);
+#pragma unroll
+            for (int k = 0; k < K; ++k) x[k] = div_fast(s, x[k]);
+            return;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) x[k] = x[k] / d;
+}
+
+// d / F (the focal length divide of UnprojectVertex); F is uniform, so its
+// reciprocal half can be hoisted out of a thread's pixel loop.
+__device__ __forceinline__ float div_focal(const FrameParams &fp, float d) {
+    if (fp.f_pow2) return d * fp.InvF;
+    float q[1] = {d};
+    div_all(fp.F, q);
+    return q[0];
+}
+
+// NormalizeVector_8x (projekt.cpp:603-620), one lane: division form (three
+// quotients over one length).
 __device__ __forceinline__ void normalize_div(float &x, float &y, float &z) {
-    float len = sqrtf((x * x + y * y) + z * z);
-    x = x / len;
-    y = y / len;
-    z = z / len;
+    const float len = sqrtf((x * x + y * y) + z * z);
+    float q[3] = {x, y, z};
+    div_all(len, q);
+    x = q[0];
+    y = q[1];
+    z = q[2];
 }
 
 // _mm_mullo_epi16/_mm_mulhi_epi16 pitch multiply (projekt.cpp:1916-1920).
@@ -550,11 +620,10 @@ __device__ __forceinline__ Edge rec_edge_in(const float *f, int32_t ymin, int32_
 // no top clip; NormalGradient = (MaxNormal - MinNormal) / YDiff).
 __device__ __forceinline__ void nrm_edge_from(Edge &E, uint32_t vtx, const float *n) {
     const int mi = (int)(vtx & 3u), ma = (int)((vtx >> 2) & 3u);
-    const float YDiff = (float)E.YMax - (float)E.YMin;
     E.N0 = n[3 * mi + 0]; E.N1 = n[3 * mi + 1]; E.N2 = n[3 * mi + 2];
-    E.NG0 = (n[3 * ma + 0] - E.N0) / YDiff;
-    E.NG1 = (n[3 * ma + 1] - E.N1) / YDiff;
-    E.NG2 = (n[3 * ma + 2] - E.N2) / YDiff;
+    float g[3] = {n[3 * ma + 0] - E.N0, n[3 * ma + 1] - E.N1, n[3 * ma + 2] - E.N2};
+    div_all((float)E.YMax - (float)E.YMin, g);  // / YDiff
+    E.NG0 = g[0]; E.NG1 = g[1]; E.NG2 = g[2];
 }
 
 // AET edge step (projekt.cpp:3811-3829), only the fields mode M reads

@@ -18,7 +18,6 @@
 //                shading runs once per pixel instead of once per fragment.
 //                A coalesced flush writes z and colour of every pixel that
 //                got a winner.
-#include <hipcub/hipcub.hpp>
 
 #include "prk_device.h"
 
@@ -197,15 +196,17 @@ __device__ __forceinline__ int span_setup_avx(const FrameParams &fp, const TileC
     const float fXD = (float)XDiff;
     float IW = 0, IU = 0, IV = 0, IZ = 0, IN0 = 0, IN1 = 0, IN2 = 0;
     if (XDiff != 0) {  // 1666-1835
-        IW = (R.W - L.W) / fXD;
-        IU = (R.U - L.U) / fXD;
-        IV = (R.V - L.V) / fXD;
-        if (SHADE) {
-            IN0 = (R.N0 - L.N0) / fXD;
-            IN1 = (R.N1 - L.N1) / fXD;
-            IN2 = (R.N2 - L.N2) / fXD;
+        // the span's increments over XDiff (div_all: one shared reciprocal)
+        if constexpr (SHADE) {
+            float q[7] = {R.W - L.W, R.U - L.U, R.V - L.V, R.N0 - L.N0, R.N1 - L.N1, R.N2 - L.N2, R.Z - L.Z};
+            div_all(fXD, q);
+            IW = q[0]; IU = q[1]; IV = q[2]; IN0 = q[3]; IN1 = q[4]; IN2 = q[5]; IZ = q[6];
+        } else {  // (visibility: plain quotients, measured 1 % faster in k_vis than div_all)
+            IW = (R.W - L.W) / fXD;
+            IU = (R.U - L.U) / fXD;
+            IV = (R.V - L.V) / fXD;
+            IZ = (R.Z - L.Z) / fXD;
         }
-        IZ = (R.Z - L.Z) / fXD;
     }
     ws.i[SI_XA][lane] = xa;
     ws.i[SI_XB][lane] = xb;
@@ -278,23 +279,20 @@ __device__ __forceinline__ int span_setup_scalar(const FrameParams &fp, const Ti
     float IW = 0, IU = 0, IV = 0, IZ = 0, IN0 = 0, IN1 = 0, IN2 = 0;
     float IC0 = 0, IC1 = 0, IC2 = 0, IC3 = 0;
     if (XDiff != 0.0f) {  // 329-360
-        if (SHADE && TR::tex) {
-            IW = (R.W - L.W) / XDiff;
-            IU = (R.U - L.U) / XDiff;
-            IV = (R.V - L.V) / XDiff;
-        }
-        if (SHADE && TR::phong) {
-            IN0 = (R.N0 - L.N0) / XDiff;
-            IN1 = (R.N1 - L.N1) / XDiff;
-            IN2 = (R.N2 - L.N2) / XDiff;
-        }
-        if (SHADE && TR::color) {
-            IC0 = (R.C0 - L.C0) / XDiff;
-            IC1 = (R.C1 - L.C1) / XDiff;
-            IC2 = (R.C2 - L.C2) / XDiff;
-            IC3 = (R.C3 - L.C3) / XDiff;
-        }
-        IZ = (R.Z - L.Z) / XDiff;
+        // the span's increments over XDiff (div_all: one shared reciprocal)
+        constexpr bool kT = SHADE && TR::tex, kP = SHADE && TR::phong, kC = SHADE && TR::color;
+        float q[1 + (kT ? 3 : 0) + (kP ? 3 : 0) + (kC ? 4 : 0)];
+        int qi = 0;
+        q[qi++] = R.Z - L.Z;
+        if (kT) { q[qi++] = R.W - L.W; q[qi++] = R.U - L.U; q[qi++] = R.V - L.V; }
+        if (kP) { q[qi++] = R.N0 - L.N0; q[qi++] = R.N1 - L.N1; q[qi++] = R.N2 - L.N2; }
+        if (kC) { q[qi++] = R.C0 - L.C0; q[qi++] = R.C1 - L.C1; q[qi++] = R.C2 - L.C2; q[qi++] = R.C3 - L.C3; }
+        div_all(XDiff, q);
+        qi = 0;
+        IZ = q[qi++];
+        if (kT) { IW = q[qi++]; IU = q[qi++]; IV = q[qi++]; }
+        if (kP) { IN0 = q[qi++]; IN1 = q[qi++]; IN2 = q[qi++]; }
+        if (kC) { IC0 = q[qi++]; IC1 = q[qi++]; IC2 = q[qi++]; IC3 = q[qi++]; }
     }
     float LeftX = L.X;  // 381-400
     if (LeftX < 0) { XOffset = -L.X; LeftX = 0; }
@@ -1174,13 +1172,10 @@ __device__ __forceinline__ void walk_record(const FrameParams &fp, const Edge &L
     const float fXD = (float)XDiff;
     float IW = 0, IU = 0, IV = 0, IZ = 0, IN0 = 0, IN1 = 0, IN2 = 0;
     if (XDiff != 0) {  // 1666-1835
-        IW = (R.W - L.W) / fXD;
-        IU = (R.U - L.U) / fXD;
-        IV = (R.V - L.V) / fXD;
-        IN0 = (R.N0 - L.N0) / fXD;
-        IN1 = (R.N1 - L.N1) / fXD;
-        IN2 = (R.N2 - L.N2) / fXD;
-        IZ = (R.Z - L.Z) / fXD;
+        // the span's increments over XDiff (div_all: one shared reciprocal)
+        float q[7] = {R.W - L.W, R.U - L.U, R.V - L.V, R.N0 - L.N0, R.N1 - L.N1, R.N2 - L.N2, R.Z - L.Z};
+        div_all(fXD, q);
+        IW = q[0]; IU = q[1]; IV = q[2]; IN0 = q[3]; IN1 = q[4]; IN2 = q[5]; IZ = q[6];
     }
     const float4 q0 = make_float4(__int_as_float((LeftXa & 0xFFFF) | (texi << 16)), XOffset, L.W, L.U);
     const float4 q1 = make_float4(L.V, L.Z, IW, IU);
@@ -1322,6 +1317,9 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
                     const int ty = k / ntx;  // pair k = (ty, tx) row-major
                     rows |= ((m[k] * 0x0102040810204080ull) >> 56) << (8 * ty);  // bytes (0/1) -> bits
                 }
+                // the walk ends at the triangle's last won row (rows below it
+                // emit nothing, and no earlier row depends on them)
+                if (rows) wk.MaxY = min(wk.MaxY, rbase + 64 - (int32_t)__clzll((long long)rows));
             }
         }
     }
@@ -1367,6 +1365,125 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
     }
     wave_lds_sync();
     if ((uint32_t)lane < cnt) walk_flush(fp, q, (int)((head + lane) & (kWalkQ - 1)), won, recs);
+}
+
+// ---------------------------------------------------------------------------
+// k_walk's triangle list: the triangles that won a pixel, grouped by how many
+// band rows they span, tallest first.  Each k_walk lane walks its own
+// triangle row by row, so a wave runs as long as its tallest triangle: with
+// the list grouped by height the 64 triangles of a wave take about the same
+// number of row steps.  List order is otherwise free (every triangle writes
+// only its own span records).
+//   k_won_count    won triangles per height class (LDS histogram, one device
+//                  atomic per class and workgroup) into hist[0, 64);
+//   k_won_scatter  class bases = exclusive prefix of the counts; each
+//                  workgroup reserves its run of every class with one atomic
+//                  on hist[64 + class] and writes its triangles; wlist[n] =
+//                  the total (k_walk reads it, the host never does).
+// hist (kWonHistBytes) is zeroed before k_won_count.
+// ---------------------------------------------------------------------------
+// PRK_WON_SORT 1 (k_won_local): each workgroup groups its own 2048
+// consecutive triangles by height and appends them as one run (one kernel;
+// neighbouring triangles, whose setup records share cache lines, stay close
+// in the list).  2: the global grouping of k_won_count + k_won_scatter.
+// 0: k_won_local with one class (plain compaction).
+#ifndef PRK_WON_SORT
+#define PRK_WON_SORT 0  // measured on C3b (serial k_walk): 0 -> 0.249 ms, 1 -> 0.278, 2 -> 0.263,
+                        // hipcub DeviceSelect (round 1) -> 0.256: height grouping loses more to
+                        // scattered record reads than it gains in lane utilisation
+#endif
+constexpr int kWonClasses = 64, kWonPer = 8, kWonThreads = 256;
+constexpr size_t kWonHistBytes = 2 * kWonClasses * sizeof(uint32_t);
+
+__device__ __forceinline__ int won_class(const TileRange &tr) {
+    if (PRK_WON_SORT == 0) return 0;
+    const int rows = (int)tr.pad1 - (int)tr.pad0;  // band rows [r0, r1) (k_bin_count)
+    return kWonClasses - 1 - min(max(rows, 0), kWonClasses - 1);
+}
+
+// One workgroup per 2048 triangles: its won triangles grouped by height, at
+// a run of the list reserved with one atomic on *count (the list length).
+__global__ void __launch_bounds__(kWonThreads) k_won_local(uint32_t n, const uint8_t *__restrict__ trwon,
+                                                           const TileRange *__restrict__ ranges,
+                                                           uint32_t *__restrict__ count, uint32_t *__restrict__ wlist) {
+    __shared__ uint32_t h[kWonClasses];
+    __shared__ uint32_t base;
+    if (threadIdx.x < kWonClasses) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t g0 = blockIdx.x * (kWonThreads * kWonPer) + threadIdx.x;
+    int cls[kWonPer];
+    uint32_t rank[kWonPer];
+#pragma unroll
+    for (int k = 0; k < kWonPer; ++k) {
+        const uint32_t g = g0 + k * kWonThreads;
+        cls[k] = -1;
+        rank[k] = 0;
+        if (g < n && trwon[g]) {
+            cls[k] = won_class(ranges[g]);
+            rank[k] = atomicAdd(&h[cls[k]], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < kWonClasses) {  // one wave: class offsets inside the run, the run's start
+        const uint32_t c = h[threadIdx.x];
+        const uint32_t incl = (uint32_t)wave_incl_scan((int)c, (int)threadIdx.x);
+        h[threadIdx.x] = incl - c;
+        if (threadIdx.x == kWonClasses - 1) base = incl ? atomicAdd(count, incl) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kWonPer; ++k)
+        if (cls[k] >= 0) wlist[base + h[cls[k]] + rank[k]] = g0 + k * kWonThreads;
+}
+
+__global__ void __launch_bounds__(kWonThreads) k_won_count(uint32_t n, const uint8_t *__restrict__ trwon,
+                                                           const TileRange *__restrict__ ranges,
+                                                           uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[kWonClasses];
+    if (threadIdx.x < kWonClasses) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t g0 = blockIdx.x * (kWonThreads * kWonPer) + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < kWonPer; ++k) {
+        const uint32_t g = g0 + k * kWonThreads;
+        if (g < n && trwon[g]) atomicAdd(&h[won_class(ranges[g])], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < kWonClasses && h[threadIdx.x]) atomicAdd(hist + threadIdx.x, h[threadIdx.x]);
+}
+
+__global__ void __launch_bounds__(kWonThreads) k_won_scatter(uint32_t n, const uint8_t *__restrict__ trwon,
+                                                             const TileRange *__restrict__ ranges,
+                                                             uint32_t *__restrict__ hist, uint32_t *__restrict__ wlist) {
+    __shared__ uint32_t base[kWonClasses], run[kWonClasses];
+    if (threadIdx.x < kWonClasses) {  // one wave: class bases
+        const uint32_t c = hist[threadIdx.x];
+        const uint32_t incl = (uint32_t)wave_incl_scan((int)c, (int)threadIdx.x);
+        base[threadIdx.x] = incl - c;
+        run[threadIdx.x] = 0;
+        if (blockIdx.x == 0 && threadIdx.x == kWonClasses - 1) wlist[n] = incl;
+    }
+    __syncthreads();
+    const uint32_t g0 = blockIdx.x * (kWonThreads * kWonPer) + threadIdx.x;
+    int cls[kWonPer];
+    uint32_t rank[kWonPer];
+#pragma unroll
+    for (int k = 0; k < kWonPer; ++k) {
+        const uint32_t g = g0 + k * kWonThreads;
+        cls[k] = -1;
+        rank[k] = 0;
+        if (g < n && trwon[g]) {
+            cls[k] = won_class(ranges[g]);
+            rank[k] = atomicAdd(&run[cls[k]], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < kWonClasses && run[threadIdx.x])
+        base[threadIdx.x] += atomicAdd(hist + kWonClasses + threadIdx.x, run[threadIdx.x]);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kWonPer; ++k)
+        if (cls[k] >= 0) wlist[base[cls[k]] + rank[k]] = g0 + k * kWonThreads;
 }
 
 // k_pix: shade the won pixels of one tile from their span records (SPAN:
@@ -1560,6 +1677,44 @@ PRK_INST(MODE_SC_PHONG, false)
 PRK_INST(MODE_SC_PHONG, true)
 #undef PRK_INST
 
+// Self-test of the shared-divisor quotients (prk_device.h DivBy): thread i
+// draws (x, d) from a hash of (seed, i) — random signs, mantissas and
+// exponents in [-64, 64) (both inside and outside the fast range), every 16th
+// x zero — and counts quotients and normalisations that differ in any bit
+// from the compiler's own x / d.
+__device__ __forceinline__ uint32_t st_hash(uint64_t v) {
+    v ^= v >> 33; v *= 0xff51afd7ed558ccdull; v ^= v >> 33; v *= 0xc4ceb9fe1a85ec53ull; v ^= v >> 33;
+    return (uint32_t)v;
+}
+__device__ __forceinline__ float st_float(uint32_t h, uint32_t e) {
+    const uint32_t ex = 127u - 64u + (e & 127u);
+    return __uint_as_float((h & 0x807FFFFFu) | (ex << 23));
+}
+__global__ void k_selftest_div(uint32_t n, uint64_t seed, unsigned long long *bad) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = seed * 0x9E3779B97F4A7C15ull + 4ull * i;
+    const uint32_t h0 = st_hash(k), h1 = st_hash(k + 1), h2 = st_hash(k + 2), h3 = st_hash(k + 3);
+    const float x = (i & 15u) == 7u ? ((h0 & 1u) ? -0.0f : 0.0f) : st_float(h0, h2);
+    const float d = st_float(h1, h2 >> 8);
+    const volatile float dv = d;  // the plain quotient sees an opaque divisor
+    float q1[1] = {x};
+    div_all(d, q1);
+    const float q0 = x / dv;
+    unsigned long long b = __float_as_uint(q0) != __float_as_uint(q1[0]) ? 1ull : 0ull;
+    // normalisation of a vector of three draws (exponents within +-24)
+    const float a0 = st_float(h0, 52u + (h3 & 47u)), a1 = st_float(h1, 52u + ((h3 >> 8) & 47u));
+    const float a2 = (i & 31u) == 3u ? 0.0f : st_float(h2, 52u + ((h3 >> 16) & 47u));
+    float n0 = a0, n1 = a1, n2 = a2;
+    normalize_div(n0, n1, n2);
+    const volatile float lv = sqrtf((a0 * a0 + a1 * a1) + a2 * a2);
+    const float len = lv;
+    if (__float_as_uint(n0) != __float_as_uint(a0 / len) || __float_as_uint(n1) != __float_as_uint(a1 / len) ||
+        __float_as_uint(n2) != __float_as_uint(a2 / len))
+        b += 1ull << 32;
+    if (b) atomicAdd(bad, b);
+}
+
 }  // namespace prk
 
 // ---------------------------------------------------------------------------
@@ -1567,10 +1722,18 @@ PRK_INST(MODE_SC_PHONG, true)
 // ---------------------------------------------------------------------------
 extern "C" {
 
-// Temp bytes hipcub's select over `n` triangle flags needs (k_walk's list).
-hipError_t prk_walk_select_bytes(uint32_t n, size_t *bytes) {
-    return hipcub::DeviceSelect::Flagged(nullptr, *bytes, hipcub::CountingInputIterator<uint32_t>(0u),
-                                         (const uint8_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr, n);
+// Shared-divisor self-test: *bad = quotient mismatches | normalisation
+// mismatches << 32 over n draws (device memory).
+hipError_t prk_selftest_div_launch(uint32_t n, uint64_t seed, unsigned long long *bad, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(prk::k_selftest_div, dim3((n + 255) / 256), dim3(256), 0, s, n, seed, bad);
+    return hipGetLastError();
+}
+
+// Scratch bytes of k_walk's list build (the height-class histogram and cursors).
+hipError_t prk_walk_select_bytes(uint32_t, size_t *bytes) {
+    *bytes = prk::kWonHistBytes;
+    return hipSuccess;
 }
 
 hipError_t prk_launch_tri_draw(const prk::DrawRec *draws, uint32_t ndraws, uint32_t *tri_draw,
@@ -1612,7 +1775,15 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
     const prk::TileRange *tr = reinterpret_cast<const prk::TileRange *>(ranges);
     const uint32_t nblk = (fp->tri_count + 255) / 256;
     const uint32_t nwblk = (fp->tri_count + 64 * prk::kWalkWaves - 1) / (64 * prk::kWalkWaves);
+    const uint32_t nwon = (fp->tri_count + prk::kWonThreads * prk::kWonPer - 1) / (prk::kWonThreads * prk::kWonPer);
     const uint2 *bins = reinterpret_cast<const uint2 *>(bins_);
+    if (modeset == prk::MODE_AVX && PRK_SPAN_RECORDS && nblk) {
+        // k_walk's list histogram, cleared before k_vis is waited for (off
+        // the k_vis -> k_walk path)
+        if (!sel_temp || sel_bytes < prk::kWonHistBytes) return hipErrorInvalidValue;
+        const hipError_t e = hipMemsetAsync(sel_temp, 0, prk::kWonHistBytes, PRK_WALK_ON_VIS ? svis : s);
+        if (e != hipSuccess) return e;
+    }
 #define PRK_VIS(MS, UNI)                                                                                             \
     do {                                                                                                             \
         hipLaunchKernelGGL((prk::k_vis<MS, UNI>), dim3(ntile), dim3(64 * prk::kVisWaves), lv, svis, *fp, offs, bins,  \
@@ -1628,11 +1799,19 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
         /* PRK_WALK_ON_VIS: k_walk follows k_vis on svis, k_pix waits for it on s */                                 \
         hipStream_t sw = PRK_WALK_ON_VIS ? svis : s;                                                                 \
         if (nblk) {                                                                                                  \
-            /* compact the won triangles (order kept); the count stays on the device */                            \
+            /* the won triangles, tallest first; the count stays on the device */                                  \
             uint32_t *nsel = wlist + fp->tri_count;                                                                  \
-            hipError_t e_ = hipcub::DeviceSelect::Flagged(sel_temp, sel_bytes, hipcub::CountingInputIterator<uint32_t>(0u), \
-                                                          trwon, wlist, nsel, fp->tri_count, sw);                   \
-            if (e_ != hipSuccess) return e_;                                                                         \
+            uint32_t *hist_ = reinterpret_cast<uint32_t *>(sel_temp);                                                \
+            if (PRK_WON_SORT == 2) {                                                                                 \
+                hipLaunchKernelGGL(prk::k_won_count, dim3(nwon), dim3(prk::kWonThreads), 0, sw, fp->tri_count, trwon, \
+                                   tr, hist_);                                                                       \
+                hipLaunchKernelGGL(prk::k_won_scatter, dim3(nwon), dim3(prk::kWonThreads), 0, sw, fp->tri_count,      \
+                                   trwon, tr, hist_, wlist);                                                         \
+            } else {                                                                                                 \
+                nsel = hist_; /* the run counter is the list length */                                               \
+                hipLaunchKernelGGL(prk::k_won_local, dim3(nwon), dim3(prk::kWonThreads), 0, sw, fp->tri_count, trwon, \
+                                   tr, hist_, wlist);                                                                \
+            }                                                                                                        \
             hipLaunchKernelGGL((prk::k_walk<UNI>), dim3(nwblk), dim3(64 * prk::kWalkWaves), 0, sw, *fp, wlist, nsel,    \
                                tri_off, tr, won,                                                                     \
                                rp, anomaly);                                                                         \

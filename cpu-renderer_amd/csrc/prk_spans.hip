@@ -172,13 +172,10 @@ __device__ __forceinline__ bool obj_span(const FrameParams &fp, const ObjEdge &L
     const float fXD = (float)XDiff;
     float IW = 0, IU = 0, IV = 0, IZ = 0, IN0 = 0, IN1 = 0, IN2 = 0;
     if (XDiff != 0) {  // 1666-1835
-        IW = (R.W - L.W) / fXD;
-        IU = (R.U - L.U) / fXD;
-        IV = (R.V - L.V) / fXD;
-        IN0 = (R.N0 - L.N0) / fXD;
-        IN1 = (R.N1 - L.N1) / fXD;
-        IN2 = (R.N2 - L.N2) / fXD;
-        IZ = (R.Z - L.Z) / fXD;
+        // the span's increments over XDiff (div_all: one shared reciprocal)
+        float q[7] = {R.W - L.W, R.U - L.U, R.V - L.V, R.N0 - L.N0, R.N1 - L.N1, R.N2 - L.N2, R.Z - L.Z};
+        div_all(fXD, q);
+        IW = q[0]; IU = q[1]; IV = q[2]; IN0 = q[3]; IN1 = q[4]; IN2 = q[5]; IZ = q[6];
     }
     rec.q0 = make_float4(__int_as_float((LeftXa & 0xFFFF) | (texi << 16)), XOffset, L.W, L.U);
     rec.q1 = make_float4(L.V, L.Z, IW, IU);

@@ -24,7 +24,8 @@ from . import scenes as scenes_mod
 from .abi import PRK_SEM_AVX, PRK_SEM_AVX_ST, PRK_SEM_SCALAR  # noqa: F401
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("PRK_LIB") or os.path.join(os.path.dirname(_HERE), "libprk_hip.so")
+_DEFAULT_LIB = os.path.join(os.path.dirname(_HERE), "libprk_hip.so")
+LIB_PATH = os.environ.get("PRK_LIB") or _DEFAULT_LIB
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "prk.h")
 
 _LIB = None
@@ -85,6 +86,7 @@ _SIGS = {
                                  C.POINTER(C.c_int32)]),
     "prk_get_device": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_void_p)]),
     "prk_band_rows": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "prk_selftest_div": (C.c_int, [C.c_int32, C.c_uint32, C.c_uint64, C.POINTER(C.c_uint64)]),
     "prk_comm_available": (C.c_int, []),
     "prk_comm_unique_id": (C.c_int, [C.c_void_p]),
     "prk_comm_init": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
@@ -113,7 +115,11 @@ def lib(path=None):
         if not os.path.exists(p):
             raise PrkError("load libprk_hip.so (%s: not built; run __graft_entry__.build())" % p, -3)
         L = C.CDLL(p)
+        # (A/B tools load older builds through PRK_LIB that may lack newer entry points)
+        variant = os.path.abspath(p) != os.path.abspath(_DEFAULT_LIB)
         for name, (res, args) in _SIGS.items():
+            if variant and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
@@ -146,6 +152,14 @@ def construct_sphere():
     _check("prk_construct_sphere", lib().prk_construct_sphere(_ptr(V), _ptr(Cc), _ptr(N), _ptr(UV),
                                                                C.byref(n)))
     return V[: n.value], Cc[: n.value], N[: n.value], UV[: n.value]
+
+
+def selftest_div(n=1 << 22, seed=1, device=0):
+    """prk_selftest_div: (quotient mismatches, normalisation mismatches) of the
+    shared-divisor division against the compiler's x / d over n draws."""
+    out = C.c_uint64()
+    _check("prk_selftest_div", lib().prk_selftest_div(device, n, seed, C.byref(out)))
+    return out.value & 0xFFFFFFFF, out.value >> 32
 
 
 def band_rows(height, rank, nranks):

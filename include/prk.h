@@ -273,6 +273,12 @@ int prk_download_winners(prk_context *ctx, int32_t *winners_host);
  * with -DPRK_PROF; zeroed by prk_timing_reset), n <= 16. */
 int prk_debug_counters(prk_context *ctx, uint64_t *out, int32_t n);
 
+/* Test: the raster kernels divide several values by one divisor through a
+ * shared reciprocal; this checks n hashed (x, d) draws and
+ * normalisations on `device` against the compiler's own division, bit for
+ * bit.  *mismatches = quotient mismatches | normalisation mismatches << 32. */
+int prk_selftest_div(int32_t device, uint32_t n, uint64_t seed, uint64_t *mismatches);
+
 /* The bound target (any pointer may be NULL) and the context's device and
  * own stream (a hipStream_t; prk_flush(ctx, NULL) runs on it). */
 int prk_get_target(prk_context *ctx, void **color, int32_t *pitch_bytes, float **zbuf, int32_t *width,

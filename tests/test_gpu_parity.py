@@ -52,6 +52,15 @@ def run_both(scene, semantics=abi.PRK_SEM_AVX, phong=True, tile=None, threads=8,
     return g, o
 
 
+@pytest.mark.parametrize("seed", [1, 2])
+def test_shared_divisor_exact(gpu, seed):
+    """The kernels' shared-reciprocal quotients (prk_device.h DivBy) equal the
+    compiler's IEEE x / d bit for bit: 2^24 hashed draws with exponents on
+    both sides of the fast range, signed zeros, and normalisations."""
+    nq, nn = prk.selftest_div(n=1 << 24, seed=seed)
+    assert (nq, nn) == (0, 0)
+
+
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_avx_soup_256(gpu, seed):
     run_both(scenes.random_soup(2000, 256, 256, radius=16, seed=seed))
