@@ -141,6 +141,9 @@ constexpr int kTagPad = 16;  // k_shade: tags past the tile's last pixel (chunke
 constexpr int kSpanFVis = 9;  // the visibility sweep reads no normals or colours (SF_IZ + 1)
 constexpr int kSpanIVis = 8;  // SI_ROW + 1
 using VisSlots = WaveSlotsT<kSpanFVis, kSpanIVis>;
+// (All-AVX frames could drop SI_OVF and the scan scratch: 32 KiB per 256x8
+// workgroup, five workgroups per CU instead of four.  Measured no faster on
+// C3b, k_vis 0.495 ms either way: it is issue-bound, not latency-bound.)
 using ShadeSlots = WaveSlotsT<kSpanF, kSpanI>;
 
 struct TileCtx {
@@ -745,9 +748,8 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // One sweep over the tile's bin for mode M.  SHADE=false: visibility keys;
 // SHADE=true: shade the winners.
-template <int M, bool SHADE, bool UNI, bool REC = false>
-__device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
-                                      std::conditional_t<SHADE, ShadeSlots, VisSlots> &ws,
+template <int M, bool SHADE, bool UNI, bool REC = false, class WS>
+__device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, WS &ws,
                                       const uint2 *__restrict__ bins, uint32_t b0, uint32_t n,
                                       const uint32_t *__restrict__ list, uint32_t *anomaly) {
     // Entries [0, n) of the tile's bin, or (list != nullptr) the n entries it names.
@@ -895,7 +897,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc,
                     if (paired) {
                         const Edge &L = wk.S0, &R = wk.S1;
                         int ni;
-                        if (M == MODE_AVX) ni = span_setup_avx<SHADE>(fp, tc, ws, slot, tag, texi, L, R, row, st != 0);
+                        if constexpr (M == MODE_AVX) ni = span_setup_avx<SHADE>(fp, tc, ws, slot, tag, texi, L, R, row, st != 0);
                         else ni = span_setup_scalar<M, SHADE>(fp, tc, ws, slot, tag, texi, L, R, row);
                         ws.i[SI_ROW][slot] = row;
                         if (multi) ws.i[SI_PRE][slot] = ni;
