@@ -11,6 +11,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Diagnostic builds only (prk_kernels.hip lists the bits); never set in a product build.
+#ifndef PRK_DIAG
+#define PRK_DIAG 0
+#endif
+
 namespace prk {
 
 constexpr int kMaxLights = 8;

@@ -23,7 +23,8 @@
 
 // Diagnostic builds only (tools/diag): 1 = skip the shading sweep, 2 = skip
 // work items, 4 = skip the AET rows (setup only), 8 = skip the shading sweep's
-// work items, 16 = no Phong/texel (winners store a dummy colour).  Never set
+// work items, 16 = no Phong/texel (winners store a dummy colour), 32 = no
+// replay of the rows above a tile.  Never set
 // in a product build.
 #ifndef PRK_DIAG
 #define PRK_DIAG 0

@@ -26,10 +26,12 @@ import prk  # noqa: E402
 from prk import abi, scenes  # noqa: E402
 
 
-def time_scene(name, s, semantics, phong, steps=10, warmup=2):
+def time_scene(name, s, semantics, phong, steps=10, warmup=2, tile=None):
     r = prk.Renderer(0)
     try:
         r.target_alloc(s.width, s.height)
+        if tile:
+            r.set_tile(*tile)
         r.set_camera(s.prk_transform(), s.prk_lights())
         g = r.geometry(s.vertices, s.colors, s.normals, s.uvs)
         draws = s.draws if s.draws is not None else [(0, s.tri_count, s.texture)]
@@ -59,7 +61,8 @@ def time_scene(name, s, semantics, phong, steps=10, warmup=2):
         ms = (time.perf_counter() - t0) * 1e3 / steps
         st = r.stats()
         n = max(1, st["frames_timed"])
-        out = dict(config=name, width=s.width, height=s.height, triangles=s.tri_count,
+        out = dict(config=name, tile="%dx%d" % tuple(tile) if tile else "default", width=s.width, height=s.height,
+                   triangles=s.tri_count,
                    semantics="avx" if semantics == abi.PRK_SEM_AVX else "scalar", phong=bool(phong),
                    ms_per_frame=ms, mpixels_s=s.width * s.height / (ms * 1e-3) / 1e6,
                    mtri_s=s.tri_count / (ms * 1e-3) / 1e6, ms_bin=st["sum_ms_bin"] / n,
@@ -72,6 +75,11 @@ def time_scene(name, s, semantics, phong, steps=10, warmup=2):
 
 
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--small-tiles":  # tile sweep of the small configs
+        for tile in (None, (128, 8), (64, 8), (32, 8), (16, 8), (32, 4), (16, 16)):
+            time_scene("C1", scenes.single_triangle(), abi.PRK_SEM_SCALAR, False, tile=tile, steps=30)
+            time_scene("C2", scenes.displaced_sphere(70000, 1920, 1080, seed=3), abi.PRK_SEM_SCALAR, True, tile=tile)
+        return
     out_path = sys.argv[1] if len(sys.argv) > 1 else None
     res = []
     res.append(time_scene("C1", scenes.single_triangle(), abi.PRK_SEM_SCALAR, False))
