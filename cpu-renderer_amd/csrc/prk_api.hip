@@ -164,6 +164,13 @@ struct prk_context {
     uint32_t pair_hint = 0;       // entry count of the last frame (counting-sort capacity)
     bool legacy_bin = false;      // PRK_BIN_LEGACY=1: radix-sort binning with the count read back first
     int32_t tile_w = 256, tile_h = 8;  // measured best for C3b
+    // Automatic tile (until prk_set_tile): 256x8, or 32x8 for frames with few
+    // bin entries per tile (under 64, i.e. under one wave's chunk per tile:
+    // C1, C2), decided from a frame's count at 256x8 and kept while the
+    // triangle count and the band stay within 2x of that frame's.
+    bool tile_auto = true, auto_small = false;
+    uint32_t auto_T = 0;
+    int32_t auto_px = 0;
     // all-AVX frames: per-triangle setup records; the AVX k_vis / k_walk read
     // them (prk_kernels.hip PRK_SETUP_REC), so they are not optional
     bool setup_rec = true;
@@ -738,6 +745,7 @@ int prk_set_tile(prk_context *c, int32_t tw, int32_t th) {
     if (!c || tw < 8 || th <= 0 || (tw & (tw - 1)) || tw * th > 8192 || tw * th < 64) return PRK_ERR_ARG;
     c->tile_w = tw;
     c->tile_h = th;
+    c->tile_auto = false;
     return PRK_OK;
 }
 
@@ -1090,6 +1098,12 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
         total = B.h_info[0];
         c->stats.bin_entries = total;
         c->pair_hint = total;
+        if (c->tile_auto && !c->auto_small && c->tile_w == 256 && total < 64u * ntiles &&
+            8u * ntiles <= prk_cs_max_tiles()) {  // (32x8 tiles stay within the counting sort)
+            c->auto_small = true;  // (from the next frame on)
+            c->auto_T = T;
+            c->auto_px = c->W * (c->row1 - c->row0);
+        }
         if (B.h_info[1]) {
             if (total > prk_cs_max_pairs()) return PRK_ERR_UNSUPPORTED;  // 29-bit pair index in the bins
             c->clear_pending = fuse;
@@ -1228,6 +1242,14 @@ int prk_flush(prk_context *c, void *stream) {
     if (!c) return PRK_ERR_ARG;
     if (!c->color) return PRK_ERR_NO_TARGET;
     if (!c->have_camera) return PRK_ERR_ARG;
+    if (c->tile_auto) {  // the frame's tile (see prk_context::tile_auto)
+        const int64_t px = (int64_t)c->W * (c->row1 - c->row0);
+        if (c->auto_small && ((uint64_t)c->pending_tris > 2ull * c->auto_T || 2ull * c->pending_tris < c->auto_T ||
+                              px > 2 * (int64_t)c->auto_px || 2 * px < (int64_t)c->auto_px))
+            c->auto_small = false;  // re-decide from this frame's count
+        c->tile_w = c->auto_small ? 32 : 256;
+        c->tile_h = 8;
+    }
     PRK_TRY(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->own_stream;
     bool any_avx = false;

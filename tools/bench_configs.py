@@ -80,6 +80,15 @@ def main():
             time_scene("C1", scenes.single_triangle(), abi.PRK_SEM_SCALAR, False, tile=tile, steps=30)
             time_scene("C2", scenes.displaced_sphere(70000, 1920, 1080, seed=3), abi.PRK_SEM_SCALAR, True, tile=tile)
         return
+    if len(sys.argv) > 1 and sys.argv[1] == "--big-tiles":  # tile sweep of the large configs
+        for tile in (None, (128, 8), (64, 8), (32, 8)):
+            time_scene("C3a", scenes.random_soup(1_000_000, 4096, 4096, radius=16, seed=2025, textured=False),
+                       abi.PRK_SEM_SCALAR, False, tile=tile)
+            time_scene("C4-nearest", scenes.sponza_like(3840, 2160, seed=1, filt=abi.PRK_FILTER_NEAREST),
+                       abi.PRK_SEM_AVX, True, tile=tile)
+            time_scene("C3b", scenes.random_soup(1_000_000, 4096, 4096, radius=16, seed=2024), abi.PRK_SEM_AVX, True,
+                       tile=tile)
+        return
     out_path = sys.argv[1] if len(sys.argv) > 1 else None
     res = []
     res.append(time_scene("C1", scenes.single_triangle(), abi.PRK_SEM_SCALAR, False))
