@@ -164,11 +164,14 @@ struct prk_context {
     uint32_t pair_hint = 0;       // entry count of the last frame (counting-sort capacity)
     bool legacy_bin = false;      // PRK_BIN_LEGACY=1: radix-sort binning with the count read back first
     int32_t tile_w = 256, tile_h = 8;  // measured best for C3b
-    // Automatic tile (until prk_set_tile): 256x8, or 32x8 for frames with few
-    // bin entries per tile (under 64, i.e. under one wave's chunk per tile:
-    // C1, C2), decided from a frame's count at 256x8 and kept while the
-    // triangle count and the band stay within 2x of that frame's.
-    bool tile_auto = true, auto_small = false;
+    // Automatic tile (until prk_set_tile): 256x8, or narrower tiles for frames
+    // with few bin entries per tile (under one wave's 64-entry chunk per
+    // tile: 32x8, C2; under 8: 64x8, C1 — the binning's per-tile passes then
+    // cost more than the extra parallelism gains), decided from a frame's
+    // count at 256x8 and kept while the triangle count and the band stay
+    // within 2x of that frame's (measured, profiles/r02b/small_config_tiles.log).
+    bool tile_auto = true;
+    int32_t auto_small = 0;  // 0: 256x8; else the small tile width (64: under 8 entries per tile, 32: under 64)
     uint32_t auto_T = 0;
     int32_t auto_px = 0;
     // all-AVX frames: per-triangle setup records; the AVX k_vis / k_walk read
@@ -1100,7 +1103,7 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
         c->pair_hint = total;
         if (c->tile_auto && !c->auto_small && c->tile_w == 256 && total < 64u * ntiles &&
             8u * ntiles <= prk_cs_max_tiles()) {  // (32x8 tiles stay within the counting sort)
-            c->auto_small = true;  // (from the next frame on)
+            c->auto_small = total < 8u * ntiles ? 64 : 32;  // (from the next frame on)
             c->auto_T = T;
             c->auto_px = c->W * (c->row1 - c->row0);
         }
@@ -1246,8 +1249,8 @@ int prk_flush(prk_context *c, void *stream) {
         const int64_t px = (int64_t)c->W * (c->row1 - c->row0);
         if (c->auto_small && ((uint64_t)c->pending_tris > 2ull * c->auto_T || 2ull * c->pending_tris < c->auto_T ||
                               px > 2 * (int64_t)c->auto_px || 2 * px < (int64_t)c->auto_px))
-            c->auto_small = false;  // re-decide from this frame's count
-        c->tile_w = c->auto_small ? 32 : 256;
+            c->auto_small = 0;  // re-decide from this frame's count
+        c->tile_w = c->auto_small ? c->auto_small : 256;
         c->tile_h = 8;
     }
     PRK_TRY(hipSetDevice(c->device));

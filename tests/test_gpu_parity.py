@@ -203,6 +203,43 @@ def test_pipelined_frames_one_target(gpu):
     assert (gc == oc).all()
 
 
+@pytest.mark.parametrize("sem,phong", [(abi.PRK_SEM_SCALAR, False), (abi.PRK_SEM_AVX, True)])
+def test_auto_tile_sparse_then_dense(gpu, sem, phong):
+    """The automatic tile: a sparse frame (a few large triangles, under 8 and
+    under 64 bin entries per 256x8 tile) switches the context to 64x8 / 32x8
+    tiles from its next frame (more bin entries), a frame with many more
+    triangles switches back; every frame, before and after each switch,
+    equals the oracle's."""
+    sparse1 = scenes.single_triangle(512, 512, textured=True, gouraud_only=False)
+    sparse2 = scenes.random_soup(40, 512, 512, radius=90, seed=91)
+    dense = scenes.random_soup(6000, 512, 512, radius=12, seed=92)
+    r = prk.Renderer(0)
+    got = []
+    try:
+        r.target_alloc(512, 512)
+        for sc, n in ((sparse1, 3), (sparse2, 3), (dense, 2)):
+            r.set_camera(sc.prk_transform(), sc.prk_lights())
+            g = r.geometry(sc.vertices, sc.colors, sc.normals, sc.uvs)
+            tex = r.texture(sc.texture)
+            for _ in range(n):
+                r.clear_on_flush()
+                if sem == abi.PRK_SEM_AVX:
+                    r.draw_model_optimized(g, sc.tri_count, P=sc.P, bitmap=tex, phong=True)
+                else:
+                    r.draw_model(g, sc.tri_count, P=sc.P, bitmap=tex, phong=False)
+                r.complete_all_work()
+                r.synchronize()
+                got.append((sc, r.stats()["bin_entries"], r.download()))
+    finally:
+        r.close()
+    ent = [e for _, e, _ in got]
+    assert ent[1] > ent[0] and ent[4] > ent[3], ent  # narrower tiles from the second frame on
+    for sc, _, (gc, gz) in got:
+        oc, oz, _, _ = O.render(sc, semantics=sem, phong=phong)
+        assert (gz.view(np.uint32) == oz.view(np.uint32)).all()
+        assert (gc == oc).all()
+
+
 def test_bin_capacity_rerun(gpu):
     """Counting-sort binning sizes its per-pair arrays from the previous
     frame's entry count; a frame with more entries leaves its bins empty and
