@@ -432,6 +432,18 @@ def test_whole_object_construct_sphere(gpu, sem):
     assert (g[2] >= 0).sum() > 10000
 
 
+@pytest.mark.parametrize("tile", [(32, 8), (64, 8)])
+def test_whole_object_narrow_tiles(gpu, tile):
+    """The span path (whole-object AETs) at the automatic tile's narrow
+    widths: ConstructSphere as one object and random 5-triangle objects."""
+    s = _sphere_scene()
+    g = prk.render_scene(s, tile=tile, tris_per_object=s.tri_count)
+    compare(g, O.render(s, tris_per_object=s.tri_count), label="sphere %dx%d" % tile)
+    s2 = scenes.random_soup(600, 256, 256, radius=40, seed=17)
+    g2 = prk.render_scene(s2, tile=tile, tris_per_object=5)
+    compare(g2, O.render(s2, tris_per_object=5), label="objects %dx%d" % tile)
+
+
 @pytest.mark.parametrize("tpo,seed", [(2, 1), (5, 2), (16, 3)])
 def test_whole_object_random_objects(gpu, tpo, seed):
     """Random objects of several triangles, clipped on every side, with ties:
