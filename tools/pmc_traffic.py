@@ -40,6 +40,8 @@ def short(name):
               "k_setup", "k_bin"):
         if k in name:
             return k
+    if "k_cs_" in name or "k_won_" in name:  # the counting sort's own kernels (their "scan" is not rocprim's)
+        return name.split("(")[0][:60]
     if "radix_sort" in name:
         return "rocprim radix sort"
     if "scan" in name:
