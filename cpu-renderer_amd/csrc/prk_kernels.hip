@@ -1,23 +1,26 @@
 // prk_kernels.hip — gfx950 kernels of the rasterizer hot path.
 //
-// Pipeline per flush: binning in prk_bin.hip produces, for
-// every tile, the triangles that may touch it in submission order; then
-//   k_raster     one workgroup per screen tile; the tile's z/colour slab lives
-//                in LDS.  Each lane owns one bin entry (a triangle), re-runs
-//                FillEdgeTable for it (projekt.cpp:3882-4121), walks its AET
-//                (3615-3871) over the tile's rows and fills its spans with the
-//                reference's exact span arithmetic (FillLineOptimized
-//                1492-2320 or DrawModel 298-538).
-//                Sweep 1 resolves visibility with 64-bit LDS atomicMax on
-//                key = (ordered z << 32) | tag(pair) (prk_device.h pair_tag): the
-//                reference's strict z '>' in submission order keeps exactly
-//                the EARLIEST fragment of maximal z, which is that max (bin
-//                entries are in submission order).  The triangles that won a
-//                pixel are then listed, and sweep 2 re-walks only those and
-//                shades only the winning fragments (texture + Phong), so
-//                shading runs once per pixel instead of once per fragment.
-//                A coalesced flush writes z and colour of every pixel that
-//                got a winner.
+// Pipeline per flush: binning (prk_bin.hip) lists, for every
+// screen tile, its (triangle, pair) entries — pair = the triangle's index
+// for that tile, numbered in submission order — and, for all-AVX frames,
+// writes one setup record per triangle (FillEdgeTable + MergeSort, projekt.cpp
+// 3882-4121, 2-72).  Then:
+//   k_vis    one workgroup per tile, the tile's 64-bit visibility keys in
+//            LDS.  Each lane takes one bin entry, walks its triangle's AET
+//            (3615-3871) over the tile's rows and spreads the spans' pixels
+//            over the wave (FillLineOptimized 1492-2320 / DrawModel 298-538
+//            arithmetic, z and the UV mask only).  LDS atomicMax of
+//            key = (ordered z << 32) | tag(pair) keeps the reference's winner
+//            (strict '>' in submission order: the EARLIEST fragment of
+//            maximal z) whatever order the bin is walked in.
+//            Out: the winning tag of every pixel, won (pair, row) flags.
+//   k_won_local + k_walk   (AVX) the triangles that won a pixel, each walked
+//            once over its whole AET with normals; every won row span
+//            becomes a 64-B lane-init record.
+//   k_pix    (AVX) one thread per pixel: winner -> record -> lane chain ->
+//            texel + Phong -> z and colour, coalesced.
+//   k_shade  (scalar DrawModel frames) per tile, re-walks the entries that won
+//            a pixel and shades only their winning fragments.
 
 #include "prk_device.h"
 
