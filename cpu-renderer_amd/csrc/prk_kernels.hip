@@ -1375,32 +1375,23 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
 }
 
 // ---------------------------------------------------------------------------
-// k_walk's triangle list: the triangles that won a pixel, grouped by how many
-// band rows they span, tallest first.  Each k_walk lane walks its own
-// triangle row by row, so a wave runs as long as its tallest triangle: with
-// the list grouped by height the 64 triangles of a wave take about the same
-// number of row steps.  List order is otherwise free (every triangle writes
-// only its own span records).
-//   k_won_count    won triangles per height class (LDS histogram, one device
-//                  atomic per class and workgroup) into hist[0, 64);
-//   k_won_scatter  class bases = exclusive prefix of the counts; each
-//                  workgroup reserves its run of every class with one atomic
-//                  on hist[64 + class] and writes its triangles; wlist[n] =
-//                  the total (k_walk reads it, the host never does).
-// hist (kWonHistBytes) is zeroed before k_won_count.
+// k_walk's triangle list: the triangles that won a pixel (k_won_local, one
+// launch, the count stays on the device).  Each workgroup appends the won
+// triangles of its 2048 consecutive triangles as one run (one atomic), so
+// neighbouring triangles — whose setup records share cache lines and whose
+// span records land close together — stay together in the list.
+// PRK_WON_SORT 1 groups each run by triangle height, tallest first (each
+// k_walk lane walks its own triangle, so a wave runs as long as its tallest
+// one); measured on C3b (serial k_walk): 0 -> 0.249 ms, 1 -> 0.278, a global
+// height grouping -> 0.263, round 1's hipcub DeviceSelect -> 0.256: the
+// scattered record traffic costs more than the lane utilisation gains.
+// The list length (kWonHistBytes of scratch) is zeroed before the launch.
 // ---------------------------------------------------------------------------
-// PRK_WON_SORT 1 (k_won_local): each workgroup groups its own 2048
-// consecutive triangles by height and appends them as one run (one kernel;
-// neighbouring triangles, whose setup records share cache lines, stay close
-// in the list).  2: the global grouping of k_won_count + k_won_scatter.
-// 0: k_won_local with one class (plain compaction).
 #ifndef PRK_WON_SORT
-#define PRK_WON_SORT 0  // measured on C3b (serial k_walk): 0 -> 0.249 ms, 1 -> 0.278, 2 -> 0.263,
-                        // hipcub DeviceSelect (round 1) -> 0.256: height grouping loses more to
-                        // scattered record reads than it gains in lane utilisation
+#define PRK_WON_SORT 0
 #endif
 constexpr int kWonClasses = 64, kWonPer = 8, kWonThreads = 256;
-constexpr size_t kWonHistBytes = 2 * kWonClasses * sizeof(uint32_t);
+constexpr size_t kWonHistBytes = 16;  // [0]: the list length
 
 __device__ __forceinline__ int won_class(const TileRange &tr) {
     if (PRK_WON_SORT == 0) return 0;
@@ -1408,8 +1399,8 @@ __device__ __forceinline__ int won_class(const TileRange &tr) {
     return kWonClasses - 1 - min(max(rows, 0), kWonClasses - 1);
 }
 
-// One workgroup per 2048 triangles: its won triangles grouped by height, at
-// a run of the list reserved with one atomic on *count (the list length).
+// One workgroup per 2048 triangles: its won triangles (grouped by height with
+// PRK_WON_SORT 1) at a run of the list reserved with one atomic on *count.
 __global__ void __launch_bounds__(kWonThreads) k_won_local(uint32_t n, const uint8_t *__restrict__ trwon,
                                                            const TileRange *__restrict__ ranges,
                                                            uint32_t *__restrict__ count, uint32_t *__restrict__ wlist) {
@@ -1441,56 +1432,6 @@ __global__ void __launch_bounds__(kWonThreads) k_won_local(uint32_t n, const uin
 #pragma unroll
     for (int k = 0; k < kWonPer; ++k)
         if (cls[k] >= 0) wlist[base + h[cls[k]] + rank[k]] = g0 + k * kWonThreads;
-}
-
-__global__ void __launch_bounds__(kWonThreads) k_won_count(uint32_t n, const uint8_t *__restrict__ trwon,
-                                                           const TileRange *__restrict__ ranges,
-                                                           uint32_t *__restrict__ hist) {
-    __shared__ uint32_t h[kWonClasses];
-    if (threadIdx.x < kWonClasses) h[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t g0 = blockIdx.x * (kWonThreads * kWonPer) + threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < kWonPer; ++k) {
-        const uint32_t g = g0 + k * kWonThreads;
-        if (g < n && trwon[g]) atomicAdd(&h[won_class(ranges[g])], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x < kWonClasses && h[threadIdx.x]) atomicAdd(hist + threadIdx.x, h[threadIdx.x]);
-}
-
-__global__ void __launch_bounds__(kWonThreads) k_won_scatter(uint32_t n, const uint8_t *__restrict__ trwon,
-                                                             const TileRange *__restrict__ ranges,
-                                                             uint32_t *__restrict__ hist, uint32_t *__restrict__ wlist) {
-    __shared__ uint32_t base[kWonClasses], run[kWonClasses];
-    if (threadIdx.x < kWonClasses) {  // one wave: class bases
-        const uint32_t c = hist[threadIdx.x];
-        const uint32_t incl = (uint32_t)wave_incl_scan((int)c, (int)threadIdx.x);
-        base[threadIdx.x] = incl - c;
-        run[threadIdx.x] = 0;
-        if (blockIdx.x == 0 && threadIdx.x == kWonClasses - 1) wlist[n] = incl;
-    }
-    __syncthreads();
-    const uint32_t g0 = blockIdx.x * (kWonThreads * kWonPer) + threadIdx.x;
-    int cls[kWonPer];
-    uint32_t rank[kWonPer];
-#pragma unroll
-    for (int k = 0; k < kWonPer; ++k) {
-        const uint32_t g = g0 + k * kWonThreads;
-        cls[k] = -1;
-        rank[k] = 0;
-        if (g < n && trwon[g]) {
-            cls[k] = won_class(ranges[g]);
-            rank[k] = atomicAdd(&run[cls[k]], 1u);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < kWonClasses && run[threadIdx.x])
-        base[threadIdx.x] += atomicAdd(hist + kWonClasses + threadIdx.x, run[threadIdx.x]);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kWonPer; ++k)
-        if (cls[k] >= 0) wlist[base[cls[k]] + rank[k]] = g0 + k * kWonThreads;
 }
 
 // k_pix: shade the won pixels of one tile from their span records (SPAN:
@@ -1809,16 +1750,9 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
             /* the won triangles, tallest first; the count stays on the device */                                  \
             uint32_t *nsel = wlist + fp->tri_count;                                                                  \
             uint32_t *hist_ = reinterpret_cast<uint32_t *>(sel_temp);                                                \
-            if (PRK_WON_SORT == 2) {                                                                                 \
-                hipLaunchKernelGGL(prk::k_won_count, dim3(nwon), dim3(prk::kWonThreads), 0, sw, fp->tri_count, trwon, \
-                                   tr, hist_);                                                                       \
-                hipLaunchKernelGGL(prk::k_won_scatter, dim3(nwon), dim3(prk::kWonThreads), 0, sw, fp->tri_count,      \
-                                   trwon, tr, hist_, wlist);                                                         \
-            } else {                                                                                                 \
-                nsel = hist_; /* the run counter is the list length */                                               \
-                hipLaunchKernelGGL(prk::k_won_local, dim3(nwon), dim3(prk::kWonThreads), 0, sw, fp->tri_count, trwon, \
-                                   tr, hist_, wlist);                                                                \
-            }                                                                                                        \
+            nsel = hist_; /* the run counter is the list length */                                                   \
+            hipLaunchKernelGGL(prk::k_won_local, dim3(nwon), dim3(prk::kWonThreads), 0, sw, fp->tri_count, trwon,     \
+                               tr, hist_, wlist);                                                                    \
             hipLaunchKernelGGL((prk::k_walk<UNI>), dim3(nwblk), dim3(64 * prk::kWalkWaves), 0, sw, *fp, wlist, nsel,    \
                                tri_off, tr, won,                                                                     \
                                rp, anomaly);                                                                         \
