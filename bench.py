@@ -78,6 +78,23 @@ def load_traffic(cfg_key):
         return None, None
 
 
+def load_valu(cfg_key, kernel):
+    """The dominant kernel's issued-VALU time estimate and lane utilisation
+    from the round's SQ counter passes (tools/profile_round.sh ->
+    tools/sqsum.py --json -> profiles/sq_valu.json), or None.  NOT measured by
+    this run: SQ counters need their own rocprofv3 passes."""
+    p = os.path.join(ROOT, "profiles", "sq_valu.json")
+    try:
+        with open(p) as f:
+            e = json.load(f)[cfg_key]
+        k = next(v for n, v in e["per_kernel"].items() if n.startswith(kernel + "<") or n == kernel)
+        return dict(kernel=kernel, valu_time_estimate_ms=k.get("valu_time_estimate_ms"),
+                    lane_utilisation=k.get("lane_utilisation"), valu_issue_floor_ms=k.get("valu_issue_floor_ms"),
+                    source="profiles/sq_valu.json[%s] (%s)" % (cfg_key, e.get("round", "?")))
+    except (OSError, ValueError, KeyError, StopIteration):
+        return None
+
+
 def cpu_topology():
     """Host CPUs this process may run on, their physical cores and SMT, and
     the cgroup CPU quota (the box's share of the host)."""
@@ -411,7 +428,10 @@ def main():
                      "traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes": alg,
                      "dominant_kernel": {"name": "k_vis", "ms_serial": serial["k_vis"],
                                          "share_of_serial_frame": serial["k_vis"] / max(
-                                             1e-9, serial["raster"] + serial["k_bin_phase"])}},
+                                             1e-9, serial["raster"] + serial["k_bin_phase"])},
+                     # the binding resource of the dominant kernel: issued VALU
+                     # (SQ counters of the committed round profile)
+                     "valu": load_valu(cfg_key, "k_vis")},
     }
     if check is not None:
         out["check"] = check

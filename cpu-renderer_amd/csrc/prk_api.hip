@@ -27,6 +27,7 @@ hipError_t prk_bin_count(const prk::FrameParams *, uint32_t *, void *, hipStream
 uint32_t prk_cs_chunks(uint32_t);
 uint32_t prk_cs_max_tiles(void);
 uint32_t prk_cs_max_pairs(void);
+int prk_cs_ready(uint32_t);
 hipError_t prk_bin_cs(const prk::FrameParams *, const void *, const uint32_t *, uint32_t *, uint32_t *, uint32_t *,
                       uint32_t *, uint32_t *, uint32_t, uint32_t *, uint32_t *, void *, uint32_t *, uint8_t *, uint32_t,
                       uint8_t *, hipStream_t);
@@ -580,7 +581,25 @@ int prk_geometry_update(prk_context *c, int32_t handle, const float *v, const fl
     const size_t comp[4] = {3, 4, 3, 2};
     for (int k = 0; k < 4; ++k) {  // an array passed as null keeps its previous contents
         const size_t bytes = (size_t)vertex_count * comp[k] * sizeof(float);
-        if (!src[k]) continue;
+        if (!src[k]) {
+            // ... and grows with the vertex count: its first cap[k] vertices
+            // kept, the new ones zero, so no draw reads past its allocation.
+            if (*dst[k] && vertex_count > g.cap[k]) {
+                const size_t old = (size_t)g.cap[k] * comp[k] * sizeof(float);
+                float *d = nullptr;
+                PRK_TRY(hipMalloc((void **)&d, bytes));
+                hipError_t e = hipMemcpy(d, *dst[k], old, hipMemcpyDeviceToDevice);
+                if (e == hipSuccess) e = hipMemset((uint8_t *)d + old, 0, bytes - old);
+                if (e != hipSuccess) {
+                    (void)hipFree(d);
+                    return status_of(e);
+                }
+                (void)hipFree((void *)*dst[k]);
+                *dst[k] = d;
+                g.cap[k] = vertex_count;
+            }
+            continue;
+        }
         if (!*dst[k] || vertex_count > g.cap[k]) {
             float *d = nullptr;
             PRK_TRY(hipMalloc((void **)&d, bytes ? bytes : 4));
@@ -987,17 +1006,17 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
         PRK_TRY(bset_ensure(B.d_seltemp, std::max<size_t>(sel_bytes, 16)));
     }
     uint8_t *won, *trwon;
-    const bool cs = !c->legacy_bin && ntiles <= prk_cs_max_tiles();
+    const bool cs = !c->legacy_bin && ntiles <= prk_cs_max_tiles() && prk_cs_ready(ntiles);
     uint32_t total = 0;
     if (cs) {
         // Counting-sort binning (prk_bin.hip k_cs_*): all sizes stay on the
         // device.  The per-pair arrays hold `cap` pairs (the last frame's
-        // count plus room; a first frame guesses 4 per triangle); a frame with
-        // more entries leaves its bins empty and is re-run below, once the
-        // count is known.
+        // count plus room; a first frame guesses 2.5 per triangle, C3b has
+        // 3.2); a frame with more entries leaves its bins empty and is re-run
+        // below, once the count is known.
         const uint32_t nch = prk_cs_chunks(T);
         const uint64_t want64 = c->pair_hint ? (uint64_t)c->pair_hint + c->pair_hint / 8 + 4096
-                                             : std::max<uint64_t>(4ull * T, 1u << 16);
+                                             : std::max<uint64_t>(5ull * T / 2, 1u << 16);
         const uint32_t want = (uint32_t)std::min<uint64_t>(want64, prk_cs_max_pairs());
         // pairs the set's per-pair arrays hold now (they never shrink)
         auto pairs_held = [&]() -> size_t {
@@ -1007,6 +1026,13 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
             if (span_rec) m = std::min(m, B.d_recs.cap / ((size_t)won_stride * 64));
             return m;
         };
+        if (pairs_held() > 4ull * want && pairs_held() > (1u << 20)) {
+            // far more room than the frames need (a big frame earlier): give
+            // it back once the set's last reader is done
+            if (B.used) PRK_TRY(hipEventSynchronize(B.free_ev));
+            DevBuf *pb[] = {&B.d_pair_tri, &B.d_bins, &B.d_list, &B.d_won, &B.d_recs};
+            for (DevBuf *b : pb) b->release();
+        }
         if (pairs_held() < want) PRK_TRY(ensure_pairs(want, false));
         const uint32_t cap = (uint32_t)std::min<size_t>(pairs_held(), prk_cs_max_pairs());
         PRK_TRY(bset_ensure(B.d_ghist, std::max<size_t>((size_t)nch * ntiles * 4, 4)));

@@ -24,6 +24,8 @@
 #include <hipcub/hipcub.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 
+#include <atomic>
+
 #include "prk_device.h"
 
 namespace prk {
@@ -583,6 +585,30 @@ hipError_t prk_bin_count(const prk::FrameParams *fp, uint32_t *tri_n, void *rang
     return hipGetLastError();
 }
 
+// The counting sort's per-tile LDS (4 B per tile) above 64 KiB needs the
+// dynamic-LDS attribute of k_cs_hist / k_cs_emit, which is per device: set
+// once per device (a process may drive several GPUs), and only when a frame
+// needs it.  0: not tried, 1: set, 2: refused (the caller bins with the
+// radix sort instead).
+static std::atomic<int> g_cs_attr[64];
+int prk_cs_ready(uint32_t ntiles) {
+    if (ntiles == 0 || ntiles > prk::kCsMaxTiles) return 0;
+    if ((size_t)ntiles * 4 <= 65536) return 1;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    int st = g_cs_attr[dev].load(std::memory_order_acquire);
+    if (st == 0) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&prk::k_cs_hist),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, prk::kCsMaxTiles * 4);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(reinterpret_cast<const void *>(&prk::k_cs_emit),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, prk::kCsMaxTiles * 4);
+        st = e == hipSuccess ? 1 : 2;
+        g_cs_attr[dev].store(st, std::memory_order_release);  // (a racing setter sets the same value)
+    }
+    return st == 1;
+}
+
 uint32_t prk_cs_chunks(uint32_t tri_count) { return (tri_count + prk::kCsChunk - 1) / prk::kCsChunk; }
 uint32_t prk_cs_max_tiles(void) { return prk::kCsMaxTiles; }
 uint32_t prk_cs_max_pairs(void) { return prk::kCsPairMask; }
@@ -596,16 +622,7 @@ hipError_t prk_bin_cs(const prk::FrameParams *fp, const void *ranges, const uint
     const uint32_t nch = prk_cs_chunks(fp->tri_count);
     const prk::TileRange *tr = reinterpret_cast<const prk::TileRange *>(ranges);
     const size_t lds = (size_t)ntiles * 4;
-    static bool attr = false;  // dynamic LDS above 64 KiB (up to kCsMaxTiles tiles)
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&prk::k_cs_hist),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, prk::kCsMaxTiles * 4);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute(reinterpret_cast<const void *>(&prk::k_cs_emit),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, prk::kCsMaxTiles * 4);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    if (!prk_cs_ready(ntiles)) return hipErrorNotSupported;
     if (nch) {
         hipLaunchKernelGGL(prk::k_cs_hist, dim3(nch), dim3(prk::kCsThreads), lds, s, *fp, tr, tri_n, ghist, chunk_tot,
                            ntiles);

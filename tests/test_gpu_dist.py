@@ -87,6 +87,51 @@ def test_gather_frame_rccl_one_rank(gpu, scene_ref):
         x.close()
 
 
+def test_c5_8192_eight_bands_gather(gpu):
+    """C5 (1M triangles, offsets +-32 px, 8192^2) split as the 8-rank run
+    splits it: 8 band contexts (prk_band_rows), each binning every triangle
+    against its 1024 rows, gathered with prk_gather_frame_local into one
+    device frame.  The gathered colour and z and every band's winner map equal
+    the full-frame oracle bit for bit."""
+    import oracle as O
+    s = scenes.random_soup(1_000_000, 8192, 8192, radius=32, seed=5)
+    oc, oz, ow, _ = O.render(s, threads=16)
+    n = 8
+    rs = []
+    wins = []
+    try:
+        for r in range(n):
+            R = prk.Renderer(0)
+            rs.append(R)
+            a, b = prk.band_rows(s.height, r, n)
+            assert (a, b) == (r * 1024, (r + 1) * 1024)
+            R.target_alloc(s.width, s.height, a, b)
+            R.clear_on_flush()
+            R.set_debug(True)
+            R.set_camera(s.prk_transform(), s.prk_lights())
+            g = R.geometry(s.vertices, None, s.normals, s.uvs)
+            t = R.texture(s.texture)
+            R.draw_model_optimized(g, s.tri_count, bitmap=t)
+            R.complete_all_work()
+        for R in rs:
+            R.synchronize()
+            wins.append(R.winners())
+        F = _frame(s)
+        rs.append(F)
+        cp, pitch, zp, *_ = F.target()
+        prk.gather_frame_local(rs[:n], cp, pitch, zp, with_z=True)
+        rs[0].synchronize()
+        gc, gz = F.download()
+    finally:
+        for R in rs:
+            R.close()
+    zbad = int((gz.view(np.uint32) != oz.view(np.uint32)).sum())
+    cbad = int((gc != oc).sum())
+    wbad = sum(int((w != ow[r * 1024:(r + 1) * 1024]).sum()) for r, w in enumerate(wins))
+    assert zbad == 0 and cbad == 0 and wbad == 0, (zbad, cbad, wbad)
+    assert (ow >= 0).mean() > 0.8
+
+
 def test_gather_rejects_wrong_band(gpu, scene_ref):
     s, _, _ = scene_ref
     rs = _band_renderers(s, 2)

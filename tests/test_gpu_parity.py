@@ -530,6 +530,34 @@ def test_whole_object_scalar_unsupported(gpu):
         r.close()
 
 
+def test_geometry_update_null_array_grows(gpu):
+    """prk_geometry_update with a NULL colour array and a larger vertex count:
+    the colour buffer grows (its old vertices kept, the new ones zero), so a
+    scalar Gouraud draw of the new triangles reads inside its allocation and
+    sees exactly those colours."""
+    a = scenes.random_soup(800, 256, 256, radius=16, seed=51, textured=False)
+    b = scenes.random_soup(3000, 256, 256, radius=16, seed=52, textured=False)
+    expect = b.subset(0, b.tri_count)
+    expect.colors = np.zeros_like(b.colors)
+    expect.colors[: a.colors.shape[0]] = a.colors
+    r = prk.Renderer()
+    try:
+        r.target_alloc(256, 256)
+        r.clear()
+        r.set_camera(b.prk_transform(), b.prk_lights())
+        g = r.geometry(a.vertices, a.colors, a.normals, a.uvs)
+        r.geometry_update(g, b.vertices, None, b.normals, b.uvs)
+        r.draw_model(g, b.tri_count, P=b.P, phong=False)
+        r.complete_all_work()
+        r.synchronize()
+        gc, gz = r.download()
+    finally:
+        r.close()
+    oc, oz, _, _ = O.render(expect, semantics=abi.PRK_SEM_SCALAR, phong=False)
+    assert (gz.view(np.uint32) == oz.view(np.uint32)).all()
+    assert (gc == oc).all()
+
+
 def test_unsupported_combinations(gpu):
     s = scenes.random_soup(10, 64, 64, seed=0)
     r = prk.Renderer()

@@ -19,8 +19,9 @@ timeout -s KILL 100 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format cs
 python3 tools/pmc_traffic.py $o 4096x4096_T1000000_r16_N1 $tag profiles/pmc_traffic.json > $o/pmct.log 2>&1 || exit $?
 timeout -s KILL 100 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_SALU --kernel-trace --output-format csv -d $o/sq1 -o p1 -- $B > $o/sq1.log 2>&1 || exit $?
 timeout -s KILL 100 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_BUSY_CYCLES SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_LDS --kernel-trace --output-format csv -d $o/sq2 -o p2 -- $B > $o/sq2.log 2>&1 || exit $?
-python3 tools/sqsum.py $o > $o/sq_summary.txt 2>&1 || exit $?
+python3 tools/sqsum.py $o --json profiles/sq_valu.json 4096x4096_T1000000_r16_N1 $tag > $o/sq_summary.txt 2>&1 || exit $?
 timeout -k 10 300 python3 bench.py > $o/bench.log 2>&1 || exit $?
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $o/stats -o stats -- python3 bench.py --steps 10 --cpu-baseline 0 > $o/stats.log 2>&1 || exit $?
 cp profiles/pmc_traffic.json $o/pmc_traffic.json
+cp profiles/sq_valu.json $o/sq_valu.json
 echo done

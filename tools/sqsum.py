@@ -15,8 +15,14 @@ import csv
 import glob
 import sys
 
-d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/sq"
-csv_out = sys.argv[2] if len(sys.argv) > 2 else None  # optional compact CSV: kernel,counter,mean
+args = sys.argv[1:]
+json_out = None  # --json OUT KEY ROUND: per-kernel VALU figures into OUT[KEY] (bench.py roofline.valu)
+if "--json" in args:
+    i = args.index("--json")
+    json_out = args[i + 1:i + 4]
+    del args[i:i + 4]
+d = args[0] if len(args) > 0 else "gpurun_out/sq"
+csv_out = args[1] if len(args) > 1 else None  # optional compact CSV: kernel,counter,mean
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for p in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(p)):
@@ -50,3 +56,31 @@ if csv_out:
         for k, cs in sorted(acc.items()):
             for c, v in sorted(cs.items()):
                 w.writerow([k, c, sum(v) / len(v), len(v)])
+if json_out:
+    import json
+    import os
+    out, key, rnd = json_out
+    kern = {}
+    for k, cs in acc.items():
+        m = {c: sum(v) / len(v) for c, v in cs.items()}
+        e = {"dispatches": len(next(iter(cs.values())))}
+        if m.get("SQ_ACTIVE_INST_VALU"):
+            e["valu_time_estimate_ms"] = m["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / 2.4e6
+            if "SQ_THREAD_CYCLES_VALU" in m:
+                e["lane_utilisation"] = m["SQ_THREAD_CYCLES_VALU"] / (64 * m["SQ_ACTIVE_INST_VALU"])
+        if "SQ_INSTS_VALU" in m:
+            e["valu_issue_floor_ms"] = m["SQ_INSTS_VALU"] * 2 / 1024 / 2.4e6
+            e["insts_valu"] = m["SQ_INSTS_VALU"]
+        if m.get("SQ_WAVE_CYCLES"):
+            e["wait_any_frac"] = m.get("SQ_WAIT_ANY", 0.0) / m["SQ_WAVE_CYCLES"]
+        kern[k] = e
+    db = {}
+    if os.path.exists(out):
+        with open(out) as fh:
+            db = json.load(fh)
+    db[key] = {"round": rnd, "source": d, "per_kernel": kern,
+               "method": "rocprofv3 --pmc SQ counters (two passes), mean per dispatch; VALU-time estimate = "
+                         "SQ_ACTIVE_INST_VALU*4/1024 SIMDs/2.4 GHz, lane utilisation = "
+                         "SQ_THREAD_CYCLES_VALU/(64*SQ_ACTIVE_INST_VALU)"}
+    with open(out, "w") as fh:
+        json.dump(db, fh, indent=1, sort_keys=True)
