@@ -41,14 +41,15 @@ hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, co
 hipError_t prk_walk_select_bytes(uint32_t, size_t *);
 hipError_t prk_selftest_div_launch(uint32_t n, uint64_t seed, unsigned long long *bad, hipStream_t s);
 hipError_t prk_obj_walk(const prk::FrameParams *, const void *, uint32_t, void *, uint32_t *, uint32_t *, int,
-                        uint32_t *, const uint32_t *, void *, void *, uint32_t *, const void *, const void *,
+                        uint32_t *, const uint32_t *, void *, void *, void *, uint32_t *, const void *, const void *,
                         hipStream_t);
 hipError_t prk_scan_u32(const uint32_t *, uint32_t *, uint32_t, void *, size_t *, hipStream_t);
 hipError_t prk_span_count(const prk::FrameParams *, const void *, uint32_t, uint32_t *, hipStream_t);
 hipError_t prk_span_bin(const prk::FrameParams *, const void *, uint32_t, const uint32_t *, uint32_t, uint32_t *,
                         uint32_t *, uint32_t *, uint32_t *, uint32_t *, void *, size_t *, hipStream_t);
 hipError_t prk_launch_spans(const prk::FrameParams *, const uint32_t *, const uint32_t *, const void *,
-                            const void *, const uint32_t *, uint32_t *, uint32_t *, hipStream_t);
+                            const void *, const void *, uint32_t, const uint32_t *, uint32_t *, uint32_t *,
+                            hipStream_t);
 }
 
 // prk_spans.hip's object descriptor.
@@ -194,7 +195,8 @@ struct prk_context {
     // Span path (whole-object AETs) scratch, reused frame to frame.
     struct SpanScratch {
         DevBuf d_draws, d_texs, d_objs, d_edges, d_ord, d_tmp, d_cnt, d_off, d_temp, d_recs, d_pos, d_span_tri,
-            d_scnt, d_soff, d_keys_a, d_vals_a, d_keys_b, d_vals_b, d_offs, d_nwin, d_wtag, d_edges_in, d_spans_in;
+            d_scnt, d_soff, d_keys_a, d_vals_a, d_keys_b, d_vals_b, d_offs, d_nwin, d_wtag, d_edges_in, d_spans_in,
+            d_srecs;
     } spans;
 };
 
@@ -304,7 +306,7 @@ int prk_destroy(prk_context *c) {
         DevBuf *sb[] = {&S.d_draws, &S.d_texs, &S.d_objs, &S.d_edges, &S.d_ord, &S.d_tmp, &S.d_cnt, &S.d_off,
                         &S.d_temp, &S.d_recs, &S.d_pos, &S.d_span_tri, &S.d_scnt, &S.d_soff, &S.d_keys_a,
                         &S.d_vals_a, &S.d_keys_b, &S.d_vals_b, &S.d_offs, &S.d_nwin, &S.d_wtag, &S.d_edges_in,
-                        &S.d_spans_in};
+                        &S.d_spans_in, &S.d_srecs};
         for (DevBuf *b : sb) b->release();
     }
     if (c->s_mark) (void)hipEventDestroy(c->s_mark);
@@ -663,9 +665,6 @@ int prk_draw_objects(prk_context *c, int32_t geometry, uint32_t first_tri, uint3
     if ((phong || !tex) && !g.N) return PRK_ERR_ARG;
     if (tex && !g.UV) return PRK_ERR_ARG;
     if ((mode == prk::MODE_SC_GOURAUD || mode == prk::MODE_SC_PHONG) && !g.C) return PRK_ERR_ARG;
-    // Whole-object AETs are emulated for the AVX semantics (the reference of
-    // record and the single-thread overload); DrawModel's (scalar) are not.
-    if (tris_per_object > 1 && mode != prk::MODE_AVX) return PRK_ERR_UNSUPPORTED;
     if (tri_count == 0) return PRK_OK;
     if ((uint64_t)c->pending_tris + tri_count >= 0xFFFFFFF0ull) return PRK_ERR_ARG;
     // A draw that continues the previous one (same geometry, the next
@@ -713,15 +712,24 @@ int prk_draw_objects(prk_context *c, int32_t geometry, uint32_t first_tri, uint3
 static int draw_src(prk_context *c, uint32_t kind, uint32_t off, uint32_t n, uint32_t ids, int32_t semantics,
                     int32_t phong, int32_t texture) {
     if (texture >= (int32_t)c->texs.size()) return PRK_ERR_ARG;
-    if (semantics != PRK_SEM_AVX && semantics != PRK_SEM_AVX_ST) {
-        return semantics == PRK_SEM_SCALAR ? PRK_ERR_UNSUPPORTED : PRK_ERR_ARG;
+    int mode = prk::MODE_AVX;
+    if (semantics == PRK_SEM_SCALAR) {
+        // DrawModel on a caller's edge list (projekt.cpp:162-601); work
+        // records (kind 2) are FillLineOptimized spans only
+        if (kind != 1) return PRK_ERR_UNSUPPORTED;
+        const bool tex = texture >= 0;
+        mode = phong ? (tex ? prk::MODE_SC_PHONG_TEX : prk::MODE_SC_PHONG)
+                     : (tex ? prk::MODE_SC_GOURAUD_TEX : prk::MODE_SC_GOURAUD);
+    } else if (semantics != PRK_SEM_AVX && semantics != PRK_SEM_AVX_ST) {
+        return PRK_ERR_ARG;
+    } else if (texture < 0 || !phong) {
+        return PRK_ERR_UNSUPPORTED;  // projekt.cpp:1506, 2285-2316
     }
-    if (texture < 0 || !phong) return PRK_ERR_UNSUPPORTED;  // projekt.cpp:1506, 2285-2316
     if ((uint64_t)c->pending_tris + ids >= 0xFFFFFFF0ull) return PRK_ERR_ARG;
     prk::DrawRec d{};
     d.first_global = c->pending_tris;
     d.tri_count = ids;
-    d.mode = prk::MODE_AVX;
+    d.mode = mode;
     d.tex = texture;
     d.flags = semantics == PRK_SEM_AVX_ST ? prk::DRAW_ST : 0u;
     d.obj_tris = 1;
@@ -1199,7 +1207,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(S.d_objs.ensure(objs.size() * sizeof(ObjDesc)));
     PRK_TRY(hipMemcpy(S.d_objs.p, objs.data(), objs.size() * sizeof(ObjDesc), hipMemcpyHostToDevice));
     const size_t es = std::max<size_t>((size_t)eslots, 1);
-    PRK_TRY(S.d_edges.ensure(es * 80));
+    PRK_TRY(S.d_edges.ensure(es * 112));  // prk_spans.hip ObjEdge
     PRK_TRY(S.d_ord.ensure(es * 4));
     PRK_TRY(S.d_tmp.ensure(es * 4));
     if (!c->pend_edges.empty()) {
@@ -1212,12 +1220,15 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
         PRK_TRY(hipMemcpy(S.d_spans_in.p, c->pend_spans.data(), c->pend_spans.size() * sizeof(prk_span),
                           hipMemcpyHostToDevice));
     }
+    uint32_t modes = 0;  // the pass's span kinds: bit per Mode
+    for (const auto &d : draws) modes |= 1u << d.mode;
+    const bool scalar = (modes & ~(1u << prk::MODE_AVX)) != 0;
     PRK_TRY(S.d_cnt.ensure(((size_t)nobj + 1) * 4));
     PRK_TRY(S.d_off.ensure(((size_t)nobj + 1) * 4));
     uint32_t *cnt = (uint32_t *)S.d_cnt.p, *off = (uint32_t *)S.d_off.p;
     PRK_TRY(hipMemsetAsync(cnt, 0, ((size_t)nobj + 1) * 4, s));
     PRK_TRY(prk_obj_walk(&fp, S.d_objs.p, nobj, S.d_edges.p, (uint32_t *)S.d_ord.p, (uint32_t *)S.d_tmp.p, 0, cnt,
-                         nullptr, nullptr, nullptr, nullptr, S.d_edges_in.p, S.d_spans_in.p, s));
+                         nullptr, nullptr, nullptr, nullptr, nullptr, S.d_edges_in.p, S.d_spans_in.p, s));
     size_t tb = 0;
     PRK_TRY(prk_scan_u32(cnt, off, nobj + 1, nullptr, &tb, s));
     PRK_TRY(S.d_temp.ensure(std::max<size_t>(tb, 16)));
@@ -1230,9 +1241,10 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(S.d_recs.ensure(ns * 64));
     PRK_TRY(S.d_pos.ensure(ns * 16));
     PRK_TRY(S.d_span_tri.ensure(ns * 4));
+    if (scalar) PRK_TRY(S.d_srecs.ensure(ns * 96));  // DrawModel span records (prk_spans.hip ScSpanRecG)
     PRK_TRY(prk_obj_walk(&fp, S.d_objs.p, nobj, S.d_edges.p, (uint32_t *)S.d_ord.p, (uint32_t *)S.d_tmp.p, 1, cnt,
-                         off, S.d_recs.p, S.d_pos.p, (uint32_t *)S.d_span_tri.p, S.d_edges_in.p, S.d_spans_in.p,
-                         s));
+                         off, S.d_recs.p, scalar ? S.d_srecs.p : nullptr, S.d_pos.p, (uint32_t *)S.d_span_tri.p,
+                         S.d_edges_in.p, S.d_spans_in.p, s));
     PRK_TRY(S.d_scnt.ensure(((size_t)nspan + 1) * 4));
     PRK_TRY(S.d_soff.ensure(((size_t)nspan + 1) * 4));
     uint32_t *scnt = (uint32_t *)S.d_scnt.p, *soff = (uint32_t *)S.d_soff.p;
@@ -1262,8 +1274,8 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(S.d_nwin.ensure((size_t)ntiles * 4));
     PRK_TRY(S.d_wtag.ensure((size_t)ntiles * c->tile_w * c->tile_h * 4));
     PRK_TRY(prk_launch_spans(&fp, (const uint32_t *)S.d_offs.p, (const uint32_t *)S.d_vals_b.p, S.d_pos.p,
-                             S.d_recs.p, (const uint32_t *)S.d_span_tri.p, (uint32_t *)S.d_nwin.p,
-                             (uint32_t *)S.d_wtag.p, s));
+                             S.d_recs.p, scalar ? S.d_srecs.p : nullptr, modes, (const uint32_t *)S.d_span_tri.p,
+                             (uint32_t *)S.d_nwin.p, (uint32_t *)S.d_wtag.p, s));
     return PRK_OK;
 }
 

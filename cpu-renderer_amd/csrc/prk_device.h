@@ -55,6 +55,11 @@ struct DrawRec {
 // z >= zbuf, so among equal z the LATEST fragment wins (and it beats an equal
 // prior z).
 enum : uint32_t { DRAW_ST = 1u };
+// Span path (whole-object AETs): SpanPos flags of a DrawModel (scalar) span,
+// whose mode sits at bits 8..15, and the first word of its FillLineOptimized
+// record slot (no AVX record has bit 31 set: texture indices are < 2^15).
+constexpr uint32_t SPAN_SCALAR = 2u;
+constexpr uint32_t kScalarSpan = 0x80000000u;
 
 // Visibility key low words.  Keys are max-reduced: a
 // fragment's key is (ordered z << 32) | tag.  Queue-semantics pairs (strict

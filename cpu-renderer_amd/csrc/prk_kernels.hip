@@ -1461,6 +1461,7 @@ __global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__r
         const float4 *q = reinterpret_cast<const float4 *>(recs + (SPAN ? (size_t)j : (size_t)j * fp.tile_h + ly));
         const float4 r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];
         const int32_t lt = __float_as_int(r0.x);
+        if (SPAN && (uint32_t)lt == kScalarSpan) continue;  // a DrawModel span won: k_span_shade
         const int32_t LeftXa = (int32_t)(int16_t)(lt & 0xFFFF);
         const TexRec tex = UNI ? fp.tex0 : fp.texs[lt >> 16];
         const int32_t rel = x - LeftXa, i = rel & 7, b = rel >> 3;
@@ -1492,16 +1493,82 @@ __global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__r
 
 // ---------------------------------------------------------------------------
 // Span path (whole-object AETs, prk_spans.hip): visibility over a tile's bin
-// of spans.  Every span is one pair of one row, given by its lane-init record
-// (SpanRec) and pixel range; its tag is its submission-order index.  The
-// items are the triangle path's visibility items (item_vis_group).
+// of spans.  Every span is one pair of one row, given by its record and pixel
+// range; its tag is its submission-order index.  FillLineOptimized spans
+// (SpanRec) take the triangle path's visibility items (item_vis_group),
+// DrawModel spans (ScSpanRec, SPAN_SCALAR) its scalar chunk items
+// (item_scalar), the one-past-the-row pixel included.
 // ---------------------------------------------------------------------------
 struct SpanPosK { int32_t row, minx, maxx; uint32_t flags; };  // == prk_spans.hip SpanPos
+struct ScSpanRec { float f[22]; int32_t tex, pad; };          // == prk_spans.hip ScSpanRecG
+static_assert(sizeof(ScSpanRec) == 96, "scalar span record");
+constexpr int32_t kAvxSlot = -2;  // SI_OVF of a slot holding a FillLineOptimized span
+
+// The wave's items: every lane holds `items` work items of the span in its
+// slot; f(slot, j) runs item j of that slot, spread over the lanes in windows
+// of 64 (item -> slot: a prefix max over span-start marks, as in sweep()).
+template <class WS, class F>
+__device__ __forceinline__ void wave_items(WS &ws, int items, int lane, F &&f) {
+    const int incl = wave_incl_scan(items, lane);
+    const int total = __builtin_amdgcn_readlane(incl, 63);
+    const int excl = incl - items;
+    ws.i[SI_PRE][lane] = excl;
+    int carry = 0;
+    for (int it0 = 0; it0 < total; it0 += 64) {
+        ws.i[SI_MARK][lane] = 0;
+        wave_lds_sync();
+        if (items > 0 && excl >= it0 && excl < it0 + 64) ws.i[SI_MARK][excl - it0] = lane + 1;
+        wave_lds_sync();
+        const int m = max(wave_incl_max(ws.i[SI_MARK][lane]), carry);
+        carry = __builtin_amdgcn_readlane(m, 63);
+        const int it = it0 + lane;
+        if (it < total) {
+            const int sl = m - 1;
+            f(sl, it - ws.i[SI_PRE][sl]);
+        }
+    }
+    wave_lds_sync();
+}
+
+// A DrawModel span's slot for tile tc (scalar items, visibility or shading):
+// the part [xa, xb) of its inclusive [MinX, MaxX] in the tile's columns of
+// its row, and the one-past-the-row pixel (Row + 1, 0) when MaxX == W and
+// that pixel lies in the tile (span_setup_scalar's ranges).  Returns the
+// item count.
+template <bool SHADE, class WS>
+__device__ __forceinline__ int span_slot_scalar(const FrameParams &fp, const TileCtx &tc, WS &ws, int lane,
+                                                const SpanPosK &sp, const ScSpanRec *__restrict__ srecs,
+                                                uint32_t sidx) {
+    const int32_t W = fp.W;
+    const int32_t MinX = sp.minx, MaxX = sp.maxx - 1;
+    const bool in_rows = sp.row >= tc.y0 && sp.row < tc.y1;
+    const int32_t xa = in_rows ? max(MinX, tc.x0) : 0;
+    const int32_t xb = in_rows ? min(MaxX + 1, tc.x1) : 0;
+    const bool ovf = tc.x0 == 0 && MaxX >= W && sp.row + 1 >= tc.y0 && sp.row + 1 < tc.y1;
+    if (xa >= xb && !ovf) return 0;
+    const ScSpanRec &r = srecs[sidx];
+    ws.i[SI_XA][lane] = xa;
+    ws.i[SI_XB][lane] = xb;
+    ws.i[SI_LEFT][lane] = MinX;
+    ws.i[SI_TAG][lane] = (int32_t)pair_tag(sidx, false);
+    ws.i[SI_OVF][lane] = ovf ? (sp.row + 1 - tc.y0) * tc.tw : -1;
+    ws.i[SI_ROW][lane] = sp.row;
+    if constexpr (SHADE) {
+        ws.i[SI_TEX][lane] = r.tex;
+#pragma unroll
+        for (int k = 0; k < kSpanF; ++k) ws.f[k][lane] = r.f[k];
+    } else {
+        ws.f[SS_Z][lane] = r.f[SS_Z];
+        ws.f[SS_IZ][lane] = r.f[SS_IZ];
+    }
+    return scalar_chunks<SHADE>(xa, xb) + (ovf ? 1 : 0);
+}
 
 __global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
     k_span_vis(FrameParams fp, const uint32_t *__restrict__ offs, const uint32_t *__restrict__ bins,
                const SpanPosK *__restrict__ pos, const SpanRec *__restrict__ recs,
-               const uint32_t *__restrict__ span_tri, uint32_t *__restrict__ nwin_out, uint32_t *__restrict__ wtag) {
+               const ScSpanRec *__restrict__ srecs, const uint32_t *__restrict__ span_tri,
+               uint32_t *__restrict__ nwin_out, uint32_t *__restrict__ wtag) {
     extern __shared__ unsigned long long lds[];
     const int ntile = fp.tiles_x * fp.tiles_y;
     const int t = blockIdx.x;
@@ -1537,7 +1604,9 @@ __global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
         if (i < n) {
             const uint32_t sidx = bins[b0 + i];
             const SpanPosK sp = pos[sidx];
-            if (sp.row >= tc.y0 && sp.row < tc.y1) {
+            if (sp.flags & SPAN_SCALAR) {
+                items = span_slot_scalar<false>(fp, tc, ws, lane, sp, srecs, sidx);
+            } else if (sp.row >= tc.y0 && sp.row < tc.y1) {
                 const int32_t xa = max(sp.minx, tc.x0), xb = min(sp.maxx, tc.x1);
                 if (xa < xb) {
                     const float4 *q = reinterpret_cast<const float4 *>(recs + sidx);
@@ -1547,6 +1616,7 @@ __global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
                     ws.i[SI_LEFT][lane] = (int32_t)(int16_t)(__float_as_int(r0.x) & 0xFFFF);
                     ws.i[SI_TAG][lane] = (int32_t)pair_tag(sidx, (sp.flags & DRAW_ST) != 0);
                     ws.i[SI_ROW][lane] = sp.row;
+                    ws.i[SI_OVF][lane] = kAvxSlot;
                     ws.f[SF_XOFF][lane] = r0.y;
                     ws.f[SF_LW][lane] = r0.z; ws.f[SF_LU][lane] = r0.w; ws.f[SF_LV][lane] = r1.x;
                     ws.f[SF_LZ][lane] = r1.y;
@@ -1556,31 +1626,10 @@ __global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
                 }
             }
         }
-        const int incl = wave_incl_scan(items, lane);
-        const int total = __builtin_amdgcn_readlane(incl, 63);
-        const int excl = incl - items;
-        ws.i[SI_PRE][lane] = excl;
-        int carry = 0;
-        for (int it0 = 0; it0 < total; it0 += 64) {
-            ws.i[SI_MARK][lane] = 0;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (items > 0 && excl >= it0 && excl < it0 + 64) ws.i[SI_MARK][excl - it0] = lane + 1;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const int m = max(wave_incl_max(ws.i[SI_MARK][lane]), carry);
-            carry = __builtin_amdgcn_readlane(m, 63);
-            const int it = it0 + lane;
-            if (it < total) {
-                const int sl = m - 1, j = it - ws.i[SI_PRE][sl];
-                item_vis_group(tc, ws, sl, j, ws.i[SI_ROW][sl]);
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_items(ws, items, lane, [&](int sl, int j) {
+            if (ws.i[SI_OVF][sl] == kAvxSlot) item_vis_group(tc, ws, sl, j, ws.i[SI_ROW][sl]);
+            else item_scalar<MODE_SC_GOURAUD, false, false>(fp, tc, ws, sl, j, ws.i[SI_ROW][sl]);
+        });
     }
     __syncthreads();
     uint32_t *tags_out = wtag + (size_t)t * npx;
@@ -1600,6 +1649,60 @@ __global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
     if (threadIdx.x == 0) nwin_out[t] = (uint32_t)anyw;
 }
 
+// Shading of the DrawModel spans of the span path, one workgroup per tile:
+// every scalar span of mode M in the tile's bin shades the pixels it won
+// (item_scalar, SHADE).  MODESET -1: one sweep per scalar mode.
+template <int M>
+__device__ __forceinline__ void span_shade_sweep(const FrameParams &fp, const TileCtx &tc, ShadeSlots &ws,
+                                                 const uint32_t *__restrict__ bins, uint32_t b0, uint32_t n,
+                                                 const SpanPosK *__restrict__ pos,
+                                                 const ScSpanRec *__restrict__ srecs) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t nwaves = blockDim.x >> 6;
+    for (uint32_t base = wave * 64; base < n; base += 64 * nwaves) {
+        const uint32_t i = base + lane;
+        int items = 0;
+        if (i < n) {
+            const uint32_t sidx = bins[b0 + i];
+            const SpanPosK sp = pos[sidx];
+            if ((sp.flags & SPAN_SCALAR) && (int)((sp.flags >> 8) & 0xFFu) == M)
+                items = span_slot_scalar<true>(fp, tc, ws, lane, sp, srecs, sidx);
+        }
+        wave_items(ws, items, lane,
+                   [&](int sl, int j) { item_scalar<M, true, false>(fp, tc, ws, sl, j, ws.i[SI_ROW][sl]); });
+    }
+}
+
+template <int MODESET>
+__global__ void __launch_bounds__(64 * kShadeWaves, PRK_SHADE_MIN_WAVES)
+    k_span_shade(FrameParams fp, const uint32_t *__restrict__ offs, const uint32_t *__restrict__ bins,
+                 const SpanPosK *__restrict__ pos, const ScSpanRec *__restrict__ srecs,
+                 const uint32_t *__restrict__ nwin_in, const uint32_t *__restrict__ wtag) {
+    extern __shared__ unsigned long long lds[];
+    const int ntile = fp.tiles_x * fp.tiles_y;
+    const int t = blockIdx.x;
+    if (t >= ntile || nwin_in[t] == 0) return;
+    const uint32_t b0 = offs[t], n = offs[t + 1] - b0;
+    TileCtx tc = tile_ctx(fp, t);
+    const int npx = fp.tile_w * fp.tile_h;
+    uint32_t *tags = reinterpret_cast<uint32_t *>(lds);
+    tc.tags = tags;
+    ShadeSlots *slots = reinterpret_cast<ShadeSlots *>(tags + npx + kTagPad);
+    ShadeSlots &ws = slots[threadIdx.x >> 6];
+    const uint32_t *tags_in = wtag + (size_t)t * npx;
+    for (int p = threadIdx.x; p < npx; p += blockDim.x) tags[p] = tags_in[p];
+    if (threadIdx.x < kTagPad) tags[npx + threadIdx.x] = 0xFFFFFFFFu;
+    __syncthreads();
+    if constexpr (MODESET >= 0) {
+        span_shade_sweep<(MODESET >= 0 ? MODESET : 1)>(fp, tc, ws, bins, b0, n, pos, srecs);
+    } else {
+        span_shade_sweep<MODE_SC_GOURAUD>(fp, tc, ws, bins, b0, n, pos, srecs);
+        span_shade_sweep<MODE_SC_GOURAUD_TEX>(fp, tc, ws, bins, b0, n, pos, srecs);
+        span_shade_sweep<MODE_SC_PHONG>(fp, tc, ws, bins, b0, n, pos, srecs);
+        span_shade_sweep<MODE_SC_PHONG_TEX>(fp, tc, ws, bins, b0, n, pos, srecs);
+    }
+}
+
 // Explicit instantiations used by the host.
 #define PRK_VIS_ARGS FrameParams, const uint32_t *, const uint2 *, uint8_t *, uint32_t *, uint32_t *, uint32_t *, \
                      const uint32_t *, uint8_t *, uint32_t *
@@ -1616,6 +1719,11 @@ template __global__ void k_walk<true>(PRK_WALK_ARGS);
 template __global__ void k_pix<false>(PRK_PIX_ARGS);
 template __global__ void k_pix<true>(PRK_PIX_ARGS);
 template __global__ void k_pix<false, true>(PRK_PIX_ARGS);
+#define PRK_SPAN_SHADE_ARGS FrameParams, const uint32_t *, const uint32_t *, const SpanPosK *, const ScSpanRec *, \
+                            const uint32_t *, const uint32_t *
+template __global__ void k_span_shade<-1>(PRK_SPAN_SHADE_ARGS);
+template __global__ void k_span_shade<MODE_SC_GOURAUD>(PRK_SPAN_SHADE_ARGS);
+template __global__ void k_span_shade<MODE_SC_PHONG>(PRK_SPAN_SHADE_ARGS);
 PRK_INST(-1, false)
 PRK_INST(MODE_AVX, false)
 PRK_INST(MODE_AVX, true)
@@ -1787,18 +1895,31 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
     return hipGetLastError();
 }
 
-// Span path: visibility then shading of the pass's spans.
+// Span path: visibility then shading of the pass's spans.  scalar_modes: bit
+// m set when the pass holds DrawModel spans of mode m (srecs non-null then);
+// bit MODE_AVX when it holds FillLineOptimized spans.
 hipError_t prk_launch_spans(const prk::FrameParams *fp, const uint32_t *offs, const uint32_t *bins, const void *pos,
-                            const void *recs, const uint32_t *span_tri, uint32_t *nwin, uint32_t *wtag,
-                            hipStream_t s) {
+                            const void *recs, const void *srecs, uint32_t modes, const uint32_t *span_tri,
+                            uint32_t *nwin, uint32_t *wtag, hipStream_t s) {
     const uint32_t ntile = (uint32_t)(fp->tiles_x * fp->tiles_y);
     if (ntile == 0) return hipSuccess;
-    const size_t lv = vis_lds(fp);
-    hipLaunchKernelGGL(prk::k_span_vis, dim3(ntile), dim3(64 * prk::kVisWaves), lv, s, *fp, offs, bins,
-                       reinterpret_cast<const prk::SpanPosK *>(pos), reinterpret_cast<const prk::SpanRec *>(recs),
-                       span_tri, nwin, wtag);
-    hipLaunchKernelGGL((prk::k_pix<false, true>), dim3(ntile * PRK_PIX_SPLIT), dim3(256), 0, s, *fp, nwin, wtag,
-                       reinterpret_cast<const prk::SpanRec *>(recs));
+    const uint32_t sc = modes & ~(1u << prk::MODE_AVX);
+    if (sc && !srecs) return hipErrorInvalidValue;
+    const size_t lv = vis_lds(fp), ls = shade_lds(fp);
+    const prk::SpanPosK *P = reinterpret_cast<const prk::SpanPosK *>(pos);
+    const prk::ScSpanRec *SR = reinterpret_cast<const prk::ScSpanRec *>(srecs);
+    hipLaunchKernelGGL(prk::k_span_vis, dim3(ntile), dim3(64 * prk::kVisWaves), lv, s, *fp, offs, bins, P,
+                       reinterpret_cast<const prk::SpanRec *>(recs), SR, span_tri, nwin, wtag);
+    if ((modes & (1u << prk::MODE_AVX)) || fp->clear_fused)
+        hipLaunchKernelGGL((prk::k_pix<false, true>), dim3(ntile * PRK_PIX_SPLIT), dim3(256), 0, s, *fp, nwin, wtag,
+                           reinterpret_cast<const prk::SpanRec *>(recs));
+#define PRK_SPAN_SHADE(MS) \
+    hipLaunchKernelGGL((prk::k_span_shade<MS>), dim3(ntile), dim3(64 * prk::kShadeWaves), ls, s, *fp, offs, bins, P, \
+                       SR, nwin, wtag)
+    if (sc == (1u << prk::MODE_SC_GOURAUD)) PRK_SPAN_SHADE(prk::MODE_SC_GOURAUD);
+    else if (sc == (1u << prk::MODE_SC_PHONG)) PRK_SPAN_SHADE(prk::MODE_SC_PHONG);
+    else if (sc) PRK_SPAN_SHADE(-1);
+#undef PRK_SPAN_SHADE
     return hipGetLastError();
 }
 

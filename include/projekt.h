@@ -492,9 +492,6 @@ inline int issue(state &st) {
             if (d.Kind == DRAW_OBJECT) {
                 const frame_object &o = st.Objects[d.First];
                 r = prk_draw_objects(c, st.Geom, o.FirstTri, o.Tris, o.Tris, o.P, d.Semantics, d.Phong, d.Texture);
-                if (r == PRK_ERR_UNSUPPORTED && d.Semantics == PRK_SEM_SCALAR && o.Tris > 1)
-                    // DrawModel's scalar whole-object AET is not emulated: per triangle
-                    r = prk_draw_objects(c, st.Geom, o.FirstTri, o.Tris, 1, o.P, d.Semantics, d.Phong, d.Texture);
             } else if (d.Kind == DRAW_EDGES) {
                 r = prk_draw_edges(c, st.Edges.data() + d.First, d.Count, d.Semantics, d.Phong, d.Texture);
             } else {

@@ -206,16 +206,17 @@ def fill_edge_table_words(scene, tri0=0, n=1, phong=True, semantics=abi.PRK_SEM_
     return words.reshape(-1, 27)[: cnt.value].copy()
 
 
-def _src_render(fn, scene, items, semantics, color, z, tri_index):
+def _src_render(fn, scene, items, semantics, color, z, tri_index, phong=True):
     W, H = scene.width, scene.height
     col = np.full((H, W), CLEAR_COLOR, np.uint32) if color is None else color
     zb = np.full((H, W), CLEAR_Z, np.float32) if z is None else z
     win = np.full((H, W), -1, np.int32)
-    k = _Keep(scene, semantics, True, 1)
+    k = _Keep(scene, semantics, phong, 1)
     tg = OrTarget(_ptr(col), W * 4, _ptr(zb), W, H, _ptr(win))
     stats = (C.c_uint64 * 3)()
     items = np.ascontiguousarray(items, np.uint32)
-    rc = fn(_ptr(items), C.c_uint32(items.shape[0]), C.c_int32(semantics), C.pointer(k.bitmap), C.c_int32(1),
+    bm = C.pointer(k.bitmap) if k.bitmap is not None else None
+    rc = fn(_ptr(items), C.c_uint32(items.shape[0]), C.c_int32(semantics), bm, C.c_int32(int(bool(phong))),
             C.c_int32(k.desc.Filter), C.c_int32(tri_index), C.byref(tg), C.byref(k.transform), C.byref(k.lights),
             stats)
     if rc != 0:
@@ -223,10 +224,10 @@ def _src_render(fn, scene, items, semantics, color, z, tri_index):
     return col, zb, win, dict(spans=stats[0], span_pixels=stats[1], writes=stats[2])
 
 
-def render_edges(scene, edge_words, semantics=abi.PRK_SEM_AVX, color=None, z=None, tri_index=0):
-    """DrawModelOptimized* of one ready edge list ([n, 27] prk_edge words)
-    with the scene's camera, lights and texture."""
-    return _src_render(lib().oracle_draw_edges, scene, edge_words, semantics, color, z, tri_index)
+def render_edges(scene, edge_words, semantics=abi.PRK_SEM_AVX, color=None, z=None, tri_index=0, phong=True):
+    """DrawModelOptimized* (or, PRK_SEM_SCALAR, DrawModel) of one ready edge
+    list ([n, 27] prk_edge words) with the scene's camera, lights and texture."""
+    return _src_render(lib().oracle_draw_edges, scene, edge_words, semantics, color, z, tri_index, phong)
 
 
 def render_spans(scene, span_words, semantics=abi.PRK_SEM_AVX, color=None, z=None, tri_index=0):

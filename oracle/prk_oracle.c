@@ -1002,8 +1002,10 @@ int oracle_draw_edges(const prk_edge *E, uint32_t n, int32_t semantics, const pr
                       int32_t filter, int32_t tri_index, const or_target *Tg, const prk_transform *T,
                       const prk_light_data *L, uint64_t *stats)
 {
-    if (semantics != PRK_SEM_AVX && semantics != PRK_SEM_AVX_ST) return PRK_ERR_UNSUPPORTED;
-    if (!Bm || !phong || (Tg->Width % 8)) return PRK_ERR_UNSUPPORTED;
+    /* DrawModelOptimized* (AVX semantics) or DrawModel (scalar, 162-601) */
+    const int scalar = semantics == PRK_SEM_SCALAR;
+    if (!scalar && semantics != PRK_SEM_AVX && semantics != PRK_SEM_AVX_ST) return PRK_ERR_UNSUPPORTED;
+    if (!scalar && (!Bm || !phong || (Tg->Width % 8))) return PRK_ERR_UNSUPPORTED;
     or_edge *Edges = (or_edge *)calloc((size_t)n + 1, sizeof(or_edge));
     if (!Edges) return PRK_ERR_NOMEM;
     for (uint32_t i = 0; i < n; ++i) {
@@ -1019,7 +1021,7 @@ int oracle_draw_edges(const prk_edge *E, uint32_t n, int32_t semantics, const pr
     or_ctx X_;
     or_ctx_for(&X_, semantics, Bm, phong, filter, Tg, T, L);
     X_.TriIndex = tri_index;
-    or_aet_walk(&X_, Edges, n, or_fill_line_optimized);
+    or_aet_walk(&X_, Edges, n, scalar ? or_fill_line_scalar : or_fill_line_optimized);
     free(Edges);
     if (stats) { stats[0] += X_.Spans; stats[1] += X_.SpanPixels; stats[2] += X_.Writes; }
     return PRK_OK;

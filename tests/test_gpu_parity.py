@@ -463,15 +463,15 @@ def test_whole_object_mixed_passes(gpu):
     run_both(s)
 
 
-def _render_src(scene, kind, words, semantics):
+def _render_src(scene, kind, words, semantics, phong=True, textured=True):
     r = prk.Renderer()
     try:
         r.target_alloc(scene.width, scene.height)
         r.clear()
         r.set_debug(True)
         r.set_camera(scene.prk_transform(), scene.prk_lights())
-        tex = r.texture(scene.texture)
-        (r.draw_edges if kind == "edges" else r.draw_spans)(words, semantics=semantics, bitmap=tex)
+        tex = r.texture(scene.texture) if textured else None
+        (r.draw_edges if kind == "edges" else r.draw_spans)(words, semantics=semantics, bitmap=tex, phong=phong)
         r.complete_all_work()
         c, z = r.download()
         return c, z, r.winners(), r.stats()
@@ -518,16 +518,58 @@ def test_draw_caller_spans(gpu, sem):
     compare(_render_src(s, "spans", w, sem), O.render_spans(s, w, semantics=sem), label="spans")
 
 
-def test_whole_object_scalar_unsupported(gpu):
-    s = scenes.random_soup(10, 64, 64, seed=0)
-    r = prk.Renderer()
-    try:
-        g = r.geometry(s.vertices, s.colors, s.normals, s.uvs)
-        with pytest.raises(prk.PrkError) as e:
-            r.draw(abi.PRK_SEM_SCALAR, g, 10, phong=False, tris_per_object=5)
-        assert e.value.code == abi.PRK_ERR_UNSUPPORTED
-    finally:
-        r.close()
+@pytest.mark.parametrize("phong", [False, True])
+def test_whole_object_scalar_construct_sphere(gpu, phong):
+    """DrawModel (projekt.cpp:162-601) on ConstructSphere submitted as ONE
+    render_entry_3d_object: one active edge table for the whole object
+    (insertion / expiry / pairing 168-300, stepping 540-598), Gouraud and
+    untextured Phong spans paired across triangles, against the oracle's
+    whole-object walk.  Differs from the per-triangle image."""
+    s = _sphere_scene()
+    s.texture = None
+    g, o = run_both(s, semantics=abi.PRK_SEM_SCALAR, phong=phong, tris_per_object=s.tri_count, threads=1,
+                    exact_color=not phong, label="sphere scalar phong=%d" % phong)
+    per_tri = O.render(s, semantics=abi.PRK_SEM_SCALAR, phong=phong)
+    assert (g[1].view(np.uint32) != per_tri[1].view(np.uint32)).any()
+    assert (g[2] >= 0).sum() > 10000
+
+
+@pytest.mark.parametrize("phong,textured", [(False, False), (True, False), (False, True), (True, True)])
+@pytest.mark.parametrize("tpo,seed", [(2, 1), (5, 2), (16, 3)])
+def test_whole_object_scalar_random_objects(gpu, tpo, seed, phong, textured):
+    """Random DrawModel objects of several triangles in every scalar mode,
+    clipped on every side (the one-past-the-row store at the right border
+    included), with ties."""
+    s = scenes.with_ties(scenes.random_soup(2000, 256, 192, radius=30, seed=seed, centroid_margin=30,
+                                            textured=textured, lights=scenes.LIGHTS_TWO,
+                                            ambient=scenes.AMBIENT_TWO), seed=seed)
+    run_both(s, semantics=abi.PRK_SEM_SCALAR, phong=phong, tris_per_object=tpo, exact_color=not phong,
+             label="scalar objects tpo=%d phong=%d tex=%d" % (tpo, phong, textured))
+
+
+def test_whole_object_scalar_bands_and_passes(gpu):
+    """Scalar whole objects in row bands (a band's first row receives the
+    one-past-the-row store of the row above it) and mixed with per-triangle
+    and AVX object passes in one frame."""
+    s = scenes.with_ties(scenes.random_soup(3000, 256, 256, radius=24, seed=9, centroid_margin=30), seed=9)
+    oc, oz, ow, _ = O.render(s, semantics=abi.PRK_SEM_SCALAR, phong=False, tris_per_object=7)
+    for r0, r1 in [(0, 96), (96, 97), (97, 256)]:
+        gc, gz, gw, _ = prk.render_scene(s, semantics=abi.PRK_SEM_SCALAR, phong=False, tris_per_object=7,
+                                         rows=(r0, r1))
+        compare((gc, gz, gw, None), (oc[r0:r1], oz[r0:r1], ow[r0:r1], None), label="band %d-%d" % (r0, r1))
+    T = s.tri_count
+    q = T // 4
+    s.draws = [(0, q, None, abi.PRK_SEM_SCALAR, 5), (q, q, s.texture, abi.PRK_SEM_AVX, 4),
+               (2 * q, q, None, abi.PRK_SEM_SCALAR, 1), (3 * q, T - 3 * q, s.texture, abi.PRK_SEM_SCALAR, 3)]
+    run_both(s, phong=True, exact_color=False, label="mixed scalar/AVX object passes")
+
+
+def test_draw_caller_edge_list_scalar(gpu):
+    """DrawModel on a ready edge_info list (prk_draw_edges, scalar)."""
+    s = scenes.random_soup(60, 256, 256, radius=60, seed=44, textured=False, centroid_margin=40)
+    words = O.fill_edge_table_words(s, 0, 60, phong=False)
+    got = _render_src(s, "edges", words, abi.PRK_SEM_SCALAR, phong=False, textured=False)
+    compare(got, O.render_edges(s, words, semantics=abi.PRK_SEM_SCALAR, phong=False), label="scalar edges")
 
 
 def test_geometry_update_null_array_grows(gpu):
