@@ -1394,6 +1394,60 @@ int prk_download_winners(prk_context *c, int32_t *w) {
     return PRK_OK;
 }
 
+// FillEdgeTable's return value (projekt.cpp:3882-4121), computed on the host
+// at the call so the drop-in can return it there: the number of edge_info
+// records the reference writes for one object, i.e. over its triangles that
+// pass the back-face test (3926-3943) the edges with MaxY > 0 (3968) and
+// MinY != MaxY (4066).  The same float operations as the device setup
+// (ProjectVertex 74-93, Normalize(a) = (1/sqrt(a.a))*a); the library is built
+// with -ffp-contract=off, so host and device round alike.  The setup itself
+// (edges, gradients, lighting, MergeSort) runs on the GPU at the flush.
+static inline void host_project(const float c[3], const prk_transform *T, float r[3]) {
+    r[0] = r[1] = r[2] = 0.0f;
+    const float d = T->DistanceAboveTarget - c[2];
+    if (d > 0.2f) {
+        const float k = (1.0f / d) * T->FocalLength;
+        const float px = k * c[0], py = k * c[1];
+        r[0] = T->ScreenCenter[0] + T->MetersToPixels * px;
+        r[1] = T->ScreenCenter[1] + T->MetersToPixels * py;
+        r[2] = d + T->MetersToPixels * 0.0f;
+    }
+}
+static inline void host_normalize(float &x, float &y, float &z) {
+    const float s = 1.0f / sqrtf((x * x + y * y) + z * z);
+    x = s * x;
+    y = s * y;
+    z = s * z;
+}
+
+int prk_fill_edge_count(const float *V, uint32_t vertex_count, const float P[3], const prk_transform *T,
+                        uint32_t *count_out) {
+    if (!count_out || !T || (!V && vertex_count >= 3)) return PRK_ERR_ARG;
+    const float p0 = P ? P[0] : 0.0f, p1 = P ? P[1] : 0.0f, p2 = P ? P[2] : 0.0f;
+    uint32_t n = 0;
+    for (uint32_t t = 0; t < vertex_count / 3; ++t) {
+        float pr[3][3];
+        for (int k = 0; k < 3; ++k) {
+            const float *v = V + 9 * (size_t)t + 3 * k;
+            const float c[3] = {v[0] + p0, v[1] + p1, v[2] + p2};  // 3898-3903
+            host_project(c, T, pr[k]);
+        }
+        float ax = pr[1][0] - pr[0][0], ay = pr[1][1] - pr[0][1], az = pr[1][2] - pr[0][2];
+        float bx = pr[2][0] - pr[0][0], by = pr[2][1] - pr[0][1], bz = pr[2][2] - pr[0][2];
+        host_normalize(ax, ay, az);
+        host_normalize(bx, by, bz);
+        const float cx = ay * bz - az * by, cy = az * bx - ax * bz, cz = ax * by - ay * bx;
+        if (!((0.0f * cx + 0.0f * cy) + (-1.0f) * cz > 0.0f)) continue;  // 3943
+        for (int e = 0; e < 3; ++e) {
+            const float y0 = pr[e][1], y1 = pr[(e + 1) % 3][1];
+            const float mn = y0 > y1 ? y1 : y0, mx = y0 > y1 ? y0 : y1;  // 3957-3966
+            if (mx > 0 && mn - mx != 0) ++n;                                // 3968, 4066
+        }
+    }
+    *count_out = n;
+    return PRK_OK;
+}
+
 // ConstructSphere (projekt.cpp:4123-4289): the reference's only test mesh.
 // 24 inclination x 48 azimuth steps, r = 0.5, 6624 vertices.
 int prk_construct_sphere(float *V, float *Col, float *N, float *UV, uint32_t *count_out) {

@@ -81,6 +81,8 @@ _SIGS = {
     "prk_set_tile": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     "prk_construct_sphere": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.POINTER(C.c_uint32)]),
+    "prk_fill_edge_count": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_float), C.POINTER(abi.PrkTransform),
+                                      C.POINTER(C.c_uint32)]),
     "prk_get_target": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int32), C.POINTER(C.c_void_p),
                                  C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                  C.POINTER(C.c_int32)]),
@@ -152,6 +154,17 @@ def construct_sphere():
     _check("prk_construct_sphere", lib().prk_construct_sphere(_ptr(V), _ptr(Cc), _ptr(N), _ptr(UV),
                                                                C.byref(n)))
     return V[: n.value], Cc[: n.value], N[: n.value], UV[: n.value]
+
+
+def fill_edge_count(vertices, P, transform):
+    """prk_fill_edge_count: FillEdgeTable's return value (projekt.cpp:4119)
+    for one object (host-side, no device needed)."""
+    v = np.ascontiguousarray(vertices, np.float32)
+    Pc = (C.c_float * 3)(*(P or (0.0, 0.0, 0.0)))
+    n = C.c_uint32(0)
+    _check("prk_fill_edge_count", lib().prk_fill_edge_count(_ptr(v), v.shape[0], Pc, C.byref(transform),
+                                                             C.byref(n)))
+    return n.value
 
 
 def selftest_div(n=1 << 22, seed=1, device=0):

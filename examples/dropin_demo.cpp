@@ -10,6 +10,11 @@
 //   st       the same through DrawModelOptimized(Buffer, ...)     (2350)
 //   scalar   the same through DrawModel, untextured Gouraud       (162)
 //   object   the whole sphere as ONE object (one active edge table)
+//   scalar_object / scalar_object_phong   the whole sphere as ONE object
+//            through DrawModel (untextured Gouraud / Phong)
+//   camera   per-triangle objects; halfway through, the caller moves the
+//            camera (ScreenCenter) and changes the light between FillEdgeTable
+//            calls: each object draws as its FillEdgeTable call saw them
 //   mutate   two frames; between them the vertices, normals and texture are
 //            rewritten in place (same pointers): frame 2 is written
 //   edges F  DrawModelOptimized on a ready edge_info list read from file F
@@ -114,8 +119,13 @@ int main(int argc, char **argv) {
         return 2;
     };
     // One frame of per-triangle objects through the chosen entry point.
+    unsigned long long edges_total = 0;  // sum of FillEdgeTable's return values
     auto per_triangle = [&](const std::string &m) {
         for (u32 t = 0; t < VertexCount / 3; ++t) {
+            if (m == "camera" && t == VertexCount / 6) {  // the caller changes camera and light mid-frame
+                Commands.Transform.ScreenCenter.x = W / 2.0f + 24.0f;
+                Commands.LightData.Lights[0].Intensity = {{0.3f, 0.9f, 0.5f, 1.0f}};
+            }
             render_entry_3d_object Object = {};
             Object.P = {{0.0f, 0.0f, 2.0f}};
             Object.VertexCount = 3;
@@ -127,6 +137,7 @@ int main(int argc, char **argv) {
             Object.EdgeMemory = EdgeMemory.data();
             Object.Bitmap = &Texture;
             const u32 EdgeCount = FillEdgeTable(&Object, &Commands, m != "scalar");
+            edges_total += EdgeCount;
             if (m == "scalar") DrawModel(&Buffer, EdgeMemory.data(), EdgeCount, &Commands, 0, 0);
             else if (m == "lines") DrawModelOptimizedLines(nullptr, &Buffer, EdgeMemory.data(), EdgeCount, &Commands, &Texture, 1);
             else if (m == "st") DrawModelOptimized(&Buffer, EdgeMemory.data(), EdgeCount, &Commands, &Texture, 1);
@@ -146,8 +157,14 @@ int main(int argc, char **argv) {
     Sphere.EdgeMemory = EdgeMemory.data();
     Sphere.Bitmap = &Texture;
 
-    if (mode == "queue" || mode == "lines" || mode == "st" || mode == "scalar") {
+    if (mode == "queue" || mode == "lines" || mode == "st" || mode == "scalar" || mode == "camera") {
         if (!per_triangle(mode)) return fail("draw");
+    } else if (mode == "scalar_object" || mode == "scalar_object_phong") {
+        const b32 Phong = mode == "scalar_object_phong";
+        const u32 EdgeCount = FillEdgeTable(&Sphere, &Commands, Phong);
+        edges_total += EdgeCount;
+        DrawModel(&Buffer, EdgeMemory.data(), EdgeCount, &Commands, 0, Phong);
+        if (PRK_LastStatus() != PRK_OK) return fail("draw");
     } else if (mode == "object") {
         const u32 EdgeCount = FillEdgeTable(&Sphere, &Commands, 1);
         DrawModelOptimized(nullptr, &Buffer, EdgeMemory.data(), EdgeCount, &Commands, &Texture, 1);
@@ -257,6 +274,6 @@ int main(int argc, char **argv) {
     std::fclose(f);
     std::fclose(g);
     PRK_Shutdown();
-    std::printf("dropin_demo: %u triangles, mode %s\n", VertexCount / 3, mode.c_str());
+    std::printf("dropin_demo: %u triangles, mode %s, edges=%llu\n", VertexCount / 3, mode.c_str(), edges_total);
     return 0;
 }

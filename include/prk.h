@@ -333,6 +333,15 @@ int prk_gather_frame_local(prk_context *const *ctxs, int32_t n, int32_t with_z, 
  * within 2x).  Results never depend on the tile. */
 int prk_set_tile(prk_context *ctx, int32_t tile_w, int32_t tile_h);
 
+/* Host utility: FillEdgeTable's return value (projekt.cpp:3882-4121, 4119)
+ * for one object of vertex_count vertices (positions v3, three per
+ * triangle) at offset P (may be NULL: 0) under transform T: the number of
+ * edges of its front-facing triangles (3926-3943) with MaxY > 0 (3968) and
+ * MinY != MaxY (4066), 0 for an object that draws nothing.  The drop-in's
+ * FillEdgeTable returns it at the call; the setup runs on the GPU. */
+int prk_fill_edge_count(const float *vertices, uint32_t vertex_count, const float P[3],
+                        const prk_transform *transform, uint32_t *count_out);
+
 /* Host utility: the reference's test mesh, ConstructSphere
  * (projekt.cpp:4123-4289).  Arrays must hold 6624 vertices; returns the
  * vertex count through *count_out. */

@@ -17,18 +17,21 @@
 // and links libprk_hip.so.  What each entry point does here:
 //  * FillEdgeTable copies the object's VertexData / ColorData / NormalData /
 //    UVData as they are at the call (the reference reads them there,
-//    3898-3925) into the frame's pinned staging arena, and leaves a token in
-//    Object->EdgeMemory that DrawModel* read back; the setup itself
-//    (projection, cull, edges, MergeSort) runs on the GPU at
-//    PRK_CompleteAllWork.  It returns 3*T, the reference's upper bound on the
-//    edge count (non-zero for any object with a triangle).
+//    3898-3925) into the frame's pinned staging arena, snapshots
+//    Commands->Transform and LightData as they are at the call (3885,
+//    3907-3909, 4022-4061), and leaves a token in Object->EdgeMemory that
+//    DrawModel* read back; the setup itself (projection, cull, edges,
+//    lighting, MergeSort) runs on the GPU at PRK_CompleteAllWork.  It
+//    returns the reference's value, the visible edge count (4119; 0 for an
+//    object that draws nothing, e.g. a back-facing triangle), computed on the
+//    host by prk_fill_edge_count.  EdgeMemory holds the token, not edge_info
+//    records.
 //  * DrawModelOptimized(RenderQueue, ...) and DrawModelOptimizedLines draw
 //    the object with FillLineOptimized semantics (FillLinesOptimized has the
 //    same block math); DrawModelOptimized(Buffer, ...) with the
 //    single-thread overload's quirks (PRK_SEM_AVX_ST); DrawModel with the
 //    scalar semantics.  An object of several triangles is ONE active edge
-//    table, as in the reference (prk_draw_objects); DrawModel's scalar
-//    whole-object AET is not emulated and is drawn per triangle.
+//    table, as in the reference (prk_draw_objects), for every semantics.
 //  * DrawModel* given edges that are NOT a FillEdgeTable token (a caller's
 //    own edge_info list, e.g. built by the reference's FillEdgeTable) draw
 //    that list as is (prk_draw_edges).  The work-queue callbacks draw the
@@ -42,8 +45,10 @@
 //    them) and the result comes down as DMA.  PRK_ClearNextFrame(color, z)
 //    replaces that upload by a clear fused into the frame's kernels.
 //  * Textures (loaded_bitmap) are read at their first use in each frame.
-//  * One camera and light set per frame: the Commands of the frame's draws as
-//    they are at PRK_CompleteAllWork.
+//  * Cameras and lights: an object draws with Commands->Transform / LightData
+//    as they were at its FillEdgeTable call (edge lists and work records: at
+//    their DrawModel* / callback call); a frame whose draws saw several
+//    cameras runs as consecutive flushes, one per change, in order.
 //  * Inputs the reference crashes on are rejected or pinned, see
 //    prk.h; PRK_LastStatus() reports the last library status.
 //
@@ -187,8 +192,15 @@ static_assert(sizeof(object_token) <= sizeof(edge_info), "token must fit one edg
 static const uint32_t kMagic = 0x4B525032u;  // "PRK2"
 
 struct frame_object {
-    uint32_t FirstTri, Tris;
+    uint32_t FirstTri, Tris;  // Tris == 0: FillEdgeTable found no edge (nothing to draw)
     float P[3];
+    uint32_t Camera;          // Commands->Transform / LightData as they were at FillEdgeTable
+};
+
+// Commands->Transform and LightData as one draw saw them.
+struct camera {
+    prk_transform T;
+    prk_light_data L;
 };
 
 enum { DRAW_OBJECT = 0, DRAW_EDGES = 1, DRAW_SPANS = 2 };
@@ -196,6 +208,7 @@ struct pending_draw {
     int Kind;
     uint32_t First, Count;  // object index / range of Edges / range of Spans
     int32_t Semantics, Phong, Texture;
+    uint32_t Camera;        // index into the frame's cameras
 };
 
 struct state {
@@ -208,6 +221,7 @@ struct state {
     int32_t Geom = -1;
     std::vector<frame_object> Objects;
     std::vector<pending_draw> Draws;
+    std::vector<camera> Cameras;               // the frame's distinct camera / light snapshots, in order
     std::vector<prk_edge> Edges;
     std::vector<prk_span> Spans;
     std::map<const void *, int32_t> Textures;  // Bitmap->Memory -> handle
@@ -325,22 +339,35 @@ inline int32_t texture_for(loaded_bitmap *Bitmap) {
     return h;
 }
 
-inline void set_camera(game_render_commands *Commands) {
-    prk_transform t;
-    t.DistanceAboveTarget = Commands->Transform.DistanceAboveTarget;
-    t.FocalLength = Commands->Transform.FocalLength;
-    t.MetersToPixels = Commands->Transform.MetersToPixels;
-    t.ScreenCenter[0] = Commands->Transform.ScreenCenter.x;
-    t.ScreenCenter[1] = Commands->Transform.ScreenCenter.y;
-    prk_light_data l;
-    memset(&l, 0, sizeof l);
-    l.LightCount = Commands->LightData.LightCount;
-    for (int c = 0; c < 4; ++c) l.AmbientIntensity[c] = Commands->LightData.AmbientIntensity.E[c];
-    for (u32 i = 0; i < l.LightCount && i < PRK_MAX_LIGHTS; ++i) {
-        for (int c = 0; c < 3; ++c) l.Lights[i].P[c] = Commands->LightData.Lights[i].P.E[c];
-        for (int c = 0; c < 4; ++c) l.Lights[i].Intensity[c] = Commands->LightData.Lights[i].Intensity.E[c];
+// Commands->Transform and LightData as they are now (FillEdgeTable reads them
+// at its call, projekt.cpp:3885, 3907-3909, 4022-4061; the span kernels read
+// them when the draw runs).
+inline camera camera_of(const game_render_commands *Commands) {
+    camera k;
+    memset(&k, 0, sizeof k);
+    k.T.DistanceAboveTarget = Commands->Transform.DistanceAboveTarget;
+    k.T.FocalLength = Commands->Transform.FocalLength;
+    k.T.MetersToPixels = Commands->Transform.MetersToPixels;
+    k.T.ScreenCenter[0] = Commands->Transform.ScreenCenter.x;
+    k.T.ScreenCenter[1] = Commands->Transform.ScreenCenter.y;
+    k.L.LightCount = Commands->LightData.LightCount;
+    for (int c = 0; c < 4; ++c) k.L.AmbientIntensity[c] = Commands->LightData.AmbientIntensity.E[c];
+    for (u32 i = 0; i < k.L.LightCount && i < PRK_MAX_LIGHTS; ++i) {
+        for (int c = 0; c < 3; ++c) k.L.Lights[i].P[c] = Commands->LightData.Lights[i].P.E[c];
+        for (int c = 0; c < 4; ++c) k.L.Lights[i].Intensity[c] = Commands->LightData.Lights[i].Intensity.E[c];
     }
-    ok(each([&](prk_context *c) { return prk_set_camera(c, &t, &l); }));
+    return k;
+}
+
+// The frame's camera index of a snapshot: the last one when unchanged (the
+// usual frame has one), else a new entry.
+inline uint32_t camera_id(state &st, const camera &k) {
+    if (st.Cameras.empty() || memcmp(&st.Cameras.back(), &k, sizeof k) != 0) st.Cameras.push_back(k);
+    return (uint32_t)st.Cameras.size() - 1;
+}
+
+inline int set_camera(const camera &k) {
+    return each([&](prk_context *c) { return prk_set_camera(c, &k.T, &k.L); });
 }
 
 inline void register_host(state &st, void *p, size_t bytes) {
@@ -433,7 +460,10 @@ inline void draw(loaded_bitmap *Buffer, edge_info *Edges, u32 EdgeCount, game_re
         d.Kind = DRAW_OBJECT;
         d.First = tok.Object;
         d.Count = 1;
+        d.Camera = st.Objects[tok.Object].Camera;  // as FillEdgeTable saw it
+        if (st.Objects[tok.Object].Tris == 0) return;  // FillEdgeTable wrote no edge: nothing to draw
     } else {  // a caller's own edge_info list, drawn as given
+        d.Camera = camera_id(st, camera_of(Commands));
         d.Kind = DRAW_EDGES;
         d.First = (uint32_t)st.Edges.size();
         d.Count = EdgeCount;
@@ -456,15 +486,18 @@ inline void draw_spans(loaded_bitmap *Buffer, game_render_commands *Commands, lo
     d.Semantics = PRK_SEM_AVX;
     d.Phong = PhongShading ? 1 : 0;
     d.Texture = Bitmap ? texture_for(Bitmap) : -1;
+    d.Camera = camera_id(st, camera_of(Commands));
     st.Spans.insert(st.Spans.end(), spans, spans + n);
     st.Draws.push_back(d);
 }
 
-// Records the frame's draws with the library, in order, with the frame's
-// camera and lights (the Commands of its draws).
+// Records the frame's draws with the library, in order.  Draws that saw
+// different cameras or lights (Commands changed between FillEdgeTable calls)
+// run as consecutive flushes, each with its own camera; a later flush z-tests
+// against what the earlier ones left, which is the reference's sequential
+// order.  The last flush is left to the caller (PRK_CompleteAllWork).
 inline int issue(state &st) {
     int rc = PRK_OK;
-    set_camera(st.Commands);
     if (st.LastStatus != PRK_OK) return st.LastStatus;
     if (st.ArenaUsed) {
         // vertex colours reach the output only through DrawModel (scalar); the
@@ -486,21 +519,38 @@ inline int issue(state &st) {
         if (create) st.Geom = g;
     }
     // every band records every draw (each bins all triangles against its rows)
-    return each([&](prk_context *c) {
-        int r = PRK_OK;
-        for (const pending_draw &d : st.Draws) {
-            if (d.Kind == DRAW_OBJECT) {
-                const frame_object &o = st.Objects[d.First];
-                r = prk_draw_objects(c, st.Geom, o.FirstTri, o.Tris, o.Tris, o.P, d.Semantics, d.Phong, d.Texture);
-            } else if (d.Kind == DRAW_EDGES) {
-                r = prk_draw_edges(c, st.Edges.data() + d.First, d.Count, d.Semantics, d.Phong, d.Texture);
-            } else {
-                r = prk_draw_spans(c, st.Spans.data() + d.First, d.Count, d.Semantics, d.Phong, d.Texture);
-            }
-            if (r != PRK_OK) return r;
+    if (st.Cameras.empty()) st.Cameras.push_back(camera_of(st.Commands));
+    size_t i = 0;
+    while (i < st.Draws.size() || i == 0) {
+        const uint32_t cam = st.Draws.empty() ? 0u : st.Draws[i].Camera;
+        size_t j = i;
+        while (j < st.Draws.size() && st.Draws[j].Camera == cam) ++j;
+        if (i > 0) {  // camera / lights changed: the draws so far run first
+            rc = each([](prk_context *k) { return prk_flush(k, nullptr); });
+            if (rc != PRK_OK) return rc;
         }
-        return r;
-    });
+        rc = set_camera(st.Cameras[cam]);
+        if (rc != PRK_OK) return rc;
+        rc = each([&](prk_context *c) {
+            int r = PRK_OK;
+            for (size_t k = i; k < j && r == PRK_OK; ++k) {
+                const pending_draw &d = st.Draws[k];
+                if (d.Kind == DRAW_OBJECT) {
+                    const frame_object &o = st.Objects[d.First];
+                    r = prk_draw_objects(c, st.Geom, o.FirstTri, o.Tris, o.Tris, o.P, d.Semantics, d.Phong,
+                                         d.Texture);
+                } else if (d.Kind == DRAW_EDGES) {
+                    r = prk_draw_edges(c, st.Edges.data() + d.First, d.Count, d.Semantics, d.Phong, d.Texture);
+                } else {
+                    r = prk_draw_spans(c, st.Spans.data() + d.First, d.Count, d.Semantics, d.Phong, d.Texture);
+                }
+            }
+            return r;
+        });
+        if (rc != PRK_OK || j == i) return rc;
+        i = j;
+    }
+    return rc;
 }
 
 inline void end_frame(state &st) {
@@ -510,6 +560,7 @@ inline void end_frame(state &st) {
     st.ArenaUsed = 0;
     st.Objects.clear();
     st.Draws.clear();
+    st.Cameras.clear();
     st.Edges.clear();
     st.Spans.clear();
     st.TexFresh.clear();
@@ -582,35 +633,46 @@ inline int PRK_CompleteAllWork(loaded_bitmap *Buffer, game_render_commands *Comm
 // ---- the reference's entry points ------------------------------------------
 // projekt.cpp:3882-4121
 inline u32 FillEdgeTable(render_entry_3d_object *Object, game_render_commands *Commands, b32 PhongShading = 0) {
-    (void)Commands;
     (void)PhongShading;  // the semantics travel with the DrawModel* call
     prk_dropin::state &st = prk_dropin::S();
-    if (!st.Ctx || !Object || !Object->EdgeMemory || !Object->VertexData || Object->VertexCount < 3) return 0;
+    if (!st.Ctx || !Object || !Commands || !Object->EdgeMemory || !Object->VertexData || Object->VertexCount < 3)
+        return 0;
     const u32 T = Object->VertexCount / 3, nv = 3 * T;
-    if (!prk_dropin::arena_reserve(st, nv)) return 0;
-    const uint32_t v0 = st.ArenaUsed;
-    memcpy(st.AV + 3 * (size_t)v0, Object->VertexData, (size_t)nv * 12);
-    if (Object->ColorData) memcpy(st.AC + 4 * (size_t)v0, Object->ColorData, (size_t)nv * 16);
-    else memset(st.AC + 4 * (size_t)v0, 0, (size_t)nv * 16);
-    if (Object->NormalData) memcpy(st.AN + 3 * (size_t)v0, Object->NormalData, (size_t)nv * 12);
-    else memset(st.AN + 3 * (size_t)v0, 0, (size_t)nv * 12);
-    if (Object->UVData) memcpy(st.AUV + 2 * (size_t)v0, Object->UVData, (size_t)nv * 8);
-    else memset(st.AUV + 2 * (size_t)v0, 0, (size_t)nv * 8);
-    st.ArenaUsed += nv;
     prk_dropin::frame_object o;
-    o.FirstTri = v0 / 3;
-    o.Tris = T;
     o.P[0] = Object->P.x;
     o.P[1] = Object->P.y;
     o.P[2] = Object->P.z;
+    // the camera and lights of this call (3885, 3907-3909, 4022-4061)
+    const prk_dropin::camera cam = prk_dropin::camera_of(Commands);
+    o.Camera = prk_dropin::camera_id(st, cam);
+    // the reference's return value: the visible edge count (4119), 0 when no
+    // edge is visible (e.g. a back-facing triangle)
+    u32 edges = 0;
+    if (!prk_dropin::ok(prk_fill_edge_count((const float *)Object->VertexData, nv, o.P, &cam.T, &edges))) return 0;
+    o.FirstTri = 0;
+    o.Tris = 0;
+    if (edges) {  // an object with no visible edge draws nothing: nothing to upload
+        if (!prk_dropin::arena_reserve(st, nv)) return 0;
+        const uint32_t v0 = st.ArenaUsed;
+        memcpy(st.AV + 3 * (size_t)v0, Object->VertexData, (size_t)nv * 12);
+        if (Object->ColorData) memcpy(st.AC + 4 * (size_t)v0, Object->ColorData, (size_t)nv * 16);
+        else memset(st.AC + 4 * (size_t)v0, 0, (size_t)nv * 16);
+        if (Object->NormalData) memcpy(st.AN + 3 * (size_t)v0, Object->NormalData, (size_t)nv * 12);
+        else memset(st.AN + 3 * (size_t)v0, 0, (size_t)nv * 12);
+        if (Object->UVData) memcpy(st.AUV + 2 * (size_t)v0, Object->UVData, (size_t)nv * 8);
+        else memset(st.AUV + 2 * (size_t)v0, 0, (size_t)nv * 8);
+        st.ArenaUsed += nv;
+        o.FirstTri = v0 / 3;
+        o.Tris = T;
+    }
     prk_dropin::object_token tok;
     tok.Magic = prk_dropin::kMagic;
     tok.Frame = st.Frame;
     tok.Object = (uint32_t)st.Objects.size();
-    tok.TriCount = T;
+    tok.TriCount = o.Tris;
     st.Objects.push_back(o);
     memcpy(Object->EdgeMemory, &tok, sizeof tok);
-    return 3 * T;
+    return edges;
 }
 
 // projekt.cpp:3615-3871 (+ FillLineOptimized 1492-2320)

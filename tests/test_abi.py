@@ -92,3 +92,28 @@ def test_dropin_header_builds_and_links(tmp_path):
     if prk.device_count() == 0:
         run = subprocess.run([str(exe), str(tmp_path / "c"), str(tmp_path / "z")], capture_output=True, text=True)
         assert run.returncode == 2 and "no HIP device" in run.stderr
+
+
+@pytest.mark.parametrize("per", [1, 5, 60])
+def test_fill_edge_count_matches_oracle(per):
+    """prk_fill_edge_count (what the drop-in's FillEdgeTable returns,
+    projekt.cpp:4119) equals the oracle's FillEdgeTable edge count for every
+    object: back-facing objects (0), the near plane, clipping on every side,
+    horizontal edges."""
+    import oracle as O
+    from prk import scenes
+    s = scenes.random_soup(1200, 256, 192, radius=60, seed=31, centroid_margin=80)
+    rng = np.random.default_rng(3)
+    v = s.vertices.reshape(-1, 3, 3)
+    flip = rng.random(v.shape[0]) < 0.3  # back-facing: swap two vertices
+    v[flip, 1], v[flip, 2] = v[flip, 2].copy(), v[flip, 1].copy()
+    v[rng.random(v.shape[0]) < 0.05, 0, 2] = 3.9  # a vertex at the near plane
+    flat = rng.random(v.shape[0]) < 0.05  # a horizontal edge
+    v[flat, 1, 1] = v[flat, 0, 1]
+    s.vertices = v.reshape(-1, 3)
+    T = s.prk_transform()
+    for t0 in range(0, s.tri_count, per):
+        n = min(per, s.tri_count - t0)
+        want = len(O.fill_edge_table(s, t0, n))
+        got = prk.fill_edge_count(s.vertices[3 * t0:3 * (t0 + n)], s.P, T)
+        assert got == want, (t0, n, got, want)

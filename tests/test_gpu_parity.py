@@ -655,11 +655,13 @@ def _dropin_scene(textured=True, salt=0):
                         scenes.AMBIENT_ONE, scenes.Texture(tex, 64, 64) if textured else None, P=(0.0, 0.0, 2.0))
 
 
-DROPIN_MODES = ["queue", "lines", "st", "scalar", "object", "mutate", "edges", "work"]
+DROPIN_MODES = ["queue", "lines", "st", "scalar", "object", "mutate", "edges", "work", "scalar_object",
+                "scalar_object_phong", "camera"]
 
 
 @pytest.mark.parametrize("mode,bands", [(m, 1) for m in DROPIN_MODES] +
-                         [("queue", 3), ("object", 2), ("mutate", 3), ("scalar", 3), ("work", 2)])
+                         [("queue", 3), ("object", 2), ("mutate", 3), ("scalar", 3), ("work", 2),
+                          ("scalar_object", 3), ("camera", 2)])
 def test_dropin_demo_matches_oracle(gpu, tmp_path, mode, bands):
     """examples/dropin_demo.cpp drives the reference's own entry points
     through include/projekt.h (FillEdgeTable, DrawModelOptimized(RenderQueue),
@@ -680,7 +682,7 @@ def test_dropin_demo_matches_oracle(gpu, tmp_path, mode, bands):
                         "-Wl,-rpath," + os.path.join(root, "cpu-renderer_amd"), "-o", str(exe)],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
-    s = _dropin_scene(textured=mode != "scalar")
+    s = _dropin_scene(textured=mode not in ("scalar", "scalar_object", "scalar_object_phong"))
     T = s.tri_count
     extra = []
     if mode == "edges":
@@ -720,6 +722,15 @@ def test_dropin_demo_matches_oracle(gpu, tmp_path, mode, bands):
         oc, oz, _, _ = O.render(s, semantics=abi.PRK_SEM_SCALAR, phong=False)
     elif mode == "object":
         oc, oz, _, _ = O.render(s, tris_per_object=T)
+    elif mode in ("scalar_object", "scalar_object_phong"):
+        oc, oz, _, _ = O.render(s, semantics=abi.PRK_SEM_SCALAR, phong=mode.endswith("phong"), tris_per_object=T)
+    elif mode == "camera":  # the second half drawn with the moved camera and the new light, over the first
+        half = T // 2
+        a, b = s.subset(0, half), s.subset(half, T)
+        b.transform = (4.0, 1.0, 128.0, 128.0 + 24.0, 128.0)
+        b.lights = [((1.0, 1.0, 3.0), (0.3, 0.9, 0.5, 1.0))]
+        oc, oz, _, _ = O.render(a)
+        oc, oz, _, _ = O.render(b, color=oc, z=oz)
     elif mode == "mutate":
         m = _dropin_scene(salt=1)
         m.vertices[:, 0] = m.vertices[:, 0] * np.float32(0.75) + np.float32(0.125)
@@ -732,9 +743,20 @@ def test_dropin_demo_matches_oracle(gpu, tmp_path, mode, bands):
         oc, oz, _, _ = O.render_spans(s, w[: n // 2])
         oc, oz, _, _ = O.render_spans(s, w[n // 2:], color=oc, z=oz)
         oc, oz, _, _ = O.render(s, semantics=abi.PRK_SEM_AVX_ST, tris_per_object=T, color=oc, z=oz)
+    cd = channel_diff(gc, oc)
     assert (gz.view(np.uint32) == oz.view(np.uint32)).all(), mode
-    assert (gc == oc).all(), mode
+    if mode == "scalar_object_phong":  # the scalar Phong contract: +-1 LSB (double pow)
+        assert (cd <= COLOR_TOL).all(), mode
+    else:
+        assert (gc == oc).all(), mode
     assert (gz > -3e38).sum() > 2000
+    # FillEdgeTable's return values (projekt.cpp:4119) summed over the frame's
+    # calls equal the oracle's edge counts: per triangle, or the whole sphere
+    edges = int(run.stdout.split("edges=")[1].split()[0])
+    if mode in ("queue", "lines", "st", "scalar", "camera"):
+        assert edges == sum(len(O.fill_edge_table(s, t, 1)) for t in range(T)), mode
+    elif mode.startswith("scalar_object"):
+        assert edges == len(O.fill_edge_table(s, 0, T, phong=mode.endswith("phong"))), mode
 
 
 @pytest.mark.parametrize("semantics,phong,textured", [(abi.PRK_SEM_SCALAR, False, False),
