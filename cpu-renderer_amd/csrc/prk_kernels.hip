@@ -117,6 +117,9 @@ __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
 #ifndef PRK_PIXEL_ITEMS
 #define PRK_PIXEL_ITEMS 1  // shading sweep (AVX): one work item per won pixel, not per lane chain
 #endif
+#ifndef PRK_TRIWALK
+#define PRK_TRIWALK 3  // regular triangles walk with TriWalker (one insertion/expiry event): 1 k_vis, 2 k_walk
+#endif
 #ifndef PRK_VIS_WAVES
 // waves per k_vis tile workgroup; each takes whole 64-entry chunks of the bin.
 // Four waves share one 16 KiB key array: 4 workgroups = 16 waves per CU.
@@ -762,6 +765,10 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
     const bool col0 = tc.x0 == 0 && M != MODE_AVX;
     const int32_t ystart = col0 ? tc.y0 - 1 : tc.y0;  // scalar: (row-1) may store into (row, 0)
     unsigned long long pt[4] = {0, 0, 0, 0};  // PRK_PROF: setup, walk, scan/map, items
+    // PRK_PROF event counts (visibility sweep): chunks, row iterations, item
+    // windows, items, active lanes summed over row iterations, spans with items,
+    // regular (TriWalker) chunks
+    unsigned long long pc[7] = {0, 0, 0, 0, 0, 0, 0};
     // Single-draw frames prefetch: the next chunk's bin entry is loaded at the
     // top of a chunk and its vertex attributes before the row walk, so both
     // loads are in flight while this chunk's setup and rows run.
@@ -783,6 +790,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
         unsigned long long t0 = PRK_T();
         const uint32_t i = base + lane;
         bool active = i < n;
+        if (PRK_PROF) pc[0] += 1;
         uint32_t e = 0, j = 0;  // bin entry, its pair index (the tie-break order)
         uint32_t st = 0;        // DRAW_ST: single-thread DrawModelOptimized(Buffer,...) semantics
         int32_t texi = 0;
@@ -874,6 +882,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
         // PRK_LANE_ROWS: every lane walks its own next row each iteration (the
         // span's row travels in its slot); else all lanes step row r together.
         if (PRK_LANE_ROWS && active) active = wk.Row < tc.y1;
+        auto rows = [&](auto &wk) {
         for (int32_t r = ystart; PRK_LANE_ROWS || r < tc.y1; ++r) {
             // Rows per lane this iteration: when few lanes still hold rows, each
             // emits up to 8 of its next rows into the wave's 64 span slots
@@ -881,6 +890,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
             // several rows share one window and the rows' per-pixel recurrences
             // run side by side instead of one row after another.
             int k = 1, rank = 0;
+            if (PRK_PROF) { pc[1] += 1; pc[4] += (unsigned long long)__popcll(__ballot(active)); }
             if (PRK_LANE_ROWS && PRK_MULTI_ROWS) {
                 const unsigned long long am = __ballot(active);
                 const int A = __popcll(am);
@@ -921,6 +931,11 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
             const int total = __builtin_amdgcn_readlane(incl, 63);
             const int excl = incl - items;
             ws.i[SI_PRE][lane] = excl;
+            if (PRK_PROF) {
+                pc[2] += (unsigned long long)((total + 63) / 64);
+                pc[3] += (unsigned long long)total;
+                pc[5] += (unsigned long long)__popcll(__ballot(items > 0));
+            }
             // Item -> span: the span lanes starting an item inside the window
             // mark their start position; a prefix max over the window (plus
             // the span carried over from the previous window) names the span
@@ -954,9 +969,27 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
             if (PRK_PROF) { const unsigned long long t1 = PRK_T(); pt[3] += t1 - t0; t0 = t1; }
             if (!__any(active)) break;
         }
+        };
+        // A wave whose entries are all regular triangles walks them with the
+        // one-event TriWalker (prk_device.h); any irregular list keeps the
+        // general RowWalker for the chunk.
+        if constexpr ((PRK_TRIWALK & 1) != 0) {
+            if (__all(!active || TriWalker<M, SHADE>::regular(wk))) {
+                if (PRK_PROF) pc[6] += 1;
+                TriWalker<M, SHADE> tw;
+                tw.from(wk);
+                rows(tw);
+            } else {
+                rows(wk);
+            }
+        } else {
+            rows(wk);
+        }
     }
     if (PRK_PROF && lane == 0)
         for (int k = 0; k < 4; ++k) atomicAdd(fp.prof + (SHADE ? 4 : 0) + k, pt[k]);
+    if (PRK_PROF && !SHADE && lane == 0)
+        for (int k = 0; k < 7; ++k) atomicAdd(fp.prof + 8 + k, pc[k]);
 }
 
 // Workgroup-wide exclusive scan of one value per thread.
@@ -1333,6 +1366,7 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
     const int32_t t0 = (int32_t)((uint32_t)tr.tx0 | ((uint32_t)tr.ty0 << 16));
     const int32_t t1 = (int32_t)((uint32_t)tr.tx1 | ((uint32_t)tr.ty1 << 16));
     uint32_t head = 0, cnt = 0;  // wave-uniform queue state
+    auto walk = [&](auto &wk) {
     while (__any(active)) {
         bool push = false, paired = false;
         int32_t Row = 0;
@@ -1369,6 +1403,15 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
             head += 64;
             cnt -= 64;
         }
+    }
+    };
+    // all lanes regular: the one-event TriWalker (as in k_vis)
+    if ((PRK_TRIWALK & 2) && __all(!active || TriWalker<M, true>::regular(wk))) {
+        TriWalker<M, true> tw;
+        tw.from(wk);
+        walk(tw);
+    } else {
+        walk(wk);
     }
     wave_lds_sync();
     if ((uint32_t)lane < cnt) walk_flush(fp, q, (int)((head + lane) & (kWalkQ - 1)), won, recs);

@@ -48,6 +48,10 @@ def main():
         for nm, off in (("vis", 0), ("shade", 4)):
             print("  %-5s cycles/frame: setup %.3g  walk %.3g  scan %.3g  items %.3g" % (
                 (nm,) + tuple(c[off + k] / n for k in range(4))))
+        e = [x / n for x in c[8:15]]
+        print("  vis events/frame: chunks %.0f  row iterations %.0f  windows %.0f  items %.0f  "
+              "active lanes/row it %.1f  spans/row it %.1f  items/window %.1f  regular chunks %.0f" % (
+                  e[0], e[1], e[2], e[3], e[4] / max(1, e[1]), e[5] / max(1, e[1]), e[3] / max(1, e[2]), e[6]))
     r.close()
 
 
