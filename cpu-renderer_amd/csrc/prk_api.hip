@@ -40,9 +40,16 @@ hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, co
                              hipStream_t, hipStream_t);
 hipError_t prk_walk_select_bytes(uint32_t, size_t *);
 hipError_t prk_selftest_div_launch(uint32_t n, uint64_t seed, unsigned long long *bad, hipStream_t s);
-hipError_t prk_obj_walk(const prk::FrameParams *, const void *, uint32_t, void *, uint32_t *, uint32_t *, int,
-                        uint32_t *, const uint32_t *, void *, void *, void *, uint32_t *, const void *, const void *,
-                        hipStream_t);
+hipError_t prk_objtri_count(const prk::FrameParams *, const void *, const uint32_t *, const uint32_t *, uint32_t,
+                            uint32_t, uint32_t *, hipStream_t);
+hipError_t prk_objtri_emit(const prk::FrameParams *, const void *, const uint32_t *, const uint32_t *, uint32_t,
+                           uint32_t, const uint32_t *, void *, void *, uint32_t *, hipStream_t);
+hipError_t prk_obj_sort(void *, uint32_t *, void *, uint32_t *, uint32_t, uint32_t, void *, size_t *, hipStream_t);
+hipError_t prk_obj_gather(const void *, const uint32_t *, const uint32_t *, const void *, const uint32_t *, uint32_t,
+                          void *, uint32_t, hipStream_t);
+hipError_t prk_obj_walk(const prk::FrameParams *, const void *, uint32_t, const uint32_t *, uint32_t, const uint32_t *,
+                        const uint32_t *, void *, int, uint32_t *, const uint32_t *, void *, void *, void *,
+                        uint32_t *, const void *, uint32_t *, hipStream_t);
 hipError_t prk_scan_u32(const uint32_t *, uint32_t *, uint32_t, void *, size_t *, hipStream_t);
 hipError_t prk_span_count(const prk::FrameParams *, const void *, uint32_t, uint32_t *, hipStream_t);
 hipError_t prk_span_bin(const prk::FrameParams *, const void *, uint32_t, const uint32_t *, uint32_t, uint32_t *,
@@ -54,8 +61,11 @@ hipError_t prk_launch_spans(const prk::FrameParams *, const uint32_t *, const ui
 
 // prk_spans.hip's object descriptor.
 struct ObjDesc {
-    uint32_t draw, g0, tris, edge_off, kind, src, nsrc, pad;
+    uint32_t draw, g0, tris, tri0, kind, src, nsrc, k1off;
 };
+constexpr uint32_t kObjWave = 0x80000000u;  // ObjDesc::k1off flag: walked by one wave
+constexpr uint32_t kObjWaveTris = 48;        // objects of this many triangles or more
+constexpr uint32_t kObjMaxEdges = 1u << 22;  // MergeSort key: recursion path of 23 bits
 
 // AVX frames shade through span records (k_walk + k_pix); must match
 // PRK_SPAN_RECORDS of prk_kernels.hip.
@@ -196,7 +206,13 @@ struct prk_context {
     struct SpanScratch {
         DevBuf d_draws, d_texs, d_objs, d_edges, d_ord, d_tmp, d_cnt, d_off, d_temp, d_recs, d_pos, d_span_tri,
             d_scnt, d_soff, d_keys_a, d_vals_a, d_keys_b, d_vals_b, d_offs, d_nwin, d_wtag, d_edges_in, d_spans_in,
-            d_srecs;
+            d_srecs, d_work, d_ekeys, d_ekeys2, d_evals, d_ecnt, d_escan, d_k0obj, d_k0tri0, d_big, d_k1src, d_err;
+        // host tables of the pass, kept until their asynchronous uploads ran
+        std::vector<ObjDesc> h_objs;
+        std::vector<uint32_t> h_k0obj, h_k0tri0, h_big, h_k1src;
+        std::vector<prk::DrawRec> h_draws;
+        std::vector<prk::TexRec> h_texs;
+        uint32_t *h_rb = nullptr;  // pinned readback words
     } spans;
 };
 
@@ -306,8 +322,10 @@ int prk_destroy(prk_context *c) {
         DevBuf *sb[] = {&S.d_draws, &S.d_texs, &S.d_objs, &S.d_edges, &S.d_ord, &S.d_tmp, &S.d_cnt, &S.d_off,
                         &S.d_temp, &S.d_recs, &S.d_pos, &S.d_span_tri, &S.d_scnt, &S.d_soff, &S.d_keys_a,
                         &S.d_vals_a, &S.d_keys_b, &S.d_vals_b, &S.d_offs, &S.d_nwin, &S.d_wtag, &S.d_edges_in,
-                        &S.d_spans_in, &S.d_srecs};
+                        &S.d_spans_in, &S.d_srecs, &S.d_work, &S.d_ekeys, &S.d_ekeys2, &S.d_evals, &S.d_ecnt,
+                        &S.d_escan, &S.d_k0obj, &S.d_k0tri0, &S.d_big, &S.d_k1src, &S.d_err};
         for (DevBuf *b : sb) b->release();
+        if (S.h_rb) (void)hipHostFree(S.h_rb);
     }
     if (c->s_mark) (void)hipEventDestroy(c->s_mark);
     if (c->h_total) (void)hipHostFree(c->h_total);
@@ -1150,10 +1168,11 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
     return PRK_OK;
 }
 
-// One pass of whole-object AETs (prk_spans.hip): walk every object's AET
-// into span records (count pass, scan, emit pass), bin the spans to tiles,
-// then visibility + shading.  Synchronous with respect to the host at the
-// two counts it reads back.
+// One pass of whole-object AETs (prk_spans.hip): FillEdgeTable per triangle,
+// MergeSort per object (one radix sort), walk every object's AET into span
+// records (count pass, scan, emit pass), bin the spans to tiles, then
+// visibility + shading.  Stream-ordered on s; the host waits at the three
+// sizes it reads back (edge count, span count, bin entry count).
 static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::DrawRec> &draws, uint32_t T,
                        uint32_t win_base) {
     prk::FrameParams fp;
@@ -1167,84 +1186,130 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     fp.clear_fused = fuse ? 1 : 0;
     if (T == 0) return PRK_OK;
     prk_context::SpanScratch &S = c->spans;
-    // Objects in submission order (ObjDesc kinds: prk_spans.hip).
-    std::vector<ObjDesc> objs;
-    uint64_t eslots = 0;
+    if (!S.h_rb) PRK_TRY(hipHostMalloc((void **)&S.h_rb, 4 * sizeof(uint32_t), hipHostMallocDefault));
+    // Objects in submission order (ObjDesc kinds: prk_spans.hip): kind 0
+    // objects' triangles numbered 0..ntri-1 in order (FillEdgeTable runs per
+    // triangle), caller edge lists' edges after the triangles' edges.
+    S.h_objs.clear();
+    S.h_k0obj.clear();
+    S.h_k0tri0.clear();
+    S.h_big.clear();
+    S.h_k1src.clear();
+    uint64_t ntri = 0, nk1 = 0;
     for (uint32_t di = 0; di < draws.size(); ++di) {
         const prk::DrawRec &d = draws[di];
         if (d.src_kind == 1) {
-            objs.push_back(ObjDesc{di, d.first_global, 0u, (uint32_t)eslots, 1u, d.src_off, d.src_n, 0u});
-            eslots += d.src_n;
+            S.h_objs.push_back(ObjDesc{di, d.first_global, 0u, 0u, 1u, d.src_off, d.src_n, (uint32_t)nk1});
+            for (uint32_t e = 0; e < d.src_n; ++e) S.h_k1src.push_back(d.src_off + e);
+            nk1 += d.src_n;
         } else if (d.src_kind == 2) {
             for (uint32_t k = 0; k < d.src_n; ++k)
-                objs.push_back(ObjDesc{di, d.first_global + k, 0u, 0u, 2u, d.src_off + k, 1u, 0u});
+                S.h_objs.push_back(ObjDesc{di, d.first_global + k, 0u, 0u, 2u, d.src_off + k, 1u, 0u});
         } else {
             const uint32_t per = std::max<uint32_t>(1u, d.obj_tris);
             for (uint32_t t = 0; t < d.tri_count; t += per) {
                 const uint32_t n = std::min(per, d.tri_count - t);
-                objs.push_back(ObjDesc{di, d.first_global + t, n, (uint32_t)eslots, 0u, 0u, 0u, 0u});
-                eslots += 3ull * n;
+                if (3ull * n >= kObjMaxEdges) return PRK_ERR_UNSUPPORTED;
+                const bool wave = n >= kObjWaveTris;
+                if (wave) S.h_big.push_back((uint32_t)S.h_objs.size());
+                S.h_k0obj.push_back((uint32_t)S.h_objs.size());
+                S.h_k0tri0.push_back((uint32_t)ntri);
+                S.h_objs.push_back(ObjDesc{di, d.first_global + t, n, (uint32_t)ntri, 0u, 0u, 0u, wave ? kObjWave : 0u});
+                ntri += n;
             }
         }
     }
-    if (eslots >= 0xFFFFFFFFull) return PRK_ERR_UNSUPPORTED;
-    const uint32_t nobj = (uint32_t)objs.size();
-    std::vector<prk::TexRec> texs(c->texs.size());
-    for (size_t i = 0; i < texs.size(); ++i)
-        texs[i] = prk::TexRec{c->texs[i].mem, c->texs[i].w, c->texs[i].h, c->texs[i].pitch, c->texs[i].filter};
-    PRK_TRY(hipDeviceSynchronize());  // the scratch below is reused frame to frame
-    PRK_TRY(S.d_draws.ensure(draws.size() * sizeof(prk::DrawRec)));
-    PRK_TRY(hipMemcpy(S.d_draws.p, draws.data(), draws.size() * sizeof(prk::DrawRec), hipMemcpyHostToDevice));
-    if (!texs.empty()) {
-        PRK_TRY(S.d_texs.ensure(texs.size() * sizeof(prk::TexRec)));
-        PRK_TRY(hipMemcpy(S.d_texs.p, texs.data(), texs.size() * sizeof(prk::TexRec), hipMemcpyHostToDevice));
-    }
+    if (3 * ntri + nk1 >= 0x7FFFFFFFull || S.h_k0obj.size() >= (1u << 25)) return PRK_ERR_UNSUPPORTED;
+    const uint32_t nobj = (uint32_t)S.h_objs.size(), nk0 = (uint32_t)S.h_k0obj.size();
+    const uint32_t nt = (uint32_t)ntri, nbig = (uint32_t)S.h_big.size();
+    S.h_texs.resize(c->texs.size());
+    for (size_t i = 0; i < S.h_texs.size(); ++i)
+        S.h_texs[i] = prk::TexRec{c->texs[i].mem, c->texs[i].w, c->texs[i].h, c->texs[i].pitch, c->texs[i].filter};
+    S.h_draws = draws;
+    // (the scratch below is reused frame to frame: stream order on s covers it)
+    auto up = [&](DevBuf &d, const void *src, size_t bytes) -> hipError_t {
+        hipError_t e = d.ensure(std::max<size_t>(bytes, 16));
+        if (e == hipSuccess && bytes) e = hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, s);
+        return e;
+    };
+    PRK_TRY(up(S.d_draws, S.h_draws.data(), S.h_draws.size() * sizeof(prk::DrawRec)));
+    PRK_TRY(up(S.d_texs, S.h_texs.data(), S.h_texs.size() * sizeof(prk::TexRec)));
     fp.draws = (const prk::DrawRec *)S.d_draws.p;
     fp.texs = (const prk::TexRec *)S.d_texs.p;
     fp.draw0 = draws[0];
     fp.tex0 = prk::TexRec{};
-    if (fp.draw0.tex >= 0 && (size_t)fp.draw0.tex < texs.size()) fp.tex0 = texs[fp.draw0.tex];
-    PRK_TRY(S.d_objs.ensure(objs.size() * sizeof(ObjDesc)));
-    PRK_TRY(hipMemcpy(S.d_objs.p, objs.data(), objs.size() * sizeof(ObjDesc), hipMemcpyHostToDevice));
-    const size_t es = std::max<size_t>((size_t)eslots, 1);
-    PRK_TRY(S.d_edges.ensure(es * 112));  // prk_spans.hip ObjEdge
-    PRK_TRY(S.d_ord.ensure(es * 4));
-    PRK_TRY(S.d_tmp.ensure(es * 4));
-    if (!c->pend_edges.empty()) {
-        PRK_TRY(S.d_edges_in.ensure(c->pend_edges.size() * sizeof(prk_edge)));
-        PRK_TRY(hipMemcpy(S.d_edges_in.p, c->pend_edges.data(), c->pend_edges.size() * sizeof(prk_edge),
-                          hipMemcpyHostToDevice));
-    }
-    if (!c->pend_spans.empty()) {
-        PRK_TRY(S.d_spans_in.ensure(c->pend_spans.size() * sizeof(prk_span)));
-        PRK_TRY(hipMemcpy(S.d_spans_in.p, c->pend_spans.data(), c->pend_spans.size() * sizeof(prk_span),
-                          hipMemcpyHostToDevice));
-    }
+    if (fp.draw0.tex >= 0 && (size_t)fp.draw0.tex < S.h_texs.size()) fp.tex0 = S.h_texs[fp.draw0.tex];
+    PRK_TRY(up(S.d_objs, S.h_objs.data(), S.h_objs.size() * sizeof(ObjDesc)));
+    PRK_TRY(up(S.d_k0obj, S.h_k0obj.data(), S.h_k0obj.size() * 4));
+    PRK_TRY(up(S.d_k0tri0, S.h_k0tri0.data(), S.h_k0tri0.size() * 4));
+    PRK_TRY(up(S.d_big, S.h_big.data(), S.h_big.size() * 4));
+    PRK_TRY(up(S.d_k1src, S.h_k1src.data(), S.h_k1src.size() * 4));
+    PRK_TRY(up(S.d_edges_in, c->pend_edges.data(), c->pend_edges.size() * sizeof(prk_edge)));
+    PRK_TRY(up(S.d_spans_in, c->pend_spans.data(), c->pend_spans.size() * sizeof(prk_span)));
     uint32_t modes = 0;  // the pass's span kinds: bit per Mode
     for (const auto &d : draws) modes |= 1u << d.mode;
     const bool scalar = (modes & ~(1u << prk::MODE_AVX)) != 0;
+    // FillEdgeTable per triangle: counts, scan, edges + MergeSort keys.
+    const size_t es = std::max<size_t>(3 * (size_t)nt, 1);
+    PRK_TRY(S.d_ecnt.ensure(((size_t)nt + 1) * 4));
+    PRK_TRY(S.d_escan.ensure(((size_t)nt + 1) * 4));
+    PRK_TRY(S.d_edges.ensure(es * 112));  // prk_spans.hip ObjEdge
+    PRK_TRY(S.d_ekeys.ensure(es * 8));
+    PRK_TRY(S.d_ekeys2.ensure(es * 8));
+    PRK_TRY(S.d_evals.ensure(es * 4));
+    PRK_TRY(S.d_ord.ensure(es * 4));
+    PRK_TRY(S.d_err.ensure(16));
+    uint32_t *escan = (uint32_t *)S.d_escan.p, *ord = (uint32_t *)S.d_ord.p;
+    const uint32_t *total0p = escan + nt;
+    size_t tb = 0;
+    if (nt) PRK_TRY(prk_objtri_count(&fp, S.d_objs.p, (const uint32_t *)S.d_k0obj.p,
+                                     (const uint32_t *)S.d_k0tri0.p, nk0, nt, (uint32_t *)S.d_ecnt.p, s));
+    else PRK_TRY(hipMemsetAsync(S.d_ecnt.p, 0, 4, s));
+    PRK_TRY(prk_scan_u32((const uint32_t *)S.d_ecnt.p, escan, nt + 1, nullptr, &tb, s));
+    PRK_TRY(S.d_temp.ensure(std::max<size_t>(tb, 16)));
+    PRK_TRY(prk_scan_u32((const uint32_t *)S.d_ecnt.p, escan, nt + 1, S.d_temp.p, &tb, s));
+    PRK_TRY(prk_objtri_emit(&fp, S.d_objs.p, (const uint32_t *)S.d_k0obj.p, (const uint32_t *)S.d_k0tri0.p, nk0, nt,
+                            escan, S.d_edges.p, S.d_ekeys.p, (uint32_t *)S.d_evals.p, s));
+    PRK_TRY(hipMemcpyAsync(S.h_rb, total0p, 4, hipMemcpyDeviceToHost, s));
+    PRK_TRY(hipMemsetAsync(S.d_err.p, 0, 4, s));
+    PRK_TRY(hipStreamSynchronize(s));
+    const uint32_t total0 = S.h_rb[0];
+    if (total0) {  // MergeSort of every object (one radix sort, prk_spans.hip)
+        PRK_TRY(prk_obj_sort(S.d_ekeys.p, (uint32_t *)S.d_evals.p, S.d_ekeys2.p, ord, total0, nk0, nullptr, &tb, s));
+        PRK_TRY(S.d_temp.ensure(std::max<size_t>(tb, 16)));
+        PRK_TRY(prk_obj_sort(S.d_ekeys.p, (uint32_t *)S.d_evals.p, S.d_ekeys2.p, ord, total0, nk0, S.d_temp.p, &tb, s));
+    }
+    const uint32_t nwork = total0 + (uint32_t)nk1;
+    PRK_TRY(S.d_work.ensure(std::max<size_t>(nwork, 1) * 112));
     PRK_TRY(S.d_cnt.ensure(((size_t)nobj + 1) * 4));
     PRK_TRY(S.d_off.ensure(((size_t)nobj + 1) * 4));
     uint32_t *cnt = (uint32_t *)S.d_cnt.p, *off = (uint32_t *)S.d_off.p;
     PRK_TRY(hipMemsetAsync(cnt, 0, ((size_t)nobj + 1) * 4, s));
-    PRK_TRY(prk_obj_walk(&fp, S.d_objs.p, nobj, S.d_edges.p, (uint32_t *)S.d_ord.p, (uint32_t *)S.d_tmp.p, 0, cnt,
-                         nullptr, nullptr, nullptr, nullptr, nullptr, S.d_edges_in.p, S.d_spans_in.p, s));
-    size_t tb = 0;
+    auto walk = [&](int pass) -> hipError_t {  // the working copy is stepped by the walk: re-made per pass
+        hipError_t e = prk_obj_gather(S.d_edges.p, ord, total0p, S.d_edges_in.p, (const uint32_t *)S.d_k1src.p,
+                                      (uint32_t)nk1, S.d_work.p, nwork, s);
+        if (e == hipSuccess)
+            e = prk_obj_walk(&fp, S.d_objs.p, nobj, (const uint32_t *)S.d_big.p, nbig, escan, total0p, S.d_work.p,
+                             pass, cnt, off, S.d_recs.p, scalar ? S.d_srecs.p : nullptr, S.d_pos.p,
+                             (uint32_t *)S.d_span_tri.p, S.d_spans_in.p, (uint32_t *)S.d_err.p, s);
+        return e;
+    };
+    PRK_TRY(walk(0));
     PRK_TRY(prk_scan_u32(cnt, off, nobj + 1, nullptr, &tb, s));
     PRK_TRY(S.d_temp.ensure(std::max<size_t>(tb, 16)));
     PRK_TRY(prk_scan_u32(cnt, off, nobj + 1, S.d_temp.p, &tb, s));
-    uint32_t nspan = 0;
-    PRK_TRY(hipMemcpyAsync(&nspan, off + nobj, 4, hipMemcpyDeviceToHost, s));
+    PRK_TRY(hipMemcpyAsync(S.h_rb, off + nobj, 4, hipMemcpyDeviceToHost, s));
+    PRK_TRY(hipMemcpyAsync(S.h_rb + 1, S.d_err.p, 4, hipMemcpyDeviceToHost, s));
     PRK_TRY(hipStreamSynchronize(s));
+    const uint32_t nspan = S.h_rb[0];
+    if (S.h_rb[1]) return PRK_ERR_UNSUPPORTED;  // an object's active list outgrew a wave's LDS
     if (nspan >= prk::kMaxPairs) return PRK_ERR_UNSUPPORTED;  // 31-bit span tags
     const size_t ns = std::max<uint32_t>(nspan, 1);
     PRK_TRY(S.d_recs.ensure(ns * 64));
     PRK_TRY(S.d_pos.ensure(ns * 16));
     PRK_TRY(S.d_span_tri.ensure(ns * 4));
     if (scalar) PRK_TRY(S.d_srecs.ensure(ns * 96));  // DrawModel span records (prk_spans.hip ScSpanRecG)
-    PRK_TRY(prk_obj_walk(&fp, S.d_objs.p, nobj, S.d_edges.p, (uint32_t *)S.d_ord.p, (uint32_t *)S.d_tmp.p, 1, cnt,
-                         off, S.d_recs.p, scalar ? S.d_srecs.p : nullptr, S.d_pos.p, (uint32_t *)S.d_span_tri.p,
-                         S.d_edges_in.p, S.d_spans_in.p, s));
+    PRK_TRY(walk(1));
     PRK_TRY(S.d_scnt.ensure(((size_t)nspan + 1) * 4));
     PRK_TRY(S.d_soff.ensure(((size_t)nspan + 1) * 4));
     uint32_t *scnt = (uint32_t *)S.d_scnt.p, *soff = (uint32_t *)S.d_soff.p;

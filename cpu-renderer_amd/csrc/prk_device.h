@@ -297,6 +297,13 @@ __device__ __forceinline__ uint32_t texel_at(const TexRec &t, int32_t off) {
     return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
+// The wave's LDS writes are visible to all its lanes (no workgroup barrier).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Ordered 32-bit key of a float z for the visibility max (strict '>' with
 // submission order == max z, earliest triangle on ties).
 // +0 and -0 compare equal in the reference, so both map to one key.
@@ -912,92 +919,6 @@ struct RowWalker {
     }
 
     // Edge step of the pair (3811-3829) and the crossing swap (3831-3841 + P3).
-    __device__ __forceinline__ void end_row(bool paired) {
-        if (paired) {
-            step_edge<M, NRM>(S0);
-            step_edge<M, NRM>(S1);
-            const bool sw = S0.X > S1.X;
-            if (sw) {
-                const Edge a = sel(sw, S1, S0), b = sel(sw, S0, S1);
-                S0 = a; S1 = b;
-            }
-        }
-        ++Row;
-    }
-};
-
-// The same AET for a REGULAR triangle, whose list logic reduces to one
-// event: rows [Row, Mid) pair the two edges of the top vertex (S0, S1 in
-// list order); at row Mid the pending edge C (the middle vertex's, YMin ==
-// Mid) is inserted and exactly one of S0, S1 (the one ending at the middle
-// vertex, YMax == Mid) expires; rows (Mid, MaxY) pair the survivor with C.
-// No other insertion or expiry happens before MaxY.  Insertion order
-// (3654-3713) then expiry (3715-3749) leave C first iff C goes before S0, or
-// S0 expires and C goes before S1.  The general RowWalker moves up to all
-// three edges through selects on an insertion or expiry row (about 120 VALU
-// in k_vis); here the event is one survivor select and one ordered pair.
-// Regularity (from_row_walker) is decided per lane after the replay of the
-// rows above the tile; a wave walks this way only when all its lanes are
-// regular (irregular lists keep RowWalker, bit for bit the same list logic).
-template <int M, bool NRM>
-struct TriWalker {
-    Edge S0, S1, C;
-    bool pend;  // C not yet inserted (its row is C.YMin)
-    int32_t MaxY, Row;
-
-    // Whether the rows a RowWalker has left (it is about to run begin_row()
-    // for w.Row) are regular.
-    __device__ __forceinline__ static bool regular(const RowWalker<M, NRM> &w) {
-        if (w.Row >= w.MaxY) return true;  // nothing left to walk
-        int32_t y0 = w.S0.YMax, y1 = w.S1.YMax;
-        bool ok = w.cnt == 2;
-        if (w.cnt == 3 && !w.pend) {
-            // three edges from this row on (the middle vertex rounds to the top
-            // row): exactly one must expire here, the other two keep their order
-            const bool k0 = !(w.S0.YMax <= w.Row), k1 = !(w.S1.YMax <= w.Row), k2 = !(w.S2.YMax <= w.Row);
-            ok = (int)k0 + (int)k1 + (int)k2 == 2;
-            y0 = k0 ? w.S0.YMax : w.S1.YMax;
-            y1 = k0 && k1 ? w.S1.YMax : w.S2.YMax;
-        }
-        const int32_t mid = w.pend ? w.S2.YMin : 0x7fffffff;
-        ok = ok && mid > w.Row;
-        ok = ok && min(y0, y1) >= min(mid, w.MaxY);  // rows [Row, Mid): no expiry
-        if (w.pend && mid < w.MaxY) {  // row Mid: exactly one of the pair ends; then none before MaxY
-            const bool e0 = y0 <= mid, e1 = y1 <= mid;
-            ok = ok && (e0 != e1) && w.S2.YMax > mid && min(e0 ? y1 : y0, w.S2.YMax) >= w.MaxY;
-        }
-        return ok;
-    }
-
-    // The state of a regular RowWalker.
-    __device__ __forceinline__ void from(const RowWalker<M, NRM> &w) {
-        MaxY = w.MaxY;
-        Row = w.Row;
-        pend = w.pend;
-        C = w.S2;
-        if (w.cnt == 3) {  // drop the edge that expires at this row
-            const bool k0 = !(w.S0.YMax <= w.Row), k1 = !(w.S1.YMax <= w.Row);
-            S0 = sel(k0, w.S0, w.S1);
-            S1 = sel(k0 && k1, w.S1, w.S2);
-        } else {
-            S0 = w.S0;
-            S1 = w.S1;
-        }
-    }
-
-    // Insertion + expiry of this->Row; the pair is always emitted.
-    __device__ __forceinline__ bool begin_row() {
-        if (pend && C.YMin == Row) {
-            const bool aexp = S0.YMax <= Row;
-            const bool cfirst = insert_before(C, S0) || (aexp && insert_before(C, S1));
-            const Edge sv = sel(aexp, S1, S0);
-            S0 = sel(cfirst, C, sv);
-            S1 = sel(cfirst, sv, C);
-            pend = false;
-        }
-        return true;
-    }
-
     __device__ __forceinline__ void end_row(bool paired) {
         if (paired) {
             step_edge<M, NRM>(S0);

@@ -117,9 +117,6 @@ __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
 #ifndef PRK_PIXEL_ITEMS
 #define PRK_PIXEL_ITEMS 1  // shading sweep (AVX): one work item per won pixel, not per lane chain
 #endif
-#ifndef PRK_TRIWALK
-#define PRK_TRIWALK 3  // regular triangles walk with TriWalker (one insertion/expiry event): 1 k_vis, 2 k_walk
-#endif
 #ifndef PRK_VIS_WAVES
 // waves per k_vis tile workgroup; each takes whole 64-entry chunks of the bin.
 // Four waves share one 16 KiB key array: 4 workgroups = 16 waves per CU.
@@ -747,12 +744,6 @@ __device__ __forceinline__ int wave_incl_max(int v) {  // v >= 0
     return v;
 }
 
-// The wave's LDS writes are visible to all its lanes (no workgroup barrier).
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // One sweep over the tile's bin for mode M.  SHADE=false: visibility keys;
 // SHADE=true: shade the winners.
@@ -766,8 +757,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
     const int32_t ystart = col0 ? tc.y0 - 1 : tc.y0;  // scalar: (row-1) may store into (row, 0)
     unsigned long long pt[4] = {0, 0, 0, 0};  // PRK_PROF: setup, walk, scan/map, items
     // PRK_PROF event counts (visibility sweep): chunks, row iterations, item
-    // windows, items, active lanes summed over row iterations, spans with items,
-    // regular (TriWalker) chunks
+    // windows, items, active lanes summed over row iterations, spans with items
     unsigned long long pc[7] = {0, 0, 0, 0, 0, 0, 0};
     // Single-draw frames prefetch: the next chunk's bin entry is loaded at the
     // top of a chunk and its vertex attributes before the row walk, so both
@@ -882,7 +872,6 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
         // PRK_LANE_ROWS: every lane walks its own next row each iteration (the
         // span's row travels in its slot); else all lanes step row r together.
         if (PRK_LANE_ROWS && active) active = wk.Row < tc.y1;
-        auto rows = [&](auto &wk) {
         for (int32_t r = ystart; PRK_LANE_ROWS || r < tc.y1; ++r) {
             // Rows per lane this iteration: when few lanes still hold rows, each
             // emits up to 8 of its next rows into the wave's 64 span slots
@@ -968,22 +957,6 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             if (PRK_PROF) { const unsigned long long t1 = PRK_T(); pt[3] += t1 - t0; t0 = t1; }
             if (!__any(active)) break;
-        }
-        };
-        // A wave whose entries are all regular triangles walks them with the
-        // one-event TriWalker (prk_device.h); any irregular list keeps the
-        // general RowWalker for the chunk.
-        if constexpr ((PRK_TRIWALK & 1) != 0) {
-            if (__all(!active || TriWalker<M, SHADE>::regular(wk))) {
-                if (PRK_PROF) pc[6] += 1;
-                TriWalker<M, SHADE> tw;
-                tw.from(wk);
-                rows(tw);
-            } else {
-                rows(wk);
-            }
-        } else {
-            rows(wk);
         }
     }
     if (PRK_PROF && lane == 0)
@@ -1366,7 +1339,6 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
     const int32_t t0 = (int32_t)((uint32_t)tr.tx0 | ((uint32_t)tr.ty0 << 16));
     const int32_t t1 = (int32_t)((uint32_t)tr.tx1 | ((uint32_t)tr.ty1 << 16));
     uint32_t head = 0, cnt = 0;  // wave-uniform queue state
-    auto walk = [&](auto &wk) {
     while (__any(active)) {
         bool push = false, paired = false;
         int32_t Row = 0;
@@ -1403,15 +1375,6 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
             head += 64;
             cnt -= 64;
         }
-    }
-    };
-    // all lanes regular: the one-event TriWalker (as in k_vis)
-    if ((PRK_TRIWALK & 2) && __all(!active || TriWalker<M, true>::regular(wk))) {
-        TriWalker<M, true> tw;
-        tw.from(wk);
-        walk(tw);
-    } else {
-        walk(wk);
     }
     wave_lds_sync();
     if ((uint32_t)lane < cnt) walk_flush(fp, q, (int)((head + lane) & (kWalkQ - 1)), won, recs);

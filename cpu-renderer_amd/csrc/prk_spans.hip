@@ -7,15 +7,26 @@
 // spans across triangles (3654-3869).  The per-triangle kernels cannot
 // express that, so objects of more than one triangle take this path:
 //
-//   k_obj_walk    one thread per object: FillEdgeTable over its triangles,
-//                 MergeSort with the reference's exact recursion (tie order
-//                 included), then the AET walk with the reference's list
-//                 operations (insertion scan, expiry, pairing, the two
-//                 crossing swaps of 3831-3853 with the P3 head/tail fix),
-//                 stepping the paired edges row by row.  Pass 0 counts the
-//                 object's emitted spans; pass 1 writes, for each span in
-//                 submission order (object, row, pair), its FillLineOptimized
-//                 lane-init record (SpanRec, 1543-1835) and its pixel range.
+//   k_objtri_count / k_objtri_emit   one thread per triangle of the pass's
+//                 objects: FillEdgeTable (3894-4117) — the visible edges of
+//                 every triangle, compacted in the reference's order (an
+//                 exclusive scan over the per-triangle counts) — and each
+//                 edge's MergeSort key.
+//   sort          MergeSort (2-72) sorts by YMin with a tie order fixed by its
+//                 recursion (merges take Half1 first on ties, a two-entry run
+//                 keeps its order); the key (object, YMin, recursion path)
+//                 reproduces it exactly under one device radix sort.
+//   k_obj_walk    the AET walk with the reference's list operations (insertion
+//                 scan, expiry, pairing, the two crossing swaps of 3831-3853
+//                 with the P3 head/tail fix), stepping the paired edges row by
+//                 row: one thread per small object or caller edge list, one
+//                 wave per large object (k_obj_walk_wave: the list in LDS, the
+//                 insertion scan, expiry compaction, the pairs' span setup and
+//                 edge steps and both swap passes spread over the lanes).
+//                 Pass 0 counts the object's emitted spans; pass 1 writes, for
+//                 each span in submission order (object, row, pair), its lane-
+//                 init record (FillLineOptimized SpanRec 1543-1835, or DrawModel
+//                 ScSpanRec 298-412) and its pixel range.
 //   k_span_count / k_span_emit   span -> (tile, span) bin entries; sorted by
 //                 tile with the radix sort of the triangle path.
 //   k_span_vis (prk_kernels.hip)  per-tile visibility over the spans with
@@ -23,6 +34,8 @@
 //   k_pix (prk_kernels.hip, span records indexed by span)  shading.
 #include <hipcub/hipcub.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
+
+#include <atomic>
 
 #include "prk_device.h"
 
@@ -41,9 +54,12 @@ struct ObjDesc {
     uint32_t draw;
     uint32_t g0;
     uint32_t tris;
-    uint32_t edge_off;  // first of its edge slots
-    uint32_t kind, src, nsrc, pad;
+    uint32_t tri0;      // kind 0: its first triangle among the pass's object triangles
+    uint32_t kind, src, nsrc;
+    uint32_t k1off;     // kind 1: its first edge slot after the pass's triangle edges;
+                        // bit 31 (kObjWave): walked by one wave (k_obj_walk_wave)
 };
+constexpr uint32_t kObjWave = 0x80000000u;
 
 // Caller edges (prk_edge = edge_info without Next, prk.h) and spans (prk_span).
 struct EdgeIn {
@@ -126,47 +142,6 @@ __device__ __forceinline__ void obj_step(ObjEdge &E) {
         E.U += E.UG;
         E.V += E.VG;
         E.W += E.WG;
-    }
-}
-
-// MergeSort (projekt.cpp:2-72) of the n edge slots named by ord[0..n), by
-// YMin, with the reference's recursion: Count 2 swaps only on '>', larger
-// counts split at Count/2 and merge taking Half0 only on strict '<'.  The
-// tie order this produces depends on the recursion shape, so it is replayed
-// (iteratively, post-order) rather than replaced by another stable sort.
-__device__ void obj_merge_sort(const ObjEdge *E, uint32_t *ord, uint32_t *tmp, uint32_t n) {
-    if (n < 2) return;  // P1: Count 0 returns (the reference recurses forever)
-    struct Fr { uint32_t first, count, stage; };
-    Fr st[64];
-    int sp = 0;
-    st[sp++] = Fr{0u, n, 0u};
-    while (sp > 0) {
-        Fr &f = st[sp - 1];
-        if (f.count == 1) { --sp; continue; }
-        if (f.count == 2) {
-            if (E[ord[f.first]].YMin > E[ord[f.first + 1]].YMin) {
-                const uint32_t t = ord[f.first];
-                ord[f.first] = ord[f.first + 1];
-                ord[f.first + 1] = t;
-            }
-            --sp;
-            continue;
-        }
-        const uint32_t h0 = f.count / 2;
-        if (f.stage == 0) { f.stage = 1; st[sp++] = Fr{f.first, h0, 0u}; continue; }
-        if (f.stage == 1) { f.stage = 2; st[sp++] = Fr{f.first + h0, f.count - h0, 0u}; continue; }
-        uint32_t r0 = f.first, r1 = f.first + h0;
-        const uint32_t m1 = f.first + h0, end = f.first + f.count;
-        for (uint32_t i = 0; i < f.count; ++i) {
-            uint32_t take;
-            if (r0 == m1) take = ord[r1++];
-            else if (r1 == end) take = ord[r0++];
-            else if (E[ord[r0]].YMin < E[ord[r1]].YMin) take = ord[r0++];
-            else take = ord[r1++];
-            tmp[i] = take;
-        }
-        for (uint32_t i = 0; i < f.count; ++i) ord[f.first + i] = tmp[i];
-        --sp;
     }
 }
 
@@ -302,72 +277,225 @@ __device__ __forceinline__ ObjEdge span_end_in(const SpanEndIn &e) {  // FillLin
     return o;
 }
 
-// The whole-object walk of one object of mode M (kind 0: its triangles;
-// kind 1: a caller's edge list).  pass 0 counts its spans, pass 1 writes them
-// at base.
-template <int M>
-__device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const DrawRec &d, ObjEdge *__restrict__ E,
-                            uint32_t *__restrict__ ord, uint32_t *__restrict__ tmp, int pass, uint32_t base,
-                            uint32_t &emitted, SpanRecG *__restrict__ recs, ScSpanRecG *__restrict__ srecs,
-                            SpanPos *__restrict__ pos, uint32_t *__restrict__ span_tri,
-                            const EdgeIn *__restrict__ edges_in) {
-    constexpr bool kScalar = M != MODE_AVX;
-    const bool st = (d.flags & DRAW_ST) != 0;
-    const bool given = od.kind == 1;  // a caller's (sorted) edge list
-    uint32_t n = 0;
-    if (given) {
-        for (uint32_t i = 0; i < od.nsrc; ++i) {
-            obj_edge_in(E[i], edges_in[od.src + i]);
-            ord[i] = i;
+// ---------------------------------------------------------------------------
+// FillEdgeTable of the pass's objects, one thread per triangle.
+// ---------------------------------------------------------------------------
+// Which of a triangle's edges {0,1},{1,2},{2,0} FillEdgeTable writes (bit k):
+// none unless it passes the back-face test (3926-3943), then those with
+// MaxY > 0 (3968) and MinY != MaxY (4066) — tri_edges' `vis`.
+__device__ __forceinline__ uint32_t tri_vis_mask(const FrameParams &fp, const DrawRec &d, uint32_t gt) {
+    V3 cam[3], proj[3];
+    load_positions(d, gt, fp, cam, proj);
+    if (!front_facing(proj)) return 0u;
+    uint32_t m = 0;
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+        const float y0 = proj[e].y, y1 = proj[(e + 1) % 3].y;
+        const bool sw = y0 > y1;  // 3957-3966
+        const float mn = sw ? y1 : y0, mx = sw ? y0 : y1;
+        if (mx > 0 && mn - mx != 0) m |= 1u << e;
+    }
+    return m;
+}
+
+// The kind-0 object (index into the pass's kind-0 list) of object triangle s.
+__device__ __forceinline__ uint32_t obj_of_tri(const uint32_t *__restrict__ k0tri0, uint32_t nk0, uint32_t s) {
+    uint32_t lo = 0, hi = nk0 - 1;
+    while (lo < hi) {  // last object with tri0 <= s
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (k0tri0[mid] <= s) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// MergeSort (projekt.cpp:2-72) as a sort key.  The recursion sorts by YMin;
+// among equal YMin it leaves a two-entry run in its order (13: swap only on
+// '>') and puts every Half1 entry before every Half0 entry (51-57: Half0 only
+// on strict '<').  So entry i of n precedes entry j of equal YMin iff, at the
+// recursion node that separates them, i is the first of a two-entry run or
+// lies in Half1: the path of branch bits from the root (Half1 = 0, Half0 = 1,
+// run position last), left-aligned in kPathBits, orders ties exactly.
+constexpr int kPathBits = 23;  // objects of up to 2^22 edges
+__device__ __forceinline__ uint32_t merge_path(uint32_t i, uint32_t n) {
+    uint32_t first = 0, count = n, path = 0;
+    int bits = 0;
+    while (count > 2) {
+        const uint32_t h0 = count / 2;  // Half0 = [first, first + h0)
+        if (i < first + h0) {
+            path = (path << 1) | 1u;
+            count = h0;
+        } else {
+            path <<= 1;
+            first += h0;
+            count -= h0;
         }
+        ++bits;
+    }
+    if (count == 2) {
+        path = (path << 1) | (i - first);
+        ++bits;
+    }
+    return path << (kPathBits - bits);
+}
+
+// Visible edge count of every object triangle (ecnt[ntri] = 0: the scan's
+// total).
+__global__ void k_objtri_count(FrameParams fp, const ObjDesc *__restrict__ objs, const uint32_t *__restrict__ k0obj,
+                               const uint32_t *__restrict__ k0tri0, uint32_t nk0, uint32_t ntri,
+                               uint32_t *__restrict__ ecnt) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s > ntri) return;
+    if (s == ntri) {
+        ecnt[s] = 0;
+        return;
+    }
+    const ObjDesc od = objs[k0obj[obj_of_tri(k0tri0, nk0, s)]];
+    const DrawRec &d = fp.draws[od.draw];
+    const uint32_t g = od.g0 + (s - od.tri0);
+    ecnt[s] = (uint32_t)__popc(tri_vis_mask(fp, d, d.geom_tri0 + (g - d.first_global)));
+}
+
+// The visible edges of every object triangle (FillEdgeTable 3947-4111, in the
+// reference's order: triangle by triangle, edges {0,1},{1,2},{2,0}) at
+// escan[s], with their MergeSort keys (object, min(YMin, 65535), path).
+template <int M>
+__device__ __forceinline__ void objtri_edges(const FrameParams &fp, const DrawRec &d, uint32_t gt, ObjEdge *out,
+                                             uint32_t mask) {
+    TriRaw<M> raw;
+    load_tri<M>(d, gt, raw);
+    Edge e[3];
+    bool vis[3];
+    tri_edges<M>(raw, d, fp, e[0], e[1], e[2], vis);
+    uint32_t k = 0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+        if ((mask >> j) & 1u) obj_edge_store(out[k++], e[j]);
+}
+
+__global__ void k_objtri_emit(FrameParams fp, const ObjDesc *__restrict__ objs, const uint32_t *__restrict__ k0obj,
+                              const uint32_t *__restrict__ k0tri0, uint32_t nk0, uint32_t ntri,
+                              const uint32_t *__restrict__ escan, ObjEdge *__restrict__ edges,
+                              unsigned long long *__restrict__ keys, uint32_t *__restrict__ vals) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ntri) return;
+    const uint32_t j = obj_of_tri(k0tri0, nk0, s);
+    const ObjDesc od = objs[k0obj[j]];
+    const DrawRec &d = fp.draws[od.draw];
+    const uint32_t g = od.g0 + (s - od.tri0);
+    const uint32_t gt = d.geom_tri0 + (g - d.first_global);
+    const uint32_t mask = tri_vis_mask(fp, d, gt);
+    if (!mask) return;
+    const uint32_t e0 = escan[s];
+    switch (d.mode) {
+        case MODE_AVX: objtri_edges<MODE_AVX>(fp, d, gt, edges + e0, mask); break;
+        case MODE_SC_GOURAUD: objtri_edges<MODE_SC_GOURAUD>(fp, d, gt, edges + e0, mask); break;
+        case MODE_SC_GOURAUD_TEX: objtri_edges<MODE_SC_GOURAUD_TEX>(fp, d, gt, edges + e0, mask); break;
+        case MODE_SC_PHONG: objtri_edges<MODE_SC_PHONG>(fp, d, gt, edges + e0, mask); break;
+        default: objtri_edges<MODE_SC_PHONG_TEX>(fp, d, gt, edges + e0, mask); break;
+    }
+    const uint32_t ob = escan[od.tri0], n = escan[od.tri0 + od.tris] - ob;
+    const uint32_t c = (uint32_t)__popc(mask);
+    for (uint32_t k = 0; k < c; ++k) {
+        const uint32_t ymin = (uint32_t)min(edges[e0 + k].YMin, 65535);
+        keys[e0 + k] = ((unsigned long long)j << (16 + kPathBits)) | ((unsigned long long)ymin << kPathBits) |
+                       merge_path(e0 + k - ob, n);
+        vals[e0 + k] = e0 + k;
+    }
+}
+
+// The walk's working copy of every object's edges: the triangle edges in
+// MergeSort order (work[i] = edges[ord[i]], i < total0), then the caller edge
+// lists (kind 1) as given.  Re-made before each walk pass (the walk steps it).
+__global__ void k_obj_gather(const ObjEdge *__restrict__ edges, const uint32_t *__restrict__ ord,
+                             const uint32_t *__restrict__ total0p, const EdgeIn *__restrict__ edges_in,
+                             const uint32_t *__restrict__ k1src, uint32_t nk1, ObjEdge *__restrict__ work) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t total0 = *total0p;
+    if (i < total0) {
+        work[i] = edges[ord[i]];
+    } else if (i - total0 < nk1) {
+        obj_edge_in(work[i], edges_in[k1src[i - total0]]);
+    }
+}
+
+// An object's edges in the working copy: [e0, e0 + n).
+__device__ __forceinline__ void obj_range(const ObjDesc &od, const uint32_t *__restrict__ escan, uint32_t total0,
+                                          uint32_t &e0, uint32_t &n) {
+    if (od.kind == 0) {
+        e0 = escan[od.tri0];
+        n = escan[od.tri0 + od.tris] - e0;
+    } else {
+        e0 = total0 + (od.k1off & ~kObjWave);
         n = od.nsrc;
     }
-    // FillEdgeTable (3894-4117): visible edges of every triangle, in order.
-    for (uint32_t t = 0; t < (given ? 0u : od.tris); ++t) {
-        const uint32_t g = od.g0 + t;
-        const uint32_t gt = d.geom_tri0 + (g - d.first_global);
-        V3 cam[3], proj[3];
-        load_positions(d, gt, fp, cam, proj);
-        if (!front_facing(proj)) continue;  // 3926-3943
-        TriRaw<M> raw;
-        load_tri<M>(d, gt, raw);
-        Edge e[3];
-        bool vis[3];
-        tri_edges<M>(raw, d, fp, e[0], e[1], e[2], vis);
-        for (int k = 0; k < 3; ++k)
-            if (vis[k]) {
-                obj_edge_store(E[n], e[k]);
-                ord[n] = n;
-                ++n;
-            }
+}
+
+// One span of the pair (L, R) at Row (pass 1 writes it at `at`).
+template <int M>
+__device__ __forceinline__ bool emit_span(const FrameParams &fp, const ObjEdge &L, const ObjEdge &R, int32_t Row,
+                                          const DrawRec &d, bool st, uint32_t g0, bool write, uint32_t at,
+                                          SpanRecG *__restrict__ recs, ScSpanRecG *__restrict__ srecs,
+                                          SpanPos *__restrict__ pos, uint32_t *__restrict__ span_tri) {
+    SpanPos sp;
+    if constexpr (M != MODE_AVX) {
+        ScSpanRecG srec;
+        if (!obj_span_scalar<M>(fp, L, R, Row, d.tex, srec, sp)) return false;
+        if (write) {
+            SpanRecG mark;
+            mark.q0 = make_float4(__uint_as_float(kScalarSpan), 0.0f, 0.0f, 0.0f);
+            mark.q1 = mark.q2 = mark.q3 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            recs[at] = mark;
+            srecs[at] = srec;
+        }
+    } else {
+        SpanRecG rec;
+        if (!obj_span(fp, L, R, Row, d.tex, st, rec, sp)) return false;
+        if (write) recs[at] = rec;
     }
-    if (!given) obj_merge_sort(E, ord, tmp, n);  // 4117
+    if (write) {
+        pos[at] = sp;
+        span_tri[at] = g0;
+    }
+    return true;
+}
+
+// The AET walk of one object by one thread (small objects, caller edge
+// lists): E = its n edges, sorted (kind 0) or as given (kind 1).
+template <int M>
+__device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const DrawRec &d, ObjEdge *__restrict__ E,
+                            uint32_t n, int pass, uint32_t base, uint32_t &emitted, SpanRecG *__restrict__ recs,
+                            ScSpanRecG *__restrict__ srecs, SpanPos *__restrict__ pos,
+                            uint32_t *__restrict__ span_tri) {
+    constexpr bool kScalar = M != MODE_AVX;
+    const bool st = (d.flags & DRAW_ST) != 0;
+    const bool given = od.kind == 1;  // a caller's edge list: scanned whole every row
     if (n == 0) return;
     // The AET walk of DrawModelOptimized(RenderQueue,...) (3626-3869) /
     // DrawModel (173-598): the same list logic.
-    const int32_t FirstRow = E[ord[0]].YMin;
-    int32_t MaxRow = E[ord[0]].YMax;
-    for (uint32_t i = 1; i < n; ++i) MaxRow = max(MaxRow, E[ord[i]].YMax);
+    const int32_t FirstRow = E[0].YMin;
+    int32_t MaxRow = E[0].YMax;
+    for (uint32_t i = 1; i < n; ++i) MaxRow = max(MaxRow, E[i].YMax);
     const int32_t MaxY = min(min(MaxRow, fp.H), fp.row1);
     // DrawModel's span of row row0-1 can store its one-past-the-row pixel
     // into (row0, 0)
     const int32_t RowLo = kScalar ? fp.row0 - 1 : fp.row0;
+    for (uint32_t i = 0; i < n; ++i) E[i].Next = -1;
     int32_t Head = -1, Tail = -1;
     uint32_t ins = 0;  // next sorted edge to insert (sorted by YMin)
     for (int32_t Row = FirstRow; Row < MaxY; ++Row) {
         // insertion (3654-3713): the edges with YMin == Row, in array
-        // order.  Sorted lists (our MergeSort) hold them contiguously; a
+        // order.  Sorted lists (MergeSort) hold them contiguously; a
         // caller's list is scanned whole, as the reference does.
         uint32_t i0 = 0, i1 = n;
         if (!given) {
-            while (ins < n && E[ord[ins]].YMin < Row) ++ins;
+            while (ins < n && E[ins].YMin < Row) ++ins;
             i0 = ins;
-            while (ins < n && E[ord[ins]].YMin == Row) ++ins;
+            while (ins < n && E[ins].YMin == Row) ++ins;
             i1 = ins;
         }
         for (uint32_t ii = i0; ii < i1; ++ii) {
-            if (E[ord[ii]].YMin != Row) continue;
-            const int32_t c = (int32_t)ord[ii];
+            if (E[ii].YMin != Row) continue;
+            const int32_t c = (int32_t)ii;
             ObjEdge &Cur = E[c];
             if (Head >= 0) {
                 if (obj_before(Cur, E[Head])) {
@@ -421,34 +549,10 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
         int32_t PrevCur = -1, PrevNext = -1;  // pairing 3751-3869
         int32_t Cur = Head, Next = E[Cur].Next;
         while (Next >= 0) {
-            if (Row >= RowLo) {  // a span of this pass's rows (3759-3809 / 298-538)
-                SpanPos sp;
-                if constexpr (kScalar) {
-                    ScSpanRecG srec;
-                    if (obj_span_scalar<M>(fp, E[Cur], E[Next], Row, d.tex, srec, sp)) {
-                        if (pass) {
-                            SpanRecG mark;
-                            mark.q0 = make_float4(__uint_as_float(kScalarSpan), 0.0f, 0.0f, 0.0f);
-                            mark.q1 = mark.q2 = mark.q3 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                            recs[base + emitted] = mark;
-                            srecs[base + emitted] = srec;
-                            pos[base + emitted] = sp;
-                            span_tri[base + emitted] = od.g0;
-                        }
-                        ++emitted;
-                    }
-                } else {
-                    SpanRecG rec;
-                    if (obj_span(fp, E[Cur], E[Next], Row, d.tex, st, rec, sp)) {
-                        if (pass) {
-                            recs[base + emitted] = rec;
-                            pos[base + emitted] = sp;
-                            span_tri[base + emitted] = od.g0;
-                        }
-                        ++emitted;
-                    }
-                }
-            }
+            if (Row >= RowLo &&  // a span of this pass's rows (3759-3809 / 298-538)
+                emit_span<M>(fp, E[Cur], E[Next], Row, d, st, od.g0, pass != 0, base + emitted, recs, srecs, pos,
+                             span_tri))
+                ++emitted;
             obj_step<M>(E[Cur]);  // 3811-3829
             obj_step<M>(E[Next]);
             if (E[Cur].X > E[Next].X) {  // 3831-3841
@@ -482,43 +586,37 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
 }
 
 __global__ void __launch_bounds__(64) k_obj_walk(FrameParams fp, const ObjDesc *__restrict__ objs, uint32_t nobj,
-                                                 ObjEdge *__restrict__ edges, uint32_t *__restrict__ ordbuf,
-                                                 uint32_t *__restrict__ tmpbuf, int pass,
-                                                 uint32_t *__restrict__ counts, const uint32_t *__restrict__ offs,
-                                                 SpanRecG *__restrict__ recs, ScSpanRecG *__restrict__ srecs,
-                                                 SpanPos *__restrict__ pos,
-                                                 uint32_t *__restrict__ span_tri, const EdgeIn *__restrict__ edges_in,
+                                                 const uint32_t *__restrict__ escan,
+                                                 const uint32_t *__restrict__ total0p, ObjEdge *__restrict__ work,
+                                                 int pass, uint32_t *__restrict__ counts,
+                                                 const uint32_t *__restrict__ offs, SpanRecG *__restrict__ recs,
+                                                 ScSpanRecG *__restrict__ srecs, SpanPos *__restrict__ pos,
+                                                 uint32_t *__restrict__ span_tri,
                                                  const SpanIn *__restrict__ spans_in) {
     const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
     if (o >= nobj) return;
     const ObjDesc od = objs[o];
+    if (od.kind != 2 && (od.k1off & kObjWave)) return;  // k_obj_walk_wave's
     const DrawRec &d = fp.draws[od.draw];
     const bool st = (d.flags & DRAW_ST) != 0;
     const uint32_t base = pass ? offs[o] : 0u;
     uint32_t emitted = 0;
     if (od.kind == 2) {  // one caller-given span (DoLineRenderWork / DoBufferLineRenderWork)
         const SpanIn sp = spans_in[od.src];
-        if (sp.Row >= fp.row0 && sp.Row < fp.row1 && sp.Row < fp.H) {
-            SpanRecG rec;
-            SpanPos ps;
-            if (obj_span(fp, span_end_in(sp.L), span_end_in(sp.R), sp.Row, d.tex, st, rec, ps)) {
-                if (pass) {
-                    recs[base] = rec;
-                    pos[base] = ps;
-                    span_tri[base] = od.g0;
-                }
-                emitted = 1;
-            }
-        }
+        if (sp.Row >= fp.row0 && sp.Row < fp.row1 && sp.Row < fp.H &&
+            emit_span<MODE_AVX>(fp, span_end_in(sp.L), span_end_in(sp.R), sp.Row, d, st, od.g0, pass != 0, base,
+                                recs, srecs, pos, span_tri))
+            emitted = 1;
         if (!pass) counts[o] = emitted;
         return;
     }
-    ObjEdge *E = edges + od.edge_off;
-    uint32_t *ord = ordbuf + od.edge_off, *tmp = tmpbuf + od.edge_off;
+    uint32_t e0, n;
+    obj_range(od, escan, *total0p, e0, n);
+    ObjEdge *E = work + e0;
     switch (d.mode) {
-#define PRK_WALK_OBJ(MM)                                                                                      \
-    case MM:                                                                                                  \
-        walk_object<MM>(fp, od, d, E, ord, tmp, pass, base, emitted, recs, srecs, pos, span_tri, edges_in);   \
+#define PRK_WALK_OBJ(MM)                                                                         \
+    case MM:                                                                                     \
+        walk_object<MM>(fp, od, d, E, n, pass, base, emitted, recs, srecs, pos, span_tri);       \
         break;
         PRK_WALK_OBJ(MODE_AVX)
         PRK_WALK_OBJ(MODE_SC_GOURAUD)
@@ -529,6 +627,203 @@ __global__ void __launch_bounds__(64) k_obj_walk(FrameParams fp, const ObjDesc *
         default: break;
     }
     if (!pass) counts[o] = emitted;
+}
+
+// ---------------------------------------------------------------------------
+// The AET walk of one large object by one wave.  The list lives in LDS as an
+// array in list order (position p = the p-th edge from ListHead) with the
+// fields the list operations read (X, Gradient, Left, YMax) beside each edge
+// index; the edges themselves stay in the working copy.  Per row, exactly
+// the reference's operations (P3 included), as array operations:
+//   insertion (3654-3713)  each new edge, in sorted order, goes before the
+//                          first entry it sorts before (a ballot over the
+//                          list), else to the tail; the tail shifts by one;
+//   expiry (3715-3749)     entries with YMax <= Row leave, order kept (a
+//                          ballot compaction);
+//   pairing (3751-3869)    entries (2k, 2k+1) pair: span, then both edges
+//                          step; then every pair swaps if Cur.X > Next.X
+//                          (3831-3841), then every boundary (2k-1, 2k) swaps
+//                          if PrevNext.X > Cur.X (3843-3853).  Pair k's second
+//                          swap reads entry 2k-1 as pair k-1's first swap left
+//                          it and entry 2k as its own first swap left it, and
+//                          pairs touch disjoint entries, so the reference's
+//                          left-to-right sequence equals the two parallel
+//                          passes.  An odd last entry neither pairs nor steps.
+// ---------------------------------------------------------------------------
+constexpr int kWaveListCap = 4096;
+struct WaveList {
+    int32_t idx[kWaveListCap];
+    float x[kWaveListCap], g[kWaveListCap];
+    int32_t left[kWaveListCap], ymax[kWaveListCap];
+};
+
+__device__ __forceinline__ int wave_max_i32(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
+
+template <int M>
+__device__ void walk_object_wave(const FrameParams &fp, const ObjDesc &od, const DrawRec &d,
+                                 ObjEdge *__restrict__ E, uint32_t n, int pass, uint32_t base, uint32_t &emitted,
+                                 WaveList &L, SpanRecG *__restrict__ recs, ScSpanRecG *__restrict__ srecs,
+                                 SpanPos *__restrict__ pos, uint32_t *__restrict__ span_tri,
+                                 uint32_t *__restrict__ err) {
+    constexpr bool kScalar = M != MODE_AVX;
+    const int lane = threadIdx.x & 63;
+    const bool st = (d.flags & DRAW_ST) != 0;
+    if (n == 0) return;
+    int32_t mr = INT32_MIN;
+    for (uint32_t i = lane; i < n; i += 64) mr = max(mr, E[i].YMax);
+    const int32_t MaxRow = wave_max_i32(mr);
+    const int32_t FirstRow = E[0].YMin;
+    const int32_t MaxY = min(min(MaxRow, fp.H), fp.row1);
+    const int32_t RowLo = kScalar ? fp.row0 - 1 : fp.row0;
+    int m = 0;         // list length (wave-uniform)
+    uint32_t ins = 0;  // next sorted edge to insert
+    for (int32_t Row = FirstRow; Row < MaxY; ++Row) {
+        while (ins < n && E[ins].YMin < Row) ++ins;
+        while (ins < n && E[ins].YMin == Row) {  // insertion 3654-3713, in sorted order
+            const float cx = E[ins].X, cg = E[ins].G;
+            const int32_t cl = E[ins].Left, cy = E[ins].YMax;
+            int p = m;
+            for (int c0 = 0; c0 < m; c0 += 64) {
+                const int q = c0 + lane;
+                bool b = false;
+                if (q < m) {
+                    const float x = L.x[q], g = L.g[q];
+                    b = cx < x || (cx == x && (cg < g || (cg == g && cl < L.left[q])));
+                }
+                const unsigned long long bal = __ballot(b);
+                if (bal) {
+                    p = c0 + (int)__builtin_ctzll(bal);
+                    break;
+                }
+            }
+            if (m >= kWaveListCap) {  // list longer than LDS holds: the pass fails
+                if (lane == 0) atomicOr(err, 1u);
+                return;
+            }
+            for (int top = m; top > p; top -= 64) {  // entries [p, m) move up one, top chunk first
+                const int q = top - 1 - lane;
+                int32_t vi = 0, vl = 0, vy = 0;
+                float vx = 0, vg = 0;
+                if (q >= p) { vi = L.idx[q]; vx = L.x[q]; vg = L.g[q]; vl = L.left[q]; vy = L.ymax[q]; }
+                wave_lds_sync();
+                if (q >= p) { L.idx[q + 1] = vi; L.x[q + 1] = vx; L.g[q + 1] = vg; L.left[q + 1] = vl; L.ymax[q + 1] = vy; }
+                wave_lds_sync();
+            }
+            if (lane == 0) { L.idx[p] = (int32_t)ins; L.x[p] = cx; L.g[p] = cg; L.left[p] = cl; L.ymax[p] = cy; }
+            wave_lds_sync();
+            ++m;
+            ++ins;
+        }
+        {  // expiry 3715-3749: keep entries with YMax > Row, in order
+            int out = 0;
+            for (int c0 = 0; c0 < m; c0 += 64) {
+                const int q = c0 + lane;
+                const bool keep = q < m && !(L.ymax[q] <= Row);
+                int32_t vi = 0, vl = 0, vy = 0;
+                float vx = 0, vg = 0;
+                if (keep) { vi = L.idx[q]; vx = L.x[q]; vg = L.g[q]; vl = L.left[q]; vy = L.ymax[q]; }
+                const unsigned long long bal = __ballot(keep);
+                const int at = out + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                wave_lds_sync();
+                if (keep) { L.idx[at] = vi; L.x[at] = vx; L.g[at] = vg; L.left[at] = vl; L.ymax[at] = vy; }
+                wave_lds_sync();
+                out += __popcll(bal);
+            }
+            m = out;
+        }
+        const int P = m / 2;  // pairing 3751-3869
+        for (int k0 = 0; k0 < P; k0 += 64) {
+            const int k = k0 + lane;
+            const bool valid = k < P;
+            bool em = false;
+            ObjEdge a, b;
+            int32_t ia = 0, ib = 0;
+            if (valid) {
+                ia = L.idx[2 * k];
+                ib = L.idx[2 * k + 1];
+                a = E[ia];
+                b = E[ib];
+                em = Row >= RowLo && emit_span<M>(fp, a, b, Row, d, st, od.g0, false, 0, recs, srecs, pos, span_tri);
+            }
+            const unsigned long long bal = __ballot(em);
+            if (em && pass) {
+                const uint32_t at = base + emitted + (uint32_t)__builtin_amdgcn_mbcnt_hi(
+                                                          (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                emit_span<M>(fp, a, b, Row, d, st, od.g0, true, at, recs, srecs, pos, span_tri);
+            }
+            emitted += (uint32_t)__popcll(bal);
+            if (valid) {  // 3811-3829
+                obj_step<M>(a);
+                obj_step<M>(b);
+                E[ia] = a;
+                E[ib] = b;
+                L.x[2 * k] = a.X;
+                L.x[2 * k + 1] = b.X;
+            }
+        }
+        wave_lds_sync();
+        for (int pass_sw = 0; pass_sw < 2; ++pass_sw) {  // 3831-3841, then 3843-3853
+            for (int k0 = pass_sw; k0 < P; k0 += 64) {
+                const int k = k0 + lane;
+                const int q = pass_sw == 0 ? 2 * k : 2 * k - 1;  // swap entries q, q + 1
+                bool sw = false;
+                int32_t i0 = 0, i1 = 0, l0 = 0, l1 = 0, y0 = 0, y1 = 0;
+                float x0 = 0, x1 = 0, g0 = 0, g1 = 0;
+                if (k < P) {
+                    x0 = L.x[q];
+                    x1 = L.x[q + 1];
+                    sw = x0 > x1;
+                    if (sw) {
+                        i0 = L.idx[q]; i1 = L.idx[q + 1]; g0 = L.g[q]; g1 = L.g[q + 1];
+                        l0 = L.left[q]; l1 = L.left[q + 1]; y0 = L.ymax[q]; y1 = L.ymax[q + 1];
+                    }
+                }
+                wave_lds_sync();
+                if (sw) {
+                    L.idx[q] = i1; L.idx[q + 1] = i0; L.x[q] = x1; L.x[q + 1] = x0; L.g[q] = g1; L.g[q + 1] = g0;
+                    L.left[q] = l1; L.left[q + 1] = l0; L.ymax[q] = y1; L.ymax[q + 1] = y0;
+                }
+                wave_lds_sync();
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(64) k_obj_walk_wave(FrameParams fp, const ObjDesc *__restrict__ objs,
+                                                      const uint32_t *__restrict__ big, const uint32_t *__restrict__ escan,
+                                                      const uint32_t *__restrict__ total0p, ObjEdge *__restrict__ work,
+                                                      int pass, uint32_t *__restrict__ counts,
+                                                      const uint32_t *__restrict__ offs, SpanRecG *__restrict__ recs,
+                                                      ScSpanRecG *__restrict__ srecs, SpanPos *__restrict__ pos,
+                                                      uint32_t *__restrict__ span_tri, uint32_t *__restrict__ err) {
+    extern __shared__ unsigned long long lds_raw[];
+    WaveList &L = *reinterpret_cast<WaveList *>(lds_raw);
+    const uint32_t o = big[blockIdx.x];
+    const ObjDesc od = objs[o];
+    const DrawRec &d = fp.draws[od.draw];
+    const uint32_t base = pass ? offs[o] : 0u;
+    uint32_t emitted = 0, e0, n;
+    obj_range(od, escan, *total0p, e0, n);
+    ObjEdge *E = work + e0;
+    switch (d.mode) {
+#define PRK_WALK_OBJ(MM)                                                                                  \
+    case MM:                                                                                              \
+        walk_object_wave<MM>(fp, od, d, E, n, pass, base, emitted, L, recs, srecs, pos, span_tri, err);   \
+        break;
+        PRK_WALK_OBJ(MODE_AVX)
+        PRK_WALK_OBJ(MODE_SC_GOURAUD)
+        PRK_WALK_OBJ(MODE_SC_GOURAUD_TEX)
+        PRK_WALK_OBJ(MODE_SC_PHONG)
+        PRK_WALK_OBJ(MODE_SC_PHONG_TEX)
+#undef PRK_WALK_OBJ
+        default: break;
+    }
+    if (!pass && threadIdx.x == 0) counts[o] = emitted;
 }
 
 // The tiles of a span: those of its row its [minx, min(maxx, W)) crosses and,
@@ -601,16 +896,74 @@ __global__ void k_span_tile_offsets(const uint32_t *__restrict__ keys, uint32_t 
 
 extern "C" {
 
-// Pass 0 / 1 of the object walk.
-hipError_t prk_obj_walk(const prk::FrameParams *fp, const void *objs, uint32_t nobj, void *edges, uint32_t *ord,
-                        uint32_t *tmp, int pass, uint32_t *counts, const uint32_t *offs, void *recs, void *srecs,
-                        void *pos, uint32_t *span_tri, const void *edges_in, const void *spans_in, hipStream_t s) {
+// FillEdgeTable of the pass's object triangles: per-triangle edge counts
+// (ntri + 1 values, the last 0) ...
+hipError_t prk_objtri_count(const prk::FrameParams *fp, const void *objs, const uint32_t *k0obj,
+                            const uint32_t *k0tri0, uint32_t nk0, uint32_t ntri, uint32_t *ecnt, hipStream_t s) {
+    hipLaunchKernelGGL(prk::k_objtri_count, dim3((ntri + 1 + 255) / 256), dim3(256), 0, s, *fp,
+                       reinterpret_cast<const prk::ObjDesc *>(objs), k0obj, k0tri0, nk0, ntri, ecnt);
+    return hipGetLastError();
+}
+// ... then the edges at their exclusive scan, with their MergeSort keys.
+hipError_t prk_objtri_emit(const prk::FrameParams *fp, const void *objs, const uint32_t *k0obj,
+                           const uint32_t *k0tri0, uint32_t nk0, uint32_t ntri, const uint32_t *escan, void *edges,
+                           void *keys, uint32_t *vals, hipStream_t s) {
+    if (ntri == 0) return hipSuccess;
+    hipLaunchKernelGGL(prk::k_objtri_emit, dim3((ntri + 255) / 256), dim3(256), 0, s, *fp,
+                       reinterpret_cast<const prk::ObjDesc *>(objs), k0obj, k0tri0, nk0, ntri, escan,
+                       reinterpret_cast<prk::ObjEdge *>(edges), reinterpret_cast<unsigned long long *>(keys), vals);
+    return hipGetLastError();
+}
+// MergeSort of every object: one radix sort of the keys (temp == nullptr:
+// size query); vals_out = the edges in sorted order.
+hipError_t prk_obj_sort(void *keys_in, uint32_t *vals_in, void *keys_out, uint32_t *vals_out, uint32_t n,
+                        uint32_t nk0, void *temp, size_t *temp_bytes, hipStream_t s) {
+    int obits = 1;
+    while ((1u << obits) < nk0 && obits < 25) ++obits;
+    const unsigned end_bit = 16 + prk::kPathBits + obits;
+    unsigned long long *ki = reinterpret_cast<unsigned long long *>(keys_in);
+    unsigned long long *ko = reinterpret_cast<unsigned long long *>(keys_out);
+    return rocprim::radix_sort_pairs(temp, *temp_bytes, ki, ko, vals_in, vals_out, n, 0, end_bit, s);
+}
+// The walk's working copy (n slots: total0 triangle edges, then nk1 caller edges).
+hipError_t prk_obj_gather(const void *edges, const uint32_t *ord, const uint32_t *total0p, const void *edges_in,
+                          const uint32_t *k1src, uint32_t nk1, void *work, uint32_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(prk::k_obj_gather, dim3((n + 255) / 256), dim3(256), 0, s,
+                       reinterpret_cast<const prk::ObjEdge *>(edges), ord, total0p,
+                       reinterpret_cast<const prk::EdgeIn *>(edges_in), k1src, nk1,
+                       reinterpret_cast<prk::ObjEdge *>(work));
+    return hipGetLastError();
+}
+// Pass 0 / 1 of the object walk: a thread per object, a wave per object of
+// big[0..nbig) (those flagged kObjWave).  err: set when an object's list
+// outgrows a wave's LDS.
+hipError_t prk_obj_walk(const prk::FrameParams *fp, const void *objs, uint32_t nobj, const uint32_t *big, uint32_t nbig,
+                        const uint32_t *escan, const uint32_t *total0p, void *work, int pass, uint32_t *counts,
+                        const uint32_t *offs, void *recs, void *srecs, void *pos, uint32_t *span_tri,
+                        const void *spans_in, uint32_t *err, hipStream_t s) {
     if (nobj == 0) return hipSuccess;
     hipLaunchKernelGGL(prk::k_obj_walk, dim3((nobj + 63) / 64), dim3(64), 0, s, *fp,
-                       reinterpret_cast<const prk::ObjDesc *>(objs), nobj, reinterpret_cast<prk::ObjEdge *>(edges),
-                       ord, tmp, pass, counts, offs, reinterpret_cast<prk::SpanRecG *>(recs),
-                       reinterpret_cast<prk::ScSpanRecG *>(srecs), reinterpret_cast<prk::SpanPos *>(pos), span_tri,
-                       reinterpret_cast<const prk::EdgeIn *>(edges_in), reinterpret_cast<const prk::SpanIn *>(spans_in));
+                       reinterpret_cast<const prk::ObjDesc *>(objs), nobj, escan, total0p,
+                       reinterpret_cast<prk::ObjEdge *>(work), pass, counts, offs,
+                       reinterpret_cast<prk::SpanRecG *>(recs), reinterpret_cast<prk::ScSpanRecG *>(srecs),
+                       reinterpret_cast<prk::SpanPos *>(pos), span_tri, reinterpret_cast<const prk::SpanIn *>(spans_in));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || nbig == 0) return e;
+    static std::atomic<int> attr[64];  // dynamic LDS above 64 KiB, per device
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    if (attr[dev].load() == 0) {
+        e = hipFuncSetAttribute(reinterpret_cast<const void *>(&prk::k_obj_walk_wave),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, sizeof(prk::WaveList));
+        if (e != hipSuccess) return e;
+        attr[dev].store(1);
+    }
+    hipLaunchKernelGGL(prk::k_obj_walk_wave, dim3(nbig), dim3(64), sizeof(prk::WaveList), s, *fp,
+                       reinterpret_cast<const prk::ObjDesc *>(objs), big, escan, total0p,
+                       reinterpret_cast<prk::ObjEdge *>(work), pass, counts, offs,
+                       reinterpret_cast<prk::SpanRecG *>(recs), reinterpret_cast<prk::ScSpanRecG *>(srecs),
+                       reinterpret_cast<prk::SpanPos *>(pos), span_tri, err);
     return hipGetLastError();
 }
 

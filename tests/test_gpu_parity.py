@@ -547,6 +547,38 @@ def test_whole_object_scalar_random_objects(gpu, tpo, seed, phong, textured):
              label="scalar objects tpo=%d phong=%d tex=%d" % (tpo, phong, textured))
 
 
+@pytest.mark.parametrize("phong", [False, True])
+def test_whole_object_scalar_c2_one_object(gpu, phong):
+    """C2 (the ~70k-triangle bunny stand-in, 1920x1080) submitted as ONE
+    object through DrawModel, Gouraud and untextured Phong: a wave walks its
+    active edge table (hundreds of edges per row), against the oracle's
+    whole-object walk."""
+    s = scenes.displaced_sphere(70000, 1920, 1080, seed=3)
+    g, o = run_both(s, semantics=abi.PRK_SEM_SCALAR, phong=phong, tris_per_object=s.tri_count, exact_color=not phong,
+                    label="C2 one object phong=%d" % phong)
+    assert (g[2] >= 0).sum() > 100000
+
+
+@pytest.mark.parametrize("sem", [abi.PRK_SEM_AVX, abi.PRK_SEM_AVX_ST, abi.PRK_SEM_SCALAR])
+@pytest.mark.parametrize("tpo", [64, 700])
+def test_whole_object_wave_walk(gpu, sem, tpo):
+    """Objects large enough for the one-wave walk (k_obj_walk_wave): random
+    triangles with ties and clipping, so spans pair unrelated triangles, lists
+    cross 64-entry chunks, both swap passes fire and entries expire mid-list."""
+    s = scenes.with_ties(scenes.random_soup(2800, 384, 256, radius=40, seed=tpo, centroid_margin=40), seed=tpo)
+    run_both(s, semantics=sem, phong=True, tris_per_object=tpo, exact_color=sem != abi.PRK_SEM_SCALAR,
+             label="wave objects tpo=%d sem=%d" % (tpo, sem))
+
+
+def test_whole_object_list_overflow_rejected(gpu):
+    """An object whose active edge list outgrows one wave's LDS list (4096
+    edges on a row) is rejected (PRK_ERR_UNSUPPORTED), not walked wrongly."""
+    s = scenes.random_soup(1_000_000, 4096, 4096, radius=16, seed=7)
+    with pytest.raises(prk.PrkError) as e:
+        prk.render_scene(s, tris_per_object=s.tri_count, debug=False)
+    assert e.value.code == abi.PRK_ERR_UNSUPPORTED
+
+
 def test_whole_object_scalar_bands_and_passes(gpu):
     """Scalar whole objects in row bands (a band's first row receives the
     one-past-the-row store of the row above it) and mixed with per-triangle
