@@ -128,6 +128,11 @@ int status_of(hipError_t e) {
 struct prk_context {
     int device = 0;
     hipStream_t own_stream = nullptr;
+    // prk_geometry_write: copies on copy_stream after read_ev (the end of the
+    // last flush); the next flush's streams wait for in_ev
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t in_ev = nullptr, read_ev = nullptr;
+    bool in_wait = false, read_rec = false;
     // target
     void *color = nullptr;
     int32_t pitch = 0;
@@ -266,6 +271,9 @@ int prk_create(int device, prk_context **out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->bin_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->vis_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->s_mark, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->in_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->read_ev, hipEventDisableTiming);
     for (int i = 0; i < prk_context::kSets && e == hipSuccess; ++i) {
         e = hipEventCreateWithFlags(&c->bset[i].free_ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->bset[i].binned_ev, hipEventDisableTiming);
@@ -328,6 +336,9 @@ int prk_destroy(prk_context *c) {
         if (S.h_rb) (void)hipHostFree(S.h_rb);
     }
     if (c->s_mark) (void)hipEventDestroy(c->s_mark);
+    if (c->in_ev) (void)hipEventDestroy(c->in_ev);
+    if (c->read_ev) (void)hipEventDestroy(c->read_ev);
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->h_total) (void)hipHostFree(c->h_total);
     for (auto &slot : c->ev)
         for (auto &e : slot)
@@ -450,6 +461,26 @@ int prk_target_upload(prk_context *c, const uint32_t *color_host, int32_t host_p
         PRK_TRY(hipMemcpy2D(c->color, c->pitch, color_host, host_pitch, (size_t)c->W * 4, rows,
                             hipMemcpyHostToDevice));
     if (z_host) PRK_TRY(hipMemcpy(c->zbuf, z_host, (size_t)c->W * rows * 4, hipMemcpyHostToDevice));
+    return PRK_OK;
+}
+
+int prk_target_upload_async(prk_context *c, const uint32_t *color_host, int32_t host_pitch, const float *z_host) {
+    if (!c) return PRK_ERR_ARG;
+    if (!c->color) return PRK_ERR_NO_TARGET;
+    PRK_TRY(hipSetDevice(c->device));
+    // after the frames already flushed (they read and write the target) and
+    // whatever the context's stream holds (a clear, an earlier upload)
+    if (c->read_rec) PRK_TRY(hipStreamWaitEvent(c->copy_stream, c->read_ev, 0));
+    PRK_TRY(hipEventRecord(c->s_mark, c->own_stream));
+    PRK_TRY(hipStreamWaitEvent(c->copy_stream, c->s_mark, 0));
+    const int rows = c->row1 - c->row0;
+    if (color_host)
+        PRK_TRY(hipMemcpy2DAsync(c->color, c->pitch, color_host, host_pitch, (size_t)c->W * 4, rows,
+                                 hipMemcpyHostToDevice, c->copy_stream));
+    if (z_host)
+        PRK_TRY(hipMemcpyAsync(c->zbuf, z_host, (size_t)c->W * rows * 4, hipMemcpyHostToDevice, c->copy_stream));
+    PRK_TRY(hipEventRecord(c->in_ev, c->copy_stream));
+    c->in_wait = true;
     return PRK_OK;
 }
 
@@ -635,6 +666,66 @@ int prk_geometry_update(prk_context *c, int32_t handle, const float *v, const fl
         if (d.src_kind == 0 && d.geom == handle) {
             d.V = g.V; d.C = g.C; d.N = g.N; d.UV = g.UV;
         }
+    return PRK_OK;
+}
+
+int prk_geometry_write(prk_context *c, int32_t handle, uint32_t first_vertex, uint32_t vertex_count,
+                       const float *v, const float *col, const float *n, const float *uv) {
+    if (!c || handle < 0 || (size_t)handle >= c->geoms.size() || first_vertex % 3 || vertex_count % 3)
+        return PRK_ERR_ARG;
+    const uint64_t end64 = (uint64_t)first_vertex + vertex_count;
+    if (end64 > 0xFFFFFFF0ull) return PRK_ERR_ARG;
+    const uint32_t end = (uint32_t)end64;
+    Geometry &g = c->geoms[handle];
+    if (!g.owned) return PRK_ERR_ARG;
+    PRK_TRY(hipSetDevice(c->device));
+    const float *src[4] = {v, col, n, uv};
+    const float **dst[4] = {&g.V, &g.C, &g.N, &g.UV};
+    const size_t comp[4] = {3, 4, 3, 2};
+    // Buffers that must grow (an array that exists, or is given now): by
+    // half again at least, so a frame streamed in chunks reallocates rarely.
+    bool grow = false;
+    for (int k = 0; k < 4; ++k) grow |= (src[k] || *dst[k]) && end > g.cap[k];
+    if (grow) {
+        PRK_TRY(hipDeviceSynchronize());  // frames in flight and earlier writes read / fill the old buffers
+        for (int k = 0; k < 4; ++k) {
+            if (!(src[k] || *dst[k]) || end <= g.cap[k]) continue;
+            const uint64_t want = std::max<uint64_t>(end, (uint64_t)g.cap[k] + g.cap[k] / 2);
+            const uint32_t cap = (uint32_t)std::min<uint64_t>(want, 0xFFFFFFF0ull);
+            const size_t bytes = (size_t)cap * comp[k] * sizeof(float);
+            const size_t old = *dst[k] ? (size_t)g.cap[k] * comp[k] * sizeof(float) : 0;
+            float *d = nullptr;
+            PRK_TRY(hipMalloc((void **)&d, bytes));
+            hipError_t e = old ? hipMemcpy(d, *dst[k], old, hipMemcpyDeviceToDevice) : hipSuccess;
+            if (e == hipSuccess) e = hipMemset((uint8_t *)d + old, 0, bytes - old);
+            if (e != hipSuccess) {
+                (void)hipFree(d);
+                return status_of(e);
+            }
+            (void)hipFree((void *)*dst[k]);
+            *dst[k] = d;
+            g.cap[k] = cap;
+        }
+        for (auto &d : c->draws)
+            if (d.src_kind == 0 && d.geom == handle) {
+                d.V = g.V; d.C = g.C; d.N = g.N; d.UV = g.UV;
+            }
+        c->read_rec = false;  // the device is idle
+    }
+    if (c->read_rec) PRK_TRY(hipStreamWaitEvent(c->copy_stream, c->read_ev, 0));
+    bool any = false;
+    for (int k = 0; k < 4; ++k) {
+        if (!src[k] || !vertex_count) continue;
+        const size_t off = (size_t)first_vertex * comp[k];
+        PRK_TRY(hipMemcpyAsync((void *)(*dst[k] + off), src[k], (size_t)vertex_count * comp[k] * sizeof(float),
+                               hipMemcpyHostToDevice, c->copy_stream));
+        any = true;
+    }
+    if (any) {
+        PRK_TRY(hipEventRecord(c->in_ev, c->copy_stream));
+        c->in_wait = true;
+    }
+    g.vertex_count = end;
     return PRK_OK;
 }
 
@@ -1358,6 +1449,12 @@ int prk_flush(prk_context *c, void *stream) {
     }
     PRK_TRY(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->own_stream;
+    if (c->in_wait) {  // prk_geometry_write copies still in flight: every stream of the frame waits for them
+        PRK_TRY(hipStreamWaitEvent(s, c->in_ev, 0));
+        PRK_TRY(hipStreamWaitEvent(c->bin_stream, c->in_ev, 0));
+        PRK_TRY(hipStreamWaitEvent(c->vis_stream, c->in_ev, 0));
+        c->in_wait = false;
+    }
     bool any_avx = false;
     for (const auto &d : c->draws) any_avx |= d.mode == prk::MODE_AVX;
     if (any_avx && (c->W % 8)) return PRK_ERR_UNSUPPORTED;  // aligned 8-wide z load, projekt.cpp:2218
@@ -1403,6 +1500,8 @@ int prk_flush(prk_context *c, void *stream) {
         rc = obj ? flush_spans(c, s, seg, T, base) : flush_tris(c, s, seg, T, base);
         i = j;
     }
+    // the frame's last reader of the geometry (the flush stream ends every pass)
+    c->read_rec = hipEventRecord(c->read_ev, s) == hipSuccess;
     return rc;
 }
 

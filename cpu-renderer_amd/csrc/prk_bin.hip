@@ -108,54 +108,43 @@ __device__ __forceinline__ uint32_t range_entries(const TileRange &tr) {
 #endif
 constexpr int kRowClassBits = 3;
 
+// The setup record of triangle g of an all-AVX frame: FillEdgeTable +
+// MergeSort + the first row's AET insertions once per triangle (TriRec,
+// prk_device.h).
+__device__ __forceinline__ void make_rec(const FrameParams &fp, uint32_t g, TriRec &r) {
+    const DrawRec *d;
+    uint32_t gt;
+    resolve_draw(fp, g, d, gt);
+    Edge s0, s1, s2;
+    TriRaw<MODE_AVX> raw;
+    load_tri<MODE_AVX>(*d, gt, raw);
+    const int n = setup_from_raw<MODE_AVX>(raw, *d, fp, s0, s1, s2);
+    uint32_t anom = 0;
+    Walker<MODE_AVX, true> w;
+    w.init(n, s0, s1, s2, fp.H, fp.H, anom);
+    rec_edge_out(s0, r.e[0], r.ymin[0], r.ymax[0]);
+    rec_edge_out(s1, r.e[1], r.ymin[1], r.ymax[1]);
+    rec_edge_out(s2, r.e[2], r.ymin[2], r.ymax[2]);
+    // regular from its first row (RowWalker::regular): the binning groups
+    // such triangles together, so k_vis / k_walk waves take the one-event step
+    RowWalker<MODE_AVX, true> rw;
+    rw.from(w);
+    const bool reg = n >= 2 && rw.regular();
+    r.head = (uint32_t)n | (w.ord << 4) | ((uint32_t)w.cnt << 12) | ((uint32_t)(w.pend + 1) << 16) |
+             (min(anom, 15u) << 20) | ((d->flags & DRAW_ST) ? (1u << 24) : 0u) | (reg ? kHeadRegular : 0u);
+    r.vtx = (uint32_t)s0.Vtx | ((uint32_t)s1.Vtx << 4) | ((uint32_t)s2.Vtx << 8);
+    r.pad[0] = r.pad[1] = 0;
+}
+
 // Records leave through LDS: a wave's 64 records are written out as
-// consecutive 16-byte chunks (one coalesced store per 64 chunks) instead of
-// ten 160-byte-strided stores per lane.
+// consecutive 16-byte chunks (one coalesced store per 64 chunks when the
+// wave's triangles are consecutive) instead of ten 160-byte-strided stores
+// per lane.
 constexpr int kCountThreads = 256;
-__global__ void __launch_bounds__(kCountThreads) k_bin_count(FrameParams fp, uint32_t *__restrict__ tri_n,
-                                                              TileRange *__restrict__ ranges) {
-    __shared__ float4 stage[kCountThreads / 64][64 * 10];
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    bool rec = false;
-    TriRec r;
-    if (g < fp.tri_count) {
-        TileRange tr;
-        if (!tri_tile_range(fp, g, tr)) {
-            tr.tx0 = 1; tr.tx1 = 0; tr.ty0 = 1; tr.ty1 = 0; tr.oty0 = 1; tr.oty1 = 0;
-        }
-        ranges[g] = tr;
-        const uint32_t ne = range_entries(tr);
-        tri_n[g] = ne;
-        if (fp.trec && ne) {
-            // All-AVX frame: FillEdgeTable + MergeSort + the first row's AET
-            // insertions once per triangle (TriRec, prk_device.h).
-            const DrawRec *d;
-            uint32_t gt;
-            resolve_draw(fp, g, d, gt);
-            Edge s0, s1, s2;
-            TriRaw<MODE_AVX> raw;
-            load_tri<MODE_AVX>(*d, gt, raw);
-            const int n = setup_from_raw<MODE_AVX>(raw, *d, fp, s0, s1, s2);
-            uint32_t anom = 0;
-            Walker<MODE_AVX, true> w;
-            w.init(n, s0, s1, s2, fp.H, fp.H, anom);
-            rec_edge_out(s0, r.e[0], r.ymin[0], r.ymax[0]);
-            rec_edge_out(s1, r.e[1], r.ymin[1], r.ymax[1]);
-            rec_edge_out(s2, r.e[2], r.ymin[2], r.ymax[2]);
-            r.head = (uint32_t)n | (w.ord << 4) | ((uint32_t)w.cnt << 12) | ((uint32_t)(w.pend + 1) << 16) |
-                     (min(anom, 15u) << 20) | ((d->flags & DRAW_ST) ? (1u << 24) : 0u);
-            r.vtx = (uint32_t)s0.Vtx | ((uint32_t)s1.Vtx << 4) | ((uint32_t)s2.Vtx << 8);
-            r.pad[0] = r.pad[1] = 0;
-            rec = true;
-        }
-    } else if (g == fp.tri_count) {
-        tri_n[g] = 0;  // sentinel: a scan's last element is the total
-    }
+__device__ __forceinline__ void store_recs(const FrameParams &fp, float4 *st, bool rec, const TriRec &r, uint32_t g) {
+    const int lane = threadIdx.x & 63;
     const uint64_t mask = __ballot(rec);
     if (mask == 0) return;
-    const uint32_t gw = g - (uint32_t)lane;  // the wave's first triangle
-    float4 *st = stage[wv];
     auto wave_sync = [] {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -167,9 +156,74 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_count(FrameParams fp, uin
         for (int k = 0; k < 10; ++k) st[lane * 10 + k] = sr[k];
     }
     wave_sync();
-    float4 *dr = reinterpret_cast<float4 *>(fp.trec + gw);
-    for (int c = lane; c < 64 * 10; c += 64)
-        if ((mask >> (c / 10)) & 1) dr[c] = st[c];
+    for (int c = lane; c < 64 * 10; c += 64) {
+        const int src = c / 10;
+        const uint32_t gs = (uint32_t)__shfl((int)g, src);
+        if ((mask >> src) & 1) reinterpret_cast<float4 *>(fp.trec + gs)[c - src * 10] = st[c];
+    }
+    wave_sync();
+}
+
+// Band test, cull, tile range and entry count of every triangle, and (recs:
+// radix-sort binning) the setup records of the triangles with entries.  The
+// counting-sort path computes the records in k_setup_rec instead.
+__global__ void __launch_bounds__(kCountThreads) k_bin_count(FrameParams fp, uint32_t *__restrict__ tri_n,
+                                                              TileRange *__restrict__ ranges, bool recs) {
+    __shared__ float4 stage[kCountThreads / 64][64 * 10];
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int wv = threadIdx.x >> 6;
+    bool rec = false;
+    TriRec r;
+    if (g < fp.tri_count) {
+        TileRange tr;
+        if (!tri_tile_range(fp, g, tr)) {
+            tr.tx0 = 1; tr.tx1 = 0; tr.ty0 = 1; tr.ty1 = 0; tr.oty0 = 1; tr.oty1 = 0;
+        }
+        ranges[g] = tr;
+        const uint32_t ne = range_entries(tr);
+        tri_n[g] = ne;
+        rec = recs && fp.trec && ne;
+    } else if (g == fp.tri_count) {
+        tri_n[g] = 0;  // sentinel: a scan's last element is the total
+    }
+    if (!recs) return;
+    if (rec) make_rec(fp, g, r);
+    store_recs(fp, stage[wv], rec, r, g);
+}
+
+// The setup records of the triangles with entries, one workgroup per run of
+// kRecRun triangles: the run's triangles with entries are listed in LDS (in
+// triangle order, a workgroup scan per 256) and set up 64 per wave, so the
+// lanes stay full when few of them have entries — a row band's rank (C3b at
+// N = 8: with the records computed in k_bin_count, a wave holding a few of
+// the band's triangles ran the whole setup at a few lanes, 99 us of a
+// 0.30 ms band frame).
+constexpr uint32_t kRecRun = 2048;
+__device__ uint32_t cs_block_excl_scan(uint32_t v, uint32_t *scratch, uint32_t &total);
+__global__ void __launch_bounds__(kCountThreads) k_setup_rec(FrameParams fp, const uint32_t *__restrict__ tri_n) {
+    __shared__ float4 stage[kCountThreads / 64][64 * 10];
+    __shared__ uint32_t list[kRecRun];
+    __shared__ uint32_t scratch[kCountThreads / 64];
+    const uint32_t g0 = blockIdx.x * kRecRun;
+    uint32_t n = 0;
+    for (uint32_t k = 0; k < kRecRun; k += kCountThreads) {
+        const uint32_t g = g0 + k + threadIdx.x;
+        const uint32_t f = g < fp.tri_count && tri_n[g] != 0 ? 1u : 0u;
+        uint32_t tot;
+        const uint32_t pos = cs_block_excl_scan(f, scratch, tot);
+        if (f) list[n + pos] = g;
+        n += tot;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint32_t b = (uint32_t)wv * 64; b < n; b += kCountThreads) {
+        const uint32_t i = b + lane;
+        const bool rec = i < n;
+        const uint32_t g = rec ? list[i] : 0u;
+        TriRec r;
+        if (rec) make_rec(fp, g, r);
+        store_recs(fp, stage[wv], rec, r, g);
+    }
 }
 
 // Sort key = tile << kRowClassBits | row class: within a tile's bin the
@@ -263,7 +317,11 @@ constexpr uint32_t kCsMaxTiles = 32768;  // LDS: one u32 per tile (128 KiB)
                         // tile (its replay length); measured k_vis +6 % on C3b (0.497 -> 0.528 ms)
 #endif
 constexpr int kRepClassBits = PRK_REPCLASS ? 2 : 0;
-constexpr int kClassBits = kRowClassBits + kRepClassBits;
+#ifndef PRK_REGCLASS
+#define PRK_REGCLASS 2  // bins also grouped by regularity (TriRec kHeadRegular): irregular lists last
+#endif
+constexpr int kRegClassBits = PRK_REGCLASS ? 1 : 0;
+constexpr int kClassBits = kRowClassBits + kRepClassBits + kRegClassBits;
 constexpr uint32_t kCsClassShift = 32 - kClassBits;  // (replay, row) class in the top bits of the emitted pair index
 constexpr uint32_t kCsPairMask = (1u << kCsClassShift) - 1u;
 constexpr int kCsClassWindow = 2048;     // k_cs_class: entries grouped per pass
@@ -427,6 +485,21 @@ __global__ void __launch_bounds__(kCsThreads) k_cs_scan(const uint32_t *__restri
     }
 }
 
+// Workgroup b runs on XCD b % 8 (round-robin dispatch); XCD x takes the
+// contiguous chunks [start(x), start(x+1)), so inside a tile's bin the
+// entries one XCD writes are contiguous and its L2 merges them into whole
+// lines (consecutive chunks on different XCDs left every line of a bin
+// written partially by several L2s: 169 MB written for ~70 MB of data).
+#ifndef PRK_CS_XCD
+#define PRK_CS_XCD 1
+#endif
+__device__ __forceinline__ uint32_t xcd_chunk(uint32_t b, uint32_t n) {
+    if (!PRK_CS_XCD) return b;
+    constexpr uint32_t kXcds = 8;
+    const uint32_t q = n / kXcds, r = n % kXcds, x = b % kXcds;
+    return x * q + min(x, r) + b / kXcds;
+}
+
 __global__ void __launch_bounds__(kCsThreads) k_cs_emit(FrameParams fp, const TileRange *__restrict__ ranges,
                                                          const uint32_t *__restrict__ tri_n,
                                                          const uint32_t *__restrict__ ghist,
@@ -438,7 +511,7 @@ __global__ void __launch_bounds__(kCsThreads) k_cs_emit(FrameParams fp, const Ti
                                                          uint32_t won_stride, uint8_t *__restrict__ trwon) {
     extern __shared__ uint32_t cur[];
     __shared__ uint32_t scratch[kCsThreads / 64];
-    const uint32_t c = blockIdx.x;
+    const uint32_t c = xcd_chunk(blockIdx.x, gridDim.x);
     const bool over = info[1] != 0;
     if (!over) {
         const uint32_t *gh = ghist + (size_t)c * ntiles;
@@ -459,9 +532,14 @@ __global__ void __launch_bounds__(kCsThreads) k_cs_emit(FrameParams fp, const Ti
         if (!n) continue;
         const TileRange tr = ranges[g];
         uint32_t j = j0;
+        // irregular lists after the regular ones (k_vis walks a wave of
+        // regular lists with the one-event row step)
+        // (PRK_REGCLASS 1: as the top class bit; 2: the lowest, inside each row class)
+        const uint32_t irr = PRK_REGCLASS && fp.trec && !(fp.trec[g].head & kHeadRegular) ? 1u : 0u;
         for_each_entry(fp, tr, [&](uint32_t tile, uint32_t cls) {
             const uint32_t pos = atomicAdd(&cur[tile], 1u);
-            bins[pos] = make_uint2(g, j | (cls << kCsClassShift));
+            const uint32_t c = PRK_REGCLASS == 2 ? (cls << 1) | irr : cls | (irr << (kRowClassBits + kRepClassBits));
+            bins[pos] = make_uint2(g, j | (c << kCsClassShift));
             pair_tri[j] = g;
             clear_won(won, won_stride, j);
             ++j;
@@ -533,7 +611,8 @@ hipError_t prk_bin_phase1(const prk::FrameParams *fp, uint32_t *tri_n, uint32_t 
     const uint32_t n = fp->tri_count + 1;
     if (!temp) return hipcub::DeviceScan::ExclusiveSum(nullptr, *temp_bytes, tri_n, scan_out, n, s);
     hipLaunchKernelGGL(prk::k_bin_count, dim3((n + prk::kCountThreads - 1) / prk::kCountThreads),
-                       dim3(prk::kCountThreads), 0, s, *fp, tri_n, reinterpret_cast<prk::TileRange *>(ranges));
+                       dim3(prk::kCountThreads), 0, s, *fp, tri_n, reinterpret_cast<prk::TileRange *>(ranges),
+                       true);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, tri_n, scan_out, n, s);
@@ -578,10 +657,17 @@ hipError_t prk_bin_phase2(const prk::FrameParams *fp, const void *ranges, const 
 // info[0] = entry count, info[1] = overflow (count > cap: bins left empty,
 // no pair written; the caller re-runs the frame with more room).
 // ghist: nchunks * ntiles u32; tile_tot: ntiles; chunk_tot / chunk_base: nchunks.
+// All-AVX frames (fp->trec): the setup records are computed by k_setup_rec.
 hipError_t prk_bin_count(const prk::FrameParams *fp, uint32_t *tri_n, void *ranges, hipStream_t s) {
     const uint32_t n = fp->tri_count + 1;
+    // A whole-frame target sets up (nearly) every triangle: inline records
+    // (C3b: 76 us against 22 + 68 us split); a row band only its own.
+    const bool band = fp->row0 > 0 || fp->row1 < fp->H;
     hipLaunchKernelGGL(prk::k_bin_count, dim3((n + prk::kCountThreads - 1) / prk::kCountThreads),
-                       dim3(prk::kCountThreads), 0, s, *fp, tri_n, reinterpret_cast<prk::TileRange *>(ranges));
+                       dim3(prk::kCountThreads), 0, s, *fp, tri_n, reinterpret_cast<prk::TileRange *>(ranges), !band);
+    if (band && fp->trec && fp->tri_count)
+        hipLaunchKernelGGL(prk::k_setup_rec, dim3((fp->tri_count + prk::kRecRun - 1) / prk::kRecRun),
+                           dim3(prk::kCountThreads), 0, s, *fp, tri_n);
     return hipGetLastError();
 }
 

@@ -97,11 +97,12 @@ struct TriRec {
     float e[3][10];      // sorted edge k: X, G, Z, ZG, W, WG, U, UG, V, VG
     int32_t ymin[3];     // YMin | Left << 31 (YMin >= 0: Maximum(0, .), 3999)
     int32_t ymax[3];
-    uint32_t head;       // n | ord << 4 | cnt << 12 | (pend + 1) << 16 | anomaly << 20 | st << 24
+    uint32_t head;       // n | ord << 4 | cnt << 12 | (pend + 1) << 16 | anomaly << 20 | st << 24 | regular << 25
     uint32_t vtx;        // sorted edge k's Vtx (mi | ma << 2) at bits 4k
     uint32_t pad[2];
 };
 static_assert(sizeof(TriRec) == 160, "TriRec is ten dwordx4");
+constexpr uint32_t kHeadRegular = 1u << 25;  // TriRec::head: the list is regular from the first row
 
 struct FrameParams {
     // projective_transform
@@ -265,10 +266,42 @@ __device__ __forceinline__ float div_focal(const FrameParams &fp, float d) {
     return q[0];
 }
 
+// sqrtf for x in [2^-96, FLT_MAX]: the compiler's correctly rounded f32
+// sqrt (denormals on) is v_sqrt_f32 plus a one-ulp correction from the two
+// neighbours' residuals, wrapped in a 2^32 pre-scale for x < 2^-96 and a
+// zero / +inf pass-through; in this range both wrappers are identities, so
+// this is the same value bit for bit (prk_selftest_div checks it).
+__device__ __forceinline__ float sqrt_mid(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float dn = __int_as_float(__float_as_int(s) - 1), up = __int_as_float(__float_as_int(s) + 1);
+    const float vp = __builtin_fmaf(-dn, s, x), vs = __builtin_fmaf(-up, s, x);
+    float r = vp <= 0.0f ? dn : s;
+    r = vs > 0.0f ? up : r;
+    return r;
+}
+
 // NormalizeVector_8x (projekt.cpp:603-620), one lane: division form (three
-// quotients over one length).
+// quotients over one length).  Fast path (wave-uniform, as div_all): the
+// squared length in [2^-64, 2^62] puts the length in [2^-32, 2^31] (sqrt is
+// correctly rounded and monotone) and every |component| below 2^32, so the
+// sqrt wrappers and the division's scale / fixup steps are identities.
+#ifndef PRK_FAST_NORM
+#define PRK_FAST_NORM 1
+#endif
 __device__ __forceinline__ void normalize_div(float &x, float &y, float &z) {
-    const float len = sqrtf((x * x + y * y) + z * z);
+    const float d = (x * x + y * y) + z * z;
+    if (PRK_SHARED_DIV && PRK_FAST_NORM) {
+        const float mn = fminf(fminf(fabsf(x), fabsf(y)), fabsf(z));
+        const bool ok = d >= 0x1p-64f && d <= 0x1p62f && mn >= 0x1p-80f;
+        if (__builtin_expect(__all(ok), 1)) {
+            const DivBy s = div_by(sqrt_mid(d));
+            x = div_fast(s, x);
+            y = div_fast(s, y);
+            z = div_fast(s, z);
+            return;
+        }
+    }
+    const float len = sqrtf(d);
     float q[3] = {x, y, z};
     div_all(len, q);
     x = q[0];
@@ -916,6 +949,39 @@ struct RowWalker {
         cnt = (int)k0 + (int)k1 + (int)k2;
         // Pairing (3751-3869): one pair; a third entry stays unpaired.
         return cnt >= 2;
+    }
+
+    // A REGULAR list (regular(), decided per lane after the replay of the
+    // rows above): the rows left hold exactly one event — at row Mid =
+    // S2.YMin the pending edge is inserted and exactly one edge of the pair
+    // (S0, S1) expires; before Mid no edge expires, after it none before
+    // MaxY.  Insertion (3654-3713) then expiry (3715-3749) reduce to: the
+    // survivor of the pair, and S2 first iff it goes before S0, or S0 expires
+    // and it goes before S1.  The general begin_row moves all three edges
+    // through selects on such rows (≈ 120 VALU in k_vis) and runs its expiry
+    // test on every row; a wave of regular lists skips both.
+    __device__ __forceinline__ bool regular() const {
+        if (Row >= MaxY) return true;  // nothing left to walk
+        if (cnt != 2) return false;
+        const int32_t y0 = S0.YMax, y1 = S1.YMax;
+        const int32_t mid = pend ? S2.YMin : 0x7fffffff;
+        bool ok = mid >= Row && min(y0, y1) >= min(mid, MaxY);  // rows [Row, Mid): no expiry
+        if (pend && mid < MaxY) {  // row Mid: exactly one of the pair ends; then none before MaxY
+            const bool e0 = y0 <= mid, e1 = y1 <= mid;
+            ok = ok && (e0 != e1) && S2.YMax > mid && min(e0 ? y1 : y0, S2.YMax) >= MaxY;
+        }
+        return ok;
+    }
+    __device__ __forceinline__ bool begin_row_regular() {
+        if (pend && S2.YMin == Row) {
+            const bool aexp = S0.YMax <= Row;
+            const bool cfirst = insert_before(S2, S0) || (aexp && insert_before(S2, S1));
+            const Edge sv = sel(aexp, S1, S0);
+            S0 = sel(cfirst, S2, sv);
+            S1 = sel(cfirst, sv, S2);
+            pend = false;
+        }
+        return true;
     }
 
     // Edge step of the pair (3811-3829) and the crossing swap (3831-3841 + P3).

@@ -50,12 +50,15 @@ _SIGS = {
     "prk_target_clear_on_flush": (C.c_int, [C.c_void_p, C.c_uint32, C.c_float]),
     "prk_target_download": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
     "prk_target_upload": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
+    "prk_target_upload_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
     "prk_set_camera": (C.c_int, [C.c_void_p, C.POINTER(abi.PrkTransform), C.POINTER(abi.PrkLightData)]),
     "prk_texture_create": (C.c_int, [C.c_void_p, C.POINTER(abi.PrkBitmap), C.POINTER(C.c_int32)]),
     "prk_texture_set_filter": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     "prk_texture_update": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(abi.PrkBitmap)]),
     "prk_geometry_update": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_uint32]),
+    "prk_geometry_write": (C.c_int, [C.c_void_p, C.c_int32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_void_p]),
     "prk_host_alloc": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
     "prk_host_free": (C.c_int, [C.c_void_p, C.c_void_p]),
     "prk_host_register": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
@@ -342,6 +345,19 @@ class Renderer:
                 for a in (vertices, colors, normals, uvs)]
         _check("prk_geometry_update", self._L.prk_geometry_update(self._h, handle, *[_ptr(a) for a in arrs],
                                                                   arrs[0].shape[0]))
+
+    def geometry_write(self, handle, first_vertex, vertices=None, colors=None, normals=None, uvs=None,
+                       count=None):
+        """prk_geometry_write of vertices [first_vertex, first_vertex+count)
+        (count: the given arrays' length); waits for the copy, since the
+        arrays here are temporaries."""
+        arrs = [None if a is None else np.ascontiguousarray(a, np.float32)
+                for a in (vertices, colors, normals, uvs)]
+        if count is None:
+            count = next(a.shape[0] for a in arrs if a is not None)
+        _check("prk_geometry_write", self._L.prk_geometry_write(self._h, handle, first_vertex, count,
+                                                                *[_ptr(a) for a in arrs]))
+        self.synchronize()
 
     def set_filter(self, texture, filt):
         """Texture sampling: PRK_FILTER_NEAREST (the reference's) or

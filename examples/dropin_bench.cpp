@@ -89,7 +89,7 @@ int main(int argc, char **argv) {
     std::printf("{\"workload\": \"C3b through include/projekt.h: %u per-triangle objects, %dx%d\", \"modes\": {", T, W, H);
     for (int m = 0; m < 2; ++m) {
         const bool clear = m == 1;
-        double calls = 0, complete = 0, total = 0, gpu = 0;
+        double calls = 0, complete = 0, total = 0, gpu = 0, issue = 0, flush = 0, down = 0;
         int timed = 0;
         for (int f = 0; f < frames + 1; ++f) {
             // the caller's own clear of its buffers (both modes: the reference caller does it)
@@ -126,15 +126,41 @@ int main(int argc, char **argv) {
                 complete += tw;
                 total += tt;
                 gpu += st.frames_timed ? (st.sum_ms_raster + st.sum_ms_bin) / st.frames_timed : 0.0;
+                issue += prk_dropin::S().LastIssueMs;
+                flush += prk_dropin::S().LastFlushMs;
+                down += prk_dropin::S().LastDownloadMs;
                 ++timed;
             }
         }
         std::printf("%s\"%s\": {\"frame_ms\": %.3f, \"host_calls_ms\": %.3f, \"complete_all_work_ms\": %.3f, "
-                    "\"gpu_bin_plus_raster_ms\": %.3f, \"mpixels_s\": %.1f}",
+                    "\"complete_split_ms\": {\"record_draws_and_tail\": %.3f, \"queue_frame\": %.3f, "
+                    "\"wait_and_download\": %.3f}, \"gpu_bin_plus_raster_ms\": %.3f, \"mpixels_s\": %.1f}",
                     m ? ", " : "", clear ? "clear" : "upload", total / timed, calls / timed, complete / timed,
-                    gpu / timed, (double)W * H / (total / timed * 1e-3) / 1e6);
+                    issue / timed, flush / timed, down / timed, gpu / timed,
+                    (double)W * H / (total / timed * 1e-3) / 1e6);
     }
-    std::printf("}, \"frames\": %d}\n", frames);
+    // The host calls split: frames of FillEdgeTable calls alone.
+    double fill = 0;
+    for (int f = 0; f < frames + 1; ++f) {
+        const auto t1 = clk::now();
+        for (u32 t = 0; t < T; ++t) {
+            render_entry_3d_object Object = {};
+            Object.VertexCount = 3;
+            Object.PhongShading = 1;
+            Object.VertexData = &V[3 * (size_t)t];
+            Object.ColorData = &C[3 * (size_t)t];
+            Object.NormalData = &N[3 * (size_t)t];
+            Object.UVData = &UV[3 * (size_t)t];
+            Object.EdgeMemory = EdgeMemory.data();
+            Object.Bitmap = &Texture;
+            (void)FillEdgeTable(&Object, &Commands, 1);
+        }
+        if (f > 0) fill += ms_since(t1);
+        // nothing was drawn (no frame is open): drop the frame's objects
+        prk_synchronize(prk_dropin::S().Ctx);
+        prk_dropin::end_frame(prk_dropin::S());
+    }
+    std::printf("}, \"fill_edge_table_only_ms\": %.3f, \"frames\": %d}\n", fill / frames, frames);
     PRK_Shutdown();
     return 0;
 }

@@ -21,8 +21,11 @@
  * projekt.cpp:2327), and crashes on several ordinary inputs;
  * here those inputs are rejected with a status code instead.
  *
- * Semantics: every triangle is its own AET, submitted in index
- * order and sharing one z-buffer ("per-triangle submission").
+ * Semantics: prk_draw submits every triangle as its own AET
+ * (one render_entry_3d_object per triangle, "per-triangle submission", SURVEY
+ * §0.6); prk_draw_objects submits objects of several triangles, each one AET
+ * as FillEdgeTable + DrawModel* build it.  Draws run in submission order and
+ * share one z-buffer.
  */
 #ifndef PRK_H
 #define PRK_H
@@ -93,8 +96,9 @@ typedef struct prk_light_data {
 } prk_light_data;
 
 /* loaded_bitmap (absent header): 0xAARRGGBB texels, Pitch in bytes.  For a
- * texture, Memory must hold Height+1 rows: the extra zeroed "guard" row is
- * what the reference's u==1 / v==1 over-read lands on. */
+ * texture, Memory holds Height rows; the library appends the zeroed "guard"
+ * row the reference's u==1 / v==1 over-read lands on (SURVEY App. A.2.3,
+ * prk_texture_create below). */
 typedef struct prk_bitmap {
     void *Memory;
     int32_t Width;
@@ -160,6 +164,12 @@ int prk_target_download(prk_context *ctx, uint32_t *color_host, int32_t host_pit
                         float *z_host);
 int prk_target_upload(prk_context *ctx, const uint32_t *color_host, int32_t host_pitch_bytes,
                       const float *z_host);
+/* prk_target_upload on the context's copy stream: returns at once; the next
+ * prk_flush's kernels wait for it.  The host buffers must be page-locked
+ * (prk_host_register) and stay unchanged until prk_target_download or
+ * prk_synchronize returns (the drop-in sends the caller's framebuffer this
+ * way at a frame's first draw, so the copy overlaps the caller's calls). */
+int prk_target_upload_async(prk_context *ctx, const uint32_t *color_host, int32_t host_pitch, const float *z_host);
 
 /* Pinned host memory for staging (prk_host_alloc / prk_host_free), and
  * page-locking of caller memory (a framebuffer, a z-buffer) so uploads and
@@ -190,10 +200,23 @@ int prk_geometry_create(prk_context *ctx, const float *vertices, const float *co
                         const float *normals, const float *uvs, uint32_t vertex_count,
                         int32_t *handle_out);
 /* New contents for a library-owned geometry (grows its buffers if needed);
- * an array passed as NULL keeps its previous contents (and must not be read
- * past them); draws already recorded read the new contents. */
+ * an array passed as NULL keeps its previous contents (vertices past them
+ * read as zero); draws already recorded read the new contents.  Waits for
+ * frames in flight; synchronous. */
 int prk_geometry_update(prk_context *ctx, int32_t handle, const float *vertices, const float *colors,
                         const float *normals, const float *uvs, uint32_t vertex_count);
+/* Asynchronous partial update: vertices [first_vertex, first_vertex +
+ * vertex_count) of the arrays given (NULL: that array unchanged there) are
+ * copied on the context's copy stream, after the frames already flushed have
+ * read the geometry and before the next prk_flush's kernels read it.  The
+ * geometry's vertex count becomes first_vertex + vertex_count; buffers grow
+ * (kept contents, zeros past them) when needed, which waits for the device.
+ * The host arrays must be page-locked (prk_host_alloc / prk_host_register)
+ * and stay unchanged until prk_synchronize or prk_target_download returns.
+ * The drop-in streams FillEdgeTable's vertices this way while the caller is
+ * still submitting objects.  first_vertex and vertex_count are multiples of 3. */
+int prk_geometry_write(prk_context *ctx, int32_t handle, uint32_t first_vertex, uint32_t vertex_count,
+                       const float *vertices, const float *colors, const float *normals, const float *uvs);
 /* Same as prk_geometry_create, but from device pointers the caller keeps
  * alive (no copy). */
 int prk_geometry_wrap_device(prk_context *ctx, const float *vertices, const float *colors,
@@ -213,8 +236,10 @@ int prk_draw(prk_context *ctx, int32_t geometry, uint32_t first_tri, uint32_t tr
  * edge table, as FillEdgeTable + DrawModelOptimized(RenderQueue,...) build it
  * (projekt.cpp:3894-4117, 3654-3869), so spans pair edges of different
  * triangles of the object.  tris_per_object == 1 is prk_draw.  Objects of
- * more than one triangle are supported for PRK_SEM_AVX / PRK_SEM_AVX_ST
- * (PRK_ERR_UNSUPPORTED for PRK_SEM_SCALAR). */
+ * more than one triangle are supported for every semantics (DrawModel's
+ * AET, 162-601, has the same list logic).  PRK_ERR_UNSUPPORTED: an object of
+ * 2^22 edges or more, or one whose active edge list exceeds 4096 edges on a
+ * row (the one-wave walk keeps the list in LDS). */
 int prk_draw_objects(prk_context *ctx, int32_t geometry, uint32_t first_tri, uint32_t tri_count,
                      uint32_t tris_per_object, const float P[3], int32_t semantics, int32_t phong,
                      int32_t texture);
@@ -222,10 +247,10 @@ int prk_draw_objects(prk_context *ctx, int32_t geometry, uint32_t first_tri, uin
 /* edge_info (projekt.h:17-37) without its list pointer: what the reference's
  * FillEdgeTable leaves in EdgeMemory and DrawModel* walk.  prk_draw_edges
  * draws one object from such a list, already sorted by YMin as FillEdgeTable
- * leaves it, exactly as DrawModelOptimized(RenderQueue,...) (3615-3871) or
- * the single-thread overload (2350-3358) walks it.  Supported for
- * PRK_SEM_AVX / PRK_SEM_AVX_ST; the winner id of its pixels is the draw's
- * position in the frame's triangle numbering (it counts as one). */
+ * leaves it, exactly as DrawModelOptimized(RenderQueue,...) (3615-3871), the
+ * single-thread overload (2350-3358) or DrawModel (162-601, PRK_SEM_SCALAR)
+ * walks it.  The winner id of its pixels is the draw's position in the
+ * frame's triangle numbering (it counts as one). */
 typedef struct prk_edge {
     int32_t YMax;
     float XMin, ZMin, OneOverZMin, Gradient, ZGradient, OneOverZGradient;

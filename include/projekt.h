@@ -17,7 +17,8 @@
 // and links libprk_hip.so.  What each entry point does here:
 //  * FillEdgeTable copies the object's VertexData / ColorData / NormalData /
 //    UVData as they are at the call (the reference reads them there,
-//    3898-3925) into the frame's pinned staging arena, snapshots
+//    3898-3925) into the frame's pinned staging arena (sent on to the GPU in
+//    chunks of 64K triangles while the caller keeps submitting), snapshots
 //    Commands->Transform and LightData as they are at the call (3885,
 //    3907-3909, 4022-4061), and leaves a token in Object->EdgeMemory that
 //    DrawModel* read back; the setup itself (projection, cull, edges,
@@ -37,8 +38,8 @@
 //    that list as is (prk_draw_edges).  The work-queue callbacks draw the
 //    spans of their work records (prk_draw_spans) or, for DoModelRenderWork,
 //    the object (single-thread overload).
-//  * PRK_CompleteAllWork (the absent platform's CompleteAllWork) uploads the
-//    frame's geometry, runs every recorded draw in order on the GPU and copies
+//  * PRK_CompleteAllWork (the absent platform's CompleteAllWork) sends the
+//    geometry's last chunk, runs every recorded draw in order on the GPU and copies
 //    colour and z back into Buffer->Memory and Commands->ZBuffer.  The device
 //    target is allocated once per size; the caller's framebuffer and z-buffer
 //    are page-locked once, so the prior contents go up (draws z-test against
@@ -60,8 +61,10 @@
 #define PRK_PROJEKT_H
 
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <map>
 #include <set>
 #include <vector>
@@ -209,6 +212,10 @@ struct pending_draw {
     uint32_t First, Count;  // object index / range of Edges / range of Spans
     int32_t Semantics, Phong, Texture;
     uint32_t Camera;        // index into the frame's cameras
+    // DRAW_OBJECT: Count objects drawn alike, consecutive in the arena, of
+    // one size and offset, RunTris triangles in all: one library call (the
+    // per-triangle objects of a reference caller make one run per frame)
+    uint32_t RunTris;
 };
 
 struct state {
@@ -218,6 +225,13 @@ struct state {
     // frame geometry: pinned staging arena (vertices), uploaded at CompleteAllWork
     float *AV = nullptr, *AC = nullptr, *AN = nullptr, *AUV = nullptr;
     uint32_t ArenaCap = 0, ArenaUsed = 0;  // vertices
+    // vertices [0, Uploaded) of the frame are on their way to every device
+    // (prk_geometry_write), sent in chunks while the caller submits objects
+    uint32_t Uploaded = 0;
+    int PushStatus = PRK_OK;               // the frame's first failed chunk write
+    // host time of the last PRK_CompleteAllWork: recording the draws (and the
+    // geometry tail), queueing the frames, waiting + downloading (ms)
+    double LastIssueMs = 0, LastFlushMs = 0, LastDownloadMs = 0;
     int32_t Geom = -1;
     std::vector<frame_object> Objects;
     std::vector<pending_draw> Draws;
@@ -276,6 +290,8 @@ inline bool arena_reserve(state &st, uint32_t more) {
     float *old[4] = {st.AV, st.AC, st.AN, st.AUV};
     for (int k = 0; k < 4; ++k)
         if (old[k]) memcpy(p[k], old[k], (size_t)st.ArenaUsed * comp[k] * sizeof(float));
+    if (st.Uploaded)  // chunk copies may still read the old arena
+        for (prk_context *c : st.Ctxs) prk_synchronize(c);
     free_arena(st);
     st.AV = (float *)p[0];
     st.AC = (float *)p[1];
@@ -293,6 +309,48 @@ inline int each(F &&f) {
         if (rc != PRK_OK) return rc;
     }
     return PRK_OK;
+}
+
+// Arena vertices [Uploaded, ArenaUsed) to every device: positions, normals
+// and uvs, asynchronously on each context's copy stream, so PCIe runs while
+// the caller is still submitting objects and PRK_CompleteAllWork waits for
+// the tail only.  Colours reach the output only through DrawModel (scalar)
+// (the FillLineOptimized paths replace them by the texel, 2029-2032): they
+// go at issue(), for frames with scalar draws.  The first push ever creates
+// the geometry (synchronously, colours included).
+// Chunk size in triangles: PRK_DROPIN_CHUNK_TRIS (0: everything at
+// PRK_CompleteAllWork, the round-2 behaviour), default 65536.
+inline uint32_t chunk_vertices() {
+    static const uint32_t v = [] {
+        const char *e = std::getenv("PRK_DROPIN_CHUNK_TRIS");
+        const long t = e ? std::atol(e) : 65536L;
+        return t > 0 && t < (1L << 28) ? 3u * (uint32_t)t : 0xFFFFFFFFu;
+    }();
+    return v;
+}
+inline int push_vertices(state &st) {
+    if (st.ArenaUsed == st.Uploaded) return PRK_OK;
+    const uint32_t a = st.Uploaded, n = st.ArenaUsed - a;
+    int rc;
+    if (st.Geom < 0) {
+        int32_t g = -1;
+        rc = each([&](prk_context *c) {
+            int32_t gc = -1;
+            const int r = prk_geometry_create(c, st.AV, st.AC, st.AN, st.AUV, st.ArenaUsed, &gc);
+            if (r == PRK_OK && g >= 0 && gc != g) return (int)PRK_ERR_ARG;
+            g = gc;
+            return r;
+        });
+        if (rc == PRK_OK) st.Geom = g;
+    } else {
+        rc = each([&](prk_context *c) {
+            return prk_geometry_write(c, st.Geom, a, n, st.AV + 3 * (size_t)a, nullptr, st.AN + 3 * (size_t)a,
+                                      st.AUV + 2 * (size_t)a);
+        });
+    }
+    if (rc == PRK_OK) st.Uploaded = st.ArenaUsed;
+    else if (st.PushStatus == PRK_OK) st.PushStatus = rc;
+    return rc;
 }
 
 // f(ctx, first colour byte, first z float) of every band's rows of the
@@ -361,8 +419,32 @@ inline camera camera_of(const game_render_commands *Commands) {
 
 // The frame's camera index of a snapshot: the last one when unchanged (the
 // usual frame has one), else a new entry.
-inline uint32_t camera_id(state &st, const camera &k) {
-    if (st.Cameras.empty() || memcmp(&st.Cameras.back(), &k, sizeof k) != 0) st.Cameras.push_back(k);
+inline bool same_bits(float a, float b) {
+    uint32_t x, y;
+    memcpy(&x, &a, 4);
+    memcpy(&y, &b, 4);
+    return x == y;
+}
+// k == camera_of(Commands), bit for bit, without building the snapshot (the
+// drop-in asks once per FillEdgeTable call).
+inline bool camera_is(const camera &k, const game_render_commands *C) {
+    const auto &T = C->Transform;
+    if (!same_bits(k.T.DistanceAboveTarget, T.DistanceAboveTarget) || !same_bits(k.T.FocalLength, T.FocalLength) ||
+        !same_bits(k.T.MetersToPixels, T.MetersToPixels) || !same_bits(k.T.ScreenCenter[0], T.ScreenCenter.x) ||
+        !same_bits(k.T.ScreenCenter[1], T.ScreenCenter.y) || k.L.LightCount != C->LightData.LightCount)
+        return false;
+    for (int c = 0; c < 4; ++c)
+        if (!same_bits(k.L.AmbientIntensity[c], C->LightData.AmbientIntensity.E[c])) return false;
+    for (u32 i = 0; i < k.L.LightCount && i < PRK_MAX_LIGHTS; ++i) {
+        for (int c = 0; c < 3; ++c)
+            if (!same_bits(k.L.Lights[i].P[c], C->LightData.Lights[i].P.E[c])) return false;
+        for (int c = 0; c < 4; ++c)
+            if (!same_bits(k.L.Lights[i].Intensity[c], C->LightData.Lights[i].Intensity.E[c])) return false;
+    }
+    return true;
+}
+inline uint32_t camera_id(state &st, const game_render_commands *C) {
+    if (st.Cameras.empty() || !camera_is(st.Cameras.back(), C)) st.Cameras.push_back(camera_of(C));
     return (uint32_t)st.Cameras.size() - 1;
 }
 
@@ -410,10 +492,16 @@ inline bool open_frame(loaded_bitmap *Buffer, game_render_commands *Commands) {
         if (!ok(each([&](prk_context *c) { return prk_target_clear_on_flush(c, st.ClearColor, st.ClearZ); })))
             return false;
         st.ClearNext = false;
-    } else if (!ok(each_band(Buffer, Commands, [&](prk_context *c, uint8_t *col, float *z) {
-                   return prk_target_upload(c, (const uint32_t *)col, Buffer->Pitch, z);
-               }))) {
-        return false;
+    } else {
+        // the prior contents go up on the copy stream while the caller keeps
+        // submitting (page-locked buffers; else a synchronous upload)
+        const bool pinned = st.Registered.count(Buffer->Memory) &&
+                            (!Commands->ZBuffer || st.Registered.count(Commands->ZBuffer));
+        if (!ok(each_band(Buffer, Commands, [&](prk_context *c, uint8_t *col, float *z) {
+                return pinned ? prk_target_upload_async(c, (const uint32_t *)col, Buffer->Pitch, z)
+                              : prk_target_upload(c, (const uint32_t *)col, Buffer->Pitch, z);
+            })))
+            return false;
     }
     st.Target = Buffer;
     st.Commands = Commands;
@@ -452,7 +540,7 @@ inline void draw(loaded_bitmap *Buffer, edge_info *Edges, u32 EdgeCount, game_re
     }
     object_token tok;
     memcpy(&tok, Edges, sizeof tok);
-    pending_draw d;
+    pending_draw d{};
     d.Semantics = semantics;
     d.Phong = PhongShading ? 1 : 0;
     d.Texture = tex;
@@ -460,10 +548,25 @@ inline void draw(loaded_bitmap *Buffer, edge_info *Edges, u32 EdgeCount, game_re
         d.Kind = DRAW_OBJECT;
         d.First = tok.Object;
         d.Count = 1;
-        d.Camera = st.Objects[tok.Object].Camera;  // as FillEdgeTable saw it
-        if (st.Objects[tok.Object].Tris == 0) return;  // FillEdgeTable wrote no edge: nothing to draw
+        const frame_object &o = st.Objects[tok.Object];
+        d.Camera = o.Camera;  // as FillEdgeTable saw it
+        d.RunTris = o.Tris;
+        if (o.Tris == 0) return;  // FillEdgeTable wrote no edge: nothing to draw
+        if (!st.Draws.empty()) {  // the next object of the previous draw's run
+            pending_draw &b = st.Draws.back();
+            if (b.Kind == DRAW_OBJECT && b.Semantics == d.Semantics && b.Phong == d.Phong &&
+                b.Texture == d.Texture && b.Camera == d.Camera) {
+                const frame_object &f = st.Objects[b.First];
+                if (o.FirstTri == f.FirstTri + b.RunTris && o.Tris == f.Tris && memcmp(o.P, f.P, sizeof o.P) == 0) {
+                    ++b.Count;
+                    b.RunTris += o.Tris;
+                    st.LastStatus = PRK_OK;
+                    return;
+                }
+            }
+        }
     } else {  // a caller's own edge_info list, drawn as given
-        d.Camera = camera_id(st, camera_of(Commands));
+        d.Camera = camera_id(st, Commands);
         d.Kind = DRAW_EDGES;
         d.First = (uint32_t)st.Edges.size();
         d.Count = EdgeCount;
@@ -479,14 +582,14 @@ inline void draw_spans(loaded_bitmap *Buffer, game_render_commands *Commands, lo
     state &st = S();
     if (!st.Ctx || n == 0) return;
     if (!open_frame(Buffer, Commands)) return;
-    pending_draw d;
+    pending_draw d{};
     d.Kind = DRAW_SPANS;
     d.First = (uint32_t)st.Spans.size();
     d.Count = n;
     d.Semantics = PRK_SEM_AVX;
     d.Phong = PhongShading ? 1 : 0;
     d.Texture = Bitmap ? texture_for(Bitmap) : -1;
-    d.Camera = camera_id(st, camera_of(Commands));
+    d.Camera = camera_id(st, Commands);
     st.Spans.insert(st.Spans.end(), spans, spans + n);
     st.Draws.push_back(d);
 }
@@ -499,24 +602,18 @@ inline void draw_spans(loaded_bitmap *Buffer, game_render_commands *Commands, lo
 inline int issue(state &st) {
     int rc = PRK_OK;
     if (st.LastStatus != PRK_OK) return st.LastStatus;
+    if (st.PushStatus != PRK_OK) return st.PushStatus;
     if (st.ArenaUsed) {
-        // vertex colours reach the output only through DrawModel (scalar); the
-        // FillLineOptimized paths replace them by the texel (2029-2032)
-        bool colors = st.Geom < 0;
-        for (const pending_draw &d : st.Draws) colors |= d.Kind == DRAW_OBJECT && d.Semantics == PRK_SEM_SCALAR;
-        const bool create = st.Geom < 0;
-        int32_t g = -1;
-        rc = each([&](prk_context *c) {
-            if (!create)
-                return prk_geometry_update(c, st.Geom, st.AV, colors ? st.AC : nullptr, st.AN, st.AUV, st.ArenaUsed);
-            int32_t gc = -1;
-            const int r = prk_geometry_create(c, st.AV, st.AC, st.AN, st.AUV, st.ArenaUsed, &gc);
-            if (r == PRK_OK && g >= 0 && gc != g) return (int)PRK_ERR_ARG;
-            g = gc;
-            return r;
-        });
+        const bool created = st.Geom < 0;
+        rc = push_vertices(st);  // the tail (most of the frame went during the host calls)
         if (rc != PRK_OK) return rc;
-        if (create) st.Geom = g;
+        bool colors = false;
+        for (const pending_draw &d : st.Draws) colors |= d.Kind == DRAW_OBJECT && d.Semantics == PRK_SEM_SCALAR;
+        if (colors && !created)
+            rc = each([&](prk_context *c) {
+                return prk_geometry_write(c, st.Geom, 0, st.ArenaUsed, nullptr, st.AC, nullptr, nullptr);
+            });
+        if (rc != PRK_OK) return rc;
     }
     // every band records every draw (each bins all triangles against its rows)
     if (st.Cameras.empty()) st.Cameras.push_back(camera_of(st.Commands));
@@ -537,7 +634,7 @@ inline int issue(state &st) {
                 const pending_draw &d = st.Draws[k];
                 if (d.Kind == DRAW_OBJECT) {
                     const frame_object &o = st.Objects[d.First];
-                    r = prk_draw_objects(c, st.Geom, o.FirstTri, o.Tris, o.Tris, o.P, d.Semantics, d.Phong,
+                    r = prk_draw_objects(c, st.Geom, o.FirstTri, d.RunTris, o.Tris, o.P, d.Semantics, d.Phong,
                                          d.Texture);
                 } else if (d.Kind == DRAW_EDGES) {
                     r = prk_draw_edges(c, st.Edges.data() + d.First, d.Count, d.Semantics, d.Phong, d.Texture);
@@ -558,6 +655,8 @@ inline void end_frame(state &st) {
     st.LastBitmapMemory = nullptr;
     st.LastTexture = -1;
     st.ArenaUsed = 0;
+    st.Uploaded = 0;
+    st.PushStatus = PRK_OK;
     st.Objects.clear();
     st.Draws.clear();
     st.Cameras.clear();
@@ -617,14 +716,25 @@ inline void PRK_ClearNextFrame(uint32_t color, float z) {
 inline int PRK_CompleteAllWork(loaded_bitmap *Buffer, game_render_commands *Commands) {
     prk_dropin::state &st = prk_dropin::S();
     if (!st.Ctx || !st.FrameOpen) return PRK_OK;
+    using clk = std::chrono::steady_clock;
+    const auto ms = [](clk::time_point a, clk::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const auto t0 = clk::now();
     int rc = prk_dropin::issue(st);
+    const auto t1 = clk::now();
     // all bands' frames are queued before the first download waits
     if (rc == PRK_OK) rc = prk_dropin::each([](prk_context *c) { return prk_flush(c, nullptr); });
-    else prk_dropin::each([](prk_context *c) { return prk_reset_draws(c); });
+    else  // nothing drawn; the arena's chunk copies finish before the next frame reuses it
+        prk_dropin::each([](prk_context *c) { return prk_reset_draws(c) | prk_synchronize(c); });
+    const auto t2 = clk::now();
     if (rc == PRK_OK)
         rc = prk_dropin::each_band(Buffer, Commands, [&](prk_context *c, uint8_t *col, float *z) {
             return prk_target_download(c, (uint32_t *)col, Buffer->Pitch, z);
         });
+    st.LastIssueMs = ms(t0, t1);
+    st.LastFlushMs = ms(t1, t2);
+    st.LastDownloadMs = ms(t2, clk::now());
     prk_dropin::end_frame(st);
     st.LastStatus = rc;
     return rc;
@@ -643,8 +753,8 @@ inline u32 FillEdgeTable(render_entry_3d_object *Object, game_render_commands *C
     o.P[1] = Object->P.y;
     o.P[2] = Object->P.z;
     // the camera and lights of this call (3885, 3907-3909, 4022-4061)
-    const prk_dropin::camera cam = prk_dropin::camera_of(Commands);
-    o.Camera = prk_dropin::camera_id(st, cam);
+    o.Camera = prk_dropin::camera_id(st, Commands);
+    const prk_dropin::camera &cam = st.Cameras[o.Camera];
     // the reference's return value: the visible edge count (4119), 0 when no
     // edge is visible (e.g. a back-facing triangle)
     u32 edges = 0;
@@ -664,6 +774,8 @@ inline u32 FillEdgeTable(render_entry_3d_object *Object, game_render_commands *C
         st.ArenaUsed += nv;
         o.FirstTri = v0 / 3;
         o.Tris = T;
+        if (st.ArenaUsed - st.Uploaded >= prk_dropin::chunk_vertices() && st.PushStatus == PRK_OK)
+            prk_dropin::push_vertices(st);  // a failure is reported by PRK_CompleteAllWork
     }
     prk_dropin::object_token tok;
     tok.Magic = prk_dropin::kMagic;

@@ -8,6 +8,8 @@ where every colour op is IEEE-exact (all but the scalar path's double pow).
 
 Oracle parity is UNPINNED: the reference cannot be built here.
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -630,6 +632,61 @@ def test_geometry_update_null_array_grows(gpu):
     oc, oz, _, _ = O.render(expect, semantics=abi.PRK_SEM_SCALAR, phong=False)
     assert (gz.view(np.uint32) == oz.view(np.uint32)).all()
     assert (gc == oc).all()
+
+
+def test_geometry_write_chunks(gpu):
+    """prk_geometry_write (the drop-in's chunked upload): a geometry created
+    from the first 800 triangles gets the rest in two asynchronous writes of
+    positions / normals / uvs (buffers growing, colours zero-extended), then
+    a colour write for a scalar draw.  A write issued right after a flush
+    waits for that frame's kernels: the frame still shows the old vertices."""
+    b = scenes.random_soup(3000, 256, 256, radius=16, seed=53)
+    old = scenes.random_soup(3000, 256, 256, radius=16, seed=54)
+    old.texture = b.texture  # one texture handle serves both geometries
+    r = prk.Renderer()
+    try:
+        r.target_alloc(256, 256)
+        r.set_camera(b.prk_transform(), b.prk_lights())
+        tex = r.texture(b.texture)
+        g = r.geometry(old.vertices[:2400], old.colors[:2400], old.normals[:2400], old.uvs[:2400])
+        r.geometry_write(g, 2400, old.vertices[2400:], None, old.normals[2400:], old.uvs[2400:])
+        r.clear()
+        r.draw_model_optimized(g, old.tri_count, bitmap=tex, P=old.P)
+        r.complete_all_work()  # no wait: the next write is ordered after this frame's reads
+        v, n, uv = b.vertices, b.normals, b.uvs
+        # the asynchronous write reads page-locked host memory (prk.h)
+        pinned = []
+        for a in (v[:2400], n[:2400], uv[:2400]):
+            p = ctypes.c_void_p()
+            assert r._L.prk_host_alloc(r._h, a.nbytes, ctypes.byref(p)) == abi.PRK_OK
+            h = np.frombuffer((ctypes.c_float * a.size).from_address(p.value), np.float32).reshape(a.shape)
+            h[...] = a
+            pinned.append(p)
+        assert r._L.prk_geometry_write(r._h, g, 0, 2400, pinned[0], None, pinned[1], pinned[2]) == abi.PRK_OK
+        c1, z1 = r.download()
+        for p in pinned:
+            r._L.prk_host_free(r._h, p)
+        r.geometry_write(g, 2400, v[2400:5700], None, n[2400:5700], uv[2400:5700])
+        r.geometry_write(g, 5700, v[5700:], None, n[5700:], uv[5700:])
+        r.clear()
+        r.draw_model_optimized(g, b.tri_count, bitmap=tex, P=b.P)
+        r.complete_all_work()
+        c2, z2 = r.download()
+        r.geometry_write(g, 0, None, b.colors, None, None)
+        r.clear()
+        r.draw_model(g, b.tri_count, P=b.P, phong=False)
+        r.complete_all_work()
+        c3, z3 = r.download()
+    finally:
+        r.close()
+    untex = b.subset(0, b.tri_count)
+    untex.texture = None
+    for f, ((gc, gz), (s, sem)) in enumerate((((c1, z1), (old, abi.PRK_SEM_AVX)), ((c2, z2), (b, abi.PRK_SEM_AVX)),
+                                              ((c3, z3), (untex, abi.PRK_SEM_SCALAR)))):
+        kw = {} if sem == abi.PRK_SEM_AVX else {"phong": False}
+        oc, oz, _, _ = O.render(s, semantics=sem, **kw)
+        assert (gz.view(np.uint32) == oz.view(np.uint32)).all(), "frame %d: z" % f
+        assert (gc == oc).all(), "frame %d: colour (%d pixels)" % (f, (gc != oc).sum())
 
 
 def test_unsupported_combinations(gpu):

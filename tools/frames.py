@@ -50,8 +50,8 @@ def main():
                 (nm,) + tuple(c[off + k] / n for k in range(4))))
         e = [x / n for x in c[8:15]]
         print("  vis events/frame: chunks %.0f  row iterations %.0f  windows %.0f  items %.0f  "
-              "active lanes/row it %.1f  spans/row it %.1f  items/window %.1f" % (
-                  e[0], e[1], e[2], e[3], e[4] / max(1, e[1]), e[5] / max(1, e[1]), e[3] / max(1, e[2])))
+              "active lanes/row it %.1f  spans/row it %.1f  items/window %.1f  regular chunks %.0f" % (
+                  e[0], e[1], e[2], e[3], e[4] / max(1, e[1]), e[5] / max(1, e[1]), e[3] / max(1, e[2]), e[6]))
     r.close()
 
 
