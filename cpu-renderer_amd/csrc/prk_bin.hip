@@ -125,13 +125,8 @@ __device__ __forceinline__ void make_rec(const FrameParams &fp, uint32_t g, TriR
     rec_edge_out(s0, r.e[0], r.ymin[0], r.ymax[0]);
     rec_edge_out(s1, r.e[1], r.ymin[1], r.ymax[1]);
     rec_edge_out(s2, r.e[2], r.ymin[2], r.ymax[2]);
-    // regular from its first row (RowWalker::regular): the binning groups
-    // such triangles together, so k_vis / k_walk waves take the one-event step
-    RowWalker<MODE_AVX, true> rw;
-    rw.from(w);
-    const bool reg = n >= 2 && rw.regular();
     r.head = (uint32_t)n | (w.ord << 4) | ((uint32_t)w.cnt << 12) | ((uint32_t)(w.pend + 1) << 16) |
-             (min(anom, 15u) << 20) | ((d->flags & DRAW_ST) ? (1u << 24) : 0u) | (reg ? kHeadRegular : 0u);
+             (min(anom, 15u) << 20) | ((d->flags & DRAW_ST) ? (1u << 24) : 0u);
     r.vtx = (uint32_t)s0.Vtx | ((uint32_t)s1.Vtx << 4) | ((uint32_t)s2.Vtx << 8);
     r.pad[0] = r.pad[1] = 0;
 }
@@ -164,9 +159,10 @@ __device__ __forceinline__ void store_recs(const FrameParams &fp, float4 *st, bo
     wave_sync();
 }
 
-// Band test, cull, tile range and entry count of every triangle, and (recs:
-// radix-sort binning) the setup records of the triangles with entries.  The
-// counting-sort path computes the records in k_setup_rec instead.
+// Band test, cull, tile range and entry count of every triangle, and (recs)
+// the setup records of the triangles with entries: whole-frame targets and
+// the radix-sort binning.  A row band's counting-sort binning computes its
+// records in k_setup_rec instead.
 __global__ void __launch_bounds__(kCountThreads) k_bin_count(FrameParams fp, uint32_t *__restrict__ tri_n,
                                                               TileRange *__restrict__ ranges, bool recs) {
     __shared__ float4 stage[kCountThreads / 64][64 * 10];
@@ -317,11 +313,7 @@ constexpr uint32_t kCsMaxTiles = 32768;  // LDS: one u32 per tile (128 KiB)
                         // tile (its replay length); measured k_vis +6 % on C3b (0.497 -> 0.528 ms)
 #endif
 constexpr int kRepClassBits = PRK_REPCLASS ? 2 : 0;
-#ifndef PRK_REGCLASS
-#define PRK_REGCLASS 2  // bins also grouped by regularity (TriRec kHeadRegular): irregular lists last
-#endif
-constexpr int kRegClassBits = PRK_REGCLASS ? 1 : 0;
-constexpr int kClassBits = kRowClassBits + kRepClassBits + kRegClassBits;
+constexpr int kClassBits = kRowClassBits + kRepClassBits;
 constexpr uint32_t kCsClassShift = 32 - kClassBits;  // (replay, row) class in the top bits of the emitted pair index
 constexpr uint32_t kCsPairMask = (1u << kCsClassShift) - 1u;
 constexpr int kCsClassWindow = 2048;     // k_cs_class: entries grouped per pass
@@ -532,14 +524,9 @@ __global__ void __launch_bounds__(kCsThreads) k_cs_emit(FrameParams fp, const Ti
         if (!n) continue;
         const TileRange tr = ranges[g];
         uint32_t j = j0;
-        // irregular lists after the regular ones (k_vis walks a wave of
-        // regular lists with the one-event row step)
-        // (PRK_REGCLASS 1: as the top class bit; 2: the lowest, inside each row class)
-        const uint32_t irr = PRK_REGCLASS && fp.trec && !(fp.trec[g].head & kHeadRegular) ? 1u : 0u;
         for_each_entry(fp, tr, [&](uint32_t tile, uint32_t cls) {
             const uint32_t pos = atomicAdd(&cur[tile], 1u);
-            const uint32_t c = PRK_REGCLASS == 2 ? (cls << 1) | irr : cls | (irr << (kRowClassBits + kRepClassBits));
-            bins[pos] = make_uint2(g, j | (c << kCsClassShift));
+            bins[pos] = make_uint2(g, j | (cls << kCsClassShift));
             pair_tri[j] = g;
             clear_won(won, won_stride, j);
             ++j;

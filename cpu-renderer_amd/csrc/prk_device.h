@@ -97,12 +97,11 @@ struct TriRec {
     float e[3][10];      // sorted edge k: X, G, Z, ZG, W, WG, U, UG, V, VG
     int32_t ymin[3];     // YMin | Left << 31 (YMin >= 0: Maximum(0, .), 3999)
     int32_t ymax[3];
-    uint32_t head;       // n | ord << 4 | cnt << 12 | (pend + 1) << 16 | anomaly << 20 | st << 24 | regular << 25
+    uint32_t head;       // n | ord << 4 | cnt << 12 | (pend + 1) << 16 | anomaly << 20 | st << 24
     uint32_t vtx;        // sorted edge k's Vtx (mi | ma << 2) at bits 4k
     uint32_t pad[2];
 };
 static_assert(sizeof(TriRec) == 160, "TriRec is ten dwordx4");
-constexpr uint32_t kHeadRegular = 1u << 25;  // TriRec::head: the list is regular from the first row
 
 struct FrameParams {
     // projective_transform
@@ -949,39 +948,6 @@ struct RowWalker {
         cnt = (int)k0 + (int)k1 + (int)k2;
         // Pairing (3751-3869): one pair; a third entry stays unpaired.
         return cnt >= 2;
-    }
-
-    // A REGULAR list (regular(), decided per lane after the replay of the
-    // rows above): the rows left hold exactly one event — at row Mid =
-    // S2.YMin the pending edge is inserted and exactly one edge of the pair
-    // (S0, S1) expires; before Mid no edge expires, after it none before
-    // MaxY.  Insertion (3654-3713) then expiry (3715-3749) reduce to: the
-    // survivor of the pair, and S2 first iff it goes before S0, or S0 expires
-    // and it goes before S1.  The general begin_row moves all three edges
-    // through selects on such rows (≈ 120 VALU in k_vis) and runs its expiry
-    // test on every row; a wave of regular lists skips both.
-    __device__ __forceinline__ bool regular() const {
-        if (Row >= MaxY) return true;  // nothing left to walk
-        if (cnt != 2) return false;
-        const int32_t y0 = S0.YMax, y1 = S1.YMax;
-        const int32_t mid = pend ? S2.YMin : 0x7fffffff;
-        bool ok = mid >= Row && min(y0, y1) >= min(mid, MaxY);  // rows [Row, Mid): no expiry
-        if (pend && mid < MaxY) {  // row Mid: exactly one of the pair ends; then none before MaxY
-            const bool e0 = y0 <= mid, e1 = y1 <= mid;
-            ok = ok && (e0 != e1) && S2.YMax > mid && min(e0 ? y1 : y0, S2.YMax) >= MaxY;
-        }
-        return ok;
-    }
-    __device__ __forceinline__ bool begin_row_regular() {
-        if (pend && S2.YMin == Row) {
-            const bool aexp = S0.YMax <= Row;
-            const bool cfirst = insert_before(S2, S0) || (aexp && insert_before(S2, S1));
-            const Edge sv = sel(aexp, S1, S0);
-            S0 = sel(cfirst, S2, sv);
-            S1 = sel(cfirst, sv, S2);
-            pend = false;
-        }
-        return true;
     }
 
     // Edge step of the pair (3811-3829) and the crossing swap (3831-3841 + P3).

@@ -117,9 +117,6 @@ __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
 #ifndef PRK_PIXEL_ITEMS
 #define PRK_PIXEL_ITEMS 1  // shading sweep (AVX): one work item per won pixel, not per lane chain
 #endif
-#ifndef PRK_REGWALK
-#define PRK_REGWALK 1  // waves of regular lists (RowWalker::regular) take the one-event row step: 1 k_vis, 2 k_walk
-#endif
 #ifndef PRK_VIS_WAVES
 // waves per k_vis tile workgroup; each takes whole 64-entry chunks of the bin.
 // Four waves share one 16 KiB key array: 4 workgroups = 16 waves per CU.
@@ -761,7 +758,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
     unsigned long long pt[4] = {0, 0, 0, 0};  // PRK_PROF: setup, walk, scan/map, items
     // PRK_PROF event counts (visibility sweep): chunks, row iterations, item
     // windows, items, active lanes summed over row iterations, spans with items
-    unsigned long long pc[7] = {0, 0, 0, 0, 0, 0, 0};  // [6]: chunks walked as regular lists
+    unsigned long long pc[7] = {0, 0, 0, 0, 0, 0, 0};
     // Single-draw frames prefetch: the next chunk's bin entry is loaded at the
     // top of a chunk and its vertex attributes before the row walk, so both
     // loads are in flight while this chunk's setup and rows run.
@@ -871,10 +868,6 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
         // triangle and tile), whatever order the bin lists them in.
         const uint32_t tag = pair_tag(j, st != 0);
         if (PRK_DIAG & 4) active = false;
-        // a wave whose lists are all regular (the binning groups regular
-        // triangles together) takes the one-event row step
-        const bool reg = (PRK_REGWALK & 1) && __all(!active || wk.regular());
-        if (PRK_PROF && reg) pc[6] += 1;
         if (PRK_PROF) { const unsigned long long t1 = PRK_T(); pt[0] += t1 - t0; t0 = t1; }
         // PRK_LANE_ROWS: every lane walks its own next row each iteration (the
         // span's row travels in its slot); else all lanes step row r together.
@@ -904,7 +897,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
                 if (active && (PRK_LANE_ROWS || wk.Row == r)) {
                     const int slot = multi ? rank * k + q : lane;
                     const int32_t row = wk.Row;
-                    const bool paired = reg ? wk.begin_row_regular() : wk.begin_row();
+                    const bool paired = wk.begin_row();
                     if (paired) {
                         const Edge &L = wk.S0, &R = wk.S1;
                         int ni;
@@ -1346,13 +1339,12 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
     const int32_t t0 = (int32_t)((uint32_t)tr.tx0 | ((uint32_t)tr.ty0 << 16));
     const int32_t t1 = (int32_t)((uint32_t)tr.tx1 | ((uint32_t)tr.ty1 << 16));
     uint32_t head = 0, cnt = 0;  // wave-uniform queue state
-    const bool reg = (PRK_REGWALK & 2) && __all(!active || wk.regular());  // (k_won_local groups them)
     while (__any(active)) {
         bool push = false, paired = false;
         int32_t Row = 0;
         if (active) {
             Row = wk.Row;
-            paired = reg ? wk.begin_row_regular() : wk.begin_row();
+            paired = wk.begin_row();
             const int32_t rb = Row - rbase;
             const bool want = !fast || (rb >= 0 && rb < 64 && ((rows >> rb) & 1ull));
             push = paired && want && Row >= fp.row0;
@@ -1407,9 +1399,8 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
 constexpr int kWonClasses = 64, kWonPer = 8, kWonThreads = 256;
 constexpr size_t kWonHistBytes = 16;  // [0]: the list length
 
-__device__ __forceinline__ int won_class(const TileRange &tr, const TriRec *__restrict__ trec, uint32_t g) {
-    // (PRK_REGCLASS: irregular lists after the regular ones, as in the bins)
-    if (PRK_WON_SORT == 0) return trec && !(trec[g].head & kHeadRegular) ? 1 : 0;
+__device__ __forceinline__ int won_class(const TileRange &tr) {
+    if (PRK_WON_SORT == 0) return 0;
     const int rows = (int)tr.pad1 - (int)tr.pad0;  // band rows [r0, r1) (k_bin_count)
     return kWonClasses - 1 - min(max(rows, 0), kWonClasses - 1);
 }
@@ -1418,7 +1409,6 @@ __device__ __forceinline__ int won_class(const TileRange &tr, const TriRec *__re
 // PRK_WON_SORT 1) at a run of the list reserved with one atomic on *count.
 __global__ void __launch_bounds__(kWonThreads) k_won_local(uint32_t n, const uint8_t *__restrict__ trwon,
                                                            const TileRange *__restrict__ ranges,
-                                                           const TriRec *__restrict__ trec,
                                                            uint32_t *__restrict__ count, uint32_t *__restrict__ wlist) {
     __shared__ uint32_t h[kWonClasses];
     __shared__ uint32_t base;
@@ -1433,7 +1423,7 @@ __global__ void __launch_bounds__(kWonThreads) k_won_local(uint32_t n, const uin
         cls[k] = -1;
         rank[k] = 0;
         if (g < n && trwon[g]) {
-            cls[k] = won_class(ranges[g], trec, g);
+            cls[k] = won_class(ranges[g]);
             rank[k] = atomicAdd(&h[cls[k]], 1u);
         }
     }
@@ -1882,7 +1872,7 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
             uint32_t *hist_ = reinterpret_cast<uint32_t *>(sel_temp);                                                \
             nsel = hist_; /* the run counter is the list length */                                                   \
             hipLaunchKernelGGL(prk::k_won_local, dim3(nwon), dim3(prk::kWonThreads), 0, sw, fp->tri_count, trwon,     \
-                               tr, (PRK_REGWALK & 2) ? fp->trec : nullptr, hist_, wlist);                                  \
+                               tr, hist_, wlist);                                                                    \
             hipLaunchKernelGGL((prk::k_walk<UNI>), dim3(nwblk), dim3(64 * prk::kWalkWaves), 0, sw, *fp, wlist, nsel,    \
                                tri_off, tr, won,                                                                     \
                                rp, anomaly);                                                                         \
