@@ -207,6 +207,30 @@ struct prk_context {
     uint32_t frame = 0;
     int last_slot = -1;
     int last_set = -1;  // scratch set of the last per-triangle pass
+    // The last per-triangle pass, whose bin entry count the host has not read
+    // yet (flush_tris with `defer`): prk_flush returns once the frame is
+    // queued, and the count is read at the next call that needs it
+    // (resolve_count) — by then the binning has long finished, so the host
+    // no longer waits for every frame's binning before queueing the next
+    // frame.  A pass whose entries overflowed the scratch is re-run there,
+    // before anything else is queued or read, with the state it was queued
+    // with (target, camera, tile, clear).
+    struct PendingCount {
+        bool active = false;
+        int set = 0;
+        hipStream_t s = nullptr;
+        std::vector<prk::DrawRec> draws;
+        uint32_t T = 0, win_base = 0, ntiles = 0;
+        bool fuse = false, debug = false;
+        void *color = nullptr;
+        int32_t pitch = 0;
+        float *zbuf = nullptr;
+        int32_t W = 0, H = 0, row0 = 0, row1 = 0, tile_w = 0, tile_h = 0;
+        prk_transform transform{};
+        prk_light_data lights{};
+        uint32_t clear_color = 0;
+        float clear_z = 0.0f;
+    } pcount;
     // Span path (whole-object AETs) scratch, reused frame to frame.
     struct SpanScratch {
         DevBuf d_draws, d_texs, d_objs, d_edges, d_ord, d_tmp, d_cnt, d_off, d_temp, d_recs, d_pos, d_span_tri,
@@ -220,6 +244,15 @@ struct prk_context {
         uint32_t *h_rb = nullptr;  // pinned readback words
     } spans;
 };
+
+static int resolve_count(prk_context *c);
+// Calls that read or replace the target, or change what a re-run of the
+// pending pass would read, first resolve its count (PendingCount).
+#define RESOLVE_COUNT(c)                             \
+    do {                                             \
+        const int _rc = resolve_count(c);            \
+        if (_rc != PRK_OK) return _rc;               \
+    } while (0)
 
 #define PRK_TRY(expr)                              \
     do {                                           \
@@ -297,6 +330,7 @@ int prk_create(int device, prk_context **out) {
 
 int prk_destroy(prk_context *c) {
     if (!c) return PRK_ERR_ARG;
+    (void)resolve_count(c);
     (void)hipSetDevice(c->device);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     (void)hipDeviceSynchronize();
@@ -366,6 +400,7 @@ int prk_target_bind(prk_context *c, void *color, int32_t pitch_bytes, float *zbu
     if (!c || !color || !zbuf || width <= 0 || height <= 0 || row0 < 0 || row1 > height || row0 >= row1 ||
         pitch_bytes < width * 4 || (pitch_bytes & 3))
         return PRK_ERR_ARG;
+    if (c->owns_target) RESOLVE_COUNT(c);
     drop_target(c);
     c->color = color;
     c->pitch = pitch_bytes;
@@ -381,6 +416,7 @@ int prk_target_bind(prk_context *c, void *color, int32_t pitch_bytes, float *zbu
 int prk_target_alloc(prk_context *c, int32_t width, int32_t height, int32_t row0, int32_t row1,
                      void **color_out, float **zbuf_out) {
     if (!c || width <= 0 || height <= 0 || row0 < 0 || row1 > height || row0 >= row1) return PRK_ERR_ARG;
+    RESOLVE_COUNT(c);
     PRK_TRY(hipSetDevice(c->device));
     drop_target(c);
     size_t px = (size_t)width * (row1 - row0);
@@ -419,6 +455,7 @@ __global__ void k_fill_target(uint32_t *color, int32_t pitch, float *z, int32_t 
 
 int prk_target_clear(prk_context *c, uint32_t color, float z) {
     if (!c) return PRK_ERR_ARG;
+    RESOLVE_COUNT(c);
     if (!c->color) return PRK_ERR_NO_TARGET;
     PRK_TRY(hipSetDevice(c->device));
     size_t n = (size_t)c->W * (c->row1 - c->row0);
@@ -439,6 +476,7 @@ int prk_target_clear_on_flush(prk_context *c, uint32_t color, float z) {
 
 int prk_target_download(prk_context *c, uint32_t *color_host, int32_t host_pitch, float *z_host) {
     if (!c) return PRK_ERR_ARG;
+    RESOLVE_COUNT(c);
     if (!c->color) return PRK_ERR_NO_TARGET;
     PRK_TRY(hipSetDevice(c->device));
     PRK_TRY(hipStreamSynchronize(c->own_stream));
@@ -453,6 +491,7 @@ int prk_target_download(prk_context *c, uint32_t *color_host, int32_t host_pitch
 
 int prk_target_upload(prk_context *c, const uint32_t *color_host, int32_t host_pitch, const float *z_host) {
     if (!c) return PRK_ERR_ARG;
+    RESOLVE_COUNT(c);
     if (!c->color) return PRK_ERR_NO_TARGET;
     PRK_TRY(hipSetDevice(c->device));
     PRK_TRY(hipStreamSynchronize(c->own_stream));
@@ -466,6 +505,7 @@ int prk_target_upload(prk_context *c, const uint32_t *color_host, int32_t host_p
 
 int prk_target_upload_async(prk_context *c, const uint32_t *color_host, int32_t host_pitch, const float *z_host) {
     if (!c) return PRK_ERR_ARG;
+    RESOLVE_COUNT(c);
     if (!c->color) return PRK_ERR_NO_TARGET;
     PRK_TRY(hipSetDevice(c->device));
     // after the frames already flushed (they read and write the target) and
@@ -527,6 +567,7 @@ int prk_texture_create(prk_context *c, const prk_bitmap *b, int32_t *handle_out)
 
 int prk_texture_update(prk_context *c, int32_t handle, const prk_bitmap *b) {
     if (!c || handle < 0 || (size_t)handle >= c->texs.size() || !bitmap_ok(b)) return PRK_ERR_ARG;
+    RESOLVE_COUNT(c);
     PRK_TRY(hipSetDevice(c->device));
     Texture &t = c->texs[handle];
     PRK_TRY(hipDeviceSynchronize());  // frames in flight may still sample it
@@ -573,6 +614,7 @@ int prk_host_unregister(prk_context *c, void *p) {
 
 int prk_texture_set_filter(prk_context *c, int32_t handle, int32_t filter) {
     if (!c || handle < 0 || (size_t)handle >= c->texs.size()) return PRK_ERR_ARG;
+    RESOLVE_COUNT(c);
     if (filter != PRK_FILTER_NEAREST && filter != PRK_FILTER_BILINEAR) return PRK_ERR_ARG;
     c->texs[handle].filter = filter;
     return PRK_OK;
@@ -623,6 +665,7 @@ int prk_geometry_create(prk_context *c, const float *v, const float *col, const 
 int prk_geometry_update(prk_context *c, int32_t handle, const float *v, const float *col, const float *n,
                         const float *uv, uint32_t vertex_count) {
     if (!c || handle < 0 || (size_t)handle >= c->geoms.size() || !v || vertex_count % 3) return PRK_ERR_ARG;
+    RESOLVE_COUNT(c);
     Geometry &g = c->geoms[handle];
     if (!g.owned) return PRK_ERR_ARG;
     PRK_TRY(hipSetDevice(c->device));
@@ -673,6 +716,7 @@ int prk_geometry_write(prk_context *c, int32_t handle, uint32_t first_vertex, ui
                        const float *v, const float *col, const float *n, const float *uv) {
     if (!c || handle < 0 || (size_t)handle >= c->geoms.size() || first_vertex % 3 || vertex_count % 3)
         return PRK_ERR_ARG;
+    RESOLVE_COUNT(c);
     const uint64_t end64 = (uint64_t)first_vertex + vertex_count;
     if (end64 > 0xFFFFFFF0ull) return PRK_ERR_ARG;
     const uint32_t end = (uint32_t)end64;
@@ -926,6 +970,7 @@ int prk_timing_reset(prk_context *c) {
 
 int prk_debug_counters(prk_context *c, uint64_t *out, int32_t n) {
     if (!c || !out || n < 0 || n > 16) return PRK_ERR_ARG;
+    RESOLVE_COUNT(c);
     PRK_TRY(hipSetDevice(c->device));
     PRK_TRY(hipDeviceSynchronize());
     for (int i = 0; i < n; ++i) out[i] = 0;
@@ -990,7 +1035,7 @@ static int fill_pending_clear(prk_context *c, hipStream_t s) {
 // raster into the target.  `draws` number their triangles from 0; winner ids
 // are win_base + that index.
 static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::DrawRec> &draws, uint32_t T,
-                      uint32_t win_base) {
+                      uint32_t win_base, bool defer = false) {
     int modeset = -2;
     for (const auto &d : draws) {
         if (modeset == -2) modeset = d.mode;
@@ -1236,27 +1281,77 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
     guard.ok = true;
     if (cs) {
         // The whole frame is queued; now the entry count (the binning's first
-        // few kernels) decides whether it fitted.  An over-capacity frame drew
-        // nothing (empty bins; with a fused clear its k_pix wrote the clear
-        // values, which the re-run writes again): re-run it with room for
-        // every entry.
-        PRK_TRY(hipEventSynchronize(B.counted_ev));
-        total = B.h_info[0];
-        c->stats.bin_entries = total;
-        c->pair_hint = total;
-        if (c->tile_auto && !c->auto_small && c->tile_w == 256 && total < 64u * ntiles &&
-            8u * ntiles <= prk_cs_max_tiles()) {  // (32x8 tiles stay within the counting sort)
-            c->auto_small = total < 8u * ntiles ? 64 : 32;  // (from the next frame on)
-            c->auto_T = T;
-            c->auto_px = c->W * (c->row1 - c->row0);
-        }
-        if (B.h_info[1]) {
-            if (total > prk_cs_max_pairs()) return PRK_ERR_UNSUPPORTED;  // 29-bit pair index in the bins
-            c->clear_pending = fuse;
-            return flush_tris(c, s, draws, T, win_base);
-        }
+        // few kernels) decides whether it fitted — read here, or, for the
+        // frame's last pass once a previous frame has sized the scratch, by
+        // the next call that needs it (resolve_count).
+        prk_context::PendingCount &P = c->pcount;
+        P.set = si;
+        P.s = s;
+        P.draws = draws;
+        P.T = T;
+        P.win_base = win_base;
+        P.ntiles = ntiles;
+        P.fuse = fuse;
+        P.debug = c->debug;
+        P.color = c->color; P.pitch = c->pitch; P.zbuf = c->zbuf;
+        P.W = c->W; P.H = c->H; P.row0 = c->row0; P.row1 = c->row1;
+        P.tile_w = c->tile_w; P.tile_h = c->tile_h;
+        P.transform = c->transform; P.lights = c->lights;
+        P.clear_color = c->clear_color; P.clear_z = c->clear_z;
+        P.active = true;
+        if (!(defer && c->pair_hint)) return resolve_count(c);
     }
     return PRK_OK;
+}
+
+// The entry count of the pending pass (PendingCount): stats, the next
+// frame's capacity and tile; an over-capacity pass drew nothing (empty bins;
+// with a fused clear its k_pix wrote the clear values, which the re-run
+// writes again) and is re-run with room for every entry, with the state it
+// was queued with.
+static int resolve_count(prk_context *c) {
+    prk_context::PendingCount &P = c->pcount;
+    if (!P.active) return PRK_OK;
+    P.active = false;
+    PRK_TRY(hipSetDevice(c->device));
+    prk_context::BinSet &B = c->bset[P.set];
+    PRK_TRY(hipEventSynchronize(B.counted_ev));
+    const uint32_t total = B.h_info[0];
+    c->stats.bin_entries = total;
+    c->pair_hint = total;
+    if (c->tile_auto && !c->auto_small && P.tile_w == 256 && total < 64u * P.ntiles &&
+        8u * P.ntiles <= prk_cs_max_tiles()) {  // (32x8 tiles stay within the counting sort)
+        c->auto_small = total < 8u * P.ntiles ? 64 : 32;  // (from the next frame on)
+        c->auto_T = P.T;
+        c->auto_px = P.W * (P.row1 - P.row0);
+    }
+    if (!B.h_info[1]) return PRK_OK;
+    if (total > prk_cs_max_pairs()) return PRK_ERR_UNSUPPORTED;  // 29-bit pair index in the bins
+    // re-run with the pass's own state, then give the caller's back
+    struct Saved {
+        void *color; int32_t pitch; float *zbuf; int32_t W, H, row0, row1, tile_w, tile_h;
+        prk_transform transform; prk_light_data lights; uint32_t clear_color; float clear_z;
+        bool clear_pending, debug;
+    } sv{c->color, c->pitch, c->zbuf, c->W, c->H, c->row0, c->row1, c->tile_w, c->tile_h,
+         c->transform, c->lights, c->clear_color, c->clear_z, c->clear_pending, c->debug};
+    c->color = P.color; c->pitch = P.pitch; c->zbuf = P.zbuf;
+    c->W = P.W; c->H = P.H; c->row0 = P.row0; c->row1 = P.row1;
+    c->tile_w = P.tile_w; c->tile_h = P.tile_h;
+    c->transform = P.transform; c->lights = P.lights;
+    c->clear_color = P.clear_color; c->clear_z = P.clear_z;
+    c->clear_pending = P.fuse;
+    c->debug = P.debug;
+    const std::vector<prk::DrawRec> draws = std::move(P.draws);
+    const int rc = flush_tris(c, P.s, draws, P.T, P.win_base);
+    c->read_rec = hipEventRecord(c->read_ev, P.s) == hipSuccess;  // (geometry writes wait for the re-run)
+    c->color = sv.color; c->pitch = sv.pitch; c->zbuf = sv.zbuf;
+    c->W = sv.W; c->H = sv.H; c->row0 = sv.row0; c->row1 = sv.row1;
+    c->tile_w = sv.tile_w; c->tile_h = sv.tile_h;
+    c->transform = sv.transform; c->lights = sv.lights;
+    c->clear_color = sv.clear_color; c->clear_z = sv.clear_z;
+    c->clear_pending = sv.clear_pending;
+    c->debug = sv.debug;
+    return rc;
 }
 
 // One pass of whole-object AETs (prk_spans.hip): FillEdgeTable per triangle,
@@ -1439,6 +1534,11 @@ int prk_flush(prk_context *c, void *stream) {
     if (!c) return PRK_ERR_ARG;
     if (!c->color) return PRK_ERR_NO_TARGET;
     if (!c->have_camera) return PRK_ERR_ARG;
+    PRK_TRY(hipSetDevice(c->device));
+    {
+        const int rc = resolve_count(c);  // the previous frame's count first: it may change the tile
+        if (rc != PRK_OK) return rc;
+    }
     if (c->tile_auto) {  // the frame's tile (see prk_context::tile_auto)
         const int64_t px = (int64_t)c->W * (c->row1 - c->row0);
         if (c->auto_small && ((uint64_t)c->pending_tris > 2ull * c->auto_T || 2ull * c->pending_tris < c->auto_T ||
@@ -1447,7 +1547,6 @@ int prk_flush(prk_context *c, void *stream) {
         c->tile_w = c->auto_small ? c->auto_small : 256;
         c->tile_h = 8;
     }
-    PRK_TRY(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->own_stream;
     if (c->in_wait) {  // prk_geometry_write copies still in flight: every stream of the frame waits for them
         PRK_TRY(hipStreamWaitEvent(s, c->in_ev, 0));
@@ -1497,7 +1596,9 @@ int prk_flush(prk_context *c, void *stream) {
             seg.push_back(d);
             ++j;
         }
-        rc = obj ? flush_spans(c, s, seg, T, base) : flush_tris(c, s, seg, T, base);
+        // (only the frame's last pass defers its count: a later pass z-tests
+        // against this one's output, so an overflow must be re-run first)
+        rc = obj ? flush_spans(c, s, seg, T, base) : flush_tris(c, s, seg, T, base, j == dr.size());
         i = j;
     }
     // the frame's last reader of the geometry (the flush stream ends every pass)
@@ -1527,8 +1628,12 @@ int prk_get_device(prk_context *c, int32_t *device, void **stream) {
     return PRK_OK;
 }
 
+// prk_dist.hip: gathers read the band's finished frame (library-internal).
+__attribute__((visibility("hidden"))) int prk_resolve_pending(prk_context *c) { return c ? resolve_count(c) : PRK_ERR_ARG; }
+
 int prk_synchronize(prk_context *c) {
     if (!c) return PRK_ERR_ARG;
+    RESOLVE_COUNT(c);
     PRK_TRY(hipSetDevice(c->device));
     PRK_TRY(hipStreamSynchronize(c->own_stream));
     PRK_TRY(hipDeviceSynchronize());
@@ -1537,6 +1642,7 @@ int prk_synchronize(prk_context *c) {
 
 int prk_get_stats(prk_context *c, prk_stats *out) {
     if (!c || !out) return PRK_ERR_ARG;
+    RESOLVE_COUNT(c);
     (void)hipSetDevice(c->device);
     for (int i = 1; i <= prk_context::kRing; ++i)  // oldest first
         harvest(c, (int)((c->frame + i) % prk_context::kRing));
@@ -1551,6 +1657,7 @@ int prk_get_stats(prk_context *c, prk_stats *out) {
 
 int prk_download_winners(prk_context *c, int32_t *w) {
     if (!c || !w) return PRK_ERR_ARG;
+    RESOLVE_COUNT(c);
     if (!c->winners_valid || !c->d_winners.p) return PRK_ERR_ARG;
     PRK_TRY(hipSetDevice(c->device));
     PRK_TRY(hipDeviceSynchronize());

@@ -195,6 +195,9 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_count(FrameParams fp, uin
 // the band's triangles ran the whole setup at a few lanes, 99 us of a
 // 0.30 ms band frame).
 constexpr uint32_t kRecRun = 2048;
+#ifndef PRK_BIN_BAND
+#define PRK_BIN_BAND 1  // row bands: k_bin_band (one launch) instead of k_bin_count + k_setup_rec
+#endif
 __device__ uint32_t cs_block_excl_scan(uint32_t v, uint32_t *scratch, uint32_t &total);
 __global__ void __launch_bounds__(kCountThreads) k_setup_rec(FrameParams fp, const uint32_t *__restrict__ tri_n) {
     __shared__ float4 stage[kCountThreads / 64][64 * 10];
@@ -205,6 +208,51 @@ __global__ void __launch_bounds__(kCountThreads) k_setup_rec(FrameParams fp, con
     for (uint32_t k = 0; k < kRecRun; k += kCountThreads) {
         const uint32_t g = g0 + k + threadIdx.x;
         const uint32_t f = g < fp.tri_count && tri_n[g] != 0 ? 1u : 0u;
+        uint32_t tot;
+        const uint32_t pos = cs_block_excl_scan(f, scratch, tot);
+        if (f) list[n + pos] = g;
+        n += tot;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint32_t b = (uint32_t)wv * 64; b < n; b += kCountThreads) {
+        const uint32_t i = b + lane;
+        const bool rec = i < n;
+        const uint32_t g = rec ? list[i] : 0u;
+        TriRec r;
+        if (rec) make_rec(fp, g, r);
+        store_recs(fp, stage[wv], rec, r, g);
+    }
+}
+
+// A row band's k_bin_count + k_setup_rec in one launch: each workgroup takes
+// a run of kRecRun triangles, writes every one's tile range and entry count
+// (256 at a time, listing the ones with entries in LDS in triangle order),
+// then sets up the listed triangles' records 64 per wave.  (Two launches
+// before: C3b at N = 8, 20 + 23 us serial, each reading the band test's
+// inputs of all 1 M triangles.)
+__global__ void __launch_bounds__(kCountThreads) k_bin_band(FrameParams fp, uint32_t *__restrict__ tri_n,
+                                                             TileRange *__restrict__ ranges) {
+    __shared__ float4 stage[kCountThreads / 64][64 * 10];
+    __shared__ uint32_t list[kRecRun];
+    __shared__ uint32_t scratch[kCountThreads / 64];
+    const uint32_t g0 = blockIdx.x * kRecRun;
+    uint32_t n = 0;
+    for (uint32_t k = 0; k < kRecRun; k += kCountThreads) {
+        const uint32_t g = g0 + k + threadIdx.x;
+        uint32_t ne = 0;
+        if (g < fp.tri_count) {
+            TileRange tr;
+            if (!tri_tile_range(fp, g, tr)) {
+                tr.tx0 = 1; tr.tx1 = 0; tr.ty0 = 1; tr.ty1 = 0; tr.oty0 = 1; tr.oty1 = 0;
+            }
+            ranges[g] = tr;
+            ne = range_entries(tr);
+            tri_n[g] = ne;
+        } else if (g == fp.tri_count) {
+            tri_n[g] = 0;  // sentinel: a scan's last element is the total
+        }
+        const uint32_t f = ne != 0 && fp.trec ? 1u : 0u;
         uint32_t tot;
         const uint32_t pos = cs_block_excl_scan(f, scratch, tot);
         if (f) list[n + pos] = g;
@@ -427,25 +475,45 @@ __global__ void __launch_bounds__(64 * kColSegs) k_cs_colscan(uint32_t *__restri
 // of the chunk totals; info[0] = entry count, info[1] = 1 if it exceeds `cap`
 // (then every bin is left empty and k_cs_emit writes no pair).
 // Exclusive scan of n values (n <= kCsThreads * kScanPer) by one workgroup:
-// each thread loads kScanPer consecutive values first, so the whole scan is
-// one round of loads and one workgroup scan.
+// wave w scans the contiguous segment [w * kScanSeg, (w + 1) * kScanSeg),
+// 64 values per load (coalesced) and one DPP wave scan per 64 with a running
+// carry, then the wave totals are scanned across the workgroup.  (Round 2
+// had each thread load kScanPer consecutive values: 64 cache lines per load
+// instruction, and a one-workgroup kernel that waited on them — 12 us alone,
+// 50-60 us when it shared its CU with k_vis / k_walk waves in a band frame.)
 constexpr uint32_t kScanPer = kCsMaxTiles / kCsThreads;
+constexpr uint32_t kScanSeg = kScanPer * 64;
 __device__ __forceinline__ uint32_t cs_scan_small(const uint32_t *__restrict__ in, uint32_t n,
                                                   uint32_t *__restrict__ out, uint32_t *scratch, uint32_t base) {
-    uint32_t v[kScanPer];
-    const uint32_t i0 = threadIdx.x * kScanPer;
-    uint32_t sum = 0;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, s0 = wave * kScanSeg;
+    uint32_t v[kScanPer], pre[kScanPer];
 #pragma unroll
     for (uint32_t k = 0; k < kScanPer; ++k) {
-        v[k] = i0 + k < n ? in[i0 + k] : 0u;
-        sum += v[k];
+        const uint32_t i = s0 + k * 64 + lane;
+        v[k] = i < n ? in[i] : 0u;
     }
-    uint32_t tot;
-    uint32_t run = base + cs_block_excl_scan(sum, scratch, tot);
+    uint32_t carry = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kScanPer; ++k) {
-        if (i0 + k < n) out[i0 + k] = run;
-        run += v[k];
+        if (s0 + k * 64 >= n) break;  // (wave-uniform)
+        const uint32_t incl = cs_wave_incl_scan(v[k]);
+        pre[k] = carry + incl - v[k];
+        carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    }
+    if (lane == 0) scratch[wave] = carry;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+    for (uint32_t w = 0; w < (uint32_t)(blockDim.x >> 6); ++w) {
+        const uint32_t x = scratch[w];
+        before += w < wave ? x : 0u;
+        tot += x;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k) {
+        const uint32_t i = s0 + k * 64 + lane;
+        if (s0 + k * 64 >= n) break;
+        if (i < n) out[i] = base + before + pre[k];
     }
     return tot;
 }
@@ -650,6 +718,11 @@ hipError_t prk_bin_count(const prk::FrameParams *fp, uint32_t *tri_n, void *rang
     // A whole-frame target sets up (nearly) every triangle: inline records
     // (C3b: 76 us against 22 + 68 us split); a row band only its own.
     const bool band = fp->row0 > 0 || fp->row1 < fp->H;
+    if (band && PRK_BIN_BAND) {  // (k_bin_band also writes the sentinel tri_n[tri_count])
+        hipLaunchKernelGGL(prk::k_bin_band, dim3((n + prk::kRecRun - 1) / prk::kRecRun), dim3(prk::kCountThreads),
+                           0, s, *fp, tri_n, reinterpret_cast<prk::TileRange *>(ranges));
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(prk::k_bin_count, dim3((n + prk::kCountThreads - 1) / prk::kCountThreads),
                        dim3(prk::kCountThreads), 0, s, *fp, tri_n, reinterpret_cast<prk::TileRange *>(ranges), !band);
     if (band && fp->trec && fp->tri_count)

@@ -26,6 +26,7 @@
 
 static_assert(PRK_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
 
+extern "C" int prk_resolve_pending(prk_context *c);  // prk_api.hip (library-internal)
 namespace {
 
 struct Rccl {
@@ -82,7 +83,9 @@ struct Band {
 };
 
 int band_of(prk_context *ctx, int32_t rank, int32_t nranks, Band &B) {
-    int rc = prk_get_target(ctx, &B.color, &B.pitch, &B.z, &B.W, &B.H, &B.row0, &B.row1);
+    int rc = prk_resolve_pending(ctx);  // the band's last frame is final (a deferred re-run queued first)
+    if (rc != PRK_OK) return rc;
+    rc = prk_get_target(ctx, &B.color, &B.pitch, &B.z, &B.W, &B.H, &B.row0, &B.row1);
     if (rc != PRK_OK) return rc;
     void *s = nullptr;
     rc = prk_get_device(ctx, &B.device, &s);

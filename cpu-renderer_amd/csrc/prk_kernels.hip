@@ -117,6 +117,9 @@ __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
 #ifndef PRK_PIXEL_ITEMS
 #define PRK_PIXEL_ITEMS 1  // shading sweep (AVX): one work item per won pixel, not per lane chain
 #endif
+#ifndef PRK_VIS_DYN
+#define PRK_VIS_DYN 1  // k_vis waves take the bin's chunks from an LDS counter
+#endif
 #ifndef PRK_VIS_WAVES
 // waves per k_vis tile workgroup; each takes whole 64-entry chunks of the bin.
 // Four waves share one 16 KiB key array: 4 workgroups = 16 waves per CU.
@@ -745,13 +748,47 @@ __device__ __forceinline__ int wave_incl_max(int v) {  // v >= 0
 }
 
 
+// The walker of a sweep's row loop.  PRK_VIS_PERM: the visibility sweep
+// keeps the three edges in fixed registers and the list as a permutation
+// (Walker): every row steps and selects a few fields (the span reads X, z,
+// 1/z, u/z, v/z of its two edges), and insertion / expiry / the crossing
+// swap move two bits.  RowWalker holds the list physically: a row steps two
+// edges with no selects, but an insertion, expiry or swap row moves whole
+// edges — and with 64 triangles per wave nearly every row has one in some
+// lane (about half of the visibility row loop's VALU instructions were those
+// moves).
+#ifndef PRK_VIS_PERM
+#define PRK_VIS_PERM 1
+#endif
+#ifndef PRK_WALK_PERM
+#define PRK_WALK_PERM 0  // 1: k_walk walks with the permutation walker too (normals included): measured k_walk +5 % (three normalisations per row instead of two)
+#endif
+template <int M, bool SHADE>
+using SweepWalker = typename std::conditional<PRK_VIS_PERM && !SHADE, Walker<M, SHADE>, RowWalker<M, SHADE>>::type;
+template <int M, bool NRM>
+__device__ __forceinline__ void wk_from(RowWalker<M, NRM> &wk, const Walker<M, NRM> &w0) { wk.from(w0); }
+template <int M, bool NRM>
+__device__ __forceinline__ void wk_from(Walker<M, NRM> &wk, const Walker<M, NRM> &w0) { wk = w0; }
+template <int M, bool NRM>
+__device__ __forceinline__ void wk_pair(const RowWalker<M, NRM> &wk, Edge &L, Edge &R) { L = wk.S0; R = wk.S1; }
+template <int M, bool NRM>
+__device__ __forceinline__ void wk_pair(const Walker<M, NRM> &wk, Edge &L, Edge &R) {
+    L = wk.get(wk.slot(0));
+    R = wk.get(wk.slot(1));
+}
+
 // One sweep over the tile's bin for mode M.  SHADE=false: visibility keys;
 // SHADE=true: shade the winners.
 template <int M, bool SHADE, bool UNI, bool REC = false, class WS>
 __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, WS &ws,
                                       const uint2 *__restrict__ bins, uint32_t b0, uint32_t n,
-                                      const uint32_t *__restrict__ list, uint32_t *anomaly) {
+                                      const uint32_t *__restrict__ list, uint32_t *anomaly,
+                                      uint32_t *chunk_ctr = nullptr) {
     // Entries [0, n) of the tile's bin, or (list != nullptr) the n entries it names.
+    // chunk_ctr (LDS, zeroed): the waves take the bin's 64-entry chunks in
+    // turn from this counter, each its next chunk when it finishes one,
+    // instead of every nwaves-th chunk (a tile of 6-7 chunks left two of its
+    // four waves idle for a chunk's time).
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const bool col0 = tc.x0 == 0 && M != MODE_AVX;
     const int32_t ystart = col0 ? tc.y0 - 1 : tc.y0;  // scalar: (row-1) may store into (row, 0)
@@ -776,7 +813,14 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
         }
     }
     const uint32_t nwaves = blockDim.x >> 6;
-    for (uint32_t base = wave * 64; base < n; base += 64 * nwaves) {
+    auto next_chunk = [&](uint32_t cur) -> uint32_t {
+        if (kPre || !chunk_ctr) return cur + 64 * nwaves;
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(chunk_ctr, 64u);
+        return (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+    };
+    const uint32_t first = (kPre || !chunk_ctr) ? wave * 64 : next_chunk(0);
+    for (uint32_t base = first; base < n; base = next_chunk(base)) {
         unsigned long long t0 = PRK_T();
         const uint32_t i = base + lane;
         bool active = i < n;
@@ -784,7 +828,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
         uint32_t e = 0, j = 0;  // bin entry, its pair index (the tie-break order)
         uint32_t st = 0;        // DRAW_ST: single-thread DrawModelOptimized(Buffer,...) semantics
         int32_t texi = 0;
-        RowWalker<M, SHADE> wk;
+        SweepWalker<M, SHADE> wk;
         uint32_t anom = 0;
         TriRaw<M> craw;
         const uint32_t inext = i + 64 * nwaves;
@@ -851,7 +895,7 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
                 // Replay the rows above the tile (edge DDA only); row by row
                 // only for irregular edge lists.
                 const int fr = w0.fast_replay(ystart, ne);
-                wk.from(w0);
+                wk_from(wk, w0);
                 if (fr < 0)
                     while (wk.Row < ystart && wk.Row < wk.MaxY) wk.end_row(wk.begin_row());
                 if (fr != 0 && !SHADE) atomicAdd(anomaly + 1, 1u);
@@ -899,7 +943,8 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
                     const int32_t row = wk.Row;
                     const bool paired = wk.begin_row();
                     if (paired) {
-                        const Edge &L = wk.S0, &R = wk.S1;
+                        Edge L, R;
+                        wk_pair(wk, L, R);
                         int ni;
                         if constexpr (M == MODE_AVX) ni = span_setup_avx<SHADE>(fp, tc, ws, slot, tag, texi, L, R, row, st != 0);
                         else ni = span_setup_scalar<M, SHADE>(fp, tc, ws, slot, tag, texi, L, R, row);
@@ -1025,6 +1070,7 @@ __global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
     VisSlots &ws = slots[threadIdx.x >> 6];
     uint32_t *scratch = reinterpret_cast<uint32_t *>(slots + kVisWaves);
 
+    if (threadIdx.x == 0) scratch[8] = 0;  // the sweep's chunk counter (PRK_VIS_DYN)
     // Prior z of the target: a fragment must beat it strictly.
     for (int p = threadIdx.x; p < npx; p += blockDim.x) {
         const int lx = p & (fp.tile_w - 1), ly = p >> fp.tile_w_log2;
@@ -1040,7 +1086,7 @@ __global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
     if constexpr (MODESET >= 0) {
         // all-AVX frames read the binning pass's setup records (TriRec)
         sweep<(MODESET >= 0 ? MODESET : 0), false, UNI, MODESET == MODE_AVX && PRK_SETUP_REC>(
-            fp, tc, ws, bins, b0, n, nullptr, anomaly);
+            fp, tc, ws, bins, b0, n, nullptr, anomaly, PRK_VIS_DYN ? scratch + 8 : nullptr);
     } else {
         sweep<MODE_AVX, false, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly);
         sweep<MODE_SC_GOURAUD, false, false>(fp, tc, ws, bins, b0, n, nullptr, anomaly);
@@ -1249,7 +1295,7 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     bool active = i < nw;
     const uint32_t g = active ? wlist[i] : 0u;  // the triangles that won a pixel (compacted)
-    RowWalker<M, true> wk;
+    typename std::conditional<PRK_WALK_PERM, Walker<M, true>, RowWalker<M, true>>::type wk;
     int32_t texi = 0;
     uint32_t st = 0;  // DRAW_ST
     TileRange tr{};
@@ -1306,7 +1352,7 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
             if constexpr (PRK_SETUP_REC) w0.init_rec(ne, s0, s1, s2, fp.H, fp.row1, rhead);
             else w0.init(ne, s0, s1, s2, fp.H, fp.row1, anom);
             const int fr = w0.fast_replay(fp.row0, ne);  // band above row0 (row bands only)
-            wk.from(w0);
+            wk_from(wk, w0);
             if (fr < 0)
                 while (wk.Row < fp.row0 && wk.Row < wk.MaxY) wk.end_row(wk.begin_row());
             if (anom) atomicAdd(anomaly, anom);
@@ -1353,7 +1399,8 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
         if (push) {
             const uint32_t slot = (head + cnt + (uint32_t)__builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))) & (kWalkQ - 1);
-            const Edge &L = wk.S0, &R = wk.S1;
+            Edge L, R;
+            wk_pair(wk, L, R);
             q.f[0][slot] = L.X; q.f[1][slot] = L.W; q.f[2][slot] = L.U; q.f[3][slot] = L.V; q.f[4][slot] = L.Z;
             q.f[5][slot] = L.N0; q.f[6][slot] = L.N1; q.f[7][slot] = L.N2;
             q.f[8][slot] = R.X; q.f[9][slot] = R.W; q.f[10][slot] = R.U; q.f[11][slot] = R.V; q.f[12][slot] = R.Z;

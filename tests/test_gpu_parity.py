@@ -279,6 +279,57 @@ def test_bin_capacity_rerun(gpu):
     assert (gc == oc).all()
 
 
+def test_deferred_count_overflow_rerun_across_rebind(gpu):
+    """prk_flush returns without reading the frame's bin entry count once a
+    previous frame has sized the scratch; the count is read by the next call
+    that needs it.  Here an over-capacity frame is drawn into target B, the
+    caller re-binds target A and queues another frame over A's contents
+    without any sync: the next flush re-runs the overflowed frame into B
+    (its own target, camera and clear) before queueing A's frame, and both
+    targets end equal to the oracle.  (A and B are device targets owned by
+    two other contexts.)"""
+    small = scenes.random_soup(3000, 512, 384, radius=16, seed=91)
+    big = scenes.random_soup(6000, 512, 384, radius=260, seed=92)
+    small2 = scenes.random_soup(2500, 512, 384, radius=20, seed=93)
+    for s in (big, small2):
+        s.texture = small.texture
+    W, H = 512, 384
+    ra, rb, r = prk.Renderer(0), prk.Renderer(0), prk.Renderer(0)
+    try:
+        ra.target_alloc(W, H)
+        rb.target_alloc(W, H)
+        pa, pb = ra.target(), rb.target()
+        r.set_camera(small.prk_transform(), small.prk_lights())
+        tex = r.texture(small.texture)
+        gs = [r.geometry(s.vertices, s.colors, s.normals, s.uvs) for s in (small, big, small2)]
+        r.target_bind(pa[0], pa[1], pa[2], W, H)
+        r.clear_on_flush()
+        r.draw_model_optimized(gs[0], small.tri_count, P=small.P, bitmap=tex, phong=True)
+        r.complete_all_work()  # first frame: counted at once (sizes the scratch)
+        r.target_bind(pb[0], pb[1], pb[2], W, H)
+        r.clear_on_flush()
+        r.draw_model_optimized(gs[1], big.tri_count, P=big.P, bitmap=tex, phong=True)
+        r.complete_all_work()  # over capacity: its count is read at the next flush
+        r.target_bind(pa[0], pa[1], pa[2], W, H)
+        r.draw_model_optimized(gs[2], small2.tri_count, P=small2.P, bitmap=tex, phong=True)
+        r.complete_all_work()  # re-runs big into B first, then small2 over A
+        r.synchronize()
+        entries = r.stats()["bin_entries"]
+        ga, gb = ra.download(), rb.download()
+    finally:
+        r.close()
+        ra.close()
+        rb.close()
+    assert entries > 0
+    oc, oz, _, _ = O.render(small)
+    oc, oz, _, _ = O.render(small2, color=oc, z=oz)
+    bc, bz, _, _ = O.render(big)
+    assert (gb[1].view(np.uint32) == bz.view(np.uint32)).all(), "target B z"
+    assert (gb[0] == bc).all(), "target B colour"
+    assert (ga[1].view(np.uint32) == oz.view(np.uint32)).all(), "target A z"
+    assert (ga[0] == oc).all(), "target A colour"
+
+
 def test_pipelined_identical_frames_and_band_rebind(gpu):
     """Identical fused-clear frames queued back to back (every scratch set in
     turn) end as the one frame; then the target is re-bound from a full frame
