@@ -351,6 +351,7 @@ def main():
     ms = dt * 1000.0 / a.steps
     # Frame download (colour + z of this rank's band, HBM -> host), outside
     # the timed region: reported separately.
+    r.synchronize()  # the last frame's bin count is read (an overflowed frame re-run) before torch reads the target
     host_c = torch.empty(color.shape, dtype=color.dtype, pin_memory=True)
     host_z = torch.empty(zbuf.shape, dtype=zbuf.dtype, pin_memory=True)
     torch.cuda.synchronize()

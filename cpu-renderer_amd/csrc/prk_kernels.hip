@@ -1219,9 +1219,15 @@ __device__ __forceinline__ void walk_record(const FrameParams &fp, const Edge &L
     const int tx0 = max((int)tr.tx0, MinX >> fp.tile_w_log2);
     const int tx1 = min((int)tr.tx1, (MaxX - 1) >> fp.tile_w_log2);
     const uint32_t jrow = jb + (uint32_t)((ty - (int)tr.ty0) * ntx - (int)tr.tx0);
-    bool any = false;
-    for (int tx = tx0; tx <= tx1; ++tx) any |= won[(size_t)(jrow + tx) * fp.tile_h + ly] != 0;
-    if (!any) return;
+    // One tile column and at most 8 tile rows: k_walk queued this row only
+    // because its won bit (loaded up front) is set, so the won flags need not
+    // be read again here (a dependent load per span).
+    const bool known = fp.tile_h == 8 && tr.tx0 == tr.tx1 && (int)tr.ty1 - (int)tr.ty0 < 8;
+    if (!known) {
+        bool any = false;
+        for (int tx = tx0; tx <= tx1; ++tx) any |= won[(size_t)(jrow + tx) * fp.tile_h + ly] != 0;
+        if (!any) return;
+    }
     const int32_t XDiff = (int32_t)((uint32_t)round_s32(R.X) - (uint32_t)round_s32(L.X));  // 1568-1570
     int32_t LeftXa = MinX;
     if (MinX & 7) {  // 1594-1609
@@ -1242,7 +1248,7 @@ __device__ __forceinline__ void walk_record(const FrameParams &fp, const Edge &L
     const float4 q3 = make_float4(L.N2, IN0, IN1, IN2);
     for (int tx = tx0; tx <= tx1; ++tx) {  // a span crossing a tile border: one record per won tile
         const size_t ri = (size_t)(jrow + tx) * fp.tile_h + ly;
-        if (!won[ri]) continue;
+        if (!known && !won[ri]) continue;
         float4 *q = reinterpret_cast<float4 *>(recs + ri);
         q[0] = q0; q[1] = q1; q[2] = q2; q[3] = q3;
     }

@@ -282,7 +282,18 @@ int prk_draw_spans(prk_context *ctx, const prk_span *spans, uint32_t count, int3
 
 /* Execute every recorded draw, in submission order, into the bound target
  * (the reference's Platform.CompleteAllWork).  `stream` is a hipStream_t or
- * NULL for the library's own stream.  Asynchronous w.r.t. the host. */
+ * NULL for the library's own stream.  Asynchronous w.r.t. the host: it
+ * returns once the frame is queued, without waiting for its binning.  The
+ * frame's bin entry count (scratch sizing, prk_stats.bin_entries) is read by
+ * the next call that needs it: the next prk_flush, prk_synchronize,
+ * prk_target_download / upload / clear, prk_get_stats, a texture or geometry
+ * update, a gather, prk_target_alloc, or prk_target_bind replacing a
+ * library-owned target.  A frame whose entries overflowed the scratch is
+ * re-run there, into the target and with the camera, tile and clear it was
+ * queued with, before anything else is queued — so a caller that reads the
+ * target through its own device pointers (not prk_target_download) after a
+ * flush calls prk_synchronize first.  (The first frame of a context is
+ * counted at once.) */
 int prk_flush(prk_context *ctx, void *stream);
 /* Drop recorded draws without executing them. */
 int prk_reset_draws(prk_context *ctx);
