@@ -111,11 +111,15 @@ __global__ void k_tri_draw(const DrawRec *__restrict__ draws, uint32_t ndraws,
 #ifndef PRK_MULTI_ROWS_AVX
 #define PRK_MULTI_ROWS_AVX 4  // AVX sweeps: multi-row iterations only with at most this many active lanes
 #endif
+static_assert(PRK_MULTI_ROWS_AVX <= 8, "8 rows per lane for at most 8 lanes: the 64 span slots");
 #ifndef PRK_VIS_GROUP
 #define PRK_VIS_GROUP 2  // visibility items: G consecutive pixels each (0: one lane chain each)
 #endif
 #ifndef PRK_PIXEL_ITEMS
 #define PRK_PIXEL_ITEMS 1  // shading sweep (AVX): one work item per won pixel, not per lane chain
+#endif
+#ifndef PRK_VIS_PREBIN
+#define PRK_VIS_PREBIN 1  // k_vis: the next chunk's bin entries load while this chunk runs
 #endif
 #ifndef PRK_VIS_DYN
 #define PRK_VIS_DYN 1  // k_vis waves take the bin's chunks from an LDS counter
@@ -820,7 +824,16 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
         return (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
     };
     const uint32_t first = (kPre || !chunk_ctr) ? wave * 64 : next_chunk(0);
-    for (uint32_t base = first; base < n; base = next_chunk(base)) {
+    // Setup-record sweeps take the next chunk when they start one and load
+    // its bin entries while this chunk runs, so a chunk's first load is its
+    // records (bin entry -> record were two dependent round trips).
+    constexpr bool kPreBin = REC && !SHADE && !kPre && PRK_VIS_PREBIN;
+    uint2 pbe = make_uint2(0u, 0u);
+    if (kPreBin && !list && first + lane < n) pbe = bins[b0 + first + lane];
+    for (uint32_t base = first, nb = 0; base < n; base = nb) {
+        const uint2 cbe = pbe;
+        nb = next_chunk(base);
+        if (kPreBin && !list && nb + lane < n) pbe = bins[b0 + nb + lane];
         unsigned long long t0 = PRK_T();
         const uint32_t i = base + lane;
         bool active = i < n;
@@ -846,14 +859,14 @@ __device__ __forceinline__ void sweep(const FrameParams &fp, const TileCtx &tc, 
         if (active) {
             if constexpr (!kPre) {
                 e = list ? list[b0 + i] : i;
-                j = bins[b0 + e].y;
+                j = (kPreBin && !list) ? cbe.y : bins[b0 + e].y;
             }
             Edge s0, s1, s2;
             int ne;
             uint32_t rhead = 0;
             if constexpr (REC) {
                 // Setup record of the binning pass: no per-entry FillEdgeTable.
-                const uint32_t g = bins[b0 + e].x;
+                const uint32_t g = (kPreBin && !list) ? cbe.x : bins[b0 + e].x;
                 const float4 *q = reinterpret_cast<const float4 *>(fp.trec + g);
                 float4 v[10];
 #pragma unroll
