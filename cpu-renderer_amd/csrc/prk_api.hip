@@ -71,16 +71,22 @@ constexpr uint32_t kObjMaxEdges = 1u << 22;  // MergeSort key: recursion path of
 // PRK_SPAN_RECORDS of prk_kernels.hip.
 #define PRK_SPAN_RECORDS_HOST 1
 // Per-frame scratch sets in flight: a frame whose target band has at most
-// kSmallBandPx pixels cycles PRK_FRAME_SETS sets, larger ones 2 (the set
+// kSmallBandPx pixels (64 Mpx) cycles PRK_FRAME_SETS sets, larger ones 2 (the set
 // count nsets; consecutive frames take consecutive sets): with three, frame k+1's binning need not wait for
-// frame k-1's raster, which pays when binning is a large share of the frame
-// (band of 512 x 4096 px, one rank of 8: 0.284 -> 0.247 ms; 1024 rows:
-// 0.405 -> 0.378) and costs ~1-3 % on bigger frames, where the extra
-// binning competes with k_vis (whole 4096^2 frame 1.147 -> 1.160 ms).
+// frame k-1's raster (round 2, band of 512 x 4096 px, one rank of 8: 0.284 ->
+// 0.247 ms; 1024 rows: 0.405 -> 0.378; the whole 4096^2 frame then 1-3 %
+// slower, with the host waiting for every frame's count).
 #ifndef PRK_FRAME_SETS
 #define PRK_FRAME_SETS 3
 #endif
-constexpr size_t kSmallBandPx = (size_t)1 << 22;
+// Round 3 (lazy bin count): three sets for every target up to 64 Mpx (C5
+// included) — the whole C3b frame 1.049-1.053 -> 1.041-1.044 ms (interleaved
+// A/B, three rounds); round 2 measured three sets 1-3 % slower there when the
+// host waited for every frame's count.
+#ifndef PRK_SMALL_BAND_LOG2
+#define PRK_SMALL_BAND_LOG2 26
+#endif
+constexpr size_t kSmallBandPx = (size_t)1 << PRK_SMALL_BAND_LOG2;
 
 namespace {
 
