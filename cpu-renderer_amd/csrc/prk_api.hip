@@ -41,16 +41,22 @@ hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, co
 hipError_t prk_walk_select_bytes(uint32_t, size_t *);
 hipError_t prk_selftest_div_launch(uint32_t n, uint64_t seed, unsigned long long *bad, hipStream_t s);
 hipError_t prk_objtri_count(const prk::FrameParams *, const void *, const uint32_t *, const uint32_t *, uint32_t,
-                            uint32_t, uint32_t *, hipStream_t);
+                            uint32_t, uint32_t *, unsigned long long *, hipStream_t);
 hipError_t prk_objtri_emit(const prk::FrameParams *, const void *, const uint32_t *, const uint32_t *, uint32_t,
-                           uint32_t, const uint32_t *, void *, void *, uint32_t *, hipStream_t);
+                           uint32_t, const uint32_t *, uint32_t, uint32_t, int32_t, void *, void *, uint32_t *,
+                           hipStream_t);
 hipError_t prk_obj_sort(void *, uint32_t *, void *, uint32_t *, uint32_t, uint32_t, void *, size_t *, hipStream_t);
 hipError_t prk_obj_gather(const void *, const uint32_t *, const uint32_t *, const void *, const uint32_t *, uint32_t,
                           void *, uint32_t, hipStream_t);
-hipError_t prk_obj_walk(const prk::FrameParams *, const void *, uint32_t, const uint32_t *, uint32_t, const uint32_t *,
-                        const uint32_t *, void *, int, uint32_t *, const uint32_t *, void *, void *, void *,
+hipError_t prk_obj_bound(const prk::FrameParams *, const void *, uint32_t, const unsigned long long *, const void *,
+                         unsigned long long *, hipStream_t);
+uint32_t prk_obj_walk_lcap(void);
+hipError_t prk_obj_walk(const prk::FrameParams *, const void *, uint32_t, const uint32_t *, uint32_t, uint32_t,
+                        const uint32_t *, const unsigned long long *, const uint32_t *, uint32_t, int32_t *,
+                        const uint32_t *, const uint32_t *, void *, const unsigned long long *, void *, void *, void *,
                         uint32_t *, const void *, uint32_t *, hipStream_t);
 hipError_t prk_scan_u32(const uint32_t *, uint32_t *, uint32_t, void *, size_t *, hipStream_t);
+hipError_t prk_scan_u64(const unsigned long long *, unsigned long long *, uint32_t, void *, size_t *, hipStream_t);
 hipError_t prk_span_count(const prk::FrameParams *, const void *, uint32_t, uint32_t *, hipStream_t);
 hipError_t prk_span_bin(const prk::FrameParams *, const void *, uint32_t, const uint32_t *, uint32_t, uint32_t *,
                         uint32_t *, uint32_t *, uint32_t *, uint32_t *, void *, size_t *, hipStream_t);
@@ -65,7 +71,7 @@ struct ObjDesc {
 };
 constexpr uint32_t kObjWave = 0x80000000u;  // ObjDesc::k1off flag: walked by one wave
 constexpr uint32_t kObjWaveTris = 48;        // objects of this many triangles or more
-constexpr uint32_t kObjMaxEdges = 1u << 22;  // MergeSort key: recursion path of 23 bits
+constexpr int kWaveListArrays = 9;           // prk_spans.hip WaveList: int32 arrays of cap + 2 entries
 
 // AVX frames shade through span records (k_walk + k_pix); must match
 // PRK_SPAN_RECORDS of prk_kernels.hip.
@@ -239,12 +245,14 @@ struct prk_context {
     } pcount;
     // Span path (whole-object AETs) scratch, reused frame to frame.
     struct SpanScratch {
-        DevBuf d_draws, d_texs, d_objs, d_edges, d_ord, d_tmp, d_cnt, d_off, d_temp, d_recs, d_pos, d_span_tri,
-            d_scnt, d_soff, d_keys_a, d_vals_a, d_keys_b, d_vals_b, d_offs, d_nwin, d_wtag, d_edges_in, d_spans_in,
-            d_srecs, d_work, d_ekeys, d_ekeys2, d_evals, d_ecnt, d_escan, d_k0obj, d_k0tri0, d_big, d_k1src, d_err;
+        DevBuf d_draws, d_texs, d_objs, d_edges, d_ord, d_temp, d_recs, d_pos, d_span_tri, d_scnt, d_soff, d_keys_a,
+            d_vals_a, d_keys_b, d_vals_b, d_offs, d_nwin, d_wtag, d_edges_in, d_spans_in, d_srecs, d_work, d_ekeys,
+            d_ekeys2, d_evals, d_ecnt, d_escan, d_rcnt, d_rscan, d_bound, d_oslot, d_k0obj, d_k0tri0, d_big_lds,
+            d_big_gl, d_big_off, d_big_cap, d_pool, d_k1src, d_err;
         // host tables of the pass, kept until their asynchronous uploads ran
         std::vector<ObjDesc> h_objs;
-        std::vector<uint32_t> h_k0obj, h_k0tri0, h_big, h_k1src;
+        std::vector<uint32_t> h_k0obj, h_k0tri0, h_big_lds, h_big_gl, h_big_cap, h_k1src;
+        std::vector<unsigned long long> h_big_off;
         std::vector<prk::DrawRec> h_draws;
         std::vector<prk::TexRec> h_texs;
         uint32_t *h_rb = nullptr;  // pinned readback words
@@ -336,7 +344,13 @@ int prk_create(int device, prk_context **out) {
 
 int prk_destroy(prk_context *c) {
     if (!c) return PRK_ERR_ARG;
-    (void)resolve_count(c);
+    // Destroy never queues GPU work: a frame whose bin count was never read
+    // (PendingCount) is dropped, not re-run — its target may already belong
+    // to someone else (a torch tensor freed at interpreter exit, a peer
+    // context), and a re-run there is exactly what a caller tearing down does
+    // not expect.  Only waits and frees follow.
+    c->pcount.active = false;
+    c->pcount.draws.clear();
     (void)hipSetDevice(c->device);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     (void)hipDeviceSynchronize();
@@ -367,11 +381,12 @@ int prk_destroy(prk_context *c) {
     for (DevBuf *b : bufs) b->release();
     {
         auto &S = c->spans;
-        DevBuf *sb[] = {&S.d_draws, &S.d_texs, &S.d_objs, &S.d_edges, &S.d_ord, &S.d_tmp, &S.d_cnt, &S.d_off,
-                        &S.d_temp, &S.d_recs, &S.d_pos, &S.d_span_tri, &S.d_scnt, &S.d_soff, &S.d_keys_a,
-                        &S.d_vals_a, &S.d_keys_b, &S.d_vals_b, &S.d_offs, &S.d_nwin, &S.d_wtag, &S.d_edges_in,
-                        &S.d_spans_in, &S.d_srecs, &S.d_work, &S.d_ekeys, &S.d_ekeys2, &S.d_evals, &S.d_ecnt,
-                        &S.d_escan, &S.d_k0obj, &S.d_k0tri0, &S.d_big, &S.d_k1src, &S.d_err};
+        DevBuf *sb[] = {&S.d_draws, &S.d_texs, &S.d_objs, &S.d_edges, &S.d_ord, &S.d_temp, &S.d_recs, &S.d_pos,
+                        &S.d_span_tri, &S.d_scnt, &S.d_soff, &S.d_keys_a, &S.d_vals_a, &S.d_keys_b, &S.d_vals_b,
+                        &S.d_offs, &S.d_nwin, &S.d_wtag, &S.d_edges_in, &S.d_spans_in, &S.d_srecs, &S.d_work,
+                        &S.d_ekeys, &S.d_ekeys2, &S.d_evals, &S.d_ecnt, &S.d_escan, &S.d_rcnt, &S.d_rscan,
+                        &S.d_bound, &S.d_oslot, &S.d_k0obj, &S.d_k0tri0, &S.d_big_lds, &S.d_big_gl, &S.d_big_off,
+                        &S.d_big_cap, &S.d_pool, &S.d_k1src, &S.d_err};
         for (DevBuf *b : sb) b->release();
         if (S.h_rb) (void)hipHostFree(S.h_rb);
     }
@@ -406,7 +421,10 @@ int prk_target_bind(prk_context *c, void *color, int32_t pitch_bytes, float *zbu
     if (!c || !color || !zbuf || width <= 0 || height <= 0 || row0 < 0 || row1 > height || row0 >= row1 ||
         pitch_bytes < width * 4 || (pitch_bytes & 3))
         return PRK_ERR_ARG;
-    if (c->owns_target) RESOLVE_COUNT(c);
+    // the pending frame's count first, whoever owns its target: an overflowed
+    // frame is re-run into the target it was queued with before a caller
+    // hands that memory to anything else (a gather, the next frame)
+    RESOLVE_COUNT(c);
     drop_target(c);
     c->color = color;
     c->pitch = pitch_bytes;
@@ -801,11 +819,22 @@ int prk_draw(prk_context *c, int32_t geometry, uint32_t first_tri, uint32_t tri_
 
 int prk_draw_objects(prk_context *c, int32_t geometry, uint32_t first_tri, uint32_t tri_count,
                      uint32_t tris_per_object, const float P[3], int32_t semantics, int32_t phong, int32_t texture) {
+    return prk_draw_objects_setup(c, geometry, first_tri, tri_count, tris_per_object, P, semantics, phong, texture,
+                                  -1);
+}
+
+int prk_draw_objects_setup(prk_context *c, int32_t geometry, uint32_t first_tri, uint32_t tri_count,
+                           uint32_t tris_per_object, const float P[3], int32_t semantics, int32_t phong,
+                           int32_t texture, int32_t setup) {
     if (!c || geometry < 0 || geometry >= (int32_t)c->geoms.size() || tris_per_object == 0) return PRK_ERR_ARG;
     const Geometry &g = c->geoms[geometry];
     if ((uint64_t)first_tri + tri_count > g.vertex_count / 3) return PRK_ERR_ARG;
     if (texture >= (int32_t)c->texs.size()) return PRK_ERR_ARG;
+    if (setup > (PRK_SETUP_PHONG | PRK_SETUP_BITMAP)) return PRK_ERR_ARG;
     const bool tex = texture >= 0;
+    // FillEdgeTable's PhongShading and Object->Bitmap (prk.h prk_setup)
+    const bool fe_phong = setup < 0 ? phong != 0 : (setup & PRK_SETUP_PHONG) != 0;
+    const bool fe_bitmap = setup < 0 ? tex : (setup & PRK_SETUP_BITMAP) != 0;
     int mode;
     uint32_t flags = 0;
     if (semantics == PRK_SEM_AVX || semantics == PRK_SEM_AVX_ST) {
@@ -821,7 +850,14 @@ int prk_draw_objects(prk_context *c, int32_t geometry, uint32_t first_tri, uint3
     } else {
         return PRK_ERR_ARG;
     }
-    if ((phong || !tex) && !g.N) return PRK_ERR_ARG;
+    // Edge fields FillEdgeTable never wrote: MinNormal without PhongShading
+    // (4012-4064), the U/V/(1/z) gradients without Object->Bitmap (4078-4089).
+    if ((phong && !fe_phong) || (tex && !fe_bitmap)) return PRK_ERR_UNSUPPORTED;
+    if (mode == prk::MODE_SC_GOURAUD) {
+        if (fe_phong) flags |= prk::DRAW_RAWCOL;        // raw colours, unlit (4014-4015)
+        else if (fe_bitmap) flags |= prk::DRAW_WHITELIT;  // lighting from white (4034-4054)
+    }
+    if ((phong || !tex) && !g.N) return PRK_ERR_ARG;  // (the Gouraud setup kernels load them in every case)
     if (tex && !g.UV) return PRK_ERR_ARG;
     if ((mode == prk::MODE_SC_GOURAUD || mode == prk::MODE_SC_PHONG) && !g.C) return PRK_ERR_ARG;
     if (tri_count == 0) return PRK_OK;
@@ -1231,7 +1267,7 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
         PRK_TRY(hipStreamSynchronize(bs));
         total = *c->h_total;
         c->stats.bin_entries = total;
-        if (total >= prk::kMaxPairs) return PRK_ERR_UNSUPPORTED;  // visibility tags hold a 31-bit pair index
+        if (total >= prk::kMaxPairs) return PRK_ERR_LIMIT;  // visibility tags hold a 31-bit pair index
         PRK_TRY(ensure_pairs(total, true));
         won = (uint8_t *)B.d_won.p;
         trwon = span_rec ? (uint8_t *)B.d_trwon.p : nullptr;
@@ -1332,7 +1368,7 @@ static int resolve_count(prk_context *c) {
         c->auto_px = P.W * (P.row1 - P.row0);
     }
     if (!B.h_info[1]) return PRK_OK;
-    if (total > prk_cs_max_pairs()) return PRK_ERR_UNSUPPORTED;  // 29-bit pair index in the bins
+    if (total > prk_cs_max_pairs()) return PRK_ERR_LIMIT;  // 29-bit pair index in the bins
     // re-run with the pass's own state, then give the caller's back
     struct Saved {
         void *color; int32_t pitch; float *zbuf; int32_t W, H, row0, row1, tile_w, tile_h;
@@ -1361,10 +1397,11 @@ static int resolve_count(prk_context *c) {
 }
 
 // One pass of whole-object AETs (prk_spans.hip): FillEdgeTable per triangle,
-// MergeSort per object (one radix sort), walk every object's AET into span
-// records (count pass, scan, emit pass), bin the spans to tiles, then
-// visibility + shading.  Stream-ordered on s; the host waits at the three
-// sizes it reads back (edge count, span count, bin entry count).
+// MergeSort per object (one radix sort), one walk of every object's AET into
+// span records (each object writing into its own slots, as many as its edges'
+// active rows allow), bin the spans to tiles, then visibility + shading.
+// Stream-ordered on s; the host waits at the two sizes it reads back (the
+// span slots, the bin entry count).
 static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::DrawRec> &draws, uint32_t T,
                        uint32_t win_base) {
     prk::FrameParams fp;
@@ -1379,15 +1416,21 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     if (T == 0) return PRK_OK;
     prk_context::SpanScratch &S = c->spans;
     if (!S.h_rb) PRK_TRY(hipHostMalloc((void **)&S.h_rb, 4 * sizeof(uint32_t), hipHostMallocDefault));
+    const uint32_t lcap = prk_obj_walk_lcap();  // LDS list capacity of the wave walk (edges)
     // Objects in submission order (ObjDesc kinds: prk_spans.hip): kind 0
     // objects' triangles numbered 0..ntri-1 in order (FillEdgeTable runs per
-    // triangle), caller edge lists' edges after the triangles' edges.
+    // triangle), caller edge lists' edges after the triangles' edges.  Objects
+    // of kObjWaveTris triangles or more are walked by one wave each, their
+    // list in LDS when all their edges fit lcap, else in a pool slice.
     S.h_objs.clear();
     S.h_k0obj.clear();
     S.h_k0tri0.clear();
-    S.h_big.clear();
+    S.h_big_lds.clear();
+    S.h_big_gl.clear();
+    S.h_big_off.clear();
+    S.h_big_cap.clear();
     S.h_k1src.clear();
-    uint64_t ntri = 0, nk1 = 0;
+    uint64_t ntri = 0, nk1 = 0, pool = 0, maxn = 1;
     for (uint32_t di = 0; di < draws.size(); ++di) {
         const prk::DrawRec &d = draws[di];
         if (d.src_kind == 1) {
@@ -1401,9 +1444,17 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
             const uint32_t per = std::max<uint32_t>(1u, d.obj_tris);
             for (uint32_t t = 0; t < d.tri_count; t += per) {
                 const uint32_t n = std::min(per, d.tri_count - t);
-                if (3ull * n >= kObjMaxEdges) return PRK_ERR_UNSUPPORTED;
+                const uint64_t edges = 3ull * n;  // the most its FillEdgeTable writes
+                maxn = std::max(maxn, edges);
                 const bool wave = n >= kObjWaveTris;
-                if (wave) S.h_big.push_back((uint32_t)S.h_objs.size());
+                if (wave && edges <= lcap) {
+                    S.h_big_lds.push_back((uint32_t)S.h_objs.size());
+                } else if (wave) {
+                    S.h_big_gl.push_back((uint32_t)S.h_objs.size());
+                    S.h_big_off.push_back(pool);
+                    S.h_big_cap.push_back((uint32_t)edges);
+                    pool += (uint64_t)kWaveListArrays * (edges + 2);
+                }
                 S.h_k0obj.push_back((uint32_t)S.h_objs.size());
                 S.h_k0tri0.push_back((uint32_t)ntri);
                 S.h_objs.push_back(ObjDesc{di, d.first_global + t, n, (uint32_t)ntri, 0u, 0u, 0u, wave ? kObjWave : 0u});
@@ -1411,9 +1462,15 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
             }
         }
     }
-    if (3 * ntri + nk1 >= 0x7FFFFFFFull || S.h_k0obj.size() >= (1u << 25)) return PRK_ERR_UNSUPPORTED;
+    // edge slots (3 per triangle + the caller edges) are indexed by 31 bits
+    if (3 * ntri + nk1 >= 0x7FFFFFFFull) return PRK_ERR_LIMIT;
     const uint32_t nobj = (uint32_t)S.h_objs.size(), nk0 = (uint32_t)S.h_k0obj.size();
-    const uint32_t nt = (uint32_t)ntri, nbig = (uint32_t)S.h_big.size();
+    const uint32_t nt = (uint32_t)ntri, nlds = (uint32_t)S.h_big_lds.size(), ngl = (uint32_t)S.h_big_gl.size();
+    // MergeSort key: (object, min(YMin, H), recursion path) in one radix sort
+    auto bitlen = [](uint64_t v) { uint32_t b = 0; while (v) { ++b; v >>= 1; } return b; };
+    const uint32_t pbits = bitlen(maxn) + 1, ybits = std::max(1u, bitlen((uint64_t)c->H));
+    const uint32_t obits = std::max(1u, bitlen(nk0 > 0 ? nk0 - 1 : 0));
+    if (obits + ybits + pbits > 64) return PRK_ERR_LIMIT;
     S.h_texs.resize(c->texs.size());
     for (size_t i = 0; i < S.h_texs.size(); ++i)
         S.h_texs[i] = prk::TexRec{c->texs[i].mem, c->texs[i].w, c->texs[i].h, c->texs[i].pitch, c->texs[i].filter};
@@ -1434,17 +1491,23 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(up(S.d_objs, S.h_objs.data(), S.h_objs.size() * sizeof(ObjDesc)));
     PRK_TRY(up(S.d_k0obj, S.h_k0obj.data(), S.h_k0obj.size() * 4));
     PRK_TRY(up(S.d_k0tri0, S.h_k0tri0.data(), S.h_k0tri0.size() * 4));
-    PRK_TRY(up(S.d_big, S.h_big.data(), S.h_big.size() * 4));
+    PRK_TRY(up(S.d_big_lds, S.h_big_lds.data(), S.h_big_lds.size() * 4));
+    PRK_TRY(up(S.d_big_gl, S.h_big_gl.data(), S.h_big_gl.size() * 4));
+    PRK_TRY(up(S.d_big_off, S.h_big_off.data(), S.h_big_off.size() * 8));
+    PRK_TRY(up(S.d_big_cap, S.h_big_cap.data(), S.h_big_cap.size() * 4));
     PRK_TRY(up(S.d_k1src, S.h_k1src.data(), S.h_k1src.size() * 4));
     PRK_TRY(up(S.d_edges_in, c->pend_edges.data(), c->pend_edges.size() * sizeof(prk_edge)));
     PRK_TRY(up(S.d_spans_in, c->pend_spans.data(), c->pend_spans.size() * sizeof(prk_span)));
+    if (ngl) PRK_TRY(S.d_pool.ensure(pool * 4));
     uint32_t modes = 0;  // the pass's span kinds: bit per Mode
     for (const auto &d : draws) modes |= 1u << d.mode;
     const bool scalar = (modes & ~(1u << prk::MODE_AVX)) != 0;
-    // FillEdgeTable per triangle: counts, scan, edges + MergeSort keys.
+    // FillEdgeTable per triangle: counts, scans, edges + MergeSort keys.
     const size_t es = std::max<size_t>(3 * (size_t)nt, 1);
     PRK_TRY(S.d_ecnt.ensure(((size_t)nt + 1) * 4));
     PRK_TRY(S.d_escan.ensure(((size_t)nt + 1) * 4));
+    PRK_TRY(S.d_rcnt.ensure(((size_t)nt + 1) * 8));
+    PRK_TRY(S.d_rscan.ensure(((size_t)nt + 1) * 8));
     PRK_TRY(S.d_edges.ensure(es * 112));  // prk_spans.hip ObjEdge
     PRK_TRY(S.d_ekeys.ensure(es * 8));
     PRK_TRY(S.d_ekeys2.ensure(es * 8));
@@ -1452,66 +1515,76 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(S.d_ord.ensure(es * 4));
     PRK_TRY(S.d_err.ensure(16));
     uint32_t *escan = (uint32_t *)S.d_escan.p, *ord = (uint32_t *)S.d_ord.p;
+    unsigned long long *rscan = (unsigned long long *)S.d_rscan.p;
     const uint32_t *total0p = escan + nt;
     size_t tb = 0;
-    if (nt) PRK_TRY(prk_objtri_count(&fp, S.d_objs.p, (const uint32_t *)S.d_k0obj.p,
-                                     (const uint32_t *)S.d_k0tri0.p, nk0, nt, (uint32_t *)S.d_ecnt.p, s));
-    else PRK_TRY(hipMemsetAsync(S.d_ecnt.p, 0, 4, s));
+    auto temp = [&](size_t b) -> hipError_t { return S.d_temp.ensure(std::max<size_t>(b, 16)); };
+    if (nt) {
+        PRK_TRY(prk_objtri_count(&fp, S.d_objs.p, (const uint32_t *)S.d_k0obj.p, (const uint32_t *)S.d_k0tri0.p, nk0,
+                                 nt, (uint32_t *)S.d_ecnt.p, (unsigned long long *)S.d_rcnt.p, s));
+    } else {
+        PRK_TRY(hipMemsetAsync(S.d_ecnt.p, 0, 4, s));
+        PRK_TRY(hipMemsetAsync(S.d_rcnt.p, 0, 8, s));
+    }
     PRK_TRY(prk_scan_u32((const uint32_t *)S.d_ecnt.p, escan, nt + 1, nullptr, &tb, s));
-    PRK_TRY(S.d_temp.ensure(std::max<size_t>(tb, 16)));
+    PRK_TRY(temp(tb));
     PRK_TRY(prk_scan_u32((const uint32_t *)S.d_ecnt.p, escan, nt + 1, S.d_temp.p, &tb, s));
+    PRK_TRY(prk_scan_u64((const unsigned long long *)S.d_rcnt.p, rscan, nt + 1, nullptr, &tb, s));
+    PRK_TRY(temp(tb));
+    PRK_TRY(prk_scan_u64((const unsigned long long *)S.d_rcnt.p, rscan, nt + 1, S.d_temp.p, &tb, s));
     PRK_TRY(prk_objtri_emit(&fp, S.d_objs.p, (const uint32_t *)S.d_k0obj.p, (const uint32_t *)S.d_k0tri0.p, nk0, nt,
-                            escan, S.d_edges.p, S.d_ekeys.p, (uint32_t *)S.d_evals.p, s));
-    PRK_TRY(hipMemcpyAsync(S.h_rb, total0p, 4, hipMemcpyDeviceToHost, s));
+                            escan, pbits, ybits, c->H, S.d_edges.p, S.d_ekeys.p, (uint32_t *)S.d_evals.p, s));
+    if (nt) {  // MergeSort of every object (one radix sort of the padded keys, prk_spans.hip)
+        const uint32_t end_bit = obits + ybits + pbits;
+        PRK_TRY(prk_obj_sort(S.d_ekeys.p, (uint32_t *)S.d_evals.p, S.d_ekeys2.p, ord, 3 * nt, end_bit, nullptr, &tb,
+                             s));
+        PRK_TRY(temp(tb));
+        PRK_TRY(prk_obj_sort(S.d_ekeys.p, (uint32_t *)S.d_evals.p, S.d_ekeys2.p, ord, 3 * nt, end_bit, S.d_temp.p,
+                             &tb, s));
+    }
+    // Span slots: each object's bound, exclusive-scanned into its first slot.
+    PRK_TRY(S.d_bound.ensure(((size_t)nobj + 1) * 8));
+    PRK_TRY(S.d_oslot.ensure(((size_t)nobj + 1) * 8));
+    unsigned long long *oslot = (unsigned long long *)S.d_oslot.p;
+    PRK_TRY(prk_obj_bound(&fp, S.d_objs.p, nobj, rscan, S.d_edges_in.p, (unsigned long long *)S.d_bound.p, s));
+    PRK_TRY(prk_scan_u64((const unsigned long long *)S.d_bound.p, oslot, nobj + 1, nullptr, &tb, s));
+    PRK_TRY(temp(tb));
+    PRK_TRY(prk_scan_u64((const unsigned long long *)S.d_bound.p, oslot, nobj + 1, S.d_temp.p, &tb, s));
+    PRK_TRY(hipMemcpyAsync(S.h_rb, oslot + nobj, 8, hipMemcpyDeviceToHost, s));
     PRK_TRY(hipMemsetAsync(S.d_err.p, 0, 4, s));
     PRK_TRY(hipStreamSynchronize(s));
-    const uint32_t total0 = S.h_rb[0];
-    if (total0) {  // MergeSort of every object (one radix sort, prk_spans.hip)
-        PRK_TRY(prk_obj_sort(S.d_ekeys.p, (uint32_t *)S.d_evals.p, S.d_ekeys2.p, ord, total0, nk0, nullptr, &tb, s));
-        PRK_TRY(S.d_temp.ensure(std::max<size_t>(tb, 16)));
-        PRK_TRY(prk_obj_sort(S.d_ekeys.p, (uint32_t *)S.d_evals.p, S.d_ekeys2.p, ord, total0, nk0, S.d_temp.p, &tb, s));
-    }
-    const uint32_t nwork = total0 + (uint32_t)nk1;
-    PRK_TRY(S.d_work.ensure(std::max<size_t>(nwork, 1) * 112));
-    PRK_TRY(S.d_cnt.ensure(((size_t)nobj + 1) * 4));
-    PRK_TRY(S.d_off.ensure(((size_t)nobj + 1) * 4));
-    uint32_t *cnt = (uint32_t *)S.d_cnt.p, *off = (uint32_t *)S.d_off.p;
-    PRK_TRY(hipMemsetAsync(cnt, 0, ((size_t)nobj + 1) * 4, s));
-    auto walk = [&](int pass) -> hipError_t {  // the working copy is stepped by the walk: re-made per pass
-        hipError_t e = prk_obj_gather(S.d_edges.p, ord, total0p, S.d_edges_in.p, (const uint32_t *)S.d_k1src.p,
-                                      (uint32_t)nk1, S.d_work.p, nwork, s);
-        if (e == hipSuccess)
-            e = prk_obj_walk(&fp, S.d_objs.p, nobj, (const uint32_t *)S.d_big.p, nbig, escan, total0p, S.d_work.p,
-                             pass, cnt, off, S.d_recs.p, scalar ? S.d_srecs.p : nullptr, S.d_pos.p,
-                             (uint32_t *)S.d_span_tri.p, S.d_spans_in.p, (uint32_t *)S.d_err.p, s);
-        return e;
-    };
-    PRK_TRY(walk(0));
-    PRK_TRY(prk_scan_u32(cnt, off, nobj + 1, nullptr, &tb, s));
-    PRK_TRY(S.d_temp.ensure(std::max<size_t>(tb, 16)));
-    PRK_TRY(prk_scan_u32(cnt, off, nobj + 1, S.d_temp.p, &tb, s));
-    PRK_TRY(hipMemcpyAsync(S.h_rb, off + nobj, 4, hipMemcpyDeviceToHost, s));
-    PRK_TRY(hipMemcpyAsync(S.h_rb + 1, S.d_err.p, 4, hipMemcpyDeviceToHost, s));
-    PRK_TRY(hipStreamSynchronize(s));
-    const uint32_t nspan = S.h_rb[0];
-    if (S.h_rb[1]) return PRK_ERR_UNSUPPORTED;  // an object's active list outgrew a wave's LDS
-    if (nspan >= prk::kMaxPairs) return PRK_ERR_UNSUPPORTED;  // 31-bit span tags
-    const size_t ns = std::max<uint32_t>(nspan, 1);
+    uint64_t nslot64;
+    std::memcpy(&nslot64, S.h_rb, 8);
+    if (nslot64 >= prk::kMaxPairs) return PRK_ERR_LIMIT;  // 31-bit span tags
+    const uint32_t nslot = (uint32_t)nslot64;
+    const size_t ns = std::max<uint32_t>(nslot, 1);
     PRK_TRY(S.d_recs.ensure(ns * 64));
     PRK_TRY(S.d_pos.ensure(ns * 16));
     PRK_TRY(S.d_span_tri.ensure(ns * 4));
     if (scalar) PRK_TRY(S.d_srecs.ensure(ns * 96));  // DrawModel span records (prk_spans.hip ScSpanRecG)
-    PRK_TRY(walk(1));
-    PRK_TRY(S.d_scnt.ensure(((size_t)nspan + 1) * 4));
-    PRK_TRY(S.d_soff.ensure(((size_t)nspan + 1) * 4));
+    // slots no span takes stay row -1: binned nowhere
+    PRK_TRY(hipMemsetAsync(S.d_pos.p, 0xFF, ns * 16, s));
+    const uint32_t nwork = 3 * nt + (uint32_t)nk1;
+    PRK_TRY(S.d_work.ensure(std::max<size_t>(nwork, 1) * 112));
+    PRK_TRY(prk_obj_gather(S.d_edges.p, ord, total0p, S.d_edges_in.p, (const uint32_t *)S.d_k1src.p, (uint32_t)nk1,
+                           S.d_work.p, nwork, s));
+    PRK_TRY(prk_obj_walk(&fp, S.d_objs.p, nobj, (const uint32_t *)S.d_big_lds.p, nlds, lcap,
+                         (const uint32_t *)S.d_big_gl.p, (const unsigned long long *)S.d_big_off.p,
+                         (const uint32_t *)S.d_big_cap.p, ngl, (int32_t *)S.d_pool.p, escan, total0p, S.d_work.p,
+                         oslot, S.d_recs.p, scalar ? S.d_srecs.p : nullptr, S.d_pos.p, (uint32_t *)S.d_span_tri.p,
+                         S.d_spans_in.p, (uint32_t *)S.d_err.p, s));
+    PRK_TRY(S.d_scnt.ensure(((size_t)nslot + 1) * 4));
+    PRK_TRY(S.d_soff.ensure(((size_t)nslot + 1) * 4));
     uint32_t *scnt = (uint32_t *)S.d_scnt.p, *soff = (uint32_t *)S.d_soff.p;
-    PRK_TRY(prk_span_count(&fp, S.d_pos.p, nspan, scnt, s));
-    PRK_TRY(prk_scan_u32(scnt, soff, nspan + 1, nullptr, &tb, s));
-    PRK_TRY(S.d_temp.ensure(std::max<size_t>(tb, 16)));
-    PRK_TRY(prk_scan_u32(scnt, soff, nspan + 1, S.d_temp.p, &tb, s));
-    uint32_t total = 0;
-    PRK_TRY(hipMemcpyAsync(&total, soff + nspan, 4, hipMemcpyDeviceToHost, s));
+    PRK_TRY(prk_span_count(&fp, S.d_pos.p, nslot, scnt, s));
+    PRK_TRY(prk_scan_u32(scnt, soff, nslot + 1, nullptr, &tb, s));
+    PRK_TRY(temp(tb));
+    PRK_TRY(prk_scan_u32(scnt, soff, nslot + 1, S.d_temp.p, &tb, s));
+    PRK_TRY(hipMemcpyAsync(S.h_rb + 2, soff + nslot, 4, hipMemcpyDeviceToHost, s));
+    PRK_TRY(hipMemcpyAsync(S.h_rb + 3, S.d_err.p, 4, hipMemcpyDeviceToHost, s));
     PRK_TRY(hipStreamSynchronize(s));
+    const uint32_t total = S.h_rb[2];
+    if (S.h_rb[3]) return PRK_ERR_DEVICE;  // a walk outside its LDS list or span slots (never)
     c->stats.triangles = T;
     c->stats.tiles = ntiles;
     c->stats.bin_entries = total;
@@ -1522,10 +1595,10 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(S.d_vals_b.ensure(ne * 4));
     PRK_TRY(S.d_offs.ensure(((size_t)ntiles + 1) * 4));
     size_t sb = 0;
-    PRK_TRY(prk_span_bin(&fp, S.d_pos.p, nspan, soff, total, (uint32_t *)S.d_keys_a.p, (uint32_t *)S.d_vals_a.p,
+    PRK_TRY(prk_span_bin(&fp, S.d_pos.p, nslot, soff, total, (uint32_t *)S.d_keys_a.p, (uint32_t *)S.d_vals_a.p,
                          (uint32_t *)S.d_keys_b.p, (uint32_t *)S.d_vals_b.p, (uint32_t *)S.d_offs.p, nullptr, &sb, s));
-    PRK_TRY(S.d_temp.ensure(std::max<size_t>(sb, 16)));
-    PRK_TRY(prk_span_bin(&fp, S.d_pos.p, nspan, soff, total, (uint32_t *)S.d_keys_a.p, (uint32_t *)S.d_vals_a.p,
+    PRK_TRY(temp(sb));
+    PRK_TRY(prk_span_bin(&fp, S.d_pos.p, nslot, soff, total, (uint32_t *)S.d_keys_a.p, (uint32_t *)S.d_vals_a.p,
                          (uint32_t *)S.d_keys_b.p, (uint32_t *)S.d_vals_b.p, (uint32_t *)S.d_offs.p, S.d_temp.p, &sb,
                          s));
     PRK_TRY(S.d_nwin.ensure((size_t)ntiles * 4));
@@ -1635,7 +1708,18 @@ int prk_get_device(prk_context *c, int32_t *device, void **stream) {
 }
 
 // prk_dist.hip: gathers read the band's finished frame (library-internal).
-__attribute__((visibility("hidden"))) int prk_resolve_pending(prk_context *c) { return c ? resolve_count(c) : PRK_ERR_ARG; }
+// The pending count is resolved first (an overflowed frame is re-run on its
+// own flush stream), then `stream` (the gather's, any stream of the
+// context's device) waits for the end of the context's last frame.
+__attribute__((visibility("hidden"))) int prk_resolve_pending(prk_context *c, void *stream) {
+    if (!c) return PRK_ERR_ARG;
+    RESOLVE_COUNT(c);
+    if (stream && c->read_rec) {
+        PRK_TRY(hipSetDevice(c->device));
+        PRK_TRY(hipStreamWaitEvent((hipStream_t)stream, c->read_ev, 0));
+    }
+    return PRK_OK;
+}
 
 int prk_synchronize(prk_context *c) {
     if (!c) return PRK_ERR_ARG;

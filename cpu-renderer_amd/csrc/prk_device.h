@@ -54,7 +54,14 @@ struct DrawRec {
 // 2508) instead of -L.X, and the z-test is predicate 29, GE_OQ (3205):
 // z >= zbuf, so among equal z the LATEST fragment wins (and it beats an equal
 // prior z).
-enum : uint32_t { DRAW_ST = 1u };
+// DRAW_RAWCOL / DRAW_WHITELIT: what FillEdgeTable left in MinColor for an
+// untextured non-Phong DrawModel (MODE_SC_GOURAUD), which depends on
+// FillEdgeTable's own inputs, not on the draw's: PhongShading != 0 stores the
+// raw vertex colours (projekt.cpp:4012-4019, so DrawModel interpolates them
+// unlit); PhongShading == 0 lights them per vertex (4020-4063), from a white
+// base when Object->Bitmap is set (4034-4054, DRAW_WHITELIT), else from the
+// vertex colour.  Every other mode's output does not depend on them.
+enum : uint32_t { DRAW_ST = 1u, DRAW_RAWCOL = 2u, DRAW_WHITELIT = 4u };
 // Span path (whole-object AETs): SpanPos flags of a DrawModel (scalar) span,
 // whose mode sits at bits 8..15, and the first word of its FillLineOptimized
 // record slot (no AVX record has bit 31 set: texture indices are < 2^15).
@@ -549,7 +556,19 @@ __device__ __forceinline__ void tri_edges(const TriRaw<M> &r, const DrawRec &d, 
             }
             E.N0 = nrm[mi].x; E.N1 = nrm[mi].y; E.N2 = nrm[mi].z;
             MaxN[0] = nrm[ma].x; MaxN[1] = nrm[ma].y; MaxN[2] = nrm[ma].z;
+        } else if (!kTex && (d.flags & DRAW_RAWCOL)) {  // FillEdgeTable(..., Phong = 1): raw colours (4014-4015)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) { MinC[c] = col[mi][c]; MaxC[c] = col[ma][c]; }
         } else if (!kTex) {  // Gouraud vertex lighting 4020-4063 (untextured only reaches output)
+            // Object->Bitmap set: Hadamard(V4(1,1,1,1), .) replaces the vertex
+            // colour (4034-4054); 1.0f * x == x, so a white base is exact
+            const bool white = (d.flags & DRAW_WHITELIT) != 0;
+            float cmi[4], cma[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                cmi[c] = white ? 1.0f : col[mi][c];
+                cma[c] = white ? 1.0f : col[ma][c];
+            }
             for (uint32_t li = 0; li < fp.light_count; ++li) {
                 V3 LP = V3{fp.lp[li][0], fp.lp[li][1], fp.lp[li][2]};
                 V3 FVL = nrm_rcp(V3{LP.x - FirstCam.x, LP.y - FirstCam.y, LP.z - FirstCam.z});
@@ -557,16 +576,16 @@ __device__ __forceinline__ void tri_edges(const TriRaw<M> &r, const DrawRec &d, 
                 if (li == 0) {
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
-                        MinC[c] = col[mi][c] * fp.amb[c];
-                        MaxC[c] = col[ma][c] * fp.amb[c];
+                        MinC[c] = cmi[c] * fp.amb[c];
+                        MaxC[c] = cma[c] * fp.amb[c];
                     }
                 }
                 float FD = clamp01((FVL.x * nrm[mi].x + FVL.y * nrm[mi].y) + FVL.z * nrm[mi].z);
                 float SD = clamp01((SVL.x * nrm[ma].x + SVL.y * nrm[ma].y) + SVL.z * nrm[ma].z);
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    MinC[c] = clamp01(MinC[c] + FD * (col[mi][c] * fp.li[li][c]));
-                    MaxC[c] = clamp01(MaxC[c] + SD * (col[ma][c] * fp.li[li][c]));
+                    MinC[c] = clamp01(MinC[c] + FD * (cmi[c] * fp.li[li][c]));
+                    MaxC[c] = clamp01(MaxC[c] + SD * (cma[c] * fp.li[li][c]));
                 }
             }
         }

@@ -26,7 +26,7 @@
 
 static_assert(PRK_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
 
-extern "C" int prk_resolve_pending(prk_context *c);  // prk_api.hip (library-internal)
+extern "C" int prk_resolve_pending(prk_context *c, void *stream);  // prk_api.hip (library-internal)
 namespace {
 
 struct Rccl {
@@ -82,15 +82,18 @@ struct Band {
     hipStream_t stream;
 };
 
-int band_of(prk_context *ctx, int32_t rank, int32_t nranks, Band &B) {
-    int rc = prk_resolve_pending(ctx);  // the band's last frame is final (a deferred re-run queued first)
+// `stream`: the stream the band's strip is read on (NULL: the context's own);
+// it is made to wait for the end of the band's last frame — whatever stream
+// that frame (or its deferred re-run, queued here first) ran on.
+int band_of(prk_context *ctx, int32_t rank, int32_t nranks, Band &B, void *stream = nullptr) {
+    void *s = nullptr;
+    int rc = prk_get_device(ctx, &B.device, &s);
+    if (rc != PRK_OK) return rc;
+    B.stream = stream ? (hipStream_t)stream : (hipStream_t)s;
+    rc = prk_resolve_pending(ctx, (void *)B.stream);
     if (rc != PRK_OK) return rc;
     rc = prk_get_target(ctx, &B.color, &B.pitch, &B.z, &B.W, &B.H, &B.row0, &B.row1);
     if (rc != PRK_OK) return rc;
-    void *s = nullptr;
-    rc = prk_get_device(ctx, &B.device, &s);
-    if (rc != PRK_OK) return rc;
-    B.stream = (hipStream_t)s;
     int32_t a, b;
     band(B.H, rank, nranks, a, b);
     if (B.row0 != a || B.row1 != b) return PRK_ERR_ARG;  // the target is not this rank's band
@@ -243,11 +246,11 @@ int prk_gather_frame(prk_context *ctx, prk_comm *comm, int32_t with_z, void *fra
     const Rccl &R = rccl();
     if (!R.ok) return PRK_ERR_UNSUPPORTED;
     Band B;
-    int rc = band_of(ctx, comm->rank, comm->nranks, B);
+    int rc = band_of(ctx, comm->rank, comm->nranks, B, stream);
     if (rc != PRK_OK) return rc;
     if (comm->rank == 0 && !frame_ok(B, frame_color, frame_pitch, with_z, frame_z)) return PRK_ERR_ARG;
     if (comm->rank != 0 && B.pitch != B.W * 4) return PRK_ERR_UNSUPPORTED;  // strips go out as packed rows
-    hipStream_t s = stream ? (hipStream_t)stream : B.stream;
+    hipStream_t s = B.stream;
     rc = hstat(hipSetDevice(B.device));
     if (rc != PRK_OK) return rc;
     if (comm->rank == 0) {

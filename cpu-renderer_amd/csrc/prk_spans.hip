@@ -282,21 +282,38 @@ __device__ __forceinline__ ObjEdge span_end_in(const SpanEndIn &e) {  // FillLin
 // ---------------------------------------------------------------------------
 // Which of a triangle's edges {0,1},{1,2},{2,0} FillEdgeTable writes (bit k):
 // none unless it passes the back-face test (3926-3943), then those with
-// MaxY > 0 (3968) and MinY != MaxY (4066) — tri_edges' `vis`.
-__device__ __forceinline__ uint32_t tri_vis_mask(const FrameParams &fp, const DrawRec &d, uint32_t gt) {
+// MaxY > 0 (3968) and MinY != MaxY (4066) — tri_edges' `vis`.  rows: the
+// rows [max(YMin, row_lo), min(YMax, row_hi)) its visible edges can be
+// active on (YMax = round(MaxY) 3988, YMin = Maximum(0, round(MinY)) 3999),
+// summed — twice the most spans they can take part in.
+__device__ __forceinline__ uint32_t tri_vis_mask(const FrameParams &fp, const DrawRec &d, uint32_t gt,
+                                                 int32_t row_lo, int32_t row_hi, uint32_t *rows = nullptr) {
     V3 cam[3], proj[3];
     load_positions(d, gt, fp, cam, proj);
     if (!front_facing(proj)) return 0u;
-    uint32_t m = 0;
+    uint32_t m = 0, r = 0;
 #pragma unroll
     for (int e = 0; e < 3; ++e) {
         const float y0 = proj[e].y, y1 = proj[(e + 1) % 3].y;
         const bool sw = y0 > y1;  // 3957-3966
         const float mn = sw ? y1 : y0, mx = sw ? y0 : y1;
-        if (mx > 0 && mn - mx != 0) m |= 1u << e;
+        if (mx > 0 && mn - mx != 0) {
+            m |= 1u << e;
+            const float rm = (float)round_s32(mn);
+            const int32_t ymin = (int32_t)(0.0f > rm ? 0.0f : rm), ymax = round_s32(mx);
+            r += (uint32_t)max(0, min(ymax, row_hi) - max(ymin, row_lo));
+        }
     }
+    if (rows) *rows = r;
     return m;
 }
+
+// Rows a draw's spans can lie on: [row0, min(H, row1)) of the pass's band,
+// from row0 - 1 for DrawModel (its one-past-the-row store, 423-538).
+__device__ __forceinline__ int32_t draw_row_lo(const FrameParams &fp, const DrawRec &d) {
+    return d.mode != MODE_AVX ? fp.row0 - 1 : fp.row0;
+}
+__device__ __forceinline__ int32_t draw_row_hi(const FrameParams &fp) { return min(fp.H, fp.row1); }
 
 // The kind-0 object (index into the pass's kind-0 list) of object triangle s.
 __device__ __forceinline__ uint32_t obj_of_tri(const uint32_t *__restrict__ k0tri0, uint32_t nk0, uint32_t s) {
@@ -314,11 +331,16 @@ __device__ __forceinline__ uint32_t obj_of_tri(const uint32_t *__restrict__ k0tr
 // on strict '<').  So entry i of n precedes entry j of equal YMin iff, at the
 // recursion node that separates them, i is the first of a two-entry run or
 // lies in Half1: the path of branch bits from the root (Half1 = 0, Half0 = 1,
-// run position last), left-aligned in kPathBits, orders ties exactly.
-constexpr int kPathBits = 23;  // objects of up to 2^22 edges
-__device__ __forceinline__ uint32_t merge_path(uint32_t i, uint32_t n) {
-    uint32_t first = 0, count = n, path = 0;
-    int bits = 0;
+// run position last), left-aligned in `pbits` (more than the recursion's
+// depth, ceil(log2 n)), orders ties exactly.
+struct SortKeyBits {
+    uint32_t pbits, ybits;  // path bits, YMin bits (YMin clamped to ycap = H: rows >= H are never walked)
+    int32_t ycap;
+};
+__device__ __forceinline__ uint64_t merge_path(uint32_t i, uint32_t n, uint32_t pbits) {
+    uint32_t first = 0, count = n;
+    uint64_t path = 0;
+    uint32_t bits = 0;
     while (count > 2) {
         const uint32_t h0 = count / 2;  // Half0 = [first, first + h0)
         if (i < first + h0) {
@@ -335,29 +357,34 @@ __device__ __forceinline__ uint32_t merge_path(uint32_t i, uint32_t n) {
         path = (path << 1) | (i - first);
         ++bits;
     }
-    return path << (kPathBits - bits);
+    return path << (pbits - bits);
 }
 
-// Visible edge count of every object triangle (ecnt[ntri] = 0: the scan's
-// total).
+// Visible edge count (ecnt) and active-row count (rcnt) of every object
+// triangle (ecnt[ntri] = rcnt[ntri] = 0: the scans' totals).
 __global__ void k_objtri_count(FrameParams fp, const ObjDesc *__restrict__ objs, const uint32_t *__restrict__ k0obj,
                                const uint32_t *__restrict__ k0tri0, uint32_t nk0, uint32_t ntri,
-                               uint32_t *__restrict__ ecnt) {
+                               uint32_t *__restrict__ ecnt, unsigned long long *__restrict__ rcnt) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s > ntri) return;
     if (s == ntri) {
         ecnt[s] = 0;
+        rcnt[s] = 0;
         return;
     }
     const ObjDesc od = objs[k0obj[obj_of_tri(k0tri0, nk0, s)]];
     const DrawRec &d = fp.draws[od.draw];
     const uint32_t g = od.g0 + (s - od.tri0);
-    ecnt[s] = (uint32_t)__popc(tri_vis_mask(fp, d, d.geom_tri0 + (g - d.first_global)));
+    uint32_t rows = 0;
+    ecnt[s] = (uint32_t)__popc(tri_vis_mask(fp, d, d.geom_tri0 + (g - d.first_global), draw_row_lo(fp, d),
+                                            draw_row_hi(fp), &rows));
+    rcnt[s] = rows;
 }
 
 // The visible edges of every object triangle (FillEdgeTable 3947-4111, in the
 // reference's order: triangle by triangle, edges {0,1},{1,2},{2,0}) at
-// escan[s], with their MergeSort keys (object, min(YMin, 65535), path).
+// escan[s], with their MergeSort keys (object, min(YMin, H), path); the key
+// slots past the visible edges keep the all-ones padding (sorted last).
 template <int M>
 __device__ __forceinline__ void objtri_edges(const FrameParams &fp, const DrawRec &d, uint32_t gt, ObjEdge *out,
                                              uint32_t mask) {
@@ -374,7 +401,7 @@ __device__ __forceinline__ void objtri_edges(const FrameParams &fp, const DrawRe
 
 __global__ void k_objtri_emit(FrameParams fp, const ObjDesc *__restrict__ objs, const uint32_t *__restrict__ k0obj,
                               const uint32_t *__restrict__ k0tri0, uint32_t nk0, uint32_t ntri,
-                              const uint32_t *__restrict__ escan, ObjEdge *__restrict__ edges,
+                              const uint32_t *__restrict__ escan, SortKeyBits kb, ObjEdge *__restrict__ edges,
                               unsigned long long *__restrict__ keys, uint32_t *__restrict__ vals) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= ntri) return;
@@ -383,7 +410,7 @@ __global__ void k_objtri_emit(FrameParams fp, const ObjDesc *__restrict__ objs, 
     const DrawRec &d = fp.draws[od.draw];
     const uint32_t g = od.g0 + (s - od.tri0);
     const uint32_t gt = d.geom_tri0 + (g - d.first_global);
-    const uint32_t mask = tri_vis_mask(fp, d, gt);
+    const uint32_t mask = tri_vis_mask(fp, d, gt, 0, 0);
     if (!mask) return;
     const uint32_t e0 = escan[s];
     switch (d.mode) {
@@ -396,11 +423,41 @@ __global__ void k_objtri_emit(FrameParams fp, const ObjDesc *__restrict__ objs, 
     const uint32_t ob = escan[od.tri0], n = escan[od.tri0 + od.tris] - ob;
     const uint32_t c = (uint32_t)__popc(mask);
     for (uint32_t k = 0; k < c; ++k) {
-        const uint32_t ymin = (uint32_t)min(edges[e0 + k].YMin, 65535);
-        keys[e0 + k] = ((unsigned long long)j << (16 + kPathBits)) | ((unsigned long long)ymin << kPathBits) |
-                       merge_path(e0 + k - ob, n);
+        const uint64_t ymin = (uint64_t)min(edges[e0 + k].YMin, kb.ycap);
+        keys[e0 + k] = ((uint64_t)j << (kb.ybits + kb.pbits)) | (ymin << kb.pbits) |
+                       merge_path(e0 + k - ob, n, kb.pbits);
         vals[e0 + k] = e0 + k;
     }
+}
+
+// Span slots of every object: the most spans its walk can emit — a span
+// pairs two entries active on its row, an entry is active on the rows
+// [YMin, YMax) of its edge walked — so half its edges' active rows (kind 0:
+// from the per-triangle counts; kind 1: its caller edges; kind 2: one).
+__global__ void k_obj_bound(FrameParams fp, const ObjDesc *__restrict__ objs, uint32_t nobj,
+                            const unsigned long long *__restrict__ rscan, const EdgeIn *__restrict__ edges_in,
+                            unsigned long long *__restrict__ bound) {
+    const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o > nobj) return;
+    if (o == nobj) {
+        bound[o] = 0;
+        return;
+    }
+    const ObjDesc od = objs[o];
+    unsigned long long b = 1;
+    if (od.kind == 0) {
+        b = (rscan[od.tri0 + od.tris] - rscan[od.tri0]) / 2;
+    } else if (od.kind == 1) {
+        const DrawRec &d = fp.draws[od.draw];
+        const int32_t lo = draw_row_lo(fp, d), hi = draw_row_hi(fp);
+        unsigned long long r = 0;
+        for (uint32_t e = 0; e < od.nsrc; ++e) {
+            const EdgeIn &E = edges_in[od.src + e];
+            r += (unsigned long long)max(0, min(E.YMax, hi) - max(E.YMin, lo));
+        }
+        b = r / 2;
+    }
+    bound[o] = b;
 }
 
 // The walk's working copy of every object's edges: the triangle edges in
@@ -430,7 +487,7 @@ __device__ __forceinline__ void obj_range(const ObjDesc &od, const uint32_t *__r
     }
 }
 
-// One span of the pair (L, R) at Row (pass 1 writes it at `at`).
+// One span of the pair (L, R) at Row, written at span slot `at` (when `write`).
 template <int M>
 __device__ __forceinline__ bool emit_span(const FrameParams &fp, const ObjEdge &L, const ObjEdge &R, int32_t Row,
                                           const DrawRec &d, bool st, uint32_t g0, bool write, uint32_t at,
@@ -460,16 +517,18 @@ __device__ __forceinline__ bool emit_span(const FrameParams &fp, const ObjEdge &
 }
 
 // The AET walk of one object by one thread (small objects, caller edge
-// lists): E = its n edges, sorted (kind 0) or as given (kind 1).
+// lists): E = its n edges, sorted (kind 0) or as given (kind 1).  Its spans
+// go to slots [base, base + bound) in emission order.
 template <int M>
 __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const DrawRec &d, ObjEdge *__restrict__ E,
-                            uint32_t n, int pass, uint32_t base, uint32_t &emitted, SpanRecG *__restrict__ recs,
+                            uint32_t n, uint32_t base, uint32_t bound, SpanRecG *__restrict__ recs,
                             ScSpanRecG *__restrict__ srecs, SpanPos *__restrict__ pos,
-                            uint32_t *__restrict__ span_tri) {
+                            uint32_t *__restrict__ span_tri, uint32_t *__restrict__ err) {
     constexpr bool kScalar = M != MODE_AVX;
     const bool st = (d.flags & DRAW_ST) != 0;
     const bool given = od.kind == 1;  // a caller's edge list: scanned whole every row
     if (n == 0) return;
+    uint32_t emitted = 0;
     // The AET walk of DrawModelOptimized(RenderQueue,...) (3626-3869) /
     // DrawModel (173-598): the same list logic.
     const int32_t FirstRow = E[0].YMin;
@@ -550,9 +609,11 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
         int32_t Cur = Head, Next = E[Cur].Next;
         while (Next >= 0) {
             if (Row >= RowLo &&  // a span of this pass's rows (3759-3809 / 298-538)
-                emit_span<M>(fp, E[Cur], E[Next], Row, d, st, od.g0, pass != 0, base + emitted, recs, srecs, pos,
-                             span_tri))
+                emit_span<M>(fp, E[Cur], E[Next], Row, d, st, od.g0, emitted < bound, base + emitted, recs, srecs,
+                             pos, span_tri)) {
+                if (emitted >= bound) atomicOr(err, 2u);  // (never: the bound holds every span)
                 ++emitted;
+            }
             obj_step<M>(E[Cur]);  // 3811-3829
             obj_step<M>(E[Next]);
             if (E[Cur].X > E[Next].X) {  // 3831-3841
@@ -588,26 +649,22 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
 __global__ void __launch_bounds__(64) k_obj_walk(FrameParams fp, const ObjDesc *__restrict__ objs, uint32_t nobj,
                                                  const uint32_t *__restrict__ escan,
                                                  const uint32_t *__restrict__ total0p, ObjEdge *__restrict__ work,
-                                                 int pass, uint32_t *__restrict__ counts,
-                                                 const uint32_t *__restrict__ offs, SpanRecG *__restrict__ recs,
-                                                 ScSpanRecG *__restrict__ srecs, SpanPos *__restrict__ pos,
-                                                 uint32_t *__restrict__ span_tri,
-                                                 const SpanIn *__restrict__ spans_in) {
+                                                 const unsigned long long *__restrict__ soff,
+                                                 SpanRecG *__restrict__ recs, ScSpanRecG *__restrict__ srecs,
+                                                 SpanPos *__restrict__ pos, uint32_t *__restrict__ span_tri,
+                                                 const SpanIn *__restrict__ spans_in, uint32_t *__restrict__ err) {
     const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
     if (o >= nobj) return;
     const ObjDesc od = objs[o];
     if (od.kind != 2 && (od.k1off & kObjWave)) return;  // k_obj_walk_wave's
     const DrawRec &d = fp.draws[od.draw];
     const bool st = (d.flags & DRAW_ST) != 0;
-    const uint32_t base = pass ? offs[o] : 0u;
-    uint32_t emitted = 0;
+    const uint32_t base = (uint32_t)soff[o], bound = (uint32_t)(soff[o + 1] - soff[o]);
     if (od.kind == 2) {  // one caller-given span (DoLineRenderWork / DoBufferLineRenderWork)
         const SpanIn sp = spans_in[od.src];
-        if (sp.Row >= fp.row0 && sp.Row < fp.row1 && sp.Row < fp.H &&
-            emit_span<MODE_AVX>(fp, span_end_in(sp.L), span_end_in(sp.R), sp.Row, d, st, od.g0, pass != 0, base,
-                                recs, srecs, pos, span_tri))
-            emitted = 1;
-        if (!pass) counts[o] = emitted;
+        if (sp.Row >= fp.row0 && sp.Row < fp.row1 && sp.Row < fp.H && bound)
+            emit_span<MODE_AVX>(fp, span_end_in(sp.L), span_end_in(sp.R), sp.Row, d, st, od.g0, true, base, recs,
+                                srecs, pos, span_tri);
         return;
     }
     uint32_t e0, n;
@@ -616,7 +673,7 @@ __global__ void __launch_bounds__(64) k_obj_walk(FrameParams fp, const ObjDesc *
     switch (d.mode) {
 #define PRK_WALK_OBJ(MM)                                                                         \
     case MM:                                                                                     \
-        walk_object<MM>(fp, od, d, E, n, pass, base, emitted, recs, srecs, pos, span_tri);       \
+        walk_object<MM>(fp, od, d, E, n, base, bound, recs, srecs, pos, span_tri, err);          \
         break;
         PRK_WALK_OBJ(MODE_AVX)
         PRK_WALK_OBJ(MODE_SC_GOURAUD)
@@ -626,18 +683,22 @@ __global__ void __launch_bounds__(64) k_obj_walk(FrameParams fp, const ObjDesc *
 #undef PRK_WALK_OBJ
         default: break;
     }
-    if (!pass) counts[o] = emitted;
 }
 
 // ---------------------------------------------------------------------------
-// The AET walk of one large object by one wave.  The list lives in LDS as an
-// array in list order (position p = the p-th edge from ListHead) with the
-// fields the list operations read (X, Gradient, Left, YMax) beside each edge
-// index; the edges themselves stay in the working copy.  Per row, exactly
-// the reference's operations (P3 included), as array operations:
-//   insertion (3654-3713)  each new edge, in sorted order, goes before the
-//                          first entry it sorts before (a ballot over the
-//                          list), else to the tail; the tail shifts by one;
+// The AET walk of one large object by one wave.  The list is an array in
+// list order (position p = the p-th edge from ListHead) holding, beside each
+// edge index, the fields the list operations read (X, Gradient, Left, YMax);
+// the edges themselves stay in the working copy.  It lives in LDS for objects
+// of at most `lcap` edges and in device memory (a slice of a pool sized by the
+// object's edge count) beyond that: the list has no length limit, as the
+// reference's pointer list has none.  Per row, exactly the reference's
+// operations (P3 included), as array operations:
+//   insertion (3654-3713)  each new edge goes before the first entry it sorts
+//                          before (by X, Gradient, Left), else to the tail —
+//                          see insert_batch for doing a row's insertions at
+//                          once; one or two (or any with a NaN key) one at a
+//                          time, by a ballot over the list and a shift;
 //   expiry (3715-3749)     entries with YMax <= Row leave, order kept (a
 //                          ballot compaction);
 //   pairing (3751-3869)    entries (2k, 2k+1) pair: span, then both edges
@@ -650,23 +711,239 @@ __global__ void __launch_bounds__(64) k_obj_walk(FrameParams fp, const ObjDesc *
 //                          left-to-right sequence equals the two parallel
 //                          passes.  An odd last entry neither pairs nor steps.
 // ---------------------------------------------------------------------------
-constexpr int kWaveListCap = 4096;
+constexpr int kWaveListArrays = 9;   // int32 arrays of cap + 2 entries each
+constexpr uint32_t kWaveListCapLds = 4096;
 struct WaveList {
-    int32_t idx[kWaveListCap];
-    float x[kWaveListCap], g[kWaveListCap];
-    int32_t left[kWaveListCap], ymax[kWaveListCap];
+    int32_t *idx;
+    float *x, *g;
+    int32_t *left, *ymax;
+    int32_t *aux;  // prefix-max positions, then the row's gap histogram and its exclusive scan
+    int32_t *nb;   // per new edge of the row: its gap
+    int32_t *bk;   // per new edge: its arrival slot in its gap, then its final position
+    int32_t *bk2;  // the row's new edges grouped by gap
+    __device__ __forceinline__ void carve(int32_t *base, uint32_t cap) {
+        const size_t s = (size_t)cap + 2;
+        idx = base;
+        x = reinterpret_cast<float *>(base + s);
+        g = reinterpret_cast<float *>(base + 2 * s);
+        left = base + 3 * s;
+        ymax = base + 4 * s;
+        aux = base + 5 * s;
+        nb = base + 6 * s;
+        bk = base + 7 * s;
+        bk2 = base + 8 * s;
+    }
 };
+
+// The wave's list writes visible to all its lanes: LDS needs no more than the
+// wave's own order; a list in device memory waits for its stores
+// (workgroup scope: the wave is the workgroup, one CU, one L1).
+template <bool GL>
+__device__ __forceinline__ void list_sync() {
+    if (GL) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    } else {
+        wave_lds_sync();
+    }
+}
 
 __device__ __forceinline__ int wave_max_i32(int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
     return v;
 }
+__device__ __forceinline__ int32_t lane_rank(unsigned long long bal) {
+    return (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+}
 
-template <int M>
+// The insertion order as a key.  "Cur sorts before E" (3663-3667) is
+// key(E) > key(Cur) for keys compared (X, Gradient, Left) lexicographically
+// with float compares, once NaNs are mapped out: an entry with a NaN X never
+// compares greater than a new edge (lowest key), one with a NaN Gradient only
+// by X (lowest Gradient and Left).  (New edges with a NaN in their key take
+// the one-at-a-time insertion.)  +0 and -0 compare equal, as in the reference.
+struct LKey {
+    float x, g;
+    int32_t l;
+};
+__device__ __forceinline__ LKey entry_key(float x, float g, int32_t l) {
+    if (x != x) return LKey{-INFINITY, -INFINITY, INT32_MIN};
+    if (g != g) return LKey{x, -INFINITY, INT32_MIN};
+    return LKey{x, g, l};
+}
+__device__ __forceinline__ bool key_gt(const LKey &a, const LKey &b) {
+    return a.x > b.x || (a.x == b.x && (a.g > b.g || (a.g == b.g && a.l > b.l)));
+}
+
+// One new edge E[c] inserted as the reference does (3654-3713): before the
+// first entry it sorts before, else at the tail.
+template <bool GL>
+__device__ __forceinline__ void insert_one(const WaveList &L, int &m, const ObjEdge &C, int32_t c) {
+    const int lane = threadIdx.x & 63;
+    const float cx = C.X, cg = C.G;
+    const int32_t cl = C.Left, cy = C.YMax;
+    int p = m;
+    for (int c0 = 0; c0 < m; c0 += 64) {
+        const int q = c0 + lane;
+        bool b = false;
+        if (q < m) {
+            const float x = L.x[q], g = L.g[q];
+            b = cx < x || (cx == x && (cg < g || (cg == g && cl < L.left[q])));
+        }
+        const unsigned long long bal = __ballot(b);
+        if (bal) {
+            p = c0 + (int)__builtin_ctzll(bal);
+            break;
+        }
+    }
+    for (int top = m; top > p; top -= 64) {  // entries [p, m) move up one, top chunk first
+        const int q = top - 1 - lane;
+        int32_t vi = 0, vl = 0, vy = 0;
+        float vx = 0, vg = 0;
+        if (q >= p) { vi = L.idx[q]; vx = L.x[q]; vg = L.g[q]; vl = L.left[q]; vy = L.ymax[q]; }
+        list_sync<GL>();
+        if (q >= p) { L.idx[q + 1] = vi; L.x[q + 1] = vx; L.g[q + 1] = vg; L.left[q + 1] = vl; L.ymax[q + 1] = vy; }
+        list_sync<GL>();
+    }
+    if (lane == 0) { L.idx[p] = c; L.x[p] = cx; L.g[p] = cg; L.left[p] = cl; L.ymax[p] = cy; }
+    list_sync<GL>();
+    ++m;
+}
+
+// The k new edges of a row (E[c0, c0 + k), in insertion order, no NaN key)
+// inserted at once, with the result of inserting them one by one.  With
+// PM(q) = the maximum key of entries [0, q], the first entry a new edge c
+// sorts before is the first q with PM(q) > key(c), and inserting c there
+// inserts key(c) into the non-decreasing PM sequence at that point (every
+// entry before it is <= key(c), every one after > key(c)): one insertion is an
+// upper-bound insertion into a sorted sequence.  So the final list is the
+// stable merge of the list (its entries weighted by PM) and the new edges
+// ordered by (key, insertion order): new edge c lands at
+//     gap(c) + #{new edges of gap < gap(c)} + #{new edges of its gap ordered before it},
+// gap(c) = the first q with PM(q) > key(c) (m: none), and entry q moves up by
+// #{new edges of gap <= q}.  O(m/64 + k/64) wave steps and a binary search per
+// new edge, instead of a list scan and a shift per new edge.
+template <bool GL>
+__device__ void insert_batch(const WaveList &L, int &m, const ObjEdge *__restrict__ E, uint32_t c0, int k) {
+    const int lane = threadIdx.x & 63;
+    // 1. aux[q] = position of a maximal key of entries [0, q]
+    {
+        LKey ck{-INFINITY, -INFINITY, INT32_MIN};
+        int32_t cp = -1;  // carry: the running maximum (none yet)
+        for (int b0 = 0; b0 < m; b0 += 64) {
+            const int q = b0 + lane;
+            LKey kk{-INFINITY, -INFINITY, INT32_MIN};
+            int32_t kp = q;
+            if (q < m) kk = entry_key(L.x[q], L.g[q], L.left[q]);
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                LKey ok;
+                ok.x = __shfl_up(kk.x, o);
+                ok.g = __shfl_up(kk.g, o);
+                ok.l = __shfl_up(kk.l, o);
+                const int32_t op = __shfl_up(kp, o);
+                if (lane >= o && key_gt(ok, kk)) { kk = ok; kp = op; }
+            }
+            if (cp >= 0 && key_gt(ck, kk)) { kk = ck; kp = cp; }
+            if (q < m) L.aux[q] = kp;
+            const int last = min(63, m - 1 - b0);
+            ck.x = __shfl(kk.x, last);
+            ck.g = __shfl(kk.g, last);
+            ck.l = __shfl(kk.l, last);
+            cp = __shfl(kp, last);
+        }
+    }
+    list_sync<GL>();
+    // 2. nb[t] = gap of new edge t: a binary search over the non-decreasing PM
+    for (int t = lane; t < k; t += 64) {
+        const ObjEdge &C = E[c0 + t];
+        const LKey kc{C.X, C.G, C.Left};
+        int lo = 0, hi = m;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            const int32_t pq = L.aux[mid];
+            if (key_gt(entry_key(L.x[pq], L.g[pq], L.left[pq]), kc)) hi = mid;
+            else lo = mid + 1;
+        }
+        L.nb[t] = lo;
+    }
+    list_sync<GL>();
+    // 3. gap histogram (aux[0, m + 2)), each new edge's arrival slot in its gap
+    for (int q = lane; q < m + 2; q += 64) L.aux[q] = 0;
+    list_sync<GL>();
+    for (int t = lane; t < k; t += 64) L.bk[t] = atomicAdd(&L.aux[L.nb[t]], 1);
+    list_sync<GL>();
+    // 4. exclusive scan: aux[g] = new edges of gaps < g (aux[m + 1] = k)
+    {
+        int32_t carry = 0;
+        for (int b0 = 0; b0 < m + 2; b0 += 64) {
+            const int q = b0 + lane;
+            const int32_t v = q < m + 2 ? L.aux[q] : 0;
+            int32_t inc = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int32_t t = __shfl_up(inc, o);
+                if (lane >= o) inc += t;
+            }
+            if (q < m + 2) L.aux[q] = carry + inc - v;
+            carry += __shfl(inc, 63);
+        }
+    }
+    list_sync<GL>();
+    // 5. the new edges grouped by gap
+    for (int t = lane; t < k; t += 64) L.bk2[L.aux[L.nb[t]] + L.bk[t]] = t;
+    list_sync<GL>();
+    // 6. final positions: gap + new edges of earlier gaps + those of its gap
+    //    ordered before it (smaller key, or an equal key inserted earlier)
+    for (int t = lane; t < k; t += 64) {
+        const ObjEdge &C = E[c0 + t];
+        const LKey kc{C.X, C.G, C.Left};
+        const int gq = L.nb[t];
+        const int32_t s0 = L.aux[gq], h = L.aux[gq + 1] - s0;
+        int32_t r = 0;
+        for (int32_t j = 0; j < h; ++j) {
+            const int32_t u = L.bk2[s0 + j];
+            if (u == t) continue;
+            const ObjEdge &U = E[c0 + u];
+            const LKey ku{U.X, U.G, U.Left};
+            r += (key_gt(kc, ku) || (!key_gt(ku, kc) && u < t)) ? 1 : 0;
+        }
+        L.bk[t] = gq + s0 + r;
+    }
+    list_sync<GL>();
+    // 7. entries move up by the new edges of gaps <= their position, top
+    //    chunk first (an entry only moves up, into slots already read)
+    for (int top = m; top > 0; top -= 64) {
+        const int q = top - 1 - lane;
+        int32_t vi = 0, vl = 0, vy = 0, to = 0;
+        float vx = 0, vg = 0;
+        if (q >= 0) {
+            to = q + L.aux[q + 1];
+            vi = L.idx[q]; vx = L.x[q]; vg = L.g[q]; vl = L.left[q]; vy = L.ymax[q];
+        }
+        list_sync<GL>();
+        if (q >= 0 && to != q) { L.idx[to] = vi; L.x[to] = vx; L.g[to] = vg; L.left[to] = vl; L.ymax[to] = vy; }
+        list_sync<GL>();
+    }
+    // 8. the new edges into the free slots
+    for (int t = lane; t < k; t += 64) {
+        const ObjEdge &C = E[c0 + t];
+        const int32_t at = L.bk[t];
+        L.idx[at] = (int32_t)(c0 + t); L.x[at] = C.X; L.g[at] = C.G; L.left[at] = C.Left; L.ymax[at] = C.YMax;
+    }
+    list_sync<GL>();
+    m += k;
+}
+
+// Emits the wave's spans of one pairing chunk at base + emitted (in list
+// order); a span past the object's bound sets err (the bound is the object's
+// active edge rows / 2, which no walk exceeds).
+template <int M, bool GL>
 __device__ void walk_object_wave(const FrameParams &fp, const ObjDesc &od, const DrawRec &d,
-                                 ObjEdge *__restrict__ E, uint32_t n, int pass, uint32_t base, uint32_t &emitted,
-                                 WaveList &L, SpanRecG *__restrict__ recs, ScSpanRecG *__restrict__ srecs,
+                                 ObjEdge *__restrict__ E, uint32_t n, uint32_t base, uint32_t bound,
+                                 const WaveList &L, SpanRecG *__restrict__ recs, ScSpanRecG *__restrict__ srecs,
                                  SpanPos *__restrict__ pos, uint32_t *__restrict__ span_tri,
                                  uint32_t *__restrict__ err) {
     constexpr bool kScalar = M != MODE_AVX;
@@ -679,44 +956,39 @@ __device__ void walk_object_wave(const FrameParams &fp, const ObjDesc &od, const
     const int32_t FirstRow = E[0].YMin;
     const int32_t MaxY = min(min(MaxRow, fp.H), fp.row1);
     const int32_t RowLo = kScalar ? fp.row0 - 1 : fp.row0;
+    uint32_t emitted = 0;
     int m = 0;         // list length (wave-uniform)
     uint32_t ins = 0;  // next sorted edge to insert
     for (int32_t Row = FirstRow; Row < MaxY; ++Row) {
-        while (ins < n && E[ins].YMin < Row) ++ins;
-        while (ins < n && E[ins].YMin == Row) {  // insertion 3654-3713, in sorted order
-            const float cx = E[ins].X, cg = E[ins].G;
-            const int32_t cl = E[ins].Left, cy = E[ins].YMax;
-            int p = m;
-            for (int c0 = 0; c0 < m; c0 += 64) {
-                const int q = c0 + lane;
-                bool b = false;
-                if (q < m) {
-                    const float x = L.x[q], g = L.g[q];
-                    b = cx < x || (cx == x && (cg < g || (cg == g && cl < L.left[q])));
-                }
-                const unsigned long long bal = __ballot(b);
-                if (bal) {
-                    p = c0 + (int)__builtin_ctzll(bal);
-                    break;
-                }
+        // The row's new edges E[ins, ins + k): YMin == Row, contiguous in the
+        // MergeSort order (entries below Row: none past the first row).
+        int k = 0;
+        for (;;) {
+            const uint32_t i = ins + (uint32_t)lane;
+            const unsigned long long lt = __ballot(i < n && E[i].YMin < Row);
+            ins += (uint32_t)__popcll(lt);
+            if (lt != ~0ull) break;
+        }
+        bool nan = false;
+        for (;;) {
+            const uint32_t i = ins + (uint32_t)k + (uint32_t)lane;
+            bool eq = false;
+            if (i < n) {
+                const ObjEdge &C = E[i];
+                eq = C.YMin == Row;
+                nan |= eq && (C.X != C.X || C.G != C.G);
             }
-            if (m >= kWaveListCap) {  // list longer than LDS holds: the pass fails
-                if (lane == 0) atomicOr(err, 1u);
-                return;
+            const unsigned long long b = __ballot(eq);
+            k += __popcll(b);
+            if (b != ~0ull) break;
+        }
+        if (k > 0) {
+            if (k <= 2 || __any(nan)) {  // insertion 3654-3713, one edge at a time in sorted order
+                for (int t = 0; t < k; ++t) insert_one<GL>(L, m, E[ins + t], (int32_t)(ins + t));
+            } else {
+                insert_batch<GL>(L, m, E, ins, k);
             }
-            for (int top = m; top > p; top -= 64) {  // entries [p, m) move up one, top chunk first
-                const int q = top - 1 - lane;
-                int32_t vi = 0, vl = 0, vy = 0;
-                float vx = 0, vg = 0;
-                if (q >= p) { vi = L.idx[q]; vx = L.x[q]; vg = L.g[q]; vl = L.left[q]; vy = L.ymax[q]; }
-                wave_lds_sync();
-                if (q >= p) { L.idx[q + 1] = vi; L.x[q + 1] = vx; L.g[q + 1] = vg; L.left[q + 1] = vl; L.ymax[q + 1] = vy; }
-                wave_lds_sync();
-            }
-            if (lane == 0) { L.idx[p] = (int32_t)ins; L.x[p] = cx; L.g[p] = cg; L.left[p] = cl; L.ymax[p] = cy; }
-            wave_lds_sync();
-            ++m;
-            ++ins;
+            ins += (uint32_t)k;
         }
         {  // expiry 3715-3749: keep entries with YMax > Row, in order
             int out = 0;
@@ -727,34 +999,53 @@ __device__ void walk_object_wave(const FrameParams &fp, const ObjDesc &od, const
                 float vx = 0, vg = 0;
                 if (keep) { vi = L.idx[q]; vx = L.x[q]; vg = L.g[q]; vl = L.left[q]; vy = L.ymax[q]; }
                 const unsigned long long bal = __ballot(keep);
-                const int at = out + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                wave_lds_sync();
+                const int at = out + lane_rank(bal);
+                list_sync<GL>();
                 if (keep) { L.idx[at] = vi; L.x[at] = vx; L.g[at] = vg; L.left[at] = vl; L.ymax[at] = vy; }
-                wave_lds_sync();
+                list_sync<GL>();
                 out += __popcll(bal);
             }
             m = out;
         }
         const int P = m / 2;  // pairing 3751-3869
         for (int k0 = 0; k0 < P; k0 += 64) {
-            const int k = k0 + lane;
-            const bool valid = k < P;
+            const int kk = k0 + lane;
+            const bool valid = kk < P;
             bool em = false;
             ObjEdge a, b;
             int32_t ia = 0, ib = 0;
+            SpanPos sp;
+            SpanRecG rec;
+            ScSpanRecG srec;
             if (valid) {
-                ia = L.idx[2 * k];
-                ib = L.idx[2 * k + 1];
+                ia = L.idx[2 * kk];
+                ib = L.idx[2 * kk + 1];
                 a = E[ia];
                 b = E[ib];
-                em = Row >= RowLo && emit_span<M>(fp, a, b, Row, d, st, od.g0, false, 0, recs, srecs, pos, span_tri);
+                if (Row >= RowLo) {
+                    if constexpr (kScalar) em = obj_span_scalar<M>(fp, a, b, Row, d.tex, srec, sp);
+                    else em = obj_span(fp, a, b, Row, d.tex, st, rec, sp);
+                }
             }
             const unsigned long long bal = __ballot(em);
-            if (em && pass) {
-                const uint32_t at = base + emitted + (uint32_t)__builtin_amdgcn_mbcnt_hi(
-                                                          (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                emit_span<M>(fp, a, b, Row, d, st, od.g0, true, at, recs, srecs, pos, span_tri);
+            if (em) {
+                const uint32_t j = emitted + (uint32_t)lane_rank(bal);
+                if (j < bound) {
+                    const uint32_t at = base + j;
+                    if constexpr (kScalar) {
+                        SpanRecG mark;
+                        mark.q0 = make_float4(__uint_as_float(kScalarSpan), 0.0f, 0.0f, 0.0f);
+                        mark.q1 = mark.q2 = mark.q3 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                        recs[at] = mark;
+                        srecs[at] = srec;
+                    } else {
+                        recs[at] = rec;
+                    }
+                    pos[at] = sp;
+                    span_tri[at] = od.g0;
+                } else {
+                    atomicOr(err, 2u);  // (never: the bound holds every span)
+                }
             }
             emitted += (uint32_t)__popcll(bal);
             if (valid) {  // 3811-3829
@@ -762,19 +1053,19 @@ __device__ void walk_object_wave(const FrameParams &fp, const ObjDesc &od, const
                 obj_step<M>(b);
                 E[ia] = a;
                 E[ib] = b;
-                L.x[2 * k] = a.X;
-                L.x[2 * k + 1] = b.X;
+                L.x[2 * kk] = a.X;
+                L.x[2 * kk + 1] = b.X;
             }
         }
-        wave_lds_sync();
+        list_sync<GL>();
         for (int pass_sw = 0; pass_sw < 2; ++pass_sw) {  // 3831-3841, then 3843-3853
             for (int k0 = pass_sw; k0 < P; k0 += 64) {
-                const int k = k0 + lane;
-                const int q = pass_sw == 0 ? 2 * k : 2 * k - 1;  // swap entries q, q + 1
+                const int kk = k0 + lane;
+                const int q = pass_sw == 0 ? 2 * kk : 2 * kk - 1;  // swap entries q, q + 1
                 bool sw = false;
                 int32_t i0 = 0, i1 = 0, l0 = 0, l1 = 0, y0 = 0, y1 = 0;
                 float x0 = 0, x1 = 0, g0 = 0, g1 = 0;
-                if (k < P) {
+                if (kk < P) {
                     x0 = L.x[q];
                     x1 = L.x[q + 1];
                     sw = x0 > x1;
@@ -783,37 +1074,50 @@ __device__ void walk_object_wave(const FrameParams &fp, const ObjDesc &od, const
                         l0 = L.left[q]; l1 = L.left[q + 1]; y0 = L.ymax[q]; y1 = L.ymax[q + 1];
                     }
                 }
-                wave_lds_sync();
+                list_sync<GL>();
                 if (sw) {
                     L.idx[q] = i1; L.idx[q + 1] = i0; L.x[q] = x1; L.x[q + 1] = x0; L.g[q] = g1; L.g[q + 1] = g0;
                     L.left[q] = l1; L.left[q + 1] = l0; L.ymax[q] = y1; L.ymax[q + 1] = y0;
                 }
-                wave_lds_sync();
+                list_sync<GL>();
             }
         }
     }
 }
 
+// One wave per large object.  GL = false: the list in LDS (objects of at
+// most lcap edges); true: in the pool slice pool + big_off[blockIdx.x]
+// (kWaveListArrays arrays of big_cap[blockIdx.x] + 2 ints).
+template <bool GL>
 __global__ void __launch_bounds__(64) k_obj_walk_wave(FrameParams fp, const ObjDesc *__restrict__ objs,
-                                                      const uint32_t *__restrict__ big, const uint32_t *__restrict__ escan,
+                                                      const uint32_t *__restrict__ big,
+                                                      const unsigned long long *__restrict__ big_off,
+                                                      const uint32_t *__restrict__ big_cap, int32_t *__restrict__ pool,
+                                                      uint32_t lcap, const uint32_t *__restrict__ escan,
                                                       const uint32_t *__restrict__ total0p, ObjEdge *__restrict__ work,
-                                                      int pass, uint32_t *__restrict__ counts,
-                                                      const uint32_t *__restrict__ offs, SpanRecG *__restrict__ recs,
-                                                      ScSpanRecG *__restrict__ srecs, SpanPos *__restrict__ pos,
-                                                      uint32_t *__restrict__ span_tri, uint32_t *__restrict__ err) {
-    extern __shared__ unsigned long long lds_raw[];
-    WaveList &L = *reinterpret_cast<WaveList *>(lds_raw);
+                                                      const unsigned long long *__restrict__ soff,
+                                                      SpanRecG *__restrict__ recs, ScSpanRecG *__restrict__ srecs,
+                                                      SpanPos *__restrict__ pos, uint32_t *__restrict__ span_tri,
+                                                      uint32_t *__restrict__ err) {
+    extern __shared__ int32_t lds_list[];
+    WaveList L;
+    if (GL) L.carve(pool + big_off[blockIdx.x], big_cap[blockIdx.x]);
+    else L.carve(lds_list, lcap);
     const uint32_t o = big[blockIdx.x];
     const ObjDesc od = objs[o];
     const DrawRec &d = fp.draws[od.draw];
-    const uint32_t base = pass ? offs[o] : 0u;
-    uint32_t emitted = 0, e0, n;
+    const uint32_t base = (uint32_t)soff[o], bound = (uint32_t)(soff[o + 1] - soff[o]);
+    uint32_t e0, n;
     obj_range(od, escan, *total0p, e0, n);
+    if (!GL && n > lcap) {  // (the host sends only objects of at most lcap edges here)
+        if (threadIdx.x == 0) atomicOr(err, 1u);
+        return;
+    }
     ObjEdge *E = work + e0;
     switch (d.mode) {
 #define PRK_WALK_OBJ(MM)                                                                                  \
     case MM:                                                                                              \
-        walk_object_wave<MM>(fp, od, d, E, n, pass, base, emitted, L, recs, srecs, pos, span_tri, err);   \
+        walk_object_wave<MM, GL>(fp, od, d, E, n, base, bound, L, recs, srecs, pos, span_tri, err);      \
         break;
         PRK_WALK_OBJ(MODE_AVX)
         PRK_WALK_OBJ(MODE_SC_GOURAUD)
@@ -823,7 +1127,6 @@ __global__ void __launch_bounds__(64) k_obj_walk_wave(FrameParams fp, const ObjD
 #undef PRK_WALK_OBJ
         default: break;
     }
-    if (!pass && threadIdx.x == 0) counts[o] = emitted;
 }
 
 // The tiles of a span: those of its row its [minx, min(maxx, W)) crosses and,
@@ -896,31 +1199,35 @@ __global__ void k_span_tile_offsets(const uint32_t *__restrict__ keys, uint32_t 
 
 extern "C" {
 
-// FillEdgeTable of the pass's object triangles: per-triangle edge counts
-// (ntri + 1 values, the last 0) ...
+// FillEdgeTable of the pass's object triangles: per-triangle edge and
+// active-row counts (ntri + 1 values each, the last 0) ...
 hipError_t prk_objtri_count(const prk::FrameParams *fp, const void *objs, const uint32_t *k0obj,
-                            const uint32_t *k0tri0, uint32_t nk0, uint32_t ntri, uint32_t *ecnt, hipStream_t s) {
+                            const uint32_t *k0tri0, uint32_t nk0, uint32_t ntri, uint32_t *ecnt,
+                            unsigned long long *rcnt, hipStream_t s) {
     hipLaunchKernelGGL(prk::k_objtri_count, dim3((ntri + 1 + 255) / 256), dim3(256), 0, s, *fp,
-                       reinterpret_cast<const prk::ObjDesc *>(objs), k0obj, k0tri0, nk0, ntri, ecnt);
+                       reinterpret_cast<const prk::ObjDesc *>(objs), k0obj, k0tri0, nk0, ntri, ecnt, rcnt);
     return hipGetLastError();
 }
-// ... then the edges at their exclusive scan, with their MergeSort keys.
+// ... then the edges at their exclusive scan, with their MergeSort keys
+// (keys: 3 * ntri slots, those past the visible edges all ones).
 hipError_t prk_objtri_emit(const prk::FrameParams *fp, const void *objs, const uint32_t *k0obj,
-                           const uint32_t *k0tri0, uint32_t nk0, uint32_t ntri, const uint32_t *escan, void *edges,
-                           void *keys, uint32_t *vals, hipStream_t s) {
+                           const uint32_t *k0tri0, uint32_t nk0, uint32_t ntri, const uint32_t *escan,
+                           uint32_t pbits, uint32_t ybits, int32_t ycap, void *edges, void *keys, uint32_t *vals,
+                           hipStream_t s) {
     if (ntri == 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(keys, 0xFF, (size_t)3 * ntri * 8, s);
+    if (e != hipSuccess) return e;
+    const prk::SortKeyBits kb{pbits, ybits, ycap};
     hipLaunchKernelGGL(prk::k_objtri_emit, dim3((ntri + 255) / 256), dim3(256), 0, s, *fp,
-                       reinterpret_cast<const prk::ObjDesc *>(objs), k0obj, k0tri0, nk0, ntri, escan,
+                       reinterpret_cast<const prk::ObjDesc *>(objs), k0obj, k0tri0, nk0, ntri, escan, kb,
                        reinterpret_cast<prk::ObjEdge *>(edges), reinterpret_cast<unsigned long long *>(keys), vals);
     return hipGetLastError();
 }
-// MergeSort of every object: one radix sort of the keys (temp == nullptr:
-// size query); vals_out = the edges in sorted order.
+// MergeSort of every object: one radix sort of the n = 3 * ntri padded keys
+// over their low end_bit bits (temp == nullptr: size query); vals_out[i],
+// i < the visible edge count, = the edges in sorted order.
 hipError_t prk_obj_sort(void *keys_in, uint32_t *vals_in, void *keys_out, uint32_t *vals_out, uint32_t n,
-                        uint32_t nk0, void *temp, size_t *temp_bytes, hipStream_t s) {
-    int obits = 1;
-    while ((1u << obits) < nk0 && obits < 25) ++obits;
-    const unsigned end_bit = 16 + prk::kPathBits + obits;
+                        uint32_t end_bit, void *temp, size_t *temp_bytes, hipStream_t s) {
     unsigned long long *ki = reinterpret_cast<unsigned long long *>(keys_in);
     unsigned long long *ko = reinterpret_cast<unsigned long long *>(keys_out);
     return rocprim::radix_sort_pairs(temp, *temp_bytes, ki, ko, vals_in, vals_out, n, 0, end_bit, s);
@@ -935,36 +1242,81 @@ hipError_t prk_obj_gather(const void *edges, const uint32_t *ord, const uint32_t
                        reinterpret_cast<prk::ObjEdge *>(work));
     return hipGetLastError();
 }
-// Pass 0 / 1 of the object walk: a thread per object, a wave per object of
-// big[0..nbig) (those flagged kObjWave).  err: set when an object's list
-// outgrows a wave's LDS.
-hipError_t prk_obj_walk(const prk::FrameParams *fp, const void *objs, uint32_t nobj, const uint32_t *big, uint32_t nbig,
-                        const uint32_t *escan, const uint32_t *total0p, void *work, int pass, uint32_t *counts,
-                        const uint32_t *offs, void *recs, void *srecs, void *pos, uint32_t *span_tri,
-                        const void *spans_in, uint32_t *err, hipStream_t s) {
+// Span slots per object (nobj + 1 values, the last 0; exclusive-scanned by
+// the caller into each object's first slot).
+hipError_t prk_obj_bound(const prk::FrameParams *fp, const void *objs, uint32_t nobj, const unsigned long long *rscan,
+                         const void *edges_in, unsigned long long *bound, hipStream_t s) {
+    hipLaunchKernelGGL(prk::k_obj_bound, dim3((nobj + 1 + 255) / 256), dim3(256), 0, s, *fp,
+                       reinterpret_cast<const prk::ObjDesc *>(objs), nobj, rscan,
+                       reinterpret_cast<const prk::EdgeIn *>(edges_in), bound);
+    return hipGetLastError();
+}
+// The LDS list capacity of the one-wave walk on the current device (edges;
+// 0: every wave walk keeps its list in device memory): the largest of 4096,
+// 2048, 1024 whose kWaveListArrays arrays the device grants as dynamic LDS.
+uint32_t prk_obj_walk_lcap(void) {
+    static std::atomic<int> cap[64];  // per device: 0 unknown, else cap + 1
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    int c = cap[dev].load();
+    if (c == 0) {
+        c = 1;
+        for (uint32_t k = prk::kWaveListCapLds; k >= 1024; k /= 2) {
+            const size_t bytes = (size_t)prk::kWaveListArrays * (k + 2) * 4;
+            if (hipFuncSetAttribute(reinterpret_cast<const void *>(&prk::k_obj_walk_wave<false>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) == hipSuccess) {
+                c = (int)k + 1;
+                break;
+            }
+            (void)hipGetLastError();
+        }
+        cap[dev].store(c);
+    }
+    return (uint32_t)(c - 1);
+}
+// The object walk, one pass: a thread per object, a wave per object of
+// big_lds[0..nlds) (list in LDS, lcap) and of big_gl[0..ngl) (list in the
+// pool at big_off, big_cap edges).  Spans go to slots soff[o] + k.  err: bit
+// 0 an LDS walk got an object above lcap, bit 1 an object emitted past its
+// bound (neither can happen).
+hipError_t prk_obj_walk(const prk::FrameParams *fp, const void *objs, uint32_t nobj, const uint32_t *big_lds,
+                        uint32_t nlds, uint32_t lcap, const uint32_t *big_gl, const unsigned long long *big_off,
+                        const uint32_t *big_cap, uint32_t ngl, int32_t *pool, const uint32_t *escan,
+                        const uint32_t *total0p, void *work, const unsigned long long *soff, void *recs, void *srecs,
+                        void *pos, uint32_t *span_tri, const void *spans_in, uint32_t *err, hipStream_t s) {
     if (nobj == 0) return hipSuccess;
     hipLaunchKernelGGL(prk::k_obj_walk, dim3((nobj + 63) / 64), dim3(64), 0, s, *fp,
                        reinterpret_cast<const prk::ObjDesc *>(objs), nobj, escan, total0p,
-                       reinterpret_cast<prk::ObjEdge *>(work), pass, counts, offs,
-                       reinterpret_cast<prk::SpanRecG *>(recs), reinterpret_cast<prk::ScSpanRecG *>(srecs),
-                       reinterpret_cast<prk::SpanPos *>(pos), span_tri, reinterpret_cast<const prk::SpanIn *>(spans_in));
+                       reinterpret_cast<prk::ObjEdge *>(work), soff, reinterpret_cast<prk::SpanRecG *>(recs),
+                       reinterpret_cast<prk::ScSpanRecG *>(srecs), reinterpret_cast<prk::SpanPos *>(pos), span_tri,
+                       reinterpret_cast<const prk::SpanIn *>(spans_in), err);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess || nbig == 0) return e;
-    static std::atomic<int> attr[64];  // dynamic LDS above 64 KiB, per device
-    int dev = -1;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-    if (attr[dev].load() == 0) {
-        e = hipFuncSetAttribute(reinterpret_cast<const void *>(&prk::k_obj_walk_wave),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, sizeof(prk::WaveList));
+    if (e != hipSuccess) return e;
+    if (nlds) {
+        const size_t bytes = (size_t)prk::kWaveListArrays * (lcap + 2) * 4;
+        hipLaunchKernelGGL(prk::k_obj_walk_wave<false>, dim3(nlds), dim3(64), bytes, s, *fp,
+                           reinterpret_cast<const prk::ObjDesc *>(objs), big_lds, nullptr, nullptr, nullptr, lcap,
+                           escan, total0p, reinterpret_cast<prk::ObjEdge *>(work), soff,
+                           reinterpret_cast<prk::SpanRecG *>(recs), reinterpret_cast<prk::ScSpanRecG *>(srecs),
+                           reinterpret_cast<prk::SpanPos *>(pos), span_tri, err);
+        e = hipGetLastError();
         if (e != hipSuccess) return e;
-        attr[dev].store(1);
     }
-    hipLaunchKernelGGL(prk::k_obj_walk_wave, dim3(nbig), dim3(64), sizeof(prk::WaveList), s, *fp,
-                       reinterpret_cast<const prk::ObjDesc *>(objs), big, escan, total0p,
-                       reinterpret_cast<prk::ObjEdge *>(work), pass, counts, offs,
-                       reinterpret_cast<prk::SpanRecG *>(recs), reinterpret_cast<prk::ScSpanRecG *>(srecs),
-                       reinterpret_cast<prk::SpanPos *>(pos), span_tri, err);
-    return hipGetLastError();
+    if (ngl) {
+        hipLaunchKernelGGL(prk::k_obj_walk_wave<true>, dim3(ngl), dim3(64), 0, s, *fp,
+                           reinterpret_cast<const prk::ObjDesc *>(objs), big_gl, big_off, big_cap, pool, 0u, escan,
+                           total0p, reinterpret_cast<prk::ObjEdge *>(work), soff,
+                           reinterpret_cast<prk::SpanRecG *>(recs), reinterpret_cast<prk::ScSpanRecG *>(srecs),
+                           reinterpret_cast<prk::SpanPos *>(pos), span_tri, err);
+        e = hipGetLastError();
+    }
+    return e;
+}
+
+// Exclusive scan of n + 1 64-bit counts (temp == nullptr: size query).
+hipError_t prk_scan_u64(const unsigned long long *in, unsigned long long *out, uint32_t n, void *temp,
+                        size_t *temp_bytes, hipStream_t s) {
+    return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, in, out, n, s);
 }
 
 // Exclusive scan of n + 1 counts (temp == nullptr: size query).

@@ -14,8 +14,11 @@ Mirrors the reference's draw interface (projekt.cpp, MacSpain/cpu-renderer):
 The HIP library is the only compute path: there is no CPU fallback, and every
 entry point raises PrkError if libprk_hip.so or the GPU is missing.
 """
+import atexit
 import ctypes as C
 import os
+import sys
+import weakref
 
 import numpy as np
 
@@ -71,6 +74,8 @@ _SIGS = {
                            C.c_int32, C.c_int32, C.c_int32]),
     "prk_draw_objects": (C.c_int, [C.c_void_p, C.c_int32, C.c_uint32, C.c_uint32, C.c_uint32,
                                    C.POINTER(C.c_float), C.c_int32, C.c_int32, C.c_int32]),
+    "prk_draw_objects_setup": (C.c_int, [C.c_void_p, C.c_int32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                         C.POINTER(C.c_float), C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     "prk_draw_edges": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int32, C.c_int32, C.c_int32]),
     "prk_draw_spans": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int32, C.c_int32, C.c_int32]),
     "prk_flush": (C.c_int, [C.c_void_p, C.c_void_p]),
@@ -203,6 +208,7 @@ class Comm:
 
     def __init__(self, handle, rank, nranks):
         self._h, self.rank, self.nranks = handle, rank, nranks
+        _LIVE.add(self)
 
     @classmethod
     def init(cls, renderer, uid, nranks, rank):
@@ -254,6 +260,27 @@ def gather_frame_local(renderers, frame_color_ptr, frame_pitch, frame_z_ptr=None
         C.c_void_p(frame_z_ptr) if frame_z_ptr else None))
 
 
+_LIVE = weakref.WeakSet()  # open Renderers / Comms, closed in a defined order at exit
+
+
+@atexit.register
+def _close_all():
+    """Interpreter exit: close every context still open, communicators first,
+    while the HIP runtime (and torch, whose tensors a target may use) is
+    still alive.  prk_destroy never queues GPU work (prk_api.hip), so a
+    context whose last frame was never read just drops it."""
+    objs = list(_LIVE)
+    for o in sorted(objs, key=lambda o: 0 if isinstance(o, Comm) else 1):
+        try:
+            o.close()
+        except Exception:
+            pass
+
+
+def _finalizing():
+    return sys.is_finalizing()
+
+
 class Renderer:
     """One GPU context: render target, camera/lights, resident geometry and
     textures, and the list of recorded draws of the current frame."""
@@ -265,6 +292,7 @@ class Renderer:
         self._h = h
         self._keep = []
         self.width = self.height = self.row0 = self.row1 = 0
+        _LIVE.add(self)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -272,6 +300,11 @@ class Renderer:
             self._h = None
 
     def __del__(self):
+        # no GPU calls while the interpreter is tearing down (module globals,
+        # torch's allocator and the HIP runtime may already be gone): the
+        # atexit handler above closed every context before that began
+        if _finalizing():
+            return
         try:
             self.close()
         except Exception:
@@ -401,11 +434,16 @@ class Renderer:
         _check("prk_set_debug", self._L.prk_set_debug(self._h, int(bool(on))))
 
     # ---- draws (the reference's entry points) -----------------------------
-    def _draw(self, geom, first_tri, tri_count, P, semantics, phong, texture, tris_per_object=1):
+    def _draw(self, geom, first_tri, tri_count, P, semantics, phong, texture, tris_per_object=1, setup=None):
         Pc = (C.c_float * 3)(*(P or (0.0, 0.0, 0.0)))
-        _check("prk_draw_objects", self._L.prk_draw_objects(self._h, geom, first_tri, tri_count, tris_per_object,
-                                                            Pc, semantics, int(bool(phong)),
-                                                            -1 if texture is None else texture))
+        tex = -1 if texture is None else texture
+        if setup is None:
+            _check("prk_draw_objects", self._L.prk_draw_objects(self._h, geom, first_tri, tri_count,
+                                                                tris_per_object, Pc, semantics, int(bool(phong)), tex))
+        else:  # FillEdgeTable's own PhongShading / Object->Bitmap (abi.PRK_SETUP_*)
+            _check("prk_draw_objects_setup", self._L.prk_draw_objects_setup(
+                self._h, geom, first_tri, tri_count, tris_per_object, Pc, semantics, int(bool(phong)), tex,
+                int(setup)))
 
     def draw_model_optimized(self, geom, tri_count, first_tri=0, P=None, bitmap=None, phong=True):
         """DrawModelOptimized(RenderQueue, ...) -> FillLineOptimized semantics
@@ -422,10 +460,13 @@ class Renderer:
         XOffset quirk (2508) and the >= z-test (3205).  Needs bitmap + phong."""
         self._draw(geom, first_tri, tri_count, P, abi.PRK_SEM_AVX_ST, phong, bitmap)
 
-    def draw(self, semantics, geom, tri_count, first_tri=0, P=None, bitmap=None, phong=True, tris_per_object=1):
+    def draw(self, semantics, geom, tri_count, first_tri=0, P=None, bitmap=None, phong=True, tris_per_object=1,
+             setup=None):
         """Any PRK_SEM_* draw; tris_per_object > 1: consecutive objects of that
-        many triangles, one active edge table each (prk_draw_objects)."""
-        self._draw(geom, first_tri, tri_count, P, semantics, phong, bitmap, tris_per_object)
+        many triangles, one active edge table each (prk_draw_objects).
+        setup: FillEdgeTable's own PhongShading / Object->Bitmap as
+        abi.PRK_SETUP_* bits (None: as the draw; prk_draw_objects_setup)."""
+        self._draw(geom, first_tri, tri_count, P, semantics, phong, bitmap, tris_per_object, setup)
 
     def draw_edges(self, edge_words, semantics=abi.PRK_SEM_AVX, bitmap=None, phong=True):
         """DrawModelOptimized* on a ready edge_info list: uint32 [n, 27] in
@@ -470,11 +511,12 @@ class Renderer:
 
 
 def render_scene(scene, semantics=abi.PRK_SEM_AVX, phong=True, device=0, tile=None, debug=True,
-                 color=None, z=None, rows=None, fused_clear=False, tris_per_object=1):
+                 color=None, z=None, rows=None, fused_clear=False, tris_per_object=1, setup=None):
     """Convenience: draw a whole scenes.Scene (per-triangle submission) and
     return (color, z, winners or None, stats).  fused_clear: upload
     color / z, then clear through prk_target_clear_on_flush (the frame must
-    overwrite them)."""
+    overwrite them).  setup: FillEdgeTable's own inputs (abi.PRK_SETUP_*) of
+    every draw."""
     r = Renderer(device)
     try:
         r0, r1 = (0, scene.height) if rows is None else rows
@@ -499,7 +541,8 @@ def render_scene(scene, semantics=abi.PRK_SEM_AVX, phong=True, device=0, tile=No
                 if id(texture) not in handles:
                     handles[id(texture)] = r.texture(texture)
                 tex = handles[id(texture)]
-            r.draw(sem, g, count, first_tri=first, P=scene.P, bitmap=tex, phong=phong, tris_per_object=tpo)
+            r.draw(sem, g, count, first_tri=first, P=scene.P, bitmap=tex, phong=phong, tris_per_object=tpo,
+                   setup=setup)
         r.complete_all_work()
         r.synchronize()
         col, zb = r.download()

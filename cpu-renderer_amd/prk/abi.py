@@ -15,10 +15,16 @@ PRK_ERR_UNSUPPORTED = -2
 PRK_ERR_DEVICE = -3
 PRK_ERR_NOMEM = -4
 PRK_ERR_NO_TARGET = -5
+PRK_ERR_LIMIT = -6
 
 PRK_SEM_SCALAR = 0  # DrawModel            projekt.cpp:162-601
 PRK_SEM_AVX = 1     # FillLineOptimized    projekt.cpp:1492-2320
 PRK_SEM_AVX_ST = 2  # DrawModelOptimized(Buffer,...) single-thread overload, projekt.cpp:2350-3358
+
+# FillEdgeTable's own inputs (prk_draw_objects_setup): its PhongShading
+# argument and Object->Bitmap != 0 (projekt.cpp:4012-4089)
+PRK_SETUP_PHONG = 1
+PRK_SETUP_BITMAP = 2
 
 PRK_FILTER_NEAREST = 0   # the reference's sampling (projekt.cpp:1881-2032)
 PRK_FILTER_BILINEAR = 1  # extension (AVX semantics)
@@ -27,6 +33,7 @@ STATUS_NAMES = {
     PRK_OK: "PRK_OK", PRK_ERR_ARG: "PRK_ERR_ARG", PRK_ERR_UNSUPPORTED: "PRK_ERR_UNSUPPORTED",
     PRK_ERR_DEVICE: "PRK_ERR_DEVICE", PRK_ERR_NOMEM: "PRK_ERR_NOMEM",
     PRK_ERR_NO_TARGET: "PRK_ERR_NO_TARGET",
+    PRK_ERR_LIMIT: "PRK_ERR_LIMIT",
 }
 
 

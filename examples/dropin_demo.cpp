@@ -8,10 +8,17 @@
 //            DrawModelOptimized(RenderQueue, ...)           (projekt.cpp:3615)
 //   lines    the same through DrawModelOptimizedLines             (3362)
 //   st       the same through DrawModelOptimized(Buffer, ...)     (2350)
-//   scalar   the same through DrawModel, untextured Gouraud       (162)
+//   scalar   the same through DrawModel, untextured Gouraud       (162); the
+//            objects carry the Bitmap, so FillEdgeTable(..., 0) lights them
+//            from white (4034-4054)
+//   vertexlit  the same with no Bitmap on the objects: lit vertex colours
+//   interp   FillEdgeTable(..., 1) + DrawModel(..., Bitmap = 0, Phong = 0):
+//            the raw vertex colours interpolated unlit (4012-4019)
 //   object   the whole sphere as ONE object (one active edge table)
 //   scalar_object / scalar_object_phong   the whole sphere as ONE object
 //            through DrawModel (untextured Gouraud / Phong)
+//   interp_object  the whole sphere as ONE object, FillEdgeTable(..., 1) +
+//            DrawModel(..., 0, 0)
 //   camera   per-triangle objects; halfway through, the caller moves the
 //            camera (ScreenCenter) and changes the light between FillEdgeTable
 //            calls: each object draws as its FillEdgeTable call saw them
@@ -135,10 +142,11 @@ int main(int argc, char **argv) {
             Object.NormalData = &N[3 * t];
             Object.UVData = &UV[3 * t];
             Object.EdgeMemory = EdgeMemory.data();
-            Object.Bitmap = &Texture;
-            const u32 EdgeCount = FillEdgeTable(&Object, &Commands, m != "scalar");
+            Object.Bitmap = m == "vertexlit" ? nullptr : &Texture;
+            const bool scalar = m == "scalar" || m == "vertexlit" || m == "interp";
+            const u32 EdgeCount = FillEdgeTable(&Object, &Commands, !scalar || m == "interp");
             edges_total += EdgeCount;
-            if (m == "scalar") DrawModel(&Buffer, EdgeMemory.data(), EdgeCount, &Commands, 0, 0);
+            if (scalar) DrawModel(&Buffer, EdgeMemory.data(), EdgeCount, &Commands, 0, 0);
             else if (m == "lines") DrawModelOptimizedLines(nullptr, &Buffer, EdgeMemory.data(), EdgeCount, &Commands, &Texture, 1);
             else if (m == "st") DrawModelOptimized(&Buffer, EdgeMemory.data(), EdgeCount, &Commands, &Texture, 1);
             else DrawModelOptimized(nullptr, &Buffer, EdgeMemory.data(), EdgeCount, &Commands, &Texture, 1);
@@ -157,11 +165,12 @@ int main(int argc, char **argv) {
     Sphere.EdgeMemory = EdgeMemory.data();
     Sphere.Bitmap = &Texture;
 
-    if (mode == "queue" || mode == "lines" || mode == "st" || mode == "scalar" || mode == "camera") {
+    if (mode == "queue" || mode == "lines" || mode == "st" || mode == "scalar" || mode == "camera" ||
+        mode == "vertexlit" || mode == "interp") {
         if (!per_triangle(mode)) return fail("draw");
-    } else if (mode == "scalar_object" || mode == "scalar_object_phong") {
+    } else if (mode == "scalar_object" || mode == "scalar_object_phong" || mode == "interp_object") {
         const b32 Phong = mode == "scalar_object_phong";
-        const u32 EdgeCount = FillEdgeTable(&Sphere, &Commands, Phong);
+        const u32 EdgeCount = FillEdgeTable(&Sphere, &Commands, Phong || mode == "interp_object");
         edges_total += EdgeCount;
         DrawModel(&Buffer, EdgeMemory.data(), EdgeCount, &Commands, 0, Phong);
         if (PRK_LastStatus() != PRK_OK) return fail("draw");

@@ -45,7 +45,10 @@ enum prk_status {
     PRK_ERR_UNSUPPORTED = -2,  /* combination the reference leaves undefined */
     PRK_ERR_DEVICE = -3,       /* HIP runtime error                      */
     PRK_ERR_NOMEM = -4,        /* device allocation failed               */
-    PRK_ERR_NO_TARGET = -5     /* flush without a render target          */
+    PRK_ERR_NO_TARGET = -5,    /* flush without a render target          */
+    PRK_ERR_LIMIT = -6         /* beyond this build's index capacity (more than
+                                  2^31 edges, span slots or bin entries in one
+                                  pass): a limit of the build, not of the input */
 };
 
 /* Which of the reference's span kernels a draw reproduces. */
@@ -237,12 +240,39 @@ int prk_draw(prk_context *ctx, int32_t geometry, uint32_t first_tri, uint32_t tr
  * (projekt.cpp:3894-4117, 3654-3869), so spans pair edges of different
  * triangles of the object.  tris_per_object == 1 is prk_draw.  Objects of
  * more than one triangle are supported for every semantics (DrawModel's
- * AET, 162-601, has the same list logic).  PRK_ERR_UNSUPPORTED: an object of
- * 2^22 edges or more, or one whose active edge list exceeds 4096 edges on a
- * row (the one-wave walk keeps the list in LDS). */
+ * AET, 162-601, has the same list logic), of any size: the active edge list
+ * has no length limit (a wave walks it in LDS, or in device memory once it
+ * outgrows LDS).  The edges are set up as FillEdgeTable(Object, Commands,
+ * phong) does for an object whose Bitmap is set iff texture >= 0. */
 int prk_draw_objects(prk_context *ctx, int32_t geometry, uint32_t first_tri, uint32_t tri_count,
                      uint32_t tris_per_object, const float P[3], int32_t semantics, int32_t phong,
                      int32_t texture);
+
+/* FillEdgeTable's own inputs, which shape the edge records independently of
+ * the later DrawModel* call (projekt.cpp:3882-4121):
+ *   PRK_SETUP_PHONG   its PhongShading argument != 0: raw vertex colours and
+ *                     normals (4012-4019); 0: per-vertex Gouraud lighting
+ *                     (4020-4063) and no normals;
+ *   PRK_SETUP_BITMAP  Object->Bitmap != 0: the lighting starts from white
+ *                     (4034-4054) and the U/V/(1/z) gradients are set
+ *                     (4078-4089); 0: no gradients.
+ * prk_draw_objects_setup draws with explicit setup flags (setup < 0: derived
+ * from the draw, as prk_draw_objects).  Combinations the reference leaves
+ * undefined are PRK_ERR_UNSUPPORTED: a Phong draw (any semantics) of edges
+ * set up without PRK_SETUP_PHONG (MinNormal never written, 4012-4064), and a
+ * textured draw of edges set up without PRK_SETUP_BITMAP (UGradient,
+ * VGradient, OneOverZGradient never written, 4078-4089).  So
+ * FillEdgeTable(..., 1) + DrawModel(..., Bitmap = 0, Phong = 0) interpolates
+ * the raw colours unlit, and an object with a Bitmap drawn by
+ * DrawModel(..., Bitmap = 0, Phong = 0) after FillEdgeTable(..., 0) gets the
+ * white-based lighting. */
+enum prk_setup {
+    PRK_SETUP_PHONG = 1,
+    PRK_SETUP_BITMAP = 2
+};
+int prk_draw_objects_setup(prk_context *ctx, int32_t geometry, uint32_t first_tri, uint32_t tri_count,
+                           uint32_t tris_per_object, const float P[3], int32_t semantics, int32_t phong,
+                           int32_t texture, int32_t setup);
 
 /* edge_info (projekt.h:17-37) without its list pointer: what the reference's
  * FillEdgeTable leaves in EdgeMemory and DrawModel* walk.  prk_draw_edges

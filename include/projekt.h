@@ -20,7 +20,11 @@
 //    3898-3925) into the frame's pinned staging arena (sent on to the GPU in
 //    chunks of 64K triangles while the caller keeps submitting), snapshots
 //    Commands->Transform and LightData as they are at the call (3885,
-//    3907-3909, 4022-4061), and leaves a token in Object->EdgeMemory that
+//    3907-3909, 4022-4061) and its own inputs PhongShading and
+//    Object->Bitmap != 0 (raw colours + normals vs per-vertex lighting,
+//    4012-4063; white-based lighting and UV gradients, 4034-4054, 4078-4089:
+//    the edges are built from them whatever DrawModel* later draws them
+//    with), and leaves a token in Object->EdgeMemory that
 //    DrawModel* read back; the setup itself (projection, cull, edges,
 //    lighting, MergeSort) runs on the GPU at PRK_CompleteAllWork.  It
 //    returns the reference's value, the visible edge count (4119; 0 for an
@@ -198,6 +202,7 @@ struct frame_object {
     uint32_t FirstTri, Tris;  // Tris == 0: FillEdgeTable found no edge (nothing to draw)
     float P[3];
     uint32_t Camera;          // Commands->Transform / LightData as they were at FillEdgeTable
+    int32_t Setup;            // FillEdgeTable's PhongShading and Object->Bitmap != 0 (PRK_SETUP_*)
 };
 
 // Commands->Transform and LightData as one draw saw them.
@@ -557,7 +562,8 @@ inline void draw(loaded_bitmap *Buffer, edge_info *Edges, u32 EdgeCount, game_re
             if (b.Kind == DRAW_OBJECT && b.Semantics == d.Semantics && b.Phong == d.Phong &&
                 b.Texture == d.Texture && b.Camera == d.Camera) {
                 const frame_object &f = st.Objects[b.First];
-                if (o.FirstTri == f.FirstTri + b.RunTris && o.Tris == f.Tris && memcmp(o.P, f.P, sizeof o.P) == 0) {
+                if (o.FirstTri == f.FirstTri + b.RunTris && o.Tris == f.Tris && o.Setup == f.Setup &&
+                    memcmp(o.P, f.P, sizeof o.P) == 0) {
                     ++b.Count;
                     b.RunTris += o.Tris;
                     st.LastStatus = PRK_OK;
@@ -634,8 +640,8 @@ inline int issue(state &st) {
                 const pending_draw &d = st.Draws[k];
                 if (d.Kind == DRAW_OBJECT) {
                     const frame_object &o = st.Objects[d.First];
-                    r = prk_draw_objects(c, st.Geom, o.FirstTri, d.RunTris, o.Tris, o.P, d.Semantics, d.Phong,
-                                         d.Texture);
+                    r = prk_draw_objects_setup(c, st.Geom, o.FirstTri, d.RunTris, o.Tris, o.P, d.Semantics,
+                                               d.Phong, d.Texture, o.Setup);
                 } else if (d.Kind == DRAW_EDGES) {
                     r = prk_draw_edges(c, st.Edges.data() + d.First, d.Count, d.Semantics, d.Phong, d.Texture);
                 } else {
@@ -743,7 +749,6 @@ inline int PRK_CompleteAllWork(loaded_bitmap *Buffer, game_render_commands *Comm
 // ---- the reference's entry points ------------------------------------------
 // projekt.cpp:3882-4121
 inline u32 FillEdgeTable(render_entry_3d_object *Object, game_render_commands *Commands, b32 PhongShading = 0) {
-    (void)PhongShading;  // the semantics travel with the DrawModel* call
     prk_dropin::state &st = prk_dropin::S();
     if (!st.Ctx || !Object || !Commands || !Object->EdgeMemory || !Object->VertexData || Object->VertexCount < 3)
         return 0;
@@ -752,6 +757,10 @@ inline u32 FillEdgeTable(render_entry_3d_object *Object, game_render_commands *C
     o.P[0] = Object->P.x;
     o.P[1] = Object->P.y;
     o.P[2] = Object->P.z;
+    // what this call's own inputs make of the edges (raw colours + normals vs
+    // Gouraud lighting, 4012-4063; white base and UV gradients with a Bitmap,
+    // 4034-4054, 4078-4089), whatever DrawModel* later draws them with
+    o.Setup = (PhongShading ? PRK_SETUP_PHONG : 0) | (Object->Bitmap ? PRK_SETUP_BITMAP : 0);
     // the camera and lights of this call (3885, 3907-3909, 4022-4061)
     o.Camera = prk_dropin::camera_id(st, Commands);
     const prk_dropin::camera &cam = st.Cameras[o.Camera];

@@ -34,7 +34,8 @@ class OrDrawDesc(C.Structure):
     _fields_ = [("Vertices", C.c_void_p), ("Colors", C.c_void_p), ("Normals", C.c_void_p),
                 ("UVs", C.c_void_p), ("TriCount", C.c_uint32), ("TrisPerObject", C.c_uint32),
                 ("P", C.c_float * 3), ("Semantics", C.c_int32), ("Phong", C.c_int32),
-                ("Bitmap", C.POINTER(abi.PrkBitmap)), ("TriIndexBase", C.c_int32), ("Filter", C.c_int32)]
+                ("Bitmap", C.POINTER(abi.PrkBitmap)), ("TriIndexBase", C.c_int32), ("Filter", C.c_int32),
+                ("Setup", C.c_int32)]
 
 
 class OrTarget(C.Structure):
@@ -81,7 +82,7 @@ def _ptr(a):
 class _Keep:
     """Holds ctypes objects alive for the duration of a call."""
 
-    def __init__(self, scene, semantics, phong, tris_per_object, tri_base=0, texture="scene"):
+    def __init__(self, scene, semantics, phong, tris_per_object, tri_base=0, texture="scene", setup=None):
         self.arrays = [np.ascontiguousarray(scene.vertices, np.float32),
                        np.ascontiguousarray(scene.colors, np.float32),
                        np.ascontiguousarray(scene.normals, np.float32),
@@ -103,19 +104,21 @@ class _Keep:
         d.Bitmap = C.pointer(self.bitmap) if self.bitmap is not None else None
         d.TriIndexBase = tri_base
         d.Filter = getattr(texture, "filter", abi.PRK_FILTER_NEAREST) if texture is not None else 0
+        d.Setup = -1 if setup is None else int(setup)  # FillEdgeTable's own inputs (PRK_SETUP_*)
         self.desc = d
         self.transform = scene.prk_transform()
         self.lights = scene.prk_lights()
 
 
 def render(scene, semantics=abi.PRK_SEM_AVX, phong=True, tris_per_object=1, threads=1,
-           color=None, z=None, winners=True, rows=None, cpu=None):
+           color=None, z=None, winners=True, rows=None, cpu=None, setup=None):
     """Draw `scene` with the oracle.  Returns (color u32[H,W], z f32[H,W],
     winners i32[H,W] or None, stats dict).  `color`/`z` (optional) are the
     prior target contents (default: reference clear values).
     cpu: None = the scalar restatement (liboracle.so); "banded" / "queue" /
     "rows" = the AVX2 CPU baseline (liborcpu.so) with that schedule over
-    `threads`."""
+    `threads`.  setup: FillEdgeTable's own PhongShading / Object->Bitmap
+    (PRK_SETUP_* bits; None: as the draw)."""
     W, H = scene.width, scene.height
     col = np.full((H, W), CLEAR_COLOR, np.uint32) if color is None else np.array(color, np.uint32)
     zb = np.full((H, W), CLEAR_Z, np.float32) if z is None else np.array(z, np.float32)
@@ -128,15 +131,16 @@ def render(scene, semantics=abi.PRK_SEM_AVX, phong=True, tris_per_object=1, thre
             sub = scene.subset(first, first + count)
             sub.texture, sub.draws = texture, None
             _, _, _, st = _render_one(sub, sem, phong, tpo, threads, col, zb, win, rows,
-                                      tri_base=first, cpu=cpu)
+                                      tri_base=first, cpu=cpu, setup=setup)
             tot = [tot[0] + st["spans"], tot[1] + st["span_pixels"], tot[2] + st["writes"]]
         return col, zb, win, dict(spans=tot[0], span_pixels=tot[1], writes=tot[2])
-    return _render_one(scene, semantics, phong, tris_per_object, threads, col, zb, win, rows, cpu=cpu)
+    return _render_one(scene, semantics, phong, tris_per_object, threads, col, zb, win, rows, cpu=cpu, setup=setup)
 
 
-def _render_one(scene, semantics, phong, tris_per_object, threads, col, zb, win, rows, tri_base=0, cpu=None):
+def _render_one(scene, semantics, phong, tris_per_object, threads, col, zb, win, rows, tri_base=0, cpu=None,
+                setup=None):
     W, H = scene.width, scene.height
-    k = _Keep(scene, semantics, phong, tris_per_object, tri_base=tri_base)
+    k = _Keep(scene, semantics, phong, tris_per_object, tri_base=tri_base, setup=setup)
     tg = OrTarget(_ptr(col), W * 4, _ptr(zb), W, H, _ptr(win))
     stats = (C.c_uint64 * 3)()
     if cpu is not None:
@@ -168,10 +172,10 @@ EDGE_FIELDS = ["YMax", "XMin", "ZMin", "OneOverZMin", "Gradient", "ZGradient",
                "MinColor", "ColorGradient", "MinNormal", "NormalGradient"]
 
 
-def fill_edge_table(scene, tri0=0, n=1, phong=True, semantics=abi.PRK_SEM_AVX):
+def fill_edge_table(scene, tri0=0, n=1, phong=True, semantics=abi.PRK_SEM_AVX, setup=None):
     """FillEdgeTable (projekt.cpp:3882-4121) on triangles [tri0, tri0+n) as one
     object; returns the sorted edge list as dicts."""
-    k = _Keep(scene, semantics, phong, n)
+    k = _Keep(scene, semantics, phong, n, setup=setup)
     words = np.zeros(27 * 3 * n, np.uint32)
     cnt = C.c_uint32(0)
     rc = lib().oracle_fill_edge_table(C.byref(k.desc), C.c_uint32(tri0), C.c_uint32(n),

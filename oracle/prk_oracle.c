@@ -799,7 +799,18 @@ typedef struct or_draw_desc {
     const prk_bitmap *Bitmap; /* host memory with guard row, or NULL */
     int32_t TriIndexBase;     /* winner id of triangle 0 */
     int32_t Filter;           /* PRK_FILTER_* (AVX semantics; extension) */
+    int32_t Setup;            /* FillEdgeTable's own inputs (prk.h PRK_SETUP_*): bit 0 its
+                                 PhongShading, bit 1 Object->Bitmap != 0; < 0: as the draw
+                                 (Phong, Bitmap != NULL) */
 } or_draw_desc;
+
+/* FillEdgeTable's PhongShading and Object->Bitmap of a draw (projekt.cpp:
+ * 4012-4089 read them; DrawModel* reads its own Phong / Bitmap). */
+static inline int or_setup_phong(const or_draw_desc *D) { return D->Setup < 0 ? D->Phong != 0 : (D->Setup & 1); }
+static inline int or_setup_bitmap(const or_draw_desc *D)
+{
+    return D->Setup < 0 ? D->Bitmap != NULL : ((D->Setup >> 1) & 1);
+}
 
 typedef struct or_target {
     uint32_t *Color;
@@ -836,6 +847,10 @@ static int or_draw_filtered(const or_draw_desc *D, const or_target *Tg, const pr
     const int avx = D->Semantics == PRK_SEM_AVX || D->Semantics == PRK_SEM_AVX_ST;
     if (avx && (!D->Bitmap || !D->Phong)) return PRK_ERR_UNSUPPORTED;
     if (avx && (Tg->Width % 8)) return PRK_ERR_UNSUPPORTED;
+    /* edge fields FillEdgeTable never wrote: MinNormal without its
+     * PhongShading (4012-4064), U/V/(1/z) gradients without Object->Bitmap
+     * (4078-4089) -- a draw reading them is undefined */
+    if ((D->Phong && !or_setup_phong(D)) || (D->Bitmap && !or_setup_bitmap(D))) return PRK_ERR_UNSUPPORTED;
     if (Lights->LightCount > PRK_MAX_LIGHTS) return PRK_ERR_ARG;
     uint32_t per = D->TrisPerObject ? D->TrisPerObject : 1;
     or_edge *Edges = (or_edge *)malloc(sizeof(or_edge) * 3 * per);
@@ -871,7 +886,7 @@ static int or_draw_filtered(const or_draw_desc *D, const or_target *Tg, const pr
             }
         }
         uint32_t ec = or_fill_edge_table(D->Vertices, D->Colors, D->Normals, D->UVs, t0, n, D->P,
-                                         D->Bitmap != NULL, D->Phong, T, Lights, Edges, Sort);
+                                         or_setup_bitmap(D), or_setup_phong(D), T, Lights, Edges, Sort);
         X_.TriIndex = D->TriIndexBase + (int32_t)t0;
         or_aet_walk(&X_, Edges, ec, Span);
     }
@@ -958,7 +973,7 @@ int oracle_fill_edge_table(const or_draw_desc *D, uint32_t tri0, uint32_t n,
     or_edge *Sort = (or_edge *)calloc(3 * (size_t)n + 1, sizeof(or_edge));
     if (!Edges || !Sort) { free(Edges); free(Sort); return PRK_ERR_NOMEM; }
     uint32_t ec = or_fill_edge_table(D->Vertices, D->Colors, D->Normals, D->UVs, tri0, n, D->P,
-                                     D->Bitmap != NULL, D->Phong, T, Lights, Edges, Sort);
+                                     or_setup_bitmap(D), or_setup_phong(D), T, Lights, Edges, Sort);
     for (uint32_t i = 0; i < ec; ++i) {
         uint32_t *w = out_words + 27 * (size_t)i;
         const or_edge *E = Edges + i;

@@ -111,8 +111,12 @@ def bilinear(tex, fu, fv):
 
 
 class Ctx:
-    def __init__(self, scene, semantics, phong, color=None, z=None):
+    def __init__(self, scene, semantics, phong, color=None, z=None, setup=None):
         self.s = scene
+        # FillEdgeTable's own PhongShading / Object->Bitmap (projekt.cpp:4012-4089);
+        # None: as the draw (PhongShading, the draw's Bitmap)
+        self.fe_phong = phong if setup is None else bool(setup & 1)
+        self.fe_bitmap = (scene.texture is not None) if setup is None else bool(setup & 2)
         self.W, self.H = scene.width, scene.height
         D, F, M2P, cx, cy = [f32(v) for v in scene.transform]
         self.D, self.F, self.M2P, self.cx, self.cy = D, F, M2P, cx, cy
@@ -146,7 +150,7 @@ def edge_table(ctx, t):
     inner = (f32(0) * cross[0] + f32(0) * cross[1]) + f32(-1) * cross[2]
     if not inner > 0:
         return []
-    textured = ctx.tex is not None
+    textured = ctx.fe_bitmap  # Object->Bitmap (4034-4054, 4078)
     edges = []
     for i0, i1 in ((0, 1), (1, 2), (2, 0)):
         mi, ma = i0, i1
@@ -178,7 +182,7 @@ def edge_table(ctx, t):
         c1 = [f32(v) for v in s.colors[3 * t + ma]]
         n0 = [f32(v) for v in s.normals[3 * t + mi]]
         n1 = [f32(v) for v in s.normals[3 * t + ma]]
-        if ctx.phong:
+        if ctx.fe_phong:  # FillEdgeTable's PhongShading (4012)
             minc, maxc, minn, maxn = c0, c1, n0, [n1[0], n1[1], n1[2]]
         else:
             minc, maxc = [f32(0)] * 4, [f32(0)] * 4
@@ -437,8 +441,8 @@ def span_scalar(ctx, t, L, R, row):
             w, u, v = w + iw, u + iu, v + iv
 
 
-def render(scene, semantics=1, phong=True):
-    ctx = Ctx(scene, semantics, phong)
+def render(scene, semantics=1, phong=True, setup=None):
+    ctx = Ctx(scene, semantics, phong, setup=setup)
     with np.errstate(all="ignore"):
         for t in range(scene.tri_count):
             walk(ctx, t, edge_table(ctx, t))

@@ -46,10 +46,11 @@ def compare(g, o, exact_color=True, label=""):
 
 
 def run_both(scene, semantics=abi.PRK_SEM_AVX, phong=True, tile=None, threads=8, exact_color=True,
-             label="", tris_per_object=1):
+             label="", tris_per_object=1, setup=None):
     o = O.render(scene, semantics=semantics, phong=phong, threads=threads if tris_per_object == 1 else 1,
-                 tris_per_object=tris_per_object)
-    g = prk.render_scene(scene, semantics=semantics, phong=phong, tile=tile, tris_per_object=tris_per_object)
+                 tris_per_object=tris_per_object, setup=setup)
+    g = prk.render_scene(scene, semantics=semantics, phong=phong, tile=tile, tris_per_object=tris_per_object,
+                         setup=setup)
     compare(g, o, exact_color=exact_color, label=label or scene.name)
     return g, o
 
@@ -623,13 +624,91 @@ def test_whole_object_wave_walk(gpu, sem, tpo):
              label="wave objects tpo=%d sem=%d" % (tpo, sem))
 
 
-def test_whole_object_list_overflow_rejected(gpu):
-    """An object whose active edge list outgrows one wave's LDS list (4096
-    edges on a row) is rejected (PRK_ERR_UNSUPPORTED), not walked wrongly."""
-    s = scenes.random_soup(1_000_000, 4096, 4096, radius=16, seed=7)
-    with pytest.raises(prk.PrkError) as e:
-        prk.render_scene(s, tris_per_object=s.tri_count, debug=False)
-    assert e.value.code == abi.PRK_ERR_UNSUPPORTED
+@pytest.mark.parametrize("sem", [abi.PRK_SEM_AVX, abi.PRK_SEM_SCALAR])
+def test_whole_object_long_active_lists(gpu, sem):
+    """One object whose active edge list holds ~14k edges per row (beyond the
+    wave walk's 4096-entry LDS list: the list lives in device memory), with
+    hundreds of insertions per row: the batched insertion against the
+    oracle's one-at-a-time list scan (projekt.cpp:3654-3713)."""
+    s = scenes.random_soup(30000, 1024, 128, radius=24, seed=17)
+    if sem == abi.PRK_SEM_SCALAR:
+        s.texture = None
+    run_both(s, semantics=sem, phong=sem != abi.PRK_SEM_SCALAR, tris_per_object=s.tri_count, threads=1,
+             label="long lists sem=%d" % sem)
+
+
+def test_whole_object_mid_lists_lds(gpu):
+    """Objects whose lists stay in LDS (<= 4096 edges per object) while
+    several hundred edges enter per row: the batched insertion in LDS."""
+    s = scenes.with_ties(scenes.random_soup(2700, 512, 64, radius=30, seed=23), seed=23)
+    run_both(s, tris_per_object=1300, threads=1, label="mid lists")
+
+
+C3B_ONE_OBJECT = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)),
+                                             "golden", "c3b_one_object.json")
+
+
+def test_c3b_one_object_golden(gpu):
+    """The headline C3b geometry (4096^2, 1M triangles, Phong + texture)
+    submitted as ONE render_entry_3d_object: one active edge table of ~3M
+    edges, ~15k active per row.  The oracle needs minutes for it (its
+    insertion scans the list per edge, as the reference does), so its frame
+    was rendered once by tools/make_golden.py and is pinned here as per-band
+    SHA-256 digests of colour, z and winner map."""
+    import hashlib
+    import json
+    ref = json.load(open(C3B_ONE_OBJECT))
+    s = scenes.random_soup(ref["tris"], ref["width"], ref["height"], radius=ref["radius"], seed=ref["seed"])
+    h = hashlib.sha256()
+    for a in (s.vertices, s.colors, s.normals, s.uvs, s.texture.texels):
+        h.update(np.ascontiguousarray(a).tobytes())
+    assert h.hexdigest() == ref["inputs"], "the generated scene differs from the one the digests were made from"
+    gc, gz, gw, st = prk.render_scene(s, tris_per_object=s.tri_count)
+    assert int((gw >= 0).sum()) == ref["covered"]
+    rows = ref["band_rows"]
+    bad = []
+    for b, want in enumerate(ref["bands"]):
+        sl = slice(b * rows, (b + 1) * rows)
+        got = [hashlib.sha256(np.ascontiguousarray(a[sl]).tobytes()).hexdigest() for a in (gc, gz, gw)]
+        if got != want:
+            bad.append(b)
+    assert not bad, "bands differing from the oracle's frame: %s" % bad[:16]
+
+
+@pytest.mark.parametrize("tpo", [1, 5, 300])
+@pytest.mark.parametrize("setup", [abi.PRK_SETUP_PHONG, abi.PRK_SETUP_BITMAP, abi.PRK_SETUP_PHONG | abi.PRK_SETUP_BITMAP,
+                                   0])
+def test_fill_edge_table_inputs(gpu, tpo, setup):
+    """FillEdgeTable's own PhongShading and Object->Bitmap decide the edge
+    colours an untextured non-Phong DrawModel interpolates
+    (projekt.cpp:4012-4063): PhongShading = 1 stores the raw colours (drawn
+    unlit), PhongShading = 0 lights them per vertex from the vertex colour,
+    or from white when the object has a Bitmap (4034-4054) — whatever the
+    DrawModel call's own flags."""
+    s = scenes.with_ties(scenes.random_soup(3000, 256, 256, radius=20, seed=31 + tpo, textured=False), seed=5)
+    run_both(s, semantics=abi.PRK_SEM_SCALAR, phong=False, tris_per_object=tpo, threads=1, setup=setup,
+             label="setup=%d tpo=%d" % (setup, tpo))
+
+
+def test_fill_edge_table_inputs_undefined_rejected(gpu):
+    """Edge fields FillEdgeTable never wrote are undefined in the reference:
+    a Phong draw of edges set up without PhongShading (MinNormal,
+    4012-4064), a textured draw of edges set up without a Bitmap (the
+    U/V/(1/z) gradients, 4078-4089)."""
+    s = scenes.random_soup(10, 64, 64, seed=0)
+    r = prk.Renderer()
+    try:
+        g = r.geometry(s.vertices, s.colors, s.normals, s.uvs)
+        tex = r.texture(s.texture)
+        for sem, phong, t, setup in [(abi.PRK_SEM_AVX, True, tex, abi.PRK_SETUP_BITMAP),
+                                     (abi.PRK_SEM_AVX, True, tex, abi.PRK_SETUP_PHONG),
+                                     (abi.PRK_SEM_SCALAR, True, None, 0),
+                                     (abi.PRK_SEM_SCALAR, False, tex, abi.PRK_SETUP_PHONG)]:
+            with pytest.raises(prk.PrkError) as e:
+                r.draw(sem, g, 10, bitmap=t, phong=phong, setup=setup)
+            assert e.value.code == abi.PRK_ERR_UNSUPPORTED
+    finally:
+        r.close()
 
 
 def test_whole_object_scalar_bands_and_passes(gpu):
@@ -796,12 +875,12 @@ def _dropin_scene(textured=True, salt=0):
 
 
 DROPIN_MODES = ["queue", "lines", "st", "scalar", "object", "mutate", "edges", "work", "scalar_object",
-                "scalar_object_phong", "camera"]
+                "scalar_object_phong", "camera", "vertexlit", "interp", "interp_object"]
 
 
 @pytest.mark.parametrize("mode,bands", [(m, 1) for m in DROPIN_MODES] +
                          [("queue", 3), ("object", 2), ("mutate", 3), ("scalar", 3), ("work", 2),
-                          ("scalar_object", 3), ("camera", 2)])
+                          ("scalar_object", 3), ("camera", 2), ("interp_object", 2)])
 def test_dropin_demo_matches_oracle(gpu, tmp_path, mode, bands):
     """examples/dropin_demo.cpp drives the reference's own entry points
     through include/projekt.h (FillEdgeTable, DrawModelOptimized(RenderQueue),
@@ -822,7 +901,13 @@ def test_dropin_demo_matches_oracle(gpu, tmp_path, mode, bands):
                         "-Wl,-rpath," + os.path.join(root, "cpu-renderer_amd"), "-o", str(exe)],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
-    s = _dropin_scene(textured=mode not in ("scalar", "scalar_object", "scalar_object_phong"))
+    scalar_modes = ("scalar", "scalar_object", "scalar_object_phong", "vertexlit", "interp", "interp_object")
+    s = _dropin_scene(textured=mode not in scalar_modes)
+    # FillEdgeTable's own PhongShading / Object->Bitmap (the demo's objects
+    # carry the Bitmap except in "vertexlit")
+    setup = {"scalar": abi.PRK_SETUP_BITMAP, "vertexlit": 0, "interp": abi.PRK_SETUP_PHONG | abi.PRK_SETUP_BITMAP,
+             "scalar_object": abi.PRK_SETUP_BITMAP, "interp_object": abi.PRK_SETUP_PHONG | abi.PRK_SETUP_BITMAP,
+             "scalar_object_phong": abi.PRK_SETUP_PHONG | abi.PRK_SETUP_BITMAP}.get(mode)
     T = s.tri_count
     extra = []
     if mode == "edges":
@@ -858,12 +943,13 @@ def test_dropin_demo_matches_oracle(gpu, tmp_path, mode, bands):
         oc, oz, _, _ = O.render(s)
     elif mode == "st":
         oc, oz, _, _ = O.render(s, semantics=abi.PRK_SEM_AVX_ST)
-    elif mode == "scalar":
-        oc, oz, _, _ = O.render(s, semantics=abi.PRK_SEM_SCALAR, phong=False)
+    elif mode in ("scalar", "vertexlit", "interp"):
+        oc, oz, _, _ = O.render(s, semantics=abi.PRK_SEM_SCALAR, phong=False, setup=setup)
     elif mode == "object":
         oc, oz, _, _ = O.render(s, tris_per_object=T)
-    elif mode in ("scalar_object", "scalar_object_phong"):
-        oc, oz, _, _ = O.render(s, semantics=abi.PRK_SEM_SCALAR, phong=mode.endswith("phong"), tris_per_object=T)
+    elif mode in ("scalar_object", "scalar_object_phong", "interp_object"):
+        oc, oz, _, _ = O.render(s, semantics=abi.PRK_SEM_SCALAR, phong=mode.endswith("phong"), tris_per_object=T,
+                                setup=setup)
     elif mode == "camera":  # the second half drawn with the moved camera and the new light, over the first
         half = T // 2
         a, b = s.subset(0, half), s.subset(half, T)
@@ -893,9 +979,9 @@ def test_dropin_demo_matches_oracle(gpu, tmp_path, mode, bands):
     # FillEdgeTable's return values (projekt.cpp:4119) summed over the frame's
     # calls equal the oracle's edge counts: per triangle, or the whole sphere
     edges = int(run.stdout.split("edges=")[1].split()[0])
-    if mode in ("queue", "lines", "st", "scalar", "camera"):
+    if mode in ("queue", "lines", "st", "scalar", "camera", "vertexlit", "interp"):
         assert edges == sum(len(O.fill_edge_table(s, t, 1)) for t in range(T)), mode
-    elif mode.startswith("scalar_object"):
+    elif mode.startswith("scalar_object") or mode == "interp_object":
         assert edges == len(O.fill_edge_table(s, 0, T, phong=mode.endswith("phong"))), mode
 
 
@@ -954,3 +1040,51 @@ def test_c5_8192_two_bands(gpu):
     for r0, r1 in ((0, 4096), (4096, 8192)):
         gc, gz, gw, _ = prk.render_scene(s, rows=(r0, r1))
         compare((gc, gz, gw, None), (oc[r0:r1], oz[r0:r1], ow[r0:r1], None), label="band %d-%d" % (r0, r1))
+
+
+EXIT_CHILD = r"""
+import sys
+sys.path[:0] = [{pkg!r}]
+import numpy as np
+import torch
+import prk
+from prk import scenes
+small = scenes.random_soup(3000, 512, 384, radius=16, seed=91)
+big = scenes.random_soup(6000, 512, 384, radius=260, seed=92)
+big.texture = small.texture
+W, H = 512, 384
+color = torch.zeros((H, W), dtype=torch.int32, device="cuda")
+z = torch.zeros((H, W), dtype=torch.float32, device="cuda")
+r = prk.Renderer(0)
+r.set_camera(small.prk_transform(), small.prk_lights())
+tex = r.texture(small.texture)
+gs = [r.geometry(s.vertices, s.colors, s.normals, s.uvs) for s in (small, big)]
+r.target_bind(color.data_ptr(), W * 4, z.data_ptr(), W, H)
+r.clear_on_flush()
+r.draw_model_optimized(gs[0], small.tri_count, P=small.P, bitmap=tex)
+r.complete_all_work()          # counted at once: sizes the scratch
+r.clear_on_flush()
+r.draw_model_optimized(gs[1], big.tri_count, P=big.P, bitmap=tex)
+r.complete_all_work()          # over capacity, its count never read
+print("queued; exiting without close", flush=True)
+{tail}
+"""
+
+
+@pytest.mark.parametrize("tail", ["", "del color, z", "import gc; r2 = r; del r; gc.collect()"])
+def test_exit_with_pending_overflowed_frame(gpu, tmp_path, tail):
+    """A process that queues an over-capacity frame into a torch-owned target
+    and exits without close(): interpreter teardown must not run GPU work or
+    free anything twice (prk_destroy never queues GPU work; the binding
+    closes open contexts at exit before torch and the HIP runtime go away).
+    Exit status 0, no glibc heap message."""
+    import os
+    import subprocess
+    import sys
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cpu-renderer_amd")
+    script = tmp_path / "child.py"
+    script.write_text(EXIT_CHILD.format(pkg=pkg, tail=tail))
+    run = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=100)
+    bad = [w for w in ("double free", "corruption", "Aborted", "Segmentation", "free():") if w in run.stderr]
+    assert run.returncode == 0 and not bad, (run.returncode, run.stderr[-2000:])
+    assert "exiting without close" in run.stdout

@@ -39,6 +39,30 @@ def test_two_restatements_agree(sem, phong, tex, seed):
     assert same(o, p)
 
 
+@pytest.mark.parametrize("setup", [abi.PRK_SETUP_PHONG, abi.PRK_SETUP_BITMAP, abi.PRK_SETUP_PHONG | abi.PRK_SETUP_BITMAP])
+def test_two_restatements_agree_fill_edge_table_inputs(setup):
+    """FillEdgeTable's own PhongShading / Object->Bitmap (projekt.cpp:
+    4012-4089) under an untextured non-Phong DrawModel: raw colours unlit
+    (Phong setup), white-based lighting (Bitmap, no Phong)."""
+    s = scenes.random_soup(60, 96, 64, radius=14, seed=60 + setup, textured=False, lights=scenes.LIGHTS_TWO,
+                           ambient=scenes.AMBIENT_TWO)
+    o = O.render(s, semantics=abi.PRK_SEM_SCALAR, phong=False, setup=setup)
+    assert same(o, pyref.render(s, abi.PRK_SEM_SCALAR, False, setup=setup))
+    # the three setups really differ from the draw-derived (vertex-lit) one
+    d = O.render(s, semantics=abi.PRK_SEM_SCALAR, phong=False)
+    assert (o[0] != d[0]).any()
+
+
+def test_oracle_rejects_undefined_setups():
+    """A draw reading edge fields its FillEdgeTable never wrote is undefined
+    (MinNormal without PhongShading, UV gradients without a Bitmap)."""
+    s = scenes.random_soup(10, 64, 64, seed=1)
+    for sem, phong, setup in [(abi.PRK_SEM_AVX, True, abi.PRK_SETUP_BITMAP),
+                              (abi.PRK_SEM_SCALAR, False, abi.PRK_SETUP_PHONG)]:
+        with pytest.raises(RuntimeError):
+            O.render(s, semantics=sem, phong=phong, setup=setup)
+
+
 @pytest.mark.parametrize("sem,phong,tex", [MODES[0], MODES[1], MODES[4], MODES[5]])
 def test_two_restatements_agree_clipping(sem, phong, tex):
     """Big triangles hanging over every screen edge (top clip, left XOffset,

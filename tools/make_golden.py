@@ -8,8 +8,16 @@ committed expected image; they do NOT pin parity with the reference itself.
 
 Each fixture holds the inputs (geometry, texture, camera, lights, semantics)
 and the expected colour, z and winning-triangle maps.
-usage: python tools/make_golden.py
+
+c3b_one_object.json: the headline C3b scene (4096^2, 1M triangles, Phong +
+texture) drawn as ONE object (one active edge table): the oracle needs
+minutes for it (its insertion scans the ~15k-entry list per edge, as the
+reference's does), so only per-band SHA-256 digests of its colour, z and
+winner maps are committed, with a digest of the generated inputs.
+usage: python tools/make_golden.py [c3b_one_object]
 """
+import hashlib
+import json
 import os
 import sys
 
@@ -84,7 +92,36 @@ def load(path):
     return s, int(d["semantics"]), bool(d["phong"]), d
 
 
+def scene_digest(s):
+    h = hashlib.sha256()
+    for a in (s.vertices, s.colors, s.normals, s.uvs, s.texture.texels if s.texture is not None else None):
+        if a is not None:
+            h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def band_digests(col, z, win, rows):
+    return [[hashlib.sha256(np.ascontiguousarray(a[b * rows:(b + 1) * rows]).tobytes()).hexdigest()
+             for a in (col, z, win)] for b in range(col.shape[0] // rows)]
+
+
+def c3b_one_object(T=1_000_000, W=4096, H=4096, R=16.0, seed=2024, rows=64):
+    import time
+    s = scenes.random_soup(T, W, H, radius=R, seed=seed)
+    t = time.time()
+    col, z, win, st = O.render(s, tris_per_object=s.tri_count)
+    out = dict(tris=T, width=W, height=H, radius=R, seed=seed, band_rows=rows, inputs=scene_digest(s),
+               spans=int(st["spans"]), span_pixels=int(st["span_pixels"]), covered=int((win >= 0).sum()),
+               bands=band_digests(col, z, win, rows))
+    with open(os.path.join(OUT, "c3b_one_object.json"), "w") as f:
+        json.dump(out, f, indent=0)
+    print("c3b_one_object: %.0f s, spans=%d covered=%d" % (time.time() - t, st["spans"], out["covered"]))
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
-    for name, s, sem, phong in cases():
-        save(name, s, sem, phong)
+    if sys.argv[1:] == ["c3b_one_object"]:
+        c3b_one_object()
+    else:
+        for name, s, sem, phong in cases():
+            save(name, s, sem, phong)
