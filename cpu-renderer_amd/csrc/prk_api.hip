@@ -23,14 +23,17 @@
 extern "C" {
 hipError_t prk_launch_tri_draw(const prk::DrawRec *, uint32_t, uint32_t *, uint32_t, hipStream_t);
 hipError_t prk_bin_phase1(const prk::FrameParams *, uint32_t *, uint32_t *, void *, void *, size_t *, hipStream_t);
-hipError_t prk_bin_count(const prk::FrameParams *, uint32_t *, void *, hipStream_t);
+hipError_t prk_bin_count(const prk::FrameParams *, uint32_t *, void *, uint32_t *, uint32_t *, uint8_t *, hipStream_t);
 uint32_t prk_cs_chunks(uint32_t);
+uint32_t prk_cs_nchunks(uint32_t, uint32_t);
+uint32_t prk_cs_band_runs_per_chunk(const prk::FrameParams *);
+uint32_t prk_bin_runs(uint32_t);
 uint32_t prk_cs_max_tiles(void);
 uint32_t prk_cs_max_pairs(void);
 int prk_cs_ready(uint32_t);
 hipError_t prk_bin_cs(const prk::FrameParams *, const void *, const uint32_t *, uint32_t *, uint32_t *, uint32_t *,
                       uint32_t *, uint32_t *, uint32_t, uint32_t *, uint32_t *, void *, uint32_t *, uint8_t *, uint32_t,
-                      uint8_t *, hipStream_t);
+                      uint8_t *, const uint32_t *, const uint32_t *, uint32_t, hipStream_t);
 hipError_t prk_bin_phase2(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, uint32_t *, void *,
                           uint32_t *, void *, uint32_t *, uint32_t *, uint8_t *, uint32_t, uint8_t *, void *, size_t *,
                           hipStream_t);
@@ -172,7 +175,7 @@ struct prk_context {
     struct BinSet {
         DevBuf d_draws, d_texs, d_tri_draw, d_ranges, d_tri_n, d_tri_off, d_pair_tri, d_keys_a, d_vals_a, d_keys_b,
             d_bins, d_offs, d_temp, d_won, d_list, d_nwin, d_wtag, d_recs, d_trwon, d_wlist, d_seltemp, d_trec,
-            d_ghist, d_tile_tot, d_chunk, d_info;
+            d_ghist, d_tile_tot, d_chunk, d_info, d_runlist, d_run_n;
         uint32_t *h_info = nullptr;       // pinned: [entry count, overflow] of the set's last binning
         hipEvent_t counted_ev = nullptr;  // h_info of this set's binning has landed
         // bytes last uploaded into d_draws / d_texs and the buffer they went
@@ -370,7 +373,7 @@ int prk_destroy(prk_context *c) {
         DevBuf *bb[] = {&B.d_draws, &B.d_texs, &B.d_tri_draw, &B.d_ranges, &B.d_tri_n, &B.d_tri_off, &B.d_pair_tri,
                         &B.d_keys_a, &B.d_vals_a, &B.d_keys_b, &B.d_bins, &B.d_offs, &B.d_temp, &B.d_won,
                         &B.d_list, &B.d_nwin, &B.d_wtag, &B.d_recs, &B.d_trwon, &B.d_wlist, &B.d_seltemp,
-                        &B.d_trec, &B.d_ghist, &B.d_tile_tot, &B.d_chunk, &B.d_info};
+                        &B.d_trec, &B.d_ghist, &B.d_tile_tot, &B.d_chunk, &B.d_info, &B.d_runlist, &B.d_run_n};
         for (DevBuf *b : bb) b->release();
         if (B.free_ev) (void)hipEventDestroy(B.free_ev);
         if (B.binned_ev) (void)hipEventDestroy(B.binned_ev);
@@ -1218,7 +1221,13 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
         // count plus room; a first frame guesses 2.5 per triangle, C3b has
         // 3.2); a frame with more entries leaves its bins empty and is re-run
         // below, once the count is known.
-        const uint32_t nch = prk_cs_chunks(T);
+        // a row band's sort walks only its triangles (listed per run by k_bin_band)
+        const uint32_t per = prk_cs_band_runs_per_chunk(&fp);
+        if (per) {
+            PRK_TRY(bset_ensure(B.d_runlist, (size_t)prk_bin_runs(T) * 2048 * 4));
+            PRK_TRY(bset_ensure(B.d_run_n, (size_t)prk_bin_runs(T) * 4));
+        }
+        const uint32_t nch = prk_cs_nchunks(T, per);
         const uint64_t want64 = c->pair_hint ? (uint64_t)c->pair_hint + c->pair_hint / 8 + 4096
                                              : std::max<uint64_t>(5ull * T / 2, 1u << 16);
         const uint32_t want = (uint32_t)std::min<uint64_t>(want64, prk_cs_max_pairs());
@@ -1246,12 +1255,13 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
         won = (uint8_t *)B.d_won.p;
         trwon = span_rec ? (uint8_t *)B.d_trwon.p : nullptr;
         PRK_TRY(hipEventRecord(c->ev[slot][0], bs));
-        PRK_TRY(prk_bin_count(&fp, (uint32_t *)B.d_tri_n.p, B.d_ranges.p, bs));
+        uint32_t *runlist = per ? (uint32_t *)B.d_runlist.p : nullptr, *run_n = per ? (uint32_t *)B.d_run_n.p : nullptr;
+        PRK_TRY(prk_bin_count(&fp, (uint32_t *)B.d_tri_n.p, B.d_ranges.p, runlist, run_n, trwon, bs));
         uint32_t *chunk = (uint32_t *)B.d_chunk.p;
         PRK_TRY(prk_bin_cs(&fp, B.d_ranges.p, (const uint32_t *)B.d_tri_n.p, (uint32_t *)B.d_ghist.p,
                            (uint32_t *)B.d_tile_tot.p, chunk, chunk + nch, (uint32_t *)B.d_offs.p, cap,
                            (uint32_t *)B.d_info.p, (uint32_t *)B.d_tri_off.p, B.d_bins.p, (uint32_t *)B.d_pair_tri.p,
-                           won, won_stride, trwon, bs));
+                           won, won_stride, trwon, runlist, run_n, per, bs));
         PRK_TRY(hipMemcpyAsync(B.h_info, B.d_info.p, 8, hipMemcpyDeviceToHost, bs));
         PRK_TRY(hipEventRecord(B.counted_ev, bs));
     } else {
@@ -1795,10 +1805,29 @@ int prk_fill_edge_count(const float *V, uint32_t vertex_count, const float P[3],
         }
         float ax = pr[1][0] - pr[0][0], ay = pr[1][1] - pr[0][1], az = pr[1][2] - pr[0][2];
         float bx = pr[2][0] - pr[0][0], by = pr[2][1] - pr[0][1], bz = pr[2][2] - pr[0][2];
-        host_normalize(ax, ay, az);
-        host_normalize(bx, by, bz);
-        const float cx = ay * bz - az * by, cy = az * bx - ax * bz, cz = ax * by - ay * bx;
-        if (!((0.0f * cx + 0.0f * cy) + (-1.0f) * cz > 0.0f)) continue;  // 3943
+        // Back-face test (3926-3943): Inner((0,0,-1), Cross(Normalize(A),
+        // Normalize(B))) > 0, i.e. cz = a.x*b.y - a.y*b.x < 0 of the normalised
+        // a, b.  Their components carry a relative error of at most ~5 ulp and
+        // are at most 1, so the rounded cz lies within ~2^-19 of the exact
+        // (Ax*By - Ay*Bx) / (|A||B|): when that exceeds 2^-16 in magnitude
+        // (computed in double from the same float A, B: products exact), its
+        // sign is the test's, and the two normalisations are skipped.  Other
+        // cases (near-degenerate, tiny / huge / non-finite) take the float ops.
+        const float ma = std::max(std::fabs(ax), std::max(std::fabs(ay), std::fabs(az)));
+        const float mb = std::max(std::fabs(bx), std::max(std::fabs(by), std::fabs(bz)));
+        bool front;
+        const double D = (double)ax * by - (double)ay * bx;
+        const double A2 = ((double)ax * ax + (double)ay * ay) + (double)az * az;
+        const double B2 = ((double)bx * bx + (double)by * by) + (double)bz * bz;
+        if (ma >= 0x1p-40f && ma <= 0x1p40f && mb >= 0x1p-40f && mb <= 0x1p40f && D * D > 0x1p-32 * A2 * B2) {
+            front = D < 0.0;
+        } else {
+            host_normalize(ax, ay, az);
+            host_normalize(bx, by, bz);
+            const float cx = ay * bz - az * by, cy = az * bx - ax * bz, cz = ax * by - ay * bx;
+            front = (0.0f * cx + 0.0f * cy) + (-1.0f) * cz > 0.0f;  // 3943
+        }
+        if (!front) continue;
         for (int e = 0; e < 3; ++e) {
             const float y0 = pr[e][1], y1 = pr[(e + 1) % 3][1];
             const float mn = y0 > y1 ? y1 : y0, mx = y0 > y1 ? y0 : y1;  // 3957-3966

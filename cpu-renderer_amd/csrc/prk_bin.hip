@@ -24,6 +24,7 @@
 #include <hipcub/hipcub.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 
+#include <algorithm>
 #include <atomic>
 
 #include "prk_device.h"
@@ -230,9 +231,21 @@ __global__ void __launch_bounds__(kCountThreads) k_setup_rec(FrameParams fp, con
 // (256 at a time, listing the ones with entries in LDS in triangle order),
 // then sets up the listed triangles' records 64 per wave.  (Two launches
 // before: C3b at N = 8, 20 + 23 us serial, each reading the band test's
-// inputs of all 1 M triangles.)
+// inputs of all 1 M triangles.)  The run's list of triangles with entries
+// also goes out (runlist[run * kRecRun + i], run_n[run]): the band's
+// counting sort walks only those (BandRuns), and the run clears the frame's
+// won flag of every one of its triangles (trwon, span-record frames).
+struct BandRuns {
+    const uint32_t *list;  // per run of kRecRun triangles: its triangles with entries, in order
+    const uint32_t *n;     // per run: how many
+    uint32_t nruns;
+    uint32_t per;          // runs per counting-sort chunk
+};
 __global__ void __launch_bounds__(kCountThreads) k_bin_band(FrameParams fp, uint32_t *__restrict__ tri_n,
-                                                             TileRange *__restrict__ ranges) {
+                                                             TileRange *__restrict__ ranges,
+                                                             uint32_t *__restrict__ runlist,
+                                                             uint32_t *__restrict__ run_n,
+                                                             uint8_t *__restrict__ trwon) {
     __shared__ float4 stage[kCountThreads / 64][64 * 10];
     __shared__ uint32_t list[kRecRun];
     __shared__ uint32_t scratch[kCountThreads / 64];
@@ -249,16 +262,22 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_band(FrameParams fp, uint
             ranges[g] = tr;
             ne = range_entries(tr);
             tri_n[g] = ne;
+            if (trwon) trwon[g] = 0;
         } else if (g == fp.tri_count) {
             tri_n[g] = 0;  // sentinel: a scan's last element is the total
         }
-        const uint32_t f = ne != 0 && fp.trec ? 1u : 0u;
+        const uint32_t f = ne != 0 ? 1u : 0u;
         uint32_t tot;
         const uint32_t pos = cs_block_excl_scan(f, scratch, tot);
-        if (f) list[n + pos] = g;
+        if (f) {
+            list[n + pos] = g;
+            runlist[g0 + n + pos] = g;
+        }
         n += tot;
     }
+    if (threadIdx.x == 0) run_n[blockIdx.x] = n;
     __syncthreads();
+    if (!fp.trec) return;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (uint32_t b = (uint32_t)wv * 64; b < n; b += kCountThreads) {
         const uint32_t i = b + lane;
@@ -418,19 +437,59 @@ __device__ __forceinline__ void for_each_entry(const FrameParams &fp, const Tile
             f((uint32_t)(ty * fp.tiles_x), PRK_ROWCLASS ? (uint32_t)((kMaxRep << kRowClassBits) | kMaxClass) : 0u);
 }
 
+// The triangles of counting-sort chunk c, in order, kCsThreads at a time:
+// a whole frame's chunk is kCsChunk consecutive triangles; a row band's (BandRuns)
+// is the listed triangles of runs [c * per, (c + 1) * per) — those with entries.
+struct ChunkTris {
+    uint32_t g0, count;       // whole frame: triangles [g0, g0 + count)
+    const uint32_t *list;     // band: null, or the chunk's runs' lists
+    uint32_t r0, nr;          // band: runs [r0, r0 + nr)
+    uint32_t pre[65];         // band: prefix of the runs' counts (per <= 64)
+};
+constexpr uint32_t kMaxRunsPerChunk = 64;
+__device__ __forceinline__ void chunk_tris(const FrameParams &fp, const BandRuns &br, uint32_t c, ChunkTris &ct) {
+    if (threadIdx.x == 0) {
+        ct.list = br.list;
+        if (!br.list) {
+            ct.g0 = c * kCsChunk;
+            ct.count = ct.g0 < fp.tri_count ? min(kCsChunk, fp.tri_count - ct.g0) : 0u;
+        } else {
+            ct.r0 = c * br.per;
+            ct.nr = min(br.per, br.nruns - ct.r0);
+            uint32_t run = 0;
+            for (uint32_t k = 0; k < ct.nr; ++k) {
+                ct.pre[k] = run;
+                run += br.n[ct.r0 + k];
+            }
+            ct.pre[ct.nr] = run;
+            ct.count = run;
+        }
+    }
+    __syncthreads();
+}
+// The p-th triangle of the chunk (p < count).
+__device__ __forceinline__ uint32_t chunk_tri(const ChunkTris &ct, uint32_t p) {
+    if (!ct.list) return ct.g0 + p;
+    uint32_t k = 0;
+    while (k + 1 < ct.nr && ct.pre[k + 1] <= p) ++k;
+    return ct.list[(size_t)(ct.r0 + k) * kRecRun + (p - ct.pre[k])];
+}
+
 __global__ void __launch_bounds__(kCsThreads) k_cs_hist(FrameParams fp, const TileRange *__restrict__ ranges,
                                                          const uint32_t *__restrict__ tri_n,
                                                          uint32_t *__restrict__ ghist,
-                                                         uint32_t *__restrict__ chunk_tot, uint32_t ntiles) {
+                                                         uint32_t *__restrict__ chunk_tot, uint32_t ntiles,
+                                                         BandRuns br) {
     extern __shared__ uint32_t h[];
     __shared__ uint32_t scratch[kCsThreads / 64];
+    __shared__ ChunkTris ct;
     for (uint32_t i = threadIdx.x; i < ntiles; i += kCsThreads) h[i] = 0;
-    __syncthreads();
     const uint32_t c = blockIdx.x;
+    chunk_tris(fp, br, c, ct);  // (its barrier also orders the zeroed histogram)
+    __syncthreads();
     uint32_t sum = 0;
-    for (uint32_t r = 0; r < kCsTrisPerThread; ++r) {
-        const uint32_t g = c * kCsChunk + r * kCsThreads + threadIdx.x;
-        if (g >= fp.tri_count) break;
+    for (uint32_t p = threadIdx.x; p < ct.count; p += kCsThreads) {
+        const uint32_t g = chunk_tri(ct, p);
         const uint32_t n = tri_n[g];
         if (!n) continue;
         sum += n;
@@ -568,19 +627,26 @@ __global__ void __launch_bounds__(kCsThreads) k_cs_emit(FrameParams fp, const Ti
                                                          const uint32_t *__restrict__ info, uint32_t ntiles,
                                                          uint32_t *__restrict__ tri_off, uint2 *__restrict__ bins,
                                                          uint32_t *__restrict__ pair_tri, uint8_t *__restrict__ won,
-                                                         uint32_t won_stride, uint8_t *__restrict__ trwon) {
+                                                         uint32_t won_stride, uint8_t *__restrict__ trwon,
+                                                         BandRuns br) {
     extern __shared__ uint32_t cur[];
     __shared__ uint32_t scratch[kCsThreads / 64];
+    __shared__ ChunkTris ct;
     const uint32_t c = xcd_chunk(blockIdx.x, gridDim.x);
     const bool over = info[1] != 0;
     if (!over) {
         const uint32_t *gh = ghist + (size_t)c * ntiles;
         for (uint32_t i = threadIdx.x; i < ntiles; i += kCsThreads) cur[i] = offs[i] + gh[i];
     }
+    chunk_tris(fp, br, c, ct);
+    // (a band's run lists hold only triangles with entries; its trwon flags
+    // were cleared by k_bin_band for every triangle)
+    if (br.list) trwon = nullptr;
     uint32_t base = chunk_base[c];
-    for (uint32_t r = 0; r < kCsTrisPerThread; ++r) {
-        const uint32_t g = c * kCsChunk + r * kCsThreads + threadIdx.x;
-        const bool in = g < fp.tri_count;
+    for (uint32_t p0 = 0; p0 < ct.count; p0 += kCsThreads) {
+        const uint32_t p = p0 + threadIdx.x;
+        const bool in = p < ct.count;
+        const uint32_t g = in ? chunk_tri(ct, p) : 0u;
         const uint32_t n = in ? tri_n[g] : 0u;
         uint32_t tot;
         const uint32_t j0 = base + cs_block_excl_scan(n, scratch, tot);  // (also orders the cursor loads)
@@ -713,14 +779,15 @@ hipError_t prk_bin_phase2(const prk::FrameParams *fp, const void *ranges, const 
 // no pair written; the caller re-runs the frame with more room).
 // ghist: nchunks * ntiles u32; tile_tot: ntiles; chunk_tot / chunk_base: nchunks.
 // All-AVX frames (fp->trec): the setup records are computed by k_setup_rec.
-hipError_t prk_bin_count(const prk::FrameParams *fp, uint32_t *tri_n, void *ranges, hipStream_t s) {
+hipError_t prk_bin_count(const prk::FrameParams *fp, uint32_t *tri_n, void *ranges, uint32_t *runlist,
+                         uint32_t *run_n, uint8_t *trwon, hipStream_t s) {
     const uint32_t n = fp->tri_count + 1;
     // A whole-frame target sets up (nearly) every triangle: inline records
     // (C3b: 76 us against 22 + 68 us split); a row band only its own.
     const bool band = fp->row0 > 0 || fp->row1 < fp->H;
-    if (band && PRK_BIN_BAND) {  // (k_bin_band also writes the sentinel tri_n[tri_count])
+    if (band && PRK_BIN_BAND && runlist) {  // (k_bin_band also writes the sentinel tri_n[tri_count])
         hipLaunchKernelGGL(prk::k_bin_band, dim3((n + prk::kRecRun - 1) / prk::kRecRun), dim3(prk::kCountThreads),
-                           0, s, *fp, tri_n, reinterpret_cast<prk::TileRange *>(ranges));
+                           0, s, *fp, tri_n, reinterpret_cast<prk::TileRange *>(ranges), runlist, run_n, trwon);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(prk::k_bin_count, dim3((n + prk::kCountThreads - 1) / prk::kCountThreads),
@@ -730,6 +797,20 @@ hipError_t prk_bin_count(const prk::FrameParams *fp, uint32_t *tri_n, void *rang
                            dim3(prk::kCountThreads), 0, s, *fp, tri_n);
     return hipGetLastError();
 }
+
+// A row band's counting sort walks only its runs' listed triangles, `per`
+// runs per chunk: about one whole-frame chunk's worth (kCsChunk) of the
+// band's share of the triangles, so a narrow band has few chunks (and a
+// small chunk x tile histogram).  0: not a band (whole-frame chunks).
+uint32_t prk_cs_band_runs_per_chunk(const prk::FrameParams *fp) {
+    const bool band = fp->row0 > 0 || fp->row1 < fp->H;
+    if (!band || !PRK_BIN_BAND) return 0;
+    const int64_t rows = std::max<int64_t>(1, (int64_t)std::min(fp->row1, fp->H) - fp->row0);
+    const int64_t share = std::max<int64_t>(1, (int64_t)fp->H / rows);  // ~ triangles per band triangle
+    const int64_t per = (int64_t)prk::kCsChunk * share / prk::kRecRun;
+    return (uint32_t)std::min<int64_t>(prk::kMaxRunsPerChunk, std::max<int64_t>(2, per));
+}
+uint32_t prk_bin_runs(uint32_t tri_count) { return (tri_count + 1 + prk::kRecRun - 1) / prk::kRecRun; }
 
 // The counting sort's per-tile LDS (4 B per tile) above 64 KiB needs the
 // dynamic-LDS attribute of k_cs_hist / k_cs_emit, which is per device: set
@@ -756,22 +837,31 @@ int prk_cs_ready(uint32_t ntiles) {
 }
 
 uint32_t prk_cs_chunks(uint32_t tri_count) { return (tri_count + prk::kCsChunk - 1) / prk::kCsChunk; }
+// Counting-sort chunks of a frame: whole-frame chunks, or (per > 0) a band's
+// chunks of `per` runs.
+uint32_t prk_cs_nchunks(uint32_t tri_count, uint32_t per) {
+    if (!per) return prk_cs_chunks(tri_count);
+    return (prk_bin_runs(tri_count) + per - 1) / per;
+}
 uint32_t prk_cs_max_tiles(void) { return prk::kCsMaxTiles; }
 uint32_t prk_cs_max_pairs(void) { return prk::kCsPairMask; }
 
 hipError_t prk_bin_cs(const prk::FrameParams *fp, const void *ranges, const uint32_t *tri_n, uint32_t *ghist,
                       uint32_t *tile_tot, uint32_t *chunk_tot, uint32_t *chunk_base, uint32_t *offs, uint32_t cap,
                       uint32_t *info, uint32_t *tri_off, void *bins, uint32_t *pair_tri, uint8_t *won,
-                      uint32_t won_stride, uint8_t *trwon, hipStream_t s) {
+                      uint32_t won_stride, uint8_t *trwon, const uint32_t *runlist, const uint32_t *run_n,
+                      uint32_t per, hipStream_t s) {
     const uint32_t ntiles = (uint32_t)(fp->tiles_x * fp->tiles_y);
     if (ntiles > prk::kCsMaxTiles || ntiles == 0) return hipErrorInvalidValue;
-    const uint32_t nch = prk_cs_chunks(fp->tri_count);
+    prk::BandRuns br{nullptr, nullptr, 0u, 0u};
+    if (per && runlist) br = prk::BandRuns{runlist, run_n, prk_bin_runs(fp->tri_count), per};
+    const uint32_t nch = prk_cs_nchunks(fp->tri_count, br.list ? per : 0u);
     const prk::TileRange *tr = reinterpret_cast<const prk::TileRange *>(ranges);
     const size_t lds = (size_t)ntiles * 4;
     if (!prk_cs_ready(ntiles)) return hipErrorNotSupported;
     if (nch) {
         hipLaunchKernelGGL(prk::k_cs_hist, dim3(nch), dim3(prk::kCsThreads), lds, s, *fp, tr, tri_n, ghist, chunk_tot,
-                           ntiles);
+                           ntiles, br);
         hipLaunchKernelGGL(prk::k_cs_colscan, dim3((ntiles + 63) / 64), dim3(64 * prk::kColSegs), 0, s, ghist, nch,
                            ntiles, tile_tot);
     } else {
@@ -783,7 +873,7 @@ hipError_t prk_bin_cs(const prk::FrameParams *fp, const void *ranges, const uint
     if (nch)
         hipLaunchKernelGGL(prk::k_cs_emit, dim3(nch), dim3(prk::kCsThreads), lds, s, *fp, tr, tri_n, ghist, offs,
                            chunk_base, info, ntiles, tri_off, reinterpret_cast<uint2 *>(bins), pair_tri, won,
-                           won_stride, trwon);
+                           won_stride, trwon, br);
     if (PRK_ROWCLASS)
         hipLaunchKernelGGL(prk::k_cs_class, dim3(ntiles), dim3(256), 0, s, offs, reinterpret_cast<uint2 *>(bins));
     return hipGetLastError();

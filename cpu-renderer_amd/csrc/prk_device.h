@@ -195,6 +195,35 @@ __device__ __forceinline__ float maxps(float a, float b) { return a > b ? a : b;
 __device__ __forceinline__ float minps(float a, float b) { return a < b ? a : b; }  // MINPS
 __device__ __forceinline__ float clamp01(float x) { return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x); }
 
+// FillLineOptimized's span ends (projekt.cpp:1545-1592): LeftX / RightX
+// clamped to [0, W-1], MinX = round(LeftX), MaxX = round(RightX), and XDiff =
+// round(R.X) - round(L.X) on the unclamped ends (1568-1570).  A clamped end
+// is 0 or W - 1, which round to themselves, so two roundings serve all four
+// (PRK_SPAN_ROUND2; 0: the literal four).  False for a NaN end (pinned: the
+// span draws nothing).  st: the single-thread overload's left-clip XOffset
+// (2508).
+#ifndef PRK_SPAN_ROUND2
+#define PRK_SPAN_ROUND2 1
+#endif
+__device__ __forceinline__ bool span_ends(float LX, float RX, int32_t W, bool st, int32_t &MinX, int32_t &MaxX,
+                                          int32_t &XDiff, float &XOffset) {
+    XOffset = 0.0f;
+    if (LX != LX || RX != RX) return false;
+    const bool lneg = LX < 0, lbig = LX >= W, rneg = RX < 0, rbig = RX >= W;
+    if (lneg) XOffset = st ? -XOffset : -LX;  // 1545-1565
+    if (PRK_SPAN_ROUND2) {
+        const int32_t rl = round_s32(LX), rr = round_s32(RX);
+        XDiff = (int32_t)((uint32_t)rr - (uint32_t)rl);
+        MinX = lneg ? 0 : (lbig ? W - 1 : rl);
+        MaxX = rneg ? 0 : (rbig ? W - 1 : rr);
+    } else {
+        XDiff = (int32_t)((uint32_t)round_s32(RX) - (uint32_t)round_s32(LX));
+        MinX = round_s32(lneg ? 0.0f : (lbig ? (float)W - 1 : LX));
+        MaxX = round_s32(rneg ? 0.0f : (rbig ? (float)W - 1 : RX));
+    }
+    return true;
+}
+
 // Normalize (pinned scalar form) — used by the AET edge step and DrawModel.
 __device__ __forceinline__ void normalize_rcp(float &x, float &y, float &z) {
     float s = 1.0f / sqrtf((x * x + y * y) + z * z);
@@ -729,8 +758,10 @@ __device__ __forceinline__ void step_edge(EdgeX &E) {
 }
 
 // AET insertion order (projekt.cpp:3663-3667).
+// (bitwise & / | : the comparisons have no side effects, and short-circuit
+// && / || compiled to a branch per term)
 __device__ __forceinline__ bool insert_before(const Edge &A, const Edge &B) {
-    return A.X < B.X || (A.X == B.X && (A.G < B.G || (A.G == B.G && A.Left < B.Left)));
+    return (A.X < B.X) | ((A.X == B.X) & ((A.G < B.G) | ((A.G == B.G) & (A.Left < B.Left))));
 }
 
 // Per-triangle active edge table of DrawModelOptimized(RenderQueue,...)
@@ -766,7 +797,7 @@ struct Walker {
     // AET insertion order (projekt.cpp:3663-3667) of edge a before edge b.
     __device__ __forceinline__ bool before(int a, int b) const {
         const float xa = X(a), xb = X(b), ga = G(a), gb = G(b);
-        return xa < xb || (xa == xb && (ga < gb || (ga == gb && Lf(a) < Lf(b))));
+        return (xa < xb) | ((xa == xb) & ((ga < gb) | ((ga == gb) & (Lf(a) < Lf(b)))));
     }
 
     __device__ __forceinline__ void insert(int k) {  // 3654-3713

@@ -189,17 +189,9 @@ __device__ __forceinline__ int span_setup_avx(const FrameParams &fp, const TileC
                                               uint32_t tag, int32_t texi, const Edge &L, const Edge &R,
                                               int32_t Row, bool st) {
     if (Row < tc.y0) return 0;
-    const int32_t W = fp.W;
-    float XOffset = 0.0f;
-    float LeftX = L.X;  // 1545-1565
-    if (LeftX < 0) { XOffset = st ? -XOffset : -L.X; LeftX = 0; }  // single-thread: -XOffset (2508)
-    else if (LeftX >= W) LeftX = (float)W - 1;
-    float RightX = R.X;
-    if (RightX < 0) RightX = 0;
-    else if (RightX >= W) RightX = (float)W - 1;
-    if (LeftX != LeftX || RightX != RightX) return 0;  // pinned: NaN edge X draws nothing
-    const int32_t XDiff = (int32_t)((uint32_t)round_s32(R.X) - (uint32_t)round_s32(L.X));  // 1568-1570
-    const int32_t MinX = round_s32(LeftX), MaxX = round_s32(RightX);  // 1588-1592
+    float XOffset;
+    int32_t MinX, MaxX, XDiff;
+    if (!span_ends(L.X, R.X, fp.W, st, MinX, MaxX, XDiff, XOffset)) return 0;  // 1545-1592
     int32_t LeftXa = MinX;
     if (MinX & 7) {  // 1594-1609
         LeftXa = MinX & ~7;
@@ -1216,16 +1208,9 @@ __device__ __forceinline__ void walk_record(const FrameParams &fp, const Edge &L
                                             int32_t texi, const TileRange &tr, uint32_t jb, int ntx,
                                             const uint8_t *__restrict__ won, SpanRec *__restrict__ recs, bool st) {
     if (Row < fp.row0) return;
-    const int32_t W = fp.W;
-    float XOffset = 0.0f;
-    float LeftX = L.X;  // 1545-1565
-    if (LeftX < 0) { XOffset = st ? -XOffset : -L.X; LeftX = 0; }  // single-thread: -XOffset (2508)
-    else if (LeftX >= W) LeftX = (float)W - 1;
-    float RightX = R.X;
-    if (RightX < 0) RightX = 0;
-    else if (RightX >= W) RightX = (float)W - 1;
-    if (LeftX != LeftX || RightX != RightX) return;  // pinned: NaN edge X draws nothing
-    const int32_t MinX = round_s32(LeftX), MaxX = round_s32(RightX);  // 1588-1592
+    float XOffset;
+    int32_t MinX, MaxX, XDiff;
+    if (!span_ends(L.X, R.X, fp.W, st, MinX, MaxX, XDiff, XOffset)) return;  // 1545-1592
     if (MinX >= MaxX) return;  // [MinX, MaxX) empty
     const int32_t rr = Row - fp.row0, ty = rr / fp.tile_h, ly = rr - ty * fp.tile_h;
     if (ty < (int)tr.ty0 || ty > (int)tr.ty1) return;  // (binning covers every span pixel)
@@ -1241,7 +1226,6 @@ __device__ __forceinline__ void walk_record(const FrameParams &fp, const Edge &L
         for (int tx = tx0; tx <= tx1; ++tx) any |= won[(size_t)(jrow + tx) * fp.tile_h + ly] != 0;
         if (!any) return;
     }
-    const int32_t XDiff = (int32_t)((uint32_t)round_s32(R.X) - (uint32_t)round_s32(L.X));  // 1568-1570
     int32_t LeftXa = MinX;
     if (MinX & 7) {  // 1594-1609
         LeftXa = MinX & ~7;

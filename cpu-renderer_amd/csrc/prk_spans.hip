@@ -150,18 +150,10 @@ __device__ __forceinline__ void obj_step(ObjEdge &E) {
 // covers nothing.
 __device__ __forceinline__ bool obj_span(const FrameParams &fp, const ObjEdge &L, const ObjEdge &R, int32_t Row,
                                          int32_t texi, bool st, SpanRecG &rec, SpanPos &pos) {
-    const int32_t W = fp.W;
-    float XOffset = 0.0f;
-    float LeftX = L.X;  // 1545-1565
-    if (LeftX < 0) { XOffset = st ? -XOffset : -L.X; LeftX = 0; }  // single-thread: -XOffset (2508)
-    else if (LeftX >= W) LeftX = (float)W - 1;
-    float RightX = R.X;
-    if (RightX < 0) RightX = 0;
-    else if (RightX >= W) RightX = (float)W - 1;
-    if (LeftX != LeftX || RightX != RightX) return false;  // pinned: NaN edge X draws nothing
-    const int32_t MinX = round_s32(LeftX), MaxX = round_s32(RightX);  // 1588-1592
+    float XOffset;
+    int32_t MinX, MaxX, XDiff;
+    if (!span_ends(L.X, R.X, fp.W, st, MinX, MaxX, XDiff, XOffset)) return false;  // 1545-1592
     if (MinX >= MaxX) return false;
-    const int32_t XDiff = (int32_t)((uint32_t)round_s32(R.X) - (uint32_t)round_s32(L.X));  // 1568-1570
     int32_t LeftXa = MinX;
     if (MinX & 7) {  // 1594-1609
         LeftXa = MinX & ~7;

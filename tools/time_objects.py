@@ -71,9 +71,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--json")
+    ap.add_argument("--only", default="", help="comma-separated case names")
     a = ap.parse_args()
+    only = set(x for x in a.only.split(",") if x)
     out = {}
     for name, s, sem, phong, tpo in cases():
+        if only and name not in only:
+            continue
         ms = time_case(s, sem, phong, tpo, a.frames)
         out[name] = {"tris": s.tri_count, "tris_per_object": tpo, "target": "%dx%d" % (s.width, s.height),
                      "ms_per_frame": round(ms, 3), "mpixels_s": round(s.width * s.height / ms / 1e3, 1)}
