@@ -54,10 +54,10 @@ hipError_t prk_obj_gather(const void *, const uint32_t *, const uint32_t *, cons
 hipError_t prk_obj_bound(const prk::FrameParams *, const void *, uint32_t, const unsigned long long *, const void *,
                          unsigned long long *, hipStream_t);
 uint32_t prk_obj_walk_lcap(void);
-hipError_t prk_obj_walk(const prk::FrameParams *, const void *, uint32_t, const uint32_t *, uint32_t, uint32_t,
-                        const uint32_t *, const unsigned long long *, const uint32_t *, uint32_t, int32_t *,
-                        const uint32_t *, const uint32_t *, void *, const unsigned long long *, void *, void *, void *,
-                        uint32_t *, const void *, uint32_t *, hipStream_t);
+hipError_t prk_obj_walk(const prk::FrameParams *, const void *, uint32_t, const uint32_t *, const uint32_t *, uint32_t,
+                        const unsigned long long *, const uint32_t *, int32_t *, const uint32_t *, const uint32_t *,
+                        void *, const unsigned long long *, void *, void *, void *, uint32_t *, const void *,
+                        uint32_t *, hipStream_t);
 hipError_t prk_scan_u32(const uint32_t *, uint32_t *, uint32_t, void *, size_t *, hipStream_t);
 hipError_t prk_scan_u64(const unsigned long long *, unsigned long long *, uint32_t, void *, size_t *, hipStream_t);
 hipError_t prk_span_count(const prk::FrameParams *, const void *, uint32_t, uint32_t *, hipStream_t);
@@ -250,11 +250,11 @@ struct prk_context {
     struct SpanScratch {
         DevBuf d_draws, d_texs, d_objs, d_edges, d_ord, d_temp, d_recs, d_pos, d_span_tri, d_scnt, d_soff, d_keys_a,
             d_vals_a, d_keys_b, d_vals_b, d_offs, d_nwin, d_wtag, d_edges_in, d_spans_in, d_srecs, d_work, d_ekeys,
-            d_ekeys2, d_evals, d_ecnt, d_escan, d_rcnt, d_rscan, d_bound, d_oslot, d_k0obj, d_k0tri0, d_big_lds,
+            d_ekeys2, d_evals, d_ecnt, d_escan, d_rcnt, d_rscan, d_bound, d_oslot, d_k0obj, d_k0tri0,
             d_big_gl, d_big_off, d_big_cap, d_pool, d_k1src, d_err;
         // host tables of the pass, kept until their asynchronous uploads ran
         std::vector<ObjDesc> h_objs;
-        std::vector<uint32_t> h_k0obj, h_k0tri0, h_big_lds, h_big_gl, h_big_cap, h_k1src;
+        std::vector<uint32_t> h_k0obj, h_k0tri0, h_big_gl, h_big_cap, h_k1src;
         std::vector<unsigned long long> h_big_off;
         std::vector<prk::DrawRec> h_draws;
         std::vector<prk::TexRec> h_texs;
@@ -388,7 +388,7 @@ int prk_destroy(prk_context *c) {
                         &S.d_span_tri, &S.d_scnt, &S.d_soff, &S.d_keys_a, &S.d_vals_a, &S.d_keys_b, &S.d_vals_b,
                         &S.d_offs, &S.d_nwin, &S.d_wtag, &S.d_edges_in, &S.d_spans_in, &S.d_srecs, &S.d_work,
                         &S.d_ekeys, &S.d_ekeys2, &S.d_evals, &S.d_ecnt, &S.d_escan, &S.d_rcnt, &S.d_rscan,
-                        &S.d_bound, &S.d_oslot, &S.d_k0obj, &S.d_k0tri0, &S.d_big_lds, &S.d_big_gl, &S.d_big_off,
+                        &S.d_bound, &S.d_oslot, &S.d_k0obj, &S.d_k0tri0, &S.d_big_gl, &S.d_big_off,
                         &S.d_big_cap, &S.d_pool, &S.d_k1src, &S.d_err};
         for (DevBuf *b : sb) b->release();
         if (S.h_rb) (void)hipHostFree(S.h_rb);
@@ -485,6 +485,8 @@ int prk_target_clear(prk_context *c, uint32_t color, float z) {
     RESOLVE_COUNT(c);
     if (!c->color) return PRK_ERR_NO_TARGET;
     PRK_TRY(hipSetDevice(c->device));
+    // after a prk_target_upload_async still in flight (it would land on top)
+    if (c->in_wait) PRK_TRY(hipStreamWaitEvent(c->own_stream, c->in_ev, 0));
     size_t n = (size_t)c->W * (c->row1 - c->row0);
     hipLaunchKernelGGL(k_fill_target, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->own_stream,
                        (uint32_t *)c->color, c->pitch, c->zbuf, c->W, c->row1 - c->row0, color, z);
@@ -522,6 +524,7 @@ int prk_target_upload(prk_context *c, const uint32_t *color_host, int32_t host_p
     if (!c->color) return PRK_ERR_NO_TARGET;
     PRK_TRY(hipSetDevice(c->device));
     PRK_TRY(hipStreamSynchronize(c->own_stream));
+    if (c->in_wait) PRK_TRY(hipEventSynchronize(c->in_ev));  // an earlier asynchronous upload lands first
     int rows = c->row1 - c->row0;
     if (color_host)
         PRK_TRY(hipMemcpy2D(c->color, c->pitch, color_host, host_pitch, (size_t)c->W * 4, rows,
@@ -1431,16 +1434,17 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     // objects' triangles numbered 0..ntri-1 in order (FillEdgeTable runs per
     // triangle), caller edge lists' edges after the triangles' edges.  Objects
     // of kObjWaveTris triangles or more are walked by one wave each, their
-    // list in LDS when all their edges fit lcap, else in a pool slice.
+    // list in LDS when their most active edges fit the launch's LDS capacity
+    // (min(lcap, the largest such object's edges)), else in their pool slice.
     S.h_objs.clear();
     S.h_k0obj.clear();
     S.h_k0tri0.clear();
-    S.h_big_lds.clear();
     S.h_big_gl.clear();
     S.h_big_off.clear();
     S.h_big_cap.clear();
     S.h_k1src.clear();
-    uint64_t ntri = 0, nk1 = 0, pool = 0, maxn = 1;
+    uint64_t ntri = 0, nk1 = 0, pool = 0, maxn = 1, maxwave = 0;
+    std::vector<uint32_t> bigm[prk::MODE_COUNT], bige[prk::MODE_COUNT];  // wave-walked objects by mode, their edges
     for (uint32_t di = 0; di < draws.size(); ++di) {
         const prk::DrawRec &d = draws[di];
         if (d.src_kind == 1) {
@@ -1457,13 +1461,10 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
                 const uint64_t edges = 3ull * n;  // the most its FillEdgeTable writes
                 maxn = std::max(maxn, edges);
                 const bool wave = n >= kObjWaveTris;
-                if (wave && edges <= lcap) {
-                    S.h_big_lds.push_back((uint32_t)S.h_objs.size());
-                } else if (wave) {
-                    S.h_big_gl.push_back((uint32_t)S.h_objs.size());
-                    S.h_big_off.push_back(pool);
-                    S.h_big_cap.push_back((uint32_t)edges);
-                    pool += (uint64_t)kWaveListArrays * (edges + 2);
+                if (wave) {
+                    maxwave = std::max(maxwave, edges);
+                    bigm[d.mode].push_back((uint32_t)S.h_objs.size());
+                    bige[d.mode].push_back((uint32_t)edges);
                 }
                 S.h_k0obj.push_back((uint32_t)S.h_objs.size());
                 S.h_k0tri0.push_back((uint32_t)ntri);
@@ -1472,10 +1473,21 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
             }
         }
     }
+    uint32_t nbig[prk::MODE_COUNT];
+    for (int mo = 0; mo < prk::MODE_COUNT; ++mo) {  // one wave launch per mode, each object a pool slice
+        nbig[mo] = (uint32_t)bigm[mo].size();
+        for (size_t i = 0; i < bigm[mo].size(); ++i) {
+            S.h_big_gl.push_back(bigm[mo][i]);
+            S.h_big_off.push_back(pool);
+            S.h_big_cap.push_back(bige[mo][i]);
+            pool += (uint64_t)kWaveListArrays * (bige[mo][i] + 2);
+        }
+    }
     // edge slots (3 per triangle + the caller edges) are indexed by 31 bits
     if (3 * ntri + nk1 >= 0x7FFFFFFFull) return PRK_ERR_LIMIT;
     const uint32_t nobj = (uint32_t)S.h_objs.size(), nk0 = (uint32_t)S.h_k0obj.size();
-    const uint32_t nt = (uint32_t)ntri, nlds = (uint32_t)S.h_big_lds.size(), ngl = (uint32_t)S.h_big_gl.size();
+    const uint32_t nt = (uint32_t)ntri, ngl = (uint32_t)S.h_big_gl.size();
+    const uint32_t wcap = (uint32_t)std::min<uint64_t>(lcap, maxwave);  // the wave walk's LDS list capacity
     // MergeSort key: (object, min(YMin, H), recursion path) in one radix sort
     auto bitlen = [](uint64_t v) { uint32_t b = 0; while (v) { ++b; v >>= 1; } return b; };
     const uint32_t pbits = bitlen(maxn) + 1, ybits = std::max(1u, bitlen((uint64_t)c->H));
@@ -1501,7 +1513,6 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(up(S.d_objs, S.h_objs.data(), S.h_objs.size() * sizeof(ObjDesc)));
     PRK_TRY(up(S.d_k0obj, S.h_k0obj.data(), S.h_k0obj.size() * 4));
     PRK_TRY(up(S.d_k0tri0, S.h_k0tri0.data(), S.h_k0tri0.size() * 4));
-    PRK_TRY(up(S.d_big_lds, S.h_big_lds.data(), S.h_big_lds.size() * 4));
     PRK_TRY(up(S.d_big_gl, S.h_big_gl.data(), S.h_big_gl.size() * 4));
     PRK_TRY(up(S.d_big_off, S.h_big_off.data(), S.h_big_off.size() * 8));
     PRK_TRY(up(S.d_big_cap, S.h_big_cap.data(), S.h_big_cap.size() * 4));
@@ -1578,9 +1589,9 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(S.d_work.ensure(std::max<size_t>(nwork, 1) * 112));
     PRK_TRY(prk_obj_gather(S.d_edges.p, ord, total0p, S.d_edges_in.p, (const uint32_t *)S.d_k1src.p, (uint32_t)nk1,
                            S.d_work.p, nwork, s));
-    PRK_TRY(prk_obj_walk(&fp, S.d_objs.p, nobj, (const uint32_t *)S.d_big_lds.p, nlds, lcap,
-                         (const uint32_t *)S.d_big_gl.p, (const unsigned long long *)S.d_big_off.p,
-                         (const uint32_t *)S.d_big_cap.p, ngl, (int32_t *)S.d_pool.p, escan, total0p, S.d_work.p,
+    PRK_TRY(prk_obj_walk(&fp, S.d_objs.p, nobj, (const uint32_t *)S.d_big_gl.p, nbig, wcap,
+                         (const unsigned long long *)S.d_big_off.p, (const uint32_t *)S.d_big_cap.p,
+                         (int32_t *)S.d_pool.p, escan, total0p, S.d_work.p,
                          oslot, S.d_recs.p, scalar ? S.d_srecs.p : nullptr, S.d_pos.p, (uint32_t *)S.d_span_tri.p,
                          S.d_spans_in.p, (uint32_t *)S.d_err.p, s));
     PRK_TRY(S.d_scnt.ensure(((size_t)nslot + 1) * 4));
@@ -1827,12 +1838,13 @@ int prk_fill_edge_count(const float *V, uint32_t vertex_count, const float P[3],
             const float cx = ay * bz - az * by, cy = az * bx - ax * bz, cz = ax * by - ay * bx;
             front = (0.0f * cx + 0.0f * cy) + (-1.0f) * cz > 0.0f;  // 3943
         }
-        if (!front) continue;
+        uint32_t ne = 0;  // (branch-free: the facing of a triangle soup is a coin toss)
         for (int e = 0; e < 3; ++e) {
             const float y0 = pr[e][1], y1 = pr[(e + 1) % 3][1];
             const float mn = y0 > y1 ? y1 : y0, mx = y0 > y1 ? y0 : y1;  // 3957-3966
-            if (mx > 0 && mn - mx != 0) ++n;                                // 3968, 4066
+            ne += (uint32_t)((mx > 0) & (mn - mx != 0));                   // 3968, 4066
         }
+        n += front ? ne : 0u;
     }
     *count_out = n;
     return PRK_OK;

@@ -259,9 +259,11 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_band(FrameParams fp, uint
             if (!tri_tile_range(fp, g, tr)) {
                 tr.tx0 = 1; tr.tx1 = 0; tr.ty0 = 1; tr.ty1 = 0; tr.oty0 = 1; tr.oty1 = 0;
             }
-            ranges[g] = tr;
             ne = range_entries(tr);
-            tri_n[g] = ne;
+            if (ne) {  // (only the listed triangles' are read: the band's sort, k_won_local of winners)
+                ranges[g] = tr;
+                tri_n[g] = ne;
+            }
             if (trwon) trwon[g] = 0;
         } else if (g == fp.tri_count) {
             tri_n[g] = 0;  // sentinel: a scan's last element is the total

@@ -579,7 +579,15 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
             Head = E[Head].Next;
             E[Rm].Next = -1;
         }
-        if (Head < 0) { Tail = -1; continue; }  // pin: the reference dereferences NULL
+        if (Head < 0) {  // pin: the reference dereferences NULL
+            Tail = -1;
+            // nothing happens on the rows before the next insertion: go there
+            if (!given) {
+                if (ins >= n) break;
+                Row = max(Row, E[ins].YMin - 1);
+            }
+            continue;
+        }
         {
             int32_t Prev = Head, Chk = Head;  // 3722-3749
             while (Chk != Tail) {
@@ -681,9 +689,10 @@ __global__ void __launch_bounds__(64) k_obj_walk(FrameParams fp, const ObjDesc *
 // The AET walk of one large object by one wave.  The list is an array in
 // list order (position p = the p-th edge from ListHead) holding, beside each
 // edge index, the fields the list operations read (X, Gradient, Left, YMax);
-// the edges themselves stay in the working copy.  It lives in LDS for objects
-// of at most `lcap` edges and in device memory (a slice of a pool sized by the
-// object's edge count) beyond that: the list has no length limit, as the
+// the edges themselves stay in the working copy.  It lives in LDS when the
+// object's most simultaneously listed edges (obj_max_active) fit `lcap`, and
+// in device memory (a slice of a pool sized by the object's edge count)
+// beyond that: the list has no length limit, as the
 // reference's pointer list has none.  Per row, exactly the reference's
 // operations (P3 included), as array operations:
 //   insertion (3654-3713)  each new edge goes before the first entry it sorts
@@ -704,7 +713,7 @@ __global__ void __launch_bounds__(64) k_obj_walk(FrameParams fp, const ObjDesc *
 //                          passes.  An odd last entry neither pairs nor steps.
 // ---------------------------------------------------------------------------
 constexpr int kWaveListArrays = 9;   // int32 arrays of cap + 2 entries each
-constexpr uint32_t kWaveListCapLds = 4096;
+constexpr uint32_t kSlotCapLds = 1024;  // walk_object_slots' largest LDS capacity (listed edges)
 struct WaveList {
     int32_t *idx;
     float *x, *g;
@@ -772,10 +781,9 @@ __device__ __forceinline__ bool key_gt(const LKey &a, const LKey &b) {
 // One new edge E[c] inserted as the reference does (3654-3713): before the
 // first entry it sorts before, else at the tail.
 template <bool GL>
-__device__ __forceinline__ void insert_one(const WaveList &L, int &m, const ObjEdge &C, int32_t c) {
+__device__ __forceinline__ void insert_one(const WaveList &L, int &m, float cx, float cg, int32_t cl, int32_t cy,
+                                           int32_t c) {
     const int lane = threadIdx.x & 63;
-    const float cx = C.X, cg = C.G;
-    const int32_t cl = C.Left, cy = C.YMax;
     int p = m;
     for (int c0 = 0; c0 < m; c0 += 64) {
         const int q = c0 + lane;
@@ -818,8 +826,11 @@ __device__ __forceinline__ void insert_one(const WaveList &L, int &m, const ObjE
 // #{new edges of gap <= q}.  O(m/64 + k/64) wave steps and a binary search per
 // new edge, instead of a list scan and a shift per new edge.
 template <bool GL>
-__device__ void insert_batch(const WaveList &L, int &m, const ObjEdge *__restrict__ E, uint32_t c0, int k) {
+__device__ void insert_batch(const WaveList &L, int &m, const ObjEdge *__restrict__ E, uint32_t c0, int k,
+                             float rx, float rg, int32_t rl, int32_t ry) {
+    // (k <= 64: new edge t = lane's key fields arrive in registers rx, rg, rl, ry)
     const int lane = threadIdx.x & 63;
+    const bool reg = k <= 64;
     // 1. aux[q] = position of a maximal key of entries [0, q]
     {
         LKey ck{-INFINITY, -INFINITY, INT32_MIN};
@@ -850,8 +861,7 @@ __device__ void insert_batch(const WaveList &L, int &m, const ObjEdge *__restric
     list_sync<GL>();
     // 2. nb[t] = gap of new edge t: a binary search over the non-decreasing PM
     for (int t = lane; t < k; t += 64) {
-        const ObjEdge &C = E[c0 + t];
-        const LKey kc{C.X, C.G, C.Left};
+        const LKey kc = reg ? LKey{rx, rg, rl} : LKey{E[c0 + t].X, E[c0 + t].G, E[c0 + t].Left};
         int lo = 0, hi = m;
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
@@ -890,8 +900,7 @@ __device__ void insert_batch(const WaveList &L, int &m, const ObjEdge *__restric
     // 6. final positions: gap + new edges of earlier gaps + those of its gap
     //    ordered before it (smaller key, or an equal key inserted earlier)
     for (int t = lane; t < k; t += 64) {
-        const ObjEdge &C = E[c0 + t];
-        const LKey kc{C.X, C.G, C.Left};
+        const LKey kc = reg ? LKey{rx, rg, rl} : LKey{E[c0 + t].X, E[c0 + t].G, E[c0 + t].Left};
         const int gq = L.nb[t];
         const int32_t s0 = L.aux[gq], h = L.aux[gq + 1] - s0;
         int32_t r = 0;
@@ -921,9 +930,13 @@ __device__ void insert_batch(const WaveList &L, int &m, const ObjEdge *__restric
     }
     // 8. the new edges into the free slots
     for (int t = lane; t < k; t += 64) {
-        const ObjEdge &C = E[c0 + t];
         const int32_t at = L.bk[t];
-        L.idx[at] = (int32_t)(c0 + t); L.x[at] = C.X; L.g[at] = C.G; L.left[at] = C.Left; L.ymax[at] = C.YMax;
+        if (reg) {
+            L.idx[at] = (int32_t)(c0 + t); L.x[at] = rx; L.g[at] = rg; L.left[at] = rl; L.ymax[at] = ry;
+        } else {
+            const ObjEdge &C = E[c0 + t];
+            L.idx[at] = (int32_t)(c0 + t); L.x[at] = C.X; L.g[at] = C.G; L.left[at] = C.Left; L.ymax[at] = C.YMax;
+        }
     }
     list_sync<GL>();
     m += k;
@@ -954,31 +967,46 @@ __device__ void walk_object_wave(const FrameParams &fp, const ObjDesc &od, const
     for (int32_t Row = FirstRow; Row < MaxY; ++Row) {
         // The row's new edges E[ins, ins + k): YMin == Row, contiguous in the
         // MergeSort order (entries below Row: none past the first row).
+        // One load per 64 edges: lane t of the first chunk keeps new edge
+        // ins + t's key fields for the insertion.
         int k = 0;
-        for (;;) {
-            const uint32_t i = ins + (uint32_t)lane;
-            const unsigned long long lt = __ballot(i < n && E[i].YMin < Row);
-            ins += (uint32_t)__popcll(lt);
-            if (lt != ~0ull) break;
-        }
         bool nan = false;
+        float rx = 0.0f, rg = 0.0f;
+        int32_t rl = 0, ry = 0;
         for (;;) {
             const uint32_t i = ins + (uint32_t)k + (uint32_t)lane;
-            bool eq = false;
+            int32_t y = INT32_MAX;
+            float x = 0.0f, g = 0.0f;
+            int32_t l = 0, ym = 0;
             if (i < n) {
                 const ObjEdge &C = E[i];
-                eq = C.YMin == Row;
-                nan |= eq && (C.X != C.X || C.G != C.G);
+                y = C.YMin; x = C.X; g = C.G; l = C.Left; ym = C.YMax;
             }
+            const unsigned long long lt = __ballot(y < Row);
+            if (lt) {  // (never past the first row of a sorted list: entries below the row are skipped)
+                ins += (uint32_t)__popcll(lt);
+                continue;
+            }
+            const bool eq = y == Row;
             const unsigned long long b = __ballot(eq);
+            if (k == 0) { rx = x; rg = g; rl = l; ry = ym; }
+            nan |= eq && (x != x || g != g);
             k += __popcll(b);
             if (b != ~0ull) break;
         }
         if (k > 0) {
             if (k <= 2 || __any(nan)) {  // insertion 3654-3713, one edge at a time in sorted order
-                for (int t = 0; t < k; ++t) insert_one<GL>(L, m, E[ins + t], (int32_t)(ins + t));
+                for (int t = 0; t < k; ++t) {
+                    if (t < 64) {
+                        insert_one<GL>(L, m, __shfl(rx, t), __shfl(rg, t), __shfl(rl, t), __shfl(ry, t),
+                                       (int32_t)(ins + t));
+                    } else {
+                        const ObjEdge &C = E[ins + t];
+                        insert_one<GL>(L, m, C.X, C.G, C.Left, C.YMax, (int32_t)(ins + t));
+                    }
+                }
             } else {
-                insert_batch<GL>(L, m, E, ins, k);
+                insert_batch<GL>(L, m, E, ins, k, rx, rg, rl, ry);
             }
             ins += (uint32_t)k;
         }
@@ -999,12 +1027,16 @@ __device__ void walk_object_wave(const FrameParams &fp, const ObjDesc &od, const
             }
             m = out;
         }
+        if (m == 0) {  // nothing happens on the rows before the next insertion: go there
+            if (ins >= n) break;
+            Row = max(Row, E[ins].YMin - 1);
+            continue;
+        }
         const int P = m / 2;  // pairing 3751-3869
         for (int k0 = 0; k0 < P; k0 += 64) {
             const int kk = k0 + lane;
             const bool valid = kk < P;
             bool em = false;
-            ObjEdge a, b;
             int32_t ia = 0, ib = 0;
             SpanPos sp;
             SpanRecG rec;
@@ -1012,8 +1044,9 @@ __device__ void walk_object_wave(const FrameParams &fp, const ObjDesc &od, const
             if (valid) {
                 ia = L.idx[2 * kk];
                 ib = L.idx[2 * kk + 1];
-                a = E[ia];
-                b = E[ib];
+            }
+            ObjEdge a = E[ia], b = E[ib];  // (edge 0 for lanes past the pairs: unused)
+            if (valid) {
                 if (Row >= RowLo) {
                     if constexpr (kScalar) em = obj_span_scalar<M>(fp, a, b, Row, d.tex, srec, sp);
                     else em = obj_span(fp, a, b, Row, d.tex, st, rec, sp);
@@ -1077,10 +1110,385 @@ __device__ void walk_object_wave(const FrameParams &fp, const ObjDesc &od, const
     }
 }
 
-// One wave per large object.  GL = false: the list in LDS (objects of at
-// most lcap edges); true: in the pool slice pool + big_off[blockIdx.x]
-// (kWaveListArrays arrays of big_cap[blockIdx.x] + 2 ints).
-template <bool GL>
+// ---------------------------------------------------------------------------
+// The same walk with everything in LDS (objects whose most active edges fit
+// the launch's capacity C): the list arrays, and the listed edges' mutable
+// state in C slots (a free-slot stack), so a row touches device memory only
+// for the sorted edges it inserts — read ahead 64 at a time into registers —
+// and the spans it writes.  Pairing keeps a chunk's entries in registers:
+// lane k holds pair k, does its first swap (3831-3841) itself and its second
+// (3843-3853) against lane k-1's second entry by a lane shift; the last pair
+// of a chunk hands its second entry to the next chunk's first lane.
+// ---------------------------------------------------------------------------
+struct SlotLds {
+    WaveList L;   // idx = the entry's slot
+    int32_t *fs;  // free slots: fs[0, top)
+    ObjEdge *st;  // edge state per slot
+    __device__ __forceinline__ void carve(int32_t *base, uint32_t cap) {
+        L.carve(base, cap);
+        fs = base + (size_t)kWaveListArrays * (cap + 2);
+        const size_t off = ((size_t)kWaveListArrays * (cap + 2) + cap) * 4;
+        st = reinterpret_cast<ObjEdge *>(reinterpret_cast<char *>(base) + ((off + 15) & ~(size_t)15));
+    }
+};
+__host__ __device__ constexpr size_t slot_lds_bytes(uint32_t cap) {
+    return ((((size_t)kWaveListArrays * (cap + 2) + cap) * 4 + 15) & ~(size_t)15) + (size_t)cap * sizeof(ObjEdge);
+}
+
+// insert_batch for k <= 64 new edges whose keys and slots lane t holds
+// (rx, rg, rl, ry, rs), the list in LDS.
+__device__ void insert_batch_regs(const WaveList &L, int &m, int k, float rx, float rg, int32_t rl, int32_t ry,
+                                  int32_t rs) {
+    const int lane = threadIdx.x & 63;
+    const bool mine = lane < k;
+    {  // 1. aux[q] = position of a maximal key of entries [0, q]
+        LKey ck{-INFINITY, -INFINITY, INT32_MIN};
+        int32_t cp = -1;
+        for (int b0 = 0; b0 < m; b0 += 64) {
+            const int q = b0 + lane;
+            LKey kk{-INFINITY, -INFINITY, INT32_MIN};
+            int32_t kp = q;
+            if (q < m) kk = entry_key(L.x[q], L.g[q], L.left[q]);
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                LKey ok;
+                ok.x = __shfl_up(kk.x, o);
+                ok.g = __shfl_up(kk.g, o);
+                ok.l = __shfl_up(kk.l, o);
+                const int32_t op = __shfl_up(kp, o);
+                if (lane >= o && key_gt(ok, kk)) { kk = ok; kp = op; }
+            }
+            if (cp >= 0 && key_gt(ck, kk)) { kk = ck; kp = cp; }
+            if (q < m) L.aux[q] = kp;
+            const int last = min(63, m - 1 - b0);
+            ck.x = __shfl(kk.x, last);
+            ck.g = __shfl(kk.g, last);
+            ck.l = __shfl(kk.l, last);
+            cp = __shfl(kp, last);
+        }
+    }
+    wave_lds_sync();
+    const LKey kc{rx, rg, rl};
+    int gq = 0;  // 2. the gap of new edge `lane`: binary search over the non-decreasing PM
+    if (mine) {
+        int lo = 0, hi = m;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            const int32_t pq = L.aux[mid];
+            if (key_gt(entry_key(L.x[pq], L.g[pq], L.left[pq]), kc)) hi = mid;
+            else lo = mid + 1;
+        }
+        gq = lo;
+    }
+    wave_lds_sync();
+    // 3. gap histogram, each new edge's arrival slot in its gap
+    for (int q = lane; q < m + 2; q += 64) L.aux[q] = 0;
+    wave_lds_sync();
+    int32_t arr = 0;
+    if (mine) arr = atomicAdd(&L.aux[gq], 1);
+    wave_lds_sync();
+    {  // 4. exclusive scan: aux[g] = new edges of gaps < g
+        int32_t carry = 0;
+        for (int b0 = 0; b0 < m + 2; b0 += 64) {
+            const int q = b0 + lane;
+            const int32_t v = q < m + 2 ? L.aux[q] : 0;
+            int32_t inc = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int32_t t = __shfl_up(inc, o);
+                if (lane >= o) inc += t;
+            }
+            if (q < m + 2) L.aux[q] = carry + inc - v;
+            carry += __shfl(inc, 63);
+        }
+    }
+    wave_lds_sync();
+    int32_t s0 = 0, h = 0;
+    if (mine) {  // 5. the new edges grouped by gap
+        s0 = L.aux[gq];
+        h = L.aux[gq + 1] - s0;
+        L.bk2[s0 + arr] = lane;
+    }
+    wave_lds_sync();
+    // 6. final positions: gap + new edges of earlier gaps + those of its gap
+    //    ordered before it (smaller key, or an equal key inserted earlier)
+    int32_t r = 0;
+    const int32_t hmax = wave_max_i32(h);
+    for (int32_t j = 0; j < hmax; ++j) {
+        const int32_t u = j < h ? L.bk2[s0 + j] : lane;
+        const LKey ku{__shfl(rx, u), __shfl(rg, u), __shfl(rl, u)};
+        if (j < h && u != lane) r += (key_gt(kc, ku) || (!key_gt(ku, kc) && u < lane)) ? 1 : 0;
+    }
+    const int32_t at = gq + s0 + r;
+    // 7. entries move up by the new edges of gaps <= their position, top chunk first
+    for (int top = m; top > 0; top -= 64) {
+        const int q = top - 1 - lane;
+        int32_t vi = 0, vl = 0, vy = 0, to = 0;
+        float vx = 0, vg = 0;
+        if (q >= 0) {
+            to = q + L.aux[q + 1];
+            vi = L.idx[q]; vx = L.x[q]; vg = L.g[q]; vl = L.left[q]; vy = L.ymax[q];
+        }
+        wave_lds_sync();
+        if (q >= 0 && to != q) { L.idx[to] = vi; L.x[to] = vx; L.g[to] = vg; L.left[to] = vl; L.ymax[to] = vy; }
+        wave_lds_sync();
+    }
+    if (mine) { L.idx[at] = rs; L.x[at] = rx; L.g[at] = rg; L.left[at] = rl; L.ymax[at] = ry; }  // 8.
+    wave_lds_sync();
+    m += k;
+}
+
+// Read-ahead window of sorted edges as seven dwordx4 (ObjEdge's layout: X, G
+// in q0.xy, YMin, YMax, Left in q4.xyz), named registers.
+#define PRK_WIN(w) float4 w##0, w##1, w##2, w##3, w##4, w##5, w##6
+#define PRK_WIN_LOAD(w, E, i, n)                                                      \
+    do {                                                                              \
+        const float4 *s_ = reinterpret_cast<const float4 *>((E) + min((i), (n) - 1)); \
+        w##0 = s_[0]; w##1 = s_[1]; w##2 = s_[2]; w##3 = s_[3];                       \
+        w##4 = s_[4]; w##5 = s_[5]; w##6 = s_[6];                                     \
+        if ((i) >= (n)) (w##4).x = __int_as_float(INT32_MAX);  /* past the end */     \
+    } while (0)
+#define PRK_WIN_COPY(d, w) \
+    do { d##0 = w##0; d##1 = w##1; d##2 = w##2; d##3 = w##3; d##4 = w##4; d##5 = w##5; d##6 = w##6; } while (0)
+#define PRK_WIN_STORE(dst, w)                                                          \
+    do {                                                                               \
+        float4 *d_ = reinterpret_cast<float4 *>(dst);                                  \
+        d_[0] = w##0; d_[1] = w##1; d_[2] = w##2; d_[3] = w##3;                        \
+        d_[4] = w##4; d_[5] = w##5; d_[6] = w##6;                                      \
+    } while (0)
+
+template <int M>
+__device__ void walk_object_slots(const FrameParams &fp, const ObjDesc &od, const DrawRec &d,
+                                  const ObjEdge *__restrict__ E, uint32_t n, int32_t MaxY, uint32_t base,
+                                  uint32_t bound, const SlotLds &S, uint32_t cap, SpanRecG *__restrict__ recs,
+                                  ScSpanRecG *__restrict__ srecs, SpanPos *__restrict__ pos,
+                                  uint32_t *__restrict__ span_tri, uint32_t *__restrict__ err) {
+    constexpr bool kScalar = M != MODE_AVX;
+    const int lane = threadIdx.x & 63;
+    const bool st = (d.flags & DRAW_ST) != 0;
+    const WaveList &L = S.L;
+    const int32_t RowLo = kScalar ? fp.row0 - 1 : fp.row0;
+    for (uint32_t q = lane; q < cap; q += 64) S.fs[q] = (int32_t)q;
+    int top = (int)cap;  // free slots
+    wave_lds_sync();
+    // read-ahead windows: lane t holds sorted edge wb + t (A) and wb + 64 + t (B)
+    uint32_t wb = 0;
+    PRK_WIN(wa);
+    PRK_WIN(wn);
+    PRK_WIN_LOAD(wa, E, (uint32_t)lane, n);
+    PRK_WIN_LOAD(wn, E, 64u + lane, n);
+    uint32_t emitted = 0;
+    int m = 0;
+    uint32_t ins = 0;
+    for (int32_t Row = E[0].YMin; Row < MaxY; ++Row) {
+        // insertion (3654-3713): the edges with YMin == Row, in sorted order,
+        // a window's worth at a time (batches in order == one at a time)
+        for (;;) {
+            if (ins == wb + 64) {
+                PRK_WIN_COPY(wa, wn);
+                wb += 64;
+                PRK_WIN_LOAD(wn, E, wb + 64 + lane, n);
+            }
+            const float wx = wa0.x, wg = wa0.y;
+            const int32_t wymin = __float_as_int(wa4.x), wymax = __float_as_int(wa4.y), wl = __float_as_int(wa4.z);
+            const int rel = lane - (int)(ins - wb);
+            const unsigned long long lt = __ballot(rel >= 0 && wymin < Row);
+            if (lt) {  // (never past the first row: entries below the row are skipped)
+                ins += (uint32_t)__popcll(lt);
+                continue;
+            }
+            const unsigned long long eq = __ballot(rel >= 0 && wymin == Row);
+            const int k = __popcll(eq);
+            if (k == 0) break;
+            const bool nw = rel >= 0 && rel < k;
+            int32_t slot = 0;
+            if (nw) {
+                slot = S.fs[top - 1 - rel];
+                PRK_WIN_STORE(&S.st[slot], wa);
+            }
+            const int src = min(63, (int)(ins - wb) + lane);
+            const float rx = __shfl(wx, src), rg = __shfl(wg, src);
+            const int32_t rl = __shfl(wl, src), ry = __shfl(wymax, src), rs = __shfl(slot, src);
+            const bool nan = __any(nw && (wx != wx || wg != wg));
+            top -= k;
+            if (k <= 2 || nan) {  // one at a time (any NaN key), 3654-3713
+                for (int t = 0; t < k; ++t)
+                    insert_one<false>(L, m, __shfl(rx, t), __shfl(rg, t), __shfl(rl, t), __shfl(ry, t),
+                                      __shfl(rs, t));
+            } else {
+                insert_batch_regs(L, m, k, rx, rg, rl, ry, rs);
+            }
+            ins += (uint32_t)k;
+            if (ins < wb + 64) break;  // the row's edges end inside the window
+        }
+        {  // expiry 3715-3749: keep entries with YMax > Row, in order; free the others' slots
+            int out = 0;
+            for (int c0 = 0; c0 < m; c0 += 64) {
+                const int q = c0 + lane;
+                int32_t vi = 0, vl = 0, vy = 0;
+                float vx = 0, vg = 0;
+                if (q < m) { vi = L.idx[q]; vx = L.x[q]; vg = L.g[q]; vl = L.left[q]; vy = L.ymax[q]; }
+                const bool keep = q < m && !(vy <= Row);
+                const bool gone = q < m && !keep;
+                const unsigned long long bal = __ballot(keep), gbal = __ballot(gone);
+                const int at = out + lane_rank(bal);
+                wave_lds_sync();
+                if (keep) { L.idx[at] = vi; L.x[at] = vx; L.g[at] = vg; L.left[at] = vl; L.ymax[at] = vy; }
+                if (gone) S.fs[top + lane_rank(gbal)] = vi;
+                wave_lds_sync();
+                out += __popcll(bal);
+                top += __popcll(gbal);
+            }
+            m = out;
+        }
+        if (m == 0) {  // nothing happens on the rows before the next insertion: go there
+            if (ins >= n) break;
+            const int32_t ny = ins < wb + 64 ? __shfl(__float_as_int(wa4.x), (int)(ins - wb))
+                                             : __shfl(__float_as_int(wn4.x), 0);
+            Row = max(Row, ny - 1);
+            continue;
+        }
+        const int P = m / 2;  // pairing 3751-3869
+        int32_t ci = 0, cl = 0, cy = 0;  // the previous chunk's last second entry (carried)
+        float cx = 0, cg = 0;
+        for (int k0 = 0; k0 < P; k0 += 64) {
+            const int kk = k0 + lane;
+            const bool valid = kk < P;
+            int32_t i0 = 0, i1 = 0, l0 = 0, l1 = 0, y0 = 0, y1 = 0;
+            float g0 = 0, g1 = 0;
+            bool em = false;
+            SpanPos sp;
+            SpanRecG rec;
+            ScSpanRecG srec;
+            if (valid) {
+                i0 = L.idx[2 * kk]; g0 = L.g[2 * kk]; l0 = L.left[2 * kk]; y0 = L.ymax[2 * kk];
+                i1 = L.idx[2 * kk + 1]; g1 = L.g[2 * kk + 1]; l1 = L.left[2 * kk + 1]; y1 = L.ymax[2 * kk + 1];
+            }
+            ObjEdge a = S.st[i0], b = S.st[i1];  // (slot 0 for lanes past the pairs: unused)
+            if (valid) {
+                if (Row >= RowLo) {
+                    if constexpr (kScalar) em = obj_span_scalar<M>(fp, a, b, Row, d.tex, srec, sp);
+                    else em = obj_span(fp, a, b, Row, d.tex, st, rec, sp);
+                }
+            }
+            const unsigned long long bal = __ballot(em);
+            if (em) {
+                const uint32_t j = emitted + (uint32_t)lane_rank(bal);
+                if (j < bound) {
+                    const uint32_t at = base + j;
+                    if constexpr (kScalar) {
+                        SpanRecG mark;
+                        mark.q0 = make_float4(__uint_as_float(kScalarSpan), 0.0f, 0.0f, 0.0f);
+                        mark.q1 = mark.q2 = mark.q3 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                        recs[at] = mark;
+                        srecs[at] = srec;
+                    } else {
+                        recs[at] = rec;
+                    }
+                    pos[at] = sp;
+                    span_tri[at] = od.g0;
+                } else {
+                    atomicOr(err, 2u);  // (never: the bound holds every span)
+                }
+            }
+            emitted += (uint32_t)__popcll(bal);
+            float x0 = 0, x1 = 0;
+            if (valid) {  // 3811-3829
+                obj_step<M>(a);
+                obj_step<M>(b);
+                S.st[i0] = a;
+                S.st[i1] = b;
+                x0 = a.X;
+                x1 = b.X;
+                if (x0 > x1) {  // 3831-3841
+                    int32_t t;
+                    float f;
+                    t = i0; i0 = i1; i1 = t;
+                    f = x0; x0 = x1; x1 = f;
+                    f = g0; g0 = g1; g1 = f;
+                    t = l0; l0 = l1; l1 = t;
+                    t = y0; y0 = y1; y1 = t;
+                }
+            }
+            // 3843-3853: pair kk's first entry against pair kk-1's second
+            int32_t pi = __shfl_up(i1, 1), pl = __shfl_up(l1, 1), py = __shfl_up(y1, 1);
+            float px = __shfl_up(x1, 1), pg = __shfl_up(g1, 1);
+            if (lane == 0) { pi = ci; px = cx; pg = cg; pl = cl; py = cy; }
+            const bool sw = valid && kk >= 1 && px > x0;
+            const bool swn = __shfl_down(sw ? 1 : 0, 1) != 0 && lane < 63;  // the next pair's swap takes my second
+            int32_t ni = __shfl_down(i0, 1), nl = __shfl_down(l0, 1), ny = __shfl_down(y0, 1);
+            float nx = __shfl_down(x0, 1), ng = __shfl_down(g0, 1);
+            const bool defer = lane == 63 && kk + 1 < P;  // my second waits for the next chunk
+            if (valid) {
+                const int q0 = 2 * kk, q1 = 2 * kk + 1;
+                if (sw) {  // entry q0 - 1 = my first, entry q0 = the previous second
+                    if (lane == 0) {
+                        L.idx[q0 - 1] = i0; L.x[q0 - 1] = x0; L.g[q0 - 1] = g0; L.left[q0 - 1] = l0;
+                        L.ymax[q0 - 1] = y0;
+                    }
+                    L.idx[q0] = pi; L.x[q0] = px; L.g[q0] = pg; L.left[q0] = pl; L.ymax[q0] = py;
+                } else {
+                    if (lane == 0 && kk >= 1) {
+                        L.idx[q0 - 1] = pi; L.x[q0 - 1] = px; L.g[q0 - 1] = pg; L.left[q0 - 1] = pl;
+                        L.ymax[q0 - 1] = py;
+                    }
+                    L.idx[q0] = i0; L.x[q0] = x0; L.g[q0] = g0; L.left[q0] = l0; L.ymax[q0] = y0;
+                }
+                if (!defer) {
+                    if (swn) { L.idx[q1] = ni; L.x[q1] = nx; L.g[q1] = ng; L.left[q1] = nl; L.ymax[q1] = ny; }
+                    else { L.idx[q1] = i1; L.x[q1] = x1; L.g[q1] = g1; L.left[q1] = l1; L.ymax[q1] = y1; }
+                }
+            }
+            ci = __shfl(i1, 63); cx = __shfl(x1, 63); cg = __shfl(g1, 63); cl = __shfl(l1, 63); cy = __shfl(y1, 63);
+        }
+        wave_lds_sync();
+    }
+}
+
+// The most entries the object's list holds at once (after a row's
+// insertion, before its expiry): an edge inserted at row YMin leaves at the
+// first row r >= YMin with YMax <= r, so it is in the list on the rows
+// [YMin, max(YMin, YMax)] of [FirstRow, MaxY).  A difference histogram over
+// those rows in h (`ints` ints, rows beyond: INT32_MAX, i.e. "unknown").
+__device__ int32_t obj_max_active(const ObjEdge *__restrict__ E, uint32_t n, int32_t FirstRow, int32_t MaxY,
+                                  int32_t *h, uint32_t ints) {
+    const int lane = threadIdx.x & 63;
+    const int64_t rows = (int64_t)MaxY - FirstRow;
+    if (rows <= 0) return 0;
+    if (rows + 1 > (int64_t)ints) return INT32_MAX;
+    const int R = (int)rows;
+    for (int q = lane; q <= R; q += 64) h[q] = 0;
+    wave_lds_sync();
+    for (uint32_t i = lane; i < n; i += 64) {
+        const int32_t y0 = E[i].YMin, y1 = E[i].YMax;
+        if (y0 >= MaxY) continue;  // never inserted
+        const int32_t lo = y0 - FirstRow, hi = min(max(y0, y1), MaxY - 1) - FirstRow;
+        atomicAdd(&h[max(lo, 0)], 1);
+        atomicAdd(&h[hi + 1], -1);
+    }
+    wave_lds_sync();
+    int32_t carry = 0, best = 0;
+    for (int b0 = 0; b0 < R; b0 += 64) {
+        const int q = b0 + lane;
+        int32_t v = q < R ? h[q] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t t = __shfl_up(v, o);
+            if (lane >= o) v += t;
+        }
+        v += carry;
+        best = max(best, wave_max_i32(q < R ? v : 0));
+        carry = __shfl(v, 63);
+    }
+    wave_lds_sync();  // (h is the list's storage next)
+    return best;
+}
+
+// One wave per large object: everything in LDS (walk_object_slots, lcap
+// slots) when its most active entries fit, else its list in its pool slice pool + big_off[blockIdx.x]
+// (kWaveListArrays arrays of big_cap[blockIdx.x] + 2 ints, big_cap >= its
+// edge count).
+template <int M>
 __global__ void __launch_bounds__(64) k_obj_walk_wave(FrameParams fp, const ObjDesc *__restrict__ objs,
                                                       const uint32_t *__restrict__ big,
                                                       const unsigned long long *__restrict__ big_off,
@@ -1092,32 +1500,31 @@ __global__ void __launch_bounds__(64) k_obj_walk_wave(FrameParams fp, const ObjD
                                                       SpanPos *__restrict__ pos, uint32_t *__restrict__ span_tri,
                                                       uint32_t *__restrict__ err) {
     extern __shared__ int32_t lds_list[];
-    WaveList L;
-    if (GL) L.carve(pool + big_off[blockIdx.x], big_cap[blockIdx.x]);
-    else L.carve(lds_list, lcap);
     const uint32_t o = big[blockIdx.x];
     const ObjDesc od = objs[o];
     const DrawRec &d = fp.draws[od.draw];
     const uint32_t base = (uint32_t)soff[o], bound = (uint32_t)(soff[o + 1] - soff[o]);
     uint32_t e0, n;
     obj_range(od, escan, *total0p, e0, n);
-    if (!GL && n > lcap) {  // (the host sends only objects of at most lcap edges here)
+    ObjEdge *E = work + e0;
+    if (n == 0) return;
+    int32_t mr = INT32_MIN;
+    for (uint32_t i = threadIdx.x; i < n; i += 64) mr = max(mr, E[i].YMax);
+    const int32_t MaxY = min(min(wave_max_i32(mr), fp.H), fp.row1);
+    const int32_t most = obj_max_active(E, n, E[0].YMin, MaxY, lds_list, (uint32_t)(slot_lds_bytes(lcap) / 4));
+    const bool gl = most > (int32_t)lcap;
+    if (gl && n > big_cap[blockIdx.x]) {  // (the host sizes every slice by the object's edges)
         if (threadIdx.x == 0) atomicOr(err, 1u);
         return;
     }
-    ObjEdge *E = work + e0;
-    switch (d.mode) {
-#define PRK_WALK_OBJ(MM)                                                                                  \
-    case MM:                                                                                              \
-        walk_object_wave<MM, GL>(fp, od, d, E, n, base, bound, L, recs, srecs, pos, span_tri, err);      \
-        break;
-        PRK_WALK_OBJ(MODE_AVX)
-        PRK_WALK_OBJ(MODE_SC_GOURAUD)
-        PRK_WALK_OBJ(MODE_SC_GOURAUD_TEX)
-        PRK_WALK_OBJ(MODE_SC_PHONG)
-        PRK_WALK_OBJ(MODE_SC_PHONG_TEX)
-#undef PRK_WALK_OBJ
-        default: break;
+    if (gl) {
+        WaveList L;
+        L.carve(pool + big_off[blockIdx.x], big_cap[blockIdx.x]);
+        walk_object_wave<M, true>(fp, od, d, E, n, base, bound, L, recs, srecs, pos, span_tri, err);
+    } else {
+        SlotLds S;
+        S.carve(lds_list, lcap);
+        walk_object_slots<M>(fp, od, d, E, n, MaxY, base, bound, S, lcap, recs, srecs, pos, span_tri, err);
     }
 }
 
@@ -1243,9 +1650,9 @@ hipError_t prk_obj_bound(const prk::FrameParams *fp, const void *objs, uint32_t 
                        reinterpret_cast<const prk::EdgeIn *>(edges_in), bound);
     return hipGetLastError();
 }
-// The LDS list capacity of the one-wave walk on the current device (edges;
-// 0: every wave walk keeps its list in device memory): the largest of 4096,
-// 2048, 1024 whose kWaveListArrays arrays the device grants as dynamic LDS.
+// The LDS capacity of the one-wave walk on the current device (listed edges;
+// 0: every wave walk keeps its list in device memory): the largest of 1024,
+// 512, 256 whose slot_lds_bytes the device grants as dynamic LDS.
 uint32_t prk_obj_walk_lcap(void) {
     static std::atomic<int> cap[64];  // per device: 0 unknown, else cap + 1
     int dev = -1;
@@ -1253,10 +1660,18 @@ uint32_t prk_obj_walk_lcap(void) {
     int c = cap[dev].load();
     if (c == 0) {
         c = 1;
-        for (uint32_t k = prk::kWaveListCapLds; k >= 1024; k /= 2) {
-            const size_t bytes = (size_t)prk::kWaveListArrays * (k + 2) * 4;
-            if (hipFuncSetAttribute(reinterpret_cast<const void *>(&prk::k_obj_walk_wave<false>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) == hipSuccess) {
+        for (uint32_t k = prk::kSlotCapLds; k >= 256; k /= 2) {
+            const size_t bytes = prk::slot_lds_bytes(k);
+            const void *fn[prk::MODE_COUNT] = {
+                reinterpret_cast<const void *>(&prk::k_obj_walk_wave<prk::MODE_AVX>),
+                reinterpret_cast<const void *>(&prk::k_obj_walk_wave<prk::MODE_SC_GOURAUD>),
+                reinterpret_cast<const void *>(&prk::k_obj_walk_wave<prk::MODE_SC_GOURAUD_TEX>),
+                reinterpret_cast<const void *>(&prk::k_obj_walk_wave<prk::MODE_SC_PHONG>),
+                reinterpret_cast<const void *>(&prk::k_obj_walk_wave<prk::MODE_SC_PHONG_TEX>)};
+            bool ok = true;
+            for (int mo = 0; mo < prk::MODE_COUNT && ok; ++mo)
+                ok = hipFuncSetAttribute(fn[mo], hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) == hipSuccess;
+            if (ok) {
                 c = (int)k + 1;
                 break;
             }
@@ -1267,15 +1682,17 @@ uint32_t prk_obj_walk_lcap(void) {
     return (uint32_t)(c - 1);
 }
 // The object walk, one pass: a thread per object, a wave per object of
-// big_lds[0..nlds) (list in LDS, lcap) and of big_gl[0..ngl) (list in the
-// pool at big_off, big_cap edges).  Spans go to slots soff[o] + k.  err: bit
-// 0 an LDS walk got an object above lcap, bit 1 an object emitted past its
-// bound (neither can happen).
-hipError_t prk_obj_walk(const prk::FrameParams *fp, const void *objs, uint32_t nobj, const uint32_t *big_lds,
-                        uint32_t nlds, uint32_t lcap, const uint32_t *big_gl, const unsigned long long *big_off,
-                        const uint32_t *big_cap, uint32_t ngl, int32_t *pool, const uint32_t *escan,
-                        const uint32_t *total0p, void *work, const unsigned long long *soff, void *recs, void *srecs,
-                        void *pos, uint32_t *span_tri, const void *spans_in, uint32_t *err, hipStream_t s) {
+// big[] (grouped by mode, nbig[mode] each: one launch per mode; in LDS of
+// lcap slots, lcap <= prk_obj_walk_lcap(), when its
+// most active entries fit, else its list in the pool at big_off, big_cap
+// edges).  Spans go to slots soff[o] + k.  err: bit 0 a pool slice smaller
+// than its object, bit 1 an object emitted past its bound (neither can
+// happen).
+hipError_t prk_obj_walk(const prk::FrameParams *fp, const void *objs, uint32_t nobj, const uint32_t *big,
+                        const uint32_t *nbig, uint32_t lcap, const unsigned long long *big_off, const uint32_t *big_cap,
+                        int32_t *pool, const uint32_t *escan, const uint32_t *total0p, void *work,
+                        const unsigned long long *soff, void *recs, void *srecs, void *pos, uint32_t *span_tri,
+                        const void *spans_in, uint32_t *err, hipStream_t s) {
     if (nobj == 0) return hipSuccess;
     hipLaunchKernelGGL(prk::k_obj_walk, dim3((nobj + 63) / 64), dim3(64), 0, s, *fp,
                        reinterpret_cast<const prk::ObjDesc *>(objs), nobj, escan, total0p,
@@ -1283,24 +1700,30 @@ hipError_t prk_obj_walk(const prk::FrameParams *fp, const void *objs, uint32_t n
                        reinterpret_cast<prk::ScSpanRecG *>(srecs), reinterpret_cast<prk::SpanPos *>(pos), span_tri,
                        reinterpret_cast<const prk::SpanIn *>(spans_in), err);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    if (nlds) {
-        const size_t bytes = (size_t)prk::kWaveListArrays * (lcap + 2) * 4;
-        hipLaunchKernelGGL(prk::k_obj_walk_wave<false>, dim3(nlds), dim3(64), bytes, s, *fp,
-                           reinterpret_cast<const prk::ObjDesc *>(objs), big_lds, nullptr, nullptr, nullptr, lcap,
-                           escan, total0p, reinterpret_cast<prk::ObjEdge *>(work), soff,
-                           reinterpret_cast<prk::SpanRecG *>(recs), reinterpret_cast<prk::ScSpanRecG *>(srecs),
-                           reinterpret_cast<prk::SpanPos *>(pos), span_tri, err);
+    const size_t bytes = prk::slot_lds_bytes(lcap);
+    uint32_t b0 = 0;
+    for (int mo = 0; mo < prk::MODE_COUNT && e == hipSuccess; ++mo) {
+        const uint32_t nb = nbig[mo];
+        if (nb == 0) continue;
+#define PRK_WALK_WAVE(MM)                                                                                           \
+    case MM:                                                                                                        \
+        hipLaunchKernelGGL(prk::k_obj_walk_wave<MM>, dim3(nb), dim3(64), bytes, s, *fp,                            \
+                           reinterpret_cast<const prk::ObjDesc *>(objs), big + b0, big_off + b0, big_cap + b0, pool, \
+                           lcap, escan, total0p, reinterpret_cast<prk::ObjEdge *>(work), soff,                      \
+                           reinterpret_cast<prk::SpanRecG *>(recs), reinterpret_cast<prk::ScSpanRecG *>(srecs),     \
+                           reinterpret_cast<prk::SpanPos *>(pos), span_tri, err);                                   \
+        break;
+        switch (mo) {
+            PRK_WALK_WAVE(prk::MODE_AVX)
+            PRK_WALK_WAVE(prk::MODE_SC_GOURAUD)
+            PRK_WALK_WAVE(prk::MODE_SC_GOURAUD_TEX)
+            PRK_WALK_WAVE(prk::MODE_SC_PHONG)
+            PRK_WALK_WAVE(prk::MODE_SC_PHONG_TEX)
+            default: break;
+        }
+#undef PRK_WALK_WAVE
         e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    if (ngl) {
-        hipLaunchKernelGGL(prk::k_obj_walk_wave<true>, dim3(ngl), dim3(64), 0, s, *fp,
-                           reinterpret_cast<const prk::ObjDesc *>(objs), big_gl, big_off, big_cap, pool, 0u, escan,
-                           total0p, reinterpret_cast<prk::ObjEdge *>(work), soff,
-                           reinterpret_cast<prk::SpanRecG *>(recs), reinterpret_cast<prk::ScSpanRecG *>(srecs),
-                           reinterpret_cast<prk::SpanPos *>(pos), span_tri, err);
-        e = hipGetLastError();
+        b0 += nb;
     }
     return e;
 }

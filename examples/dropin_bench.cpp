@@ -160,7 +160,39 @@ int main(int argc, char **argv) {
         prk_synchronize(prk_dropin::S().Ctx);
         prk_dropin::end_frame(prk_dropin::S());
     }
-    std::printf("}, \"fill_edge_table_only_ms\": %.3f, \"frames\": %d}\n", fill / frames, frames);
+    // ... and its parts: the visible-edge count (the call's return value) and
+    // the vertex snapshot into pinned memory, each alone.
+    double count = 0, copy = 0;
+    {
+        const prk_dropin::camera cam = prk_dropin::camera_of(&Commands);
+        const float P[3] = {0.0f, 0.0f, 0.0f};
+        float *a[4] = {nullptr, nullptr, nullptr, nullptr};
+        const size_t comp[4] = {3, 4, 3, 2};
+        for (int k = 0; k < 4; ++k) prk_host_alloc(prk_dropin::S().Ctx, 3 * (size_t)T * comp[k] * 4, (void **)&a[k]);
+        uint64_t sink = 0;
+        for (int f = 0; f < frames + 1; ++f) {
+            auto t1 = clk::now();
+            for (u32 t = 0; t < T; ++t) {
+                u32 e = 0;
+                prk_fill_edge_count((const float *)&V[3 * (size_t)t], 3, P, &cam.T, &e);
+                sink += e;
+            }
+            if (f > 0) count += ms_since(t1);
+            t1 = clk::now();
+            if (a[0] && a[1] && a[2] && a[3])
+                for (u32 t = 0; t < T; ++t) {
+                    memcpy(a[0] + 9 * (size_t)t, &V[3 * (size_t)t], 36);
+                    memcpy(a[1] + 12 * (size_t)t, &C[3 * (size_t)t], 48);
+                    memcpy(a[2] + 9 * (size_t)t, &N[3 * (size_t)t], 36);
+                    memcpy(a[3] + 6 * (size_t)t, &UV[3 * (size_t)t], 24);
+                }
+            if (f > 0) copy += ms_since(t1);
+        }
+        for (int k = 0; k < 4; ++k) prk_host_free(prk_dropin::S().Ctx, a[k]);
+        if (sink == 1) std::printf(" ");
+    }
+    std::printf("}, \"fill_edge_table_only_ms\": %.3f, \"edge_count_only_ms\": %.3f, \"snapshot_copy_only_ms\": %.3f, "
+                "\"frames\": %d}\n", fill / frames, count / frames, copy / frames, frames);
     PRK_Shutdown();
     return 0;
 }

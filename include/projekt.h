@@ -773,13 +773,20 @@ inline u32 FillEdgeTable(render_entry_3d_object *Object, game_render_commands *C
     if (edges) {  // an object with no visible edge draws nothing: nothing to upload
         if (!prk_dropin::arena_reserve(st, nv)) return 0;
         const uint32_t v0 = st.ArenaUsed;
-        memcpy(st.AV + 3 * (size_t)v0, Object->VertexData, (size_t)nv * 12);
-        if (Object->ColorData) memcpy(st.AC + 4 * (size_t)v0, Object->ColorData, (size_t)nv * 16);
-        else memset(st.AC + 4 * (size_t)v0, 0, (size_t)nv * 16);
-        if (Object->NormalData) memcpy(st.AN + 3 * (size_t)v0, Object->NormalData, (size_t)nv * 12);
-        else memset(st.AN + 3 * (size_t)v0, 0, (size_t)nv * 12);
-        if (Object->UVData) memcpy(st.AUV + 2 * (size_t)v0, Object->UVData, (size_t)nv * 8);
-        else memset(st.AUV + 2 * (size_t)v0, 0, (size_t)nv * 8);
+        if (nv == 3 && Object->ColorData && Object->NormalData && Object->UVData) {  // one triangle: fixed-size copies
+            memcpy(st.AV + 3 * (size_t)v0, Object->VertexData, 36);
+            memcpy(st.AC + 4 * (size_t)v0, Object->ColorData, 48);
+            memcpy(st.AN + 3 * (size_t)v0, Object->NormalData, 36);
+            memcpy(st.AUV + 2 * (size_t)v0, Object->UVData, 24);
+        } else {
+            memcpy(st.AV + 3 * (size_t)v0, Object->VertexData, (size_t)nv * 12);
+            if (Object->ColorData) memcpy(st.AC + 4 * (size_t)v0, Object->ColorData, (size_t)nv * 16);
+            else memset(st.AC + 4 * (size_t)v0, 0, (size_t)nv * 16);
+            if (Object->NormalData) memcpy(st.AN + 3 * (size_t)v0, Object->NormalData, (size_t)nv * 12);
+            else memset(st.AN + 3 * (size_t)v0, 0, (size_t)nv * 12);
+            if (Object->UVData) memcpy(st.AUV + 2 * (size_t)v0, Object->UVData, (size_t)nv * 8);
+            else memset(st.AUV + 2 * (size_t)v0, 0, (size_t)nv * 8);
+        }
         st.ArenaUsed += nv;
         o.FirstTri = v0 / 3;
         o.Tris = T;
