@@ -56,8 +56,9 @@ hipError_t prk_obj_bound(const prk::FrameParams *, const void *, uint32_t, const
 uint32_t prk_obj_walk_lcap(void);
 hipError_t prk_obj_walk(const prk::FrameParams *, const void *, uint32_t, const uint32_t *, const uint32_t *, uint32_t,
                         const unsigned long long *, const uint32_t *, int32_t *, const uint32_t *, const uint32_t *,
-                        void *, const unsigned long long *, void *, void *, void *, uint32_t *, const void *,
-                        uint32_t *, hipStream_t);
+                        void *, const unsigned long long *, void *, void *, void *, void *, uint32_t *,
+                        const void *, uint32_t *, hipStream_t);
+hipError_t prk_span_finish(const prk::FrameParams *, const void *, uint32_t, void *, void *, void *, hipStream_t);
 hipError_t prk_scan_u32(const uint32_t *, uint32_t *, uint32_t, void *, size_t *, hipStream_t);
 hipError_t prk_scan_u64(const unsigned long long *, unsigned long long *, uint32_t, void *, size_t *, hipStream_t);
 hipError_t prk_span_count(const prk::FrameParams *, const void *, uint32_t, uint32_t *, hipStream_t);
@@ -248,10 +249,15 @@ struct prk_context {
     } pcount;
     // Span path (whole-object AETs) scratch, reused frame to frame.
     struct SpanScratch {
-        DevBuf d_draws, d_texs, d_objs, d_edges, d_ord, d_temp, d_recs, d_pos, d_span_tri, d_scnt, d_soff, d_keys_a,
-            d_vals_a, d_keys_b, d_vals_b, d_offs, d_nwin, d_wtag, d_edges_in, d_spans_in, d_srecs, d_work, d_ekeys,
-            d_ekeys2, d_evals, d_ecnt, d_escan, d_rcnt, d_rscan, d_bound, d_oslot, d_k0obj, d_k0tri0,
-            d_big_gl, d_big_off, d_big_cap, d_pool, d_k1src, d_err;
+        DevBuf d_stage, d_edges, d_ord, d_temp, d_recs, d_pos, d_span_tri, d_scnt, d_soff, d_keys_a, d_vals_a,
+            d_keys_b, d_vals_b, d_offs, d_nwin, d_wtag, d_srecs, d_work, d_ekeys, d_ekeys2, d_evals, d_ecnt, d_escan,
+            d_rcnt, d_rscan, d_bound, d_oslot, d_pool, d_err, d_raw;
+        // the pass's host tables, packed into pinned memory for one upload
+        // (stage_ev: that upload, before the staging is rewritten)
+        char *h_stage = nullptr;
+        size_t stage_cap = 0;
+        hipEvent_t stage_ev = nullptr;
+        bool stage_busy = false;
         // host tables of the pass, kept until their asynchronous uploads ran
         std::vector<ObjDesc> h_objs;
         std::vector<uint32_t> h_k0obj, h_k0tri0, h_big_gl, h_big_cap, h_k1src;
@@ -384,14 +390,18 @@ int prk_destroy(prk_context *c) {
     for (DevBuf *b : bufs) b->release();
     {
         auto &S = c->spans;
-        DevBuf *sb[] = {&S.d_draws, &S.d_texs, &S.d_objs, &S.d_edges, &S.d_ord, &S.d_temp, &S.d_recs, &S.d_pos,
-                        &S.d_span_tri, &S.d_scnt, &S.d_soff, &S.d_keys_a, &S.d_vals_a, &S.d_keys_b, &S.d_vals_b,
-                        &S.d_offs, &S.d_nwin, &S.d_wtag, &S.d_edges_in, &S.d_spans_in, &S.d_srecs, &S.d_work,
-                        &S.d_ekeys, &S.d_ekeys2, &S.d_evals, &S.d_ecnt, &S.d_escan, &S.d_rcnt, &S.d_rscan,
-                        &S.d_bound, &S.d_oslot, &S.d_k0obj, &S.d_k0tri0, &S.d_big_gl, &S.d_big_off,
-                        &S.d_big_cap, &S.d_pool, &S.d_k1src, &S.d_err};
+        DevBuf *sb[] = {&S.d_stage, &S.d_edges, &S.d_ord, &S.d_temp, &S.d_recs, &S.d_pos, &S.d_span_tri, &S.d_scnt,
+                        &S.d_soff, &S.d_keys_a, &S.d_vals_a, &S.d_keys_b, &S.d_vals_b, &S.d_offs, &S.d_nwin,
+                        &S.d_wtag, &S.d_srecs, &S.d_work, &S.d_ekeys, &S.d_ekeys2, &S.d_evals, &S.d_ecnt,
+                        &S.d_escan, &S.d_rcnt, &S.d_rscan, &S.d_bound, &S.d_oslot, &S.d_pool, &S.d_err,
+                        &S.d_raw};
         for (DevBuf *b : sb) b->release();
         if (S.h_rb) (void)hipHostFree(S.h_rb);
+        if (S.stage_ev) {
+            if (S.stage_busy) (void)hipEventSynchronize(S.stage_ev);
+            (void)hipEventDestroy(S.stage_ev);
+        }
+        if (S.h_stage) (void)hipHostFree(S.h_stage);
     }
     if (c->s_mark) (void)hipEventDestroy(c->s_mark);
     if (c->in_ev) (void)hipEventDestroy(c->in_ev);
@@ -1498,27 +1508,59 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
         S.h_texs[i] = prk::TexRec{c->texs[i].mem, c->texs[i].w, c->texs[i].h, c->texs[i].pitch, c->texs[i].filter};
     S.h_draws = draws;
     // (the scratch below is reused frame to frame: stream order on s covers it)
-    auto up = [&](DevBuf &d, const void *src, size_t bytes) -> hipError_t {
-        hipError_t e = d.ensure(std::max<size_t>(bytes, 16));
-        if (e == hipSuccess && bytes) e = hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, s);
-        return e;
-    };
-    PRK_TRY(up(S.d_draws, S.h_draws.data(), S.h_draws.size() * sizeof(prk::DrawRec)));
-    PRK_TRY(up(S.d_texs, S.h_texs.data(), S.h_texs.size() * sizeof(prk::TexRec)));
-    fp.draws = (const prk::DrawRec *)S.d_draws.p;
-    fp.texs = (const prk::TexRec *)S.d_texs.p;
+    // The pass's host tables go up in one copy from pinned staging (a pageable
+    // hipMemcpyAsync per table held the host for each).
+    enum { T_DRAWS, T_TEXS, T_OBJS, T_K0OBJ, T_K0TRI0, T_BIG, T_BIG_OFF, T_BIG_CAP, T_K1SRC, T_EDGES, T_SPANS, T_N };
+    struct Part {
+        const void *src;
+        size_t bytes, off;
+    } parts[T_N] = {{S.h_draws.data(), S.h_draws.size() * sizeof(prk::DrawRec), 0},
+                    {S.h_texs.data(), S.h_texs.size() * sizeof(prk::TexRec), 0},
+                    {S.h_objs.data(), S.h_objs.size() * sizeof(ObjDesc), 0},
+                    {S.h_k0obj.data(), S.h_k0obj.size() * 4, 0},
+                    {S.h_k0tri0.data(), S.h_k0tri0.size() * 4, 0},
+                    {S.h_big_gl.data(), S.h_big_gl.size() * 4, 0},
+                    {S.h_big_off.data(), S.h_big_off.size() * 8, 0},
+                    {S.h_big_cap.data(), S.h_big_cap.size() * 4, 0},
+                    {S.h_k1src.data(), S.h_k1src.size() * 4, 0},
+                    {c->pend_edges.data(), c->pend_edges.size() * sizeof(prk_edge), 0},
+                    {c->pend_spans.data(), c->pend_spans.size() * sizeof(prk_span), 0}};
+    size_t stage_bytes = 0;
+    for (Part &pt : parts) {
+        pt.off = stage_bytes;
+        stage_bytes = (stage_bytes + pt.bytes + 255) & ~(size_t)255;
+    }
+    stage_bytes = std::max<size_t>(stage_bytes, 256);
+    if (!S.stage_ev) PRK_TRY(hipEventCreateWithFlags(&S.stage_ev, hipEventDisableTiming));
+    if (S.stage_busy) {  // the previous pass's upload still reads the staging
+        PRK_TRY(hipEventSynchronize(S.stage_ev));
+        S.stage_busy = false;
+    }
+    if (stage_bytes > S.stage_cap) {
+        if (S.h_stage) (void)hipHostFree(S.h_stage);
+        S.h_stage = nullptr;
+        S.stage_cap = 0;
+        const size_t want = stage_bytes + stage_bytes / 4;
+        PRK_TRY(hipHostMalloc((void **)&S.h_stage, want, hipHostMallocDefault));
+        S.stage_cap = want;
+    }
+    for (const Part &pt : parts)
+        if (pt.bytes) std::memcpy(S.h_stage + pt.off, pt.src, pt.bytes);
+    PRK_TRY(S.d_stage.ensure(stage_bytes));
+    PRK_TRY(hipMemcpyAsync(S.d_stage.p, S.h_stage, stage_bytes, hipMemcpyHostToDevice, s));
+    PRK_TRY(hipEventRecord(S.stage_ev, s));
+    S.stage_busy = true;
+    auto dev = [&](int t) -> void * { return static_cast<char *>(S.d_stage.p) + parts[t].off; };
+    fp.draws = (const prk::DrawRec *)dev(T_DRAWS);
+    fp.texs = (const prk::TexRec *)dev(T_TEXS);
     fp.draw0 = draws[0];
     fp.tex0 = prk::TexRec{};
     if (fp.draw0.tex >= 0 && (size_t)fp.draw0.tex < S.h_texs.size()) fp.tex0 = S.h_texs[fp.draw0.tex];
-    PRK_TRY(up(S.d_objs, S.h_objs.data(), S.h_objs.size() * sizeof(ObjDesc)));
-    PRK_TRY(up(S.d_k0obj, S.h_k0obj.data(), S.h_k0obj.size() * 4));
-    PRK_TRY(up(S.d_k0tri0, S.h_k0tri0.data(), S.h_k0tri0.size() * 4));
-    PRK_TRY(up(S.d_big_gl, S.h_big_gl.data(), S.h_big_gl.size() * 4));
-    PRK_TRY(up(S.d_big_off, S.h_big_off.data(), S.h_big_off.size() * 8));
-    PRK_TRY(up(S.d_big_cap, S.h_big_cap.data(), S.h_big_cap.size() * 4));
-    PRK_TRY(up(S.d_k1src, S.h_k1src.data(), S.h_k1src.size() * 4));
-    PRK_TRY(up(S.d_edges_in, c->pend_edges.data(), c->pend_edges.size() * sizeof(prk_edge)));
-    PRK_TRY(up(S.d_spans_in, c->pend_spans.data(), c->pend_spans.size() * sizeof(prk_span)));
+    void *d_objs = dev(T_OBJS), *d_edges_in = dev(T_EDGES), *d_spans_in = dev(T_SPANS);
+    const uint32_t *d_k0obj = (const uint32_t *)dev(T_K0OBJ), *d_k0tri0 = (const uint32_t *)dev(T_K0TRI0);
+    const uint32_t *d_big = (const uint32_t *)dev(T_BIG), *d_big_cap = (const uint32_t *)dev(T_BIG_CAP);
+    const uint32_t *d_k1src = (const uint32_t *)dev(T_K1SRC);
+    const unsigned long long *d_big_off = (const unsigned long long *)dev(T_BIG_OFF);
     if (ngl) PRK_TRY(S.d_pool.ensure(pool * 4));
     uint32_t modes = 0;  // the pass's span kinds: bit per Mode
     for (const auto &d : draws) modes |= 1u << d.mode;
@@ -1541,7 +1583,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     size_t tb = 0;
     auto temp = [&](size_t b) -> hipError_t { return S.d_temp.ensure(std::max<size_t>(b, 16)); };
     if (nt) {
-        PRK_TRY(prk_objtri_count(&fp, S.d_objs.p, (const uint32_t *)S.d_k0obj.p, (const uint32_t *)S.d_k0tri0.p, nk0,
+        PRK_TRY(prk_objtri_count(&fp, d_objs, d_k0obj, d_k0tri0, nk0,
                                  nt, (uint32_t *)S.d_ecnt.p, (unsigned long long *)S.d_rcnt.p, s));
     } else {
         PRK_TRY(hipMemsetAsync(S.d_ecnt.p, 0, 4, s));
@@ -1553,7 +1595,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(prk_scan_u64((const unsigned long long *)S.d_rcnt.p, rscan, nt + 1, nullptr, &tb, s));
     PRK_TRY(temp(tb));
     PRK_TRY(prk_scan_u64((const unsigned long long *)S.d_rcnt.p, rscan, nt + 1, S.d_temp.p, &tb, s));
-    PRK_TRY(prk_objtri_emit(&fp, S.d_objs.p, (const uint32_t *)S.d_k0obj.p, (const uint32_t *)S.d_k0tri0.p, nk0, nt,
+    PRK_TRY(prk_objtri_emit(&fp, d_objs, d_k0obj, d_k0tri0, nk0, nt,
                             escan, pbits, ybits, c->H, S.d_edges.p, S.d_ekeys.p, (uint32_t *)S.d_evals.p, s));
     if (nt) {  // MergeSort of every object (one radix sort of the padded keys, prk_spans.hip)
         const uint32_t end_bit = obits + ybits + pbits;
@@ -1567,7 +1609,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(S.d_bound.ensure(((size_t)nobj + 1) * 8));
     PRK_TRY(S.d_oslot.ensure(((size_t)nobj + 1) * 8));
     unsigned long long *oslot = (unsigned long long *)S.d_oslot.p;
-    PRK_TRY(prk_obj_bound(&fp, S.d_objs.p, nobj, rscan, S.d_edges_in.p, (unsigned long long *)S.d_bound.p, s));
+    PRK_TRY(prk_obj_bound(&fp, d_objs, nobj, rscan, d_edges_in, (unsigned long long *)S.d_bound.p, s));
     PRK_TRY(prk_scan_u64((const unsigned long long *)S.d_bound.p, oslot, nobj + 1, nullptr, &tb, s));
     PRK_TRY(temp(tb));
     PRK_TRY(prk_scan_u64((const unsigned long long *)S.d_bound.p, oslot, nobj + 1, S.d_temp.p, &tb, s));
@@ -1583,17 +1625,20 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(S.d_pos.ensure(ns * 16));
     PRK_TRY(S.d_span_tri.ensure(ns * 4));
     if (scalar) PRK_TRY(S.d_srecs.ensure(ns * 96));  // DrawModel span records (prk_spans.hip ScSpanRecG)
+    const uint32_t nbig_all = (uint32_t)S.h_big_gl.size();
+    if (nbig_all) PRK_TRY(S.d_raw.ensure(ns * 96));   // the slot walks' pairs (prk_spans.hip PairRaw)
     // slots no span takes stay row -1: binned nowhere
     PRK_TRY(hipMemsetAsync(S.d_pos.p, 0xFF, ns * 16, s));
     const uint32_t nwork = 3 * nt + (uint32_t)nk1;
     PRK_TRY(S.d_work.ensure(std::max<size_t>(nwork, 1) * 112));
-    PRK_TRY(prk_obj_gather(S.d_edges.p, ord, total0p, S.d_edges_in.p, (const uint32_t *)S.d_k1src.p, (uint32_t)nk1,
+    PRK_TRY(prk_obj_gather(S.d_edges.p, ord, total0p, d_edges_in, d_k1src, (uint32_t)nk1,
                            S.d_work.p, nwork, s));
-    PRK_TRY(prk_obj_walk(&fp, S.d_objs.p, nobj, (const uint32_t *)S.d_big_gl.p, nbig, wcap,
-                         (const unsigned long long *)S.d_big_off.p, (const uint32_t *)S.d_big_cap.p,
+    PRK_TRY(prk_obj_walk(&fp, d_objs, nobj, d_big, nbig, wcap, d_big_off, d_big_cap,
                          (int32_t *)S.d_pool.p, escan, total0p, S.d_work.p,
-                         oslot, S.d_recs.p, scalar ? S.d_srecs.p : nullptr, S.d_pos.p, (uint32_t *)S.d_span_tri.p,
-                         S.d_spans_in.p, (uint32_t *)S.d_err.p, s));
+                         oslot, S.d_recs.p, scalar ? S.d_srecs.p : nullptr, S.d_raw.p, S.d_pos.p,
+                         (uint32_t *)S.d_span_tri.p, d_spans_in, (uint32_t *)S.d_err.p, s));
+    if (nbig_all)  // the slot walks' pairs into span records
+        PRK_TRY(prk_span_finish(&fp, S.d_raw.p, nslot, S.d_recs.p, scalar ? S.d_srecs.p : nullptr, S.d_pos.p, s));
     PRK_TRY(S.d_scnt.ensure(((size_t)nslot + 1) * 4));
     PRK_TRY(S.d_soff.ensure(((size_t)nslot + 1) * 4));
     uint32_t *scnt = (uint32_t *)S.d_scnt.p, *soff = (uint32_t *)S.d_soff.p;

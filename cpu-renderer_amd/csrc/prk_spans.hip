@@ -40,6 +40,15 @@
 #include "prk_device.h"
 
 namespace prk {
+// Diagnostic builds (-DPRK_WPROF=1): walk_object_slots accumulates its
+// phases' cycles into fp.prof (prk_debug_counters): 0 insertion, 1 expiry,
+// 2 pairing, 3 rows walked, 4 batches (insert_batch_s), 5 small batches,
+// 6 one-at-a-time insertions, 7 the whole walk, 8 new edges, 9-13
+// insert_batch_s: prefix max, gap search, histogram + scan, ranks, moves.
+#ifndef PRK_WPROF
+#define PRK_WPROF 0
+#endif
+#define PRK_WT() (PRK_WPROF ? __builtin_amdgcn_s_memtime() : 0ull)
 
 // One object of the span path.
 //   kind 0: triangles [g0, g0 + tris) of its draw's geometry: FillEdgeTable +
@@ -733,6 +742,7 @@ struct WaveList {
         nb = base + 6 * s;
         bk = base + 7 * s;
         bk2 = base + 8 * s;
+        static_assert(kWaveListArrays == 9, "carve cuts kWaveListArrays arrays");
     }
 };
 
@@ -750,11 +760,43 @@ __device__ __forceinline__ void list_sync() {
     }
 }
 
-__device__ __forceinline__ int wave_max_i32(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+// Lane moves without the LDS (DPP, GFX9): row_shr:n inside each 16-lane row,
+// row_bcast:15 / row_bcast:31 across rows, wave_shr:1 / wave_shl:1 across the
+// wave; a lane without a source keeps `old`.  (__shfl* go through
+// ds_bpermute: an LDS round trip each, the one-wave walks' critical path.)
+template <int CTRL, int ROW = 0xf>
+__device__ __forceinline__ int32_t dpp_i(int32_t old, int32_t v) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, ROW, 0xf, false);
+}
+template <int CTRL, int ROW = 0xf>
+__device__ __forceinline__ float dpp_f(float old, float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, ROW, 0xf, false));
+}
+constexpr int kDppShr1 = 0x111, kDppShr2 = 0x112, kDppShr4 = 0x114, kDppShr8 = 0x118;
+constexpr int kDppBcast15 = 0x142, kDppBcast31 = 0x143, kDppWaveShl1 = 0x130, kDppWaveShr1 = 0x138;
+__device__ __forceinline__ int32_t wave_incl_sum_i32(int32_t v) {
+    v += dpp_i<kDppShr1>(0, v);
+    v += dpp_i<kDppShr2>(0, v);
+    v += dpp_i<kDppShr4>(0, v);
+    v += dpp_i<kDppShr8>(0, v);
+    v += dpp_i<kDppBcast15, 0xa>(0, v);
+    v += dpp_i<kDppBcast31, 0xc>(0, v);
     return v;
 }
+__device__ __forceinline__ int32_t wave_incl_max_i32(int32_t v) {
+    v = max(v, dpp_i<kDppShr1>(INT32_MIN, v));
+    v = max(v, dpp_i<kDppShr2>(INT32_MIN, v));
+    v = max(v, dpp_i<kDppShr4>(INT32_MIN, v));
+    v = max(v, dpp_i<kDppShr8>(INT32_MIN, v));
+    v = max(v, dpp_i<kDppBcast15, 0xa>(INT32_MIN, v));
+    v = max(v, dpp_i<kDppBcast31, 0xc>(INT32_MIN, v));
+    return v;
+}
+__device__ __forceinline__ int32_t readlane_i(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ int wave_max_i32(int v) { return readlane_i(wave_incl_max_i32(v), 63); }
 __device__ __forceinline__ int32_t lane_rank(unsigned long long bal) {
     return (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
 }
@@ -776,6 +818,22 @@ __device__ __forceinline__ LKey entry_key(float x, float g, int32_t l) {
 }
 __device__ __forceinline__ bool key_gt(const LKey &a, const LKey &b) {
     return a.x > b.x || (a.x == b.x && (a.g > b.g || (a.g == b.g && a.l > b.l)));
+}
+// Inclusive prefix maximum of the lanes' keys (lane order), with the lane
+// position of a maximum as payload.
+template <int CTRL, int ROW = 0xf>
+__device__ __forceinline__ void key_max_step(LKey &k, int32_t &p) {
+    const LKey o{dpp_f<CTRL, ROW>(-INFINITY, k.x), dpp_f<CTRL, ROW>(-INFINITY, k.g), dpp_i<CTRL, ROW>(INT32_MIN, k.l)};
+    const int32_t op = dpp_i<CTRL, ROW>(-1, p);
+    if (key_gt(o, k)) { k = o; p = op; }
+}
+__device__ __forceinline__ void wave_key_prefix_max(LKey &k, int32_t &p) {
+    key_max_step<kDppShr1>(k, p);
+    key_max_step<kDppShr2>(k, p);
+    key_max_step<kDppShr4>(k, p);
+    key_max_step<kDppShr8>(k, p);
+    key_max_step<kDppBcast15, 0xa>(k, p);
+    key_max_step<kDppBcast31, 0xc>(k, p);
 }
 
 // One new edge E[c] inserted as the reference does (3654-3713): before the
@@ -840,22 +898,14 @@ __device__ void insert_batch(const WaveList &L, int &m, const ObjEdge *__restric
             LKey kk{-INFINITY, -INFINITY, INT32_MIN};
             int32_t kp = q;
             if (q < m) kk = entry_key(L.x[q], L.g[q], L.left[q]);
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                LKey ok;
-                ok.x = __shfl_up(kk.x, o);
-                ok.g = __shfl_up(kk.g, o);
-                ok.l = __shfl_up(kk.l, o);
-                const int32_t op = __shfl_up(kp, o);
-                if (lane >= o && key_gt(ok, kk)) { kk = ok; kp = op; }
-            }
+            wave_key_prefix_max(kk, kp);
             if (cp >= 0 && key_gt(ck, kk)) { kk = ck; kp = cp; }
             if (q < m) L.aux[q] = kp;
             const int last = min(63, m - 1 - b0);
-            ck.x = __shfl(kk.x, last);
-            ck.g = __shfl(kk.g, last);
-            ck.l = __shfl(kk.l, last);
-            cp = __shfl(kp, last);
+            ck.x = readlane_f(kk.x, last);
+            ck.g = readlane_f(kk.g, last);
+            ck.l = readlane_i(kk.l, last);
+            cp = readlane_i(kp, last);
         }
     }
     list_sync<GL>();
@@ -883,14 +933,9 @@ __device__ void insert_batch(const WaveList &L, int &m, const ObjEdge *__restric
         for (int b0 = 0; b0 < m + 2; b0 += 64) {
             const int q = b0 + lane;
             const int32_t v = q < m + 2 ? L.aux[q] : 0;
-            int32_t inc = v;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int32_t t = __shfl_up(inc, o);
-                if (lane >= o) inc += t;
-            }
+            const int32_t inc = wave_incl_sum_i32(v);
             if (q < m + 2) L.aux[q] = carry + inc - v;
-            carry += __shfl(inc, 63);
+            carry += readlane_i(inc, 63);
         }
     }
     list_sync<GL>();
@@ -1112,134 +1157,245 @@ __device__ void walk_object_wave(const FrameParams &fp, const ObjDesc &od, const
 
 // ---------------------------------------------------------------------------
 // The same walk with everything in LDS (objects whose most active edges fit
-// the launch's capacity C): the list arrays, and the listed edges' mutable
-// state in C slots (a free-slot stack), so a row touches device memory only
-// for the sorted edges it inserts — read ahead 64 at a time into registers —
-// and the spans it writes.  Pairing keeps a chunk's entries in registers:
-// lane k holds pair k, does its first swap (3831-3841) itself and its second
-// (3843-3853) against lane k-1's second entry by a lane shift; the last pair
-// of a chunk hands its second entry to the next chunk's first lane.
+// the launch's capacity C): the listed edges' mutable state in C slots (a
+// free-slot stack), and the list as an array of slot numbers only — its
+// operations move one int per entry and read the keys (X, Gradient, Left,
+// YMax) from the slots.  A row touches device memory only for the sorted
+// edges it inserts (read ahead 64 at a time into registers) and the spans it
+// writes.  Pairing keeps a chunk's entries in registers: lane k holds pair k,
+// does its first swap (3831-3841) itself and its second (3843-3853) against
+// lane k-1's second entry by a DPP lane shift; the last pair of a chunk hands
+// its second entry to the next chunk's first lane.
 // ---------------------------------------------------------------------------
+constexpr int kSlotListArrays = 5;  // int arrays of cap + 2: idx (slots), aux, nb, bk, bk2
 struct SlotLds {
-    WaveList L;   // idx = the entry's slot
-    int32_t *fs;  // free slots: fs[0, top)
-    ObjEdge *st;  // edge state per slot
+    int32_t *idx;  // the list: slot of each entry, in list order
+    int32_t *aux, *nb, *bk, *bk2;  // insertion scratch (insert_batch_s)
+    int32_t *fs;   // free slots: fs[0, top)
+    ObjEdge *st;   // edge state per slot
     __device__ __forceinline__ void carve(int32_t *base, uint32_t cap) {
-        L.carve(base, cap);
-        fs = base + (size_t)kWaveListArrays * (cap + 2);
-        const size_t off = ((size_t)kWaveListArrays * (cap + 2) + cap) * 4;
+        const size_t s = (size_t)cap + 2;
+        idx = base;
+        aux = base + s;
+        nb = base + 2 * s;
+        bk = base + 3 * s;
+        bk2 = base + 4 * s;
+        fs = base + kSlotListArrays * s;
+        const size_t off = ((size_t)kSlotListArrays * s + cap) * 4;
         st = reinterpret_cast<ObjEdge *>(reinterpret_cast<char *>(base) + ((off + 15) & ~(size_t)15));
+    }
+    __device__ __forceinline__ LKey key(int32_t sl) const {
+        return entry_key(st[sl].X, st[sl].G, st[sl].Left);
     }
 };
 __host__ __device__ constexpr size_t slot_lds_bytes(uint32_t cap) {
-    return ((((size_t)kWaveListArrays * (cap + 2) + cap) * 4 + 15) & ~(size_t)15) + (size_t)cap * sizeof(ObjEdge);
+    return ((((size_t)kSlotListArrays * (cap + 2) + cap) * 4 + 15) & ~(size_t)15) + (size_t)cap * sizeof(ObjEdge);
 }
 
-// insert_batch for k <= 64 new edges whose keys and slots lane t holds
-// (rx, rg, rl, ry, rs), the list in LDS.
-__device__ void insert_batch_regs(const WaveList &L, int &m, int k, float rx, float rg, int32_t rl, int32_t ry,
-                                  int32_t rs) {
+// insert_one on the slot list: new edge (key c, slot sl) before the first
+// entry it sorts before (3663-3667), else at the tail.
+__device__ __forceinline__ void insert_one_s(const SlotLds &S, int &m, const LKey &c, int32_t sl) {
+    const int lane = threadIdx.x & 63;
+    int p = m;
+    for (int c0 = 0; c0 < m; c0 += 64) {
+        const int q = c0 + lane;
+        bool b = false;
+        if (q < m) {
+            const int32_t e = S.idx[q];
+            const float x = S.st[e].X, g = S.st[e].G;
+            b = c.x < x || (c.x == x && (c.g < g || (c.g == g && c.l < S.st[e].Left)));
+        }
+        const unsigned long long bal = __ballot(b);
+        if (bal) {
+            p = c0 + (int)__builtin_ctzll(bal);
+            break;
+        }
+    }
+    for (int top = m; top > p; top -= 64) {  // entries [p, m) move up one, top chunk first
+        const int q = top - 1 - lane;
+        const int32_t v = q >= p ? S.idx[q] : 0;
+        wave_lds_sync();
+        if (q >= p) S.idx[q + 1] = v;
+        wave_lds_sync();
+    }
+    if (lane == 0) S.idx[p] = sl;
+    wave_lds_sync();
+    ++m;
+}
+
+// insert_batch on the slot list for k <= 64 new edges whose keys and slots
+// lane t holds (kc, rs).  The gap of a new edge (the first q with PM(q) >
+// key) is non-decreasing in its key, so the order (gap, key, insertion) of
+// insert_batch is the order (key, insertion): new edge t lands at
+// gap(t) + rank(t), rank(t) = #{u : (key(u), u) < (key(t), t)} (by
+// broadcasts, no grouping), and entry q moves up by #{t : gap(t) <= q}.
+__device__ void insert_batch_s(const SlotLds &S, int &m, int k, const LKey &kc, int32_t rs,
+                               unsigned long long *wp = nullptr) {
     const int lane = threadIdx.x & 63;
     const bool mine = lane < k;
-    {  // 1. aux[q] = position of a maximal key of entries [0, q]
+    unsigned long long tq = PRK_WT();
+#define PRK_WQ(i)                                                       \
+    if (PRK_WPROF && wp) {                                              \
+        const unsigned long long t_ = PRK_WT();                         \
+        wp[i] += t_ - tq;                                               \
+        tq = t_;                                                        \
+    }
+    // 1. PM(q) = the maximum key of entries [0, q], its (x, g, l) in (nb, bk, aux);
+    //    two chunks per step (two independent lane scans in flight)
+    float *pmx = reinterpret_cast<float *>(S.nb), *pmg = reinterpret_cast<float *>(S.bk);
+    {
         LKey ck{-INFINITY, -INFINITY, INT32_MIN};
-        int32_t cp = -1;
-        for (int b0 = 0; b0 < m; b0 += 64) {
-            const int q = b0 + lane;
-            LKey kk{-INFINITY, -INFINITY, INT32_MIN};
-            int32_t kp = q;
-            if (q < m) kk = entry_key(L.x[q], L.g[q], L.left[q]);
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                LKey ok;
-                ok.x = __shfl_up(kk.x, o);
-                ok.g = __shfl_up(kk.g, o);
-                ok.l = __shfl_up(kk.l, o);
-                const int32_t op = __shfl_up(kp, o);
-                if (lane >= o && key_gt(ok, kk)) { kk = ok; kp = op; }
-            }
-            if (cp >= 0 && key_gt(ck, kk)) { kk = ck; kp = cp; }
-            if (q < m) L.aux[q] = kp;
-            const int last = min(63, m - 1 - b0);
-            ck.x = __shfl(kk.x, last);
-            ck.g = __shfl(kk.g, last);
-            ck.l = __shfl(kk.l, last);
-            cp = __shfl(kp, last);
+        for (int b0 = 0; b0 < m; b0 += 128) {
+            const int q0 = b0 + lane, q1 = b0 + 64 + lane;
+            LKey k0{-INFINITY, -INFINITY, INT32_MIN}, k1{-INFINITY, -INFINITY, INT32_MIN};
+            int32_t p0 = 0, p1 = 0;
+            if (q0 < m) k0 = S.key(S.idx[q0]);
+            if (q1 < m) k1 = S.key(S.idx[q1]);
+            wave_key_prefix_max(k0, p0);
+            wave_key_prefix_max(k1, p1);
+            if (key_gt(ck, k0)) k0 = ck;
+            const LKey c0{readlane_f(k0.x, 63), readlane_f(k0.g, 63), readlane_i(k0.l, 63)};
+            if (key_gt(c0, k1)) k1 = c0;
+            if (q0 < m) { pmx[q0] = k0.x; pmg[q0] = k0.g; S.aux[q0] = k0.l; }
+            if (q1 < m) { pmx[q1] = k1.x; pmg[q1] = k1.g; S.aux[q1] = k1.l; }
+            ck = LKey{readlane_f(k1.x, 63), readlane_f(k1.g, 63), readlane_i(k1.l, 63)};
         }
     }
     wave_lds_sync();
-    const LKey kc{rx, rg, rl};
+    PRK_WQ(0)
     int gq = 0;  // 2. the gap of new edge `lane`: binary search over the non-decreasing PM
     if (mine) {
         int lo = 0, hi = m;
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
-            const int32_t pq = L.aux[mid];
-            if (key_gt(entry_key(L.x[pq], L.g[pq], L.left[pq]), kc)) hi = mid;
+            if (key_gt(LKey{pmx[mid], pmg[mid], S.aux[mid]}, kc)) hi = mid;
             else lo = mid + 1;
         }
         gq = lo;
     }
     wave_lds_sync();
-    // 3. gap histogram, each new edge's arrival slot in its gap
-    for (int q = lane; q < m + 2; q += 64) L.aux[q] = 0;
-    wave_lds_sync();
-    int32_t arr = 0;
-    if (mine) arr = atomicAdd(&L.aux[gq], 1);
-    wave_lds_sync();
-    {  // 4. exclusive scan: aux[g] = new edges of gaps < g
+    PRK_WQ(1)
+    // 3. entry q's move: #{t : gap(t) <= q}; by broadcasts for few (k x chunks),
+    //    else a gap histogram and its scan (aux[g] = new edges of gaps < g)
+    const int nch = (m + 63) >> 6;
+    const bool hist = k * nch > 64;
+    if (hist) {
+        for (int q = lane; q < m + 2; q += 64) S.aux[q] = 0;
+        wave_lds_sync();
+        if (mine) atomicAdd(&S.aux[gq], 1);
+        wave_lds_sync();
         int32_t carry = 0;
         for (int b0 = 0; b0 < m + 2; b0 += 64) {
             const int q = b0 + lane;
-            const int32_t v = q < m + 2 ? L.aux[q] : 0;
-            int32_t inc = v;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int32_t t = __shfl_up(inc, o);
-                if (lane >= o) inc += t;
-            }
-            if (q < m + 2) L.aux[q] = carry + inc - v;
-            carry += __shfl(inc, 63);
+            const int32_t v = q < m + 2 ? S.aux[q] : 0;
+            const int32_t inc = wave_incl_sum_i32(v);
+            if (q < m + 2) S.aux[q] = carry + inc - v;
+            carry += readlane_i(inc, 63);
         }
+        wave_lds_sync();
     }
-    wave_lds_sync();
-    int32_t s0 = 0, h = 0;
-    if (mine) {  // 5. the new edges grouped by gap
-        s0 = L.aux[gq];
-        h = L.aux[gq + 1] - s0;
-        L.bk2[s0 + arr] = lane;
+    PRK_WQ(2)
+    // 4. rank by (key, insertion order)
+    int32_t at = gq;
+    for (int u = 0; u < k; ++u) {
+        const LKey ku{readlane_f(kc.x, u), readlane_f(kc.g, u), readlane_i(kc.l, u)};
+        at += (key_gt(kc, ku) || (u < lane && !key_gt(ku, kc))) ? 1 : 0;
     }
-    wave_lds_sync();
-    // 6. final positions: gap + new edges of earlier gaps + those of its gap
-    //    ordered before it (smaller key, or an equal key inserted earlier)
-    int32_t r = 0;
-    const int32_t hmax = wave_max_i32(h);
-    for (int32_t j = 0; j < hmax; ++j) {
-        const int32_t u = j < h ? L.bk2[s0 + j] : lane;
-        const LKey ku{__shfl(rx, u), __shfl(rg, u), __shfl(rl, u)};
-        if (j < h && u != lane) r += (key_gt(kc, ku) || (!key_gt(ku, kc) && u < lane)) ? 1 : 0;
-    }
-    const int32_t at = gq + s0 + r;
-    // 7. entries move up by the new edges of gaps <= their position, top chunk first
+    PRK_WQ(3)
+    // 5. entries move up, top chunk first; 6. the new edges into the free slots
     for (int top = m; top > 0; top -= 64) {
         const int q = top - 1 - lane;
-        int32_t vi = 0, vl = 0, vy = 0, to = 0;
-        float vx = 0, vg = 0;
+        int32_t v = 0, to = q;
         if (q >= 0) {
-            to = q + L.aux[q + 1];
-            vi = L.idx[q]; vx = L.x[q]; vg = L.g[q]; vl = L.left[q]; vy = L.ymax[q];
+            v = S.idx[q];
+            if (hist) {
+                to += S.aux[q + 1];
+            } else {
+                for (int t = 0; t < k; ++t) to += readlane_i(gq, t) <= q ? 1 : 0;
+            }
         }
         wave_lds_sync();
-        if (q >= 0 && to != q) { L.idx[to] = vi; L.x[to] = vx; L.g[to] = vg; L.left[to] = vl; L.ymax[to] = vy; }
+        if (q >= 0 && to != q) S.idx[to] = v;
         wave_lds_sync();
     }
-    if (mine) { L.idx[at] = rs; L.x[at] = rx; L.g[at] = rg; L.left[at] = rl; L.ymax[at] = ry; }  // 8.
+    if (mine) S.idx[at] = rs;
     wave_lds_sync();
+    PRK_WQ(4)
+#undef PRK_WQ
     m += k;
 }
 
+// A pair of the slot walk, before its span setup: both edges' values at the
+// row (the fields obj_span / obj_span_scalar read), written by the walk; its
+// SpanPos holds the row, the draw (in minx) and SPAN_RAW until k_span_finish
+// turns it into the span's record (or row -1 when it covers nothing).  The
+// setup's ~300 instructions per span leave the walk's row-serial path.
+constexpr uint32_t SPAN_RAW = 0x40000000u;
+struct PairRaw {
+    float4 l0, l1, l2, r0, r1, r2;  // X Z W U | V N0 N1 N2 | C0 C1 C2 C3, left then right edge
+};
+static_assert(sizeof(PairRaw) == 96, "six dwordx4");
+__device__ __forceinline__ void pair_raw_out(const ObjEdge &a, const ObjEdge &b, PairRaw &o) {
+    o.l0 = make_float4(a.X, a.Z, a.W, a.U);
+    o.l1 = make_float4(a.V, a.N0, a.N1, a.N2);
+    o.l2 = make_float4(a.C0, a.C1, a.C2, a.C3);
+    o.r0 = make_float4(b.X, b.Z, b.W, b.U);
+    o.r1 = make_float4(b.V, b.N0, b.N1, b.N2);
+    o.r2 = make_float4(b.C0, b.C1, b.C2, b.C3);
+}
+__device__ __forceinline__ ObjEdge pair_raw_in(const float4 &q0, const float4 &q1, const float4 &q2) {
+    ObjEdge e = ObjEdge{};
+    e.X = q0.x; e.Z = q0.y; e.W = q0.z; e.U = q0.w;
+    e.V = q1.x; e.N0 = q1.y; e.N1 = q1.z; e.N2 = q1.w;
+    e.C0 = q2.x; e.C1 = q2.y; e.C2 = q2.z; e.C3 = q2.w;
+    return e;
+}
+__global__ void k_span_finish(FrameParams fp, const PairRaw *__restrict__ raw, uint32_t nslot,
+                              SpanRecG *__restrict__ recs, ScSpanRecG *__restrict__ srecs,
+                              SpanPos *__restrict__ pos) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nslot) return;
+    SpanPos p = pos[s];
+    if (p.flags != SPAN_RAW) return;  // (unused slots: all ones)
+    const PairRaw r = raw[s];
+    const ObjEdge L = pair_raw_in(r.l0, r.l1, r.l2), R = pair_raw_in(r.r0, r.r1, r.r2);
+    const DrawRec &d = fp.draws[p.minx];
+    const int32_t Row = p.row;
+    bool em = false;
+    switch (d.mode) {
+        case MODE_AVX: {
+            SpanRecG rec;
+            em = obj_span(fp, L, R, Row, d.tex, (d.flags & DRAW_ST) != 0, rec, p);
+            if (em) recs[s] = rec;
+            break;
+        }
+#define PRK_FINISH_SC(MM)                                                          \
+    case MM: {                                                                     \
+        ScSpanRecG srec;                                                           \
+        em = obj_span_scalar<MM>(fp, L, R, Row, d.tex, srec, p);                   \
+        if (em) {                                                                  \
+            SpanRecG mark;                                                         \
+            mark.q0 = make_float4(__uint_as_float(kScalarSpan), 0.0f, 0.0f, 0.0f); \
+            mark.q1 = mark.q2 = mark.q3 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);     \
+            recs[s] = mark;                                                        \
+            srecs[s] = srec;                                                       \
+        }                                                                          \
+        break;                                                                     \
+    }
+        PRK_FINISH_SC(MODE_SC_GOURAUD)
+        PRK_FINISH_SC(MODE_SC_GOURAUD_TEX)
+        PRK_FINISH_SC(MODE_SC_PHONG)
+        PRK_FINISH_SC(MODE_SC_PHONG_TEX)
+#undef PRK_FINISH_SC
+        default: break;
+    }
+    if (!em) p = SpanPos{-1, 0, 0, 0u};  // covers nothing: binned nowhere
+    pos[s] = p;
+}
+
 // Read-ahead window of sorted edges as seven dwordx4 (ObjEdge's layout: X, G
-// in q0.xy, YMin, YMax, Left in q4.xyz), named registers.
+// in q0.xy, YMin, YMax, Left in q4.xyz), named registers (an ObjEdge copy in
+// a loop-carried variable went to scratch).
 #define PRK_WIN(w) float4 w##0, w##1, w##2, w##3, w##4, w##5, w##6
 #define PRK_WIN_LOAD(w, E, i, n)                                                      \
     do {                                                                              \
@@ -1247,6 +1403,21 @@ __device__ void insert_batch_regs(const WaveList &L, int &m, int k, float rx, fl
         w##0 = s_[0]; w##1 = s_[1]; w##2 = s_[2]; w##3 = s_[3];                       \
         w##4 = s_[4]; w##5 = s_[5]; w##6 = s_[6];                                     \
         if ((i) >= (n)) (w##4).x = __int_as_float(INT32_MAX);  /* past the end */     \
+    } while (0)
+// The window's loads complete right where they are issued (s_waitcnt
+// vmcnt(0), once per 64 edges), and the registers are redefined by an empty
+// asm, so no later use waits on the load again: a window register still in
+// flight across the row loop's back edge made the compiler wait for every
+// outstanding access (the previous row's stores included) at the top of
+// every row.
+#define PRK_WIN_WAIT() __builtin_amdgcn_s_waitcnt(0x0F70)  // vmcnt(0) expcnt(7) lgkmcnt(15)
+#define PRK_Q4(q) "+v"(q.x), "+v"(q.y), "+v"(q.z), "+v"(q.w)
+#define PRK_WIN_LAUNDER(w)                                      \
+    do {                                                        \
+        asm volatile("" : PRK_Q4(w##0), PRK_Q4(w##1));          \
+        asm volatile("" : PRK_Q4(w##2), PRK_Q4(w##3));          \
+        asm volatile("" : PRK_Q4(w##4), PRK_Q4(w##5));          \
+        asm volatile("" : PRK_Q4(w##6));                        \
     } while (0)
 #define PRK_WIN_COPY(d, w) \
     do { d##0 = w##0; d##1 = w##1; d##2 = w##2; d##3 = w##3; d##4 = w##4; d##5 = w##5; d##6 = w##6; } while (0)
@@ -1260,14 +1431,14 @@ __device__ void insert_batch_regs(const WaveList &L, int &m, int k, float rx, fl
 template <int M>
 __device__ void walk_object_slots(const FrameParams &fp, const ObjDesc &od, const DrawRec &d,
                                   const ObjEdge *__restrict__ E, uint32_t n, int32_t MaxY, uint32_t base,
-                                  uint32_t bound, const SlotLds &S, uint32_t cap, SpanRecG *__restrict__ recs,
-                                  ScSpanRecG *__restrict__ srecs, SpanPos *__restrict__ pos,
-                                  uint32_t *__restrict__ span_tri, uint32_t *__restrict__ err) {
+                                  uint32_t bound, const SlotLds &S, uint32_t cap, PairRaw *__restrict__ raw,
+                                  SpanPos *__restrict__ pos, uint32_t *__restrict__ span_tri,
+                                  uint32_t *__restrict__ err) {
     constexpr bool kScalar = M != MODE_AVX;
     const int lane = threadIdx.x & 63;
-    const bool st = (d.flags & DRAW_ST) != 0;
-    const WaveList &L = S.L;
     const int32_t RowLo = kScalar ? fp.row0 - 1 : fp.row0;
+    unsigned long long wp[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const unsigned long long wt0 = PRK_WT();
     for (uint32_t q = lane; q < cap; q += 64) S.fs[q] = (int32_t)q;
     int top = (int)cap;  // free slots
     wave_lds_sync();
@@ -1277,10 +1448,15 @@ __device__ void walk_object_slots(const FrameParams &fp, const ObjDesc &od, cons
     PRK_WIN(wn);
     PRK_WIN_LOAD(wa, E, (uint32_t)lane, n);
     PRK_WIN_LOAD(wn, E, 64u + lane, n);
+    PRK_WIN_WAIT();
+    PRK_WIN_LAUNDER(wa);
+    PRK_WIN_LAUNDER(wn);
     uint32_t emitted = 0;
     int m = 0;
     uint32_t ins = 0;
     for (int32_t Row = E[0].YMin; Row < MaxY; ++Row) {
+        unsigned long long t0 = PRK_WT();
+        if (PRK_WPROF) wp[3] += 1;
         // insertion (3654-3713): the edges with YMin == Row, in sorted order,
         // a window's worth at a time (batches in order == one at a time)
         for (;;) {
@@ -1288,9 +1464,11 @@ __device__ void walk_object_slots(const FrameParams &fp, const ObjDesc &od, cons
                 PRK_WIN_COPY(wa, wn);
                 wb += 64;
                 PRK_WIN_LOAD(wn, E, wb + 64 + lane, n);
+                PRK_WIN_WAIT();
+                PRK_WIN_LAUNDER(wn);
             }
             const float wx = wa0.x, wg = wa0.y;
-            const int32_t wymin = __float_as_int(wa4.x), wymax = __float_as_int(wa4.y), wl = __float_as_int(wa4.z);
+            const int32_t wymin = __float_as_int(wa4.x), wl = __float_as_int(wa4.z);
             const int rel = lane - (int)(ins - wb);
             const unsigned long long lt = __ballot(rel >= 0 && wymin < Row);
             if (lt) {  // (never past the first row: entries below the row are skipped)
@@ -1306,89 +1484,82 @@ __device__ void walk_object_slots(const FrameParams &fp, const ObjDesc &od, cons
                 slot = S.fs[top - 1 - rel];
                 PRK_WIN_STORE(&S.st[slot], wa);
             }
-            const int src = min(63, (int)(ins - wb) + lane);
-            const float rx = __shfl(wx, src), rg = __shfl(wg, src);
-            const int32_t rl = __shfl(wl, src), ry = __shfl(wymax, src), rs = __shfl(slot, src);
             const bool nan = __any(nw && (wx != wx || wg != wg));
             top -= k;
+            if (PRK_WPROF) {
+                wp[8] += (unsigned long long)k;
+                wp[(k <= 2 || nan) ? 6 : 4] += 1;
+            }
             if (k <= 2 || nan) {  // one at a time (any NaN key), 3654-3713
-                for (int t = 0; t < k; ++t)
-                    insert_one<false>(L, m, __shfl(rx, t), __shfl(rg, t), __shfl(rl, t), __shfl(ry, t),
-                                      __shfl(rs, t));
-            } else {
-                insert_batch_regs(L, m, k, rx, rg, rl, ry, rs);
+                for (int t = 0; t < k; ++t) {
+                    const int sl = (int)(ins - wb) + t;
+                    insert_one_s(S, m, LKey{readlane_f(wx, sl), readlane_f(wg, sl), readlane_i(wl, sl)},
+                                 readlane_i(slot, sl));
+                }
+            } else {  // new edge `lane` in lane `lane` (a permute of the window's lanes)
+                const int src = min(63, (int)(ins - wb) + lane);
+                const LKey kn{__shfl(wx, src), __shfl(wg, src), __shfl(wl, src)};
+                insert_batch_s(S, m, k, kn, __shfl(slot, src), PRK_WPROF ? wp + 9 : nullptr);
             }
             ins += (uint32_t)k;
             if (ins < wb + 64) break;  // the row's edges end inside the window
         }
+        if (PRK_WPROF) { const unsigned long long t1 = PRK_WT(); wp[0] += t1 - t0; t0 = t1; }
         {  // expiry 3715-3749: keep entries with YMax > Row, in order; free the others' slots
             int out = 0;
             for (int c0 = 0; c0 < m; c0 += 64) {
                 const int q = c0 + lane;
-                int32_t vi = 0, vl = 0, vy = 0;
-                float vx = 0, vg = 0;
-                if (q < m) { vi = L.idx[q]; vx = L.x[q]; vg = L.g[q]; vl = L.left[q]; vy = L.ymax[q]; }
-                const bool keep = q < m && !(vy <= Row);
+                int32_t e = 0;
+                bool keep = false;
+                if (q < m) {
+                    e = S.idx[q];
+                    keep = !(S.st[e].YMax <= Row);
+                }
                 const bool gone = q < m && !keep;
                 const unsigned long long bal = __ballot(keep), gbal = __ballot(gone);
-                const int at = out + lane_rank(bal);
                 wave_lds_sync();
-                if (keep) { L.idx[at] = vi; L.x[at] = vx; L.g[at] = vg; L.left[at] = vl; L.ymax[at] = vy; }
-                if (gone) S.fs[top + lane_rank(gbal)] = vi;
+                if (keep) S.idx[out + lane_rank(bal)] = e;
+                if (gone) S.fs[top + lane_rank(gbal)] = e;
                 wave_lds_sync();
                 out += __popcll(bal);
                 top += __popcll(gbal);
             }
             m = out;
         }
+        if (PRK_WPROF) { const unsigned long long t1 = PRK_WT(); wp[1] += t1 - t0; t0 = t1; }
         if (m == 0) {  // nothing happens on the rows before the next insertion: go there
             if (ins >= n) break;
-            const int32_t ny = ins < wb + 64 ? __shfl(__float_as_int(wa4.x), (int)(ins - wb))
-                                             : __shfl(__float_as_int(wn4.x), 0);
+            const int32_t ny = ins < wb + 64 ? readlane_i(__float_as_int(wa4.x), (int)(ins - wb))
+                                             : readlane_i(__float_as_int(wn4.x), 0);
             Row = max(Row, ny - 1);
             continue;
         }
         const int P = m / 2;  // pairing 3751-3869
-        int32_t ci = 0, cl = 0, cy = 0;  // the previous chunk's last second entry (carried)
-        float cx = 0, cg = 0;
+        int32_t ci = 0;  // the previous chunk's last second entry (carried) and its X
+        float cx = 0;
         for (int k0 = 0; k0 < P; k0 += 64) {
             const int kk = k0 + lane;
             const bool valid = kk < P;
-            int32_t i0 = 0, i1 = 0, l0 = 0, l1 = 0, y0 = 0, y1 = 0;
-            float g0 = 0, g1 = 0;
-            bool em = false;
-            SpanPos sp;
-            SpanRecG rec;
-            ScSpanRecG srec;
+            int32_t i0 = 0, i1 = 0;
             if (valid) {
-                i0 = L.idx[2 * kk]; g0 = L.g[2 * kk]; l0 = L.left[2 * kk]; y0 = L.ymax[2 * kk];
-                i1 = L.idx[2 * kk + 1]; g1 = L.g[2 * kk + 1]; l1 = L.left[2 * kk + 1]; y1 = L.ymax[2 * kk + 1];
+                i0 = S.idx[2 * kk];
+                i1 = S.idx[2 * kk + 1];
             }
             ObjEdge a = S.st[i0], b = S.st[i1];  // (slot 0 for lanes past the pairs: unused)
-            if (valid) {
-                if (Row >= RowLo) {
-                    if constexpr (kScalar) em = obj_span_scalar<M>(fp, a, b, Row, d.tex, srec, sp);
-                    else em = obj_span(fp, a, b, Row, d.tex, st, rec, sp);
-                }
-            }
+            // every pair of the pass's rows takes a slot, its span set up later (k_span_finish)
+            const bool em = valid && Row >= RowLo;
             const unsigned long long bal = __ballot(em);
             if (em) {
                 const uint32_t j = emitted + (uint32_t)lane_rank(bal);
                 if (j < bound) {
                     const uint32_t at = base + j;
-                    if constexpr (kScalar) {
-                        SpanRecG mark;
-                        mark.q0 = make_float4(__uint_as_float(kScalarSpan), 0.0f, 0.0f, 0.0f);
-                        mark.q1 = mark.q2 = mark.q3 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                        recs[at] = mark;
-                        srecs[at] = srec;
-                    } else {
-                        recs[at] = rec;
-                    }
-                    pos[at] = sp;
+                    PairRaw pr;
+                    pair_raw_out(a, b, pr);
+                    raw[at] = pr;
+                    pos[at] = SpanPos{Row, (int32_t)od.draw, 0, SPAN_RAW};
                     span_tri[at] = od.g0;
                 } else {
-                    atomicOr(err, 2u);  // (never: the bound holds every span)
+                    atomicOr(err, 2u);  // (never: the bound holds every pair)
                 }
             }
             emitted += (uint32_t)__popcll(bal);
@@ -1401,47 +1572,33 @@ __device__ void walk_object_slots(const FrameParams &fp, const ObjDesc &od, cons
                 x0 = a.X;
                 x1 = b.X;
                 if (x0 > x1) {  // 3831-3841
-                    int32_t t;
-                    float f;
-                    t = i0; i0 = i1; i1 = t;
-                    f = x0; x0 = x1; x1 = f;
-                    f = g0; g0 = g1; g1 = f;
-                    t = l0; l0 = l1; l1 = t;
-                    t = y0; y0 = y1; y1 = t;
+                    const int32_t t = i0; i0 = i1; i1 = t;
+                    const float f = x0; x0 = x1; x1 = f;
                 }
             }
             // 3843-3853: pair kk's first entry against pair kk-1's second
-            int32_t pi = __shfl_up(i1, 1), pl = __shfl_up(l1, 1), py = __shfl_up(y1, 1);
-            float px = __shfl_up(x1, 1), pg = __shfl_up(g1, 1);
-            if (lane == 0) { pi = ci; px = cx; pg = cg; pl = cl; py = cy; }
+            // (lane 0: the carried entry)
+            const int32_t pi = dpp_i<kDppWaveShr1>(ci, i1);
+            const float px = dpp_f<kDppWaveShr1>(cx, x1);
             const bool sw = valid && kk >= 1 && px > x0;
-            const bool swn = __shfl_down(sw ? 1 : 0, 1) != 0 && lane < 63;  // the next pair's swap takes my second
-            int32_t ni = __shfl_down(i0, 1), nl = __shfl_down(l0, 1), ny = __shfl_down(y0, 1);
-            float nx = __shfl_down(x0, 1), ng = __shfl_down(g0, 1);
+            const bool swn = dpp_i<kDppWaveShl1>(0, sw ? 1 : 0) != 0;  // the next pair's swap takes my second
+            const int32_t ni = dpp_i<kDppWaveShl1>(0, i0);
             const bool defer = lane == 63 && kk + 1 < P;  // my second waits for the next chunk
             if (valid) {
-                const int q0 = 2 * kk, q1 = 2 * kk + 1;
-                if (sw) {  // entry q0 - 1 = my first, entry q0 = the previous second
-                    if (lane == 0) {
-                        L.idx[q0 - 1] = i0; L.x[q0 - 1] = x0; L.g[q0 - 1] = g0; L.left[q0 - 1] = l0;
-                        L.ymax[q0 - 1] = y0;
-                    }
-                    L.idx[q0] = pi; L.x[q0] = px; L.g[q0] = pg; L.left[q0] = pl; L.ymax[q0] = py;
-                } else {
-                    if (lane == 0 && kk >= 1) {
-                        L.idx[q0 - 1] = pi; L.x[q0 - 1] = px; L.g[q0 - 1] = pg; L.left[q0 - 1] = pl;
-                        L.ymax[q0 - 1] = py;
-                    }
-                    L.idx[q0] = i0; L.x[q0] = x0; L.g[q0] = g0; L.left[q0] = l0; L.ymax[q0] = y0;
-                }
-                if (!defer) {
-                    if (swn) { L.idx[q1] = ni; L.x[q1] = nx; L.g[q1] = ng; L.left[q1] = nl; L.ymax[q1] = ny; }
-                    else { L.idx[q1] = i1; L.x[q1] = x1; L.g[q1] = g1; L.left[q1] = l1; L.ymax[q1] = y1; }
-                }
+                const int q0 = 2 * kk;
+                if (lane == 0 && kk >= 1) S.idx[q0 - 1] = sw ? i0 : pi;  // the carried slot's position
+                S.idx[q0] = sw ? pi : i0;
+                if (!defer) S.idx[q0 + 1] = swn ? ni : i1;
             }
-            ci = __shfl(i1, 63); cx = __shfl(x1, 63); cg = __shfl(g1, 63); cl = __shfl(l1, 63); cy = __shfl(y1, 63);
+            ci = readlane_i(i1, 63);
+            cx = readlane_f(x1, 63);
         }
         wave_lds_sync();
+        if (PRK_WPROF) wp[2] += PRK_WT() - t0;
+    }
+    if (PRK_WPROF && lane == 0) {
+        wp[7] = PRK_WT() - wt0;
+        for (int k = 0; k < 14; ++k) atomicAdd(fp.prof + k, wp[k]);
     }
 }
 
@@ -1470,15 +1627,9 @@ __device__ int32_t obj_max_active(const ObjEdge *__restrict__ E, uint32_t n, int
     int32_t carry = 0, best = 0;
     for (int b0 = 0; b0 < R; b0 += 64) {
         const int q = b0 + lane;
-        int32_t v = q < R ? h[q] : 0;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t t = __shfl_up(v, o);
-            if (lane >= o) v += t;
-        }
-        v += carry;
+        int32_t v = wave_incl_sum_i32(q < R ? h[q] : 0) + carry;
         best = max(best, wave_max_i32(q < R ? v : 0));
-        carry = __shfl(v, 63);
+        carry = readlane_i(v, 63);
     }
     wave_lds_sync();  // (h is the list's storage next)
     return best;
@@ -1497,8 +1648,8 @@ __global__ void __launch_bounds__(64) k_obj_walk_wave(FrameParams fp, const ObjD
                                                       const uint32_t *__restrict__ total0p, ObjEdge *__restrict__ work,
                                                       const unsigned long long *__restrict__ soff,
                                                       SpanRecG *__restrict__ recs, ScSpanRecG *__restrict__ srecs,
-                                                      SpanPos *__restrict__ pos, uint32_t *__restrict__ span_tri,
-                                                      uint32_t *__restrict__ err) {
+                                                      PairRaw *__restrict__ raw, SpanPos *__restrict__ pos,
+                                                      uint32_t *__restrict__ span_tri, uint32_t *__restrict__ err) {
     extern __shared__ int32_t lds_list[];
     const uint32_t o = big[blockIdx.x];
     const ObjDesc od = objs[o];
@@ -1524,7 +1675,7 @@ __global__ void __launch_bounds__(64) k_obj_walk_wave(FrameParams fp, const ObjD
     } else {
         SlotLds S;
         S.carve(lds_list, lcap);
-        walk_object_slots<M>(fp, od, d, E, n, MaxY, base, bound, S, lcap, recs, srecs, pos, span_tri, err);
+        walk_object_slots<M>(fp, od, d, E, n, MaxY, base, bound, S, lcap, raw, pos, span_tri, err);
     }
 }
 
@@ -1691,8 +1842,8 @@ uint32_t prk_obj_walk_lcap(void) {
 hipError_t prk_obj_walk(const prk::FrameParams *fp, const void *objs, uint32_t nobj, const uint32_t *big,
                         const uint32_t *nbig, uint32_t lcap, const unsigned long long *big_off, const uint32_t *big_cap,
                         int32_t *pool, const uint32_t *escan, const uint32_t *total0p, void *work,
-                        const unsigned long long *soff, void *recs, void *srecs, void *pos, uint32_t *span_tri,
-                        const void *spans_in, uint32_t *err, hipStream_t s) {
+                        const unsigned long long *soff, void *recs, void *srecs, void *raw, void *pos,
+                        uint32_t *span_tri, const void *spans_in, uint32_t *err, hipStream_t s) {
     if (nobj == 0) return hipSuccess;
     hipLaunchKernelGGL(prk::k_obj_walk, dim3((nobj + 63) / 64), dim3(64), 0, s, *fp,
                        reinterpret_cast<const prk::ObjDesc *>(objs), nobj, escan, total0p,
@@ -1711,7 +1862,8 @@ hipError_t prk_obj_walk(const prk::FrameParams *fp, const void *objs, uint32_t n
                            reinterpret_cast<const prk::ObjDesc *>(objs), big + b0, big_off + b0, big_cap + b0, pool, \
                            lcap, escan, total0p, reinterpret_cast<prk::ObjEdge *>(work), soff,                      \
                            reinterpret_cast<prk::SpanRecG *>(recs), reinterpret_cast<prk::ScSpanRecG *>(srecs),     \
-                           reinterpret_cast<prk::SpanPos *>(pos), span_tri, err);                                   \
+                           reinterpret_cast<prk::PairRaw *>(raw), reinterpret_cast<prk::SpanPos *>(pos), span_tri,  \
+                           err);                                                                                    \
         break;
         switch (mo) {
             PRK_WALK_WAVE(prk::MODE_AVX)
@@ -1726,6 +1878,15 @@ hipError_t prk_obj_walk(const prk::FrameParams *fp, const void *objs, uint32_t n
         b0 += nb;
     }
     return e;
+}
+// The slot walk's pairs (SPAN_RAW) into span records, one thread per slot.
+hipError_t prk_span_finish(const prk::FrameParams *fp, const void *raw, uint32_t nslot, void *recs, void *srecs,
+                           void *pos, hipStream_t s) {
+    if (nslot == 0) return hipSuccess;
+    hipLaunchKernelGGL(prk::k_span_finish, dim3((nslot + 255) / 256), dim3(256), 0, s, *fp,
+                       reinterpret_cast<const prk::PairRaw *>(raw), nslot, reinterpret_cast<prk::SpanRecG *>(recs),
+                       reinterpret_cast<prk::ScSpanRecG *>(srecs), reinterpret_cast<prk::SpanPos *>(pos));
+    return hipGetLastError();
 }
 
 // Exclusive scan of n + 1 64-bit counts (temp == nullptr: size query).
