@@ -1168,9 +1168,11 @@ __device__ void walk_object_wave(const FrameParams &fp, const ObjDesc &od, const
 // its second entry to the next chunk's first lane.
 // ---------------------------------------------------------------------------
 constexpr int kSlotListArrays = 5;  // int arrays of cap + 2: idx (slots), aux, nb, bk, bk2
+constexpr int kSlotBatchKeys = 3 * 64;  // a batch's new-edge keys (x, g, l of up to 64)
 struct SlotLds {
     int32_t *idx;  // the list: slot of each entry, in list order
     int32_t *aux, *nb, *bk, *bk2;  // insertion scratch (insert_batch_s)
+    int32_t *nk;   // the batch's new-edge keys: x[64], g[64], l[64]
     int32_t *fs;   // free slots: fs[0, top)
     ObjEdge *st;   // edge state per slot
     __device__ __forceinline__ void carve(int32_t *base, uint32_t cap) {
@@ -1180,8 +1182,9 @@ struct SlotLds {
         nb = base + 2 * s;
         bk = base + 3 * s;
         bk2 = base + 4 * s;
-        fs = base + kSlotListArrays * s;
-        const size_t off = ((size_t)kSlotListArrays * s + cap) * 4;
+        nk = base + kSlotListArrays * s;
+        fs = nk + kSlotBatchKeys;
+        const size_t off = ((size_t)kSlotListArrays * s + kSlotBatchKeys + cap) * 4;
         st = reinterpret_cast<ObjEdge *>(reinterpret_cast<char *>(base) + ((off + 15) & ~(size_t)15));
     }
     __device__ __forceinline__ LKey key(int32_t sl) const {
@@ -1189,7 +1192,8 @@ struct SlotLds {
     }
 };
 __host__ __device__ constexpr size_t slot_lds_bytes(uint32_t cap) {
-    return ((((size_t)kSlotListArrays * (cap + 2) + cap) * 4 + 15) & ~(size_t)15) + (size_t)cap * sizeof(ObjEdge);
+    return ((((size_t)kSlotListArrays * (cap + 2) + kSlotBatchKeys + cap) * 4 + 15) & ~(size_t)15) +
+           (size_t)cap * sizeof(ObjEdge);
 }
 
 // insert_one on the slot list: new edge (key c, slot sl) before the first
@@ -1224,11 +1228,7 @@ __device__ __forceinline__ void insert_one_s(const SlotLds &S, int &m, const LKe
 }
 
 // insert_batch on the slot list for k <= 64 new edges whose keys and slots
-// lane t holds (kc, rs).  The gap of a new edge (the first q with PM(q) >
-// key) is non-decreasing in its key, so the order (gap, key, insertion) of
-// insert_batch is the order (key, insertion): new edge t lands at
-// gap(t) + rank(t), rank(t) = #{u : (key(u), u) < (key(t), t)} (by
-// broadcasts, no grouping), and entry q moves up by #{t : gap(t) <= q}.
+// lane t holds (kc, rs).
 __device__ void insert_batch_s(const SlotLds &S, int &m, int k, const LKey &kc, int32_t rs,
                                unsigned long long *wp = nullptr) {
     const int lane = threadIdx.x & 63;
@@ -1275,15 +1275,13 @@ __device__ void insert_batch_s(const SlotLds &S, int &m, int k, const LKey &kc, 
     }
     wave_lds_sync();
     PRK_WQ(1)
-    // 3. entry q's move: #{t : gap(t) <= q}; by broadcasts for few (k x chunks),
-    //    else a gap histogram and its scan (aux[g] = new edges of gaps < g)
-    const int nch = (m + 63) >> 6;
-    const bool hist = k * nch > 64;
-    if (hist) {
-        for (int q = lane; q < m + 2; q += 64) S.aux[q] = 0;
-        wave_lds_sync();
-        if (mine) atomicAdd(&S.aux[gq], 1);
-        wave_lds_sync();
+    // 3. gap histogram, each new edge's arrival slot in its gap
+    for (int q = lane; q < m + 2; q += 64) S.aux[q] = 0;
+    wave_lds_sync();
+    int32_t arr = 0;
+    if (mine) arr = atomicAdd(&S.aux[gq], 1);
+    wave_lds_sync();
+    {  // 4. exclusive scan: aux[g] = new edges of gaps < g
         int32_t carry = 0;
         for (int b0 = 0; b0 < m + 2; b0 += 64) {
             const int q = b0 + lane;
@@ -1292,36 +1290,94 @@ __device__ void insert_batch_s(const SlotLds &S, int &m, int k, const LKey &kc, 
             if (q < m + 2) S.aux[q] = carry + inc - v;
             carry += readlane_i(inc, 63);
         }
-        wave_lds_sync();
     }
+    wave_lds_sync();
+    int32_t s0 = 0, h = 0;
+    if (mine) {  // 5. the new edges grouped by gap
+        s0 = S.aux[gq];
+        h = S.aux[gq + 1] - s0;
+        S.bk2[s0 + arr] = lane;
+    }
+    wave_lds_sync();
     PRK_WQ(2)
-    // 4. rank by (key, insertion order)
-    int32_t at = gq;
-    for (int u = 0; u < k; ++u) {
-        const LKey ku{readlane_f(kc.x, u), readlane_f(kc.g, u), readlane_i(kc.l, u)};
-        at += (key_gt(kc, ku) || (u < lane && !key_gt(ku, kc))) ? 1 : 0;
+    // 6. final positions: gap + new edges of earlier gaps + those of its gap
+    //    ordered before it (smaller key, or an equal key inserted earlier)
+    int32_t r = 0;
+    const int32_t hmax = wave_max_i32(h);
+    for (int32_t j = 0; j < hmax; ++j) {
+        const int32_t u = j < h ? S.bk2[s0 + j] : lane;
+        const LKey ku{__shfl(kc.x, u), __shfl(kc.g, u), __shfl(kc.l, u)};
+        if (j < h && u != lane) r += (key_gt(kc, ku) || (!key_gt(ku, kc) && u < lane)) ? 1 : 0;
     }
+    const int32_t at = gq + s0 + r;
     PRK_WQ(3)
-    // 5. entries move up, top chunk first; 6. the new edges into the free slots
+    // 7. entries move up by the new edges of gaps <= their position, top chunk first
     for (int top = m; top > 0; top -= 64) {
         const int q = top - 1 - lane;
-        int32_t v = 0, to = q;
+        int32_t v = 0, to = 0;
         if (q >= 0) {
+            to = q + S.aux[q + 1];
             v = S.idx[q];
-            if (hist) {
-                to += S.aux[q + 1];
-            } else {
-                for (int t = 0; t < k; ++t) to += readlane_i(gq, t) <= q ? 1 : 0;
-            }
         }
         wave_lds_sync();
         if (q >= 0 && to != q) S.idx[to] = v;
         wave_lds_sync();
     }
-    if (mine) S.idx[at] = rs;
+    if (mine) S.idx[at] = rs;  // 8.
     wave_lds_sync();
     PRK_WQ(4)
 #undef PRK_WQ
+    m += k;
+}
+
+// insert_batch_s for a few new edges (k <= kSmallBatch): each gap counted
+// by ballots over the list's prefix maxima (registers, no LDS search), the
+// ranks among the new edges by broadcasts, then one top-down move.
+constexpr int kSmallBatch = 8;
+__device__ void insert_small_s(const SlotLds &S, int &m, int k, const LKey &kc, int32_t rs) {
+    const int lane = threadIdx.x & 63;
+    int32_t gap = 0;  // lane t < k: the gap of new edge t = #{q : PM(q) <= key(t)}
+    {
+        LKey ck{-INFINITY, -INFINITY, INT32_MIN};
+        for (int b0 = 0; b0 < m; b0 += 64) {
+            const int q = b0 + lane;
+            LKey kk{-INFINITY, -INFINITY, INT32_MIN};
+            int32_t kp = 0;
+            if (q < m) kk = S.key(S.idx[q]);
+            wave_key_prefix_max(kk, kp);
+            if (key_gt(ck, kk)) kk = ck;
+            for (int t = 0; t < k; ++t) {
+                const LKey kt{readlane_f(kc.x, t), readlane_f(kc.g, t), readlane_i(kc.l, t)};
+                const int c = __popcll(__ballot(q < m && !key_gt(kk, kt)));
+                if (lane == t) gap += c;
+            }
+            const int last = min(63, m - 1 - b0);
+            ck.x = readlane_f(kk.x, last);
+            ck.g = readlane_f(kk.g, last);
+            ck.l = readlane_i(kk.l, last);
+        }
+    }
+    int32_t at = gap;  // + the new edges ordered before it: smaller gap, key, or insertion
+    for (int u = 0; u < k; ++u) {
+        const int32_t gu = readlane_i(gap, u);
+        const LKey ku{readlane_f(kc.x, u), readlane_f(kc.g, u), readlane_i(kc.l, u)};
+        const bool before = gu < gap || (gu == gap && (key_gt(kc, ku) || (!key_gt(ku, kc) && u < lane)));
+        at += (u != lane && before) ? 1 : 0;
+    }
+    // entries move up by the new edges of gaps <= their position, top chunk first
+    for (int top = m; top > 0; top -= 64) {
+        const int q = top - 1 - lane;
+        int32_t v = 0, to = q;
+        if (q >= 0) {
+            v = S.idx[q];
+            for (int t = 0; t < k; ++t) to += readlane_i(gap, t) <= q ? 1 : 0;
+        }
+        wave_lds_sync();
+        if (q >= 0 && to != q) S.idx[to] = v;
+        wave_lds_sync();
+    }
+    if (lane < k) S.idx[at] = rs;
+    wave_lds_sync();
     m += k;
 }
 
@@ -1488,7 +1544,7 @@ __device__ void walk_object_slots(const FrameParams &fp, const ObjDesc &od, cons
             top -= k;
             if (PRK_WPROF) {
                 wp[8] += (unsigned long long)k;
-                wp[(k <= 2 || nan) ? 6 : 4] += 1;
+                wp[(k <= 2 || nan) ? 6 : (k <= kSmallBatch ? 5 : 4)] += 1;
             }
             if (k <= 2 || nan) {  // one at a time (any NaN key), 3654-3713
                 for (int t = 0; t < k; ++t) {
@@ -1499,7 +1555,8 @@ __device__ void walk_object_slots(const FrameParams &fp, const ObjDesc &od, cons
             } else {  // new edge `lane` in lane `lane` (a permute of the window's lanes)
                 const int src = min(63, (int)(ins - wb) + lane);
                 const LKey kn{__shfl(wx, src), __shfl(wg, src), __shfl(wl, src)};
-                insert_batch_s(S, m, k, kn, __shfl(slot, src), PRK_WPROF ? wp + 9 : nullptr);
+                if (k <= kSmallBatch) insert_small_s(S, m, k, kn, __shfl(slot, src));
+                else insert_batch_s(S, m, k, kn, __shfl(slot, src), PRK_WPROF ? wp + 9 : nullptr);
             }
             ins += (uint32_t)k;
             if (ins < wb + 64) break;  // the row's edges end inside the window
