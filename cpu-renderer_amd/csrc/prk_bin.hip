@@ -35,12 +35,27 @@ namespace prk {
 // are edge-DDA values that stay on their segment up to float error
 // (DESIGN.md §4.1), so [min x, max x] of the projected vertices widened by
 // that error bounds every covered pixel; rows lie in [floor(min y), ceil(max y)).
+__device__ __forceinline__ bool tri_tile_range_proj(const FrameParams &fp, const DrawRec *d, const V3 *proj,
+                                                    TileRange &tr);
 __device__ __forceinline__ bool tri_tile_range(const FrameParams &fp, uint32_t g, TileRange &tr) {
     const DrawRec *d;
     uint32_t gt;
     resolve_draw(fp, g, d, gt);
     V3 cam[3], proj[3];
     load_positions(*d, gt, fp, cam, proj);
+    return tri_tile_range_proj(fp, d, proj, tr);
+}
+// The same from triangle g's nine position floats already loaded (v).
+__device__ __forceinline__ bool tri_tile_range_raw(const FrameParams &fp, const DrawRec *d, const float *v,
+                                                   TileRange &tr) {
+    V3 proj[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        proj[k] = project_vertex(V3{v[3 * k + 0] + d->P[0], v[3 * k + 1] + d->P[1], v[3 * k + 2] + d->P[2]}, fp);
+    return tri_tile_range_proj(fp, d, proj, tr);
+}
+__device__ __forceinline__ bool tri_tile_range_proj(const FrameParams &fp, const DrawRec *d, const V3 *proj,
+                                                    TileRange &tr) {
     const float ymin = fminf(proj[0].y, fminf(proj[1].y, proj[2].y));
     const float ymax = fmaxf(proj[0].y, fmaxf(proj[1].y, proj[2].y));
     const float fr0 = floorf(ymin), fr1 = ceilf(ymax);
@@ -251,12 +266,31 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_band(FrameParams fp, uint
     __shared__ uint32_t scratch[kCountThreads / 64];
     const uint32_t g0 = blockIdx.x * kRecRun;
     uint32_t n = 0;
-    for (uint32_t k = 0; k < kRecRun; k += kCountThreads) {
+    // the run's positions (8 triangles per thread) are all requested first, so
+    // their loads overlap instead of one round trip per 256 triangles
+    constexpr int kIt = kRecRun / kCountThreads;
+    float pv[kIt][9];
+    const DrawRec *pd[kIt];
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+        const uint32_t g = g0 + it * kCountThreads + threadIdx.x;
+        pd[it] = fp.draws;
+        if (g < fp.tri_count) {
+            uint32_t gt;
+            resolve_draw(fp, g, pd[it], gt);
+            const float *v = pd[it]->V + 9 * (size_t)gt;
+#pragma unroll
+            for (int j = 0; j < 9; ++j) pv[it][j] = v[j];
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+        const uint32_t k = (uint32_t)it * kCountThreads;
         const uint32_t g = g0 + k + threadIdx.x;
         uint32_t ne = 0;
         if (g < fp.tri_count) {
             TileRange tr;
-            if (!tri_tile_range(fp, g, tr)) {
+            if (!tri_tile_range_raw(fp, pd[it], pv[it], tr)) {
                 tr.tx0 = 1; tr.tx1 = 0; tr.ty0 = 1; tr.ty1 = 0; tr.oty0 = 1; tr.oty1 = 0;
             }
             ne = range_entries(tr);
@@ -804,13 +838,23 @@ hipError_t prk_bin_count(const prk::FrameParams *fp, uint32_t *tri_n, void *rang
 // runs per chunk: about one whole-frame chunk's worth (kCsChunk) of the
 // band's share of the triangles, so a narrow band has few chunks (and a
 // small chunk x tile histogram).  0: not a band (whole-frame chunks).
+uint32_t prk_bin_runs(uint32_t tri_count);
+#ifndef PRK_BAND_MIN_CHUNKS
+#define PRK_BAND_MIN_CHUNKS 128  // > 0: at least about this many chunks (smaller ones) per band frame
+                                 // (C3b N = 8: 31 chunks of 1024 threads left the sort on 31 CUs;
+                                 // serial binning 0.128 -> 0.094-0.109 ms, N = 4 0.134 -> 0.115)
+#endif
 uint32_t prk_cs_band_runs_per_chunk(const prk::FrameParams *fp) {
     const bool band = fp->row0 > 0 || fp->row1 < fp->H;
     if (!band || !PRK_BIN_BAND) return 0;
     const int64_t rows = std::max<int64_t>(1, (int64_t)std::min(fp->row1, fp->H) - fp->row0);
     const int64_t share = std::max<int64_t>(1, (int64_t)fp->H / rows);  // ~ triangles per band triangle
-    const int64_t per = (int64_t)prk::kCsChunk * share / prk::kRecRun;
-    return (uint32_t)std::min<int64_t>(prk::kMaxRunsPerChunk, std::max<int64_t>(2, per));
+    int64_t per = (int64_t)prk::kCsChunk * share / prk::kRecRun;
+    if (PRK_BAND_MIN_CHUNKS > 0) {
+        const int64_t nruns = (int64_t)prk_bin_runs(fp->tri_count);
+        per = std::min<int64_t>(per, nruns / std::max(1, PRK_BAND_MIN_CHUNKS));
+    }
+    return (uint32_t)std::min<int64_t>(prk::kMaxRunsPerChunk, std::max<int64_t>(1, per));
 }
 uint32_t prk_bin_runs(uint32_t tri_count) { return (tri_count + 1 + prk::kRecRun - 1) / prk::kRecRun; }
 
