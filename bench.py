@@ -78,18 +78,21 @@ def load_traffic(cfg_key):
         return None, None
 
 
-def load_valu(cfg_key, kernel):
+def load_valu(cfg_key, kernel, ms_frame=None):
     """The dominant kernel's issued-VALU time estimate and lane utilisation
     from the round's SQ counter passes (tools/profile_round.sh ->
-    tools/sqsum.py --json -> profiles/sq_valu.json), or None.  NOT measured by
+    tools/sqsum.py --json -> profiles/sq_valu.json), or None, and that VALU
+    time's share of this run's frame (`valu_frac_of_frame`).  NOT measured by
     this run: SQ counters need their own rocprofv3 passes."""
     p = os.path.join(ROOT, "profiles", "sq_valu.json")
     try:
         with open(p) as f:
             e = json.load(f)[cfg_key]
         k = next(v for n, v in e["per_kernel"].items() if n.startswith(kernel + "<") or n == kernel)
-        return dict(kernel=kernel, valu_time_estimate_ms=k.get("valu_time_estimate_ms"),
-                    lane_utilisation=k.get("lane_utilisation"), valu_issue_floor_ms=k.get("valu_issue_floor_ms"),
+        vt = k.get("valu_time_estimate_ms")
+        return dict(kernel=kernel, valu_time_estimate_ms=vt, lane_utilisation=k.get("lane_utilisation"),
+                    valu_issue_floor_ms=k.get("valu_issue_floor_ms"), valu_insts=k.get("insts_valu"),
+                    valu_frac_of_frame=(vt / ms_frame) if (vt and ms_frame) else None,
                     source="profiles/sq_valu.json[%s] (%s)" % (cfg_key, e.get("round", "?")))
     except (OSError, ValueError, KeyError, StopIteration):
         return None
@@ -421,10 +424,13 @@ def main():
         "ms_upload": ms_upload,
         "ms_download": ms_download,
         # Whole frame against HBM: SURVEY §8(d) algorithmic bytes / ms_per_step.
-        # The dominant kernel (k_vis) is VALU/latency-bound, not HBM-bound
-        # (profiles/*sq*): its serial time and the same bytes
-        # over it are reported beside the frame figure.
-        "roofline": {"bound": "hbm", "kernel": "whole frame (binning + k_vis + k_walk + k_pix)",
+        # `bound` names the roofline `frac` is priced on (the contract's
+        # hbm|mfma); what actually limits the frame is `limiter`: the dominant
+        # kernel (k_vis) is VALU-issue-bound, not HBM-bound (DESIGN.md §5,
+        # profiles/r04/sq_summary.txt), its VALU time and that time's share
+        # of the frame are in `valu`.
+        "roofline": {"bound": "hbm", "limiter": "valu-issue (k_vis); no kernel of the frame is HBM-bound",
+                     "kernel": "whole frame (binning + k_vis + k_walk + k_pix)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes": alg,
                      "dominant_kernel": {"name": "k_vis", "ms_serial": serial["k_vis"],
@@ -432,7 +438,7 @@ def main():
                                              1e-9, serial["raster"] + serial["k_bin_phase"])},
                      # the binding resource of the dominant kernel: issued VALU
                      # (SQ counters of the committed round profile)
-                     "valu": load_valu(cfg_key, "k_vis")},
+                     "valu": load_valu(cfg_key, "k_vis", ms)},
     }
     if check is not None:
         out["check"] = check
