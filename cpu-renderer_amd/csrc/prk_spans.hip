@@ -40,11 +40,10 @@
 #include "prk_device.h"
 
 namespace prk {
-// Diagnostic builds (-DPRK_WPROF=1): walk_object_slots accumulates its
+// Diagnostic builds (-DPRK_WPROF=1): walk_object_block accumulates its
 // phases' cycles into fp.prof (prk_debug_counters): 0 insertion, 1 expiry,
-// 2 pairing, 3 rows walked, 4 batches (insert_batch_s), 5 small batches,
-// 6 one-at-a-time insertions, 7 the whole walk, 8 new edges, 9-13
-// insert_batch_s: prefix max, gap search, histogram + scan, ranks, moves.
+// 2 pairing, 3 rows walked, 4 batches (insert_batch_b), 6 one-at-a-time
+// insertions, 7 the whole walk, 8 new edges.
 #ifndef PRK_WPROF
 #define PRK_WPROF 0
 #endif
@@ -722,7 +721,7 @@ __global__ void __launch_bounds__(64) k_obj_walk(FrameParams fp, const ObjDesc *
 //                          passes.  An odd last entry neither pairs nor steps.
 // ---------------------------------------------------------------------------
 constexpr int kWaveListArrays = 9;   // int32 arrays of cap + 2 entries each
-constexpr uint32_t kSlotCapLds = 1024;  // walk_object_slots' largest LDS capacity (listed edges)
+constexpr uint32_t kSlotCapLds = 1022;  // walk_object_block's largest LDS capacity (listed edges; 1024 threads)
 struct WaveList {
     int32_t *idx;
     float *x, *g;
@@ -761,8 +760,8 @@ __device__ __forceinline__ void list_sync() {
 }
 
 // Lane moves without the LDS (DPP, GFX9): row_shr:n inside each 16-lane row,
-// row_bcast:15 / row_bcast:31 across rows, wave_shr:1 / wave_shl:1 across the
-// wave; a lane without a source keeps `old`.  (__shfl* go through
+// row_bcast:15 / row_bcast:31 across rows; a lane without a source keeps
+// `old`.  (__shfl* go through
 // ds_bpermute: an LDS round trip each, the one-wave walks' critical path.)
 template <int CTRL, int ROW = 0xf>
 __device__ __forceinline__ int32_t dpp_i(int32_t old, int32_t v) {
@@ -773,7 +772,7 @@ __device__ __forceinline__ float dpp_f(float old, float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, ROW, 0xf, false));
 }
 constexpr int kDppShr1 = 0x111, kDppShr2 = 0x112, kDppShr4 = 0x114, kDppShr8 = 0x118;
-constexpr int kDppBcast15 = 0x142, kDppBcast31 = 0x143, kDppWaveShl1 = 0x130, kDppWaveShr1 = 0x138;
+constexpr int kDppBcast15 = 0x142, kDppBcast31 = 0x143;
 __device__ __forceinline__ int32_t wave_incl_sum_i32(int32_t v) {
     v += dpp_i<kDppShr1>(0, v);
     v += dpp_i<kDppShr2>(0, v);
@@ -1156,35 +1155,47 @@ __device__ void walk_object_wave(const FrameParams &fp, const ObjDesc &od, const
 }
 
 // ---------------------------------------------------------------------------
-// The same walk with everything in LDS (objects whose most active edges fit
-// the launch's capacity C): the listed edges' mutable state in C slots (a
-// free-slot stack), and the list as an array of slot numbers only — its
-// operations move one int per entry and read the keys (X, Gradient, Left,
-// YMax) from the slots.  A row touches device memory only for the sorted
-// edges it inserts (read ahead 64 at a time into registers) and the spans it
-// writes.  Pairing keeps a chunk's entries in registers: lane k holds pair k,
-// does its first swap (3831-3841) itself and its second (3843-3853) against
-// lane k-1's second entry by a DPP lane shift; the last pair of a chunk hands
-// its second entry to the next chunk's first lane.
+// The same walk by a whole workgroup, everything in LDS (objects whose most
+// active edges fit the launch's capacity C <= 1022): the listed edges'
+// mutable state in C slots (a free-slot stack), and the list as an array of
+// slot numbers only — its operations move one int per entry and read the
+// keys (X, Gradient, Left, YMax) from the slots.  The workgroup has NT >= C + 2
+// threads, so every list operation is one step: thread q holds entry q, the
+// scans and searches are workgroup scans (a DPP wave scan plus the waves'
+// totals through LDS).  A lone wave walking a long list in 64-entry chunks
+// ran each row's chain of dependent steps chunk after chunk (C2 as one
+// object: ~80 k clocks a row); here a row is ~20 barriers.  A row touches
+// device memory only for the sorted edges it inserts (read ahead NT at a
+// time, one per thread) and the pairs it writes.  Pairing: thread k holds
+// pair k, does its first swap (3831-3841) itself and its second (3843-3853)
+// against pair k-1's second entry through LDS.
 // ---------------------------------------------------------------------------
 constexpr int kSlotListArrays = 5;  // int arrays of cap + 2: idx (slots), aux, nb, bk, bk2
-constexpr int kSlotBatchKeys = 3 * 64;  // a batch's new-edge keys (x, g, l of up to 64)
+constexpr uint32_t kSlotMaxThreads = 1024;
+__host__ __device__ constexpr uint32_t slot_threads(uint32_t cap) {  // NT: >= cap + 2, a multiple of 64
+    return ((cap + 2 + 63) / 64) * 64 > kSlotMaxThreads ? kSlotMaxThreads : ((cap + 2 + 63) / 64) * 64;
+}
 struct SlotLds {
     int32_t *idx;  // the list: slot of each entry, in list order
-    int32_t *aux, *nb, *bk, *bk2;  // insertion scratch (insert_batch_s)
-    int32_t *nk;   // the batch's new-edge keys: x[64], g[64], l[64]
+    int32_t *aux, *nb, *bk, *bk2;  // insertion / pairing scratch
+    float *nkx, *nkg;              // the batch's new edges: keys (x, g, l) and slots, NT each
+    int32_t *nkl, *nks;
     int32_t *fs;   // free slots: fs[0, top)
     ObjEdge *st;   // edge state per slot
-    __device__ __forceinline__ void carve(int32_t *base, uint32_t cap) {
+    __device__ __forceinline__ void carve(int32_t *base, uint32_t cap, uint32_t nt) {
         const size_t s = (size_t)cap + 2;
         idx = base;
         aux = base + s;
         nb = base + 2 * s;
         bk = base + 3 * s;
         bk2 = base + 4 * s;
-        nk = base + kSlotListArrays * s;
-        fs = nk + kSlotBatchKeys;
-        const size_t off = ((size_t)kSlotListArrays * s + kSlotBatchKeys + cap) * 4;
+        int32_t *k = base + kSlotListArrays * s;
+        nkx = reinterpret_cast<float *>(k);
+        nkg = reinterpret_cast<float *>(k + nt);
+        nkl = k + 2 * nt;
+        nks = k + 3 * nt;
+        fs = k + 4 * nt;
+        const size_t off = ((size_t)kSlotListArrays * s + 4 * (size_t)nt + cap) * 4;
         st = reinterpret_cast<ObjEdge *>(reinterpret_cast<char *>(base) + ((off + 15) & ~(size_t)15));
     }
     __device__ __forceinline__ LKey key(int32_t sl) const {
@@ -1192,79 +1203,144 @@ struct SlotLds {
     }
 };
 __host__ __device__ constexpr size_t slot_lds_bytes(uint32_t cap) {
-    return ((((size_t)kSlotListArrays * (cap + 2) + kSlotBatchKeys + cap) * 4 + 15) & ~(size_t)15) +
+    return ((((size_t)kSlotListArrays * (cap + 2) + 4 * (size_t)slot_threads(cap) + cap) * 4 + 15) & ~(size_t)15) +
            (size_t)cap * sizeof(ObjEdge);
 }
 
-// insert_one on the slot list: new edge (key c, slot sl) before the first
-// entry it sorts before (3663-3667), else at the tail.
-__device__ __forceinline__ void insert_one_s(const SlotLds &S, int &m, const LKey &c, int32_t sl) {
-    const int lane = threadIdx.x & 63;
-    int p = m;
-    for (int c0 = 0; c0 < m; c0 += 64) {
-        const int q = c0 + lane;
-        bool b = false;
-        if (q < m) {
-            const int32_t e = S.idx[q];
-            const float x = S.st[e].X, g = S.st[e].G;
-            b = c.x < x || (c.x == x && (c.g < g || (c.g == g && c.l < S.st[e].Left)));
-        }
-        const unsigned long long bal = __ballot(b);
-        if (bal) {
-            p = c0 + (int)__builtin_ctzll(bal);
-            break;
-        }
+// Workgroup reductions and scans over thread order (R: the waves' partials;
+// every caller reaches them with the whole workgroup).
+struct BlockRed {
+    int32_t a[16], b[16], c[16];
+    float x[16], g[16];
+};
+__device__ __forceinline__ int32_t blk_excl_sum(BlockRed &R, int32_t v, int32_t &tot) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int32_t inc = wave_incl_sum_i32(v);
+    if (lane == 63) R.a[w] = inc;
+    __syncthreads();
+    int32_t before = 0, t = 0;
+    for (int i = 0; i < nw; ++i) {
+        const int32_t x = R.a[i];
+        before += i < w ? x : 0;
+        t += x;
     }
-    for (int top = m; top > p; top -= 64) {  // entries [p, m) move up one, top chunk first
-        const int q = top - 1 - lane;
-        const int32_t v = q >= p ? S.idx[q] : 0;
-        wave_lds_sync();
-        if (q >= p) S.idx[q + 1] = v;
-        wave_lds_sync();
+    __syncthreads();
+    tot = t;
+    return before + inc - v;
+}
+// Two exclusive scans at once (one barrier pair).
+__device__ __forceinline__ void blk_excl_sum2(BlockRed &R, int32_t v1, int32_t v2, int32_t &e1, int32_t &e2,
+                                              int32_t &t1, int32_t &t2) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int32_t i1 = wave_incl_sum_i32(v1), i2 = wave_incl_sum_i32(v2);
+    if (lane == 63) { R.a[w] = i1; R.b[w] = i2; }
+    __syncthreads();
+    int32_t b1 = 0, b2 = 0, s1 = 0, s2 = 0;
+    for (int i = 0; i < nw; ++i) {
+        const int32_t x = R.a[i], y = R.b[i];
+        b1 += i < w ? x : 0;
+        b2 += i < w ? y : 0;
+        s1 += x;
+        s2 += y;
     }
-    if (lane == 0) S.idx[p] = sl;
-    wave_lds_sync();
+    __syncthreads();
+    e1 = b1 + i1 - v1;
+    e2 = b2 + i2 - v2;
+    t1 = s1;
+    t2 = s2;
+}
+// Three sums.
+__device__ __forceinline__ void blk_sum3(BlockRed &R, int32_t v1, int32_t v2, int32_t v3, int32_t &t1, int32_t &t2,
+                                         int32_t &t3) {
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int32_t s1 = readlane_i(wave_incl_sum_i32(v1), 63), s2 = readlane_i(wave_incl_sum_i32(v2), 63),
+                  s3 = readlane_i(wave_incl_sum_i32(v3), 63);
+    if ((threadIdx.x & 63) == 0) { R.a[w] = s1; R.b[w] = s2; R.c[w] = s3; }
+    __syncthreads();
+    t1 = t2 = t3 = 0;
+    for (int i = 0; i < nw; ++i) { t1 += R.a[i]; t2 += R.b[i]; t3 += R.c[i]; }
+    __syncthreads();
+}
+__device__ __forceinline__ int32_t blk_max(BlockRed &R, int32_t v) {
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int32_t m = wave_max_i32(v);
+    if ((threadIdx.x & 63) == 0) R.a[w] = m;
+    __syncthreads();
+    int32_t r = INT32_MIN;
+    for (int i = 0; i < nw; ++i) r = max(r, R.a[i]);
+    __syncthreads();
+    return r;
+}
+// The first thread with b (INT32_MAX: none).
+__device__ __forceinline__ int32_t blk_first(BlockRed &R, bool b) {
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const unsigned long long bal = __ballot(b);
+    if ((threadIdx.x & 63) == 0) R.a[w] = bal ? w * 64 + (int)__builtin_ctzll(bal) : INT32_MAX;
+    __syncthreads();
+    int32_t r = INT32_MAX;
+    for (int i = 0; i < nw; ++i) r = min(r, R.a[i]);
+    __syncthreads();
+    return r;
+}
+// Inclusive prefix maximum of the threads' keys.
+__device__ __forceinline__ void blk_key_prefix_max(BlockRed &R, LKey &k) {
+    const int w = threadIdx.x >> 6;
+    int32_t p = 0;
+    wave_key_prefix_max(k, p);
+    if ((threadIdx.x & 63) == 63) { R.x[w] = k.x; R.g[w] = k.g; R.a[w] = k.l; }
+    __syncthreads();
+    LKey c{-INFINITY, -INFINITY, INT32_MIN};
+    for (int i = 0; i < w; ++i) {
+        const LKey o{R.x[i], R.g[i], R.a[i]};
+        if (key_gt(o, c)) c = o;
+    }
+    if (key_gt(c, k)) k = c;
+    __syncthreads();
+}
+
+// One new edge (key c, slot sl) before the first entry it sorts before
+// (3663-3667), else at the tail (thread q: entry q).
+__device__ void insert_one_b(const SlotLds &S, BlockRed &R, int &m, const LKey &c, int32_t sl) {
+    const int q = threadIdx.x;
+    bool b = false;
+    if (q < m) {
+        const int32_t e = S.idx[q];
+        const float x = S.st[e].X, g = S.st[e].G;
+        b = c.x < x || (c.x == x && (c.g < g || (c.g == g && c.l < S.st[e].Left)));
+    }
+    const int p = min(blk_first(R, b), m);
+    const bool mv = q >= p && q < m;  // entries [p, m) move up one
+    const int32_t v = mv ? S.idx[q] : 0;
+    __syncthreads();
+    if (mv) S.idx[q + 1] = v;
+    if (q == 0) S.idx[p] = sl;
+    __syncthreads();
     ++m;
 }
 
-// insert_batch on the slot list for k <= 64 new edges whose keys and slots
-// lane t holds (kc, rs).
-__device__ void insert_batch_s(const SlotLds &S, int &m, int k, const LKey &kc, int32_t rs,
-                               unsigned long long *wp = nullptr) {
-    const int lane = threadIdx.x & 63;
-    const bool mine = lane < k;
-    unsigned long long tq = PRK_WT();
-#define PRK_WQ(i)                                                       \
-    if (PRK_WPROF && wp) {                                              \
-        const unsigned long long t_ = PRK_WT();                         \
-        wp[i] += t_ - tq;                                               \
-        tq = t_;                                                        \
-    }
-    // 1. PM(q) = the maximum key of entries [0, q], its (x, g, l) in (nb, bk, aux);
-    //    two chunks per step (two independent lane scans in flight)
+// The k new edges of the batch (S.nk*[0, k), in insertion order, no NaN key)
+// inserted at once with the result of inserting them one by one (see
+// insert_batch: each new edge lands at its gap + the new edges of earlier
+// gaps + those of its gap ordered before it; entry q moves up by the new
+// edges of gaps <= q).  Thread q: entry q and new edge q.
+__device__ void insert_batch_b(const SlotLds &S, BlockRed &R, int &m, int k) {
+    const int q = threadIdx.x;
+    const bool mine = q < k;
+    // 1. PM(q) = the maximum key of entries [0, q], its (x, g, l) in (nb, bk, aux)
     float *pmx = reinterpret_cast<float *>(S.nb), *pmg = reinterpret_cast<float *>(S.bk);
     {
-        LKey ck{-INFINITY, -INFINITY, INT32_MIN};
-        for (int b0 = 0; b0 < m; b0 += 128) {
-            const int q0 = b0 + lane, q1 = b0 + 64 + lane;
-            LKey k0{-INFINITY, -INFINITY, INT32_MIN}, k1{-INFINITY, -INFINITY, INT32_MIN};
-            int32_t p0 = 0, p1 = 0;
-            if (q0 < m) k0 = S.key(S.idx[q0]);
-            if (q1 < m) k1 = S.key(S.idx[q1]);
-            wave_key_prefix_max(k0, p0);
-            wave_key_prefix_max(k1, p1);
-            if (key_gt(ck, k0)) k0 = ck;
-            const LKey c0{readlane_f(k0.x, 63), readlane_f(k0.g, 63), readlane_i(k0.l, 63)};
-            if (key_gt(c0, k1)) k1 = c0;
-            if (q0 < m) { pmx[q0] = k0.x; pmg[q0] = k0.g; S.aux[q0] = k0.l; }
-            if (q1 < m) { pmx[q1] = k1.x; pmg[q1] = k1.g; S.aux[q1] = k1.l; }
-            ck = LKey{readlane_f(k1.x, 63), readlane_f(k1.g, 63), readlane_i(k1.l, 63)};
-        }
+        LKey kk{-INFINITY, -INFINITY, INT32_MIN};
+        if (q < m) kk = S.key(S.idx[q]);
+        blk_key_prefix_max(R, kk);
+        if (q < m) { pmx[q] = kk.x; pmg[q] = kk.g; S.aux[q] = kk.l; }
     }
-    wave_lds_sync();
-    PRK_WQ(0)
-    int gq = 0;  // 2. the gap of new edge `lane`: binary search over the non-decreasing PM
+    __syncthreads();
+    // 2. the gap of new edge q: binary search over the non-decreasing PM
+    LKey kc{0.0f, 0.0f, 0};
+    int32_t rs = 0, gq = 0;
     if (mine) {
+        kc = LKey{S.nkx[q], S.nkg[q], S.nkl[q]};
+        rs = S.nks[q];
         int lo = 0, hi = m;
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
@@ -1273,111 +1349,49 @@ __device__ void insert_batch_s(const SlotLds &S, int &m, int k, const LKey &kc, 
         }
         gq = lo;
     }
-    wave_lds_sync();
-    PRK_WQ(1)
-    // 3. gap histogram, each new edge's arrival slot in its gap
-    for (int q = lane; q < m + 2; q += 64) S.aux[q] = 0;
-    wave_lds_sync();
+    __syncthreads();
+    // 3. gap histogram (aux[0, m + 2)), each new edge's arrival slot in its gap
+    if (q < m + 2) S.aux[q] = 0;
+    __syncthreads();
     int32_t arr = 0;
     if (mine) arr = atomicAdd(&S.aux[gq], 1);
-    wave_lds_sync();
+    __syncthreads();
     {  // 4. exclusive scan: aux[g] = new edges of gaps < g
-        int32_t carry = 0;
-        for (int b0 = 0; b0 < m + 2; b0 += 64) {
-            const int q = b0 + lane;
-            const int32_t v = q < m + 2 ? S.aux[q] : 0;
-            const int32_t inc = wave_incl_sum_i32(v);
-            if (q < m + 2) S.aux[q] = carry + inc - v;
-            carry += readlane_i(inc, 63);
-        }
+        const int32_t v = q < m + 2 ? S.aux[q] : 0;
+        int32_t tot;
+        const int32_t ex = blk_excl_sum(R, v, tot);
+        if (q < m + 2) S.aux[q] = ex;
     }
-    wave_lds_sync();
+    __syncthreads();
     int32_t s0 = 0, h = 0;
     if (mine) {  // 5. the new edges grouped by gap
         s0 = S.aux[gq];
         h = S.aux[gq + 1] - s0;
-        S.bk2[s0 + arr] = lane;
+        S.bk2[s0 + arr] = q;
     }
-    wave_lds_sync();
-    PRK_WQ(2)
+    const int32_t hmax = blk_max(R, h);
     // 6. final positions: gap + new edges of earlier gaps + those of its gap
     //    ordered before it (smaller key, or an equal key inserted earlier)
     int32_t r = 0;
-    const int32_t hmax = wave_max_i32(h);
     for (int32_t j = 0; j < hmax; ++j) {
-        const int32_t u = j < h ? S.bk2[s0 + j] : lane;
-        const LKey ku{__shfl(kc.x, u), __shfl(kc.g, u), __shfl(kc.l, u)};
-        if (j < h && u != lane) r += (key_gt(kc, ku) || (!key_gt(ku, kc) && u < lane)) ? 1 : 0;
-    }
-    const int32_t at = gq + s0 + r;
-    PRK_WQ(3)
-    // 7. entries move up by the new edges of gaps <= their position, top chunk first
-    for (int top = m; top > 0; top -= 64) {
-        const int q = top - 1 - lane;
-        int32_t v = 0, to = 0;
-        if (q >= 0) {
-            to = q + S.aux[q + 1];
-            v = S.idx[q];
-        }
-        wave_lds_sync();
-        if (q >= 0 && to != q) S.idx[to] = v;
-        wave_lds_sync();
-    }
-    if (mine) S.idx[at] = rs;  // 8.
-    wave_lds_sync();
-    PRK_WQ(4)
-#undef PRK_WQ
-    m += k;
-}
-
-// insert_batch_s for a few new edges (k <= kSmallBatch): each gap counted
-// by ballots over the list's prefix maxima (registers, no LDS search), the
-// ranks among the new edges by broadcasts, then one top-down move.
-constexpr int kSmallBatch = 8;
-__device__ void insert_small_s(const SlotLds &S, int &m, int k, const LKey &kc, int32_t rs) {
-    const int lane = threadIdx.x & 63;
-    int32_t gap = 0;  // lane t < k: the gap of new edge t = #{q : PM(q) <= key(t)}
-    {
-        LKey ck{-INFINITY, -INFINITY, INT32_MIN};
-        for (int b0 = 0; b0 < m; b0 += 64) {
-            const int q = b0 + lane;
-            LKey kk{-INFINITY, -INFINITY, INT32_MIN};
-            int32_t kp = 0;
-            if (q < m) kk = S.key(S.idx[q]);
-            wave_key_prefix_max(kk, kp);
-            if (key_gt(ck, kk)) kk = ck;
-            for (int t = 0; t < k; ++t) {
-                const LKey kt{readlane_f(kc.x, t), readlane_f(kc.g, t), readlane_i(kc.l, t)};
-                const int c = __popcll(__ballot(q < m && !key_gt(kk, kt)));
-                if (lane == t) gap += c;
+        if (j < h) {
+            const int32_t u = S.bk2[s0 + j];
+            if (u != q) {
+                const LKey ku{S.nkx[u], S.nkg[u], S.nkl[u]};
+                r += (key_gt(kc, ku) || (!key_gt(ku, kc) && u < q)) ? 1 : 0;
             }
-            const int last = min(63, m - 1 - b0);
-            ck.x = readlane_f(kk.x, last);
-            ck.g = readlane_f(kk.g, last);
-            ck.l = readlane_i(kk.l, last);
         }
     }
-    int32_t at = gap;  // + the new edges ordered before it: smaller gap, key, or insertion
-    for (int u = 0; u < k; ++u) {
-        const int32_t gu = readlane_i(gap, u);
-        const LKey ku{readlane_f(kc.x, u), readlane_f(kc.g, u), readlane_i(kc.l, u)};
-        const bool before = gu < gap || (gu == gap && (key_gt(kc, ku) || (!key_gt(ku, kc) && u < lane)));
-        at += (u != lane && before) ? 1 : 0;
+    // 7. entries move up by the new edges of gaps <= their position; 8. the new edges
+    int32_t v = 0, to = 0;
+    if (q < m) {
+        to = q + S.aux[q + 1];
+        v = S.idx[q];
     }
-    // entries move up by the new edges of gaps <= their position, top chunk first
-    for (int top = m; top > 0; top -= 64) {
-        const int q = top - 1 - lane;
-        int32_t v = 0, to = q;
-        if (q >= 0) {
-            v = S.idx[q];
-            for (int t = 0; t < k; ++t) to += readlane_i(gap, t) <= q ? 1 : 0;
-        }
-        wave_lds_sync();
-        if (q >= 0 && to != q) S.idx[to] = v;
-        wave_lds_sync();
-    }
-    if (lane < k) S.idx[at] = rs;
-    wave_lds_sync();
+    __syncthreads();
+    if (q < m) S.idx[to] = v;
+    if (mine) S.idx[gq + s0 + r] = rs;
+    __syncthreads();
     m += k;
 }
 
@@ -1485,175 +1499,158 @@ __global__ void k_span_finish(FrameParams fp, const PairRaw *__restrict__ raw, u
     } while (0)
 
 template <int M>
-__device__ void walk_object_slots(const FrameParams &fp, const ObjDesc &od, const DrawRec &d,
-                                  const ObjEdge *__restrict__ E, uint32_t n, int32_t MaxY, uint32_t base,
-                                  uint32_t bound, const SlotLds &S, uint32_t cap, PairRaw *__restrict__ raw,
-                                  SpanPos *__restrict__ pos, uint32_t *__restrict__ span_tri,
-                                  uint32_t *__restrict__ err) {
+__device__ void walk_object_block(const FrameParams &fp, const ObjDesc &od, const ObjEdge *__restrict__ E,
+                                  uint32_t n, int32_t MaxY, uint32_t base, uint32_t bound, const SlotLds &S,
+                                  BlockRed &R, uint32_t cap, PairRaw *__restrict__ raw, SpanPos *__restrict__ pos,
+                                  uint32_t *__restrict__ span_tri, uint32_t *__restrict__ err) {
     constexpr bool kScalar = M != MODE_AVX;
-    const int lane = threadIdx.x & 63;
+    const int tid = threadIdx.x;
+    const uint32_t NT = blockDim.x;
     const int32_t RowLo = kScalar ? fp.row0 - 1 : fp.row0;
     unsigned long long wp[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const unsigned long long wt0 = PRK_WT();
-    for (uint32_t q = lane; q < cap; q += 64) S.fs[q] = (int32_t)q;
-    int top = (int)cap;  // free slots
-    wave_lds_sync();
-    // read-ahead windows: lane t holds sorted edge wb + t (A) and wb + 64 + t (B)
+    for (uint32_t q = tid; q < cap; q += NT) S.fs[q] = (int32_t)q;
+    int top = (int)cap;  // free slots (the same value in every thread, as every uniform below)
+    // read-ahead window: thread t holds sorted edge wb + t
     uint32_t wb = 0;
     PRK_WIN(wa);
-    PRK_WIN(wn);
-    PRK_WIN_LOAD(wa, E, (uint32_t)lane, n);
-    PRK_WIN_LOAD(wn, E, 64u + lane, n);
+    PRK_WIN_LOAD(wa, E, (uint32_t)tid, n);
     PRK_WIN_WAIT();
     PRK_WIN_LAUNDER(wa);
-    PRK_WIN_LAUNDER(wn);
     uint32_t emitted = 0;
     int m = 0;
     uint32_t ins = 0;
+    __syncthreads();
     for (int32_t Row = E[0].YMin; Row < MaxY; ++Row) {
         unsigned long long t0 = PRK_WT();
         if (PRK_WPROF) wp[3] += 1;
         // insertion (3654-3713): the edges with YMin == Row, in sorted order,
-        // a window's worth at a time (batches in order == one at a time)
+        // a window at a time (batches in order == one at a time)
         for (;;) {
-            if (ins == wb + 64) {
-                PRK_WIN_COPY(wa, wn);
-                wb += 64;
-                PRK_WIN_LOAD(wn, E, wb + 64 + lane, n);
+            if (ins == wb + NT) {
+                wb += NT;
+                PRK_WIN_LOAD(wa, E, wb + tid, n);
                 PRK_WIN_WAIT();
-                PRK_WIN_LAUNDER(wn);
+                PRK_WIN_LAUNDER(wa);
             }
             const float wx = wa0.x, wg = wa0.y;
             const int32_t wymin = __float_as_int(wa4.x), wl = __float_as_int(wa4.z);
-            const int rel = lane - (int)(ins - wb);
-            const unsigned long long lt = __ballot(rel >= 0 && wymin < Row);
+            const int rel = tid - (int)(ins - wb);
+            const bool eqr = rel >= 0 && wymin == Row;
+            int32_t lt, k, nanc;
+            blk_sum3(R, (rel >= 0 && wymin < Row) ? 1 : 0, eqr ? 1 : 0, (eqr && (wx != wx || wg != wg)) ? 1 : 0, lt,
+                     k, nanc);
             if (lt) {  // (never past the first row: entries below the row are skipped)
-                ins += (uint32_t)__popcll(lt);
+                ins += (uint32_t)lt;
                 continue;
             }
-            const unsigned long long eq = __ballot(rel >= 0 && wymin == Row);
-            const int k = __popcll(eq);
             if (k == 0) break;
-            const bool nw = rel >= 0 && rel < k;
-            int32_t slot = 0;
-            if (nw) {
-                slot = S.fs[top - 1 - rel];
+            if (rel >= 0 && rel < k) {  // the row's new edges take slots; their keys go to nk*
+                const int32_t slot = S.fs[top - 1 - rel];
                 PRK_WIN_STORE(&S.st[slot], wa);
+                S.nkx[rel] = wx;
+                S.nkg[rel] = wg;
+                S.nkl[rel] = wl;
+                S.nks[rel] = slot;
             }
-            const bool nan = __any(nw && (wx != wx || wg != wg));
             top -= k;
+            __syncthreads();
             if (PRK_WPROF) {
                 wp[8] += (unsigned long long)k;
-                wp[(k <= 2 || nan) ? 6 : (k <= kSmallBatch ? 5 : 4)] += 1;
+                wp[(k <= 2 || nanc) ? 6 : 4] += 1;
             }
-            if (k <= 2 || nan) {  // one at a time (any NaN key), 3654-3713
-                for (int t = 0; t < k; ++t) {
-                    const int sl = (int)(ins - wb) + t;
-                    insert_one_s(S, m, LKey{readlane_f(wx, sl), readlane_f(wg, sl), readlane_i(wl, sl)},
-                                 readlane_i(slot, sl));
-                }
-            } else {  // new edge `lane` in lane `lane` (a permute of the window's lanes)
-                const int src = min(63, (int)(ins - wb) + lane);
-                const LKey kn{__shfl(wx, src), __shfl(wg, src), __shfl(wl, src)};
-                if (k <= kSmallBatch) insert_small_s(S, m, k, kn, __shfl(slot, src));
-                else insert_batch_s(S, m, k, kn, __shfl(slot, src), PRK_WPROF ? wp + 9 : nullptr);
+            if (k <= 2 || nanc) {  // one at a time (any NaN key), 3654-3713
+                for (int t = 0; t < k; ++t)
+                    insert_one_b(S, R, m, LKey{S.nkx[t], S.nkg[t], S.nkl[t]}, S.nks[t]);
+            } else {
+                insert_batch_b(S, R, m, k);
             }
             ins += (uint32_t)k;
-            if (ins < wb + 64) break;  // the row's edges end inside the window
+            if (ins < wb + NT) break;  // the row's edges end inside the window
         }
         if (PRK_WPROF) { const unsigned long long t1 = PRK_WT(); wp[0] += t1 - t0; t0 = t1; }
         {  // expiry 3715-3749: keep entries with YMax > Row, in order; free the others' slots
-            int out = 0;
-            for (int c0 = 0; c0 < m; c0 += 64) {
-                const int q = c0 + lane;
-                int32_t e = 0;
-                bool keep = false;
-                if (q < m) {
-                    e = S.idx[q];
-                    keep = !(S.st[e].YMax <= Row);
-                }
-                const bool gone = q < m && !keep;
-                const unsigned long long bal = __ballot(keep), gbal = __ballot(gone);
-                wave_lds_sync();
-                if (keep) S.idx[out + lane_rank(bal)] = e;
-                if (gone) S.fs[top + lane_rank(gbal)] = e;
-                wave_lds_sync();
-                out += __popcll(bal);
-                top += __popcll(gbal);
+            int32_t e = 0;
+            bool keep = false;
+            if (tid < m) {
+                e = S.idx[tid];
+                keep = !(S.st[e].YMax <= Row);
             }
-            m = out;
+            const bool gone = tid < m && !keep;
+            int32_t kp, gp, kt, gt;
+            blk_excl_sum2(R, keep ? 1 : 0, gone ? 1 : 0, kp, gp, kt, gt);
+            if (keep) S.idx[kp] = e;
+            if (gone) S.fs[top + gp] = e;
+            m = kt;
+            top += gt;
+            __syncthreads();
         }
         if (PRK_WPROF) { const unsigned long long t1 = PRK_WT(); wp[1] += t1 - t0; t0 = t1; }
         if (m == 0) {  // nothing happens on the rows before the next insertion: go there
             if (ins >= n) break;
-            const int32_t ny = ins < wb + 64 ? readlane_i(__float_as_int(wa4.x), (int)(ins - wb))
-                                             : readlane_i(__float_as_int(wn4.x), 0);
-            Row = max(Row, ny - 1);
+            Row = max(Row, E[ins].YMin - 1);
             continue;
         }
-        const int P = m / 2;  // pairing 3751-3869
-        int32_t ci = 0;  // the previous chunk's last second entry (carried) and its X
-        float cx = 0;
-        for (int k0 = 0; k0 < P; k0 += 64) {
-            const int kk = k0 + lane;
-            const bool valid = kk < P;
-            int32_t i0 = 0, i1 = 0;
-            if (valid) {
-                i0 = S.idx[2 * kk];
-                i1 = S.idx[2 * kk + 1];
+        const int P = m / 2;  // pairing 3751-3869: thread k holds pair k
+        const bool valid = tid < P;
+        const bool emit = Row >= RowLo;  // every pair of the pass's rows takes a slot (k_span_finish sets it up)
+        int32_t i0 = 0, i1 = 0;
+        float x0 = 0.0f, x1 = 0.0f;
+        if (valid) {
+            i0 = S.idx[2 * tid];
+            i1 = S.idx[2 * tid + 1];
+            const uint32_t j = emitted + (uint32_t)tid;
+            const bool w = emit && j < bound;
+            if (emit && j >= bound) atomicOr(err, 2u);  // (never: the bound holds every pair)
+            const uint32_t at = base + j;
+            ObjEdge a = S.st[i0];  // left edge: its values at the row, then its step (3811-3829)
+            if (w) {
+                raw[at].l0 = make_float4(a.X, a.Z, a.W, a.U);
+                raw[at].l1 = make_float4(a.V, a.N0, a.N1, a.N2);
+                raw[at].l2 = make_float4(a.C0, a.C1, a.C2, a.C3);
             }
-            ObjEdge a = S.st[i0], b = S.st[i1];  // (slot 0 for lanes past the pairs: unused)
-            // every pair of the pass's rows takes a slot, its span set up later (k_span_finish)
-            const bool em = valid && Row >= RowLo;
-            const unsigned long long bal = __ballot(em);
-            if (em) {
-                const uint32_t j = emitted + (uint32_t)lane_rank(bal);
-                if (j < bound) {
-                    const uint32_t at = base + j;
-                    PairRaw pr;
-                    pair_raw_out(a, b, pr);
-                    raw[at] = pr;
-                    pos[at] = SpanPos{Row, (int32_t)od.draw, 0, SPAN_RAW};
-                    span_tri[at] = od.g0;
-                } else {
-                    atomicOr(err, 2u);  // (never: the bound holds every pair)
-                }
+            obj_step<M>(a);
+            S.st[i0] = a;
+            x0 = a.X;
+            ObjEdge b = S.st[i1];  // right edge
+            if (w) {
+                raw[at].r0 = make_float4(b.X, b.Z, b.W, b.U);
+                raw[at].r1 = make_float4(b.V, b.N0, b.N1, b.N2);
+                raw[at].r2 = make_float4(b.C0, b.C1, b.C2, b.C3);
+                pos[at] = SpanPos{Row, (int32_t)od.draw, 0, SPAN_RAW};
+                span_tri[at] = od.g0;
             }
-            emitted += (uint32_t)__popcll(bal);
-            float x0 = 0, x1 = 0;
-            if (valid) {  // 3811-3829
-                obj_step<M>(a);
-                obj_step<M>(b);
-                S.st[i0] = a;
-                S.st[i1] = b;
-                x0 = a.X;
-                x1 = b.X;
-                if (x0 > x1) {  // 3831-3841
-                    const int32_t t = i0; i0 = i1; i1 = t;
-                    const float f = x0; x0 = x1; x1 = f;
-                }
+            obj_step<M>(b);
+            S.st[i1] = b;
+            x1 = b.X;
+            if (x0 > x1) {  // 3831-3841
+                const int32_t t = i0; i0 = i1; i1 = t;
+                const float f = x0; x0 = x1; x1 = f;
             }
-            // 3843-3853: pair kk's first entry against pair kk-1's second
-            // (lane 0: the carried entry)
-            const int32_t pi = dpp_i<kDppWaveShr1>(ci, i1);
-            const float px = dpp_f<kDppWaveShr1>(cx, x1);
-            const bool sw = valid && kk >= 1 && px > x0;
-            const bool swn = dpp_i<kDppWaveShl1>(0, sw ? 1 : 0) != 0;  // the next pair's swap takes my second
-            const int32_t ni = dpp_i<kDppWaveShl1>(0, i0);
-            const bool defer = lane == 63 && kk + 1 < P;  // my second waits for the next chunk
-            if (valid) {
-                const int q0 = 2 * kk;
-                if (lane == 0 && kk >= 1) S.idx[q0 - 1] = sw ? i0 : pi;  // the carried slot's position
-                S.idx[q0] = sw ? pi : i0;
-                if (!defer) S.idx[q0 + 1] = swn ? ni : i1;
-            }
-            ci = readlane_i(i1, 63);
-            cx = readlane_f(x1, 63);
+            // pair k's entries after its first swap, for its neighbours
+            S.nb[tid] = i0;
+            S.bk[tid] = __float_as_int(x0);
+            S.aux[tid] = i1;
+            S.bk2[tid] = __float_as_int(x1);
         }
-        wave_lds_sync();
+        __syncthreads();
+        if (valid) {  // 3843-3853: pair k's first entry against pair k-1's second
+            const bool sw = tid >= 1 && __int_as_float(S.bk2[tid - 1]) > x0;
+            const bool swn = tid + 1 < P && x1 > __int_as_float(S.bk[tid + 1]);  // pair k+1's swap takes my second
+            const int32_t nf = sw ? S.aux[tid - 1] : i0, ns = swn ? S.nb[tid + 1] : i1;
+            i0 = nf;
+            i1 = ns;
+        }
+        __syncthreads();
+        if (valid) {
+            S.idx[2 * tid] = i0;
+            S.idx[2 * tid + 1] = i1;
+        }
+        if (emit) emitted += (uint32_t)P;
+        __syncthreads();
         if (PRK_WPROF) wp[2] += PRK_WT() - t0;
     }
-    if (PRK_WPROF && lane == 0) {
+    if (PRK_WPROF && tid == 0) {
         wp[7] = PRK_WT() - wt0;
         for (int k = 0; k < 14; ++k) atomicAdd(fp.prof + k, wp[k]);
     }
@@ -1692,12 +1689,13 @@ __device__ int32_t obj_max_active(const ObjEdge *__restrict__ E, uint32_t n, int
     return best;
 }
 
-// One wave per large object: everything in LDS (walk_object_slots, lcap
-// slots) when its most active entries fit, else its list in its pool slice pool + big_off[blockIdx.x]
-// (kWaveListArrays arrays of big_cap[blockIdx.x] + 2 ints, big_cap >= its
-// edge count).
+// One workgroup per large object (slot_threads(lcap) threads): everything
+// in LDS (walk_object_block, lcap slots) when its most active entries fit,
+// else its first wave walks it with the list in its pool slice
+// pool + big_off[blockIdx.x] (kWaveListArrays arrays of big_cap[blockIdx.x]
+// + 2 ints, big_cap >= its edge count) and the other waves leave.
 template <int M>
-__global__ void __launch_bounds__(64) k_obj_walk_wave(FrameParams fp, const ObjDesc *__restrict__ objs,
+__global__ void __launch_bounds__(kSlotMaxThreads) k_obj_walk_wave(FrameParams fp, const ObjDesc *__restrict__ objs,
                                                       const uint32_t *__restrict__ big,
                                                       const unsigned long long *__restrict__ big_off,
                                                       const uint32_t *__restrict__ big_cap, int32_t *__restrict__ pool,
@@ -1708,6 +1706,8 @@ __global__ void __launch_bounds__(64) k_obj_walk_wave(FrameParams fp, const ObjD
                                                       PairRaw *__restrict__ raw, SpanPos *__restrict__ pos,
                                                       uint32_t *__restrict__ span_tri, uint32_t *__restrict__ err) {
     extern __shared__ int32_t lds_list[];
+    __shared__ BlockRed R;
+    __shared__ int32_t most_s;
     const uint32_t o = big[blockIdx.x];
     const ObjDesc od = objs[o];
     const DrawRec &d = fp.draws[od.draw];
@@ -1715,25 +1715,30 @@ __global__ void __launch_bounds__(64) k_obj_walk_wave(FrameParams fp, const ObjD
     uint32_t e0, n;
     obj_range(od, escan, *total0p, e0, n);
     ObjEdge *E = work + e0;
-    if (n == 0) return;
+    if (n == 0) return;  // (the whole workgroup)
     int32_t mr = INT32_MIN;
-    for (uint32_t i = threadIdx.x; i < n; i += 64) mr = max(mr, E[i].YMax);
-    const int32_t MaxY = min(min(wave_max_i32(mr), fp.H), fp.row1);
-    const int32_t most = obj_max_active(E, n, E[0].YMin, MaxY, lds_list, (uint32_t)(slot_lds_bytes(lcap) / 4));
-    const bool gl = most > (int32_t)lcap;
-    if (gl && n > big_cap[blockIdx.x]) {  // (the host sizes every slice by the object's edges)
-        if (threadIdx.x == 0) atomicOr(err, 1u);
-        return;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) mr = max(mr, E[i].YMax);
+    const int32_t MaxY = min(min(blk_max(R, mr), fp.H), fp.row1);
+    if (threadIdx.x < 64) {  // the first wave counts the most active entries
+        const int32_t most =
+            obj_max_active(E, n, E[0].YMin, MaxY, lds_list, (uint32_t)(slot_lds_bytes(lcap) / 4));
+        if (threadIdx.x == 0) most_s = most;
     }
-    if (gl) {
+    __syncthreads();
+    if (most_s > (int32_t)lcap) {  // the list in device memory, one wave
+        if (threadIdx.x >= 64) return;
+        if (n > big_cap[blockIdx.x]) {  // (the host sizes every slice by the object's edges)
+            if (threadIdx.x == 0) atomicOr(err, 1u);
+            return;
+        }
         WaveList L;
         L.carve(pool + big_off[blockIdx.x], big_cap[blockIdx.x]);
         walk_object_wave<M, true>(fp, od, d, E, n, base, bound, L, recs, srecs, pos, span_tri, err);
-    } else {
-        SlotLds S;
-        S.carve(lds_list, lcap);
-        walk_object_slots<M>(fp, od, d, E, n, MaxY, base, bound, S, lcap, raw, pos, span_tri, err);
+        return;
     }
+    SlotLds S;
+    S.carve(lds_list, lcap, blockDim.x);
+    walk_object_block<M>(fp, od, E, n, MaxY, base, bound, S, R, lcap, raw, pos, span_tri, err);
 }
 
 // The tiles of a span: those of its row its [minx, min(maxx, W)) crosses and,
@@ -1858,9 +1863,9 @@ hipError_t prk_obj_bound(const prk::FrameParams *fp, const void *objs, uint32_t 
                        reinterpret_cast<const prk::EdgeIn *>(edges_in), bound);
     return hipGetLastError();
 }
-// The LDS capacity of the one-wave walk on the current device (listed edges;
-// 0: every wave walk keeps its list in device memory): the largest of 1024,
-// 512, 256 whose slot_lds_bytes the device grants as dynamic LDS.
+// The LDS capacity of the workgroup walk on the current device (listed edges;
+// 0: every walk keeps its list in device memory): the largest of 1022, 510,
+// 254 whose slot_lds_bytes the device grants as dynamic LDS.
 uint32_t prk_obj_walk_lcap(void) {
     static std::atomic<int> cap[64];  // per device: 0 unknown, else cap + 1
     int dev = -1;
@@ -1868,7 +1873,7 @@ uint32_t prk_obj_walk_lcap(void) {
     int c = cap[dev].load();
     if (c == 0) {
         c = 1;
-        for (uint32_t k = prk::kSlotCapLds; k >= 256; k /= 2) {
+        for (uint32_t k = prk::kSlotCapLds; k >= 254; k = (k + 2) / 2 - 2) {
             const size_t bytes = prk::slot_lds_bytes(k);
             const void *fn[prk::MODE_COUNT] = {
                 reinterpret_cast<const void *>(&prk::k_obj_walk_wave<prk::MODE_AVX>),
@@ -1909,13 +1914,14 @@ hipError_t prk_obj_walk(const prk::FrameParams *fp, const void *objs, uint32_t n
                        reinterpret_cast<const prk::SpanIn *>(spans_in), err);
     hipError_t e = hipGetLastError();
     const size_t bytes = prk::slot_lds_bytes(lcap);
+    const uint32_t nt = prk::slot_threads(lcap);
     uint32_t b0 = 0;
     for (int mo = 0; mo < prk::MODE_COUNT && e == hipSuccess; ++mo) {
         const uint32_t nb = nbig[mo];
         if (nb == 0) continue;
 #define PRK_WALK_WAVE(MM)                                                                                           \
     case MM:                                                                                                        \
-        hipLaunchKernelGGL(prk::k_obj_walk_wave<MM>, dim3(nb), dim3(64), bytes, s, *fp,                            \
+        hipLaunchKernelGGL(prk::k_obj_walk_wave<MM>, dim3(nb), dim3(nt), bytes, s, *fp,                            \
                            reinterpret_cast<const prk::ObjDesc *>(objs), big + b0, big_off + b0, big_cap + b0, pool, \
                            lcap, escan, total0p, reinterpret_cast<prk::ObjEdge *>(work), soff,                      \
                            reinterpret_cast<prk::SpanRecG *>(recs), reinterpret_cast<prk::ScSpanRecG *>(srecs),     \

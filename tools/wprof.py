@@ -28,12 +28,10 @@ for name, s, sem, phong, tpo in T.cases():
             r.synchronize()
         c = [int(x) for x in r.debug_counters(16)]
         rows = max(1, c[3])
-        print("%s: rows %d new edges %d batches %d small %d one-at-a-time %d | cycles per row: insert %.0f "
-              "expiry %.0f pair %.0f (walk total %.0f, %.1f us at 100 MHz memtime? / core clock)"
-              % (name, c[3], c[8], c[4], c[5], c[6], c[0] / rows, c[1] / rows, c[2] / rows, c[7] / rows,
-                 c[7] / 1e2), flush=True)
-        nb = max(1, c[4])
-        print("   insert_batch_s cycles per call: prefix max %.0f, gap search %.0f, histogram+scan %.0f, "
-              "ranks %.0f, moves %.0f" % tuple(c[9 + i] / nb for i in range(5)), flush=True)
+        print("%s: rows %d new edges %d batches %d one-at-a-time %d | clocks per row (s_memtime): insert %.0f "
+              "expiry %.0f pair %.0f, walk %.0f per row, %.0f in all"
+              % (name, c[3], c[8], c[4], c[6], c[0] / rows, c[1] / rows, c[2] / rows, c[7] / rows, c[7]),
+              flush=True)
+
     finally:
         r.close()
