@@ -54,10 +54,16 @@ hipError_t prk_obj_gather(const void *, const uint32_t *, const uint32_t *, cons
 hipError_t prk_obj_bound(const prk::FrameParams *, const void *, uint32_t, const unsigned long long *, const void *,
                          unsigned long long *, hipStream_t);
 uint32_t prk_obj_walk_lcap(void);
-hipError_t prk_obj_walk(const prk::FrameParams *, const void *, uint32_t, const uint32_t *, const uint32_t *, uint32_t,
-                        const unsigned long long *, const uint32_t *, int32_t *, const uint32_t *, const uint32_t *,
-                        void *, const unsigned long long *, void *, void *, void *, void *, uint32_t *,
-                        const void *, uint32_t *, hipStream_t);
+hipError_t prk_obj_walk(const prk::FrameParams *, const void *, uint32_t, const uint32_t *, const uint32_t *, void *,
+                        const unsigned long long *, void *, void *, void *, uint32_t *, const void *, uint32_t *,
+                        hipStream_t);
+hipError_t prk_obj_maxact(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, const uint32_t *,
+                          const uint32_t *, const void *, int32_t *, hipStream_t);
+uint32_t prk_obj_walk_threads(uint32_t);
+hipError_t prk_obj_walk_group(const prk::FrameParams *, int32_t, uint32_t, const void *, const uint32_t *,
+                              const unsigned long long *, const uint32_t *, uint32_t, int32_t *, const uint32_t *,
+                              const uint32_t *, void *, const unsigned long long *, void *, void *, void *, void *,
+                              uint32_t *, uint32_t *, hipStream_t);
 hipError_t prk_span_finish(const prk::FrameParams *, const void *, uint32_t, void *, void *, void *, hipStream_t);
 hipError_t prk_scan_u32(const uint32_t *, uint32_t *, uint32_t, void *, size_t *, hipStream_t);
 hipError_t prk_scan_u64(const unsigned long long *, unsigned long long *, uint32_t, void *, size_t *, hipStream_t);
@@ -135,6 +141,8 @@ struct Texture {
 
 int status_of(hipError_t e) {
     if (e == hipSuccess) return PRK_OK;
+    static const bool trace = std::getenv("PRK_TRACE_HIP") != nullptr;  // diagnostics: name the HIP error
+    if (trace) std::fprintf(stderr, "prk: HIP error %d (%s)\n", (int)e, hipGetErrorName(e));
     if (e == hipErrorOutOfMemory) return PRK_ERR_NOMEM;
     return PRK_ERR_DEVICE;
 }
@@ -251,7 +259,7 @@ struct prk_context {
     struct SpanScratch {
         DevBuf d_stage, d_edges, d_ord, d_temp, d_recs, d_pos, d_span_tri, d_scnt, d_soff, d_keys_a, d_vals_a,
             d_keys_b, d_vals_b, d_offs, d_nwin, d_wtag, d_srecs, d_work, d_ekeys, d_ekeys2, d_evals, d_ecnt, d_escan,
-            d_rcnt, d_rscan, d_bound, d_oslot, d_pool, d_err, d_raw;
+            d_rcnt, d_rscan, d_bound, d_oslot, d_pool, d_err, d_raw, d_most, d_cls;
         // the pass's host tables, packed into pinned memory for one upload
         // (stage_ev: that upload, before the staging is rewritten)
         char *h_stage = nullptr;
@@ -265,6 +273,8 @@ struct prk_context {
         std::vector<prk::DrawRec> h_draws;
         std::vector<prk::TexRec> h_texs;
         uint32_t *h_rb = nullptr;  // pinned readback words
+        char *h_cls = nullptr;     // pinned: the large objects' most active entries, then their walk groups
+        size_t cls_cap = 0;
     } spans;
 };
 
@@ -394,7 +404,7 @@ int prk_destroy(prk_context *c) {
                         &S.d_soff, &S.d_keys_a, &S.d_vals_a, &S.d_keys_b, &S.d_vals_b, &S.d_offs, &S.d_nwin,
                         &S.d_wtag, &S.d_srecs, &S.d_work, &S.d_ekeys, &S.d_ekeys2, &S.d_evals, &S.d_ecnt,
                         &S.d_escan, &S.d_rcnt, &S.d_rscan, &S.d_bound, &S.d_oslot, &S.d_pool, &S.d_err,
-                        &S.d_raw};
+                        &S.d_raw, &S.d_most, &S.d_cls};
         for (DevBuf *b : sb) b->release();
         if (S.h_rb) (void)hipHostFree(S.h_rb);
         if (S.stage_ev) {
@@ -402,6 +412,7 @@ int prk_destroy(prk_context *c) {
             (void)hipEventDestroy(S.stage_ev);
         }
         if (S.h_stage) (void)hipHostFree(S.h_stage);
+        if (S.h_cls) (void)hipHostFree(S.h_cls);
     }
     if (c->s_mark) (void)hipEventDestroy(c->s_mark);
     if (c->in_ev) (void)hipEventDestroy(c->in_ev);
@@ -1453,7 +1464,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     S.h_big_off.clear();
     S.h_big_cap.clear();
     S.h_k1src.clear();
-    uint64_t ntri = 0, nk1 = 0, pool = 0, maxn = 1, maxwave = 0;
+    uint64_t ntri = 0, nk1 = 0, pool = 0, maxn = 1;
     std::vector<uint32_t> bigm[prk::MODE_COUNT], bige[prk::MODE_COUNT];  // wave-walked objects by mode, their edges
     for (uint32_t di = 0; di < draws.size(); ++di) {
         const prk::DrawRec &d = draws[di];
@@ -1472,7 +1483,6 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
                 maxn = std::max(maxn, edges);
                 const bool wave = n >= kObjWaveTris;
                 if (wave) {
-                    maxwave = std::max(maxwave, edges);
                     bigm[d.mode].push_back((uint32_t)S.h_objs.size());
                     bige[d.mode].push_back((uint32_t)edges);
                 }
@@ -1483,21 +1493,12 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
             }
         }
     }
-    uint32_t nbig[prk::MODE_COUNT];
-    for (int mo = 0; mo < prk::MODE_COUNT; ++mo) {  // one wave launch per mode, each object a pool slice
-        nbig[mo] = (uint32_t)bigm[mo].size();
-        for (size_t i = 0; i < bigm[mo].size(); ++i) {
-            S.h_big_gl.push_back(bigm[mo][i]);
-            S.h_big_off.push_back(pool);
-            S.h_big_cap.push_back(bige[mo][i]);
-            pool += (uint64_t)kWaveListArrays * (bige[mo][i] + 2);
-        }
-    }
+    for (int mo = 0; mo < prk::MODE_COUNT; ++mo)  // the large objects, by mode (their walk groups: after the readback)
+        for (size_t i = 0; i < bigm[mo].size(); ++i) S.h_big_gl.push_back(bigm[mo][i]);
     // edge slots (3 per triangle + the caller edges) are indexed by 31 bits
     if (3 * ntri + nk1 >= 0x7FFFFFFFull) return PRK_ERR_LIMIT;
     const uint32_t nobj = (uint32_t)S.h_objs.size(), nk0 = (uint32_t)S.h_k0obj.size();
-    const uint32_t nt = (uint32_t)ntri, ngl = (uint32_t)S.h_big_gl.size();
-    const uint32_t wcap = (uint32_t)std::min<uint64_t>(lcap, maxwave);  // the wave walk's LDS list capacity
+    const uint32_t nt = (uint32_t)ntri, nbig_all = (uint32_t)S.h_big_gl.size();
     // MergeSort key: (object, min(YMin, H), recursion path) in one radix sort
     auto bitlen = [](uint64_t v) { uint32_t b = 0; while (v) { ++b; v >>= 1; } return b; };
     const uint32_t pbits = bitlen(maxn) + 1, ybits = std::max(1u, bitlen((uint64_t)c->H));
@@ -1520,8 +1521,8 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
                     {S.h_k0obj.data(), S.h_k0obj.size() * 4, 0},
                     {S.h_k0tri0.data(), S.h_k0tri0.size() * 4, 0},
                     {S.h_big_gl.data(), S.h_big_gl.size() * 4, 0},
-                    {S.h_big_off.data(), S.h_big_off.size() * 8, 0},
-                    {S.h_big_cap.data(), S.h_big_cap.size() * 4, 0},
+                    {nullptr, 0, 0},
+                    {nullptr, 0, 0},
                     {S.h_k1src.data(), S.h_k1src.size() * 4, 0},
                     {c->pend_edges.data(), c->pend_edges.size() * sizeof(prk_edge), 0},
                     {c->pend_spans.data(), c->pend_spans.size() * sizeof(prk_span), 0}};
@@ -1545,7 +1546,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
         S.stage_cap = want;
     }
     for (const Part &pt : parts)
-        if (pt.bytes) std::memcpy(S.h_stage + pt.off, pt.src, pt.bytes);
+        if (pt.bytes && pt.src) std::memcpy(S.h_stage + pt.off, pt.src, pt.bytes);
     PRK_TRY(S.d_stage.ensure(stage_bytes));
     PRK_TRY(hipMemcpyAsync(S.d_stage.p, S.h_stage, stage_bytes, hipMemcpyHostToDevice, s));
     PRK_TRY(hipEventRecord(S.stage_ev, s));
@@ -1558,10 +1559,8 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     if (fp.draw0.tex >= 0 && (size_t)fp.draw0.tex < S.h_texs.size()) fp.tex0 = S.h_texs[fp.draw0.tex];
     void *d_objs = dev(T_OBJS), *d_edges_in = dev(T_EDGES), *d_spans_in = dev(T_SPANS);
     const uint32_t *d_k0obj = (const uint32_t *)dev(T_K0OBJ), *d_k0tri0 = (const uint32_t *)dev(T_K0TRI0);
-    const uint32_t *d_big = (const uint32_t *)dev(T_BIG), *d_big_cap = (const uint32_t *)dev(T_BIG_CAP);
+    const uint32_t *d_big = (const uint32_t *)dev(T_BIG);
     const uint32_t *d_k1src = (const uint32_t *)dev(T_K1SRC);
-    const unsigned long long *d_big_off = (const unsigned long long *)dev(T_BIG_OFF);
-    if (ngl) PRK_TRY(S.d_pool.ensure(pool * 4));
     uint32_t modes = 0;  // the pass's span kinds: bit per Mode
     for (const auto &d : draws) modes |= 1u << d.mode;
     const bool scalar = (modes & ~(1u << prk::MODE_AVX)) != 0;
@@ -1613,6 +1612,25 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(prk_scan_u64((const unsigned long long *)S.d_bound.p, oslot, nobj + 1, nullptr, &tb, s));
     PRK_TRY(temp(tb));
     PRK_TRY(prk_scan_u64((const unsigned long long *)S.d_bound.p, oslot, nobj + 1, S.d_temp.p, &tb, s));
+    // The walk's working copy, and each large object's most active edges
+    // (read back with the slot total: they size its walk's workgroup).
+    const uint32_t nwork = 3 * nt + (uint32_t)nk1;
+    PRK_TRY(S.d_work.ensure(std::max<size_t>(nwork, 1) * 112));
+    PRK_TRY(prk_obj_gather(S.d_edges.p, ord, total0p, d_edges_in, d_k1src, (uint32_t)nk1, S.d_work.p, nwork, s));
+    const size_t cls_bytes = (size_t)nbig_all * 20 + 64;  // most (4) | big (4) | off (8) | cap (4) per object
+    if (cls_bytes > S.cls_cap) {
+        if (S.h_cls) (void)hipHostFree(S.h_cls);
+        S.h_cls = nullptr;
+        S.cls_cap = 0;
+        PRK_TRY(hipHostMalloc((void **)&S.h_cls, cls_bytes + cls_bytes / 4, hipHostMallocDefault));
+        S.cls_cap = cls_bytes + cls_bytes / 4;
+    }
+    int32_t *h_most = reinterpret_cast<int32_t *>(S.h_cls);
+    if (nbig_all) {
+        PRK_TRY(S.d_most.ensure((size_t)nbig_all * 4));
+        PRK_TRY(prk_obj_maxact(&fp, d_objs, d_big, nbig_all, escan, total0p, S.d_work.p, (int32_t *)S.d_most.p, s));
+        PRK_TRY(hipMemcpyAsync(h_most, S.d_most.p, (size_t)nbig_all * 4, hipMemcpyDeviceToHost, s));
+    }
     PRK_TRY(hipMemcpyAsync(S.h_rb, oslot + nobj, 8, hipMemcpyDeviceToHost, s));
     PRK_TRY(hipMemsetAsync(S.d_err.p, 0, 4, s));
     PRK_TRY(hipStreamSynchronize(s));
@@ -1625,18 +1643,71 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(S.d_pos.ensure(ns * 16));
     PRK_TRY(S.d_span_tri.ensure(ns * 4));
     if (scalar) PRK_TRY(S.d_srecs.ensure(ns * 96));  // DrawModel span records (prk_spans.hip ScSpanRecG)
-    const uint32_t nbig_all = (uint32_t)S.h_big_gl.size();
     if (nbig_all) PRK_TRY(S.d_raw.ensure(ns * 96));   // the slot walks' pairs (prk_spans.hip PairRaw)
     // slots no span takes stay row -1: binned nowhere
     PRK_TRY(hipMemsetAsync(S.d_pos.p, 0xFF, ns * 16, s));
-    const uint32_t nwork = 3 * nt + (uint32_t)nk1;
-    PRK_TRY(S.d_work.ensure(std::max<size_t>(nwork, 1) * 112));
-    PRK_TRY(prk_obj_gather(S.d_edges.p, ord, total0p, d_edges_in, d_k1src, (uint32_t)nk1,
-                           S.d_work.p, nwork, s));
-    PRK_TRY(prk_obj_walk(&fp, d_objs, nobj, d_big, nbig, wcap, d_big_off, d_big_cap,
-                         (int32_t *)S.d_pool.p, escan, total0p, S.d_work.p,
-                         oslot, S.d_recs.p, scalar ? S.d_srecs.p : nullptr, S.d_raw.p, S.d_pos.p,
-                         (uint32_t *)S.d_span_tri.p, d_spans_in, (uint32_t *)S.d_err.p, s));
+    // Walk groups: per mode, the large objects by the workgroup their list
+    // needs (slot_threads(lcap) >= most + 2, lcap <= the device's), the rest
+    // (more than lcap, or rows past k_obj_maxact's histogram) one wave each
+    // with the list in a pool slice.
+    struct Group {
+        int32_t mode;
+        uint32_t lcap, start, count;
+    };
+    std::vector<Group> groups;
+    uint32_t *cls_big = reinterpret_cast<uint32_t *>(S.h_cls + (size_t)nbig_all * 4);
+    unsigned long long *cls_off = reinterpret_cast<unsigned long long *>(S.h_cls + ((((size_t)nbig_all * 8) + 7) & ~(size_t)7));
+    uint32_t *cls_cap = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(cls_off) + (size_t)nbig_all * 8);
+    {
+        static const uint32_t kCaps[] = {62, 126, 254, 510, 1022};
+        uint32_t k = 0, b = 0;
+        for (int mo = 0; mo < prk::MODE_COUNT; ++mo) {
+            const uint32_t b0 = b;
+            for (int ci = 0; ci <= 5; ++ci) {  // ci 5: the device-memory lists
+                const uint32_t capc = ci < 5 ? kCaps[ci] : 0u;
+                if (ci < 5 && capc > lcap) continue;
+                const uint32_t start = k;
+                for (uint32_t i = 0; i < bigm[mo].size(); ++i) {
+                    const int32_t most = h_most[b0 + i];
+                    uint32_t want = 0;  // the class this object takes
+                    for (int cj = 0; cj < 5; ++cj)
+                        if (kCaps[cj] <= lcap && most >= 0 && (uint32_t)most <= kCaps[cj]) {
+                            want = kCaps[cj];
+                            break;
+                        }
+                    if (want != capc) continue;
+                    cls_big[k] = bigm[mo][i];
+                    cls_off[k] = capc ? 0ull : pool;
+                    cls_cap[k] = capc ? 0u : bige[mo][i];
+                    if (!capc) pool += (uint64_t)kWaveListArrays * (bige[mo][i] + 2);
+                    ++k;
+                }
+                if (k > start) groups.push_back(Group{mo, capc, start, k - start});
+            }
+            b += (uint32_t)bigm[mo].size();
+        }
+    }
+    const uint32_t *d_cbig = nullptr, *d_ccap = nullptr;
+    const unsigned long long *d_coff = nullptr;
+    if (nbig_all) {
+        const size_t lo = (size_t)nbig_all * 4, hi = reinterpret_cast<char *>(cls_cap + nbig_all) - S.h_cls;
+        PRK_TRY(S.d_cls.ensure(hi));
+        PRK_TRY(hipMemcpyAsync(static_cast<char *>(S.d_cls.p) + lo, S.h_cls + lo, hi - lo, hipMemcpyHostToDevice, s));
+        d_cbig = reinterpret_cast<const uint32_t *>(static_cast<char *>(S.d_cls.p) + lo);
+        d_coff = reinterpret_cast<const unsigned long long *>(static_cast<char *>(S.d_cls.p) +
+                                                              (reinterpret_cast<char *>(cls_off) - S.h_cls));
+        d_ccap = reinterpret_cast<const uint32_t *>(static_cast<char *>(S.d_cls.p) +
+                                                    (reinterpret_cast<char *>(cls_cap) - S.h_cls));
+        if (pool) PRK_TRY(S.d_pool.ensure(pool * 4));
+    }
+    PRK_TRY(prk_obj_walk(&fp, d_objs, nobj, escan, total0p, S.d_work.p, oslot, S.d_recs.p,
+                         scalar ? S.d_srecs.p : nullptr, S.d_pos.p, (uint32_t *)S.d_span_tri.p, d_spans_in,
+                         (uint32_t *)S.d_err.p, s));
+    for (const Group &g : groups)
+        PRK_TRY(prk_obj_walk_group(&fp, g.mode, g.lcap, d_objs, d_cbig + g.start, d_coff + g.start, d_ccap + g.start,
+                                   g.count, (int32_t *)S.d_pool.p, escan, total0p, S.d_work.p, oslot, S.d_recs.p,
+                                   scalar ? S.d_srecs.p : nullptr, S.d_raw.p, S.d_pos.p, (uint32_t *)S.d_span_tri.p,
+                                   (uint32_t *)S.d_err.p, s));
     if (nbig_all)  // the slot walks' pairs into span records
         PRK_TRY(prk_span_finish(&fp, S.d_raw.p, nslot, S.d_recs.p, scalar ? S.d_srecs.p : nullptr, S.d_pos.p, s));
     PRK_TRY(S.d_scnt.ensure(((size_t)nslot + 1) * 4));

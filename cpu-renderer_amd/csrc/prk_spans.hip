@@ -698,7 +698,7 @@ __global__ void __launch_bounds__(64) k_obj_walk(FrameParams fp, const ObjDesc *
 // list order (position p = the p-th edge from ListHead) holding, beside each
 // edge index, the fields the list operations read (X, Gradient, Left, YMax);
 // the edges themselves stay in the working copy.  It lives in LDS when the
-// object's most simultaneously listed edges (obj_max_active) fit `lcap`, and
+// object's most simultaneously listed edges (k_obj_maxact) fit `lcap`, and
 // in device memory (a slice of a pool sized by the object's edge count)
 // beyond that: the list has no length limit, as the
 // reference's pointer list has none.  Per row, exactly the reference's
@@ -1369,17 +1369,16 @@ __device__ void insert_batch_b(const SlotLds &S, BlockRed &R, int &m, int k) {
         h = S.aux[gq + 1] - s0;
         S.bk2[s0 + arr] = q;
     }
-    const int32_t hmax = blk_max(R, h);
+    __syncthreads();
     // 6. final positions: gap + new edges of earlier gaps + those of its gap
     //    ordered before it (smaller key, or an equal key inserted earlier)
+    //    (a per-thread loop: no barrier inside)
     int32_t r = 0;
-    for (int32_t j = 0; j < hmax; ++j) {
-        if (j < h) {
-            const int32_t u = S.bk2[s0 + j];
-            if (u != q) {
-                const LKey ku{S.nkx[u], S.nkg[u], S.nkl[u]};
-                r += (key_gt(kc, ku) || (!key_gt(ku, kc) && u < q)) ? 1 : 0;
-            }
+    for (int32_t j = 0; j < h; ++j) {
+        const int32_t u = S.bk2[s0 + j];
+        if (u != q) {
+            const LKey ku{S.nkx[u], S.nkg[u], S.nkl[u]};
+            r += (key_gt(kc, ku) || (!key_gt(ku, kc) && u < q)) ? 1 : 0;
         }
     }
     // 7. entries move up by the new edges of gaps <= their position; 8. the new edges
@@ -1656,44 +1655,65 @@ __device__ void walk_object_block(const FrameParams &fp, const ObjDesc &od, cons
     }
 }
 
-// The most entries the object's list holds at once (after a row's
-// insertion, before its expiry): an edge inserted at row YMin leaves at the
-// first row r >= YMin with YMax <= r, so it is in the list on the rows
-// [YMin, max(YMin, YMax)] of [FirstRow, MaxY).  A difference histogram over
-// those rows in h (`ints` ints, rows beyond: INT32_MAX, i.e. "unknown").
-__device__ int32_t obj_max_active(const ObjEdge *__restrict__ E, uint32_t n, int32_t FirstRow, int32_t MaxY,
-                                  int32_t *h, uint32_t ints) {
-    const int lane = threadIdx.x & 63;
+// The most entries each large object's list holds at once (thread block
+// per object, a difference histogram of its listed edges over up to
+// kMaxactRows rows; more rows: INT32_MAX, its list goes to device memory).
+// The host reads them back with the span slot total and launches each
+// object's walk with a workgroup just large enough (slot_threads).
+constexpr int32_t kMaxactRows = 16000;  // (the histogram is static LDS: < 64 KiB)
+__global__ void __launch_bounds__(kSlotMaxThreads) k_obj_maxact(FrameParams fp, const ObjDesc *__restrict__ objs,
+                                                               const uint32_t *__restrict__ big,
+                                                               const uint32_t *__restrict__ escan,
+                                                               const uint32_t *__restrict__ total0p,
+                                                               const ObjEdge *__restrict__ work,
+                                                               int32_t *__restrict__ most) {
+    __shared__ int32_t h[kMaxactRows + 1];
+    __shared__ BlockRed R;
+    const ObjDesc od = objs[big[blockIdx.x]];
+    uint32_t e0, n;
+    obj_range(od, escan, *total0p, e0, n);
+    const ObjEdge *E = work + e0;
+    const int tid = threadIdx.x, NT = blockDim.x;
+    if (n == 0) {
+        if (tid == 0) most[blockIdx.x] = 0;
+        return;
+    }
+    int32_t mr = INT32_MIN;
+    for (uint32_t i = tid; i < n; i += NT) mr = max(mr, E[i].YMax);
+    const int32_t MaxY = min(min(blk_max(R, mr), fp.H), fp.row1), FirstRow = E[0].YMin;
     const int64_t rows = (int64_t)MaxY - FirstRow;
-    if (rows <= 0) return 0;
-    if (rows + 1 > (int64_t)ints) return INT32_MAX;
-    const int R = (int)rows;
-    for (int q = lane; q <= R; q += 64) h[q] = 0;
-    wave_lds_sync();
-    for (uint32_t i = lane; i < n; i += 64) {
+    if (rows <= 0 || rows + 1 > kMaxactRows) {
+        if (tid == 0) most[blockIdx.x] = rows <= 0 ? 0 : INT32_MAX;
+        return;
+    }
+    const int Rn = (int)rows;
+    for (int q = tid; q <= Rn; q += NT) h[q] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += NT) {  // an edge is listed on rows [YMin, max(YMin, YMax)]
         const int32_t y0 = E[i].YMin, y1 = E[i].YMax;
         if (y0 >= MaxY) continue;  // never inserted
-        const int32_t lo = y0 - FirstRow, hi = min(max(y0, y1), MaxY - 1) - FirstRow;
-        atomicAdd(&h[max(lo, 0)], 1);
-        atomicAdd(&h[hi + 1], -1);
+        atomicAdd(&h[y0 - FirstRow], 1);
+        atomicAdd(&h[min(max(y0, y1), MaxY - 1) - FirstRow + 1], -1);
     }
-    wave_lds_sync();
+    __syncthreads();
     int32_t carry = 0, best = 0;
-    for (int b0 = 0; b0 < R; b0 += 64) {
-        const int q = b0 + lane;
-        int32_t v = wave_incl_sum_i32(q < R ? h[q] : 0) + carry;
-        best = max(best, wave_max_i32(q < R ? v : 0));
-        carry = readlane_i(v, 63);
+    for (int b0 = 0; b0 < Rn; b0 += NT) {
+        const int q = b0 + tid;
+        const int32_t v = q < Rn ? h[q] : 0;
+        int32_t tot;
+        const int32_t ex = blk_excl_sum(R, v, tot);
+        if (q < Rn) best = max(best, carry + ex + v);
+        carry += tot;
     }
-    wave_lds_sync();  // (h is the list's storage next)
-    return best;
+    best = blk_max(R, best);
+    if (tid == 0) most[blockIdx.x] = best;
 }
 
-// One workgroup per large object (slot_threads(lcap) threads): everything
-// in LDS (walk_object_block, lcap slots) when its most active entries fit,
-// else its first wave walks it with the list in its pool slice
-// pool + big_off[blockIdx.x] (kWaveListArrays arrays of big_cap[blockIdx.x]
-// + 2 ints, big_cap >= its edge count) and the other waves leave.
+// One workgroup per large object: lcap > 0, everything in LDS
+// (walk_object_block, lcap slots, slot_threads(lcap) threads); lcap == 0, the
+// list in the object's pool slice pool + big_off[blockIdx.x]
+// (kWaveListArrays arrays of big_cap[blockIdx.x] + 2 ints, big_cap >= its
+// edge count), walked by one wave (64 threads).
 template <int M>
 __global__ void __launch_bounds__(kSlotMaxThreads) k_obj_walk_wave(FrameParams fp, const ObjDesc *__restrict__ objs,
                                                       const uint32_t *__restrict__ big,
@@ -1707,7 +1727,6 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_obj_walk_wave(FrameParams f
                                                       uint32_t *__restrict__ span_tri, uint32_t *__restrict__ err) {
     extern __shared__ int32_t lds_list[];
     __shared__ BlockRed R;
-    __shared__ int32_t most_s;
     const uint32_t o = big[blockIdx.x];
     const ObjDesc od = objs[o];
     const DrawRec &d = fp.draws[od.draw];
@@ -1716,16 +1735,7 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_obj_walk_wave(FrameParams f
     obj_range(od, escan, *total0p, e0, n);
     ObjEdge *E = work + e0;
     if (n == 0) return;  // (the whole workgroup)
-    int32_t mr = INT32_MIN;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) mr = max(mr, E[i].YMax);
-    const int32_t MaxY = min(min(blk_max(R, mr), fp.H), fp.row1);
-    if (threadIdx.x < 64) {  // the first wave counts the most active entries
-        const int32_t most =
-            obj_max_active(E, n, E[0].YMin, MaxY, lds_list, (uint32_t)(slot_lds_bytes(lcap) / 4));
-        if (threadIdx.x == 0) most_s = most;
-    }
-    __syncthreads();
-    if (most_s > (int32_t)lcap) {  // the list in device memory, one wave
+    if (lcap == 0) {  // the list in device memory, one wave
         if (threadIdx.x >= 64) return;
         if (n > big_cap[blockIdx.x]) {  // (the host sizes every slice by the object's edges)
             if (threadIdx.x == 0) atomicOr(err, 1u);
@@ -1736,6 +1746,9 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_obj_walk_wave(FrameParams f
         walk_object_wave<M, true>(fp, od, d, E, n, base, bound, L, recs, srecs, pos, span_tri, err);
         return;
     }
+    int32_t mr = INT32_MIN;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) mr = max(mr, E[i].YMax);
+    const int32_t MaxY = min(min(blk_max(R, mr), fp.H), fp.row1);
     SlotLds S;
     S.carve(lds_list, lcap, blockDim.x);
     walk_object_block<M>(fp, od, E, n, MaxY, base, bound, S, R, lcap, raw, pos, span_tri, err);
@@ -1894,53 +1907,61 @@ uint32_t prk_obj_walk_lcap(void) {
     }
     return (uint32_t)(c - 1);
 }
-// The object walk, one pass: a thread per object, a wave per object of
-// big[] (grouped by mode, nbig[mode] each: one launch per mode; in LDS of
-// lcap slots, lcap <= prk_obj_walk_lcap(), when its
-// most active entries fit, else its list in the pool at big_off, big_cap
-// edges).  Spans go to slots soff[o] + k.  err: bit 0 a pool slice smaller
-// than its object, bit 1 an object emitted past its bound (neither can
-// happen).
-hipError_t prk_obj_walk(const prk::FrameParams *fp, const void *objs, uint32_t nobj, const uint32_t *big,
-                        const uint32_t *nbig, uint32_t lcap, const unsigned long long *big_off, const uint32_t *big_cap,
-                        int32_t *pool, const uint32_t *escan, const uint32_t *total0p, void *work,
-                        const unsigned long long *soff, void *recs, void *srecs, void *raw, void *pos,
-                        uint32_t *span_tri, const void *spans_in, uint32_t *err, hipStream_t s) {
+// The object walk: a thread per small object or caller edge list ...
+hipError_t prk_obj_walk(const prk::FrameParams *fp, const void *objs, uint32_t nobj, const uint32_t *escan,
+                        const uint32_t *total0p, void *work, const unsigned long long *soff, void *recs, void *srecs,
+                        void *pos, uint32_t *span_tri, const void *spans_in, uint32_t *err, hipStream_t s) {
     if (nobj == 0) return hipSuccess;
     hipLaunchKernelGGL(prk::k_obj_walk, dim3((nobj + 63) / 64), dim3(64), 0, s, *fp,
                        reinterpret_cast<const prk::ObjDesc *>(objs), nobj, escan, total0p,
                        reinterpret_cast<prk::ObjEdge *>(work), soff, reinterpret_cast<prk::SpanRecG *>(recs),
                        reinterpret_cast<prk::ScSpanRecG *>(srecs), reinterpret_cast<prk::SpanPos *>(pos), span_tri,
                        reinterpret_cast<const prk::SpanIn *>(spans_in), err);
-    hipError_t e = hipGetLastError();
-    const size_t bytes = prk::slot_lds_bytes(lcap);
-    const uint32_t nt = prk::slot_threads(lcap);
-    uint32_t b0 = 0;
-    for (int mo = 0; mo < prk::MODE_COUNT && e == hipSuccess; ++mo) {
-        const uint32_t nb = nbig[mo];
-        if (nb == 0) continue;
+    return hipGetLastError();
+}
+// ... the most active entries of the large ones (big[0, nbig)) ...
+hipError_t prk_obj_maxact(const prk::FrameParams *fp, const void *objs, const uint32_t *big, uint32_t nbig,
+                          const uint32_t *escan, const uint32_t *total0p, const void *work, int32_t *most,
+                          hipStream_t s) {
+    if (nbig == 0) return hipSuccess;
+    hipLaunchKernelGGL(prk::k_obj_maxact, dim3(nbig), dim3(prk::kSlotMaxThreads), 0, s, *fp,
+                       reinterpret_cast<const prk::ObjDesc *>(objs), big, escan, total0p,
+                       reinterpret_cast<const prk::ObjEdge *>(work), most);
+    return hipGetLastError();
+}
+// ... and a workgroup per large object of mode `mode` (big[0, nbig)): lcap > 0
+// (<= prk_obj_walk_lcap()), slot_threads(lcap) threads, the list in LDS; lcap
+// == 0, one wave, the list in the pool at big_off, big_cap edges.  Spans go to
+// slots soff[o] + k.  err: bit 0 a pool slice smaller than its object, bit 1
+// an object emitted past its bound (neither can happen).
+uint32_t prk_obj_walk_threads(uint32_t lcap) { return lcap ? prk::slot_threads(lcap) : 64u; }
+hipError_t prk_obj_walk_group(const prk::FrameParams *fp, int32_t mode, uint32_t lcap, const void *objs,
+                              const uint32_t *big, const unsigned long long *big_off, const uint32_t *big_cap,
+                              uint32_t nbig, int32_t *pool, const uint32_t *escan, const uint32_t *total0p,
+                              void *work, const unsigned long long *soff, void *recs, void *srecs, void *raw,
+                              void *pos, uint32_t *span_tri, uint32_t *err, hipStream_t s) {
+    if (nbig == 0) return hipSuccess;
+    const size_t bytes = lcap ? prk::slot_lds_bytes(lcap) : 0;
+    const uint32_t nt = prk_obj_walk_threads(lcap);
+    switch (mode) {
 #define PRK_WALK_WAVE(MM)                                                                                           \
     case MM:                                                                                                        \
-        hipLaunchKernelGGL(prk::k_obj_walk_wave<MM>, dim3(nb), dim3(nt), bytes, s, *fp,                            \
-                           reinterpret_cast<const prk::ObjDesc *>(objs), big + b0, big_off + b0, big_cap + b0, pool, \
-                           lcap, escan, total0p, reinterpret_cast<prk::ObjEdge *>(work), soff,                      \
+        hipLaunchKernelGGL(prk::k_obj_walk_wave<MM>, dim3(nbig), dim3(nt), bytes, s, *fp,                          \
+                           reinterpret_cast<const prk::ObjDesc *>(objs), big, big_off, big_cap, pool, lcap, escan,  \
+                           total0p, reinterpret_cast<prk::ObjEdge *>(work), soff,                                   \
                            reinterpret_cast<prk::SpanRecG *>(recs), reinterpret_cast<prk::ScSpanRecG *>(srecs),     \
                            reinterpret_cast<prk::PairRaw *>(raw), reinterpret_cast<prk::SpanPos *>(pos), span_tri,  \
                            err);                                                                                    \
         break;
-        switch (mo) {
-            PRK_WALK_WAVE(prk::MODE_AVX)
-            PRK_WALK_WAVE(prk::MODE_SC_GOURAUD)
-            PRK_WALK_WAVE(prk::MODE_SC_GOURAUD_TEX)
-            PRK_WALK_WAVE(prk::MODE_SC_PHONG)
-            PRK_WALK_WAVE(prk::MODE_SC_PHONG_TEX)
-            default: break;
-        }
+        PRK_WALK_WAVE(prk::MODE_AVX)
+        PRK_WALK_WAVE(prk::MODE_SC_GOURAUD)
+        PRK_WALK_WAVE(prk::MODE_SC_GOURAUD_TEX)
+        PRK_WALK_WAVE(prk::MODE_SC_PHONG)
+        PRK_WALK_WAVE(prk::MODE_SC_PHONG_TEX)
 #undef PRK_WALK_WAVE
-        e = hipGetLastError();
-        b0 += nb;
+        default: return hipErrorInvalidValue;
     }
-    return e;
+    return hipGetLastError();
 }
 // The slot walk's pairs (SPAN_RAW) into span records, one thread per slot.
 hipError_t prk_span_finish(const prk::FrameParams *fp, const void *raw, uint32_t nslot, void *recs, void *srecs,

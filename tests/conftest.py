@@ -28,3 +28,22 @@ def gpu():
     if n <= 0:
         pytest.fail("gpu-marked test but no HIP device visible")
     return n
+
+
+@pytest.fixture(autouse=True)
+def _hip_last_error_trace(request):
+    """Diagnostics (PRK_TRACE_HIP=1): the thread's sticky HIP error after each
+    test, so a call that failed silently is pinned to the test that made it."""
+    yield
+    if not os.environ.get("PRK_TRACE_HIP") or request.node.get_closest_marker("gpu") is None:
+        return
+    import ctypes
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+    except OSError:
+        return
+    e = hip.hipGetLastError()
+    if e:
+        hip.hipGetErrorName.restype = ctypes.c_char_p
+        sys.stderr.write("PRK_TRACE_HIP: %s left HIP error %d (%s)\n"
+                         % (request.node.nodeid, e, hip.hipGetErrorName(e).decode()))
