@@ -299,6 +299,7 @@ def main():
             done.record(comm_stream)
             pending[b] = [done]  # Event.wait(): the render stream waits for it
         elif world > 1:  # RCCL over xGMI: strips -> rank 0's frame
+            r.resolve(stream)  # an overflowed frame is re-run before its strip is sent
             _, pending[b] = pdist.gather_strips_start(dist, colors[b], rank, world, H, out=frames[b])
 
     def drain():

@@ -1858,6 +1858,8 @@ __attribute__((visibility("hidden"))) int prk_resolve_pending(prk_context *c, vo
     return PRK_OK;
 }
 
+int prk_resolve(prk_context *c, void *stream) { return prk_resolve_pending(c, stream); }
+
 int prk_synchronize(prk_context *c) {
     if (!c) return PRK_ERR_ARG;
     RESOLVE_COUNT(c);

@@ -81,6 +81,7 @@ _SIGS = {
     "prk_flush": (C.c_int, [C.c_void_p, C.c_void_p]),
     "prk_reset_draws": (C.c_int, [C.c_void_p]),
     "prk_synchronize": (C.c_int, [C.c_void_p]),
+    "prk_resolve": (C.c_int, [C.c_void_p, C.c_void_p]),
     "prk_get_stats": (C.c_int, [C.c_void_p, C.POINTER(abi.PrkStats)]),
     "prk_timing_reset": (C.c_int, [C.c_void_p]),
     "prk_set_debug": (C.c_int, [C.c_void_p, C.c_int32]),
@@ -124,6 +125,17 @@ def lib(path=None):
         p = path or LIB_PATH
         if not os.path.exists(p):
             raise PrkError("load libprk_hip.so (%s: not built; run __graft_entry__.build())" % p, -3)
+        # One ROCm runtime per process: torch ships its own libamdhip64 /
+        # librccl / librocm_smi64 under names (libamdhip64.so, librccl.so) that
+        # do not match this library's (libamdhip64.so.7 via /opt/rocm, and the
+        # librccl.so.1 prk_comm_* dlopens).  Loaded first, torch's copies
+        # satisfy ours by SONAME; loaded after us, torch would map a second
+        # copy of each, and two librocm_smi64 copies destroy the same
+        # interposed static map at exit (glibc "double free").
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(p)
         # (A/B tools load older builds through PRK_LIB that may lack newer entry points)
         variant = os.path.abspath(p) != os.path.abspath(_DEFAULT_LIB)
@@ -495,6 +507,12 @@ class Renderer:
 
     def synchronize(self):
         _check("prk_synchronize", self._L.prk_synchronize(self._h))
+
+    def resolve(self, stream=None):
+        """Resolve the last flush's bin count (an overflowed frame is re-run
+        first) and make `stream` wait for the frame's end, host-asynchronously:
+        call before reading the target on another stream (prk.dist gathers)."""
+        _check("prk_resolve", self._L.prk_resolve(self._h, None if stream is None else C.c_void_p(stream)))
 
     def timing_reset(self):
         _check("prk_timing_reset", self._L.prk_timing_reset(self._h))

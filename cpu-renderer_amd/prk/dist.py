@@ -39,7 +39,12 @@ def gather_strips_start(dist, strip, rank, world, height, out=None):
     rank 0 / None elsewhere, the pending requests): on RCCL the transfers run
     on the communicator's stream, so rendering the next frame into another
     strip buffer overlaps them; req.wait() orders the current stream after
-    them (call it before the strip or frame is reused)."""
+    them (call it before the strip or frame is reused).
+
+    When `strip` is a prk target just flushed, call Renderer.resolve(stream)
+    (prk_resolve) first: a frame whose bin entries overflowed the scratch is
+    re-run when its count is resolved, and the sends must come after that
+    (prk_gather_frame does this itself)."""
     import torch
 
     W = strip.shape[1]

@@ -328,6 +328,13 @@ int prk_flush(prk_context *ctx, void *stream);
 /* Drop recorded draws without executing them. */
 int prk_reset_draws(prk_context *ctx);
 int prk_synchronize(prk_context *ctx);
+/* Resolve the last flush's pending bin count (re-running an overflowed frame,
+ * as above) and make `stream` (a hipStream_t of the context's device, or NULL
+ * for none) wait for the end of the context's last frame, without blocking
+ * the host on the frame's raster.  For callers that read the target through
+ * their own device pointers on their own stream (a torch RCCL strip gather):
+ * the asynchronous counterpart of prk_synchronize. */
+int prk_resolve(prk_context *ctx, void *stream);
 int prk_get_stats(prk_context *ctx, prk_stats *out); /* waits for timed flushes */
 int prk_timing_reset(prk_context *ctx);
 

@@ -9,8 +9,23 @@ for p in (os.path.join(ROOT, "cpu-renderer_amd"), os.path.join(ROOT, "oracle"), 
         sys.path.insert(0, p)
 
 
+def _abort_bt_install():
+    """Diagnostics (PRK_ABORT_BT=1): a native backtrace on SIGABRT
+    (tools/abort_bt.c), installed again at interpreter exit because pytest's
+    faulthandler restores the handlers it replaced when the session ends."""
+    import ctypes
+    lib = os.path.join(ROOT, "tools", "libabort_bt.so")
+    if os.path.exists(lib):
+        ctypes.CDLL(lib).abort_bt_install()
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libprk_hip.so on the device)")
+    if os.environ.get("PRK_ABORT_BT"):
+        import atexit
+        import prk  # noqa: F401  (its own exit hook registers first, runs after ours)
+        _abort_bt_install()
+        atexit.register(_abort_bt_install)
 
 
 def gpu_available():

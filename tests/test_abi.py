@@ -8,10 +8,12 @@
 * The C++ drop-in header (include/projekt.h) compiles against the reference's
   call pattern (examples/dropin_demo.cpp) and links against the library.
 """
+import ast
 import ctypes as C
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -117,3 +119,29 @@ def test_fill_edge_count_matches_oracle(per):
         want = len(O.fill_edge_table(s, t0, n))
         got = prk.fill_edge_count(s.vertices[3 * t0:3 * (t0 + n)], s.P, T)
         assert got == want, (t0, n, got, want)
+
+
+ROCM_MAP_RE = r"(/\S*(?:libamdhip64|librccl|librocm_smi64|libhsa-runtime64)\S*)"
+LOAD_ORDER_CHILD = """
+import re, sys
+sys.path.insert(0, {pkg!r})
+import prk
+assert prk.comm_available()  # dlopens librccl, as prk.Comm does
+import torch  # noqa: F401
+print(sorted(set(re.findall({rx!r}, open('/proc/self/maps').read()))))
+"""
+
+
+def test_one_rocm_runtime_per_process():
+    """The binding loads torch's ROCm libraries before libprk_hip.so, so a
+    process that uses both maps one HIP runtime, one RCCL and one
+    librocm_smi64: loaded the other way round, the process maps
+    /opt/rocm's copies and torch's side by side, and the two librocm_smi64
+    copies' exit-time destructors free one interposed static map twice (glibc
+    "double free or corruption", rc 134 — the round-3/4 exit aborts)."""
+    code = LOAD_ORDER_CHILD.format(pkg=os.path.join(ROOT, "cpu-renderer_amd"), rx=ROCM_MAP_RE)
+    run = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert run.returncode == 0 and "double free" not in run.stderr, (run.returncode, run.stderr[-2000:])
+    libs = ast.literal_eval(run.stdout.strip().splitlines()[-1])
+    for name in ("libamdhip64", "librccl", "librocm_smi64", "libhsa-runtime64"):
+        assert len([p for p in libs if name in os.path.basename(p)]) == 1, libs

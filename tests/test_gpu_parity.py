@@ -331,6 +331,48 @@ def test_deferred_count_overflow_rerun_across_rebind(gpu):
     assert (ga[0] == oc).all(), "target A colour"
 
 
+def test_resolve_before_strip_read_on_another_stream(gpu):
+    """A caller that reads the target through its own pointers on its own
+    stream (bench.py's torch RCCL strip gather) calls Renderer.resolve(stream)
+    after the flush: an over-capacity frame is re-run first and the reading
+    stream waits for the re-run's end, so the copy it takes is the finished
+    frame — with no host sync in between."""
+    import torch
+
+    small = scenes.random_soup(3000, 512, 384, radius=16, seed=91)
+    big = scenes.random_soup(6000, 512, 384, radius=260, seed=92)
+    big.texture = small.texture
+    W, H = 512, 384
+    dev = torch.device("cuda:0")
+    color = torch.empty((H, W), dtype=torch.int32, device=dev)
+    zbuf = torch.empty((H, W), dtype=torch.float32, device=dev)
+    r = prk.Renderer(0)
+    try:
+        r.target_bind(color.data_ptr(), W * 4, zbuf.data_ptr(), W, H)
+        r.set_camera(small.prk_transform(), small.prk_lights())
+        tex = r.texture(small.texture)
+        gs = [r.geometry(s.vertices, s.colors, s.normals, s.uvs) for s in (small, big)]
+        stream = torch.cuda.current_stream().cuda_stream
+        r.clear_on_flush()
+        r.draw_model_optimized(gs[0], small.tri_count, P=small.P, bitmap=tex, phong=True)
+        r.complete_all_work(stream)  # first frame: counted at once (sizes the scratch)
+        r.clear_on_flush()
+        r.draw_model_optimized(gs[1], big.tri_count, P=big.P, bitmap=tex, phong=True)
+        r.complete_all_work(stream)  # over capacity: re-run when resolved
+        side = torch.cuda.Stream(device=dev)
+        r.resolve(side.cuda_stream)
+        with torch.cuda.stream(side):
+            got_c, got_z = color.clone(), zbuf.clone()
+        side.synchronize()
+        entries = r.stats()["bin_entries"]
+    finally:
+        r.close()
+    bc, bz, _, _ = O.render(big)
+    assert entries > 0
+    assert (got_z.cpu().numpy().view(np.uint32) == bz.view(np.uint32)).all(), "z"
+    assert (got_c.cpu().numpy().view(np.uint32) == bc.view(np.uint32)).all(), "colour"
+
+
 def test_pipelined_identical_frames_and_band_rebind(gpu):
     """Identical fused-clear frames queued back to back (every scratch set in
     turn) end as the one frame; then the target is re-bound from a full frame
