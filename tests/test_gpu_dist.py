@@ -143,3 +143,42 @@ def test_gather_rejects_wrong_band(gpu, scene_ref):
         prk.gather_frame_local(rs, cp, pitch, None, with_z=True)
     for R in rs + [F]:
         R.close()
+
+
+def test_gather_after_overflowed_frame_on_explicit_stream(gpu):
+    """prk_gather_frame right after a frame whose bin entries overflowed the
+    scratch, on a caller stream (torch): the gather resolves the count first,
+    so the re-run lands in the band before it is sent, and the caller stream
+    waits for it — the gathered frame is the finished frame (no host sync
+    between the flush and the gather)."""
+    import torch
+
+    import oracle as O
+    if not prk.comm_available():
+        pytest.fail("librccl did not load")
+    small = scenes.random_soup(3000, 512, 384, radius=16, seed=91)
+    big = scenes.random_soup(6000, 512, 384, radius=260, seed=92)
+    big.texture = small.texture
+    (R,) = _band_renderers(small, 1)  # first frame: counted at once (sizes the scratch)
+    F = _frame(big)
+    cp, _, zp, *_ = F.target()
+    c = prk.Comm.init(R, prk.comm_unique_id(), 1, 0)
+    try:
+        g = R.geometry(big.vertices, big.colors, big.normals, big.uvs)
+        t = R.texture(big.texture)
+        R.clear_on_flush()
+        R.draw_model_optimized(g, big.tri_count, P=big.P, bitmap=t)
+        R.complete_all_work()  # over capacity: its count is read by the gather
+        side = torch.cuda.Stream(device=torch.device("cuda:0"))
+        c.gather(R, cp, zp, with_z=True, stream=side.cuda_stream)
+        side.synchronize()
+        gc, gz = F.download()
+        entries = R.stats()["bin_entries"]
+    finally:
+        c.close()
+        R.close()
+        F.close()
+    oc, oz, _, _ = O.render(big)
+    assert entries > 0
+    assert (gz.view(np.uint32) == oz.view(np.uint32)).all(), "z"
+    assert (gc == oc).all(), "colour"
