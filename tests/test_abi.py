@@ -62,6 +62,8 @@ def test_argument_errors_without_device():
     assert L.prk_device_count(None) == abi.PRK_ERR_ARG
     assert L.prk_create(0, None) == abi.PRK_ERR_ARG
     assert L.prk_construct_sphere(None, None, None, None, None) == abi.PRK_ERR_ARG
+    assert L.prk_resolve(None, None) == abi.PRK_ERR_ARG
+    assert L.prk_synchronize(None) == abi.PRK_ERR_ARG
     assert L.prk_version() .startswith(b"prk")
 
 
