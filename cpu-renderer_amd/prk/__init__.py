@@ -134,7 +134,7 @@ def lib(path=None):
         # interposed static map at exit (glibc "double free").
         try:
             import torch  # noqa: F401
-        except ImportError:
+        except Exception:  # no (usable) torch: this library's own ROCm stack alone
             pass
         L = C.CDLL(p)
         # (A/B tools load older builds through PRK_LIB that may lack newer entry points)
