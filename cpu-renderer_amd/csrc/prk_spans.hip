@@ -516,14 +516,55 @@ __device__ __forceinline__ bool emit_span(const FrameParams &fp, const ObjEdge &
     return true;
 }
 
+// The list fields of the thread walk (links, keys, row range), read and
+// written through one of two stores: the working copy itself (GLinks), or
+// per-thread LDS mirrors (LLinks: objects of at most kLinkCap edges), so the
+// list's chains of dependent accesses (insertion scans, expiry, pairing and
+// swaps) run at LDS latency; the edge records stay in device memory, read
+// for a span and stepped per pair, off those chains.  LLinks steps its X
+// mirror with obj_step's own add.
+struct GLinks {
+    ObjEdge *E;
+    __device__ __forceinline__ int32_t next(int i) const { return E[i].Next; }
+    __device__ __forceinline__ void set_next(int i, int32_t v) const { E[i].Next = v; }
+    __device__ __forceinline__ float x(int i) const { return E[i].X; }
+    __device__ __forceinline__ int32_t ymin(int i) const { return E[i].YMin; }
+    __device__ __forceinline__ int32_t ymax(int i) const { return E[i].YMax; }
+    __device__ __forceinline__ bool before(int a, int b) const { return obj_before(E[a], E[b]); }
+    __device__ __forceinline__ void stepped(int) const {}  // (obj_step stepped E[i].X)
+};
+constexpr int kLinkCap = 48;     // edges per object with LDS links (C3b as 16-triangle objects: 48)
+constexpr int kLinkThreads = 64;  // k_obj_walk's workgroup
+struct LinkLds {
+    float x[kLinkCap * kLinkThreads], g[kLinkCap * kLinkThreads];
+    int32_t ymin[kLinkCap * kLinkThreads], ymax[kLinkCap * kLinkThreads];
+    int16_t nxt[kLinkCap * kLinkThreads];
+    int8_t left[kLinkCap * kLinkThreads];
+};
+struct LLinks {
+    LinkLds *L;
+    int lane;
+    __device__ __forceinline__ int at(int i) const { return i * kLinkThreads + lane; }
+    __device__ __forceinline__ int32_t next(int i) const { return L->nxt[at(i)]; }
+    __device__ __forceinline__ void set_next(int i, int32_t v) const { L->nxt[at(i)] = (int16_t)v; }
+    __device__ __forceinline__ float x(int i) const { return L->x[at(i)]; }
+    __device__ __forceinline__ int32_t ymin(int i) const { return L->ymin[at(i)]; }
+    __device__ __forceinline__ int32_t ymax(int i) const { return L->ymax[at(i)]; }
+    __device__ __forceinline__ bool before(int a, int b) const {
+        const float ax = x(a), bx = x(b), ag = L->g[at(a)], bg = L->g[at(b)];
+        return ax < bx || (ax == bx && (ag < bg || (ag == bg && L->left[at(a)] < L->left[at(b)])));
+    }
+    __device__ __forceinline__ void stepped(int i) const { L->x[at(i)] += L->g[at(i)]; }  // E.X += E.G (obj_step)
+};
+
 // The AET walk of one object by one thread (small objects, caller edge
 // lists): E = its n edges, sorted (kind 0) or as given (kind 1).  Its spans
 // go to slots [base, base + bound) in emission order.
-template <int M>
+template <int M, class LK>
 __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const DrawRec &d, ObjEdge *__restrict__ E,
                             uint32_t n, uint32_t base, uint32_t bound, SpanRecG *__restrict__ recs,
                             ScSpanRecG *__restrict__ srecs, SpanPos *__restrict__ pos,
-                            uint32_t *__restrict__ span_tri, uint32_t *__restrict__ err) {
+                            uint32_t *__restrict__ span_tri, uint32_t *__restrict__ err, const LK lk) {
     constexpr bool kScalar = M != MODE_AVX;
     const bool st = (d.flags & DRAW_ST) != 0;
     const bool given = od.kind == 1;  // a caller's edge list: scanned whole every row
@@ -531,14 +572,14 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
     uint32_t emitted = 0;
     // The AET walk of DrawModelOptimized(RenderQueue,...) (3626-3869) /
     // DrawModel (173-598): the same list logic.
-    const int32_t FirstRow = E[0].YMin;
-    int32_t MaxRow = E[0].YMax;
-    for (uint32_t i = 1; i < n; ++i) MaxRow = max(MaxRow, E[i].YMax);
+    const int32_t FirstRow = lk.ymin(0);
+    int32_t MaxRow = lk.ymax(0);
+    for (uint32_t i = 1; i < n; ++i) MaxRow = max(MaxRow, lk.ymax((int)i));
     const int32_t MaxY = min(min(MaxRow, fp.H), fp.row1);
     // DrawModel's span of row row0-1 can store its one-past-the-row pixel
     // into (row0, 0)
     const int32_t RowLo = kScalar ? fp.row0 - 1 : fp.row0;
-    for (uint32_t i = 0; i < n; ++i) E[i].Next = -1;
+    for (uint32_t i = 0; i < n; ++i) lk.set_next((int)i, -1);
     int32_t Head = -1, Tail = -1;
     uint32_t ins = 0;  // next sorted edge to insert (sorted by YMin)
     for (int32_t Row = FirstRow; Row < MaxY; ++Row) {
@@ -547,33 +588,32 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
         // caller's list is scanned whole, as the reference does.
         uint32_t i0 = 0, i1 = n;
         if (!given) {
-            while (ins < n && E[ins].YMin < Row) ++ins;
+            while (ins < n && lk.ymin((int)ins) < Row) ++ins;
             i0 = ins;
-            while (ins < n && E[ins].YMin == Row) ++ins;
+            while (ins < n && lk.ymin((int)ins) == Row) ++ins;
             i1 = ins;
         }
         for (uint32_t ii = i0; ii < i1; ++ii) {
-            if (E[ii].YMin != Row) continue;
+            if (lk.ymin((int)ii) != Row) continue;
             const int32_t c = (int32_t)ii;
-            ObjEdge &Cur = E[c];
             if (Head >= 0) {
-                if (obj_before(Cur, E[Head])) {
-                    Cur.Next = Head;
+                if (lk.before(c, Head)) {
+                    lk.set_next(c, Head);
                     Head = c;
                 } else {
                     int32_t Cmp = Head, Prev = Head;
                     while (Cmp != Tail) {
-                        Cmp = E[Cmp].Next;
-                        if (obj_before(Cur, E[Cmp])) {
-                            Cur.Next = Cmp;
-                            E[Prev].Next = c;
+                        Cmp = lk.next(Cmp);
+                        if (lk.before(c, Cmp)) {
+                            lk.set_next(c, Cmp);
+                            lk.set_next(Prev, c);
                             Cmp = Tail;
                         } else {
                             Prev = Cmp;
                         }
                     }
                     if (Prev == Cmp) {
-                        E[Tail].Next = c;
+                        lk.set_next(Tail, c);
                         Tail = c;
                     }
                 }
@@ -582,31 +622,31 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
                 Tail = c;
             }
         }
-        while (Head >= 0 && E[Head].YMax <= Row) {  // expiry 3715-3720
+        while (Head >= 0 && lk.ymax(Head) <= Row) {  // expiry 3715-3720
             const int32_t Rm = Head;
-            Head = E[Head].Next;
-            E[Rm].Next = -1;
+            Head = lk.next(Head);
+            lk.set_next(Rm, -1);
         }
         if (Head < 0) {  // pin: the reference dereferences NULL
             Tail = -1;
             // nothing happens on the rows before the next insertion: go there
             if (!given) {
                 if (ins >= n) break;
-                Row = max(Row, E[ins].YMin - 1);
+                Row = max(Row, lk.ymin((int)ins) - 1);
             }
             continue;
         }
         {
             int32_t Prev = Head, Chk = Head;  // 3722-3749
             while (Chk != Tail) {
-                Chk = E[Chk].Next;
-                if (E[Chk].YMax <= Row) {
+                Chk = lk.next(Chk);
+                if (lk.ymax(Chk) <= Row) {
                     if (Chk == Tail) {
                         Tail = Prev;
-                        E[Tail].Next = -1;
+                        lk.set_next(Tail, -1);
                         Chk = Tail;
                     } else {
-                        E[Prev].Next = E[Chk].Next;
+                        lk.set_next(Prev, lk.next(Chk));
                         Chk = Prev;
                     }
                 }
@@ -614,7 +654,7 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
             }
         }
         int32_t PrevCur = -1, PrevNext = -1;  // pairing 3751-3869
-        int32_t Cur = Head, Next = E[Cur].Next;
+        int32_t Cur = Head, Next = lk.next(Cur);
         while (Next >= 0) {
             if (Row >= RowLo &&  // a span of this pass's rows (3759-3809 / 298-538)
                 emit_span<M>(fp, E[Cur], E[Next], Row, d, st, od.g0, emitted < bound, base + emitted, recs, srecs,
@@ -624,29 +664,31 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
             }
             obj_step<M>(E[Cur]);  // 3811-3829
             obj_step<M>(E[Next]);
-            if (E[Cur].X > E[Next].X) {  // 3831-3841
-                E[Cur].Next = E[Next].Next;
-                E[Next].Next = Cur;
-                if (PrevNext >= 0) E[PrevNext].Next = Next;
+            lk.stepped(Cur);
+            lk.stepped(Next);
+            if (lk.x(Cur) > lk.x(Next)) {  // 3831-3841
+                lk.set_next(Cur, lk.next(Next));
+                lk.set_next(Next, Cur);
+                if (PrevNext >= 0) lk.set_next(PrevNext, Next);
                 else Head = Next;               // P3
                 if (Tail == Next) Tail = Cur;   // P3
                 Cur = Next;
-                Next = E[Cur].Next;
+                Next = lk.next(Cur);
             }
             if (PrevNext >= 0) {  // 3843-3853
-                if (E[PrevNext].X > E[Cur].X) {
-                    E[PrevNext].Next = E[Cur].Next;
-                    E[Cur].Next = PrevNext;
-                    E[PrevCur].Next = Cur;
+                if (lk.x(PrevNext) > lk.x(Cur)) {
+                    lk.set_next(PrevNext, lk.next(Cur));
+                    lk.set_next(Cur, PrevNext);
+                    lk.set_next(PrevCur, Cur);
                     PrevNext = Cur;
-                    Cur = E[PrevNext].Next;
+                    Cur = lk.next(PrevNext);
                 }
             }
             PrevCur = Cur;
             PrevNext = Next;
-            if (E[Next].Next >= 0) {
-                Cur = E[Next].Next;
-                Next = E[Cur].Next;
+            if (lk.next(Next) >= 0) {
+                Cur = lk.next(Next);
+                Next = lk.next(Cur);
             } else {
                 Next = -1;
             }
@@ -654,7 +696,10 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
     }
 }
 
-__global__ void __launch_bounds__(64) k_obj_walk(FrameParams fp, const ObjDesc *__restrict__ objs, uint32_t nobj,
+#ifndef PRK_OBJ_LDS_LINKS
+#define PRK_OBJ_LDS_LINKS 1
+#endif
+__global__ void __launch_bounds__(kLinkThreads) k_obj_walk(FrameParams fp, const ObjDesc *__restrict__ objs, uint32_t nobj,
                                                  const uint32_t *__restrict__ escan,
                                                  const uint32_t *__restrict__ total0p, ObjEdge *__restrict__ work,
                                                  const unsigned long long *__restrict__ soff,
@@ -678,10 +723,28 @@ __global__ void __launch_bounds__(64) k_obj_walk(FrameParams fp, const ObjDesc *
     uint32_t e0, n;
     obj_range(od, escan, *total0p, e0, n);
     ObjEdge *E = work + e0;
+    __shared__ LinkLds lds;
+    // (triangle edges only: their Left is 0 / 1, a caller's edge_info.Left any b32)
+    const bool in_lds = PRK_OBJ_LDS_LINKS && od.kind == 0 && n <= (uint32_t)kLinkCap;
+    if (in_lds) {  // the list fields' mirrors
+        const int lane = (int)threadIdx.x;
+        for (uint32_t i = 0; i < n; ++i) {
+            const int a = (int)i * kLinkThreads + lane;
+            lds.x[a] = E[i].X;
+            lds.g[a] = E[i].G;
+            lds.ymin[a] = E[i].YMin;
+            lds.ymax[a] = E[i].YMax;
+            lds.left[a] = (int8_t)E[i].Left;
+        }
+    }
     switch (d.mode) {
-#define PRK_WALK_OBJ(MM)                                                                         \
-    case MM:                                                                                     \
-        walk_object<MM>(fp, od, d, E, n, base, bound, recs, srecs, pos, span_tri, err);          \
+#define PRK_WALK_OBJ(MM)                                                                                 \
+    case MM:                                                                                             \
+        if (in_lds)                                                                                      \
+            walk_object<MM>(fp, od, d, E, n, base, bound, recs, srecs, pos, span_tri, err,               \
+                            LLinks{&lds, (int)threadIdx.x});                                             \
+        else                                                                                             \
+            walk_object<MM>(fp, od, d, E, n, base, bound, recs, srecs, pos, span_tri, err, GLinks{E});   \
         break;
         PRK_WALK_OBJ(MODE_AVX)
         PRK_WALK_OBJ(MODE_SC_GOURAUD)
