@@ -55,8 +55,9 @@ hipError_t prk_obj_bound(const prk::FrameParams *, const void *, uint32_t, const
                          unsigned long long *, hipStream_t);
 uint32_t prk_obj_walk_lcap(void);
 hipError_t prk_obj_walk(const prk::FrameParams *, const void *, uint32_t, const uint32_t *, const uint32_t *, void *,
-                        const unsigned long long *, void *, void *, void *, uint32_t *, const void *, uint32_t *,
+                        const unsigned long long *, void *, void *, void *, uint32_t *, const void *, uint32_t *, int,
                         hipStream_t);
+uint32_t prk_obj_link_cap(void);
 hipError_t prk_obj_maxact(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, const uint32_t *,
                           const uint32_t *, const void *, int32_t *, hipStream_t);
 uint32_t prk_obj_walk_threads(uint32_t);
@@ -1465,6 +1466,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     S.h_big_cap.clear();
     S.h_k1src.clear();
     uint64_t ntri = 0, nk1 = 0, pool = 0, maxn = 1;
+    bool thread_links = false;  // a thread-walked triangle object small enough for LDS list links
     std::vector<uint32_t> bigm[prk::MODE_COUNT], bige[prk::MODE_COUNT];  // wave-walked objects by mode, their edges
     for (uint32_t di = 0; di < draws.size(); ++di) {
         const prk::DrawRec &d = draws[di];
@@ -1482,6 +1484,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
                 const uint64_t edges = 3ull * n;  // the most its FillEdgeTable writes
                 maxn = std::max(maxn, edges);
                 const bool wave = n >= kObjWaveTris;
+                thread_links = thread_links || (!wave && edges <= prk_obj_link_cap());
                 if (wave) {
                     bigm[d.mode].push_back((uint32_t)S.h_objs.size());
                     bige[d.mode].push_back((uint32_t)edges);
@@ -1702,7 +1705,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     }
     PRK_TRY(prk_obj_walk(&fp, d_objs, nobj, escan, total0p, S.d_work.p, oslot, S.d_recs.p,
                          scalar ? S.d_srecs.p : nullptr, S.d_pos.p, (uint32_t *)S.d_span_tri.p, d_spans_in,
-                         (uint32_t *)S.d_err.p, s));
+                         (uint32_t *)S.d_err.p, thread_links ? 1 : 0, s));
     for (const Group &g : groups)
         PRK_TRY(prk_obj_walk_group(&fp, g.mode, g.lcap, d_objs, d_cbig + g.start, d_coff + g.start, d_ccap + g.start,
                                    g.count, (int32_t *)S.d_pool.p, escan, total0p, S.d_work.p, oslot, S.d_recs.p,

@@ -699,6 +699,9 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
 #ifndef PRK_OBJ_LDS_LINKS
 #define PRK_OBJ_LDS_LINKS 1
 #endif
+// LINKS: the launch holds triangle objects small enough for LDS links (the
+// 58-KB mirror is allocated only then: it limits a CU to two workgroups).
+template <bool LINKS>
 __global__ void __launch_bounds__(kLinkThreads) k_obj_walk(FrameParams fp, const ObjDesc *__restrict__ objs, uint32_t nobj,
                                                  const uint32_t *__restrict__ escan,
                                                  const uint32_t *__restrict__ total0p, ObjEdge *__restrict__ work,
@@ -723,9 +726,10 @@ __global__ void __launch_bounds__(kLinkThreads) k_obj_walk(FrameParams fp, const
     uint32_t e0, n;
     obj_range(od, escan, *total0p, e0, n);
     ObjEdge *E = work + e0;
-    __shared__ LinkLds lds;
+    __shared__ typename std::conditional<LINKS, LinkLds, char>::type lds_;
+    LinkLds &lds = *reinterpret_cast<LinkLds *>(&lds_);
     // (triangle edges only: their Left is 0 / 1, a caller's edge_info.Left any b32)
-    const bool in_lds = PRK_OBJ_LDS_LINKS && od.kind == 0 && n <= (uint32_t)kLinkCap;
+    const bool in_lds = LINKS && od.kind == 0 && n <= (uint32_t)kLinkCap;
     if (in_lds) {  // the list fields' mirrors
         const int lane = (int)threadIdx.x;
         for (uint32_t i = 0; i < n; ++i) {
@@ -1973,15 +1977,22 @@ uint32_t prk_obj_walk_lcap(void) {
 // The object walk: a thread per small object or caller edge list ...
 hipError_t prk_obj_walk(const prk::FrameParams *fp, const void *objs, uint32_t nobj, const uint32_t *escan,
                         const uint32_t *total0p, void *work, const unsigned long long *soff, void *recs, void *srecs,
-                        void *pos, uint32_t *span_tri, const void *spans_in, uint32_t *err, hipStream_t s) {
+                        void *pos, uint32_t *span_tri, const void *spans_in, uint32_t *err, int links,
+                        hipStream_t s) {
     if (nobj == 0) return hipSuccess;
-    hipLaunchKernelGGL(prk::k_obj_walk, dim3((nobj + 63) / 64), dim3(64), 0, s, *fp,
-                       reinterpret_cast<const prk::ObjDesc *>(objs), nobj, escan, total0p,
-                       reinterpret_cast<prk::ObjEdge *>(work), soff, reinterpret_cast<prk::SpanRecG *>(recs),
-                       reinterpret_cast<prk::ScSpanRecG *>(srecs), reinterpret_cast<prk::SpanPos *>(pos), span_tri,
-                       reinterpret_cast<const prk::SpanIn *>(spans_in), err);
+#define PRK_OBJ_WALK_LAUNCH(LK)                                                                                    \
+    hipLaunchKernelGGL(prk::k_obj_walk<LK>, dim3((nobj + prk::kLinkThreads - 1) / prk::kLinkThreads),              \
+                       dim3(prk::kLinkThreads), 0, s, *fp, reinterpret_cast<const prk::ObjDesc *>(objs), nobj, escan, \
+                       total0p, reinterpret_cast<prk::ObjEdge *>(work), soff,                                      \
+                       reinterpret_cast<prk::SpanRecG *>(recs), reinterpret_cast<prk::ScSpanRecG *>(srecs),        \
+                       reinterpret_cast<prk::SpanPos *>(pos), span_tri,                                            \
+                       reinterpret_cast<const prk::SpanIn *>(spans_in), err)
+    if (links && PRK_OBJ_LDS_LINKS) PRK_OBJ_WALK_LAUNCH(true);
+    else PRK_OBJ_WALK_LAUNCH(false);
+#undef PRK_OBJ_WALK_LAUNCH
     return hipGetLastError();
 }
+uint32_t prk_obj_link_cap(void) { return (uint32_t)prk::kLinkCap; }
 // ... the most active entries of the large ones (big[0, nbig)) ...
 hipError_t prk_obj_maxact(const prk::FrameParams *fp, const void *objs, const uint32_t *big, uint32_t nbig,
                           const uint32_t *escan, const uint32_t *total0p, const void *work, int32_t *most,
