@@ -535,21 +535,26 @@ struct GLinks {
 };
 constexpr int kLinkCap = 48;     // edges per object with LDS links (C3b as 16-triangle objects: 48)
 constexpr int kLinkThreads = 64;  // k_obj_walk's workgroup
+// 13 B per edge (YMax relative to the object's first row; YMin is read from
+// the working copy, only where the sorted insertion scan advances), so four
+// 64-thread workgroups fit a CU's LDS.
 struct LinkLds {
     float x[kLinkCap * kLinkThreads], g[kLinkCap * kLinkThreads];
-    int32_t ymin[kLinkCap * kLinkThreads], ymax[kLinkCap * kLinkThreads];
+    int16_t ymax[kLinkCap * kLinkThreads];
     int16_t nxt[kLinkCap * kLinkThreads];
     int8_t left[kLinkCap * kLinkThreads];
 };
 struct LLinks {
     LinkLds *L;
+    const ObjEdge *E;
     int lane;
+    int32_t row0;  // the object's first row: YMax - row0 in (0, 32767]
     __device__ __forceinline__ int at(int i) const { return i * kLinkThreads + lane; }
     __device__ __forceinline__ int32_t next(int i) const { return L->nxt[at(i)]; }
     __device__ __forceinline__ void set_next(int i, int32_t v) const { L->nxt[at(i)] = (int16_t)v; }
     __device__ __forceinline__ float x(int i) const { return L->x[at(i)]; }
-    __device__ __forceinline__ int32_t ymin(int i) const { return L->ymin[at(i)]; }
-    __device__ __forceinline__ int32_t ymax(int i) const { return L->ymax[at(i)]; }
+    __device__ __forceinline__ int32_t ymin(int i) const { return E[i].YMin; }
+    __device__ __forceinline__ int32_t ymax(int i) const { return row0 + (int32_t)L->ymax[at(i)]; }
     __device__ __forceinline__ bool before(int a, int b) const {
         const float ax = x(a), bx = x(b), ag = L->g[at(a)], bg = L->g[at(b)];
         return ax < bx || (ax == bx && (ag < bg || (ag == bg && L->left[at(a)] < L->left[at(b)])));
@@ -582,19 +587,20 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
     for (uint32_t i = 0; i < n; ++i) lk.set_next((int)i, -1);
     int32_t Head = -1, Tail = -1;
     uint32_t ins = 0;  // next sorted edge to insert (sorted by YMin)
+    int32_t nym = FirstRow;  // its YMin (INT32_MAX past the end)
     for (int32_t Row = FirstRow; Row < MaxY; ++Row) {
         // insertion (3654-3713): the edges with YMin == Row, in array
         // order.  Sorted lists (MergeSort) hold them contiguously; a
         // caller's list is scanned whole, as the reference does.
         uint32_t i0 = 0, i1 = n;
         if (!given) {
-            while (ins < n && lk.ymin((int)ins) < Row) ++ins;
+            while (ins < n && nym < Row) nym = ++ins < n ? lk.ymin((int)ins) : INT32_MAX;
             i0 = ins;
-            while (ins < n && lk.ymin((int)ins) == Row) ++ins;
+            while (ins < n && nym == Row) nym = ++ins < n ? lk.ymin((int)ins) : INT32_MAX;
             i1 = ins;
         }
         for (uint32_t ii = i0; ii < i1; ++ii) {
-            if (lk.ymin((int)ii) != Row) continue;
+            if (given && lk.ymin((int)ii) != Row) continue;  // (sorted: all of [i0, i1) start here)
             const int32_t c = (int32_t)ii;
             if (Head >= 0) {
                 if (lk.before(c, Head)) {
@@ -632,7 +638,7 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
             // nothing happens on the rows before the next insertion: go there
             if (!given) {
                 if (ins >= n) break;
-                Row = max(Row, lk.ymin((int)ins) - 1);
+                Row = max(Row, nym - 1);
             }
             continue;
         }
@@ -700,7 +706,7 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
 #define PRK_OBJ_LDS_LINKS 1
 #endif
 // LINKS: the launch holds triangle objects small enough for LDS links (the
-// 58-KB mirror is allocated only then: it limits a CU to two workgroups).
+// 40-KB mirror is allocated only then: it limits a CU to four workgroups).
 template <bool LINKS>
 __global__ void __launch_bounds__(kLinkThreads) k_obj_walk(FrameParams fp, const ObjDesc *__restrict__ objs, uint32_t nobj,
                                                  const uint32_t *__restrict__ escan,
@@ -729,15 +735,20 @@ __global__ void __launch_bounds__(kLinkThreads) k_obj_walk(FrameParams fp, const
     __shared__ typename std::conditional<LINKS, LinkLds, char>::type lds_;
     LinkLds &lds = *reinterpret_cast<LinkLds *>(&lds_);
     // (triangle edges only: their Left is 0 / 1, a caller's edge_info.Left any b32)
-    const bool in_lds = LINKS && od.kind == 0 && n <= (uint32_t)kLinkCap;
+    bool in_lds = LINKS && od.kind == 0 && n > 0 && n <= (uint32_t)kLinkCap;
+    const int32_t row0 = n ? E[0].YMin : 0;  // (sorted: the smallest YMin)
+    if (in_lds) {
+        int32_t hi = row0;
+        for (uint32_t i = 0; i < n; ++i) hi = max(hi, E[i].YMax);
+        in_lds = hi - row0 <= 32767;
+    }
     if (in_lds) {  // the list fields' mirrors
         const int lane = (int)threadIdx.x;
         for (uint32_t i = 0; i < n; ++i) {
             const int a = (int)i * kLinkThreads + lane;
             lds.x[a] = E[i].X;
             lds.g[a] = E[i].G;
-            lds.ymin[a] = E[i].YMin;
-            lds.ymax[a] = E[i].YMax;
+            lds.ymax[a] = (int16_t)(E[i].YMax - row0);
             lds.left[a] = (int8_t)E[i].Left;
         }
     }
@@ -746,7 +757,7 @@ __global__ void __launch_bounds__(kLinkThreads) k_obj_walk(FrameParams fp, const
     case MM:                                                                                             \
         if (in_lds)                                                                                      \
             walk_object<MM>(fp, od, d, E, n, base, bound, recs, srecs, pos, span_tri, err,               \
-                            LLinks{&lds, (int)threadIdx.x});                                             \
+                            LLinks{&lds, E, (int)threadIdx.x, row0});                                    \
         else                                                                                             \
             walk_object<MM>(fp, od, d, E, n, base, bound, recs, srecs, pos, span_tri, err, GLinks{E});   \
         break;
