@@ -532,6 +532,7 @@ struct GLinks {
     __device__ __forceinline__ int32_t ymax(int i) const { return E[i].YMax; }
     __device__ __forceinline__ bool before(int a, int b) const { return obj_before(E[a], E[b]); }
     __device__ __forceinline__ void stepped(int) const {}  // (obj_step stepped E[i].X)
+    static constexpr bool kCache = false;  // (the list reads the records' X and links)
 };
 constexpr int kLinkCap = 48;     // edges per object with LDS links (C3b as 16-triangle objects: 48)
 constexpr int kLinkThreads = 64;  // k_obj_walk's workgroup
@@ -560,7 +561,59 @@ struct LLinks {
         return ax < bx || (ax == bx && (ag < bg || (ag == bg && L->left[at(a)] < L->left[at(b)])));
     }
     __device__ __forceinline__ void stepped(int i) const { L->x[at(i)] += L->g[at(i)]; }  // E.X += E.G (obj_step)
+#ifndef PRK_OBJ_PAIR_CACHE
+#define PRK_OBJ_PAIR_CACHE 1
+#endif
+    static constexpr bool kCache = PRK_OBJ_PAIR_CACHE;
 };
+
+// An edge record held in seven named float4 registers (ObjEdge's layout): a
+// loop-carried ObjEdge went to scratch.
+#define PRK_ER(w) float4 w##0, w##1, w##2, w##3, w##4, w##5, w##6
+#define PRK_ER_ZERO(w) \
+    do { w##0 = w##1 = w##2 = w##3 = w##4 = w##5 = w##6 = make_float4(0.0f, 0.0f, 0.0f, 0.0f); } while (0)
+#define PRK_ER_LOAD(w, p)                                                      \
+    do {                                                                       \
+        const float4 *s_ = reinterpret_cast<const float4 *>(p);               \
+        w##0 = s_[0]; w##1 = s_[1]; w##2 = s_[2]; w##3 = s_[3];               \
+        w##4 = s_[4]; w##5 = s_[5]; w##6 = s_[6];                             \
+    } while (0)
+#define PRK_ER_STORE(p, w)                                                     \
+    do {                                                                       \
+        float4 *d_ = reinterpret_cast<float4 *>(p);                           \
+        d_[0] = w##0; d_[1] = w##1; d_[2] = w##2; d_[3] = w##3;               \
+        d_[4] = w##4; d_[5] = w##5; d_[6] = w##6;                             \
+    } while (0)
+#define PRK_ER_SWAP(a, b)                                                                 \
+    do {                                                                                  \
+        float4 t_;                                                                        \
+        t_ = a##0; a##0 = b##0; b##0 = t_; t_ = a##1; a##1 = b##1; b##1 = t_;             \
+        t_ = a##2; a##2 = b##2; b##2 = t_; t_ = a##3; a##3 = b##3; b##3 = t_;             \
+        t_ = a##4; a##4 = b##4; b##4 = t_; t_ = a##5; a##5 = b##5; b##5 = t_;             \
+        t_ = a##6; a##6 = b##6; b##6 = t_;                                                \
+    } while (0)
+__device__ __forceinline__ ObjEdge er_edge(float4 q0, float4 q1, float4 q2, float4 q3, float4 q4, float4 q5,
+                                           float4 q6) {
+    ObjEdge e;
+    e.X = q0.x; e.G = q0.y; e.Z = q0.z; e.ZG = q0.w;
+    e.W = q1.x; e.WG = q1.y; e.U = q1.z; e.UG = q1.w;
+    e.V = q2.x; e.VG = q2.y; e.N0 = q2.z; e.N1 = q2.w;
+    e.N2 = q3.x; e.NG0 = q3.y; e.NG1 = q3.z; e.NG2 = q3.w;
+    e.YMin = __float_as_int(q4.x); e.YMax = __float_as_int(q4.y); e.Left = __float_as_int(q4.z);
+    e.Next = __float_as_int(q4.w);
+    e.C0 = q5.x; e.C1 = q5.y; e.C2 = q5.z; e.C3 = q5.w;
+    e.CG0 = q6.x; e.CG1 = q6.y; e.CG2 = q6.z; e.CG3 = q6.w;
+    return e;
+}
+#define PRK_ER_EDGE(w) er_edge(w##0, w##1, w##2, w##3, w##4, w##5, w##6)
+#define PRK_ER_FROM(w, e)                                                                              \
+    do {                                                                                               \
+        w##0 = make_float4((e).X, (e).G, (e).Z, (e).ZG);                                               \
+        w##1 = make_float4((e).W, (e).WG, (e).U, (e).UG);                                              \
+        w##2 = make_float4((e).V, (e).VG, (e).N0, (e).N1);                                             \
+        w##3 = make_float4((e).N2, (e).NG0, (e).NG1, (e).NG2);                                         \
+        w##5 = make_float4((e).C0, (e).C1, (e).C2, (e).C3);                                            \
+    } while (0)  /* (q4, q6: row range, link, colour gradient — not stepped) */
 
 // The AET walk of one object by one thread (small objects, caller edge
 // lists): E = its n edges, sorted (kind 0) or as given (kind 1).  Its spans
@@ -588,6 +641,15 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
     int32_t Head = -1, Tail = -1;
     uint32_t ins = 0;  // next sorted edge to insert (sorted by YMin)
     int32_t nym = FirstRow;  // its YMin (INT32_MAX past the end)
+    // (LK::kCache) the last pair's records, stepped in registers, written back
+    // when another pair needs the registers (the list fields live in LK, so
+    // nothing reads a record's stale copy meanwhile; the working copy is not
+    // read after the walk)
+    PRK_ER(ca);
+    PRK_ER(cb);
+    PRK_ER_ZERO(ca);
+    PRK_ER_ZERO(cb);
+    int32_t ia = -1, ib = -1;
     for (int32_t Row = FirstRow; Row < MaxY; ++Row) {
         // insertion (3654-3713): the edges with YMin == Row, in array
         // order.  Sorted lists (MergeSort) hold them contiguously; a
@@ -662,14 +724,47 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
         int32_t PrevCur = -1, PrevNext = -1;  // pairing 3751-3869
         int32_t Cur = Head, Next = lk.next(Cur);
         while (Next >= 0) {
-            if (Row >= RowLo &&  // a span of this pass's rows (3759-3809 / 298-538)
-                emit_span<M>(fp, E[Cur], E[Next], Row, d, st, od.g0, emitted < bound, base + emitted, recs, srecs,
-                             pos, span_tri)) {
-                if (emitted >= bound) atomicOr(err, 2u);  // (never: the bound holds every span)
-                ++emitted;
+            if constexpr (LK::kCache) {
+                // the pair's records: in registers while the same two edges
+                // pair row after row (either order), else written back and
+                // the new pair's loaded
+                if (!(Cur == ia && Next == ib)) {
+                    if (Cur == ib && Next == ia) {
+                        PRK_ER_SWAP(ca, cb);
+                        ib = ia;
+                        ia = Cur;
+                    } else {
+                        if (ia >= 0) {
+                            PRK_ER_STORE(&E[ia], ca);
+                            PRK_ER_STORE(&E[ib], cb);
+                        }
+                        PRK_ER_LOAD(ca, &E[Cur]);
+                        PRK_ER_LOAD(cb, &E[Next]);
+                        ia = Cur;
+                        ib = Next;
+                    }
+                }
+                ObjEdge eA = PRK_ER_EDGE(ca), eB = PRK_ER_EDGE(cb);
+                if (Row >= RowLo &&  // a span of this pass's rows (3759-3809 / 298-538)
+                    emit_span<M>(fp, eA, eB, Row, d, st, od.g0, emitted < bound, base + emitted, recs, srecs, pos,
+                                 span_tri)) {
+                    if (emitted >= bound) atomicOr(err, 2u);  // (never: the bound holds every span)
+                    ++emitted;
+                }
+                obj_step<M>(eA);  // 3811-3829
+                obj_step<M>(eB);
+                PRK_ER_FROM(ca, eA);
+                PRK_ER_FROM(cb, eB);
+            } else {
+                if (Row >= RowLo &&
+                    emit_span<M>(fp, E[Cur], E[Next], Row, d, st, od.g0, emitted < bound, base + emitted, recs,
+                                 srecs, pos, span_tri)) {
+                    if (emitted >= bound) atomicOr(err, 2u);
+                    ++emitted;
+                }
+                obj_step<M>(E[Cur]);
+                obj_step<M>(E[Next]);
             }
-            obj_step<M>(E[Cur]);  // 3811-3829
-            obj_step<M>(E[Next]);
             lk.stepped(Cur);
             lk.stepped(Next);
             if (lk.x(Cur) > lk.x(Next)) {  // 3831-3841
@@ -708,7 +803,7 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
 // LINKS: the launch holds triangle objects small enough for LDS links (the
 // 40-KB mirror is allocated only then: it limits a CU to four workgroups).
 template <bool LINKS>
-__global__ void __launch_bounds__(kLinkThreads) k_obj_walk(FrameParams fp, const ObjDesc *__restrict__ objs, uint32_t nobj,
+__global__ void __launch_bounds__(kLinkThreads, 1) k_obj_walk(FrameParams fp, const ObjDesc *__restrict__ objs, uint32_t nobj,
                                                  const uint32_t *__restrict__ escan,
                                                  const uint32_t *__restrict__ total0p, ObjEdge *__restrict__ work,
                                                  const unsigned long long *__restrict__ soff,
