@@ -540,10 +540,13 @@ def test_whole_object_narrow_tiles(gpu, tile):
     compare(g2, O.render(s2, tris_per_object=5), label="objects %dx%d" % tile)
 
 
-@pytest.mark.parametrize("tpo,seed", [(2, 1), (5, 2), (16, 3)])
+@pytest.mark.parametrize("tpo,seed", [(2, 1), (5, 2), (16, 3), (24, 4), (40, 5)])
 def test_whole_object_random_objects(gpu, tpo, seed):
     """Random objects of several triangles, clipped on every side, with ties:
-    spans across unrelated triangles, crossing swaps, expiry mid-list."""
+    spans across unrelated triangles, crossing swaps, expiry mid-list.  The
+    thread walk keeps the list in LDS for objects of up to 48 edges and the
+    walked pair's records in registers (dense rows evict them pair by pair);
+    24 and 40 triangles mix objects under and over that size in one launch."""
     s = scenes.with_ties(scenes.random_soup(3000, 256, 256, radius=30, seed=seed, centroid_margin=30), seed=seed)
     run_both(s, tris_per_object=tpo)
 
