@@ -131,6 +131,14 @@ def cpu_topology():
                 host_cpus=os.cpu_count())
 
 
+def _cpu_share(threads, topo):
+    """The CPUs the baseline actually had: its thread count, capped by the
+    cgroup CPU quota (on the GPU box 16 CPUs of a 256-CPU host: 64 threads
+    there time-share 16 CPUs' worth)."""
+    q = topo.get("cgroup_cpu_quota")
+    return min(float(threads), float(q)) if q else float(threads)
+
+
 def cpu_baseline(scene, threads, max_tris, frames=3, scan=(16, 64)):
     """The CPU path on the same scene, on the host cores (SURVEY §8(d) "CPU
     path timing"): the AVX2 restatement (oracle/prk_cpu_avx.c, bit-exact to
@@ -160,7 +168,8 @@ def cpu_baseline(scene, threads, max_tris, frames=3, scan=(16, 64)):
         t0 = time.perf_counter()
         _, _, _, st = O.render(sub, semantics=abi.PRK_SEM_AVX, phong=True, threads=threads, winners=False)
         frame = (time.perf_counter() - t0) * (T / n)
-        return dict(value=px / frame / 1e6, unit="Mpixels/s", cores=threads, kind="port",
+        return dict(value=px / frame / 1e6, unit="Mpixels/s", cores=_cpu_share(threads, topo), threads=threads,
+                    kind="port",
                     sample="scalar oracle (no AVX2 on this host), %d of %d triangles, banded over %d threads"
                            % (n, T, threads), frame_s=frame, span_pixels=st["span_pixels"] if n == T else None,
                     **topo)
@@ -201,7 +210,7 @@ def cpu_baseline(scene, threads, max_tris, frames=3, scan=(16, 64)):
                            "sample": "first %d triangles, median of 2 frames, scaled to T" % nq}
     best = min(variants, key=lambda k: variants[k]["frame_ms"])
     frame = variants[best]["frame_ms"] * 1e-3
-    return dict(value=px / frame / 1e6, unit="Mpixels/s", cores=tbest, kind="port",
+    return dict(value=px / frame / 1e6, unit="Mpixels/s", cores=_cpu_share(tbest, topo), threads=tbest, kind="port",
                 sample="AVX2 restatement of FillLineOptimized (oracle/prk_cpu_avx.c); banded schedule scanned "
                        "over %s threads (%d = every CPU of the affinity mask), value = fastest schedule (%s) at "
                        "the fastest count (%d threads); banded: %s; queue/rows: %s"

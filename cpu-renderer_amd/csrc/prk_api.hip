@@ -8,8 +8,12 @@
 // There is no CPU fallback: every entry point that computes pixels needs the
 // HIP device and fails with PRK_ERR_DEVICE without one.
 #include <hip/hip_runtime.h>
+#include <link.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
+#include <string>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -28,6 +32,7 @@ uint32_t prk_cs_chunks(uint32_t);
 uint32_t prk_cs_nchunks(uint32_t, uint32_t);
 uint32_t prk_cs_band_runs_per_chunk(const prk::FrameParams *);
 uint32_t prk_bin_runs(uint32_t);
+uint32_t prk_bin_run_len(void);
 uint32_t prk_cs_max_tiles(void);
 uint32_t prk_cs_max_pairs(void);
 int prk_cs_ready(uint32_t);
@@ -164,9 +169,13 @@ struct prk_context {
     float *zbuf = nullptr;
     int32_t W = 0, H = 0, row0 = 0, row1 = 0;
     bool owns_target = false;
-    // camera + lights
+    // camera + lights: transform / lights set the draws up (FillEdgeTable's
+    // ProjectVertex and Gouraud lighting), shade_* shade their spans (Phong and
+    // UnprojectVertex, read when DrawModel* runs); prk_set_camera sets both
     prk_transform transform{};
     prk_light_data lights{};
+    prk_transform shade_transform{};
+    prk_light_data shade_lights{};
     bool have_camera = false;
     bool clear_pending = false;  // prk_target_clear_on_flush
     uint32_t clear_color = 0;
@@ -251,8 +260,8 @@ struct prk_context {
         int32_t pitch = 0;
         float *zbuf = nullptr;
         int32_t W = 0, H = 0, row0 = 0, row1 = 0, tile_w = 0, tile_h = 0;
-        prk_transform transform{};
-        prk_light_data lights{};
+        prk_transform transform{}, shade_transform{};
+        prk_light_data lights{}, shade_lights{};
         uint32_t clear_color = 0;
         float clear_z = 0.0f;
     } pcount;
@@ -294,7 +303,53 @@ static int resolve_count(prk_context *c);
         if (_e != hipSuccess) return status_of(_e); \
     } while (0)
 
+// ---- one ROCm runtime per process (prk.h prk_create) ------
+namespace {
+struct MapScan {
+    std::vector<std::string> hip, smi;  // distinct mapped files of each library
+};
+int scan_object(struct dl_phdr_info *info, size_t, void *data) {
+    MapScan &m = *static_cast<MapScan *>(data);
+    const char *path = info->dlpi_name;
+    if (!path || !*path) return 0;
+    const char *base = std::strrchr(path, '/');
+    base = base ? base + 1 : path;
+    std::vector<std::string> *v = nullptr;
+    if (std::strncmp(base, "libamdhip64", 11) == 0) v = &m.hip;
+    else if (std::strncmp(base, "librocm_smi64", 13) == 0) v = &m.smi;
+    if (!v) return 0;
+    char real[4096];
+    const std::string key = realpath(path, real) ? std::string(real) : std::string(path);
+    if (std::find(v->begin(), v->end(), key) == v->end()) v->push_back(key);
+    return 0;
+}
+// Runs before the destructors of every library loaded earlier (exit handlers
+// run last-registered first): ends the process with its own exit status
+// before the duplicated librocm_smi64 destructors free one map twice.
+void exit_guard(int status, void *) {
+    std::fflush(nullptr);
+    _exit(status);
+}
+std::atomic<bool> g_guarded{false};
+}  // namespace
+
 extern "C" {
+
+int prk_runtime_check(void) {
+    MapScan m;
+    dl_iterate_phdr(scan_object, &m);
+    if (m.hip.size() <= 1 && m.smi.size() <= 1) return PRK_OK;
+    if (!g_guarded.exchange(true)) {
+        std::fprintf(stderr,
+                     "prk: %zu copies of libamdhip64 and %zu of librocm_smi64 are mapped in this process (e.g. "
+                     "/opt/rocm's, loaded with libprk_hip.so, and torch's own): load torch (or the framework that "
+                     "ships its own ROCm) BEFORE libprk_hip.so (INTEGRATION.md, 'One ROCm stack per process'); "
+                     "the process will end at exit before their destructors run\n",
+                     m.hip.size(), m.smi.size());
+        on_exit(exit_guard, nullptr);
+    }
+    return PRK_ERR_RUNTIME_MIX;
+}
 
 const char *prk_version(void) { return "prk 0.1 (gfx950)"; }
 
@@ -327,6 +382,10 @@ int prk_selftest_div(int32_t device, uint32_t n, uint64_t seed, uint64_t *mismat
 int prk_create(int device, prk_context **out) {
     if (!out) return PRK_ERR_ARG;
     *out = nullptr;
+    {
+        const int rc = prk_runtime_check();
+        if (rc != PRK_OK) return rc;
+    }
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return PRK_ERR_DEVICE;
     if (device < 0 || device >= n) return PRK_ERR_ARG;
@@ -364,6 +423,7 @@ int prk_create(int device, prk_context **out) {
 
 int prk_destroy(prk_context *c) {
     if (!c) return PRK_ERR_ARG;
+    (void)prk_runtime_check();  // (a runtime loaded since prk_create: guard the exit)
     // Destroy never queues GPU work: a frame whose bin count was never read
     // (PendingCount) is dropped, not re-run — its target may already belong
     // to someone else (a torch tensor freed at interpreter exit, a peer
@@ -580,7 +640,17 @@ int prk_set_camera(prk_context *c, const prk_transform *t, const prk_light_data 
     if (!c || !t || !l || l->LightCount > PRK_MAX_LIGHTS) return PRK_ERR_ARG;
     c->transform = *t;
     c->lights = *l;
+    c->shade_transform = *t;
+    c->shade_lights = *l;
     c->have_camera = true;
+    return PRK_OK;
+}
+
+int prk_set_shade_camera(prk_context *c, const prk_transform *t, const prk_light_data *l) {
+    if (!c || !t || !l || l->LightCount > PRK_MAX_LIGHTS) return PRK_ERR_ARG;
+    if (!c->have_camera) return PRK_ERR_ARG;  // the setup camera first (prk_set_camera)
+    c->shade_transform = *t;
+    c->shade_lights = *l;
     return PRK_OK;
 }
 
@@ -1069,6 +1139,27 @@ static void frame_params(const prk_context *c, prk::FrameParams &fp) {
         for (int k = 0; k < 3; ++k) fp.lp[l][k] = c->lights.Lights[l].P[k];
         for (int k = 0; k < 4; ++k) fp.li[l][k] = c->lights.Lights[l].Intensity[k];
     }
+    // the span shading's camera and lights (prk_set_shade_camera)
+    {
+        const prk_transform &t = c->shade_transform;
+        const prk_light_data &L = c->shade_lights;
+        prk::ShadeCam &sh = fp.sh;
+        sh.D = t.DistanceAboveTarget;
+        sh.F = t.FocalLength;
+        sh.Cx = t.ScreenCenter[0];
+        sh.Cy = t.ScreenCenter[1];
+        sh.InvM2P = 1.0f / t.MetersToPixels;
+        int e = 0;
+        const float m = std::frexp(sh.F, &e);  // F = m * 2^e, |m| in [0.5, 1)
+        sh.f_pow2 = (std::isfinite(sh.F) && (m == 0.5f || m == -0.5f) && e - 1 >= -125 && e - 1 <= 126) ? 1 : 0;
+        sh.InvF = sh.f_pow2 ? 1.0f / sh.F : 0.0f;
+        sh.light_count = L.LightCount;
+        for (int k = 0; k < 4; ++k) sh.amb[k] = L.AmbientIntensity[k];
+        for (uint32_t l = 0; l < PRK_MAX_LIGHTS; ++l) {
+            for (int k = 0; k < 3; ++k) sh.lp[l][k] = L.Lights[l].P[k];
+            for (int k = 0; k < 4; ++k) sh.li[l][k] = L.Lights[l].Intensity[k];
+        }
+    }
     fp.W = c->W;
     fp.H = c->H;
     fp.row0 = c->row0;
@@ -1249,7 +1340,7 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
         // a row band's sort walks only its triangles (listed per run by k_bin_band)
         const uint32_t per = prk_cs_band_runs_per_chunk(&fp);
         if (per) {
-            PRK_TRY(bset_ensure(B.d_runlist, (size_t)prk_bin_runs(T) * 2048 * 4));
+            PRK_TRY(bset_ensure(B.d_runlist, (size_t)prk_bin_runs(T) * prk_bin_run_len() * 4));
             PRK_TRY(bset_ensure(B.d_run_n, (size_t)prk_bin_runs(T) * 4));
         }
         const uint32_t nch = prk_cs_nchunks(T, per);
@@ -1374,6 +1465,7 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
         P.W = c->W; P.H = c->H; P.row0 = c->row0; P.row1 = c->row1;
         P.tile_w = c->tile_w; P.tile_h = c->tile_h;
         P.transform = c->transform; P.lights = c->lights;
+        P.shade_transform = c->shade_transform; P.shade_lights = c->shade_lights;
         P.clear_color = c->clear_color; P.clear_z = c->clear_z;
         P.active = true;
         if (!(defer && c->pair_hint)) return resolve_count(c);
@@ -1407,14 +1499,16 @@ static int resolve_count(prk_context *c) {
     // re-run with the pass's own state, then give the caller's back
     struct Saved {
         void *color; int32_t pitch; float *zbuf; int32_t W, H, row0, row1, tile_w, tile_h;
-        prk_transform transform; prk_light_data lights; uint32_t clear_color; float clear_z;
-        bool clear_pending, debug;
+        prk_transform transform, shade_transform; prk_light_data lights, shade_lights;
+        uint32_t clear_color; float clear_z; bool clear_pending, debug;
     } sv{c->color, c->pitch, c->zbuf, c->W, c->H, c->row0, c->row1, c->tile_w, c->tile_h,
-         c->transform, c->lights, c->clear_color, c->clear_z, c->clear_pending, c->debug};
+         c->transform, c->shade_transform, c->lights, c->shade_lights, c->clear_color, c->clear_z,
+         c->clear_pending, c->debug};
     c->color = P.color; c->pitch = P.pitch; c->zbuf = P.zbuf;
     c->W = P.W; c->H = P.H; c->row0 = P.row0; c->row1 = P.row1;
     c->tile_w = P.tile_w; c->tile_h = P.tile_h;
     c->transform = P.transform; c->lights = P.lights;
+    c->shade_transform = P.shade_transform; c->shade_lights = P.shade_lights;
     c->clear_color = P.clear_color; c->clear_z = P.clear_z;
     c->clear_pending = P.fuse;
     c->debug = P.debug;
@@ -1425,6 +1519,7 @@ static int resolve_count(prk_context *c) {
     c->W = sv.W; c->H = sv.H; c->row0 = sv.row0; c->row1 = sv.row1;
     c->tile_w = sv.tile_w; c->tile_h = sv.tile_h;
     c->transform = sv.transform; c->lights = sv.lights;
+    c->shade_transform = sv.shade_transform; c->shade_lights = sv.shade_lights;
     c->clear_color = sv.clear_color; c->clear_z = sv.clear_z;
     c->clear_pending = sv.clear_pending;
     c->debug = sv.debug;

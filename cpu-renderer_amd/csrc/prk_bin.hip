@@ -839,6 +839,7 @@ hipError_t prk_bin_count(const prk::FrameParams *fp, uint32_t *tri_n, void *rang
 // band's share of the triangles, so a narrow band has few chunks (and a
 // small chunk x tile histogram).  0: not a band (whole-frame chunks).
 uint32_t prk_bin_runs(uint32_t tri_count);
+uint32_t prk_bin_run_len(void);
 #ifndef PRK_BAND_MIN_CHUNKS
 #define PRK_BAND_MIN_CHUNKS 128  // > 0: at least about this many chunks (smaller ones) per band frame
                                  // (C3b N = 8: 31 chunks of 1024 threads left the sort on 31 CUs;
@@ -857,6 +858,8 @@ uint32_t prk_cs_band_runs_per_chunk(const prk::FrameParams *fp) {
     return (uint32_t)std::min<int64_t>(prk::kMaxRunsPerChunk, std::max<int64_t>(1, per));
 }
 uint32_t prk_bin_runs(uint32_t tri_count) { return (tri_count + 1 + prk::kRecRun - 1) / prk::kRecRun; }
+// Entries of one run of the band run list (k_bin_band writes runlist[run * this + i]).
+uint32_t prk_bin_run_len(void) { return prk::kRecRun; }
 
 // The counting sort's per-tile LDS (4 B per tile) above 64 KiB needs the
 // dynamic-LDS attribute of k_cs_hist / k_cs_emit, which is per device: set

@@ -110,16 +110,32 @@ struct TriRec {
 };
 static_assert(sizeof(TriRec) == 160, "TriRec is ten dwordx4");
 
-struct FrameParams {
-    // projective_transform
-    float D, F, M2P, Cx, Cy, InvM2P;
+// The camera and lights a span is shaded with: UnprojectVertex(_8x) and the
+// Phong loop read Commands->Transform / LightData when the span runs
+// (DrawModel 452-458, FillLineOptimized 2042-2046, the single-thread overload
+// 3030-3034), which need not be what FillEdgeTable saw (prk_set_shade_camera).
+struct ShadeCam {
+    float D, F, Cx, Cy, InvM2P;
     float InvF;       // 1/F, exact when f_pow2
     int32_t f_pow2;   // F = 2^k (k in [-125,126]): d/F == d*InvF bit for bit
-    // light_data
     uint32_t light_count;
     float amb[4];
     float lp[kMaxLights][3];
     float li[kMaxLights][4];
+};
+
+struct FrameParams {
+    // projective_transform and light_data of the setup (FillEdgeTable:
+    // ProjectVertex 3906-3910, Gouraud lighting 4020-4063)
+    float D, F, M2P, Cx, Cy, InvM2P;
+    float InvF;
+    int32_t f_pow2;
+    uint32_t light_count;
+    float amb[4];
+    float lp[kMaxLights][3];
+    float li[kMaxLights][4];
+    // ... and of the span shading
+    ShadeCam sh;
     // target band: frame rows [row0,row1) of a W x H frame
     int32_t W, H, row0, row1;
     int32_t pitch;   // colour pitch in bytes
@@ -295,9 +311,9 @@ __device__ __forceinline__ void div_all(float d, float (&x)[K]) {
 // d / F (the focal length divide of UnprojectVertex); F is uniform, so its
 // reciprocal half can be hoisted out of a thread's pixel loop.
 __device__ __forceinline__ float div_focal(const FrameParams &fp, float d) {
-    if (fp.f_pow2) return d * fp.InvF;
+    if (fp.sh.f_pow2) return d * fp.sh.InvF;
     float q[1] = {d};
-    div_all(fp.F, q);
+    div_all(fp.sh.F, q);
     return q[0];
 }
 

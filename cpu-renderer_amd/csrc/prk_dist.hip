@@ -172,6 +172,10 @@ int prk_comm_unique_id(void *id) {
 }
 
 int prk_comm_init(prk_context *ctx, const void *id, int32_t nranks, int32_t rank, prk_comm **out) {
+    {  // librccl (and its librocm_smi64) beside another framework's copies
+        const int rc = prk_runtime_check();
+        if (rc != PRK_OK) return rc;
+    }
     if (!ctx || !id || !out || nranks <= 0 || rank < 0 || rank >= nranks) return PRK_ERR_ARG;
     *out = nullptr;
     const Rccl &R = rccl();

@@ -396,19 +396,20 @@ __device__ __forceinline__ Texel4 sample_avx(const TexRec &tex, float fu, float 
 __device__ __forceinline__ uint32_t shade_avx_texel(const FrameParams &fp, const Texel4 &c4, float z, float n0,
                                                     float n1, float n2, int32_t x, int32_t i, int32_t Row) {
     const float CA = c4.a, CR = c4.r, CG = c4.g, CB = c4.b;
-    // Phong (2040-2128) at UnprojectVertex_8x (102-145).
-    const float d = fp.D - z;
+    // Phong (2040-2128) at UnprojectVertex_8x (102-145), with the shading camera
+    // (Commands as the span reads it, 2042-2046).
+    const float d = fp.sh.D - z;
     const float Xf = (float)(x - i) + (float)i, Yf = (float)Row + 0.0f;
-    const float AX = (Xf - fp.Cx) * fp.InvM2P, AY = (Yf - fp.Cy) * fp.InvM2P;
+    const float AX = (Xf - fp.sh.Cx) * fp.sh.InvM2P, AY = (Yf - fp.sh.Cy) * fp.sh.InvM2P;
     const float dF = div_focal(fp, d);
     const float PX = dF * AX, PY = dF * AY, PZ = z;
     float Fr = 0, Fg = 0, Fb = 0, Fa = 0;
-    for (uint32_t li = 0; li < fp.light_count; ++li) {
+    for (uint32_t li = 0; li < fp.sh.light_count; ++li) {
         if (li == 0) {
-            Fr = CR * fp.amb[0]; Fg = CG * fp.amb[1];
-            Fb = CB * fp.amb[2]; Fa = CA * fp.amb[3];
+            Fr = CR * fp.sh.amb[0]; Fg = CG * fp.sh.amb[1];
+            Fb = CB * fp.sh.amb[2]; Fa = CA * fp.sh.amb[3];
         }
-        float Lx = fp.lp[li][0] - PX, Ly = fp.lp[li][1] - PY, Lz = fp.lp[li][2] - PZ;
+        float Lx = fp.sh.lp[li][0] - PX, Ly = fp.sh.lp[li][1] - PY, Lz = fp.sh.lp[li][2] - PZ;
         normalize_div(Lx, Ly, Lz);
         const float Cos = minps(1.0f, maxps(0.0f, (n0 * Lx + n1 * Ly) + n2 * Lz));
         float Vx = 0.0f - PX, Vy = 0.0f - PY, Vz = 0.0f - PZ;
@@ -417,7 +418,7 @@ __device__ __forceinline__ uint32_t shade_avx_texel(const FrameParams &fp, const
         normalize_div(Hx, Hy, Hz);
         float Ph = minps(1.0f, maxps(0.0f, (n0 * Hx + n1 * Hy) + n2 * Hz));
         Ph = Ph * Ph; Ph = Ph * Ph; Ph = Ph * Ph; Ph = Ph * Ph;
-        const float *I = fp.li[li];
+        const float *I = fp.sh.li[li];
         Fr = Fr + ((Cos * (CR * I[0])) + (Ph * (1.0f * I[0])));
         Fg = Fg + ((Cos * (CG * I[1])) + (Ph * (1.0f * I[1])));
         Fb = Fb + ((Cos * (CB * I[2])) + (Ph * (1.0f * I[2])));
@@ -669,17 +670,17 @@ __device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx
                     C[2] = u8_unit(t & 0xFF);
                 }
                 float F[4];
-                if (TR::phong) {  // 448-484 with UnprojectVertex (147-160)
-                    const float d = fp.D - z;
+                if (TR::phong) {  // 448-484 with UnprojectVertex (147-160); the shading camera (452-458)
+                    const float d = fp.sh.D - z;
                     const float dF = div_focal(fp, d);
-                    const float PX = dF * (((float)x - fp.Cx) * fp.InvM2P);
-                    const float PY = dF * (((float)Row - fp.Cy) * fp.InvM2P);
+                    const float PX = dF * (((float)x - fp.sh.Cx) * fp.sh.InvM2P);
+                    const float PY = dF * (((float)Row - fp.sh.Cy) * fp.sh.InvM2P);
                     const float PZ = z;
                     F[0] = F[1] = F[2] = F[3] = 0.0f;
-                    for (uint32_t li = 0; li < fp.light_count; ++li) {
+                    for (uint32_t li = 0; li < fp.sh.light_count; ++li) {
                         if (li == 0)
-                            for (int c = 0; c < 4; ++c) F[c] = C[c] * fp.amb[c];
-                        float Lx = fp.lp[li][0] - PX, Ly = fp.lp[li][1] - PY, Lz = fp.lp[li][2] - PZ;
+                            for (int c = 0; c < 4; ++c) F[c] = C[c] * fp.sh.amb[c];
+                        float Lx = fp.sh.lp[li][0] - PX, Ly = fp.sh.lp[li][1] - PY, Lz = fp.sh.lp[li][2] - PZ;
                         normalize_rcp(Lx, Ly, Lz);
                         const float Cos = clamp01((n0 * Lx + n1 * Ly) + n2 * Lz);
                         float Vx = -PX, Vy = -PY, Vz = -PZ;
@@ -696,7 +697,7 @@ __device__ __forceinline__ void item_scalar(const FrameParams &fp, const TileCtx
                         ph = ph * ph; ph = ph * ph; ph = ph * ph; ph = ph * ph;
                         Ph = (float)ph;
                         for (int c = 0; c < 4; ++c)
-                            F[c] = F[c] + ((Cos * (C[c] * fp.li[li][c])) + (Ph * (1.0f * fp.li[li][c])));
+                            F[c] = F[c] + ((Cos * (C[c] * fp.sh.li[li][c])) + (Ph * (1.0f * fp.sh.li[li][c])));
                     }
                     for (int c = 0; c < 4; ++c) F[c] = clamp01(F[c]);
                 } else {

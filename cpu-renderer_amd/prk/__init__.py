@@ -43,6 +43,7 @@ class PrkError(RuntimeError):
 _SIGS = {
     "prk_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
     "prk_destroy": (C.c_int, [C.c_void_p]),
+    "prk_runtime_check": (C.c_int, []),
     "prk_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "prk_version": (C.c_char_p, []),
     "prk_target_bind": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_int32,
@@ -55,6 +56,7 @@ _SIGS = {
     "prk_target_upload": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
     "prk_target_upload_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
     "prk_set_camera": (C.c_int, [C.c_void_p, C.POINTER(abi.PrkTransform), C.POINTER(abi.PrkLightData)]),
+    "prk_set_shade_camera": (C.c_int, [C.c_void_p, C.POINTER(abi.PrkTransform), C.POINTER(abi.PrkLightData)]),
     "prk_texture_create": (C.c_int, [C.c_void_p, C.POINTER(abi.PrkBitmap), C.POINTER(C.c_int32)]),
     "prk_texture_set_filter": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     "prk_texture_update": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(abi.PrkBitmap)]),
@@ -132,10 +134,14 @@ def lib(path=None):
         # satisfy ours by SONAME; loaded after us, torch would map a second
         # copy of each, and two librocm_smi64 copies destroy the same
         # interposed static map at exit (glibc "double free").
-        try:
-            import torch  # noqa: F401
-        except Exception:  # no (usable) torch: this library's own ROCm stack alone
-            pass
+        # PRK_NO_TORCH_PRELOAD=1 skips this (a process that never imports
+        # torch: the library's own /opt/rocm stack alone, no torch import cost).
+        if os.environ.get("PRK_NO_TORCH_PRELOAD", "0") != "1":
+            try:
+                import torch  # noqa: F401
+            except Exception:  # no (usable) torch: this library's own ROCm stack alone
+                pass
+        atexit.register(_close_all)  # after torch's handlers: runs before them
         L = C.CDLL(p)
         # (A/B tools load older builds through PRK_LIB that may lack newer entry points)
         variant = os.path.abspath(p) != os.path.abspath(_DEFAULT_LIB)
@@ -275,12 +281,13 @@ def gather_frame_local(renderers, frame_color_ptr, frame_pitch, frame_z_ptr=None
 _LIVE = weakref.WeakSet()  # open Renderers / Comms, closed in a defined order at exit
 
 
-@atexit.register
 def _close_all():
     """Interpreter exit: close every context still open, communicators first,
-    while the HIP runtime (and torch, whose tensors a target may use) is
-    still alive.  prk_destroy never queues GPU work (prk_api.hip), so a
-    context whose last frame was never read just drops it."""
+    while the HIP runtime (and torch, whose tensors a target may use) is still
+    alive.  atexit runs the last-registered handler first; lib() registers
+    this one right after it imports torch, so it runs before torch's.
+    prk_destroy never queues GPU work (prk_api.hip), so a context whose last
+    frame was never read just drops it."""
     objs = list(_LIVE)
     for o in sorted(objs, key=lambda o: 0 if isinstance(o, Comm) else 1):
         try:
@@ -368,6 +375,14 @@ class Renderer:
     def set_camera(self, transform, lights):
         self._cam = (transform, lights)
         _check("prk_set_camera", self._L.prk_set_camera(self._h, C.byref(transform), C.byref(lights)))
+
+    def set_shade_camera(self, transform, lights):
+        """After set_camera: the span shading (Phong, unprojection) uses these
+        instead -- Commands as DrawModel* sees them when the caller changed
+        them after FillEdgeTable (projekt.cpp:452-458, 2042-2046)."""
+        self._shade_cam = (transform, lights)
+        _check("prk_set_shade_camera", self._L.prk_set_shade_camera(self._h, C.byref(transform),
+                                                                    C.byref(lights)))
 
     def texture(self, tex):
         """tex: scenes.Texture (uint32 texels with the zeroed guard row)."""
@@ -529,12 +544,14 @@ class Renderer:
 
 
 def render_scene(scene, semantics=abi.PRK_SEM_AVX, phong=True, device=0, tile=None, debug=True,
-                 color=None, z=None, rows=None, fused_clear=False, tris_per_object=1, setup=None):
+                 color=None, z=None, rows=None, fused_clear=False, tris_per_object=1, setup=None,
+                 shade_camera=None):
     """Convenience: draw a whole scenes.Scene (per-triangle submission) and
     return (color, z, winners or None, stats).  fused_clear: upload
     color / z, then clear through prk_target_clear_on_flush (the frame must
     overwrite them).  setup: FillEdgeTable's own inputs (abi.PRK_SETUP_*) of
-    every draw."""
+    every draw.  shade_camera: a scene whose transform / lights shade the
+    spans (set_shade_camera); `scene`'s set the draws up."""
     r = Renderer(device)
     try:
         r0, r1 = (0, scene.height) if rows is None else rows
@@ -549,6 +566,8 @@ def render_scene(scene, semantics=abi.PRK_SEM_AVX, phong=True, device=0, tile=No
             r.set_tile(*tile)
         r.set_debug(debug)
         r.set_camera(scene.prk_transform(), scene.prk_lights())
+        if shade_camera is not None:
+            r.set_shade_camera(shade_camera.prk_transform(), shade_camera.prk_lights())
         g = r.geometry(scene.vertices, scene.colors, scene.normals, scene.uvs)
         draws = scene.draws if scene.draws is not None else [(0, scene.tri_count, scene.texture)]
         handles = {}

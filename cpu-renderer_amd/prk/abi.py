@@ -16,6 +16,7 @@ PRK_ERR_DEVICE = -3
 PRK_ERR_NOMEM = -4
 PRK_ERR_NO_TARGET = -5
 PRK_ERR_LIMIT = -6
+PRK_ERR_RUNTIME_MIX = -7
 
 PRK_SEM_SCALAR = 0  # DrawModel            projekt.cpp:162-601
 PRK_SEM_AVX = 1     # FillLineOptimized    projekt.cpp:1492-2320
@@ -32,7 +33,7 @@ PRK_FILTER_BILINEAR = 1  # extension (AVX semantics)
 STATUS_NAMES = {
     PRK_OK: "PRK_OK", PRK_ERR_ARG: "PRK_ERR_ARG", PRK_ERR_UNSUPPORTED: "PRK_ERR_UNSUPPORTED",
     PRK_ERR_DEVICE: "PRK_ERR_DEVICE", PRK_ERR_NOMEM: "PRK_ERR_NOMEM",
-    PRK_ERR_NO_TARGET: "PRK_ERR_NO_TARGET",
+    PRK_ERR_NO_TARGET: "PRK_ERR_NO_TARGET", PRK_ERR_RUNTIME_MIX: "PRK_ERR_RUNTIME_MIX",
     PRK_ERR_LIMIT: "PRK_ERR_LIMIT",
 }
 

@@ -22,6 +22,13 @@
 //   camera   per-triangle objects; halfway through, the caller moves the
 //            camera (ScreenCenter) and changes the light between FillEdgeTable
 //            calls: each object draws as its FillEdgeTable call saw them
+//   split_st / split_queue   per-triangle objects; every FillEdgeTable runs
+//            under camera and lights A, then the caller switches Commands to B
+//            and draws through the single-thread overload / the queue overload,
+//            then back to A: set up under A (3885-4063), shaded under B
+//            (3030-3034 / 2042-2046)
+//   split_object  the sphere as ONE object, FillEdgeTable(..., 1) under A,
+//            DrawModel(..., Bitmap = 0, Phong = 1) under B (452-458)
 //   mutate   two frames; between them the vertices, normals and texture are
 //            rewritten in place (same pointers): frame 2 is written
 //   edges F  DrawModelOptimized on a ready edge_info list read from file F
@@ -125,6 +132,21 @@ int main(int argc, char **argv) {
         std::fprintf(stderr, "dropin_demo: %s failed (status %d)\n", what, PRK_LastStatus());
         return 2;
     };
+    // Camera and lights B of the split modes (A is the above).
+    auto to_b = [&]() {
+        Commands.Transform.DistanceAboveTarget = 4.5f;
+        Commands.Transform.ScreenCenter.x = W / 2.0f + 24.0f;
+        Commands.LightData.Lights[0].P = {{-1.0f, 2.0f, 2.5f}};
+        Commands.LightData.Lights[0].Intensity = {{0.3f, 0.9f, 0.5f, 1.0f}};
+        Commands.LightData.AmbientIntensity = {{0.1f, 0.15f, 0.3f, 1.0f}};
+    };
+    auto to_a = [&]() {
+        Commands.Transform.DistanceAboveTarget = 4.0f;
+        Commands.Transform.ScreenCenter.x = W / 2.0f;
+        Commands.LightData.Lights[0].P = {{1.0f, 1.0f, 3.0f}};
+        Commands.LightData.Lights[0].Intensity = {{0.8f, 0.8f, 0.8f, 1.0f}};
+        Commands.LightData.AmbientIntensity = {{0.2f, 0.2f, 0.2f, 1.0f}};
+    };
     // One frame of per-triangle objects through the chosen entry point.
     unsigned long long edges_total = 0;  // sum of FillEdgeTable's return values
     auto per_triangle = [&](const std::string &m) {
@@ -146,7 +168,12 @@ int main(int argc, char **argv) {
             const bool scalar = m == "scalar" || m == "vertexlit" || m == "interp";
             const u32 EdgeCount = FillEdgeTable(&Object, &Commands, !scalar || m == "interp");
             edges_total += EdgeCount;
-            if (scalar) DrawModel(&Buffer, EdgeMemory.data(), EdgeCount, &Commands, 0, 0);
+            if (m == "split_st" || m == "split_queue") {  // the draw under B, the next setup under A
+                to_b();
+                if (m == "split_st") DrawModelOptimized(&Buffer, EdgeMemory.data(), EdgeCount, &Commands, &Texture, 1);
+                else DrawModelOptimized(nullptr, &Buffer, EdgeMemory.data(), EdgeCount, &Commands, &Texture, 1);
+                to_a();
+            } else if (scalar) DrawModel(&Buffer, EdgeMemory.data(), EdgeCount, &Commands, 0, 0);
             else if (m == "lines") DrawModelOptimizedLines(nullptr, &Buffer, EdgeMemory.data(), EdgeCount, &Commands, &Texture, 1);
             else if (m == "st") DrawModelOptimized(&Buffer, EdgeMemory.data(), EdgeCount, &Commands, &Texture, 1);
             else DrawModelOptimized(nullptr, &Buffer, EdgeMemory.data(), EdgeCount, &Commands, &Texture, 1);
@@ -166,8 +193,14 @@ int main(int argc, char **argv) {
     Sphere.Bitmap = &Texture;
 
     if (mode == "queue" || mode == "lines" || mode == "st" || mode == "scalar" || mode == "camera" ||
-        mode == "vertexlit" || mode == "interp") {
+        mode == "vertexlit" || mode == "interp" || mode == "split_st" || mode == "split_queue") {
         if (!per_triangle(mode)) return fail("draw");
+    } else if (mode == "split_object") {
+        const u32 EdgeCount = FillEdgeTable(&Sphere, &Commands, 1);
+        edges_total += EdgeCount;
+        to_b();
+        DrawModel(&Buffer, EdgeMemory.data(), EdgeCount, &Commands, 0, 1);
+        if (PRK_LastStatus() != PRK_OK) return fail("draw");
     } else if (mode == "scalar_object" || mode == "scalar_object_phong" || mode == "interp_object") {
         const b32 Phong = mode == "scalar_object_phong";
         const u32 EdgeCount = FillEdgeTable(&Sphere, &Commands, Phong || mode == "interp_object");

@@ -46,9 +46,13 @@ enum prk_status {
     PRK_ERR_DEVICE = -3,       /* HIP runtime error                      */
     PRK_ERR_NOMEM = -4,        /* device allocation failed               */
     PRK_ERR_NO_TARGET = -5,    /* flush without a render target          */
-    PRK_ERR_LIMIT = -6         /* beyond this build's index capacity (more than
+    PRK_ERR_LIMIT = -6,        /* beyond this build's index capacity (more than
                                   2^31 edges, span slots or bin entries in one
                                   pass): a limit of the build, not of the input */
+    PRK_ERR_RUNTIME_MIX = -7   /* two copies of the ROCm runtime are mapped in
+                                  this process (e.g. /opt/rocm's, pulled in by
+                                  this library, and torch's own, loaded after
+                                  it): see prk_create */
 };
 
 /* Which of the reference's span kernels a draw reproduces. */
@@ -136,9 +140,29 @@ typedef struct prk_stats {
 
 typedef struct prk_context prk_context;
 
-/* Library / device lifetime. */
+/* Library / device lifetime.
+ * prk_create checks that the process maps ONE copy of libamdhip64 and of
+ * librocm_smi64.  A host that loads this library (and so /opt/rocm's
+ * runtime, plus its RCCL once prk_comm_* runs) before a framework that ships
+ * its own copies under other names (torch) ends up with two; their
+ * librocm_smi64 copies then free one interposed static map twice at exit
+ * (glibc "double free", SIGABRT).  prk_create returns
+ * PRK_ERR_RUNTIME_MIX then, names the fix on stderr (load the framework
+ * before libprk_hip.so), and guards the exit: an on_exit handler registered
+ * after both copies' destructors flushes stdio and ends the process with its
+ * own exit status before those destructors run.  prk_destroy and
+ * prk_comm_init run the same check (and install the same guard). */
 int prk_create(int device, prk_context **out);
+/* prk_destroy queues no GPU work: it waits for the context's streams and frees
+ * what the context owns.  A frame whose bin count is still unresolved (prk_flush
+ * returned, nothing has read the count since) is DROPPED, not re-run: if its
+ * entries overflowed the scratch, a caller-owned target (prk_target_bind) is
+ * left with the frame's cleared or partial contents.  A caller that reads its
+ * own target after destroying the context calls prk_synchronize (or
+ * prk_resolve) first. */
 int prk_destroy(prk_context *ctx);
+/* The check alone: PRK_OK, or PRK_ERR_RUNTIME_MIX (guard installed). */
+int prk_runtime_check(void);
 int prk_device_count(int *out);
 const char *prk_version(void);
 
@@ -182,9 +206,24 @@ int prk_host_free(prk_context *ctx, void *p);
 int prk_host_register(prk_context *ctx, void *p, size_t bytes);
 int prk_host_unregister(prk_context *ctx, void *p);
 
-/* Camera and lights (game_render_commands::Transform / LightData). */
+/* Camera and lights (game_render_commands::Transform / LightData) of the
+ * draws executed by the next prk_flush, for both what FillEdgeTable reads
+ * (ProjectVertex 3906-3910, Gouraud vertex lighting 4020-4063) and what the
+ * span kernels read (Phong + UnprojectVertex: DrawModel 452-458,
+ * FillLineOptimized 2042-2046, the single-thread overload 3030-3034). */
 int prk_set_camera(prk_context *ctx, const prk_transform *transform,
                    const prk_light_data *lights);
+/* After prk_set_camera: the span shading (Phong lighting and unprojection)
+ * of the next flush uses (transform, lights) instead, the setup keeps
+ * prk_set_camera's.  The reference's FillEdgeTable and DrawModel* each read
+ * Commands when they run, so a caller that changes Commands between an
+ * object's FillEdgeTable and its DrawModel* call gets the setup of the first
+ * and the shading of the second; the drop-in passes them this way.  (For the
+ * queue overload the spans run on workers that read Commands as they go,
+ * 2042-2046; the drop-in uses Commands as they are at the DrawModel* call.)
+ * PRK_ERR_ARG before any prk_set_camera. */
+int prk_set_shade_camera(prk_context *ctx, const prk_transform *transform,
+                         const prk_light_data *lights);
 
 /* Textures.  `bitmap->Memory` is host memory of Height rows of Pitch bytes
  * (loaded_bitmap as the reference reads it, projekt.cpp:1506, 1881-1935); the
@@ -316,9 +355,10 @@ int prk_draw_spans(prk_context *ctx, const prk_span *spans, uint32_t count, int3
  * returns once the frame is queued, without waiting for its binning.  The
  * frame's bin entry count (scratch sizing, prk_stats.bin_entries) is read by
  * the next call that needs it: the next prk_flush, prk_synchronize,
- * prk_target_download / upload / clear, prk_get_stats, a texture or geometry
- * update, a gather, prk_target_alloc, or prk_target_bind replacing a
- * library-owned target.  A frame whose entries overflowed the scratch is
+ * prk_resolve, prk_target_download / upload / clear, prk_get_stats, a texture
+ * or geometry update, a gather, prk_target_alloc, or prk_target_bind (any
+ * target: rebinding waits on the host for the previous frame's count, so a
+ * caller rotating its own buffers pays that wait at the bind).  A frame whose entries overflowed the scratch is
  * re-run there, into the target and with the camera, tile and clear it was
  * queued with, before anything else is queued — so a caller that reads the
  * target through its own device pointers (not prk_target_download) after a

@@ -50,9 +50,12 @@
 //    them) and the result comes down as DMA.  PRK_ClearNextFrame(color, z)
 //    replaces that upload by a clear fused into the frame's kernels.
 //  * Textures (loaded_bitmap) are read at their first use in each frame.
-//  * Cameras and lights: an object draws with Commands->Transform / LightData
-//    as they were at its FillEdgeTable call (edge lists and work records: at
-//    their DrawModel* / callback call); a frame whose draws saw several
+//  * Cameras and lights: an object is set up (projection, Gouraud lighting)
+//    with Commands->Transform / LightData as they were at its FillEdgeTable
+//    call and shaded (Phong, unprojection) with them as they are at its
+//    DrawModel* call, as the reference reads them (3885-4063; 452-458,
+//    2042-2046, 3030-3034); edge lists and work records use them as they are
+//    at their DrawModel* / callback call.  A frame whose draws saw several
 //    cameras runs as consecutive flushes, one per change, in order.
 //  * Inputs the reference crashes on are rejected or pinned, see
 //    prk.h; PRK_LastStatus() reports the last library status.
@@ -216,7 +219,10 @@ struct pending_draw {
     int Kind;
     uint32_t First, Count;  // object index / range of Edges / range of Spans
     int32_t Semantics, Phong, Texture;
-    uint32_t Camera;        // index into the frame's cameras
+    // indices into the frame's cameras: the one FillEdgeTable saw (setup:
+    // projection, Gouraud lighting, 3885-4063) and the one the DrawModel* call
+    // sees (span shading: Phong + unprojection, 452-458, 2042-2046, 3030-3034)
+    uint32_t SetupCamera, Camera;
     // DRAW_OBJECT: Count objects drawn alike, consecutive in the arena, of
     // one size and offset, RunTris triangles in all: one library call (the
     // per-triangle objects of a reference caller make one run per frame)
@@ -241,6 +247,11 @@ struct state {
     std::vector<frame_object> Objects;
     std::vector<pending_draw> Draws;
     std::vector<camera> Cameras;               // the frame's distinct camera / light snapshots, in order
+    // the raw bytes of Commands->Transform and LightData at the last camera
+    // lookup and the camera they gave: an unchanged Commands (every call of a
+    // usual frame) is one memcmp
+    unsigned char RawCam[sizeof(projective_transform) + sizeof(light_data)];
+    uint32_t RawCamId = 0xFFFFFFFFu;
     std::vector<prk_edge> Edges;
     std::vector<prk_span> Spans;
     std::map<const void *, int32_t> Textures;  // Bitmap->Memory -> handle
@@ -449,12 +460,29 @@ inline bool camera_is(const camera &k, const game_render_commands *C) {
     return true;
 }
 inline uint32_t camera_id(state &st, const game_render_commands *C) {
-    if (st.Cameras.empty() || !camera_is(st.Cameras.back(), C)) st.Cameras.push_back(camera_of(C));
-    return (uint32_t)st.Cameras.size() - 1;
+    unsigned char raw[sizeof st.RawCam];
+    memcpy(raw, &C->Transform, sizeof(projective_transform));
+    memcpy(raw + sizeof(projective_transform), &C->LightData, sizeof(light_data));
+    if (st.RawCamId < st.Cameras.size() && memcmp(raw, st.RawCam, sizeof raw) == 0) return st.RawCamId;
+    // a camera seen lately (a caller switching between two, e.g. one for
+    // FillEdgeTable and one for DrawModel*), else a new entry
+    uint32_t id = (uint32_t)st.Cameras.size();
+    for (uint32_t k = 0; k < 4 && k < st.Cameras.size(); ++k)
+        if (camera_is(st.Cameras[st.Cameras.size() - 1 - k], C)) {
+            id = (uint32_t)st.Cameras.size() - 1 - k;
+            break;
+        }
+    if (id == st.Cameras.size()) st.Cameras.push_back(camera_of(C));
+    memcpy(st.RawCam, raw, sizeof raw);
+    st.RawCamId = id;
+    return id;
 }
 
-inline int set_camera(const camera &k) {
-    return each([&](prk_context *c) { return prk_set_camera(c, &k.T, &k.L); });
+inline int set_camera(const camera &setup, const camera &shade, bool split) {
+    return each([&](prk_context *c) {
+        const int rc = prk_set_camera(c, &setup.T, &setup.L);
+        return rc == PRK_OK && split ? prk_set_shade_camera(c, &shade.T, &shade.L) : rc;
+    });
 }
 
 inline void register_host(state &st, void *p, size_t bytes) {
@@ -554,13 +582,14 @@ inline void draw(loaded_bitmap *Buffer, edge_info *Edges, u32 EdgeCount, game_re
         d.First = tok.Object;
         d.Count = 1;
         const frame_object &o = st.Objects[tok.Object];
-        d.Camera = o.Camera;  // as FillEdgeTable saw it
         d.RunTris = o.Tris;
         if (o.Tris == 0) return;  // FillEdgeTable wrote no edge: nothing to draw
+        d.SetupCamera = o.Camera;           // as FillEdgeTable saw it
+        d.Camera = camera_id(st, Commands);  // as this call sees it (shading)
         if (!st.Draws.empty()) {  // the next object of the previous draw's run
             pending_draw &b = st.Draws.back();
             if (b.Kind == DRAW_OBJECT && b.Semantics == d.Semantics && b.Phong == d.Phong &&
-                b.Texture == d.Texture && b.Camera == d.Camera) {
+                b.Texture == d.Texture && b.Camera == d.Camera && b.SetupCamera == d.SetupCamera) {
                 const frame_object &f = st.Objects[b.First];
                 if (o.FirstTri == f.FirstTri + b.RunTris && o.Tris == f.Tris && o.Setup == f.Setup &&
                     memcmp(o.P, f.P, sizeof o.P) == 0) {
@@ -572,7 +601,7 @@ inline void draw(loaded_bitmap *Buffer, edge_info *Edges, u32 EdgeCount, game_re
             }
         }
     } else {  // a caller's own edge_info list, drawn as given
-        d.Camera = camera_id(st, Commands);
+        d.Camera = d.SetupCamera = camera_id(st, Commands);
         d.Kind = DRAW_EDGES;
         d.First = (uint32_t)st.Edges.size();
         d.Count = EdgeCount;
@@ -595,16 +624,18 @@ inline void draw_spans(loaded_bitmap *Buffer, game_render_commands *Commands, lo
     d.Semantics = PRK_SEM_AVX;
     d.Phong = PhongShading ? 1 : 0;
     d.Texture = Bitmap ? texture_for(Bitmap) : -1;
-    d.Camera = camera_id(st, Commands);
+    d.Camera = d.SetupCamera = camera_id(st, Commands);
     st.Spans.insert(st.Spans.end(), spans, spans + n);
     st.Draws.push_back(d);
 }
 
 // Records the frame's draws with the library, in order.  Draws that saw
-// different cameras or lights (Commands changed between FillEdgeTable calls)
-// run as consecutive flushes, each with its own camera; a later flush z-tests
-// against what the earlier ones left, which is the reference's sequential
-// order.  The last flush is left to the caller (PRK_CompleteAllWork).
+// different cameras or lights (Commands changed between calls) run as
+// consecutive flushes, one per (setup camera, shading camera) run, each set up
+// with the camera its FillEdgeTable saw and shaded with the one its DrawModel*
+// call saw (prk_set_shade_camera); a later flush z-tests against what the
+// earlier ones left, which is the reference's sequential order.  The last
+// flush is left to the caller (PRK_CompleteAllWork).
 inline int issue(state &st) {
     int rc = PRK_OK;
     if (st.LastStatus != PRK_OK) return st.LastStatus;
@@ -626,13 +657,14 @@ inline int issue(state &st) {
     size_t i = 0;
     while (i < st.Draws.size() || i == 0) {
         const uint32_t cam = st.Draws.empty() ? 0u : st.Draws[i].Camera;
+        const uint32_t scam = st.Draws.empty() ? 0u : st.Draws[i].SetupCamera;
         size_t j = i;
-        while (j < st.Draws.size() && st.Draws[j].Camera == cam) ++j;
+        while (j < st.Draws.size() && st.Draws[j].Camera == cam && st.Draws[j].SetupCamera == scam) ++j;
         if (i > 0) {  // camera / lights changed: the draws so far run first
             rc = each([](prk_context *k) { return prk_flush(k, nullptr); });
             if (rc != PRK_OK) return rc;
         }
-        rc = set_camera(st.Cameras[cam]);
+        rc = set_camera(st.Cameras[scam], st.Cameras[cam], scam != cam);
         if (rc != PRK_OK) return rc;
         rc = each([&](prk_context *c) {
             int r = PRK_OK;
@@ -666,6 +698,7 @@ inline void end_frame(state &st) {
     st.Objects.clear();
     st.Draws.clear();
     st.Cameras.clear();
+    st.RawCamId = 0xFFFFFFFFu;
     st.Edges.clear();
     st.Spans.clear();
     st.TexFresh.clear();

@@ -35,7 +35,7 @@ class OrDrawDesc(C.Structure):
                 ("UVs", C.c_void_p), ("TriCount", C.c_uint32), ("TrisPerObject", C.c_uint32),
                 ("P", C.c_float * 3), ("Semantics", C.c_int32), ("Phong", C.c_int32),
                 ("Bitmap", C.POINTER(abi.PrkBitmap)), ("TriIndexBase", C.c_int32), ("Filter", C.c_int32),
-                ("Setup", C.c_int32)]
+                ("Setup", C.c_int32), ("SetupT", C.c_void_p), ("SetupLights", C.c_void_p)]
 
 
 class OrTarget(C.Structure):
@@ -82,7 +82,8 @@ def _ptr(a):
 class _Keep:
     """Holds ctypes objects alive for the duration of a call."""
 
-    def __init__(self, scene, semantics, phong, tris_per_object, tri_base=0, texture="scene", setup=None):
+    def __init__(self, scene, semantics, phong, tris_per_object, tri_base=0, texture="scene", setup=None,
+                 setup_camera=None):
         self.arrays = [np.ascontiguousarray(scene.vertices, np.float32),
                        np.ascontiguousarray(scene.colors, np.float32),
                        np.ascontiguousarray(scene.normals, np.float32),
@@ -105,20 +106,27 @@ class _Keep:
         d.TriIndexBase = tri_base
         d.Filter = getattr(texture, "filter", abi.PRK_FILTER_NEAREST) if texture is not None else 0
         d.Setup = -1 if setup is None else int(setup)  # FillEdgeTable's own inputs (PRK_SETUP_*)
-        self.desc = d
         self.transform = scene.prk_transform()
         self.lights = scene.prk_lights()
+        if setup_camera is not None:  # FillEdgeTable's camera / lights (a scene), the draw's shade
+            self.setup_transform = setup_camera.prk_transform()
+            self.setup_lights = setup_camera.prk_lights()
+            d.SetupT = C.cast(C.pointer(self.setup_transform), C.c_void_p)
+            d.SetupLights = C.cast(C.pointer(self.setup_lights), C.c_void_p)
+        self.desc = d
 
 
 def render(scene, semantics=abi.PRK_SEM_AVX, phong=True, tris_per_object=1, threads=1,
-           color=None, z=None, winners=True, rows=None, cpu=None, setup=None):
+           color=None, z=None, winners=True, rows=None, cpu=None, setup=None, setup_camera=None):
     """Draw `scene` with the oracle.  Returns (color u32[H,W], z f32[H,W],
     winners i32[H,W] or None, stats dict).  `color`/`z` (optional) are the
     prior target contents (default: reference clear values).
     cpu: None = the scalar restatement (liboracle.so); "banded" / "queue" /
     "rows" = the AVX2 CPU baseline (liborcpu.so) with that schedule over
     `threads`.  setup: FillEdgeTable's own PhongShading / Object->Bitmap
-    (PRK_SETUP_* bits; None: as the draw)."""
+    (PRK_SETUP_* bits; None: as the draw).  setup_camera: a scene whose
+    transform / lights FillEdgeTable saw (the caller changed Commands before
+    DrawModel*); `scene`'s own shade the spans.  None: `scene`'s for both."""
     W, H = scene.width, scene.height
     col = np.full((H, W), CLEAR_COLOR, np.uint32) if color is None else np.array(color, np.uint32)
     zb = np.full((H, W), CLEAR_Z, np.float32) if z is None else np.array(z, np.float32)
@@ -131,16 +139,17 @@ def render(scene, semantics=abi.PRK_SEM_AVX, phong=True, tris_per_object=1, thre
             sub = scene.subset(first, first + count)
             sub.texture, sub.draws = texture, None
             _, _, _, st = _render_one(sub, sem, phong, tpo, threads, col, zb, win, rows,
-                                      tri_base=first, cpu=cpu, setup=setup)
+                                      tri_base=first, cpu=cpu, setup=setup, setup_camera=setup_camera)
             tot = [tot[0] + st["spans"], tot[1] + st["span_pixels"], tot[2] + st["writes"]]
         return col, zb, win, dict(spans=tot[0], span_pixels=tot[1], writes=tot[2])
-    return _render_one(scene, semantics, phong, tris_per_object, threads, col, zb, win, rows, cpu=cpu, setup=setup)
+    return _render_one(scene, semantics, phong, tris_per_object, threads, col, zb, win, rows, cpu=cpu, setup=setup,
+                       setup_camera=setup_camera)
 
 
 def _render_one(scene, semantics, phong, tris_per_object, threads, col, zb, win, rows, tri_base=0, cpu=None,
-                setup=None):
+                setup=None, setup_camera=None):
     W, H = scene.width, scene.height
-    k = _Keep(scene, semantics, phong, tris_per_object, tri_base=tri_base, setup=setup)
+    k = _Keep(scene, semantics, phong, tris_per_object, tri_base=tri_base, setup=setup, setup_camera=setup_camera)
     tg = OrTarget(_ptr(col), W * 4, _ptr(zb), W, H, _ptr(win))
     stats = (C.c_uint64 * 3)()
     if cpu is not None:

@@ -516,7 +516,7 @@ static int cpu_avx_draw_tasks(const or_draw_desc *D, const or_target *Tg, const 
     for (uint32_t t0 = 0; t0 < D->TriCount; t0 += per) {
         uint32_t n = D->TriCount - t0 < per ? D->TriCount - t0 : per;
         uint32_t ec = or_fill_edge_table(D->Vertices, D->Colors, D->Normals, D->UVs, t0, n, D->P, 1, D->Phong,
-                                         T, Lights, Edges, Sort);
+                                         or_setup_t(D, T), or_setup_l(D, Lights), Edges, Sort);
         P.TriIndex = D->TriIndexBase + (int32_t)t0;
         or_aet_walk(&P, Edges, ec, rows ? cpu_post_row_pair : cpu_post_span);
         if (rows) cpu_row_flush(); /* the object's last row (3609) */

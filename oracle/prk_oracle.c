@@ -802,7 +802,22 @@ typedef struct or_draw_desc {
     int32_t Setup;            /* FillEdgeTable's own inputs (prk.h PRK_SETUP_*): bit 0 its
                                  PhongShading, bit 1 Object->Bitmap != 0; < 0: as the draw
                                  (Phong, Bitmap != NULL) */
+    /* The camera and lights FillEdgeTable saw (ProjectVertex 3906-3910, Gouraud
+     * lighting 4020-4063), when the caller changed Commands between the
+     * object's FillEdgeTable and its DrawModel* call; NULL: the draw's own
+     * (the span shading always reads the draw's: 452-458, 2042-2046, 3030-3034). */
+    const prk_transform *SetupT;
+    const prk_light_data *SetupLights;
 } or_draw_desc;
+
+static inline const prk_transform *or_setup_t(const or_draw_desc *D, const prk_transform *T)
+{
+    return D->SetupT ? D->SetupT : T;
+}
+static inline const prk_light_data *or_setup_l(const or_draw_desc *D, const prk_light_data *L)
+{
+    return D->SetupLights ? D->SetupLights : L;
+}
 
 /* FillEdgeTable's PhongShading and Object->Bitmap of a draw (projekt.cpp:
  * 4012-4089 read them; DrawModel* reads its own Phong / Bitmap). */
@@ -852,6 +867,7 @@ static int or_draw_filtered(const or_draw_desc *D, const or_target *Tg, const pr
      * (4078-4089) -- a draw reading them is undefined */
     if ((D->Phong && !or_setup_phong(D)) || (D->Bitmap && !or_setup_bitmap(D))) return PRK_ERR_UNSUPPORTED;
     if (Lights->LightCount > PRK_MAX_LIGHTS) return PRK_ERR_ARG;
+    if (D->SetupLights && D->SetupLights->LightCount > PRK_MAX_LIGHTS) return PRK_ERR_ARG;
     uint32_t per = D->TrisPerObject ? D->TrisPerObject : 1;
     or_edge *Edges = (or_edge *)malloc(sizeof(or_edge) * 3 * per);
     or_edge *Sort = (or_edge *)malloc(sizeof(or_edge) * 3 * per);
@@ -874,7 +890,7 @@ static int or_draw_filtered(const or_draw_desc *D, const or_target *Tg, const pr
             /* Skip objects that cannot touch a row this call draws (a pure
              * speed-up: the walk of such an object never reaches Span). */
             int32_t lo, hi;
-            or_object_rows(D, t0, n, T, &lo, &hi);
+            or_object_rows(D, t0, n, or_setup_t(D, T), &lo, &hi);
             if (D->Semantics == PRK_SEM_SCALAR && hi < INT32_MAX / 2) hi += 1; /* row-overflow pixel */
             if (lo < row_lo) lo = row_lo;
             if (hi > row_hi) hi = row_hi;
@@ -886,7 +902,8 @@ static int or_draw_filtered(const or_draw_desc *D, const or_target *Tg, const pr
             }
         }
         uint32_t ec = or_fill_edge_table(D->Vertices, D->Colors, D->Normals, D->UVs, t0, n, D->P,
-                                         or_setup_bitmap(D), or_setup_phong(D), T, Lights, Edges, Sort);
+                                         or_setup_bitmap(D), or_setup_phong(D), or_setup_t(D, T),
+                                         or_setup_l(D, Lights), Edges, Sort);
         X_.TriIndex = D->TriIndexBase + (int32_t)t0;
         or_aet_walk(&X_, Edges, ec, Span);
     }

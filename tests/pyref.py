@@ -110,9 +110,21 @@ def bilinear(tex, fu, fv):
     return out
 
 
+class Cam:
+    """Commands->Transform and LightData of a scene, as float32."""
+
+    def __init__(self, scene):
+        self.D, self.F, self.M2P, self.cx, self.cy = [f32(v) for v in scene.transform]
+        self.lights = [([f32(c) for c in p], [f32(c) for c in i]) for p, i in scene.lights]
+        self.amb = [f32(c) for c in scene.ambient]
+
+
 class Ctx:
-    def __init__(self, scene, semantics, phong, color=None, z=None, setup=None):
+    def __init__(self, scene, semantics, phong, color=None, z=None, setup=None, setup_camera=None):
         self.s = scene
+        # the camera FillEdgeTable saw (project + Gouraud lighting); the spans
+        # shade with the scene's own (Commands at DrawModel*, 452-458, 2042-2046)
+        self.su = Cam(scene if setup_camera is None else setup_camera)
         # FillEdgeTable's own PhongShading / Object->Bitmap (projekt.cpp:4012-4089);
         # None: as the draw (PhongShading, the draw's Bitmap)
         self.fe_phong = phong if setup is None else bool(setup & 1)
@@ -143,7 +155,7 @@ def edge_table(ctx, t):
     s = ctx.s
     P = [f32(v) for v in s.P]
     cam = [[s.vertices[3 * t + k][i] + P[i] for i in range(3)] for k in range(3)]
-    proj = [project(ctx, c) for c in cam]
+    proj = [project(ctx.su, c) for c in cam]
     a = norm_rcp([proj[1][i] - proj[0][i] for i in range(3)])
     b = norm_rcp([proj[2][i] - proj[0][i] for i in range(3)])
     cross = [a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]]
@@ -187,12 +199,12 @@ def edge_table(ctx, t):
         else:
             minc, maxc = [f32(0)] * 4, [f32(0)] * 4
             minn, maxn = [f32(0)] * 3, [f32(0)] * 3
-            for li, (lp, lint) in enumerate(ctx.lights):
+            for li, (lp, lint) in enumerate(ctx.su.lights):
                 fv = norm_rcp([lp[k] - cam[mi][k] for k in range(3)])
                 sv = norm_rcp([lp[k] - cam[ma][k] for k in range(3)])
                 if li == 0:
-                    minc = [(f32(1) if textured else c0[k]) * ctx.amb[k] for k in range(4)]
-                    maxc = [(f32(1) if textured else c1[k]) * ctx.amb[k] for k in range(4)]
+                    minc = [(f32(1) if textured else c0[k]) * ctx.su.amb[k] for k in range(4)]
+                    maxc = [(f32(1) if textured else c1[k]) * ctx.su.amb[k] for k in range(4)]
                 fd = clamp01((fv[0] * n0[0] + fv[1] * n0[1]) + fv[2] * n0[2])
                 sd = clamp01((sv[0] * n1[0] + sv[1] * n1[1]) + sv[2] * n1[2])
                 minc = [clamp01(minc[k] + fd * ((f32(1) if textured else c0[k]) * lint[k])) for k in range(4)]
@@ -441,8 +453,8 @@ def span_scalar(ctx, t, L, R, row):
             w, u, v = w + iw, u + iu, v + iv
 
 
-def render(scene, semantics=1, phong=True, setup=None):
-    ctx = Ctx(scene, semantics, phong, setup=setup)
+def render(scene, semantics=1, phong=True, setup=None, setup_camera=None):
+    ctx = Ctx(scene, semantics, phong, setup=setup, setup_camera=setup_camera)
     with np.errstate(all="ignore"):
         for t in range(scene.tri_count):
             walk(ctx, t, edge_table(ctx, t))

@@ -34,7 +34,7 @@ def declared():
 def test_every_declared_symbol_is_exported():
     names = declared()
     assert len(names) >= 20
-    lib = C.CDLL(prk.LIB_PATH)
+    lib = prk.lib()  # (the binding's load order: torch's ROCm first)
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(prk.exported_symbols())
@@ -134,6 +134,44 @@ print(sorted(set(re.findall({rx!r}, open('/proc/self/maps').read()))))
 """
 
 
+def _needs_torch_and_rccl():
+    pytest.importorskip("torch")
+    if not prk.comm_available():
+        pytest.skip("librccl not loadable here")
+
+
+REVERSED_ORDER_CHILD = """
+import ctypes, sys
+L = ctypes.CDLL({lib!r})                       # /opt/rocm's HIP runtime, first
+assert L.prk_comm_available() == 1             # dlopens /opt/rocm's librccl (+ librocm_smi64)
+import torch  # noqa: F401                     # torch's own copies beside them
+h = ctypes.c_void_p()
+print("create", L.prk_create(0, ctypes.byref(h)), "check", L.prk_runtime_check())
+"""
+
+
+def test_reversed_load_order_reported_and_exit_guarded():
+    """libprk_hip.so and RCCL loaded BEFORE torch (the order the binding
+    avoids): prk_create returns PRK_ERR_RUNTIME_MIX, names the fix on stderr,
+    and the process still exits 0 -- the on_exit guard ends it before the two
+    librocm_smi64 copies' destructors free one map twice."""
+    _needs_torch_and_rccl()
+    code = REVERSED_ORDER_CHILD.format(lib=prk.LIB_PATH)
+    run = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert run.returncode == 0 and "double free" not in run.stderr, (run.returncode, run.stderr[-2000:])
+    assert "create %d check %d" % (abi.PRK_ERR_RUNTIME_MIX, abi.PRK_ERR_RUNTIME_MIX) in run.stdout, run.stdout
+    assert "BEFORE libprk_hip.so" in run.stderr
+    # ... and with an exit status of its own, that status survives the guard
+    run = subprocess.run([sys.executable, "-c", code + "sys.exit(3)\n"], capture_output=True, text=True,
+                         timeout=300)
+    assert run.returncode == 3, (run.returncode, run.stderr[-2000:])
+
+
+def test_runtime_check_clean_process():
+    """One ROCm stack (this test process, the binding's load order): OK."""
+    assert prk.lib().prk_runtime_check() == abi.PRK_OK
+
+
 def test_one_rocm_runtime_per_process():
     """The binding loads torch's ROCm libraries before libprk_hip.so, so a
     process that uses both maps one HIP runtime, one RCCL and one
@@ -141,6 +179,7 @@ def test_one_rocm_runtime_per_process():
     /opt/rocm's copies and torch's side by side, and the two librocm_smi64
     copies' exit-time destructors free one interposed static map twice (glibc
     "double free or corruption", rc 134 — the round-3/4 exit aborts)."""
+    _needs_torch_and_rccl()
     code = LOAD_ORDER_CHILD.format(pkg=os.path.join(ROOT, "cpu-renderer_amd"), rx=ROCM_MAP_RE)
     run = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert run.returncode == 0 and "double free" not in run.stderr, (run.returncode, run.stderr[-2000:])

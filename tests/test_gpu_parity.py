@@ -55,6 +55,32 @@ def run_both(scene, semantics=abi.PRK_SEM_AVX, phong=True, tile=None, threads=8,
     return g, o
 
 
+@pytest.mark.parametrize("semantics,phong,textured,tpo", [
+    (abi.PRK_SEM_AVX, True, True, 1), (abi.PRK_SEM_AVX_ST, True, True, 1), (abi.PRK_SEM_SCALAR, True, False, 1),
+    (abi.PRK_SEM_SCALAR, False, False, 1), (abi.PRK_SEM_SCALAR, True, True, 1), (abi.PRK_SEM_AVX, True, True, 8),
+    (abi.PRK_SEM_SCALAR, True, False, 8), (abi.PRK_SEM_AVX, True, True, 64)])
+def test_split_setup_and_shade_camera(gpu, semantics, phong, textured, tpo):
+    """prk_set_camera + prk_set_shade_camera: the setup (projection, Gouraud
+    lighting) with FillEdgeTable's camera, the span shading (Phong,
+    unprojection) with the one DrawModel* reads (projekt.cpp:3885-4063 vs
+    452-458, 2042-2046, 3030-3034), per triangle and as whole objects, against
+    the oracle's split (or_draw_desc.SetupT / SetupLights)."""
+    import copy
+    s = scenes.random_soup(6000, 256, 256, radius=16, seed=41, textured=textured, lights=scenes.LIGHTS_TWO,
+                           ambient=scenes.AMBIENT_TWO)
+    b = copy.copy(s)
+    D, F, M2P, cx, cy = s.transform
+    b.transform = (D * 1.25, F, M2P, cx + 9.0, cy - 5.0)
+    b.lights = [((-1.0, 2.0, 2.5), (0.3, 0.9, 0.5, 1.0))]
+    b.ambient = (0.1, 0.15, 0.3, 1.0)
+    o = O.render(b, semantics=semantics, phong=phong, tris_per_object=tpo, setup_camera=s)
+    g = prk.render_scene(s, semantics=semantics, phong=phong, tris_per_object=tpo, shade_camera=b)
+    scalar_phong = semantics == abi.PRK_SEM_SCALAR and phong
+    compare(g, o, exact_color=not scalar_phong, label="split camera")
+    if phong:  # the shading camera made a difference
+        assert (channel_diff(g[0], O.render(s, semantics=semantics, phong=phong, tris_per_object=tpo)[0]) > 1).any()
+
+
 @pytest.mark.parametrize("seed", [1, 2])
 def test_shared_divisor_exact(gpu, seed):
     """The kernels' shared-reciprocal quotients (prk_device.h DivBy) equal the
@@ -920,12 +946,24 @@ def _dropin_scene(textured=True, salt=0):
 
 
 DROPIN_MODES = ["queue", "lines", "st", "scalar", "object", "mutate", "edges", "work", "scalar_object",
-                "scalar_object_phong", "camera", "vertexlit", "interp", "interp_object"]
+                "scalar_object_phong", "camera", "vertexlit", "interp", "interp_object", "split_st", "split_queue",
+                "split_object"]
+
+
+def _camera_b(s):
+    """examples/dropin_demo.cpp's camera and lights B (the split modes)."""
+    import copy
+    b = copy.copy(s)
+    b.transform = (4.5, 1.0, 128.0, 128.0 + 24.0, 128.0)
+    b.lights = [((-1.0, 2.0, 2.5), (0.3, 0.9, 0.5, 1.0))]
+    b.ambient = (0.1, 0.15, 0.3, 1.0)
+    return b
 
 
 @pytest.mark.parametrize("mode,bands", [(m, 1) for m in DROPIN_MODES] +
                          [("queue", 3), ("object", 2), ("mutate", 3), ("scalar", 3), ("work", 2),
-                          ("scalar_object", 3), ("camera", 2), ("interp_object", 2)])
+                          ("scalar_object", 3), ("camera", 2), ("interp_object", 2), ("split_st", 2),
+                          ("split_object", 2)])
 def test_dropin_demo_matches_oracle(gpu, tmp_path, mode, bands):
     """examples/dropin_demo.cpp drives the reference's own entry points
     through include/projekt.h (FillEdgeTable, DrawModelOptimized(RenderQueue),
@@ -946,7 +984,8 @@ def test_dropin_demo_matches_oracle(gpu, tmp_path, mode, bands):
                         "-Wl,-rpath," + os.path.join(root, "cpu-renderer_amd"), "-o", str(exe)],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
-    scalar_modes = ("scalar", "scalar_object", "scalar_object_phong", "vertexlit", "interp", "interp_object")
+    scalar_modes = ("scalar", "scalar_object", "scalar_object_phong", "vertexlit", "interp", "interp_object",
+                    "split_object")
     s = _dropin_scene(textured=mode not in scalar_modes)
     # FillEdgeTable's own PhongShading / Object->Bitmap (the demo's objects
     # carry the Bitmap except in "vertexlit")
@@ -1002,6 +1041,14 @@ def test_dropin_demo_matches_oracle(gpu, tmp_path, mode, bands):
         b.lights = [((1.0, 1.0, 3.0), (0.3, 0.9, 0.5, 1.0))]
         oc, oz, _, _ = O.render(a)
         oc, oz, _, _ = O.render(b, color=oc, z=oz)
+    elif mode in ("split_st", "split_queue"):  # set up under A, shaded under B (the draw call's Commands)
+        sem = abi.PRK_SEM_AVX_ST if mode == "split_st" else abi.PRK_SEM_AVX
+        oc, oz, _, _ = O.render(_camera_b(s), semantics=sem, setup_camera=s)
+        a_only = O.render(s, semantics=sem)[0]
+        assert (oc != a_only).any()  # the shading camera matters
+    elif mode == "split_object":
+        oc, oz, _, _ = O.render(_camera_b(s), semantics=abi.PRK_SEM_SCALAR, phong=True, tris_per_object=T,
+                                setup=abi.PRK_SETUP_PHONG | abi.PRK_SETUP_BITMAP, setup_camera=s)
     elif mode == "mutate":
         m = _dropin_scene(salt=1)
         m.vertices[:, 0] = m.vertices[:, 0] * np.float32(0.75) + np.float32(0.125)
@@ -1016,7 +1063,7 @@ def test_dropin_demo_matches_oracle(gpu, tmp_path, mode, bands):
         oc, oz, _, _ = O.render(s, semantics=abi.PRK_SEM_AVX_ST, tris_per_object=T, color=oc, z=oz)
     cd = channel_diff(gc, oc)
     assert (gz.view(np.uint32) == oz.view(np.uint32)).all(), mode
-    if mode == "scalar_object_phong":  # the scalar Phong contract: +-1 LSB (double pow)
+    if mode in ("scalar_object_phong", "split_object"):  # the scalar Phong contract: +-1 LSB (double pow)
         assert (cd <= COLOR_TOL).all(), mode
     else:
         assert (gc == oc).all(), mode
@@ -1024,7 +1071,7 @@ def test_dropin_demo_matches_oracle(gpu, tmp_path, mode, bands):
     # FillEdgeTable's return values (projekt.cpp:4119) summed over the frame's
     # calls equal the oracle's edge counts: per triangle, or the whole sphere
     edges = int(run.stdout.split("edges=")[1].split()[0])
-    if mode in ("queue", "lines", "st", "scalar", "camera", "vertexlit", "interp"):
+    if mode in ("queue", "lines", "st", "scalar", "camera", "vertexlit", "interp", "split_st", "split_queue"):
         assert edges == sum(len(O.fill_edge_table(s, t, 1)) for t in range(T)), mode
     elif mode.startswith("scalar_object") or mode == "interp_object":
         assert edges == len(O.fill_edge_table(s, 0, T, phong=mode.endswith("phong"))), mode

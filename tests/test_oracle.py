@@ -53,6 +53,40 @@ def test_two_restatements_agree_fill_edge_table_inputs(setup):
     assert (o[0] != d[0]).any()
 
 
+def split_camera_scenes(s):
+    """(setup scene, draw scene): the caller moved the camera and changed the
+    lights between FillEdgeTable and DrawModel* (projekt.cpp:3885-3910 vs
+    452-458 / 2042-2046)."""
+    import copy
+    a = copy.copy(s)
+    b = copy.copy(s)
+    D, F, M2P, cx, cy = s.transform
+    b.transform = (D * 1.25, F, M2P, cx + 9.0, cy - 5.0)
+    b.lights = [((-1.0, 2.0, 2.5), (0.3, 0.9, 0.5, 1.0))]
+    b.ambient = (0.1, 0.15, 0.3, 1.0)
+    return a, b
+
+
+@pytest.mark.parametrize("sem,phong,tex", [MODES[0], MODES[1], MODES[2], MODES[4], MODES[5]])
+def test_two_restatements_agree_split_camera(sem, phong, tex):
+    """Setup with FillEdgeTable's camera and lights, span shading with the
+    ones DrawModel* reads: both restatements agree, and the frame differs from
+    either camera alone where the path reads it (Phong shading reads the
+    draw's, Gouraud setup lighting and the projection FillEdgeTable's)."""
+    s = scenes.random_soup(50, 96, 64, radius=14, seed=31, textured=tex, lights=scenes.LIGHTS_TWO,
+                           ambient=scenes.AMBIENT_TWO)
+    su, dr = split_camera_scenes(s)
+    o = O.render(dr, semantics=sem, phong=phong, setup_camera=su)
+    assert same(o, pyref.render(dr, sem, phong, setup_camera=su))
+    # geometry (z, coverage) is FillEdgeTable's camera's
+    g = O.render(su, semantics=sem, phong=phong)
+    assert (o[1].view(np.uint32) == g[1].view(np.uint32)).all() and (o[2] == g[2]).all()
+    if phong:  # the shading is the draw's camera's
+        assert (o[0] != g[0]).any()
+    else:  # Gouraud: every colour comes from the setup
+        assert (o[0] == g[0]).all()
+
+
 def test_oracle_rejects_undefined_setups():
     """A draw reading edge fields its FillEdgeTable never wrote is undefined
     (MinNormal without PhongShading, UV gradients without a Bitmap)."""
