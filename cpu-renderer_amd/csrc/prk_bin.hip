@@ -214,6 +214,9 @@ constexpr uint32_t kRecRun = 2048;
 #ifndef PRK_BIN_BAND
 #define PRK_BIN_BAND 1  // row bands: k_bin_band (one launch) instead of k_bin_count + k_setup_rec
 #endif
+#ifndef PRK_BAND_COALESCED
+#define PRK_BAND_COALESCED 1  // k_bin_band: a one-draw run's positions as coalesced float4 loads through LDS
+#endif
 __device__ uint32_t cs_block_excl_scan(uint32_t v, uint32_t *scratch, uint32_t &total);
 __global__ void __launch_bounds__(kCountThreads) k_setup_rec(FrameParams fp, const uint32_t *__restrict__ tri_n) {
     __shared__ float4 stage[kCountThreads / 64][64 * 10];
@@ -266,31 +269,64 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_band(FrameParams fp, uint
     __shared__ uint32_t scratch[kCountThreads / 64];
     const uint32_t g0 = blockIdx.x * kRecRun;
     uint32_t n = 0;
-    // the run's positions (8 triangles per thread) are all requested first, so
-    // their loads overlap instead of one round trip per 256 triangles
     constexpr int kIt = kRecRun / kCountThreads;
+    // The run's positions.  One draw whose run is 16-byte aligned in its
+    // geometry (the usual frame): the run's 9 * kRecRun floats are contiguous,
+    // so each half of it comes in as coalesced float4 loads (a wave
+    // instruction reads 1 KiB in a row) into LDS (the record stage's space)
+    // and each thread takes its triangle's nine floats from there.  Otherwise
+    // every thread loads its triangles' nine floats itself, all requested up
+    // front so the loads overlap (a wave instruction then touches 18 cache
+    // lines for 256 bytes).
+    constexpr int kHalf = kRecRun / 2;                  // triangles per LDS half
+    constexpr int kV4 = kHalf * 9 / 4 / kCountThreads;  // float4 per thread per half
+    static_assert(kHalf * 9 % (4 * kCountThreads) == 0 && kHalf * 9 * 4 <= (int)sizeof(stage), "LDS half");
+    const uint32_t gt0 = fp.draw0.geom_tri0 + (g0 - fp.draw0.first_global);
+    const bool coal = PRK_BAND_COALESCED && fp.ndraws == 1 && (gt0 & 3u) == 0 &&
+                      g0 + (uint32_t)kRecRun <= fp.tri_count;  // (a whole run: no tail to mask)
     float pv[kIt][9];
     const DrawRec *pd[kIt];
+    if (!coal) {
 #pragma unroll
-    for (int it = 0; it < kIt; ++it) {
-        const uint32_t g = g0 + it * kCountThreads + threadIdx.x;
-        pd[it] = fp.draws;
-        if (g < fp.tri_count) {
-            uint32_t gt;
-            resolve_draw(fp, g, pd[it], gt);
-            const float *v = pd[it]->V + 9 * (size_t)gt;
+        for (int it = 0; it < kIt; ++it) {
+            const uint32_t g = g0 + it * kCountThreads + threadIdx.x;
+            pd[it] = fp.draws;
+            if (g < fp.tri_count) {
+                uint32_t gt;
+                resolve_draw(fp, g, pd[it], gt);
+                const float *v = pd[it]->V + 9 * (size_t)gt;
 #pragma unroll
-            for (int j = 0; j < 9; ++j) pv[it][j] = v[j];
+                for (int j = 0; j < 9; ++j) pv[it][j] = v[j];
+            }
         }
     }
+    const float *lf = reinterpret_cast<const float *>(&stage[0][0]);
 #pragma unroll
     for (int it = 0; it < kIt; ++it) {
         const uint32_t k = (uint32_t)it * kCountThreads;
         const uint32_t g = g0 + k + threadIdx.x;
+        if (coal && it % (kIt / 2) == 0) {  // this half's positions into LDS
+            const float4 *src = reinterpret_cast<const float4 *>(fp.draw0.V + 9 * ((size_t)gt0 + it * kCountThreads));
+            if (it) __syncthreads();  // (the previous half's reads)
+            float4 *lv = &stage[0][0];
+#pragma unroll
+            for (int kk = 0; kk < kV4; ++kk) lv[kk * kCountThreads + threadIdx.x] = src[kk * kCountThreads + threadIdx.x];
+            __syncthreads();
+        }
         uint32_t ne = 0;
         if (g < fp.tri_count) {
             TileRange tr;
-            if (!tri_tile_range_raw(fp, pd[it], pv[it], tr)) {
+            bool hit;
+            if (coal) {
+                float v9[9];
+                const int t = (it % (kIt / 2)) * kCountThreads + (int)threadIdx.x;
+#pragma unroll
+                for (int j = 0; j < 9; ++j) v9[j] = lf[9 * t + j];
+                hit = tri_tile_range_raw(fp, fp.draws, v9, tr);
+            } else {
+                hit = tri_tile_range_raw(fp, pd[it], pv[it], tr);
+            }
+            if (!hit) {
                 tr.tx0 = 1; tr.tx1 = 0; tr.ty0 = 1; tr.ty1 = 0; tr.oty0 = 1; tr.oty1 = 0;
             }
             ne = range_entries(tr);

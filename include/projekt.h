@@ -247,10 +247,11 @@ struct state {
     std::vector<frame_object> Objects;
     std::vector<pending_draw> Draws;
     std::vector<camera> Cameras;               // the frame's distinct camera / light snapshots, in order
-    // the raw bytes of Commands->Transform and LightData at the last camera
-    // lookup and the camera they gave: an unchanged Commands (every call of a
-    // usual frame) is one memcmp
-    unsigned char RawCam[sizeof(projective_transform) + sizeof(light_data)];
+    // Commands->Transform and the used part of LightData at the last camera
+    // lookup, as raw bytes, and the camera they gave: an unchanged Commands
+    // (every call of a usual frame) costs a compare of ~70 bytes
+    projective_transform RawT;
+    light_data RawL;
     uint32_t RawCamId = 0xFFFFFFFFu;
     std::vector<prk_edge> Edges;
     std::vector<prk_span> Spans;
@@ -459,11 +460,21 @@ inline bool camera_is(const camera &k, const game_render_commands *C) {
     }
     return true;
 }
+// The bytes a camera lookup compares: the transform, the light count and
+// ambient term, and the lights in use.
+// (fixed-size compares, inlined: this runs twice per drawn object)
+inline bool raw_camera_same(const state &st, const game_render_commands *C) {
+    const light_data &a = C->LightData, &b = st.RawL;
+    if (__builtin_memcmp(&C->Transform, &st.RawT, sizeof(projective_transform)) != 0 || a.LightCount != b.LightCount ||
+        a.LightCount > PRK_MAX_LIGHTS ||
+        __builtin_memcmp(&a.AmbientIntensity, &b.AmbientIntensity, sizeof a.AmbientIntensity) != 0)
+        return false;
+    for (u32 i = 0; i < a.LightCount; ++i)
+        if (__builtin_memcmp(&a.Lights[i], &b.Lights[i], sizeof(a.Lights[0])) != 0) return false;
+    return true;
+}
 inline uint32_t camera_id(state &st, const game_render_commands *C) {
-    unsigned char raw[sizeof st.RawCam];
-    memcpy(raw, &C->Transform, sizeof(projective_transform));
-    memcpy(raw + sizeof(projective_transform), &C->LightData, sizeof(light_data));
-    if (st.RawCamId < st.Cameras.size() && memcmp(raw, st.RawCam, sizeof raw) == 0) return st.RawCamId;
+    if (st.RawCamId < st.Cameras.size() && raw_camera_same(st, C)) return st.RawCamId;
     // a camera seen lately (a caller switching between two, e.g. one for
     // FillEdgeTable and one for DrawModel*), else a new entry
     uint32_t id = (uint32_t)st.Cameras.size();
@@ -473,7 +484,8 @@ inline uint32_t camera_id(state &st, const game_render_commands *C) {
             break;
         }
     if (id == st.Cameras.size()) st.Cameras.push_back(camera_of(C));
-    memcpy(st.RawCam, raw, sizeof raw);
+    memcpy(&st.RawT, &C->Transform, sizeof(projective_transform));
+    memcpy(&st.RawL, &C->LightData, sizeof(light_data));
     st.RawCamId = id;
     return id;
 }
@@ -592,7 +604,7 @@ inline void draw(loaded_bitmap *Buffer, edge_info *Edges, u32 EdgeCount, game_re
                 b.Texture == d.Texture && b.Camera == d.Camera && b.SetupCamera == d.SetupCamera) {
                 const frame_object &f = st.Objects[b.First];
                 if (o.FirstTri == f.FirstTri + b.RunTris && o.Tris == f.Tris && o.Setup == f.Setup &&
-                    memcmp(o.P, f.P, sizeof o.P) == 0) {
+                    __builtin_memcmp(o.P, f.P, sizeof o.P) == 0) {
                     ++b.Count;
                     b.RunTris += o.Tris;
                     st.LastStatus = PRK_OK;

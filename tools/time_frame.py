@@ -48,5 +48,8 @@ if os.environ.get("PRK_PROF_PRINT"):
         tot = sum(c[off:off + 4]) or 1
         print("  %-5s cycles: setup %.3g (%.0f%%)  walk %.3g (%.0f%%)  scan %.3g (%.0f%%)  items %.3g (%.0f%%)" % (
             (name,) + tuple(v for k in range(4) for v in (c[off + k], 100.0 * c[off + k] / tot))))
-    print("  spans (per frame): vis %d (nonempty %d, items %d)  shade %d (won %d, won px %d, px of won spans %d)" % (
-        c[8] / 12, c[9] / 12, c[10] / 12, c[12] / 12, c[13] / 12, c[14] / 12, c[15] / 12))
+    f = float(steps)
+    ch, it, win, items, act, sp = [c[8 + k] / f for k in range(6)]
+    print("  vis events per frame: chunks %.0f  row iterations %.0f (%.2f per chunk)  item windows %.0f "
+          "(%.2f per iteration)  items %.0f (%.1f per window)  active lanes %.1f per iteration  spans with items %.0f"
+          % (ch, it, it / max(ch, 1), win, win / max(it, 1), items, items / max(win, 1), act / max(it, 1), sp))
