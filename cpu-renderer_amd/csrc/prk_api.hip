@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/prk.h"
+#include "../../include/prk_edge_count.h"
 #include "prk_device.h"
 
 extern "C" {
@@ -2000,68 +2001,13 @@ int prk_download_winners(prk_context *c, int32_t *w) {
 // (ProjectVertex 74-93, Normalize(a) = (1/sqrt(a.a))*a); the library is built
 // with -ffp-contract=off, so host and device round alike.  The setup itself
 // (edges, gradients, lighting, MergeSort) runs on the GPU at the flush.
-static inline void host_project(const float c[3], const prk_transform *T, float r[3]) {
-    r[0] = r[1] = r[2] = 0.0f;
-    const float d = T->DistanceAboveTarget - c[2];
-    if (d > 0.2f) {
-        const float k = (1.0f / d) * T->FocalLength;
-        const float px = k * c[0], py = k * c[1];
-        r[0] = T->ScreenCenter[0] + T->MetersToPixels * px;
-        r[1] = T->ScreenCenter[1] + T->MetersToPixels * py;
-        r[2] = d + T->MetersToPixels * 0.0f;
-    }
-}
-static inline void host_normalize(float &x, float &y, float &z) {
-    const float s = 1.0f / sqrtf((x * x + y * y) + z * z);
-    x = s * x;
-    y = s * y;
-    z = s * z;
-}
-
+// Per triangle: include/prk_edge_count.h (the drop-in header inlines it).
 int prk_fill_edge_count(const float *V, uint32_t vertex_count, const float P[3], const prk_transform *T,
                         uint32_t *count_out) {
     if (!count_out || !T || (!V && vertex_count >= 3)) return PRK_ERR_ARG;
     const float p0 = P ? P[0] : 0.0f, p1 = P ? P[1] : 0.0f, p2 = P ? P[2] : 0.0f;
     uint32_t n = 0;
-    for (uint32_t t = 0; t < vertex_count / 3; ++t) {
-        float pr[3][3];
-        for (int k = 0; k < 3; ++k) {
-            const float *v = V + 9 * (size_t)t + 3 * k;
-            const float c[3] = {v[0] + p0, v[1] + p1, v[2] + p2};  // 3898-3903
-            host_project(c, T, pr[k]);
-        }
-        float ax = pr[1][0] - pr[0][0], ay = pr[1][1] - pr[0][1], az = pr[1][2] - pr[0][2];
-        float bx = pr[2][0] - pr[0][0], by = pr[2][1] - pr[0][1], bz = pr[2][2] - pr[0][2];
-        // Back-face test (3926-3943): Inner((0,0,-1), Cross(Normalize(A),
-        // Normalize(B))) > 0, i.e. cz = a.x*b.y - a.y*b.x < 0 of the normalised
-        // a, b.  Their components carry a relative error of at most ~5 ulp and
-        // are at most 1, so the rounded cz lies within ~2^-19 of the exact
-        // (Ax*By - Ay*Bx) / (|A||B|): when that exceeds 2^-16 in magnitude
-        // (computed in double from the same float A, B: products exact), its
-        // sign is the test's, and the two normalisations are skipped.  Other
-        // cases (near-degenerate, tiny / huge / non-finite) take the float ops.
-        const float ma = std::max(std::fabs(ax), std::max(std::fabs(ay), std::fabs(az)));
-        const float mb = std::max(std::fabs(bx), std::max(std::fabs(by), std::fabs(bz)));
-        bool front;
-        const double D = (double)ax * by - (double)ay * bx;
-        const double A2 = ((double)ax * ax + (double)ay * ay) + (double)az * az;
-        const double B2 = ((double)bx * bx + (double)by * by) + (double)bz * bz;
-        if (ma >= 0x1p-40f && ma <= 0x1p40f && mb >= 0x1p-40f && mb <= 0x1p40f && D * D > 0x1p-32 * A2 * B2) {
-            front = D < 0.0;
-        } else {
-            host_normalize(ax, ay, az);
-            host_normalize(bx, by, bz);
-            const float cx = ay * bz - az * by, cy = az * bx - ax * bz, cz = ax * by - ay * bx;
-            front = (0.0f * cx + 0.0f * cy) + (-1.0f) * cz > 0.0f;  // 3943
-        }
-        uint32_t ne = 0;  // (branch-free: the facing of a triangle soup is a coin toss)
-        for (int e = 0; e < 3; ++e) {
-            const float y0 = pr[e][1], y1 = pr[(e + 1) % 3][1];
-            const float mn = y0 > y1 ? y1 : y0, mx = y0 > y1 ? y0 : y1;  // 3957-3966
-            ne += (uint32_t)((mx > 0) & (mn - mx != 0));                   // 3968, 4066
-        }
-        n += front ? ne : 0u;
-    }
+    for (uint32_t t = 0; t < vertex_count / 3; ++t) n += prk_tri_edge_count(V + 9 * (size_t)t, p0, p1, p2, T);
     *count_out = n;
     return PRK_OK;
 }

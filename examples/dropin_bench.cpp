@@ -139,6 +139,38 @@ int main(int argc, char **argv) {
                     issue / timed, flush / timed, down / timed, gpu / timed,
                     (double)W * H / (total / timed * 1e-3) / 1e6);
     }
+    // The host calls split by entry point: every object's FillEdgeTable into
+    // an EdgeMemory of its own, then every DrawModelOptimized, timed apart
+    // (the frame is then run and downloaded as above, untimed).
+    double fill_pass = 0, draw_pass = 0;
+    {
+        std::vector<edge_info> EM(T);
+        std::vector<u32> ne(T);
+        for (int f = 0; f < frames + 1; ++f) {
+            PRK_ClearNextFrame(0xFF000000u, -FLT_MAX);
+            auto t1 = clk::now();
+            for (u32 t = 0; t < T; ++t) {
+                render_entry_3d_object Object = {};
+                Object.VertexCount = 3;
+                Object.PhongShading = 1;
+                Object.VertexData = &V[3 * (size_t)t];
+                Object.ColorData = &C[3 * (size_t)t];
+                Object.NormalData = &N[3 * (size_t)t];
+                Object.UVData = &UV[3 * (size_t)t];
+                Object.EdgeMemory = &EM[t];
+                Object.Bitmap = &Texture;
+                ne[t] = FillEdgeTable(&Object, &Commands, 1);
+            }
+            if (f > 0) fill_pass += ms_since(t1);
+            t1 = clk::now();
+            for (u32 t = 0; t < T; ++t) DrawModelOptimized(nullptr, &Buffer, &EM[t], ne[t], &Commands, &Texture, 1);
+            if (f > 0) draw_pass += ms_since(t1);
+            if (PRK_CompleteAllWork(&Buffer, &Commands) != PRK_OK) {
+                std::fprintf(stderr, "dropin_bench: CompleteAllWork failed (status %d)\n", PRK_LastStatus());
+                return 2;
+            }
+        }
+    }
     // The host calls split: frames of FillEdgeTable calls alone.
     double fill = 0;
     for (int f = 0; f < frames + 1; ++f) {
@@ -162,13 +194,19 @@ int main(int argc, char **argv) {
     }
     // ... and its parts: the visible-edge count (the call's return value) and
     // the vertex snapshot into pinned memory, each alone.
-    double count = 0, copy = 0;
+    double count = 0, count_inline = 0, copy = 0, copy_heap = 0, copy_nt = 0;
     {
         const prk_dropin::camera cam = prk_dropin::camera_of(&Commands);
         const float P[3] = {0.0f, 0.0f, 0.0f};
         float *a[4] = {nullptr, nullptr, nullptr, nullptr};
         const size_t comp[4] = {3, 4, 3, 2};
         for (int k = 0; k < 4; ++k) prk_host_alloc(prk_dropin::S().Ctx, 3 * (size_t)T * comp[k] * 4, (void **)&a[k]);
+        float *h[4] = {nullptr, nullptr, nullptr, nullptr};
+        for (int k = 0; k < 4; ++k) {
+            const size_t bytes = ((3 * (size_t)T * comp[k] * 4) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+            h[k] = (float *)std::aligned_alloc(2u << 20, bytes);
+            if (h[k]) memset(h[k], 0, bytes);
+        }
         uint64_t sink = 0;
         for (int f = 0; f < frames + 1; ++f) {
             auto t1 = clk::now();
@@ -178,6 +216,15 @@ int main(int argc, char **argv) {
                 sink += e;
             }
             if (f > 0) count += ms_since(t1);
+#if PRK_EC_SSE
+            t1 = clk::now();
+            for (u32 t = 0; t < T; ++t) {
+                const float *v = (const float *)&V[3 * (size_t)t];
+                sink += prk_tri_edge_count_sse(_mm_loadu_ps(v), _mm_loadu_ps(v + 4), _mm_load_ss(v + 8), P[0], P[1],
+                                               P[2], &cam.T);
+            }
+            if (f > 0) count_inline += ms_since(t1);
+#endif
             t1 = clk::now();
             if (a[0] && a[1] && a[2] && a[3])
                 for (u32 t = 0; t < T; ++t) {
@@ -187,12 +234,44 @@ int main(int argc, char **argv) {
                     memcpy(a[3] + 6 * (size_t)t, &UV[3 * (size_t)t], 24);
                 }
             if (f > 0) copy += ms_since(t1);
+            // the same copy into pageable heap memory (transparent huge pages)
+            t1 = clk::now();
+            if (h[0] && h[1] && h[2] && h[3])
+                for (u32 t = 0; t < T; ++t) {
+                    memcpy(h[0] + 9 * (size_t)t, &V[3 * (size_t)t], 36);
+                    memcpy(h[1] + 12 * (size_t)t, &C[3 * (size_t)t], 48);
+                    memcpy(h[2] + 9 * (size_t)t, &N[3 * (size_t)t], 36);
+                    memcpy(h[3] + 6 * (size_t)t, &UV[3 * (size_t)t], 24);
+                }
+            if (f > 0) copy_heap += ms_since(t1);
+#if PRK_EC_SSE
+            // ... and into pinned memory with streaming stores, four triangles
+            // (whole 16-byte blocks of every array) at a time
+            t1 = clk::now();
+            if (a[0] && a[1] && a[2] && a[3]) {
+                const float *src[4] = {(const float *)V.data(), (const float *)C.data(), (const float *)N.data(),
+                                       (const float *)UV.data()};
+                for (u32 t = 0; t + 4 <= T; t += 4)
+                    for (int k = 0; k < 4; ++k) {
+                        const size_t w = 3 * comp[k];  // floats per triangle
+                        const float *sp = src[k] + w * t;
+                        float *dp = a[k] + w * t;
+                        for (size_t q = 0; q < w; ++q) _mm_stream_ps(dp + 4 * q, _mm_loadu_ps(sp + 4 * q));
+                    }
+                _mm_sfence();
+            }
+            if (f > 0) copy_nt += ms_since(t1);
+#endif
         }
         for (int k = 0; k < 4; ++k) prk_host_free(prk_dropin::S().Ctx, a[k]);
+        for (int k = 0; k < 4; ++k) std::free(h[k]);
         if (sink == 1) std::printf(" ");
     }
-    std::printf("}, \"fill_edge_table_only_ms\": %.3f, \"edge_count_only_ms\": %.3f, \"snapshot_copy_only_ms\": %.3f, "
-                "\"frames\": %d}\n", fill / frames, count / frames, copy / frames, frames);
+    std::printf("}, \"fill_edge_table_pass_ms\": %.3f, \"draw_model_pass_ms\": %.3f, \"fill_edge_table_only_ms\": %.3f, "
+                "\"edge_count_only_ms\": %.3f, \"edge_count_inline_ms\": %.3f, \"snapshot_copy_only_ms\": %.3f, "
+                "\"snapshot_copy_heap_ms\": %.3f, \"snapshot_copy_stream_ms\": %.3f, \"frames\": %d}\n",
+                fill_pass / frames, draw_pass / frames, fill / frames, count / frames, count_inline / frames,
+                copy / frames, copy_heap / frames, copy_nt / frames, frames);
     PRK_Shutdown();
     return 0;
 }

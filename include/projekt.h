@@ -24,13 +24,14 @@
 //    Object->Bitmap != 0 (raw colours + normals vs per-vertex lighting,
 //    4012-4063; white-based lighting and UV gradients, 4034-4054, 4078-4089:
 //    the edges are built from them whatever DrawModel* later draws them
-//    with), and leaves a token in Object->EdgeMemory that
-//    DrawModel* read back; the setup itself (projection, cull, edges,
-//    lighting, MergeSort) runs on the GPU at PRK_CompleteAllWork.  It
-//    returns the reference's value, the visible edge count (4119; 0 for an
-//    object that draws nothing, e.g. a back-facing triangle), computed on the
-//    host by prk_fill_edge_count.  EdgeMemory holds the token, not edge_info
-//    records.
+//    with), and leaves a token in Object->EdgeMemory (the object's arena
+//    range, P, camera and setup: 36 bytes) that DrawModel* read back; the
+//    setup itself (projection, cull, edges, lighting, MergeSort) runs on the
+//    GPU at PRK_CompleteAllWork.  It returns the reference's value, the
+//    visible edge count (4119; 0 for an object that draws nothing, e.g. a
+//    back-facing triangle), computed on the host (include/prk_edge_count.h,
+//    inline for one-triangle objects, else prk_fill_edge_count).  EdgeMemory
+//    holds the token, not edge_info records.
 //  * DrawModelOptimized(RenderQueue, ...) and DrawModelOptimizedLines draw
 //    the object with FillLineOptimized semantics (FillLinesOptimized has the
 //    same block math); DrawModelOptimized(Buffer, ...) with the
@@ -77,6 +78,7 @@
 #include <vector>
 
 #include "prk.h"
+#include "prk_edge_count.h"
 
 #ifndef PRK_CALLER_TYPES
 typedef float r32;
@@ -191,22 +193,20 @@ struct model_render_work {
 
 namespace prk_dropin {
 
-// Token FillEdgeTable leaves in Object->EdgeMemory for DrawModel*.
+// What FillEdgeTable leaves in Object->EdgeMemory for DrawModel*: the
+// object itself (its triangles in the frame's arena, P, camera and setup), so
+// the draw reads back the record its FillEdgeTable just wrote, and the frame
+// keeps no per-object table.
 struct object_token {
     uint32_t Magic;
-    uint32_t Frame;    // frame serial the object was filled in
-    uint32_t Object;   // index into the frame's object table
-    uint32_t TriCount;
-};
-static_assert(sizeof(object_token) <= sizeof(edge_info), "token must fit one edge_info");
-static const uint32_t kMagic = 0x4B525032u;  // "PRK2"
-
-struct frame_object {
-    uint32_t FirstTri, Tris;  // Tris == 0: FillEdgeTable found no edge (nothing to draw)
+    uint32_t Frame;           // frame serial the object was filled in
+    uint32_t FirstTri, Tris;  // its triangles in the arena; Tris == 0: no edge (nothing to draw)
     float P[3];
     uint32_t Camera;          // Commands->Transform / LightData as they were at FillEdgeTable
     int32_t Setup;            // FillEdgeTable's PhongShading and Object->Bitmap != 0 (PRK_SETUP_*)
 };
+static_assert(sizeof(object_token) <= sizeof(edge_info), "token must fit one edge_info");
+static const uint32_t kMagic = 0x4B525033u;  // "PRK3"
 
 // Commands->Transform and LightData as one draw saw them.
 struct camera {
@@ -217,16 +217,19 @@ struct camera {
 enum { DRAW_OBJECT = 0, DRAW_EDGES = 1, DRAW_SPANS = 2 };
 struct pending_draw {
     int Kind;
-    uint32_t First, Count;  // object index / range of Edges / range of Spans
+    uint32_t First, Count;  // DRAW_OBJECT: first triangle, objects; else range of Edges / Spans
     int32_t Semantics, Phong, Texture;
     // indices into the frame's cameras: the one FillEdgeTable saw (setup:
     // projection, Gouraud lighting, 3885-4063) and the one the DrawModel* call
     // sees (span shading: Phong + unprojection, 452-458, 2042-2046, 3030-3034)
     uint32_t SetupCamera, Camera;
     // DRAW_OBJECT: Count objects drawn alike, consecutive in the arena, of
-    // one size and offset, RunTris triangles in all: one library call (the
-    // per-triangle objects of a reference caller make one run per frame)
-    uint32_t RunTris;
+    // ObjTris triangles each, one offset P and setup, RunTris triangles in
+    // all: one library call (the per-triangle objects of a reference caller
+    // make one run per frame)
+    uint32_t RunTris, ObjTris;
+    float P[3];
+    int32_t Setup;
 };
 
 struct state {
@@ -244,7 +247,6 @@ struct state {
     // geometry tail), queueing the frames, waiting + downloading (ms)
     double LastIssueMs = 0, LastFlushMs = 0, LastDownloadMs = 0;
     int32_t Geom = -1;
-    std::vector<frame_object> Objects;
     std::vector<pending_draw> Draws;
     std::vector<camera> Cameras;               // the frame's distinct camera / light snapshots, in order
     // Commands->Transform and the used part of LightData at the last camera
@@ -473,8 +475,9 @@ inline bool raw_camera_same(const state &st, const game_render_commands *C) {
         if (__builtin_memcmp(&a.Lights[i], &b.Lights[i], sizeof(a.Lights[0])) != 0) return false;
     return true;
 }
-inline uint32_t camera_id(state &st, const game_render_commands *C) {
-    if (st.RawCamId < st.Cameras.size() && raw_camera_same(st, C)) return st.RawCamId;
+// (the lookup when the raw bytes changed: out of line, so the per-call fast
+// path below stays a few compares)
+__attribute__((noinline)) inline uint32_t camera_id_slow(state &st, const game_render_commands *C) {
     // a camera seen lately (a caller switching between two, e.g. one for
     // FillEdgeTable and one for DrawModel*), else a new entry
     uint32_t id = (uint32_t)st.Cameras.size();
@@ -488,6 +491,11 @@ inline uint32_t camera_id(state &st, const game_render_commands *C) {
     memcpy(&st.RawL, &C->LightData, sizeof(light_data));
     st.RawCamId = id;
     return id;
+}
+// (RawCamId is reset with the frame's cameras, end_frame)
+inline uint32_t camera_id(state &st, const game_render_commands *C) {
+    if (st.RawCamId != 0xFFFFFFFFu && raw_camera_same(st, C)) return st.RawCamId;
+    return camera_id_slow(st, C);
 }
 
 inline int set_camera(const camera &setup, const camera &shade, bool split) {
@@ -572,7 +580,7 @@ inline void draw(loaded_bitmap *Buffer, edge_info *Edges, u32 EdgeCount, game_re
                  loaded_bitmap *Bitmap, b32 PhongShading, int32_t semantics) {
     state &st = S();
     if (!st.Ctx || !Edges || EdgeCount == 0) return;  // 0 edges: nothing to draw (P1)
-    if (!open_frame(Buffer, Commands)) return;
+    if (!(st.FrameOpen && st.Target == Buffer && st.Commands == Commands) && !open_frame(Buffer, Commands)) return;
     int32_t tex = -1;
     if (Bitmap) {  // the same bitmap as the previous draw: its handle, already fresh this frame
         if (Bitmap == st.LastBitmap && Bitmap->Memory == st.LastBitmapMemory) tex = st.LastTexture;
@@ -583,44 +591,52 @@ inline void draw(loaded_bitmap *Buffer, edge_info *Edges, u32 EdgeCount, game_re
             st.LastTexture = tex;
         }
     }
-    object_token tok;
-    memcpy(&tok, Edges, sizeof tok);
-    pending_draw d{};
-    d.Semantics = semantics;
-    d.Phong = PhongShading ? 1 : 0;
-    d.Texture = tex;
-    if (tok.Magic == kMagic && tok.Frame == st.Frame && tok.Object < st.Objects.size()) {
-        d.Kind = DRAW_OBJECT;
-        d.First = tok.Object;
-        d.Count = 1;
-        const frame_object &o = st.Objects[tok.Object];
-        d.RunTris = o.Tris;
+    object_token o;
+    memcpy(&o, Edges, sizeof o);
+    const int32_t phong = PhongShading ? 1 : 0;
+    // a token of this frame whose triangles are in the arena (a stale or
+    // foreign one is drawn as an edge list, which is what it then is)
+    if (o.Magic == kMagic && o.Frame == st.Frame && o.Camera < st.Cameras.size() &&
+        (uint64_t)o.FirstTri + o.Tris <= st.ArenaUsed / 3) {
         if (o.Tris == 0) return;  // FillEdgeTable wrote no edge: nothing to draw
-        d.SetupCamera = o.Camera;           // as FillEdgeTable saw it
-        d.Camera = camera_id(st, Commands);  // as this call sees it (shading)
+        const uint32_t cam = camera_id(st, Commands);  // as this call sees it (shading)
         if (!st.Draws.empty()) {  // the next object of the previous draw's run
             pending_draw &b = st.Draws.back();
-            if (b.Kind == DRAW_OBJECT && b.Semantics == d.Semantics && b.Phong == d.Phong &&
-                b.Texture == d.Texture && b.Camera == d.Camera && b.SetupCamera == d.SetupCamera) {
-                const frame_object &f = st.Objects[b.First];
-                if (o.FirstTri == f.FirstTri + b.RunTris && o.Tris == f.Tris && o.Setup == f.Setup &&
-                    __builtin_memcmp(o.P, f.P, sizeof o.P) == 0) {
-                    ++b.Count;
-                    b.RunTris += o.Tris;
-                    st.LastStatus = PRK_OK;
-                    return;
-                }
+            if (b.Kind == DRAW_OBJECT && o.FirstTri == b.First + b.RunTris && o.Tris == b.ObjTris &&
+                b.Camera == cam && b.SetupCamera == o.Camera && b.Semantics == semantics && b.Phong == phong &&
+                b.Texture == tex && b.Setup == o.Setup && __builtin_memcmp(o.P, b.P, sizeof o.P) == 0) {
+                ++b.Count;
+                b.RunTris += o.Tris;
+                st.LastStatus = PRK_OK;
+                return;
             }
         }
+        pending_draw d{};
+        d.Kind = DRAW_OBJECT;
+        d.Semantics = semantics;
+        d.Phong = phong;
+        d.Texture = tex;
+        d.First = o.FirstTri;
+        d.Count = 1;
+        d.RunTris = d.ObjTris = o.Tris;
+        memcpy(d.P, o.P, sizeof d.P);
+        d.Setup = o.Setup;
+        d.SetupCamera = o.Camera;  // as FillEdgeTable saw it
+        d.Camera = cam;
+        st.Draws.push_back(d);
     } else {  // a caller's own edge_info list, drawn as given
+        pending_draw d{};
+        d.Semantics = semantics;
+        d.Phong = phong;
+        d.Texture = tex;
         d.Camera = d.SetupCamera = camera_id(st, Commands);
         d.Kind = DRAW_EDGES;
         d.First = (uint32_t)st.Edges.size();
         d.Count = EdgeCount;
         st.Edges.resize(st.Edges.size() + EdgeCount);
         for (u32 i = 0; i < EdgeCount; ++i) edge_in(st.Edges[d.First + i], Edges[i]);
+        st.Draws.push_back(d);
     }
-    st.Draws.push_back(d);
     st.LastStatus = PRK_OK;
 }
 
@@ -683,9 +699,8 @@ inline int issue(state &st) {
             for (size_t k = i; k < j && r == PRK_OK; ++k) {
                 const pending_draw &d = st.Draws[k];
                 if (d.Kind == DRAW_OBJECT) {
-                    const frame_object &o = st.Objects[d.First];
-                    r = prk_draw_objects_setup(c, st.Geom, o.FirstTri, d.RunTris, o.Tris, o.P, d.Semantics,
-                                               d.Phong, d.Texture, o.Setup);
+                    r = prk_draw_objects_setup(c, st.Geom, d.First, d.RunTris, d.ObjTris, d.P, d.Semantics,
+                                               d.Phong, d.Texture, d.Setup);
                 } else if (d.Kind == DRAW_EDGES) {
                     r = prk_draw_edges(c, st.Edges.data() + d.First, d.Count, d.Semantics, d.Phong, d.Texture);
                 } else {
@@ -707,7 +722,6 @@ inline void end_frame(state &st) {
     st.ArenaUsed = 0;
     st.Uploaded = 0;
     st.PushStatus = PRK_OK;
-    st.Objects.clear();
     st.Draws.clear();
     st.Cameras.clear();
     st.RawCamId = 0xFFFFFFFFu;
@@ -798,7 +812,9 @@ inline u32 FillEdgeTable(render_entry_3d_object *Object, game_render_commands *C
     if (!st.Ctx || !Object || !Commands || !Object->EdgeMemory || !Object->VertexData || Object->VertexCount < 3)
         return 0;
     const u32 T = Object->VertexCount / 3, nv = 3 * T;
-    prk_dropin::frame_object o;
+    prk_dropin::object_token o;
+    o.Magic = prk_dropin::kMagic;
+    o.Frame = st.Frame;
     o.P[0] = Object->P.x;
     o.P[1] = Object->P.y;
     o.P[2] = Object->P.z;
@@ -812,14 +828,36 @@ inline u32 FillEdgeTable(render_entry_3d_object *Object, game_render_commands *C
     // the reference's return value: the visible edge count (4119), 0 when no
     // edge is visible (e.g. a back-facing triangle)
     u32 edges = 0;
-    if (!prk_dropin::ok(prk_fill_edge_count((const float *)Object->VertexData, nv, o.P, &cam.T, &edges))) return 0;
+#if PRK_EC_SSE && !defined(PRK_DROPIN_LIB_COUNT)
+    // one triangle (the per-triangle objects of a reference caller): counted
+    // inline from the registers the snapshot then stores
+    const bool one = nv == 3;
+    __m128 q0 = _mm_setzero_ps(), q1 = q0, q2 = q0;
+    if (one) {
+        const float *v = (const float *)Object->VertexData;
+        q0 = _mm_loadu_ps(v);
+        q1 = _mm_loadu_ps(v + 4);
+        q2 = _mm_load_ss(v + 8);
+        edges = prk_tri_edge_count_sse(q0, q1, q2, o.P[0], o.P[1], o.P[2], &cam.T);
+        st.LastStatus = PRK_OK;
+    } else
+#endif
+        if (!prk_dropin::ok(prk_fill_edge_count((const float *)Object->VertexData, nv, o.P, &cam.T, &edges)))
+        return 0;
     o.FirstTri = 0;
     o.Tris = 0;
     if (edges) {  // an object with no visible edge draws nothing: nothing to upload
         if (!prk_dropin::arena_reserve(st, nv)) return 0;
         const uint32_t v0 = st.ArenaUsed;
         if (nv == 3 && Object->ColorData && Object->NormalData && Object->UVData) {  // one triangle: fixed-size copies
+#if PRK_EC_SSE && !defined(PRK_DROPIN_LIB_COUNT)
+            float *av = st.AV + 3 * (size_t)v0;  // (the registers the count read)
+            _mm_storeu_ps(av, q0);
+            _mm_storeu_ps(av + 4, q1);
+            _mm_store_ss(av + 8, q2);
+#else
             memcpy(st.AV + 3 * (size_t)v0, Object->VertexData, 36);
+#endif
             memcpy(st.AC + 4 * (size_t)v0, Object->ColorData, 48);
             memcpy(st.AN + 3 * (size_t)v0, Object->NormalData, 36);
             memcpy(st.AUV + 2 * (size_t)v0, Object->UVData, 24);
@@ -838,13 +876,7 @@ inline u32 FillEdgeTable(render_entry_3d_object *Object, game_render_commands *C
         if (st.ArenaUsed - st.Uploaded >= prk_dropin::chunk_vertices() && st.PushStatus == PRK_OK)
             prk_dropin::push_vertices(st);  // a failure is reported by PRK_CompleteAllWork
     }
-    prk_dropin::object_token tok;
-    tok.Magic = prk_dropin::kMagic;
-    tok.Frame = st.Frame;
-    tok.Object = (uint32_t)st.Objects.size();
-    tok.TriCount = o.Tris;
-    st.Objects.push_back(o);
-    memcpy(Object->EdgeMemory, &tok, sizeof tok);
+    memcpy(Object->EdgeMemory, &o, sizeof o);
     return edges;
 }
 
