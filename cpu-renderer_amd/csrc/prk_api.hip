@@ -9,6 +9,7 @@
 // HIP device and fails with PRK_ERR_DEVICE without one.
 #include <hip/hip_runtime.h>
 #include <link.h>
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -18,6 +19,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -707,17 +710,60 @@ int prk_texture_update(prk_context *c, int32_t handle, const prk_bitmap *b) {
     return PRK_OK;
 }
 
+// Allocations of 2 MB and more: heap memory on transparent huge pages,
+// page-locked with hipHostRegister, instead of hipHostMalloc's 4-KB pinned
+// pages -- the drop-in's staging arena takes ~150 MB of per-call vertex
+// snapshots a frame, which the 2-MB pages make cheaper for the CPU (TLB).
+// PRK_HOST_ALLOC_THP=0: hipHostMalloc for every size.
+static std::mutex g_thp_mu;
+static std::map<void *, size_t> g_thp;  // (any context may free)
+static bool host_alloc_thp() {
+    static const bool on = [] {
+        const char *e = std::getenv("PRK_HOST_ALLOC_THP");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 int prk_host_alloc(prk_context *c, size_t bytes, void **out) {
     if (!c || !out) return PRK_ERR_ARG;
     *out = nullptr;
     PRK_TRY(hipSetDevice(c->device));
+    constexpr size_t kHuge = (size_t)2 << 20;
+    if (bytes >= kHuge && host_alloc_thp()) {
+        const size_t sz = (bytes + kHuge - 1) & ~(kHuge - 1);
+        void *p = std::aligned_alloc(kHuge, sz);
+        if (!p) return PRK_ERR_NOMEM;
+        (void)madvise(p, sz, MADV_HUGEPAGE);  // (best effort)
+        memset(p, 0, sz);                      // (faulted in on huge pages before the pinning)
+        const hipError_t e = hipHostRegister(p, sz, hipHostRegisterPortable);
+        if (e != hipSuccess) {
+            std::free(p);
+            return status_of(e);
+        }
+        std::lock_guard<std::mutex> g(g_thp_mu);
+        g_thp[p] = sz;
+        *out = p;
+        return PRK_OK;
+    }
     PRK_TRY(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
     return PRK_OK;
 }
 
 int prk_host_free(prk_context *c, void *p) {
     if (!c) return PRK_ERR_ARG;
-    if (p) PRK_TRY(hipHostFree(p));
+    if (!p) return PRK_OK;
+    {
+        std::lock_guard<std::mutex> g(g_thp_mu);
+        auto it = g_thp.find(p);
+        if (it != g_thp.end()) {
+            g_thp.erase(it);
+            const hipError_t e = hipHostUnregister(p);
+            std::free(p);
+            return e == hipSuccess ? PRK_OK : status_of(e);
+        }
+    }
+    PRK_TRY(hipHostFree(p));
     return PRK_OK;
 }
 

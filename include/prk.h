@@ -200,7 +200,10 @@ int prk_target_upload_async(prk_context *ctx, const uint32_t *color_host, int32_
 
 /* Pinned host memory for staging (prk_host_alloc / prk_host_free), and
  * page-locking of caller memory (a framebuffer, a z-buffer) so uploads and
- * downloads run as DMA at full PCIe rate. */
+ * downloads run as DMA at full PCIe rate.  Allocations of 2 MB and more are
+ * heap memory on transparent huge pages, page-locked for every device
+ * (cheaper for the CPU to fill than 4-KB pinned pages;
+ * PRK_HOST_ALLOC_THP=0 turns this off).  Free with prk_host_free only. */
 int prk_host_alloc(prk_context *ctx, size_t bytes, void **out);
 int prk_host_free(prk_context *ctx, void *p);
 int prk_host_register(prk_context *ctx, void *p, size_t bytes);
