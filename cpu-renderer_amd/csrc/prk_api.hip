@@ -73,7 +73,14 @@ uint32_t prk_obj_walk_threads(uint32_t);
 hipError_t prk_obj_walk_group(const prk::FrameParams *, int32_t, uint32_t, const void *, const uint32_t *,
                               const unsigned long long *, const uint32_t *, uint32_t, int32_t *, const uint32_t *,
                               const uint32_t *, void *, const unsigned long long *, void *, void *, void *, void *,
-                              uint32_t *, uint32_t *, hipStream_t);
+                              uint32_t *, uint32_t *, const uint32_t *, hipStream_t);
+hipError_t prk_pr_walk_begin(const prk::FrameParams *, const prk::PrWalkArgs *, hipStream_t);
+hipError_t prk_pr_walk_group(const prk::FrameParams *, const prk::PrWalkArgs *, int32_t, uint32_t, const uint32_t *,
+                             uint32_t, uint32_t, hipStream_t);
+hipError_t prk_pr_walk_end(const prk::PrWalkArgs *, hipStream_t);
+uint32_t prk_pr_chunk_rows(void);
+int32_t prk_pr_max_row_entries(void);
+int32_t prk_pr_max_rows(void);
 hipError_t prk_span_finish(const prk::FrameParams *, const void *, uint32_t, void *, void *, void *, hipStream_t);
 hipError_t prk_scan_u32(const uint32_t *, uint32_t *, uint32_t, void *, size_t *, hipStream_t);
 hipError_t prk_scan_u64(const unsigned long long *, unsigned long long *, uint32_t, void *, size_t *, hipStream_t);
@@ -91,6 +98,7 @@ struct ObjDesc {
 };
 constexpr uint32_t kObjWave = 0x80000000u;  // ObjDesc::k1off flag: walked by one wave
 constexpr uint32_t kObjWaveTris = 48;        // objects of this many triangles or more
+constexpr uint64_t kPrMaxEntries = 1ull << 23;  // the chunked walk's list entries per pass (~3 GB of scratch)
 constexpr int kWaveListArrays = 9;           // prk_spans.hip WaveList: int32 arrays of cap + 2 entries
 
 // AVX frames shade through span records (k_walk + k_pix); must match
@@ -273,7 +281,8 @@ struct prk_context {
     struct SpanScratch {
         DevBuf d_stage, d_edges, d_ord, d_temp, d_recs, d_pos, d_span_tri, d_scnt, d_soff, d_keys_a, d_vals_a,
             d_keys_b, d_vals_b, d_offs, d_nwin, d_wtag, d_srecs, d_work, d_ekeys, d_ekeys2, d_evals, d_ecnt, d_escan,
-            d_rcnt, d_rscan, d_bound, d_oslot, d_pool, d_err, d_raw, d_most, d_cls;
+            d_rcnt, d_rscan, d_bound, d_oslot, d_pool, d_err, d_raw, d_most, d_cls, d_prrow, d_prcnt, d_preoff,
+            d_prfge, d_prccur, d_prkey, d_prest, d_prsst, d_preend, d_preendm, d_prmatch, d_prstat;
         // the pass's host tables, packed into pinned memory for one upload
         // (stage_ev: that upload, before the staging is rewritten)
         char *h_stage = nullptr;
@@ -469,7 +478,9 @@ int prk_destroy(prk_context *c) {
                         &S.d_soff, &S.d_keys_a, &S.d_vals_a, &S.d_keys_b, &S.d_vals_b, &S.d_offs, &S.d_nwin,
                         &S.d_wtag, &S.d_srecs, &S.d_work, &S.d_ekeys, &S.d_ekeys2, &S.d_evals, &S.d_ecnt,
                         &S.d_escan, &S.d_rcnt, &S.d_rscan, &S.d_bound, &S.d_oslot, &S.d_pool, &S.d_err,
-                        &S.d_raw, &S.d_most, &S.d_cls};
+                        &S.d_raw, &S.d_most, &S.d_cls, &S.d_prrow, &S.d_prcnt, &S.d_preoff, &S.d_prfge,
+                        &S.d_prccur, &S.d_prkey, &S.d_prest, &S.d_prsst, &S.d_preend, &S.d_preendm,
+                        &S.d_prmatch, &S.d_prstat};
         for (DevBuf *b : sb) b->release();
         if (S.h_rb) (void)hipHostFree(S.h_rb);
         if (S.stage_ev) {
@@ -1592,7 +1603,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     fp.clear_fused = fuse ? 1 : 0;
     if (T == 0) return PRK_OK;
     prk_context::SpanScratch &S = c->spans;
-    if (!S.h_rb) PRK_TRY(hipHostMalloc((void **)&S.h_rb, 4 * sizeof(uint32_t), hipHostMallocDefault));
+    if (!S.h_rb) PRK_TRY(hipHostMalloc((void **)&S.h_rb, 8 * sizeof(uint32_t), hipHostMallocDefault));
     const uint32_t lcap = prk_obj_walk_lcap();  // LDS list capacity of the wave walk (edges)
     // Objects in submission order (ObjDesc kinds: prk_spans.hip): kind 0
     // objects' triangles numbered 0..ntri-1 in order (FillEdgeTable runs per
@@ -1638,8 +1649,12 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
             }
         }
     }
+    std::vector<uint32_t> big_edges;  // (h_big_gl order)
     for (int mo = 0; mo < prk::MODE_COUNT; ++mo)  // the large objects, by mode (their walk groups: after the readback)
-        for (size_t i = 0; i < bigm[mo].size(); ++i) S.h_big_gl.push_back(bigm[mo][i]);
+        for (size_t i = 0; i < bigm[mo].size(); ++i) {
+            S.h_big_gl.push_back(bigm[mo][i]);
+            big_edges.push_back(bige[mo][i]);
+        }
     // edge slots (3 per triangle + the caller edges) are indexed by 31 bits
     if (3 * ntri + nk1 >= 0x7FFFFFFFull) return PRK_ERR_LIMIT;
     const uint32_t nobj = (uint32_t)S.h_objs.size(), nk0 = (uint32_t)S.h_k0obj.size();
@@ -1762,7 +1777,10 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     const uint32_t nwork = 3 * nt + (uint32_t)nk1;
     PRK_TRY(S.d_work.ensure(std::max<size_t>(nwork, 1) * 112));
     PRK_TRY(prk_obj_gather(S.d_edges.p, ord, total0p, d_edges_in, d_k1src, (uint32_t)nk1, S.d_work.p, nwork, s));
-    const size_t cls_bytes = (size_t)nbig_all * 20 + 64;  // most (4) | big (4) | off (8) | cap (4) per object
+    // per large object: most, rows, entries (12, k_obj_maxact) | big (4) |
+    // off (8) | cap (4) | the chunked walk's table (32, prk_spans.hip PrObj)
+    // and groups (4)
+    const size_t cls_bytes = (size_t)nbig_all * 64 + 64;
     if (cls_bytes > S.cls_cap) {
         if (S.h_cls) (void)hipHostFree(S.h_cls);
         S.h_cls = nullptr;
@@ -1772,12 +1790,12 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     }
     int32_t *h_most = reinterpret_cast<int32_t *>(S.h_cls);
     if (nbig_all) {
-        PRK_TRY(S.d_most.ensure((size_t)nbig_all * 4));
+        PRK_TRY(S.d_most.ensure((size_t)nbig_all * 12));
         PRK_TRY(prk_obj_maxact(&fp, d_objs, d_big, nbig_all, escan, total0p, S.d_work.p, (int32_t *)S.d_most.p, s));
-        PRK_TRY(hipMemcpyAsync(h_most, S.d_most.p, (size_t)nbig_all * 4, hipMemcpyDeviceToHost, s));
+        PRK_TRY(hipMemcpyAsync(h_most, S.d_most.p, (size_t)nbig_all * 12, hipMemcpyDeviceToHost, s));
     }
     PRK_TRY(hipMemcpyAsync(S.h_rb, oslot + nobj, 8, hipMemcpyDeviceToHost, s));
-    PRK_TRY(hipMemsetAsync(S.d_err.p, 0, 4, s));
+    PRK_TRY(hipMemsetAsync(S.d_err.p, 0, 12, s));  // (error bits, then the parallel-rows tally)
     PRK_TRY(hipStreamSynchronize(s));
     uint64_t nslot64;
     std::memcpy(&nslot64, S.h_rb, 8);
@@ -1800,9 +1818,11 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
         uint32_t lcap, start, count;
     };
     std::vector<Group> groups;
-    uint32_t *cls_big = reinterpret_cast<uint32_t *>(S.h_cls + (size_t)nbig_all * 4);
-    unsigned long long *cls_off = reinterpret_cast<unsigned long long *>(S.h_cls + ((((size_t)nbig_all * 8) + 7) & ~(size_t)7));
+    uint32_t *cls_big = reinterpret_cast<uint32_t *>(S.h_cls + (size_t)nbig_all * 12);
+    unsigned long long *cls_off = reinterpret_cast<unsigned long long *>(S.h_cls + ((((size_t)nbig_all * 16) + 7) & ~(size_t)7));
     uint32_t *cls_cap = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(cls_off) + (size_t)nbig_all * 8);
+    uint32_t *cls_pr = cls_cap + nbig_all;  // PrObj[npr] (8 words each)
+    uint32_t *cls_grp = cls_pr + 8 * (size_t)nbig_all;  // its objects grouped by (mode, LDS capacity)
     {
         static const uint32_t kCaps[] = {62, 126, 254, 510, 1022};
         uint32_t k = 0, b = 0;
@@ -1832,10 +1852,74 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
             b += (uint32_t)bigm[mo].size();
         }
     }
+    // The chunked walk (prk_spans.hip k_pr_*): the large objects walked with
+    // their lists in LDS whose rows fit its histogram (PRK_OBJ_ROWS=0: none;
+    // every object then takes the workgroup walk alone).  Objects by
+    // (mode, LDS capacity class), as the walk groups.
+    struct PrGroup {
+        int32_t mode;
+        uint32_t cap, start, count, max_chunks;
+    };
+    std::vector<PrGroup> prgroups;
+    uint32_t npr = 0, pr_rows = 0, pr_chunks = 0, pr_max_edges = 0;
+    uint64_t pr_ents = 0;
+    {
+        const char *env = std::getenv("PRK_OBJ_ROWS");
+        const bool on = !(env && env[0] == '0');
+        const uint32_t K = prk_pr_chunk_rows();
+        const int32_t *h_rows = h_most + nbig_all;
+        static const uint32_t kCapsPr[] = {62, 126, 254, 510, 1022};
+        uint32_t b = 0;
+        for (int mo = 0; on && mo < prk::MODE_COUNT; ++mo) {
+            const uint32_t b0 = b;
+            for (int ci = 0; ci < 5; ++ci) {
+                const uint32_t capc = kCapsPr[ci];
+                if (capc > lcap) continue;
+                PrGroup g{mo, capc, npr, 0, 0};
+                for (uint32_t i = 0; i < bigm[mo].size(); ++i) {
+                    const uint32_t bi = b0 + i;
+                    const int32_t most = h_most[bi], rows = h_rows[bi];
+                    if (most <= 0 || most > prk_pr_max_row_entries() || rows <= 0 || rows > prk_pr_max_rows())
+                        continue;
+                    uint32_t want = 0;  // its capacity class (the walk groups' rule)
+                    for (int cj = 0; cj < 5; ++cj)
+                        if (kCapsPr[cj] <= lcap && (uint32_t)most <= kCapsPr[cj]) {
+                            want = kCapsPr[cj];
+                            break;
+                        }
+                    if (want != capc) continue;
+                    const uint32_t nch = ((uint32_t)rows + K - 1) / K;
+                    const uint64_t ents = (uint64_t)most * nch;
+                    if (pr_ents + ents > kPrMaxEntries || npr >= 65535 || (uint64_t)pr_rows + rows + 1 > 0x7FFFFFFFull)
+                        continue;
+                    uint32_t *q = cls_pr + 8 * (size_t)npr;
+                    q[0] = S.h_big_gl[bi];
+                    q[1] = pr_rows;
+                    q[2] = (uint32_t)rows;
+                    q[3] = pr_chunks;
+                    q[4] = (uint32_t)most;
+                    q[5] = (uint32_t)pr_ents;
+                    q[6] = q[7] = 0;
+                    cls_grp[npr] = npr;
+                    pr_rows += (uint32_t)rows + 1;
+                    pr_chunks += nch;
+                    pr_ents += ents;
+                    pr_max_edges = std::max(pr_max_edges, big_edges[bi]);
+                    g.max_chunks = std::max(g.max_chunks, nch);
+                    ++g.count;
+                    ++npr;
+                }
+                if (g.count) prgroups.push_back(g);
+            }
+            b += (uint32_t)bigm[mo].size();
+        }
+    }
     const uint32_t *d_cbig = nullptr, *d_ccap = nullptr;
     const unsigned long long *d_coff = nullptr;
+    const void *d_cpr = nullptr;
+    const uint32_t *d_cgrp = nullptr;
     if (nbig_all) {
-        const size_t lo = (size_t)nbig_all * 4, hi = reinterpret_cast<char *>(cls_cap + nbig_all) - S.h_cls;
+        const size_t lo = (size_t)nbig_all * 12, hi = reinterpret_cast<char *>(cls_grp + npr) - S.h_cls;
         PRK_TRY(S.d_cls.ensure(hi));
         PRK_TRY(hipMemcpyAsync(static_cast<char *>(S.d_cls.p) + lo, S.h_cls + lo, hi - lo, hipMemcpyHostToDevice, s));
         d_cbig = reinterpret_cast<const uint32_t *>(static_cast<char *>(S.d_cls.p) + lo);
@@ -1843,7 +1927,57 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
                                                               (reinterpret_cast<char *>(cls_off) - S.h_cls));
         d_ccap = reinterpret_cast<const uint32_t *>(static_cast<char *>(S.d_cls.p) +
                                                     (reinterpret_cast<char *>(cls_cap) - S.h_cls));
+        d_cpr = static_cast<char *>(S.d_cls.p) + (reinterpret_cast<char *>(cls_pr) - S.h_cls);
+        d_cgrp = reinterpret_cast<const uint32_t *>(static_cast<char *>(S.d_cls.p) +
+                                                    (reinterpret_cast<char *>(cls_grp) - S.h_cls));
         if (pool) PRK_TRY(S.d_pool.ensure(pool * 4));
+    }
+    const uint32_t *d_prstat = nullptr;
+    if (npr) {
+        PRK_TRY(S.d_prstat.ensure((size_t)nobj * 4));
+        PRK_TRY(hipMemsetAsync(S.d_prstat.p, 0, (size_t)nobj * 4, s));
+        PRK_TRY(S.d_prrow.ensure((size_t)npr * 8));
+        PRK_TRY(S.d_prcnt.ensure((size_t)pr_rows * 4));
+        PRK_TRY(S.d_preoff.ensure((size_t)pr_rows * 4));
+        PRK_TRY(S.d_prfge.ensure((size_t)pr_rows * 4));
+        PRK_TRY(S.d_prccur.ensure((size_t)pr_chunks * 4));
+        PRK_TRY(S.d_preendm.ensure((size_t)pr_chunks * 4));
+        PRK_TRY(S.d_prmatch.ensure((size_t)pr_chunks * 4));
+        PRK_TRY(S.d_prkey.ensure(pr_ents * 16));
+        PRK_TRY(S.d_prest.ensure(pr_ents * 112));  // prk_spans.hip ObjEdge
+        PRK_TRY(S.d_prsst.ensure(pr_ents * 112));
+        PRK_TRY(S.d_preend.ensure(pr_ents * 112));
+        prk::PrWalkArgs pa{};
+        pa.objs = d_objs;
+        pa.pro = d_cpr;
+        pa.npr = npr;
+        pa.nchunks = pr_chunks;
+        pa.max_edges = pr_max_edges;
+        pa.escan = escan;
+        pa.total0p = total0p;
+        pa.work = S.d_work.p;
+        pa.prrow = S.d_prrow.p;
+        pa.cnt = (uint32_t *)S.d_prcnt.p;
+        pa.eoff = (uint32_t *)S.d_preoff.p;
+        pa.fge = (uint32_t *)S.d_prfge.p;
+        pa.ccur = (uint32_t *)S.d_prccur.p;
+        pa.key = S.d_prkey.p;
+        pa.est = S.d_prest.p;
+        pa.sst = S.d_prsst.p;
+        pa.eend = S.d_preend.p;
+        pa.eend_m = (uint32_t *)S.d_preendm.p;
+        pa.match = (uint32_t *)S.d_prmatch.p;
+        pa.prstat = (uint32_t *)S.d_prstat.p;
+        pa.soff = oslot;
+        pa.raw = S.d_raw.p;
+        pa.pos = S.d_pos.p;
+        pa.span_tri = (uint32_t *)S.d_span_tri.p;
+        pa.err = (uint32_t *)S.d_err.p;
+        PRK_TRY(prk_pr_walk_begin(&fp, &pa, s));
+        for (const PrGroup &g : prgroups)
+            PRK_TRY(prk_pr_walk_group(&fp, &pa, g.mode, g.cap, d_cgrp + g.start, g.count, g.max_chunks, s));
+        PRK_TRY(prk_pr_walk_end(&pa, s));
+        d_prstat = (const uint32_t *)S.d_prstat.p;
     }
     PRK_TRY(prk_obj_walk(&fp, d_objs, nobj, escan, total0p, S.d_work.p, oslot, S.d_recs.p,
                          scalar ? S.d_srecs.p : nullptr, S.d_pos.p, (uint32_t *)S.d_span_tri.p, d_spans_in,
@@ -1852,7 +1986,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
         PRK_TRY(prk_obj_walk_group(&fp, g.mode, g.lcap, d_objs, d_cbig + g.start, d_coff + g.start, d_ccap + g.start,
                                    g.count, (int32_t *)S.d_pool.p, escan, total0p, S.d_work.p, oslot, S.d_recs.p,
                                    scalar ? S.d_srecs.p : nullptr, S.d_raw.p, S.d_pos.p, (uint32_t *)S.d_span_tri.p,
-                                   (uint32_t *)S.d_err.p, s));
+                                   (uint32_t *)S.d_err.p, d_prstat, s));
     if (nbig_all)  // the slot walks' pairs into span records
         PRK_TRY(prk_span_finish(&fp, S.d_raw.p, nslot, S.d_recs.p, scalar ? S.d_srecs.p : nullptr, S.d_pos.p, s));
     PRK_TRY(S.d_scnt.ensure(((size_t)nslot + 1) * 4));
@@ -1863,10 +1997,15 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(temp(tb));
     PRK_TRY(prk_scan_u32(scnt, soff, nslot + 1, S.d_temp.p, &tb, s));
     PRK_TRY(hipMemcpyAsync(S.h_rb + 2, soff + nslot, 4, hipMemcpyDeviceToHost, s));
-    PRK_TRY(hipMemcpyAsync(S.h_rb + 3, S.d_err.p, 4, hipMemcpyDeviceToHost, s));
+    PRK_TRY(hipMemcpyAsync(S.h_rb + 3, S.d_err.p, 12, hipMemcpyDeviceToHost, s));
     PRK_TRY(hipStreamSynchronize(s));
     const uint32_t total = S.h_rb[2];
     if (S.h_rb[3]) return PRK_ERR_DEVICE;  // a walk outside its LDS list or span slots (never)
+    if (std::getenv("PRK_PR_DEBUG"))
+        std::fprintf(stderr, "prk: large objects %u, by rows: taken %u done %u failed %u (rows %u, entries %llu)\n",
+                     nbig_all, npr, S.h_rb[4], S.h_rb[5], pr_rows, (unsigned long long)pr_ents);
+    c->stats.objects_chunked += S.h_rb[4];
+    c->stats.objects_walked += nbig_all - S.h_rb[4];
     c->stats.triangles = T;
     c->stats.tiles = ntiles;
     c->stats.bin_entries = total;

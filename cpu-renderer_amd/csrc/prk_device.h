@@ -1031,4 +1031,25 @@ struct RowWalker {
     }
 };
 
+// The chunked walk of large objects (prk_spans.hip k_pr_*): its pass-wide
+// buffers and sizes, set by flush_spans (prk_api.hip).
+struct PrWalkArgs {
+    const void *objs;           // ObjDesc[]
+    const void *pro;            // PrObj[npr]
+    uint32_t npr;               // objects
+    uint32_t nchunks;           // their chunks
+    uint32_t max_edges;         // most edges of one object
+    const uint32_t *escan, *total0p;
+    const void *work;           // the walk's working copy (ObjEdge[])
+    void *prrow;                // PrRow[npr]
+    uint32_t *cnt, *eoff, *fge; // per row: rows + 1 per object
+    uint32_t *ccur;             // per chunk: its first row's entries
+    void *key;                  // float4 per entry (chunk j of an object: ent_off + j * most)
+    void *est, *sst, *eend;     // ObjEdge per entry: arrival order / canonical list / a walk's end list
+    uint32_t *eend_m, *match;   // per chunk
+    uint32_t *prstat;           // per object of the pass
+    const unsigned long long *soff;
+    void *raw, *pos;            // PairRaw / SpanPos per span slot
+    uint32_t *span_tri, *err;
+};
 }  // namespace prk

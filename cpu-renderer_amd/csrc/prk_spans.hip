@@ -68,6 +68,9 @@ struct ObjDesc {
                         // bit 31 (kObjWave): walked by one wave (k_obj_walk_wave)
 };
 constexpr uint32_t kObjWave = 0x80000000u;
+// An object's status in the parallel-rows walk (k_pr_*): 0 not taken,
+// walked by rows, or failed its check (the workgroup walk takes it).
+constexpr uint32_t kPrDone = 1u, kPrFailed = 2u;
 
 // Caller edges (prk_edge = edge_info without Next, prk.h) and spans (prk_span).
 struct EdgeIn {
@@ -1834,21 +1837,26 @@ __device__ void walk_object_block(const FrameParams &fp, const ObjDesc &od, cons
 // The host reads them back with the span slot total and launches each
 // object's walk with a workgroup just large enough (slot_threads).
 constexpr int32_t kMaxactRows = 16000;  // (the histogram is static LDS: < 64 KiB)
+// (most[nbig + b]: the rows its walk visits, MaxY - FirstRow (0 when none,
+// INT32_MAX past the histogram); most[2 * nbig + b]: its list entries over
+// them, the sum over its edges of their rows [YMin, min(YMax, MaxY)),
+// saturated at INT32_MAX: the sizes of the parallel-rows walk, k_pr_*.)
 __global__ void __launch_bounds__(kSlotMaxThreads) k_obj_maxact(FrameParams fp, const ObjDesc *__restrict__ objs,
-                                                               const uint32_t *__restrict__ big,
+                                                               const uint32_t *__restrict__ big, uint32_t nbig,
                                                                const uint32_t *__restrict__ escan,
                                                                const uint32_t *__restrict__ total0p,
                                                                const ObjEdge *__restrict__ work,
                                                                int32_t *__restrict__ most) {
     __shared__ int32_t h[kMaxactRows + 1];
     __shared__ BlockRed R;
+    __shared__ unsigned long long ents;
     const ObjDesc od = objs[big[blockIdx.x]];
     uint32_t e0, n;
     obj_range(od, escan, *total0p, e0, n);
     const ObjEdge *E = work + e0;
     const int tid = threadIdx.x, NT = blockDim.x;
     if (n == 0) {
-        if (tid == 0) most[blockIdx.x] = 0;
+        if (tid == 0) most[blockIdx.x] = most[nbig + blockIdx.x] = most[2 * nbig + blockIdx.x] = 0;
         return;
     }
     int32_t mr = INT32_MIN;
@@ -1856,19 +1864,30 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_obj_maxact(FrameParams fp, 
     const int32_t MaxY = min(min(blk_max(R, mr), fp.H), fp.row1), FirstRow = E[0].YMin;
     const int64_t rows = (int64_t)MaxY - FirstRow;
     if (rows <= 0 || rows + 1 > kMaxactRows) {
-        if (tid == 0) most[blockIdx.x] = rows <= 0 ? 0 : INT32_MAX;
+        if (tid == 0) {
+            most[blockIdx.x] = most[nbig + blockIdx.x] = rows <= 0 ? 0 : INT32_MAX;
+            most[2 * nbig + blockIdx.x] = 0;
+        }
         return;
     }
     const int Rn = (int)rows;
     for (int q = tid; q <= Rn; q += NT) h[q] = 0;
+    if (tid == 0) ents = 0;
     __syncthreads();
+    unsigned long long mine = 0;
     for (uint32_t i = tid; i < n; i += NT) {  // an edge is listed on rows [YMin, max(YMin, YMax)]
         const int32_t y0 = E[i].YMin, y1 = E[i].YMax;
         if (y0 >= MaxY) continue;  // never inserted
         atomicAdd(&h[y0 - FirstRow], 1);
         atomicAdd(&h[min(max(y0, y1), MaxY - 1) - FirstRow + 1], -1);
+        mine += (unsigned long long)max(0, min(y1, MaxY) - y0);
     }
+    if (mine) atomicAdd(&ents, mine);
     __syncthreads();
+    if (tid == 0) {
+        most[nbig + blockIdx.x] = Rn;
+        most[2 * nbig + blockIdx.x] = (int32_t)min(ents, (unsigned long long)INT32_MAX);
+    }
     int32_t carry = 0, best = 0;
     for (int b0 = 0; b0 < Rn; b0 += NT) {
         const int q = b0 + tid;
@@ -1897,10 +1916,12 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_obj_walk_wave(FrameParams f
                                                       const unsigned long long *__restrict__ soff,
                                                       SpanRecG *__restrict__ recs, ScSpanRecG *__restrict__ srecs,
                                                       PairRaw *__restrict__ raw, SpanPos *__restrict__ pos,
-                                                      uint32_t *__restrict__ span_tri, uint32_t *__restrict__ err) {
+                                                      uint32_t *__restrict__ span_tri, uint32_t *__restrict__ err,
+                                                      const uint32_t *__restrict__ prstat) {
     extern __shared__ int32_t lds_list[];
     __shared__ BlockRed R;
     const uint32_t o = big[blockIdx.x];
+    if (prstat && prstat[o] == kPrDone) return;  // walked by rows (k_pr_*)
     const ObjDesc od = objs[o];
     const DrawRec &d = fp.draws[od.draw];
     const uint32_t base = (uint32_t)soff[o], bound = (uint32_t)(soff[o + 1] - soff[o]);
@@ -1925,6 +1946,523 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_obj_walk_wave(FrameParams f
     SlotLds S;
     S.carve(lds_list, lcap, blockDim.x);
     walk_object_block<M>(fp, od, E, n, MaxY, base, bound, S, R, lcap, raw, pos, span_tri, err);
+}
+
+// ---------------------------------------------------------------------------
+// The chunked walk of large objects (objects of kObjWaveTris triangles or
+// more whose rows and lists fit: k_obj_maxact's sizes, host-checked).
+//
+// The walk is serial in rows: the list at row r is a function of the list at
+// r - 1.  But a row's list is usually just its active edges sorted by the
+// insertion key (X, Gradient, Left), ties in MergeSort order -- the canonical
+// list C(r) (a batch inserted into an empty list is exactly that; a mesh's
+// edges seldom cross).  So the object's rows are cut into chunks of kPrChunk
+// rows, and every chunk is walked at once, speculatively, from the canonical
+// list of its first row, by the workgroup walk's own list operations
+// (walk_chunk = walk_object_block from a given list, for a given row range).
+// Each chunk then compares the list its walk reaches at the next chunk's
+// first row with that row's canonical list.  The first chunk starts from the
+// true list; a chunk whose predecessor reached its canonical start list
+// started from the true list too; any other chunk is walked again, in order,
+// from its predecessor's true end list (k_pr_fix: one workgroup per object,
+// chunk after chunk, walking only those).  The spans of a chunk go to the
+// slots its rows take in the sequential walk -- every row pairs all its
+// entries (objects with an odd row are left to k_obj_walk_wave), so a row's
+// pairs are its entries / 2, whatever their order -- in the same order.
+//   k_pr_hist   workgroup per object: its rows' entry counts and their scan
+//               (the span slots), the first sorted edge of every row
+//   k_pr_fill   thread per edge: stepped row by row as the walk steps it
+//               (obj_step), its state and key at every chunk's first row
+//   k_pr_start  workgroup per chunk: the canonical list of its first row
+//               (rank sort), as edge states
+//   k_pr_chunk  workgroup per chunk: the speculative walk
+//   k_pr_fix    workgroup per object: the chunks whose start was not the
+//               true list, walked again in order
+// ---------------------------------------------------------------------------
+#ifndef PRK_PR_CHUNK
+#define PRK_PR_CHUNK 16
+#endif
+constexpr int32_t kPrChunk = PRK_PR_CHUNK;  // rows per chunk
+constexpr int32_t kPrMaxM = 1022;           // most entries of a list (the workgroup walk's largest LDS list)
+struct PrObj {                              // per object of the walk (host: flush_spans)
+    uint32_t o;                             // object index
+    uint32_t row_off;                       // its first row in the pass's row arrays (rows + 1 each)
+    uint32_t rows;                          // MaxY - FirstRow (k_obj_maxact)
+    uint32_t chunk_off;                     // its first chunk in the pass's chunk arrays
+    uint32_t most;                          // k_obj_maxact's most entries (the list stride per chunk)
+    uint32_t ent_off;                       // its first list entry: chunk j's lists at ent_off + j * most
+    uint32_t pad0, pad1;
+};
+struct PrRow {                              // per object, set by k_pr_hist
+    int32_t first_row, max_y;
+};
+__device__ __forceinline__ uint32_t pr_chunks(const PrObj &P) { return (P.rows + kPrChunk - 1) / kPrChunk; }
+__device__ __forceinline__ bool pr_key_lt(float ax, float ag, int32_t al, uint32_t ai, float bx, float bg, int32_t bl,
+                                          uint32_t bi) {
+    return ax < bx || (ax == bx && (ag < bg || (ag == bg && (al < bl || (al == bl && ai < bi)))));
+}
+
+// cnt[row_off + j]: entries of row first_row + j; eoff: their exclusive scan
+// (row + 1 values: eoff[rows] = the total); fge[row_off + j]: the first sorted
+// edge with YMin >= first_row + j (j <= rows).
+__global__ void __launch_bounds__(kSlotMaxThreads) k_pr_hist(FrameParams fp, const ObjDesc *__restrict__ objs,
+                                                            const PrObj *__restrict__ pro,
+                                                            const uint32_t *__restrict__ escan,
+                                                            const uint32_t *__restrict__ total0p,
+                                                            const ObjEdge *__restrict__ work, PrRow *__restrict__ prrow,
+                                                            uint32_t *__restrict__ cnt, uint32_t *__restrict__ eoff,
+                                                            uint32_t *__restrict__ fge, uint32_t *__restrict__ prstat) {
+    __shared__ int32_t h[kMaxactRows + 1];
+    __shared__ BlockRed R;
+    const PrObj P = pro[blockIdx.x];
+    const ObjDesc od = objs[P.o];
+    uint32_t e0, n;
+    obj_range(od, escan, *total0p, e0, n);
+    const ObjEdge *E = work + e0;
+    const int tid = threadIdx.x, NT = blockDim.x;
+    int32_t mr = INT32_MIN;
+    for (uint32_t i = tid; i < n; i += NT) mr = max(mr, E[i].YMax);
+    const int32_t MaxY = min(min(blk_max(R, mr), fp.H), fp.row1), FirstRow = n ? E[0].YMin : 0;
+    const int Rn = (int)P.rows;
+    if (n == 0 || (int64_t)MaxY - FirstRow != (int64_t)Rn || Rn + 1 > kMaxactRows) {  // (never: k_obj_maxact sized it)
+        if (tid == 0) prstat[P.o] = kPrFailed;
+        return;
+    }
+    for (int q = tid; q <= Rn; q += NT) h[q] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += NT) {  // active on rows [YMin, min(YMax, MaxY))
+        const int32_t y0 = E[i].YMin, y1 = min(E[i].YMax, MaxY);
+        // the first edge of rows (YMin[i - 1], YMin[i]] (sorted by YMin)
+        const int32_t lo = i ? E[i - 1].YMin : FirstRow - 1, hi = min(y0, MaxY);
+        for (int32_t r = max(lo + 1, FirstRow); r <= hi; ++r) fge[P.row_off + (uint32_t)(r - FirstRow)] = i;
+        if (i + 1 == n)
+            for (int32_t r = max(y0 + 1, FirstRow); r <= MaxY; ++r) fge[P.row_off + (uint32_t)(r - FirstRow)] = n;
+        if (y0 >= y1) continue;
+        atomicAdd(&h[y0 - FirstRow], 1);
+        atomicAdd(&h[y1 - FirstRow], -1);
+    }
+    __syncthreads();
+    int32_t carry = 0, carry_e = 0, odd = 0;
+    for (int b0 = 0; b0 < Rn; b0 += NT) {
+        const int q = b0 + tid;
+        const int32_t v = q < Rn ? h[q] : 0;
+        int32_t tot;
+        const int32_t m = carry + blk_excl_sum(R, v, tot) + v;  // entries of row q
+        const int32_t mm = q < Rn ? m : 0;
+        int32_t tot_e;
+        const int32_t ex = blk_excl_sum(R, mm, tot_e);
+        if (q < Rn) {
+            cnt[P.row_off + q] = (uint32_t)m;
+            eoff[P.row_off + q] = (uint32_t)(carry_e + ex);
+            odd |= m & 1;
+        }
+        carry += tot;
+        carry_e += tot_e;
+    }
+    odd = blk_max(R, odd);
+    if (tid == 0) {
+        eoff[P.row_off + Rn] = (uint32_t)carry_e;
+        prrow[blockIdx.x] = PrRow{FirstRow, MaxY};
+        prstat[P.o] = odd ? kPrFailed : kPrDone;  // every row pairs all its entries
+    }
+}
+
+// Each edge's state at its chunks' first rows (stepped every row: every
+// entry is paired every row, k_pr_hist), into the chunk's entry block at
+// ent_off + j * most, in arrival order (k_pr_start sorts them).
+template <int M>
+__device__ __forceinline__ void pr_fill_edge(ObjEdge e, int32_t r1, uint32_t idx, const PrObj &P, int32_t first_row,
+                                             uint32_t *__restrict__ ccur, float4 *__restrict__ key,
+                                             ObjEdge *__restrict__ est) {
+    for (int32_t r = e.YMin; r < r1; ++r) {
+        const int32_t j = r - first_row;
+        if (j % kPrChunk == 0) {
+            const uint32_t c = (uint32_t)(j / kPrChunk);
+            const uint32_t at = atomicAdd(&ccur[P.chunk_off + c], 1u);
+            if (at < P.most) {  // (always: most bounds every row's list)
+                const uint32_t g = P.ent_off + c * P.most + at;
+                key[g] = make_float4(e.X, e.G, __int_as_float(e.Left), __uint_as_float(idx));
+                ObjEdge s = e;
+                s.Next = (int32_t)idx;
+                est[g] = s;
+            }
+        }
+        obj_step<M>(e);  // 3811-3829
+    }
+}
+__global__ void k_pr_fill(FrameParams fp, const ObjDesc *__restrict__ objs, const PrObj *__restrict__ pro,
+                          const PrRow *__restrict__ prrow, const uint32_t *__restrict__ escan,
+                          const uint32_t *__restrict__ total0p, const ObjEdge *__restrict__ work,
+                          uint32_t *__restrict__ ccur, float4 *__restrict__ key, ObjEdge *__restrict__ est,
+                          const uint32_t *__restrict__ prstat) {
+    const PrObj P = pro[blockIdx.y];
+    if (prstat[P.o] != kPrDone) return;
+    const ObjDesc od = objs[P.o];
+    uint32_t e0, n;
+    obj_range(od, escan, *total0p, e0, n);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const PrRow pr = prrow[blockIdx.y];
+    const ObjEdge e = work[e0 + i];
+    const int32_t r1 = min(e.YMax, pr.max_y);
+    if (e.YMin >= r1) return;
+    switch (fp.draws[od.draw].mode) {
+#define PRK_PR_FILL(MM)                                                                  \
+    case MM:                                                                             \
+        pr_fill_edge<MM>(e, r1, i, P, pr.first_row, ccur, key, est);                     \
+        break;
+        PRK_PR_FILL(MODE_AVX)
+        PRK_PR_FILL(MODE_SC_GOURAUD)
+        PRK_PR_FILL(MODE_SC_GOURAUD_TEX)
+        PRK_PR_FILL(MODE_SC_PHONG)
+        PRK_PR_FILL(MODE_SC_PHONG_TEX)
+#undef PRK_PR_FILL
+        default: break;
+    }
+}
+
+// The object of chunk c of the pass (the last with chunk_off <= c).
+__device__ __forceinline__ uint32_t pr_obj_of_chunk(const PrObj *__restrict__ pro, uint32_t npr, uint32_t c) {
+    uint32_t lo = 0, hi = npr;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pro[mid].chunk_off <= c) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// The canonical list of every chunk's first row: its entries ranked by
+// (X, Gradient, Left, MergeSort index), their states (est, arrival order)
+// into sst in list order.
+constexpr int kPrStartThreads = 256;
+__global__ void __launch_bounds__(kPrStartThreads) k_pr_start(const PrObj *__restrict__ pro, uint32_t npr,
+                                                              const uint32_t *__restrict__ ccur,
+                                                              const float4 *__restrict__ key,
+                                                              const ObjEdge *__restrict__ est,
+                                                              ObjEdge *__restrict__ sst, uint32_t *__restrict__ prstat) {
+    __shared__ float sx[kPrMaxM], sg[kPrMaxM];
+    __shared__ int32_t sl[kPrMaxM];
+    __shared__ uint32_t si[kPrMaxM];
+    __shared__ uint32_t st0;
+    const uint32_t c = blockIdx.x;
+    const PrObj P = pro[pr_obj_of_chunk(pro, npr, c)];
+    const int tid = threadIdx.x;
+    if (tid == 0) st0 = prstat[P.o];
+    __syncthreads();
+    if (st0 != kPrDone) return;
+    const uint32_t j = c - P.chunk_off;
+    const int m = (int)ccur[c];
+    if (m > (int)P.most || m > kPrMaxM) {  // (never: most bounds every row's list)
+        if (tid == 0) atomicMax(&prstat[P.o], kPrFailed);
+        return;
+    }
+    const uint32_t g0 = P.ent_off + j * P.most;
+    bool bad = false;
+    for (int q = tid; q < m; q += kPrStartThreads) {
+        const float4 k = key[g0 + q];
+        sx[q] = k.x;
+        sg[q] = k.y;
+        sl[q] = __float_as_int(k.z);
+        si[q] = __float_as_uint(k.w);
+        bad |= k.x != k.x || k.y != k.y;  // a NaN key: no canonical order (the walk takes the object)
+    }
+    __syncthreads();
+    for (int q = tid; q < m; q += kPrStartThreads) {
+        const float x = sx[q], g = sg[q];
+        const int32_t l = sl[q];
+        const uint32_t i = si[q];
+        int rank = 0;
+        for (int p = 0; p < m; ++p) rank += pr_key_lt(sx[p], sg[p], sl[p], si[p], x, g, l, i) ? 1 : 0;
+        sst[g0 + rank] = est[g0 + q];
+    }
+    if (__any(bad) && (tid & 63) == 0) atomicMax(&prstat[P.o], kPrFailed);
+}
+
+// walk_object_block over the rows [r0, r1) of an object, from the list
+// start[0, m0) at row r0 (states at r0, their sorted edge index in Next; the
+// row's insertion and expiry done), its spans from slot base + emitted0 on.
+// At r1 < MaxY: the list after r1's insertion and expiry goes to end[] /
+// *end_m, and the return value says whether it is canon[0, mc) (edge by
+// edge).  Every thread returns the same.
+template <int M>
+__device__ bool walk_chunk(const FrameParams &fp, const ObjDesc &od, const ObjEdge *__restrict__ E, uint32_t n,
+                           int32_t MaxY, uint32_t base, uint32_t bound, const SlotLds &S, BlockRed &R, uint32_t cap,
+                           int32_t r0, int32_t r1, uint32_t ins0, const ObjEdge *__restrict__ start, int m0,
+                           uint32_t emitted0, const ObjEdge *__restrict__ canon, int mc, ObjEdge *__restrict__ end,
+                           uint32_t *__restrict__ end_m, PairRaw *__restrict__ raw, SpanPos *__restrict__ pos,
+                           uint32_t *__restrict__ span_tri, uint32_t *__restrict__ err) {
+    constexpr bool kScalar = M != MODE_AVX;
+    const int tid = threadIdx.x;
+    const uint32_t NT = blockDim.x;
+    const int32_t RowLo = kScalar ? fp.row0 - 1 : fp.row0;
+    // the start list in slots [0, m0), the free slots above
+    for (int q = tid; q < m0; q += (int)NT) {
+        S.st[q] = start[q];
+        S.idx[q] = q;
+    }
+    for (uint32_t q = tid; q + m0 < cap; q += NT) S.fs[q] = (int32_t)(q + m0);
+    int top = (int)cap - m0;
+    int m = m0;
+    uint32_t ins = ins0;  // the first sorted edge with YMin > r0
+    uint32_t wb = ins;
+    PRK_WIN(wa);
+    PRK_WIN_LOAD(wa, E, wb + (uint32_t)tid, n);
+    PRK_WIN_WAIT();
+    PRK_WIN_LAUNDER(wa);
+    uint32_t emitted = emitted0;
+    __syncthreads();
+    for (int32_t Row = r0;; ++Row) {
+        if (Row != r0) {
+            if (Row >= MaxY) break;  // (the last chunk: no list after it)
+            // insertion (3654-3713), as walk_object_block
+            for (;;) {
+                if (ins == wb + NT) {
+                    wb += NT;
+                    PRK_WIN_LOAD(wa, E, wb + tid, n);
+                    PRK_WIN_WAIT();
+                    PRK_WIN_LAUNDER(wa);
+                }
+                const float wx = wa0.x, wg = wa0.y;
+                const int32_t wymin = __float_as_int(wa4.x), wl = __float_as_int(wa4.z);
+                const int rel = tid - (int)(ins - wb);
+                const bool eqr = rel >= 0 && wymin == Row;
+                int32_t lt, k, nanc;
+                blk_sum3(R, (rel >= 0 && wymin < Row) ? 1 : 0, eqr ? 1 : 0, (eqr && (wx != wx || wg != wg)) ? 1 : 0,
+                         lt, k, nanc);
+                if (lt) {
+                    ins += (uint32_t)lt;
+                    continue;
+                }
+                if (k == 0) break;
+                if (k > top) {  // (never: cap >= the most listed edges)
+                    if (tid == 0) atomicOr(err, 1u);
+                    return false;
+                }
+                if (rel >= 0 && rel < k) {
+                    const int32_t slot = S.fs[top - 1 - rel];
+                    PRK_WIN_STORE(&S.st[slot], wa);
+                    S.st[slot].Next = (int32_t)(ins + (uint32_t)rel);  // (its sorted index)
+                    S.nkx[rel] = wx;
+                    S.nkg[rel] = wg;
+                    S.nkl[rel] = wl;
+                    S.nks[rel] = slot;
+                }
+                top -= k;
+                __syncthreads();
+                if (k <= 2 || nanc) {
+                    for (int t = 0; t < k; ++t)
+                        insert_one_b(S, R, m, LKey{S.nkx[t], S.nkg[t], S.nkl[t]}, S.nks[t]);
+                } else {
+                    insert_batch_b(S, R, m, k);
+                }
+                ins += (uint32_t)k;
+                if (ins < wb + NT) break;
+            }
+            {  // expiry 3715-3749
+                int32_t e = 0;
+                bool keep = false;
+                if (tid < m) {
+                    e = S.idx[tid];
+                    keep = !(S.st[e].YMax <= Row);
+                }
+                const bool gone = tid < m && !keep;
+                int32_t kp, gp, kt, gt;
+                blk_excl_sum2(R, keep ? 1 : 0, gone ? 1 : 0, kp, gp, kt, gt);
+                if (keep) S.idx[kp] = e;
+                if (gone) S.fs[top + gp] = e;
+                m = kt;
+                top += gt;
+                __syncthreads();
+            }
+        }
+        if (Row >= r1) break;
+        if (m == 0) {  // nothing happens on the rows before the next insertion (or r1): go there
+            const int32_t nx = ins < n ? E[ins].YMin : INT32_MAX;
+            Row = max(Row, min(nx, r1) - 1);
+            continue;
+        }
+        const int P = m / 2;  // pairing 3751-3869, as walk_object_block
+        const bool valid = tid < P;
+        const bool emit = Row >= RowLo;
+        int32_t i0 = 0, i1 = 0;
+        float x0 = 0.0f, x1 = 0.0f;
+        if (valid) {
+            i0 = S.idx[2 * tid];
+            i1 = S.idx[2 * tid + 1];
+            const uint32_t j = emitted + (uint32_t)tid;
+            const bool w = emit && j < bound;
+            if (emit && j >= bound) atomicOr(err, 2u);
+            const uint32_t at = base + j;
+            ObjEdge a = S.st[i0];
+            if (w) {
+                raw[at].l0 = make_float4(a.X, a.Z, a.W, a.U);
+                raw[at].l1 = make_float4(a.V, a.N0, a.N1, a.N2);
+                raw[at].l2 = make_float4(a.C0, a.C1, a.C2, a.C3);
+            }
+            obj_step<M>(a);
+            S.st[i0] = a;
+            x0 = a.X;
+            ObjEdge b = S.st[i1];
+            if (w) {
+                raw[at].r0 = make_float4(b.X, b.Z, b.W, b.U);
+                raw[at].r1 = make_float4(b.V, b.N0, b.N1, b.N2);
+                raw[at].r2 = make_float4(b.C0, b.C1, b.C2, b.C3);
+                pos[at] = SpanPos{Row, (int32_t)od.draw, 0, SPAN_RAW};
+                span_tri[at] = od.g0;
+            }
+            obj_step<M>(b);
+            S.st[i1] = b;
+            x1 = b.X;
+            if (x0 > x1) {
+                const int32_t t = i0; i0 = i1; i1 = t;
+                const float f = x0; x0 = x1; x1 = f;
+            }
+            S.nb[tid] = i0;
+            S.bk[tid] = __float_as_int(x0);
+            S.aux[tid] = i1;
+            S.bk2[tid] = __float_as_int(x1);
+        }
+        __syncthreads();
+        if (valid) {
+            const bool sw = tid >= 1 && __int_as_float(S.bk2[tid - 1]) > x0;
+            const bool swn = tid + 1 < P && x1 > __int_as_float(S.bk[tid + 1]);
+            const int32_t nf = sw ? S.aux[tid - 1] : i0, ns = swn ? S.nb[tid + 1] : i1;
+            i0 = nf;
+            i1 = ns;
+        }
+        __syncthreads();
+        if (valid) {
+            S.idx[2 * tid] = i0;
+            S.idx[2 * tid + 1] = i1;
+        }
+        if (emit) emitted += (uint32_t)P;
+        __syncthreads();
+    }
+    if (r1 >= MaxY) return true;
+    // the list at r1: out, and against the canonical one
+    bool same = m == mc;
+    for (int q = tid; q < m; q += (int)NT) {
+        const ObjEdge &e = S.st[S.idx[q]];
+        end[q] = e;
+        if (q < mc) same = same && e.Next == canon[q].Next;
+    }
+    if (tid == 0) *end_m = (uint32_t)m;
+    return blk_max(R, same ? 0 : 1) == 0;
+}
+
+// Chunk c of the objects of one mode (pro[pi], pi in group [0, ngroup)):
+// grid (chunks of the group's longest object, ngroup).
+template <int M>
+__global__ void __launch_bounds__(kSlotMaxThreads) k_pr_chunk(FrameParams fp, const ObjDesc *__restrict__ objs,
+                                                            const PrObj *__restrict__ pro, const uint32_t *__restrict__ grp,
+                                                            uint32_t cap, const PrRow *__restrict__ prrow,
+                                                            const uint32_t *__restrict__ cnt,
+                                                            const uint32_t *__restrict__ eoff,
+                                                            const uint32_t *__restrict__ fge,
+                                                            const uint32_t *__restrict__ escan,
+                                                            const uint32_t *__restrict__ total0p,
+                                                            const ObjEdge *__restrict__ work,
+                                                            const unsigned long long *__restrict__ soff,
+                                                            const ObjEdge *__restrict__ sst, ObjEdge *__restrict__ eend,
+                                                            uint32_t *__restrict__ eend_m, uint32_t *__restrict__ match,
+                                                            const uint32_t *__restrict__ prstat, PairRaw *__restrict__ raw,
+                                                            SpanPos *__restrict__ pos, uint32_t *__restrict__ span_tri,
+                                                            uint32_t *__restrict__ err) {
+    extern __shared__ int32_t lds_list[];
+    __shared__ BlockRed R;
+    const uint32_t pi = grp[blockIdx.y];
+    const PrObj P = pro[pi];
+    const uint32_t j = blockIdx.x;
+    if (j >= pr_chunks(P) || prstat[P.o] != kPrDone) return;  // (prstat is final here: k_pr_start ran)
+    const ObjDesc od = objs[P.o];
+    uint32_t e0, n;
+    obj_range(od, escan, *total0p, e0, n);
+    const ObjEdge *E = work + e0;
+    const PrRow pr = prrow[pi];
+    const int32_t r0 = pr.first_row + (int32_t)(j * kPrChunk), r1 = min(r0 + kPrChunk, pr.max_y);
+    const uint32_t jr0 = j * kPrChunk, jr1 = (uint32_t)(r1 - pr.first_row);
+    const int32_t RowLo = fp.draws[od.draw].mode != MODE_AVX ? fp.row0 - 1 : fp.row0;
+    const uint32_t jlo = (uint32_t)min(max(0, RowLo - pr.first_row), (int32_t)P.rows);
+    const uint32_t emitted0 = (eoff[P.row_off + max(jr0, jlo)] - eoff[P.row_off + jlo]) / 2;
+    const uint32_t base = (uint32_t)soff[P.o], bound = (uint32_t)(soff[P.o + 1] - soff[P.o]);
+    SlotLds S;
+    S.carve(lds_list, cap, blockDim.x);
+    const uint32_t c = P.chunk_off + j;
+    const uint32_t g0 = P.ent_off + j * P.most, g1 = g0 + P.most;
+    const bool last = r1 >= pr.max_y;
+    const bool same = walk_chunk<M>(fp, od, E, n, pr.max_y, base, bound, S, R, cap, r0, r1,
+                                    fge[P.row_off + jr0 + 1], sst + g0, (int)cnt[P.row_off + jr0], emitted0,
+                                    last ? nullptr : sst + g1, last ? 0 : (int)cnt[P.row_off + jr1],
+                                    last ? nullptr : eend + g1, eend_m + c, raw, pos, span_tri, err);
+    if (threadIdx.x == 0) match[c] = same ? 1u : 0u;
+}
+
+// Per object of the group: the chunks whose start list was not the true one,
+// walked again in order from their predecessor's true end list.
+template <int M>
+__global__ void __launch_bounds__(kSlotMaxThreads) k_pr_fix(FrameParams fp, const ObjDesc *__restrict__ objs,
+                                                          const PrObj *__restrict__ pro, const uint32_t *__restrict__ grp,
+                                                          uint32_t cap, const PrRow *__restrict__ prrow,
+                                                          const uint32_t *__restrict__ cnt,
+                                                          const uint32_t *__restrict__ eoff,
+                                                          const uint32_t *__restrict__ fge,
+                                                          const uint32_t *__restrict__ escan,
+                                                          const uint32_t *__restrict__ total0p,
+                                                          const ObjEdge *__restrict__ work,
+                                                          const unsigned long long *__restrict__ soff,
+                                                          const ObjEdge *__restrict__ sst, ObjEdge *__restrict__ eend,
+                                                          uint32_t *__restrict__ eend_m, uint32_t *__restrict__ match,
+                                                          const uint32_t *__restrict__ prstat,
+                                                          PairRaw *__restrict__ raw, SpanPos *__restrict__ pos,
+                                                          uint32_t *__restrict__ span_tri, uint32_t *__restrict__ err) {
+    extern __shared__ int32_t lds_list[];
+    __shared__ BlockRed R;
+    const uint32_t pi = grp[blockIdx.x];
+    const PrObj P = pro[pi];
+    if (prstat[P.o] != kPrDone) return;
+    const ObjDesc od = objs[P.o];
+    uint32_t e0, n;
+    obj_range(od, escan, *total0p, e0, n);
+    const ObjEdge *E = work + e0;
+    const PrRow pr = prrow[pi];
+    const int32_t RowLo = fp.draws[od.draw].mode != MODE_AVX ? fp.row0 - 1 : fp.row0;
+    const uint32_t jlo = (uint32_t)min(max(0, RowLo - pr.first_row), (int32_t)P.rows);
+    const uint32_t base = (uint32_t)soff[P.o], bound = (uint32_t)(soff[P.o + 1] - soff[P.o]);
+    SlotLds S;
+    S.carve(lds_list, cap, blockDim.x);
+    const uint32_t nch = pr_chunks(P);
+    bool prev_true = true;  // chunk j - 1 ended on its next chunk's canonical start (chunk 0: the true start)
+    for (uint32_t j = 0; j < nch; ++j) {
+        const uint32_t c = P.chunk_off + j;
+        if (prev_true) {  // its speculative walk started from the true list: keep it
+            prev_true = match[c] != 0;
+            continue;
+        }
+        // walk it again from the true list: chunk j - 1's end (eend at its entry block)
+        const int32_t r0 = pr.first_row + (int32_t)(j * kPrChunk), r1 = min(r0 + kPrChunk, pr.max_y);
+        const uint32_t jr0 = j * kPrChunk, jr1 = (uint32_t)(r1 - pr.first_row);
+        const uint32_t emitted0 = (eoff[P.row_off + max(jr0, jlo)] - eoff[P.row_off + jlo]) / 2;
+        const uint32_t g0 = P.ent_off + j * P.most, g1 = g0 + P.most;
+        const bool last = r1 >= pr.max_y;
+        __syncthreads();  // (the previous walk's LDS and eend writes)
+        prev_true = walk_chunk<M>(fp, od, E, n, pr.max_y, base, bound, S, R, cap, r0, r1, fge[P.row_off + jr0 + 1],
+                                  eend + g0, (int)eend_m[c - 1], emitted0, last ? nullptr : sst + g1,
+                                  last ? 0 : (int)cnt[P.row_off + jr1], last ? nullptr : eend + g1, eend_m + c, raw,
+                                  pos, span_tri, err);
+    }
+}
+
+// The walk's outcome: err[1] += objects done, err[2] += objects failed.
+__global__ void k_pr_tally(const PrObj *__restrict__ pro, uint32_t npr, const uint32_t *__restrict__ prstat,
+                           uint32_t *__restrict__ err) {
+    uint32_t done = 0, failed = 0;
+    for (uint32_t i = threadIdx.x; i < npr; i += blockDim.x) {
+        const uint32_t st = prstat[pro[i].o];
+        done += st == kPrDone;
+        failed += st == kPrFailed;
+    }
+    if (done) atomicAdd(&err[1], done);
+    if (failed) atomicAdd(&err[2], failed);
 }
 
 // The tiles of a span: those of its row its [minx, min(maxx, W)) crosses and,
@@ -2067,9 +2605,22 @@ uint32_t prk_obj_walk_lcap(void) {
                 reinterpret_cast<const void *>(&prk::k_obj_walk_wave<prk::MODE_SC_GOURAUD_TEX>),
                 reinterpret_cast<const void *>(&prk::k_obj_walk_wave<prk::MODE_SC_PHONG>),
                 reinterpret_cast<const void *>(&prk::k_obj_walk_wave<prk::MODE_SC_PHONG_TEX>)};
+            const void *fc[2 * prk::MODE_COUNT] = {  // (the chunked walk's kernels: the same slot lists)
+                reinterpret_cast<const void *>(&prk::k_pr_chunk<prk::MODE_AVX>),
+                reinterpret_cast<const void *>(&prk::k_pr_chunk<prk::MODE_SC_GOURAUD>),
+                reinterpret_cast<const void *>(&prk::k_pr_chunk<prk::MODE_SC_GOURAUD_TEX>),
+                reinterpret_cast<const void *>(&prk::k_pr_chunk<prk::MODE_SC_PHONG>),
+                reinterpret_cast<const void *>(&prk::k_pr_chunk<prk::MODE_SC_PHONG_TEX>),
+                reinterpret_cast<const void *>(&prk::k_pr_fix<prk::MODE_AVX>),
+                reinterpret_cast<const void *>(&prk::k_pr_fix<prk::MODE_SC_GOURAUD>),
+                reinterpret_cast<const void *>(&prk::k_pr_fix<prk::MODE_SC_GOURAUD_TEX>),
+                reinterpret_cast<const void *>(&prk::k_pr_fix<prk::MODE_SC_PHONG>),
+                reinterpret_cast<const void *>(&prk::k_pr_fix<prk::MODE_SC_PHONG_TEX>)};
             bool ok = true;
             for (int mo = 0; mo < prk::MODE_COUNT && ok; ++mo)
                 ok = hipFuncSetAttribute(fn[mo], hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) == hipSuccess;
+            for (int q = 0; q < 2 * prk::MODE_COUNT && ok; ++q)
+                ok = hipFuncSetAttribute(fc[q], hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) == hipSuccess;
             if (ok) {
                 c = (int)k + 1;
                 break;
@@ -2100,12 +2651,13 @@ hipError_t prk_obj_walk(const prk::FrameParams *fp, const void *objs, uint32_t n
 }
 uint32_t prk_obj_link_cap(void) { return (uint32_t)prk::kLinkCap; }
 // ... the most active entries of the large ones (big[0, nbig)) ...
+// (most: 3 * nbig values, see k_obj_maxact)
 hipError_t prk_obj_maxact(const prk::FrameParams *fp, const void *objs, const uint32_t *big, uint32_t nbig,
                           const uint32_t *escan, const uint32_t *total0p, const void *work, int32_t *most,
                           hipStream_t s) {
     if (nbig == 0) return hipSuccess;
     hipLaunchKernelGGL(prk::k_obj_maxact, dim3(nbig), dim3(prk::kSlotMaxThreads), 0, s, *fp,
-                       reinterpret_cast<const prk::ObjDesc *>(objs), big, escan, total0p,
+                       reinterpret_cast<const prk::ObjDesc *>(objs), big, nbig, escan, total0p,
                        reinterpret_cast<const prk::ObjEdge *>(work), most);
     return hipGetLastError();
 }
@@ -2119,7 +2671,8 @@ hipError_t prk_obj_walk_group(const prk::FrameParams *fp, int32_t mode, uint32_t
                               const uint32_t *big, const unsigned long long *big_off, const uint32_t *big_cap,
                               uint32_t nbig, int32_t *pool, const uint32_t *escan, const uint32_t *total0p,
                               void *work, const unsigned long long *soff, void *recs, void *srecs, void *raw,
-                              void *pos, uint32_t *span_tri, uint32_t *err, hipStream_t s) {
+                              void *pos, uint32_t *span_tri, uint32_t *err, const uint32_t *prstat,
+                              hipStream_t s) {
     if (nbig == 0) return hipSuccess;
     const size_t bytes = lcap ? prk::slot_lds_bytes(lcap) : 0;
     const uint32_t nt = prk_obj_walk_threads(lcap);
@@ -2131,7 +2684,7 @@ hipError_t prk_obj_walk_group(const prk::FrameParams *fp, int32_t mode, uint32_t
                            total0p, reinterpret_cast<prk::ObjEdge *>(work), soff,                                   \
                            reinterpret_cast<prk::SpanRecG *>(recs), reinterpret_cast<prk::ScSpanRecG *>(srecs),     \
                            reinterpret_cast<prk::PairRaw *>(raw), reinterpret_cast<prk::SpanPos *>(pos), span_tri,  \
-                           err);                                                                                    \
+                           err, prstat);                                                                            \
         break;
         PRK_WALK_WAVE(prk::MODE_AVX)
         PRK_WALK_WAVE(prk::MODE_SC_GOURAUD)
@@ -2143,6 +2696,76 @@ hipError_t prk_obj_walk_group(const prk::FrameParams *fp, int32_t mode, uint32_t
     }
     return hipGetLastError();
 }
+// The chunked walk of large objects (prk_spans.hip k_pr_*), in three calls:
+// begin (every object: rows, chunk starts, canonical lists), a group call per
+// (mode, LDS capacity) of objects (grp: indices into the PrObj table; the
+// speculative chunk walks, then the walks again of chunks whose start was not
+// the true list), end (the outcome into err[1], err[2]).
+hipError_t prk_pr_walk_begin(const prk::FrameParams *fp, const prk::PrWalkArgs *a, hipStream_t s) {
+    if (a->npr == 0) return hipSuccess;
+    if (a->npr > 65535 || a->max_edges == 0) return hipErrorInvalidValue;
+    const prk::PrObj *P = reinterpret_cast<const prk::PrObj *>(a->pro);
+    prk::PrRow *PR = reinterpret_cast<prk::PrRow *>(a->prrow);
+    const prk::ObjDesc *O = reinterpret_cast<const prk::ObjDesc *>(a->objs);
+    const prk::ObjEdge *W = reinterpret_cast<const prk::ObjEdge *>(a->work);
+    hipLaunchKernelGGL(prk::k_pr_hist, dim3(a->npr), dim3(prk::kSlotMaxThreads), 0, s, *fp, O, P, a->escan,
+                       a->total0p, W, PR, a->cnt, a->eoff, a->fge, a->prstat);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemsetAsync(a->ccur, 0, (size_t)a->nchunks * 4, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(prk::k_pr_fill, dim3((a->max_edges + 255) / 256, a->npr), dim3(256), 0, s, *fp, O, P, PR,
+                       a->escan, a->total0p, W, a->ccur, reinterpret_cast<float4 *>(a->key),
+                       reinterpret_cast<prk::ObjEdge *>(a->est), a->prstat);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(prk::k_pr_start, dim3(a->nchunks), dim3(prk::kPrStartThreads), 0, s, P, a->npr, a->ccur,
+                       reinterpret_cast<const float4 *>(a->key), reinterpret_cast<const prk::ObjEdge *>(a->est),
+                       reinterpret_cast<prk::ObjEdge *>(a->sst), a->prstat);
+    return hipGetLastError();
+}
+hipError_t prk_pr_walk_group(const prk::FrameParams *fp, const prk::PrWalkArgs *a, int32_t mode, uint32_t cap,
+                             const uint32_t *grp, uint32_t ngroup, uint32_t max_chunks, hipStream_t s) {
+    if (ngroup == 0 || max_chunks == 0) return hipSuccess;
+    if (cap == 0 || ngroup > 65535) return hipErrorInvalidValue;
+    const size_t bytes = prk::slot_lds_bytes(cap);
+    const uint32_t nt = prk::slot_threads(cap);
+    const prk::PrObj *P = reinterpret_cast<const prk::PrObj *>(a->pro);
+    const prk::PrRow *PR = reinterpret_cast<const prk::PrRow *>(a->prrow);
+    const prk::ObjDesc *O = reinterpret_cast<const prk::ObjDesc *>(a->objs);
+    const prk::ObjEdge *W = reinterpret_cast<const prk::ObjEdge *>(a->work);
+    const prk::ObjEdge *SST = reinterpret_cast<const prk::ObjEdge *>(a->sst);
+    prk::ObjEdge *EE = reinterpret_cast<prk::ObjEdge *>(a->eend);
+    prk::PairRaw *RAW = reinterpret_cast<prk::PairRaw *>(a->raw);
+    prk::SpanPos *POS = reinterpret_cast<prk::SpanPos *>(a->pos);
+    switch (mode) {
+#define PRK_PR_GROUP(MM)                                                                                             \
+    case MM:                                                                                                         \
+        hipLaunchKernelGGL(prk::k_pr_chunk<MM>, dim3(max_chunks, ngroup), dim3(nt), bytes, s, *fp, O, P, grp, cap,  \
+                           PR, a->cnt, a->eoff, a->fge, a->escan, a->total0p, W, a->soff, SST, EE, a->eend_m,       \
+                           a->match, a->prstat, RAW, POS, a->span_tri, a->err);                                      \
+        if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;                                          \
+        hipLaunchKernelGGL(prk::k_pr_fix<MM>, dim3(ngroup), dim3(nt), bytes, s, *fp, O, P, grp, cap, PR, a->cnt,    \
+                           a->eoff, a->fge, a->escan, a->total0p, W, a->soff, SST, EE, a->eend_m, a->match,         \
+                           a->prstat, RAW, POS, a->span_tri, a->err);                                                \
+        break;
+        PRK_PR_GROUP(prk::MODE_AVX)
+        PRK_PR_GROUP(prk::MODE_SC_GOURAUD)
+        PRK_PR_GROUP(prk::MODE_SC_GOURAUD_TEX)
+        PRK_PR_GROUP(prk::MODE_SC_PHONG)
+        PRK_PR_GROUP(prk::MODE_SC_PHONG_TEX)
+#undef PRK_PR_GROUP
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+hipError_t prk_pr_walk_end(const prk::PrWalkArgs *a, hipStream_t s) {
+    if (a->npr == 0) return hipSuccess;
+    hipLaunchKernelGGL(prk::k_pr_tally, dim3(1), dim3(256), 0, s, reinterpret_cast<const prk::PrObj *>(a->pro),
+                       a->npr, a->prstat, a->err);
+    return hipGetLastError();
+}
+uint32_t prk_pr_chunk_rows(void) { return (uint32_t)prk::kPrChunk; }
+int32_t prk_pr_max_row_entries(void) { return prk::kPrMaxM; }
+int32_t prk_pr_max_rows(void) { return prk::kMaxactRows - 1; }
 // The slot walk's pairs (SPAN_RAW) into span records, one thread per slot.
 hipError_t prk_span_finish(const prk::FrameParams *fp, const void *raw, uint32_t nslot, void *recs, void *srecs,
                            void *pos, hipStream_t s) {

@@ -61,7 +61,8 @@ class PrkStats(C.Structure):
     _fields_ = [("triangles", C.c_uint64), ("bin_entries", C.c_uint64), ("tiles", C.c_uint32),
                 ("frames_timed", C.c_uint32), ("ms_bin", C.c_float), ("ms_raster", C.c_float),
                 ("sum_ms_bin", C.c_double), ("sum_ms_raster", C.c_double),
-                ("anomalies", C.c_uint32), ("slow_replays", C.c_uint32), ("sum_ms_vis", C.c_double), ("sum_ms_span", C.c_double)]
+                ("anomalies", C.c_uint32), ("slow_replays", C.c_uint32), ("sum_ms_vis", C.c_double), ("sum_ms_span", C.c_double),
+                ("objects_chunked", C.c_uint32), ("objects_walked", C.c_uint32)]
 
 
 def make_transform(D, F, M2P, cx, cy):

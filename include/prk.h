@@ -136,6 +136,14 @@ typedef struct prk_stats {
                                 of sum_ms_raster */
     double sum_ms_span;      /* accumulated: the k_walk part (AVX frames:
                                 raster = k_vis + k_walk + k_pix) */
+    uint32_t objects_chunked; /* large objects (48+ triangles) whose AET walk
+                                 ran as chunks of rows walked at once, each
+                                 from its first row's sorted list, checked and
+                                 walked again where that was not the true
+                                 list; cumulative */
+    uint32_t objects_walked;  /* large objects walked row after row from the
+                                 first (an odd row, a NaN key, lists past the
+                                 LDS); cumulative */
 } prk_stats;
 
 typedef struct prk_context prk_context;

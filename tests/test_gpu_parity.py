@@ -685,6 +685,57 @@ def test_whole_object_scalar_c2_one_object(gpu, phong):
 
 
 @pytest.mark.parametrize("sem", [abi.PRK_SEM_AVX, abi.PRK_SEM_AVX_ST, abi.PRK_SEM_SCALAR])
+def test_whole_object_chunked_walk(gpu, sem, monkeypatch):
+    """The chunked walk of large objects (prk_spans.hip k_pr_*): the rows cut
+    into chunks walked at once, each from its first row's sorted list, the
+    chunks whose start was not the true list walked again in order.
+    ConstructSphere as one object: bit for bit the oracle's sequential walk
+    and the plain workgroup walk (PRK_OBJ_ROWS=0).  Overlapping random
+    700-triangle objects (crossing edges: many chunk starts are not the sorted
+    list) against both too.  Sphere strips next to soup objects whose
+    triangles cross the top border (rows with one active edge: walked row by
+    row from the first) in one pass."""
+    s = _sphere_scene()
+    if sem == abi.PRK_SEM_SCALAR:
+        s.texture = None
+    g, o = run_both(s, semantics=sem, phong=True, tris_per_object=s.tri_count, threads=1,
+                    exact_color=sem != abi.PRK_SEM_SCALAR, label="sphere chunked sem=%d" % sem)
+    assert g[3]["objects_chunked"] == 1 and g[3]["objects_walked"] == 0, g[3]
+    monkeypatch.setenv("PRK_OBJ_ROWS", "0")
+    w = prk.render_scene(s, semantics=sem, phong=True, tris_per_object=s.tri_count)
+    monkeypatch.delenv("PRK_OBJ_ROWS")
+    assert w[3]["objects_chunked"] == 0 and w[3]["objects_walked"] == 1, w[3]
+    for k in range(3):
+        assert np.array_equal(g[k].view(np.uint32), w[k].view(np.uint32)), k
+    soup = scenes.with_ties(scenes.random_soup(2800, 384, 256, radius=40, seed=9, centroid_margin=40), seed=9)
+    if sem == abi.PRK_SEM_SCALAR:
+        soup.texture = None
+    inner = scenes.random_soup(2800, 384, 256, radius=40, seed=19, centroid_margin=-45)  # on screen: even rows
+    if sem == abi.PRK_SEM_SCALAR:
+        inner.texture = None
+    c, _ = run_both(inner, semantics=sem, phong=True, tris_per_object=700, threads=1,
+                    exact_color=sem != abi.PRK_SEM_SCALAR, label="crossing objects chunked sem=%d" % sem)
+    assert c[3]["objects_chunked"] == 4, c[3]
+    monkeypatch.setenv("PRK_OBJ_ROWS", "0")
+    cw = prk.render_scene(inner, semantics=sem, phong=True, tris_per_object=700)
+    monkeypatch.delenv("PRK_OBJ_ROWS")
+    for k in range(3):
+        assert np.array_equal(c[k].view(np.uint32), cw[k].view(np.uint32)), k
+    # sphere strips (chunked) and soup objects crossing the top border (walked) in one pass
+    V, Cc, N, UV = prk.construct_sphere()
+    big = scenes.Scene(384, 256, np.concatenate([V[:3 * 64 * 20] * 0.6, soup.vertices[:3 * 64 * 10]]),
+                       np.concatenate([Cc[:3 * 64 * 20], soup.colors[:3 * 64 * 10]]),
+                       np.concatenate([N[:3 * 64 * 20], soup.normals[:3 * 64 * 10]]),
+                       np.concatenate([UV[:3 * 64 * 20], soup.uvs[:3 * 64 * 10]]), soup.transform, soup.lights,
+                       soup.ambient, soup.texture, P=(0.0, 0.0, 2.0), name="mixed rows")
+    g2, _ = run_both(big, semantics=sem, phong=True, tris_per_object=64, threads=1,
+                     exact_color=sem != abi.PRK_SEM_SCALAR, label="mixed rows sem=%d" % sem)
+    st = g2[3]
+    assert st["objects_chunked"] > 0 and st["objects_walked"] > 0, st
+    assert st["objects_chunked"] + st["objects_walked"] == 30, st
+
+
+@pytest.mark.parametrize("sem", [abi.PRK_SEM_AVX, abi.PRK_SEM_AVX_ST, abi.PRK_SEM_SCALAR])
 @pytest.mark.parametrize("tpo", [64, 700])
 def test_whole_object_wave_walk(gpu, sem, tpo):
     """Objects large enough for the one-wave walk (k_obj_walk_wave): random

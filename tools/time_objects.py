@@ -27,8 +27,24 @@ def sphere_scene(W, H):
                         base.texture, P=(0.0, 0.0, 2.0), name="sphere")
 
 
+def spheres64_scene(W, H):
+    """64 ConstructSphere instances (r = 0.175 m) on an 8 x 8 grid, one
+    object each (their offsets baked into the vertices, P = (0, 0, 2))."""
+    V, Cc, N, UV = prk.construct_sphere()
+    base = scenes.random_soup(1, W, H, seed=0)
+    vs = []
+    for i in range(8):
+        for j in range(8):
+            vs.append(V * 0.35 + np.array([(i - 3.5) * 0.5, (j - 3.5) * 0.5, 0.0], np.float32))
+    k = 64
+    return scenes.Scene(W, H, np.concatenate(vs).astype(np.float32), np.tile(Cc, (k, 1)), np.tile(N, (k, 1)),
+                        np.tile(UV, (k, 1)), base.transform, scenes.LIGHTS_ONE, scenes.AMBIENT_ONE, base.texture,
+                        P=(0.0, 0.0, 2.0), name="spheres64")
+
+
 def cases():
     sph = sphere_scene(1024, 1024)
+    sph64 = spheres64_scene(2048, 2048)
     c2 = scenes.displaced_sphere(70000, 1920, 1080, seed=3)
     c2t = c2.subset(0, c2.tri_count)
     c2t.texture = sph.texture  # FillLineOptimized needs a Bitmap (projekt.cpp:1506)
@@ -39,7 +55,9 @@ def cases():
         ("sphere_1obj_scalar_phong", sph, abi.PRK_SEM_SCALAR, True, sph.tri_count),
         ("c2_1obj_scalar_phong", c2, abi.PRK_SEM_SCALAR, True, c2.tri_count),
         ("c2_1obj_avx", c2t, abi.PRK_SEM_AVX, True, c2.tri_count),
+        ("spheres64_64obj_avx", sph64, abi.PRK_SEM_AVX, True, sph.tri_count),
         ("c3b_obj16_avx", soup, abi.PRK_SEM_AVX, True, 16),
+        ("c3b_1obj_avx", soup, abi.PRK_SEM_AVX, True, soup.tri_count),
         ("c3b_obj1_avx", soup, abi.PRK_SEM_AVX, True, 1),
     ]
 
@@ -62,7 +80,8 @@ def time_case(s, sem, phong, tpo, frames):
             r.synchronize()
             if i >= 2:
                 dts.append(time.perf_counter() - t0)
-        return float(np.median(dts)) * 1e3
+        st = r.stats()  # (cumulative over the frames + 2 warm-ups)
+        return float(np.median(dts)) * 1e3, st["objects_chunked"] // (frames + 2), st["objects_walked"] // (frames + 2)
     finally:
         r.close()
 
@@ -78,9 +97,11 @@ def main():
     for name, s, sem, phong, tpo in cases():
         if only and name not in only:
             continue
-        ms = time_case(s, sem, phong, tpo, a.frames)
+        # (one object of the whole C3b soup: its walk takes long, fewer frames)
+        ms, by_rows, walked = time_case(s, sem, phong, tpo, min(a.frames, 2) if name == "c3b_1obj_avx" else a.frames)
         out[name] = {"tris": s.tri_count, "tris_per_object": tpo, "target": "%dx%d" % (s.width, s.height),
-                     "ms_per_frame": round(ms, 3), "mpixels_s": round(s.width * s.height / ms / 1e3, 1)}
+                     "ms_per_frame": round(ms, 3), "mpixels_s": round(s.width * s.height / ms / 1e3, 1),
+                     "large_objects_chunked": by_rows, "large_objects_walked": walked}
         print(json.dumps({name: out[name]}), flush=True)
     if a.json:
         with open(a.json, "w") as f:
