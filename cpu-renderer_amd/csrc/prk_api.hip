@@ -282,7 +282,7 @@ struct prk_context {
         DevBuf d_stage, d_edges, d_ord, d_temp, d_recs, d_pos, d_span_tri, d_scnt, d_soff, d_keys_a, d_vals_a,
             d_keys_b, d_vals_b, d_offs, d_nwin, d_wtag, d_srecs, d_work, d_ekeys, d_ekeys2, d_evals, d_ecnt, d_escan,
             d_rcnt, d_rscan, d_bound, d_oslot, d_pool, d_err, d_raw, d_most, d_cls, d_prrow, d_prcnt, d_preoff,
-            d_prfge, d_prccur, d_prkey, d_prest, d_prsst, d_preend, d_preendm, d_prmatch, d_prstat;
+            d_prfge, d_prccur, d_prkey, d_prest, d_prsst, d_preend, d_preendm, d_prmatch, d_prsidx, d_prsm, d_prstat;
         // the pass's host tables, packed into pinned memory for one upload
         // (stage_ev: that upload, before the staging is rewritten)
         char *h_stage = nullptr;
@@ -480,7 +480,7 @@ int prk_destroy(prk_context *c) {
                         &S.d_escan, &S.d_rcnt, &S.d_rscan, &S.d_bound, &S.d_oslot, &S.d_pool, &S.d_err,
                         &S.d_raw, &S.d_most, &S.d_cls, &S.d_prrow, &S.d_prcnt, &S.d_preoff, &S.d_prfge,
                         &S.d_prccur, &S.d_prkey, &S.d_prest, &S.d_prsst, &S.d_preend, &S.d_preendm,
-                        &S.d_prmatch, &S.d_prstat};
+                        &S.d_prmatch, &S.d_prsidx, &S.d_prsm, &S.d_prstat};
         for (DevBuf *b : sb) b->release();
         if (S.h_rb) (void)hipHostFree(S.h_rb);
         if (S.stage_ev) {
@@ -1795,7 +1795,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
         PRK_TRY(hipMemcpyAsync(h_most, S.d_most.p, (size_t)nbig_all * 12, hipMemcpyDeviceToHost, s));
     }
     PRK_TRY(hipMemcpyAsync(S.h_rb, oslot + nobj, 8, hipMemcpyDeviceToHost, s));
-    PRK_TRY(hipMemsetAsync(S.d_err.p, 0, 12, s));  // (error bits, then the parallel-rows tally)
+    PRK_TRY(hipMemsetAsync(S.d_err.p, 0, 16, s));  // (error bits, then the chunked walk's tally)
     PRK_TRY(hipStreamSynchronize(s));
     uint64_t nslot64;
     std::memcpy(&nslot64, S.h_rb, 8);
@@ -1943,6 +1943,8 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
         PRK_TRY(S.d_prccur.ensure((size_t)pr_chunks * 4));
         PRK_TRY(S.d_preendm.ensure((size_t)pr_chunks * 4));
         PRK_TRY(S.d_prmatch.ensure((size_t)pr_chunks * 4));
+        PRK_TRY(S.d_prsm.ensure((size_t)pr_chunks * 4));
+        PRK_TRY(S.d_prsidx.ensure(pr_ents * 4));
         PRK_TRY(S.d_prkey.ensure(pr_ents * 16));
         PRK_TRY(S.d_prest.ensure(pr_ents * 112));  // prk_spans.hip ObjEdge
         PRK_TRY(S.d_prsst.ensure(pr_ents * 112));
@@ -1967,6 +1969,8 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
         pa.eend = S.d_preend.p;
         pa.eend_m = (uint32_t *)S.d_preendm.p;
         pa.match = (uint32_t *)S.d_prmatch.p;
+        pa.sidx = (uint32_t *)S.d_prsidx.p;
+        pa.s_m = (uint32_t *)S.d_prsm.p;
         pa.prstat = (uint32_t *)S.d_prstat.p;
         pa.soff = oslot;
         pa.raw = S.d_raw.p;
@@ -1997,13 +2001,13 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(temp(tb));
     PRK_TRY(prk_scan_u32(scnt, soff, nslot + 1, S.d_temp.p, &tb, s));
     PRK_TRY(hipMemcpyAsync(S.h_rb + 2, soff + nslot, 4, hipMemcpyDeviceToHost, s));
-    PRK_TRY(hipMemcpyAsync(S.h_rb + 3, S.d_err.p, 12, hipMemcpyDeviceToHost, s));
+    PRK_TRY(hipMemcpyAsync(S.h_rb + 3, S.d_err.p, 16, hipMemcpyDeviceToHost, s));
     PRK_TRY(hipStreamSynchronize(s));
     const uint32_t total = S.h_rb[2];
     if (S.h_rb[3]) return PRK_ERR_DEVICE;  // a walk outside its LDS list or span slots (never)
     if (std::getenv("PRK_PR_DEBUG"))
-        std::fprintf(stderr, "prk: large objects %u, by rows: taken %u done %u failed %u (rows %u, entries %llu)\n",
-                     nbig_all, npr, S.h_rb[4], S.h_rb[5], pr_rows, (unsigned long long)pr_ents);
+        std::fprintf(stderr, "prk: large objects %u, chunked: taken %u done %u failed %u; chunks %u, walked again %u\n",
+                     nbig_all, npr, S.h_rb[4], S.h_rb[5], pr_chunks, S.h_rb[6]);
     c->stats.objects_chunked += S.h_rb[4];
     c->stats.objects_walked += nbig_all - S.h_rb[4];
     c->stats.triangles = T;

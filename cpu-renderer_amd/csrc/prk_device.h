@@ -1047,6 +1047,7 @@ struct PrWalkArgs {
     void *key;                  // float4 per entry (chunk j of an object: ent_off + j * most)
     void *est, *sst, *eend;     // ObjEdge per entry: arrival order / canonical list / a walk's end list
     uint32_t *eend_m, *match;   // per chunk
+    uint32_t *sidx, *s_m;       // per entry / per chunk: a chunk's list at its first row (edge indices)
     uint32_t *prstat;           // per object of the pass
     const unsigned long long *soff;
     void *raw, *pos;            // PairRaw / SpanPos per span slot

@@ -1953,34 +1953,39 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_obj_walk_wave(FrameParams f
 // more whose rows and lists fit: k_obj_maxact's sizes, host-checked).
 //
 // The walk is serial in rows: the list at row r is a function of the list at
-// r - 1.  But a row's list is usually just its active edges sorted by the
-// insertion key (X, Gradient, Left), ties in MergeSort order -- the canonical
-// list C(r) (a batch inserted into an empty list is exactly that; a mesh's
-// edges seldom cross).  So the object's rows are cut into chunks of kPrChunk
-// rows, and every chunk is walked at once, speculatively, from the canonical
-// list of its first row, by the workgroup walk's own list operations
-// (walk_chunk = walk_object_block from a given list, for a given row range).
-// Each chunk then compares the list its walk reaches at the next chunk's
-// first row with that row's canonical list.  The first chunk starts from the
-// true list; a chunk whose predecessor reached its canonical start list
-// started from the true list too; any other chunk is walked again, in order,
-// from its predecessor's true end list (k_pr_fix: one workgroup per object,
-// chunk after chunk, walking only those).  The spans of a chunk go to the
+// r - 1.  But that dependence fades: entries expire, crossings swap back, so
+// a walk started a few rows early from a plausible list -- the row's active
+// edges sorted by the insertion key (X, Gradient, Left), ties in MergeSort
+// order, which is what a batch inserted into an empty list is -- usually
+// reaches the true list.  So the object's rows are cut into chunks of
+// kPrChunk rows and every chunk is walked at once by the workgroup walk's
+// own list operations (walk_chunk = walk_object_block from a given list over
+// a given row range): chunk j > 0 from the sorted list of chunk j - 1's first
+// row, walking chunk j - 1's rows as a warm-up (stepping, no spans), then its
+// own rows (spans).  Exactness is checked, not assumed: chunk j's list at its
+// first row must equal the list chunk j - 1 ended with (k_pr_cmp); chunk 0
+// starts from the true list; a chunk whose predecessor walked from the true
+// list and ended on its start list walked from the true list too; any other
+// chunk is walked again, in order, from its predecessor's true end list
+// (k_pr_fix: one workgroup per object, chunk after chunk, walking only
+// those; C2 and ConstructSphere need none).  The spans of a chunk go to the
 // slots its rows take in the sequential walk -- every row pairs all its
 // entries (objects with an odd row are left to k_obj_walk_wave), so a row's
-// pairs are its entries / 2, whatever their order -- in the same order.
+// pairs are its entries / 2 whatever their order -- in the same order.
 //   k_pr_hist   workgroup per object: its rows' entry counts and their scan
 //               (the span slots), the first sorted edge of every row
 //   k_pr_fill   thread per edge: stepped row by row as the walk steps it
 //               (obj_step), its state and key at every chunk's first row
-//   k_pr_start  workgroup per chunk: the canonical list of its first row
-//               (rank sort), as edge states
-//   k_pr_chunk  workgroup per chunk: the speculative walk
-//   k_pr_fix    workgroup per object: the chunks whose start was not the
+//   k_pr_start  workgroup per chunk: the sorted list of its first row (rank
+//               sort), as edge states
+//   k_pr_chunk  workgroup per chunk: the warm-up and the chunk's walk
+//   k_pr_cmp    workgroup per chunk: its end list against the next chunk's
+//               start list
+//   k_pr_fix    workgroup per object: the chunks that did not walk from the
 //               true list, walked again in order
 // ---------------------------------------------------------------------------
 #ifndef PRK_PR_CHUNK
-#define PRK_PR_CHUNK 16
+#define PRK_PR_CHUNK 8
 #endif
 constexpr int32_t kPrChunk = PRK_PR_CHUNK;  // rows per chunk
 constexpr int32_t kPrMaxM = 1022;           // most entries of a list (the workgroup walk's largest LDS list)
@@ -2180,15 +2185,18 @@ __global__ void __launch_bounds__(kPrStartThreads) k_pr_start(const PrObj *__res
 
 // walk_object_block over the rows [r0, r1) of an object, from the list
 // start[0, m0) at row r0 (states at r0, their sorted edge index in Next; the
-// row's insertion and expiry done), its spans from slot base + emitted0 on.
-// At r1 < MaxY: the list after r1's insertion and expiry goes to end[] /
-// *end_m, and the return value says whether it is canon[0, mc) (edge by
-// edge).  Every thread returns the same.
+// row's insertion and expiry done); its spans from row re >= r0 on (the rows
+// before: a warm-up, walked and stepped but not emitted), from slot base +
+// emitted0.  re > r0: the list at re (its sorted edge indices) goes to
+// sidx[] / *s_m.  r1 < MaxY: the list after r1's insertion and expiry goes to
+// end[] / *end_m, and the return value says whether its edges are
+// cmp[0, mc) in order (cmp null: false).  Every thread returns the same.
 template <int M>
 __device__ bool walk_chunk(const FrameParams &fp, const ObjDesc &od, const ObjEdge *__restrict__ E, uint32_t n,
                            int32_t MaxY, uint32_t base, uint32_t bound, const SlotLds &S, BlockRed &R, uint32_t cap,
-                           int32_t r0, int32_t r1, uint32_t ins0, const ObjEdge *__restrict__ start, int m0,
-                           uint32_t emitted0, const ObjEdge *__restrict__ canon, int mc, ObjEdge *__restrict__ end,
+                           int32_t r0, int32_t re, int32_t r1, uint32_t ins0, const ObjEdge *__restrict__ start, int m0,
+                           uint32_t emitted0, uint32_t *__restrict__ sidx, uint32_t *__restrict__ s_m,
+                           const uint32_t *__restrict__ cmp, int mc, ObjEdge *__restrict__ end,
                            uint32_t *__restrict__ end_m, PairRaw *__restrict__ raw, SpanPos *__restrict__ pos,
                            uint32_t *__restrict__ span_tri, uint32_t *__restrict__ err) {
     constexpr bool kScalar = M != MODE_AVX;
@@ -2276,14 +2284,18 @@ __device__ bool walk_chunk(const FrameParams &fp, const ObjDesc &od, const ObjEd
             }
         }
         if (Row >= r1) break;
-        if (m == 0) {  // nothing happens on the rows before the next insertion (or r1): go there
+        if (Row == re && re > r0) {  // the list where the spans begin
+            for (int q = tid; q < m; q += (int)NT) sidx[q] = (uint32_t)S.st[S.idx[q]].Next;
+            if (tid == 0) *s_m = (uint32_t)m;
+        }
+        if (m == 0) {  // nothing happens on the rows before the next insertion (or re, r1): go there
             const int32_t nx = ins < n ? E[ins].YMin : INT32_MAX;
-            Row = max(Row, min(nx, r1) - 1);
+            Row = max(Row, min(nx, Row < re ? re : r1) - 1);
             continue;
         }
         const int P = m / 2;  // pairing 3751-3869, as walk_object_block
         const bool valid = tid < P;
-        const bool emit = Row >= RowLo;
+        const bool emit = Row >= RowLo && Row >= re;
         int32_t i0 = 0, i1 = 0;
         float x0 = 0.0f, x1 = 0.0f;
         if (valid) {
@@ -2339,19 +2351,23 @@ __device__ bool walk_chunk(const FrameParams &fp, const ObjDesc &od, const ObjEd
         __syncthreads();
     }
     if (r1 >= MaxY) return true;
-    // the list at r1: out, and against the canonical one
-    bool same = m == mc;
+    // the list at r1: out, and against cmp
+    bool same = cmp != nullptr && m == mc;
     for (int q = tid; q < m; q += (int)NT) {
         const ObjEdge &e = S.st[S.idx[q]];
         end[q] = e;
-        if (q < mc) same = same && e.Next == canon[q].Next;
+        if (cmp && q < mc) same = same && (uint32_t)e.Next == cmp[q];
     }
     if (tid == 0) *end_m = (uint32_t)m;
     return blk_max(R, same ? 0 : 1) == 0;
 }
 
-// Chunk c of the objects of one mode (pro[pi], pi in group [0, ngroup)):
-// grid (chunks of the group's longest object, ngroup).
+// Chunk j of the objects of one mode (pro[pi], pi in group [0, ngroup)):
+// grid (chunks of the group's longest object, ngroup).  Chunk j > 0 starts
+// one chunk early, from the sorted list of chunk j - 1's first row, and
+// walks those rows as a warm-up (the list's order converges on the true one
+// as entries expire and neighbours swap), then its own rows; its list at its
+// first row goes to sidx (k_pr_cmp compares it with chunk j - 1's end).
 template <int M>
 __global__ void __launch_bounds__(kSlotMaxThreads) k_pr_chunk(FrameParams fp, const ObjDesc *__restrict__ objs,
                                                             const PrObj *__restrict__ pro, const uint32_t *__restrict__ grp,
@@ -2364,7 +2380,8 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_pr_chunk(FrameParams fp, co
                                                             const ObjEdge *__restrict__ work,
                                                             const unsigned long long *__restrict__ soff,
                                                             const ObjEdge *__restrict__ sst, ObjEdge *__restrict__ eend,
-                                                            uint32_t *__restrict__ eend_m, uint32_t *__restrict__ match,
+                                                            uint32_t *__restrict__ eend_m, uint32_t *__restrict__ sidx,
+                                                            uint32_t *__restrict__ s_m,
                                                             const uint32_t *__restrict__ prstat, PairRaw *__restrict__ raw,
                                                             SpanPos *__restrict__ pos, uint32_t *__restrict__ span_tri,
                                                             uint32_t *__restrict__ err) {
@@ -2379,22 +2396,44 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_pr_chunk(FrameParams fp, co
     obj_range(od, escan, *total0p, e0, n);
     const ObjEdge *E = work + e0;
     const PrRow pr = prrow[pi];
-    const int32_t r0 = pr.first_row + (int32_t)(j * kPrChunk), r1 = min(r0 + kPrChunk, pr.max_y);
-    const uint32_t jr0 = j * kPrChunk, jr1 = (uint32_t)(r1 - pr.first_row);
+    const int32_t re = pr.first_row + (int32_t)(j * kPrChunk), r1 = min(re + kPrChunk, pr.max_y);
+    const uint32_t js = j ? j - 1 : 0;  // the chunk whose first row it starts from
+    const int32_t r0 = pr.first_row + (int32_t)(js * kPrChunk);
+    const uint32_t jr0 = js * kPrChunk, jre = j * kPrChunk;
     const int32_t RowLo = fp.draws[od.draw].mode != MODE_AVX ? fp.row0 - 1 : fp.row0;
     const uint32_t jlo = (uint32_t)min(max(0, RowLo - pr.first_row), (int32_t)P.rows);
-    const uint32_t emitted0 = (eoff[P.row_off + max(jr0, jlo)] - eoff[P.row_off + jlo]) / 2;
+    const uint32_t emitted0 = (eoff[P.row_off + max(jre, jlo)] - eoff[P.row_off + jlo]) / 2;
     const uint32_t base = (uint32_t)soff[P.o], bound = (uint32_t)(soff[P.o + 1] - soff[P.o]);
     SlotLds S;
     S.carve(lds_list, cap, blockDim.x);
     const uint32_t c = P.chunk_off + j;
-    const uint32_t g0 = P.ent_off + j * P.most, g1 = g0 + P.most;
+    const uint32_t gs = P.ent_off + js * P.most, ge = P.ent_off + j * P.most, g1 = ge + P.most;
     const bool last = r1 >= pr.max_y;
-    const bool same = walk_chunk<M>(fp, od, E, n, pr.max_y, base, bound, S, R, cap, r0, r1,
-                                    fge[P.row_off + jr0 + 1], sst + g0, (int)cnt[P.row_off + jr0], emitted0,
-                                    last ? nullptr : sst + g1, last ? 0 : (int)cnt[P.row_off + jr1],
-                                    last ? nullptr : eend + g1, eend_m + c, raw, pos, span_tri, err);
-    if (threadIdx.x == 0) match[c] = same ? 1u : 0u;
+    (void)walk_chunk<M>(fp, od, E, n, pr.max_y, base, bound, S, R, cap, r0, re, r1, fge[P.row_off + jr0 + 1],
+                        sst + gs, (int)cnt[P.row_off + jr0], emitted0, sidx + ge, s_m + c, nullptr, 0,
+                        last ? nullptr : eend + g1, eend_m + c, raw, pos, span_tri, err);
+}
+
+// match[c] = chunk c's end list (eend) is chunk c + 1's list at its first
+// row (sidx): then chunk c + 1 walked its rows from the true list whenever
+// chunk c did.  Workgroup per chunk.
+__global__ void k_pr_cmp(const PrObj *__restrict__ pro, uint32_t npr, const uint32_t *__restrict__ prstat,
+                         const ObjEdge *__restrict__ eend, const uint32_t *__restrict__ eend_m,
+                         const uint32_t *__restrict__ sidx, const uint32_t *__restrict__ s_m,
+                         uint32_t *__restrict__ match) {
+    __shared__ int32_t diff;
+    const uint32_t c = blockIdx.x;
+    const PrObj P = pro[pr_obj_of_chunk(pro, npr, c)];
+    const uint32_t j = c - P.chunk_off;
+    if (j + 1 >= pr_chunks(P) || prstat[P.o] != kPrDone) return;
+    if (threadIdx.x == 0) diff = eend_m[c] != s_m[c + 1];
+    __syncthreads();
+    const uint32_t g1 = P.ent_off + (j + 1) * P.most, m = eend_m[c];
+    if (!diff)
+        for (uint32_t q = threadIdx.x; q < m; q += blockDim.x)
+            if ((uint32_t)eend[g1 + q].Next != sidx[g1 + q]) diff = 1;
+    __syncthreads();
+    if (threadIdx.x == 0) match[c] = diff ? 0u : 1u;
 }
 
 // Per object of the group: the chunks whose start list was not the true one,
@@ -2410,8 +2449,10 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_pr_fix(FrameParams fp, cons
                                                           const uint32_t *__restrict__ total0p,
                                                           const ObjEdge *__restrict__ work,
                                                           const unsigned long long *__restrict__ soff,
-                                                          const ObjEdge *__restrict__ sst, ObjEdge *__restrict__ eend,
-                                                          uint32_t *__restrict__ eend_m, uint32_t *__restrict__ match,
+                                                          ObjEdge *__restrict__ eend, uint32_t *__restrict__ eend_m,
+                                                          const uint32_t *__restrict__ sidx,
+                                                          const uint32_t *__restrict__ s_m,
+                                                          const uint32_t *__restrict__ match,
                                                           const uint32_t *__restrict__ prstat,
                                                           PairRaw *__restrict__ raw, SpanPos *__restrict__ pos,
                                                           uint32_t *__restrict__ span_tri, uint32_t *__restrict__ err) {
@@ -2431,7 +2472,7 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_pr_fix(FrameParams fp, cons
     SlotLds S;
     S.carve(lds_list, cap, blockDim.x);
     const uint32_t nch = pr_chunks(P);
-    bool prev_true = true;  // chunk j - 1 ended on its next chunk's canonical start (chunk 0: the true start)
+    bool prev_true = true;  // chunk j walked its rows from the true list (chunk 0: from the first row)
     for (uint32_t j = 0; j < nch; ++j) {
         const uint32_t c = P.chunk_off + j;
         if (prev_true) {  // its speculative walk started from the true list: keep it
@@ -2439,20 +2480,23 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_pr_fix(FrameParams fp, cons
             continue;
         }
         // walk it again from the true list: chunk j - 1's end (eend at its entry block)
+        if (threadIdx.x == 0) atomicAdd(&err[3], 1u);  // (the pass's re-walked chunks)
         const int32_t r0 = pr.first_row + (int32_t)(j * kPrChunk), r1 = min(r0 + kPrChunk, pr.max_y);
         const uint32_t jr0 = j * kPrChunk, jr1 = (uint32_t)(r1 - pr.first_row);
         const uint32_t emitted0 = (eoff[P.row_off + max(jr0, jlo)] - eoff[P.row_off + jlo]) / 2;
         const uint32_t g0 = P.ent_off + j * P.most, g1 = g0 + P.most;
         const bool last = r1 >= pr.max_y;
         __syncthreads();  // (the previous walk's LDS and eend writes)
-        prev_true = walk_chunk<M>(fp, od, E, n, pr.max_y, base, bound, S, R, cap, r0, r1, fge[P.row_off + jr0 + 1],
-                                  eend + g0, (int)eend_m[c - 1], emitted0, last ? nullptr : sst + g1,
-                                  last ? 0 : (int)cnt[P.row_off + jr1], last ? nullptr : eend + g1, eend_m + c, raw,
-                                  pos, span_tri, err);
+        prev_true = walk_chunk<M>(fp, od, E, n, pr.max_y, base, bound, S, R, cap, r0, r0, r1, fge[P.row_off + jr0 + 1],
+                                  eend + g0, (int)eend_m[c - 1], emitted0, nullptr, nullptr,
+                                  last ? nullptr : sidx + g1, last ? 0 : (int)s_m[c + 1],
+                                  last ? nullptr : eend + g1, eend_m + c, raw, pos, span_tri, err);
+        (void)jr1;
     }
 }
 
-// The walk's outcome: err[1] += objects done, err[2] += objects failed.
+// The walk's outcome: err[1] += objects done, err[2] += objects failed
+// (err[3]: chunks walked again, k_pr_fix).
 __global__ void k_pr_tally(const PrObj *__restrict__ pro, uint32_t npr, const uint32_t *__restrict__ prstat,
                            uint32_t *__restrict__ err) {
     uint32_t done = 0, failed = 0;
@@ -2741,11 +2785,14 @@ hipError_t prk_pr_walk_group(const prk::FrameParams *fp, const prk::PrWalkArgs *
     case MM:                                                                                                         \
         hipLaunchKernelGGL(prk::k_pr_chunk<MM>, dim3(max_chunks, ngroup), dim3(nt), bytes, s, *fp, O, P, grp, cap,  \
                            PR, a->cnt, a->eoff, a->fge, a->escan, a->total0p, W, a->soff, SST, EE, a->eend_m,       \
-                           a->match, a->prstat, RAW, POS, a->span_tri, a->err);                                      \
+                           a->sidx, a->s_m, a->prstat, RAW, POS, a->span_tri, a->err);                               \
+        if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;                                          \
+        hipLaunchKernelGGL(prk::k_pr_cmp, dim3(a->nchunks), dim3(256), 0, s, P, a->npr, a->prstat, EE, a->eend_m,    \
+                           a->sidx, a->s_m, a->match);                                                               \
         if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;                                          \
         hipLaunchKernelGGL(prk::k_pr_fix<MM>, dim3(ngroup), dim3(nt), bytes, s, *fp, O, P, grp, cap, PR, a->cnt,    \
-                           a->eoff, a->fge, a->escan, a->total0p, W, a->soff, SST, EE, a->eend_m, a->match,         \
-                           a->prstat, RAW, POS, a->span_tri, a->err);                                                \
+                           a->eoff, a->fge, a->escan, a->total0p, W, a->soff, EE, a->eend_m, a->sidx, a->s_m,       \
+                           a->match, a->prstat, RAW, POS, a->span_tri, a->err);                                      \
         break;
         PRK_PR_GROUP(prk::MODE_AVX)
         PRK_PR_GROUP(prk::MODE_SC_GOURAUD)
