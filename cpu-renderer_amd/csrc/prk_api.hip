@@ -1977,6 +1977,8 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
         pa.pos = S.d_pos.p;
         pa.span_tri = (uint32_t *)S.d_span_tri.p;
         pa.err = (uint32_t *)S.d_err.p;
+        const char *warm = std::getenv("PRK_OBJ_CHUNK_WARMUP");  // 0: no warm-up (tests: every fix-up path)
+        pa.warmup = !(warm && warm[0] == '0');
         PRK_TRY(prk_pr_walk_begin(&fp, &pa, s));
         for (const PrGroup &g : prgroups)
             PRK_TRY(prk_pr_walk_group(&fp, &pa, g.mode, g.cap, d_cgrp + g.start, g.count, g.max_chunks, s));
@@ -2010,6 +2012,8 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
                      nbig_all, npr, S.h_rb[4], S.h_rb[5], pr_chunks, S.h_rb[6]);
     c->stats.objects_chunked += S.h_rb[4];
     c->stats.objects_walked += nbig_all - S.h_rb[4];
+    c->stats.object_chunks += pr_chunks;
+    c->stats.object_chunks_rewalked += S.h_rb[6];
     c->stats.triangles = T;
     c->stats.tiles = ntiles;
     c->stats.bin_entries = total;

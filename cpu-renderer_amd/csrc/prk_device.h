@@ -1037,6 +1037,7 @@ struct PrWalkArgs {
     const void *objs;           // ObjDesc[]
     const void *pro;            // PrObj[npr]
     uint32_t npr;               // objects
+    uint32_t warmup;            // chunks start one chunk early (0: from their own first row)
     uint32_t nchunks;           // their chunks
     uint32_t max_edges;         // most edges of one object
     const uint32_t *escan, *total0p;

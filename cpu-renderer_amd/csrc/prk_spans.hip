@@ -2187,7 +2187,7 @@ __global__ void __launch_bounds__(kPrStartThreads) k_pr_start(const PrObj *__res
 // start[0, m0) at row r0 (states at r0, their sorted edge index in Next; the
 // row's insertion and expiry done); its spans from row re >= r0 on (the rows
 // before: a warm-up, walked and stepped but not emitted), from slot base +
-// emitted0.  re > r0: the list at re (its sorted edge indices) goes to
+// emitted0.  sidx: the list at re (its sorted edge indices) goes to
 // sidx[] / *s_m.  r1 < MaxY: the list after r1's insertion and expiry goes to
 // end[] / *end_m, and the return value says whether its edges are
 // cmp[0, mc) in order (cmp null: false).  Every thread returns the same.
@@ -2284,7 +2284,7 @@ __device__ bool walk_chunk(const FrameParams &fp, const ObjDesc &od, const ObjEd
             }
         }
         if (Row >= r1) break;
-        if (Row == re && re > r0) {  // the list where the spans begin
+        if (Row == re && sidx) {  // the list where the spans begin
             for (int q = tid; q < m; q += (int)NT) sidx[q] = (uint32_t)S.st[S.idx[q]].Next;
             if (tid == 0) *s_m = (uint32_t)m;
         }
@@ -2384,7 +2384,7 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_pr_chunk(FrameParams fp, co
                                                             uint32_t *__restrict__ s_m,
                                                             const uint32_t *__restrict__ prstat, PairRaw *__restrict__ raw,
                                                             SpanPos *__restrict__ pos, uint32_t *__restrict__ span_tri,
-                                                            uint32_t *__restrict__ err) {
+                                                            uint32_t *__restrict__ err, uint32_t warmup) {
     extern __shared__ int32_t lds_list[];
     __shared__ BlockRed R;
     const uint32_t pi = grp[blockIdx.y];
@@ -2397,7 +2397,7 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_pr_chunk(FrameParams fp, co
     const ObjEdge *E = work + e0;
     const PrRow pr = prrow[pi];
     const int32_t re = pr.first_row + (int32_t)(j * kPrChunk), r1 = min(re + kPrChunk, pr.max_y);
-    const uint32_t js = j ? j - 1 : 0;  // the chunk whose first row it starts from
+    const uint32_t js = j && warmup ? j - 1 : j;  // the chunk whose first row it starts from
     const int32_t r0 = pr.first_row + (int32_t)(js * kPrChunk);
     const uint32_t jr0 = js * kPrChunk, jre = j * kPrChunk;
     const int32_t RowLo = fp.draws[od.draw].mode != MODE_AVX ? fp.row0 - 1 : fp.row0;
@@ -2785,7 +2785,7 @@ hipError_t prk_pr_walk_group(const prk::FrameParams *fp, const prk::PrWalkArgs *
     case MM:                                                                                                         \
         hipLaunchKernelGGL(prk::k_pr_chunk<MM>, dim3(max_chunks, ngroup), dim3(nt), bytes, s, *fp, O, P, grp, cap,  \
                            PR, a->cnt, a->eoff, a->fge, a->escan, a->total0p, W, a->soff, SST, EE, a->eend_m,       \
-                           a->sidx, a->s_m, a->prstat, RAW, POS, a->span_tri, a->err);                               \
+                           a->sidx, a->s_m, a->prstat, RAW, POS, a->span_tri, a->err, a->warmup);                    \
         if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;                                          \
         hipLaunchKernelGGL(prk::k_pr_cmp, dim3(a->nchunks), dim3(256), 0, s, P, a->npr, a->prstat, EE, a->eend_m,    \
                            a->sidx, a->s_m, a->match);                                                               \

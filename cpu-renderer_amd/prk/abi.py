@@ -62,7 +62,8 @@ class PrkStats(C.Structure):
                 ("frames_timed", C.c_uint32), ("ms_bin", C.c_float), ("ms_raster", C.c_float),
                 ("sum_ms_bin", C.c_double), ("sum_ms_raster", C.c_double),
                 ("anomalies", C.c_uint32), ("slow_replays", C.c_uint32), ("sum_ms_vis", C.c_double), ("sum_ms_span", C.c_double),
-                ("objects_chunked", C.c_uint32), ("objects_walked", C.c_uint32)]
+                ("objects_chunked", C.c_uint32), ("objects_walked", C.c_uint32),
+                ("object_chunks", C.c_uint32), ("object_chunks_rewalked", C.c_uint32)]
 
 
 def make_transform(D, F, M2P, cx, cy):

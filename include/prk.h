@@ -144,6 +144,9 @@ typedef struct prk_stats {
     uint32_t objects_walked;  /* large objects walked row after row from the
                                  first (an odd row, a NaN key, lists past the
                                  LDS); cumulative */
+    uint32_t object_chunks;   /* the chunked walk's chunks; cumulative */
+    uint32_t object_chunks_rewalked; /* ... walked a second time (their start
+                                 was not the true list); cumulative */
 } prk_stats;
 
 typedef struct prk_context prk_context;

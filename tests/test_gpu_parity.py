@@ -721,6 +721,14 @@ def test_whole_object_chunked_walk(gpu, sem, monkeypatch):
     monkeypatch.delenv("PRK_OBJ_ROWS")
     for k in range(3):
         assert np.array_equal(c[k].view(np.uint32), cw[k].view(np.uint32)), k
+    # without the warm-up most chunks start from a list that is not the true
+    # one: the check catches them and k_pr_fix walks them again
+    monkeypatch.setenv("PRK_OBJ_CHUNK_WARMUP", "0")
+    cf = prk.render_scene(inner, semantics=sem, phong=True, tris_per_object=700)
+    monkeypatch.delenv("PRK_OBJ_CHUNK_WARMUP")
+    assert cf[3]["object_chunks_rewalked"] > 0, cf[3]
+    for k in range(3):
+        assert np.array_equal(cf[k].view(np.uint32), cw[k].view(np.uint32)), k
     # sphere strips (chunked) and soup objects crossing the top border (walked) in one pass
     V, Cc, N, UV = prk.construct_sphere()
     big = scenes.Scene(384, 256, np.concatenate([V[:3 * 64 * 20] * 0.6, soup.vertices[:3 * 64 * 10]]),
