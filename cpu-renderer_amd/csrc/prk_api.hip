@@ -59,13 +59,15 @@ hipError_t prk_objtri_emit(const prk::FrameParams *, const void *, const uint32_
                            hipStream_t);
 hipError_t prk_obj_sort(void *, uint32_t *, void *, uint32_t *, uint32_t, uint32_t, void *, size_t *, hipStream_t);
 hipError_t prk_obj_gather(const void *, const uint32_t *, const uint32_t *, const void *, const uint32_t *, uint32_t,
-                          void *, uint32_t, hipStream_t);
+                          void *, uint32_t, void *, hipStream_t);
 hipError_t prk_obj_bound(const prk::FrameParams *, const void *, uint32_t, const unsigned long long *, const void *,
                          unsigned long long *, hipStream_t);
 uint32_t prk_obj_walk_lcap(void);
 hipError_t prk_obj_walk(const prk::FrameParams *, const void *, uint32_t, const uint32_t *, const uint32_t *, void *,
                         const unsigned long long *, void *, void *, void *, uint32_t *, const void *, uint32_t *, int,
-                        hipStream_t);
+                        const void *, const uint32_t *, uint32_t, hipStream_t);
+hipError_t prk_obj_seg(const prk::FrameParams *, const void *, uint32_t, const uint32_t *, const uint32_t *,
+                       const void *, const unsigned long long *, uint32_t *, const uint32_t *, void *, hipStream_t);
 uint32_t prk_obj_link_cap(void);
 hipError_t prk_obj_maxact(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, const uint32_t *,
                           const uint32_t *, const void *, int32_t *, hipStream_t);
@@ -282,7 +284,8 @@ struct prk_context {
         DevBuf d_stage, d_edges, d_ord, d_temp, d_recs, d_pos, d_span_tri, d_scnt, d_soff, d_keys_a, d_vals_a,
             d_keys_b, d_vals_b, d_offs, d_nwin, d_wtag, d_srecs, d_work, d_ekeys, d_ekeys2, d_evals, d_ecnt, d_escan,
             d_rcnt, d_rscan, d_bound, d_oslot, d_pool, d_err, d_raw, d_most, d_cls, d_prrow, d_prcnt, d_preoff,
-            d_prfge, d_prccur, d_prkey, d_prest, d_prsst, d_preend, d_preendm, d_prmatch, d_prsidx, d_prsm, d_prstat;
+            d_prfge, d_prccur, d_prkey, d_prest, d_prsst, d_preend, d_preendm, d_prmatch, d_prsidx, d_prsm, d_prstat,
+            d_segcnt, d_segoff, d_segs, d_wy;
         // the pass's host tables, packed into pinned memory for one upload
         // (stage_ev: that upload, before the staging is rewritten)
         char *h_stage = nullptr;
@@ -480,7 +483,8 @@ int prk_destroy(prk_context *c) {
                         &S.d_escan, &S.d_rcnt, &S.d_rscan, &S.d_bound, &S.d_oslot, &S.d_pool, &S.d_err,
                         &S.d_raw, &S.d_most, &S.d_cls, &S.d_prrow, &S.d_prcnt, &S.d_preoff, &S.d_prfge,
                         &S.d_prccur, &S.d_prkey, &S.d_prest, &S.d_prsst, &S.d_preend, &S.d_preendm,
-                        &S.d_prmatch, &S.d_prsidx, &S.d_prsm, &S.d_prstat};
+                        &S.d_prmatch, &S.d_prsidx, &S.d_prsm, &S.d_prstat, &S.d_segcnt, &S.d_segoff,
+                        &S.d_segs, &S.d_wy};
         for (DevBuf *b : sb) b->release();
         if (S.h_rb) (void)hipHostFree(S.h_rb);
         if (S.stage_ev) {
@@ -1618,7 +1622,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     S.h_big_off.clear();
     S.h_big_cap.clear();
     S.h_k1src.clear();
-    uint64_t ntri = 0, nk1 = 0, pool = 0, maxn = 1;
+    uint64_t ntri = 0, nk1 = 0, pool = 0, maxn = 1, small_tris = 0;
     bool thread_links = false;  // a thread-walked triangle object small enough for LDS list links
     std::vector<uint32_t> bigm[prk::MODE_COUNT], bige[prk::MODE_COUNT];  // wave-walked objects by mode, their edges
     for (uint32_t di = 0; di < draws.size(); ++di) {
@@ -1641,6 +1645,8 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
                 if (wave) {
                     bigm[d.mode].push_back((uint32_t)S.h_objs.size());
                     bige[d.mode].push_back((uint32_t)edges);
+                } else {
+                    small_tris += n;
                 }
                 S.h_k0obj.push_back((uint32_t)S.h_objs.size());
                 S.h_k0tri0.push_back((uint32_t)ntri);
@@ -1776,7 +1782,18 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     // (read back with the slot total: they size its walk's workgroup).
     const uint32_t nwork = 3 * nt + (uint32_t)nk1;
     PRK_TRY(S.d_work.ensure(std::max<size_t>(nwork, 1) * 112));
-    PRK_TRY(prk_obj_gather(S.d_edges.p, ord, total0p, d_edges_in, d_k1src, (uint32_t)nk1, S.d_work.p, nwork, s));
+    // The small triangle objects' segments (prk_spans.hip k_obj_seg, below):
+    // a thread per stretch of rows with a non-empty list (PRK_OBJ_SEGMENTS=0:
+    // a thread per object).
+    const uint64_t max_segs = 3 * small_tris;
+    bool segmented = false;
+    {
+        const char *env = std::getenv("PRK_OBJ_SEGMENTS");
+        segmented = max_segs && max_segs < 0x7FFFFFFFull && !(env && env[0] == '0');
+    }
+    if (segmented) PRK_TRY(S.d_wy.ensure((size_t)std::max<uint64_t>(3 * nt, 1) * 8));
+    PRK_TRY(prk_obj_gather(S.d_edges.p, ord, total0p, d_edges_in, d_k1src, (uint32_t)nk1, S.d_work.p, nwork,
+                           segmented ? S.d_wy.p : nullptr, s));
     // per large object: most, rows, entries (12, k_obj_maxact) | big (4) |
     // off (8) | cap (4) | the chunked walk's table (32, prk_spans.hip PrObj)
     // and groups (4)
@@ -1985,9 +2002,26 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
         PRK_TRY(prk_pr_walk_end(&pa, s));
         d_prstat = (const uint32_t *)S.d_prstat.p;
     }
+    const void *d_segs = nullptr;  // (the segments)
+    const uint32_t *d_nseg = nullptr;
+    {
+        if (segmented) {
+            PRK_TRY(S.d_segcnt.ensure(((size_t)nobj + 1) * 4));
+            PRK_TRY(S.d_segoff.ensure(((size_t)nobj + 1) * 4));
+            PRK_TRY(S.d_segs.ensure((size_t)max_segs * 24));  // prk_spans.hip ObjSeg
+            uint32_t *segcnt = (uint32_t *)S.d_segcnt.p, *segoff = (uint32_t *)S.d_segoff.p;
+            PRK_TRY(prk_obj_seg(&fp, d_objs, nobj, escan, total0p, S.d_wy.p, oslot, segcnt, segoff, nullptr, s));
+            PRK_TRY(prk_scan_u32(segcnt, segoff, nobj + 1, nullptr, &tb, s));
+            PRK_TRY(temp(tb));
+            PRK_TRY(prk_scan_u32(segcnt, segoff, nobj + 1, S.d_temp.p, &tb, s));
+            PRK_TRY(prk_obj_seg(&fp, d_objs, nobj, escan, total0p, S.d_wy.p, oslot, segcnt, segoff, S.d_segs.p, s));
+            d_segs = S.d_segs.p;
+            d_nseg = segoff + nobj;
+        }
+    }
     PRK_TRY(prk_obj_walk(&fp, d_objs, nobj, escan, total0p, S.d_work.p, oslot, S.d_recs.p,
                          scalar ? S.d_srecs.p : nullptr, S.d_pos.p, (uint32_t *)S.d_span_tri.p, d_spans_in,
-                         (uint32_t *)S.d_err.p, thread_links ? 1 : 0, s));
+                         (uint32_t *)S.d_err.p, thread_links ? 1 : 0, d_segs, d_nseg, (uint32_t)max_segs, s));
     for (const Group &g : groups)
         PRK_TRY(prk_obj_walk_group(&fp, g.mode, g.lcap, d_objs, d_cbig + g.start, d_coff + g.start, d_ccap + g.start,
                                    g.count, (int32_t *)S.d_pool.p, escan, total0p, S.d_work.p, oslot, S.d_recs.p,

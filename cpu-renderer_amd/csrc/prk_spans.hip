@@ -466,13 +466,17 @@ __global__ void k_obj_bound(FrameParams fp, const ObjDesc *__restrict__ objs, ui
 // The walk's working copy of every object's edges: the triangle edges in
 // MergeSort order (work[i] = edges[ord[i]], i < total0), then the caller edge
 // lists (kind 1) as given.  Re-made before each walk pass (the walk steps it).
+// (wy, when given: the triangle edges' (YMin, YMax), for k_obj_seg)
 __global__ void k_obj_gather(const ObjEdge *__restrict__ edges, const uint32_t *__restrict__ ord,
                              const uint32_t *__restrict__ total0p, const EdgeIn *__restrict__ edges_in,
-                             const uint32_t *__restrict__ k1src, uint32_t nk1, ObjEdge *__restrict__ work) {
+                             const uint32_t *__restrict__ k1src, uint32_t nk1, ObjEdge *__restrict__ work,
+                             int2 *__restrict__ wy) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t total0 = *total0p;
     if (i < total0) {
-        work[i] = edges[ord[i]];
+        const ObjEdge e = edges[ord[i]];
+        work[i] = e;
+        if (wy) wy[i] = make_int2(e.YMin, e.YMax);
     } else if (i - total0 < nk1) {
         obj_edge_in(work[i], edges_in[k1src[i - total0]]);
     }
@@ -542,14 +546,19 @@ constexpr int kLinkThreads = 64;  // k_obj_walk's workgroup
 // 13 B per edge (YMax relative to the object's first row; YMin is read from
 // the working copy, only where the sorted insertion scan advances), so four
 // 64-thread workgroups fit a CU's LDS.
-struct LinkLds {
-    float x[kLinkCap * kLinkThreads], g[kLinkCap * kLinkThreads];
-    int16_t ymax[kLinkCap * kLinkThreads];
-    int16_t nxt[kLinkCap * kLinkThreads];
-    int8_t left[kLinkCap * kLinkThreads];
+// (CAP: edges per thread; k_obj_walk_seg's segments take a smaller mirror,
+// so more of its waves fit a CU)
+template <int CAP>
+struct LinkLdsT {
+    float x[CAP * kLinkThreads], g[CAP * kLinkThreads];
+    int16_t ymax[CAP * kLinkThreads];
+    int16_t nxt[CAP * kLinkThreads];
+    int8_t left[CAP * kLinkThreads];
 };
-struct LLinks {
-    LinkLds *L;
+using LinkLds = LinkLdsT<kLinkCap>;
+template <int CAP>
+struct LLinksT {
+    LinkLdsT<CAP> *L;
     const ObjEdge *E;
     int lane;
     int32_t row0;  // the object's first row: YMax - row0 in (0, 32767]
@@ -569,6 +578,7 @@ struct LLinks {
 #endif
     static constexpr bool kCache = PRK_OBJ_PAIR_CACHE;
 };
+using LLinks = LLinksT<kLinkCap>;
 
 // An edge record held in seven named float4 registers (ObjEdge's layout): a
 // loop-carried ObjEdge went to scratch.
@@ -812,11 +822,13 @@ __global__ void __launch_bounds__(kLinkThreads, 1) k_obj_walk(FrameParams fp, co
                                                  const unsigned long long *__restrict__ soff,
                                                  SpanRecG *__restrict__ recs, ScSpanRecG *__restrict__ srecs,
                                                  SpanPos *__restrict__ pos, uint32_t *__restrict__ span_tri,
-                                                 const SpanIn *__restrict__ spans_in, uint32_t *__restrict__ err) {
+                                                 const SpanIn *__restrict__ spans_in, uint32_t *__restrict__ err,
+                                                 uint32_t segmented) {
     const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
     if (o >= nobj) return;
     const ObjDesc od = objs[o];
     if (od.kind != 2 && (od.k1off & kObjWave)) return;  // k_obj_walk_wave's
+    if (od.kind == 0 && segmented) return;             // k_obj_walk_seg's
     const DrawRec &d = fp.draws[od.draw];
     const bool st = (d.flags & DRAW_ST) != 0;
     const uint32_t base = (uint32_t)soff[o], bound = (uint32_t)(soff[o + 1] - soff[o]);
@@ -865,6 +877,126 @@ __global__ void __launch_bounds__(kLinkThreads, 1) k_obj_walk(FrameParams fp, co
         PRK_WALK_OBJ(MODE_SC_PHONG)
         PRK_WALK_OBJ(MODE_SC_PHONG_TEX)
 #undef PRK_WALK_OBJ
+        default: break;
+    }
+}
+
+// Segments of the small triangle objects (k_obj_walk's thread walk): an
+// object's sorted edges split where the list runs empty -- before edge i when
+// every earlier edge has expired by i's first row (YMin[i] >= their YMax) --
+// and every segment walked by a thread of its own (k_obj_walk_seg), from an
+// empty list as the sequential walk is there: new edges inserted in one row
+// end up in their sorted order whatever expiring entries they scan past, so
+// the list after that row's expiry is the same.  The segments' spans keep
+// the walk's order: segment k takes the slots after segments 0..k-1's bounds
+// (half their edges' active rows, as k_obj_bound's), a slot a segment leaves
+// unused stays row -1.  Random scattered triangles grouped 16 at a time
+// (C3b as 16-triangle objects) make ~12 segments of a few edges per object.
+struct ObjSeg {
+    uint32_t o;      // object
+    uint32_t e0, n;  // its sorted edges [e0, e0 + n) (object-relative)
+    uint32_t base, bound;  // span slots
+    uint32_t pad;
+};
+// One thread per object: the segments' count (WRITE false; segcnt[nobj] = 0)
+// or descriptors (at segoff[o]), in object order.  (Ordering them by length
+// instead, so a wave's segments end together, made the walk slower.)
+template <bool WRITE>
+__global__ void k_obj_seg(FrameParams fp, const ObjDesc *__restrict__ objs, uint32_t nobj,
+                          const uint32_t *__restrict__ escan, const uint32_t *__restrict__ total0p,
+                          const int2 *__restrict__ wy, const unsigned long long *__restrict__ soff,
+                          uint32_t *__restrict__ segcnt, const uint32_t *__restrict__ segoff,
+                          ObjSeg *__restrict__ segs) {
+    const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o > nobj) return;
+    if (o == nobj) {
+        if (!WRITE) segcnt[o] = 0;
+        return;
+    }
+    const ObjDesc od = objs[o];
+    uint32_t k = 0;
+    if (od.kind == 0 && !(od.k1off & kObjWave)) {
+        uint32_t e0, n;
+        obj_range(od, escan, *total0p, e0, n);
+        const int2 *Y = wy + e0;
+        const DrawRec &d = fp.draws[od.draw];
+        const int32_t lo = draw_row_lo(fp, d), hi = draw_row_hi(fp);
+        uint32_t at = (uint32_t)soff[o], rows = 0, first = 0;
+        int32_t runmax = INT32_MIN;
+        for (uint32_t i = 0; i < n; ++i) {
+            const int2 yy = Y[i];
+            if (i > 0 && yy.x >= runmax) {  // the list is empty at YMin[i]: edges [first, i) are a segment
+                if (WRITE) segs[segoff[o] + k] = ObjSeg{o, first, i - first, at, rows / 2, 0u};
+                at += rows / 2;
+                rows = 0;
+                first = i;
+                ++k;
+            }
+            runmax = max(runmax, yy.y);
+            rows += (uint32_t)max(0, min(yy.y, hi) - max(yy.x, lo));
+        }
+        if (n) {
+            if (WRITE) segs[segoff[o] + k] = ObjSeg{o, first, n - first, at, rows / 2, 0u};
+            ++k;
+        }
+    }
+    if (!WRITE) segcnt[o] = k;
+}
+
+#ifndef PRK_SEG_LINK_CAP
+#define PRK_SEG_LINK_CAP 16
+#endif
+constexpr int kSegLinkCap = PRK_SEG_LINK_CAP;  // edges per segment with LDS links (k_obj_walk_seg)
+__global__ void __launch_bounds__(kLinkThreads) k_obj_walk_seg(FrameParams fp, const ObjDesc *__restrict__ objs,
+                                                  const ObjSeg *__restrict__ segs,
+                                                  const uint32_t *__restrict__ nsegp,
+                                                  const uint32_t *__restrict__ escan,
+                                                  const uint32_t *__restrict__ total0p, ObjEdge *__restrict__ work,
+                                                  SpanRecG *__restrict__ recs, ScSpanRecG *__restrict__ srecs,
+                                                  SpanPos *__restrict__ pos, uint32_t *__restrict__ span_tri,
+                                                  uint32_t *__restrict__ err) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= *nsegp) return;
+    const ObjSeg sg = segs[q];
+    const ObjDesc od = objs[sg.o];
+    const DrawRec &d = fp.draws[od.draw];
+    uint32_t e0, n0;
+    obj_range(od, escan, *total0p, e0, n0);
+    ObjEdge *E = work + e0 + sg.e0;
+    const uint32_t n = sg.n;
+    __shared__ LinkLdsT<kSegLinkCap> lds;
+    bool in_lds = n > 0 && n <= (uint32_t)kSegLinkCap;
+    const int32_t row0 = n ? E[0].YMin : 0;
+    if (in_lds) {
+        int32_t hi = row0;
+        for (uint32_t i = 0; i < n; ++i) hi = max(hi, E[i].YMax);
+        in_lds = hi - row0 <= 32767;
+    }
+    if (in_lds) {
+        const int lane = (int)threadIdx.x;
+        for (uint32_t i = 0; i < n; ++i) {
+            const int a = (int)i * kLinkThreads + lane;
+            lds.x[a] = E[i].X;
+            lds.g[a] = E[i].G;
+            lds.ymax[a] = (int16_t)(E[i].YMax - row0);
+            lds.left[a] = (int8_t)E[i].Left;
+        }
+    }
+    switch (d.mode) {
+#define PRK_WALK_SEG(MM)                                                                                     \
+    case MM:                                                                                                 \
+        if (in_lds)                                                                                          \
+            walk_object<MM>(fp, od, d, E, n, sg.base, sg.bound, recs, srecs, pos, span_tri, err,             \
+                            LLinksT<kSegLinkCap>{&lds, E, (int)threadIdx.x, row0});                          \
+        else                                                                                                 \
+            walk_object<MM>(fp, od, d, E, n, sg.base, sg.bound, recs, srecs, pos, span_tri, err, GLinks{E}); \
+        break;
+        PRK_WALK_SEG(MODE_AVX)
+        PRK_WALK_SEG(MODE_SC_GOURAUD)
+        PRK_WALK_SEG(MODE_SC_GOURAUD_TEX)
+        PRK_WALK_SEG(MODE_SC_PHONG)
+        PRK_WALK_SEG(MODE_SC_PHONG_TEX)
+#undef PRK_WALK_SEG
         default: break;
     }
 }
@@ -2613,13 +2745,14 @@ hipError_t prk_obj_sort(void *keys_in, uint32_t *vals_in, void *keys_out, uint32
     return rocprim::radix_sort_pairs(temp, *temp_bytes, ki, ko, vals_in, vals_out, n, 0, end_bit, s);
 }
 // The walk's working copy (n slots: total0 triangle edges, then nk1 caller edges).
+// (wy: null, or the triangle edges' (YMin, YMax) as int2, for prk_obj_seg)
 hipError_t prk_obj_gather(const void *edges, const uint32_t *ord, const uint32_t *total0p, const void *edges_in,
-                          const uint32_t *k1src, uint32_t nk1, void *work, uint32_t n, hipStream_t s) {
+                          const uint32_t *k1src, uint32_t nk1, void *work, uint32_t n, void *wy, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(prk::k_obj_gather, dim3((n + 255) / 256), dim3(256), 0, s,
                        reinterpret_cast<const prk::ObjEdge *>(edges), ord, total0p,
                        reinterpret_cast<const prk::EdgeIn *>(edges_in), k1src, nk1,
-                       reinterpret_cast<prk::ObjEdge *>(work));
+                       reinterpret_cast<prk::ObjEdge *>(work), reinterpret_cast<int2 *>(wy));
     return hipGetLastError();
 }
 // Span slots per object (nobj + 1 values, the last 0; exclusive-scanned by
@@ -2676,24 +2809,53 @@ uint32_t prk_obj_walk_lcap(void) {
     return (uint32_t)(c - 1);
 }
 // The object walk: a thread per small object or caller edge list ...
+// (segs: the small triangle objects' segments, prk_obj_seg, walked a thread
+// each; null: a thread per object)
 hipError_t prk_obj_walk(const prk::FrameParams *fp, const void *objs, uint32_t nobj, const uint32_t *escan,
                         const uint32_t *total0p, void *work, const unsigned long long *soff, void *recs, void *srecs,
                         void *pos, uint32_t *span_tri, const void *spans_in, uint32_t *err, int links,
-                        hipStream_t s) {
+                        const void *segs, const uint32_t *nsegp, uint32_t max_segs, hipStream_t s) {
     if (nobj == 0) return hipSuccess;
+    const uint32_t segmented = segs ? 1u : 0u;
+    if (segs && max_segs) {
+        hipLaunchKernelGGL(prk::k_obj_walk_seg, dim3((max_segs + prk::kLinkThreads - 1) / prk::kLinkThreads),
+                           dim3(prk::kLinkThreads), 0, s, *fp, reinterpret_cast<const prk::ObjDesc *>(objs),
+                           reinterpret_cast<const prk::ObjSeg *>(segs), nsegp, escan, total0p,
+                           reinterpret_cast<prk::ObjEdge *>(work), reinterpret_cast<prk::SpanRecG *>(recs),
+                           reinterpret_cast<prk::ScSpanRecG *>(srecs), reinterpret_cast<prk::SpanPos *>(pos), span_tri,
+                           err);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
 #define PRK_OBJ_WALK_LAUNCH(LK)                                                                                    \
     hipLaunchKernelGGL(prk::k_obj_walk<LK>, dim3((nobj + prk::kLinkThreads - 1) / prk::kLinkThreads),              \
                        dim3(prk::kLinkThreads), 0, s, *fp, reinterpret_cast<const prk::ObjDesc *>(objs), nobj, escan, \
                        total0p, reinterpret_cast<prk::ObjEdge *>(work), soff,                                      \
                        reinterpret_cast<prk::SpanRecG *>(recs), reinterpret_cast<prk::ScSpanRecG *>(srecs),        \
                        reinterpret_cast<prk::SpanPos *>(pos), span_tri,                                            \
-                       reinterpret_cast<const prk::SpanIn *>(spans_in), err)
+                       reinterpret_cast<const prk::SpanIn *>(spans_in), err, segmented)
     if (links && PRK_OBJ_LDS_LINKS) PRK_OBJ_WALK_LAUNCH(true);
     else PRK_OBJ_WALK_LAUNCH(false);
 #undef PRK_OBJ_WALK_LAUNCH
     return hipGetLastError();
 }
 uint32_t prk_obj_link_cap(void) { return (uint32_t)prk::kLinkCap; }
+// The small triangle objects' segments (k_obj_seg): counts (nobj + 1 values,
+// the last 0) when segs is null, else the descriptors at segoff[o].
+hipError_t prk_obj_seg(const prk::FrameParams *fp, const void *objs, uint32_t nobj, const uint32_t *escan,
+                       const uint32_t *total0p, const void *wy, const unsigned long long *soff, uint32_t *segcnt,
+                       const uint32_t *segoff, void *segs, hipStream_t s) {
+    const dim3 g((nobj + 1 + 255) / 256), b(256);
+    const prk::ObjDesc *O = reinterpret_cast<const prk::ObjDesc *>(objs);
+    const int2 *W = reinterpret_cast<const int2 *>(wy);
+    if (!segs)
+        hipLaunchKernelGGL(prk::k_obj_seg<false>, g, b, 0, s, *fp, O, nobj, escan, total0p, W, soff, segcnt, segoff,
+                           nullptr);
+    else
+        hipLaunchKernelGGL(prk::k_obj_seg<true>, g, b, 0, s, *fp, O, nobj, escan, total0p, W, soff, segcnt, segoff,
+                           reinterpret_cast<prk::ObjSeg *>(segs));
+    return hipGetLastError();
+}
 // ... the most active entries of the large ones (big[0, nbig)) ...
 // (most: 3 * nbig values, see k_obj_maxact)
 hipError_t prk_obj_maxact(const prk::FrameParams *fp, const void *objs, const uint32_t *big, uint32_t nbig,

@@ -744,6 +744,27 @@ def test_whole_object_chunked_walk(gpu, sem, monkeypatch):
 
 
 @pytest.mark.parametrize("sem", [abi.PRK_SEM_AVX, abi.PRK_SEM_AVX_ST, abi.PRK_SEM_SCALAR])
+@pytest.mark.parametrize("tpo", [3, 16, 40])
+def test_whole_object_segments(gpu, sem, tpo, monkeypatch):
+    """Small objects walked as segments (prk_spans.hip k_obj_seg): an
+    object's rows split where its list runs empty, each stretch walked by a
+    thread of its own from an empty list.  Scattered triangles (many
+    segments per object, some overlapping: crossings and ties inside a
+    segment), clipped on every side: the oracle's whole-object walk, and the
+    thread-per-object walk (PRK_OBJ_SEGMENTS=0), bit for bit."""
+    s = scenes.with_ties(scenes.random_soup(4000, 512, 384, radius=24, seed=tpo, centroid_margin=24), seed=tpo)
+    if sem == abi.PRK_SEM_SCALAR:
+        s.texture = None
+    g, _ = run_both(s, semantics=sem, phong=True, tris_per_object=tpo, threads=1,
+                    exact_color=sem != abi.PRK_SEM_SCALAR, label="segments tpo=%d sem=%d" % (tpo, sem))
+    monkeypatch.setenv("PRK_OBJ_SEGMENTS", "0")
+    w = prk.render_scene(s, semantics=sem, phong=True, tris_per_object=tpo)
+    monkeypatch.delenv("PRK_OBJ_SEGMENTS")
+    for k in range(3):
+        assert np.array_equal(g[k].view(np.uint32), w[k].view(np.uint32)), k
+
+
+@pytest.mark.parametrize("sem", [abi.PRK_SEM_AVX, abi.PRK_SEM_AVX_ST, abi.PRK_SEM_SCALAR])
 @pytest.mark.parametrize("tpo", [64, 700])
 def test_whole_object_wave_walk(gpu, sem, tpo):
     """Objects large enough for the one-wave walk (k_obj_walk_wave): random
