@@ -98,6 +98,23 @@ def load_valu(cfg_key, kernel, ms_frame=None):
         return None
 
 
+def load_valu_frame(cfg_key, ms_frame):
+    """The frame's issued-VALU time: the sum over every kernel of the round's
+    SQ counter passes (profiles/sq_valu.json, as load_valu) of its VALU time
+    estimate, and that sum's share of this run's ms_per_step -- how far the
+    frame as a whole is from its VALU-issue floor.  None without the file."""
+    p = os.path.join(ROOT, "profiles", "sq_valu.json")
+    try:
+        with open(p) as f:
+            e = json.load(f)[cfg_key]
+        per = {n: v.get("valu_time_estimate_ms") or 0.0 for n, v in e["per_kernel"].items()}
+        tot = sum(per.values())
+        return dict(valu_time_ms=tot, frac_of_frame=tot / ms_frame if ms_frame else None, kernels=len(per),
+                    source="profiles/sq_valu.json[%s] (%s)" % (cfg_key, e.get("round", "?")))
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def cpu_topology():
     """Host CPUs this process may run on, their physical cores and SMT, and
     the cgroup CPU quota (the box's share of the host)."""
@@ -448,7 +465,9 @@ def main():
                                              1e-9, serial["raster"] + serial["k_bin_phase"])},
                      # the binding resource of the dominant kernel: issued VALU
                      # (SQ counters of the committed round profile)
-                     "valu": load_valu(cfg_key, "k_vis", ms)},
+                     "valu": load_valu(cfg_key, "k_vis", ms),
+                     # every kernel's VALU time over the frame (SQ counters)
+                     "valu_frame": load_valu_frame(cfg_key, ms)},
     }
     if check is not None:
         out["check"] = check
