@@ -1,9 +1,9 @@
 #!/bin/bash
 # End-of-round measurement set (GPU box), every step under its own limit;
 # outputs under gpurun_out/final_$1 (copy what is judged into profiles/).
-# usage: tools/round_final.sh r04
+# usage: tools/round_final.sh r05
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 3
-tag=${1:-r04}
+tag=${1:-r05}
 o=gpurun_out/final_$tag
 mkdir -p $o
 exec tools/gpu_run.sh \
@@ -15,4 +15,5 @@ exec tools/gpu_run.sh \
   "200|final_wprof|PRK_LIB=cpu-renderer_amd/libprk_hip_wprof.so python3 tools/wprof.py sphere_1obj_avx c2_1obj_avx > $o/wprof.log 2>&1 && cat $o/wprof.log" \
   "300|final_dropin|examples/dropin_bench 5 > $o/dropin_bench.json 2>&1 && cat $o/dropin_bench.json" \
   "200|final_oprof|tools/oprof.sh sphere_1obj_avx 3 $o/oprof_sphere" \
+  "200|final_oprof16|tools/oprof.sh c3b_obj16_avx 3 $o/oprof_obj16" \
   "900|final_prof|tools/profile_round.sh $tag"
