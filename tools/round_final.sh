@@ -12,7 +12,6 @@ exec tools/gpu_run.sh \
   "300|final_band_c3b|python3 tools/time_band.py --scene c3b --json $o/band_c3b_final.json" \
   "300|final_band_c5|python3 tools/time_band.py --scene c5 --json $o/band_c5_final.json" \
   "300|final_objects|python3 tools/time_objects.py --json $o/objects_final.json" \
-  "200|final_wprof|PRK_LIB=cpu-renderer_amd/libprk_hip_wprof.so python3 tools/wprof.py sphere_1obj_avx c2_1obj_avx > $o/wprof.log 2>&1 && cat $o/wprof.log" \
   "300|final_dropin|examples/dropin_bench 5 > $o/dropin_bench.json 2>&1 && cat $o/dropin_bench.json" \
   "200|final_oprof|tools/oprof.sh sphere_1obj_avx 3 $o/oprof_sphere" \
   "200|final_oprof16|tools/oprof.sh c3b_obj16_avx 3 $o/oprof_obj16" \
