@@ -272,10 +272,8 @@ struct state {
     void *LastBitmapMemory = nullptr;
     int32_t LastTexture = -1;
 };
-inline state &S() {
-    static state s;
-    return s;
-}
+inline state g_state;  // (a namespace-scope inline variable: no guard check per call)
+inline state &S() { return g_state; }
 
 inline bool ok(int rc) {
     S().LastStatus = rc;
