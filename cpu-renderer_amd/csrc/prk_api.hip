@@ -55,8 +55,10 @@ hipError_t prk_selftest_div_launch(uint32_t n, uint64_t seed, unsigned long long
 hipError_t prk_objtri_count(const prk::FrameParams *, const void *, const uint32_t *, const uint32_t *, uint32_t,
                             uint32_t, uint32_t *, unsigned long long *, hipStream_t);
 hipError_t prk_objtri_emit(const prk::FrameParams *, const void *, const uint32_t *, const uint32_t *, uint32_t,
-                           uint32_t, const uint32_t *, uint32_t, uint32_t, int32_t, void *, void *, uint32_t *,
+                           uint32_t, const uint32_t *, uint32_t, uint32_t, int32_t, void *, void *, uint32_t *, int,
                            hipStream_t);
+hipError_t prk_obj_sort_local(const void *, const uint32_t *, uint32_t, const uint32_t *, const void *, const void *,
+                              void *, void *, uint32_t *, hipStream_t);
 hipError_t prk_obj_sort(void *, uint32_t *, void *, uint32_t *, uint32_t, uint32_t, void *, size_t *, hipStream_t);
 hipError_t prk_obj_gather(const void *, const uint32_t *, const uint32_t *, const void *, const uint32_t *, uint32_t,
                           void *, uint32_t, void *, hipStream_t);
@@ -87,8 +89,8 @@ hipError_t prk_span_finish(const prk::FrameParams *, const void *, uint32_t, voi
 hipError_t prk_scan_u32(const uint32_t *, uint32_t *, uint32_t, void *, size_t *, hipStream_t);
 hipError_t prk_scan_u64(const unsigned long long *, unsigned long long *, uint32_t, void *, size_t *, hipStream_t);
 hipError_t prk_span_count(const prk::FrameParams *, const void *, uint32_t, uint32_t *, hipStream_t);
-hipError_t prk_span_bin(const prk::FrameParams *, const void *, uint32_t, const uint32_t *, uint32_t, uint32_t *,
-                        uint32_t *, uint32_t *, uint32_t *, uint32_t *, void *, size_t *, hipStream_t);
+hipError_t prk_span_bin(const prk::FrameParams *, const void *, uint32_t, const uint32_t *, uint32_t *, uint32_t *,
+                        hipStream_t);
 hipError_t prk_launch_spans(const prk::FrameParams *, const uint32_t *, const uint32_t *, const void *,
                             const void *, const void *, uint32_t, const uint32_t *, uint32_t *, uint32_t *,
                             hipStream_t);
@@ -1742,6 +1744,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(S.d_evals.ensure(es * 4));
     PRK_TRY(S.d_ord.ensure(es * 4));
     PRK_TRY(S.d_err.ensure(16));
+    PRK_TRY(hipMemsetAsync(S.d_err.p, 0, 16, s));  // (error bits, then the chunked walk's tally)
     uint32_t *escan = (uint32_t *)S.d_escan.p, *ord = (uint32_t *)S.d_ord.p;
     unsigned long long *rscan = (unsigned long long *)S.d_rscan.p;
     const uint32_t *total0p = escan + nt;
@@ -1760,9 +1763,17 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(prk_scan_u64((const unsigned long long *)S.d_rcnt.p, rscan, nt + 1, nullptr, &tb, s));
     PRK_TRY(temp(tb));
     PRK_TRY(prk_scan_u64((const unsigned long long *)S.d_rcnt.p, rscan, nt + 1, S.d_temp.p, &tb, s));
-    PRK_TRY(prk_objtri_emit(&fp, d_objs, d_k0obj, d_k0tri0, nk0, nt,
-                            escan, pbits, ybits, c->H, S.d_edges.p, S.d_ekeys.p, (uint32_t *)S.d_evals.p, s));
-    if (nt) {  // MergeSort of every object (one radix sort of the padded keys, prk_spans.hip)
+    // MergeSort of every object: per object when none has more than 64
+    // edges (k_obj_sort_local, with the gather), else one radix sort of the
+    // padded keys (prk_spans.hip); PRK_OBJ_LOCAL_SORT=0 forces the radix sort
+    bool local_sort = nt && maxn <= 64;
+    {
+        const char *env = std::getenv("PRK_OBJ_LOCAL_SORT");
+        if (env && env[0] == '0') local_sort = false;
+    }
+    PRK_TRY(prk_objtri_emit(&fp, d_objs, d_k0obj, d_k0tri0, nk0, nt, escan, pbits, ybits, c->H, S.d_edges.p,
+                            S.d_ekeys.p, (uint32_t *)S.d_evals.p, local_sort ? 0 : 1, s));
+    if (nt && !local_sort) {
         const uint32_t end_bit = obits + ybits + pbits;
         PRK_TRY(prk_obj_sort(S.d_ekeys.p, (uint32_t *)S.d_evals.p, S.d_ekeys2.p, ord, 3 * nt, end_bit, nullptr, &tb,
                              s));
@@ -1792,8 +1803,12 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
         segmented = max_segs && max_segs < 0x7FFFFFFFull && !(env && env[0] == '0');
     }
     if (segmented) PRK_TRY(S.d_wy.ensure((size_t)std::max<uint64_t>(3 * nt, 1) * 8));
-    PRK_TRY(prk_obj_gather(S.d_edges.p, ord, total0p, d_edges_in, d_k1src, (uint32_t)nk1, S.d_work.p, nwork,
-                           segmented ? S.d_wy.p : nullptr, s));
+    if (local_sort)
+        PRK_TRY(prk_obj_sort_local(d_objs, d_k0obj, nk0, escan, S.d_ekeys.p, S.d_edges.p, S.d_work.p,
+                                   segmented ? S.d_wy.p : nullptr, (uint32_t *)S.d_err.p, s));
+    if (!local_sort || nk1)
+        PRK_TRY(prk_obj_gather(S.d_edges.p, local_sort ? nullptr : ord, total0p, d_edges_in, d_k1src, (uint32_t)nk1,
+                               S.d_work.p, nwork, segmented ? S.d_wy.p : nullptr, s));
     // per large object: most, rows, entries (12, k_obj_maxact) | big (4) |
     // off (8) | cap (4) | the chunked walk's table (32, prk_spans.hip PrObj)
     // and groups (4)
@@ -1812,7 +1827,6 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
         PRK_TRY(hipMemcpyAsync(h_most, S.d_most.p, (size_t)nbig_all * 12, hipMemcpyDeviceToHost, s));
     }
     PRK_TRY(hipMemcpyAsync(S.h_rb, oslot + nobj, 8, hipMemcpyDeviceToHost, s));
-    PRK_TRY(hipMemsetAsync(S.d_err.p, 0, 16, s));  // (error bits, then the chunked walk's tally)
     PRK_TRY(hipStreamSynchronize(s));
     uint64_t nslot64;
     std::memcpy(&nslot64, S.h_rb, 8);
@@ -2029,14 +2043,16 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
                                    (uint32_t *)S.d_err.p, d_prstat, s));
     if (nbig_all)  // the slot walks' pairs into span records
         PRK_TRY(prk_span_finish(&fp, S.d_raw.p, nslot, S.d_recs.p, scalar ? S.d_srecs.p : nullptr, S.d_pos.p, s));
-    PRK_TRY(S.d_scnt.ensure(((size_t)nslot + 1) * 4));
-    PRK_TRY(S.d_soff.ensure(((size_t)nslot + 1) * 4));
-    uint32_t *scnt = (uint32_t *)S.d_scnt.p, *soff = (uint32_t *)S.d_soff.p;
-    PRK_TRY(prk_span_count(&fp, S.d_pos.p, nslot, scnt, s));
-    PRK_TRY(prk_scan_u32(scnt, soff, nslot + 1, nullptr, &tb, s));
+    // span -> tile bin entries: the tiles' counts and their scan (the
+    // total comes back with the walk's status), then every span placed
+    PRK_TRY(S.d_scnt.ensure(((size_t)ntiles + 1) * 4));
+    PRK_TRY(S.d_offs.ensure(((size_t)ntiles + 1) * 4));
+    uint32_t *tcnt = (uint32_t *)S.d_scnt.p, *toff = (uint32_t *)S.d_offs.p;
+    PRK_TRY(prk_span_count(&fp, S.d_pos.p, nslot, tcnt, s));
+    PRK_TRY(prk_scan_u32(tcnt, toff, ntiles + 1, nullptr, &tb, s));
     PRK_TRY(temp(tb));
-    PRK_TRY(prk_scan_u32(scnt, soff, nslot + 1, S.d_temp.p, &tb, s));
-    PRK_TRY(hipMemcpyAsync(S.h_rb + 2, soff + nslot, 4, hipMemcpyDeviceToHost, s));
+    PRK_TRY(prk_scan_u32(tcnt, toff, ntiles + 1, S.d_temp.p, &tb, s));
+    PRK_TRY(hipMemcpyAsync(S.h_rb + 2, toff + ntiles, 4, hipMemcpyDeviceToHost, s));
     PRK_TRY(hipMemcpyAsync(S.h_rb + 3, S.d_err.p, 16, hipMemcpyDeviceToHost, s));
     PRK_TRY(hipStreamSynchronize(s));
     const uint32_t total = S.h_rb[2];
@@ -2051,19 +2067,8 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     c->stats.triangles = T;
     c->stats.tiles = ntiles;
     c->stats.bin_entries = total;
-    const size_t ne = std::max<uint32_t>(total, 1);
-    PRK_TRY(S.d_keys_a.ensure(ne * 4));
-    PRK_TRY(S.d_vals_a.ensure(ne * 4));
-    PRK_TRY(S.d_keys_b.ensure(ne * 4));
-    PRK_TRY(S.d_vals_b.ensure(ne * 4));
-    PRK_TRY(S.d_offs.ensure(((size_t)ntiles + 1) * 4));
-    size_t sb = 0;
-    PRK_TRY(prk_span_bin(&fp, S.d_pos.p, nslot, soff, total, (uint32_t *)S.d_keys_a.p, (uint32_t *)S.d_vals_a.p,
-                         (uint32_t *)S.d_keys_b.p, (uint32_t *)S.d_vals_b.p, (uint32_t *)S.d_offs.p, nullptr, &sb, s));
-    PRK_TRY(temp(sb));
-    PRK_TRY(prk_span_bin(&fp, S.d_pos.p, nslot, soff, total, (uint32_t *)S.d_keys_a.p, (uint32_t *)S.d_vals_a.p,
-                         (uint32_t *)S.d_keys_b.p, (uint32_t *)S.d_vals_b.p, (uint32_t *)S.d_offs.p, S.d_temp.p, &sb,
-                         s));
+    PRK_TRY(S.d_vals_b.ensure((size_t)std::max<uint32_t>(total, 1) * 4));
+    PRK_TRY(prk_span_bin(&fp, S.d_pos.p, nslot, toff, tcnt, (uint32_t *)S.d_vals_b.p, s));
     PRK_TRY(S.d_nwin.ensure((size_t)ntiles * 4));
     PRK_TRY(S.d_wtag.ensure((size_t)ntiles * c->tile_w * c->tile_h * 4));
     PRK_TRY(prk_launch_spans(&fp, (const uint32_t *)S.d_offs.p, (const uint32_t *)S.d_vals_b.p, S.d_pos.p,

@@ -27,8 +27,10 @@
 //                 each span in submission order (object, row, pair), its lane-
 //                 init record (FillLineOptimized SpanRec 1543-1835, or DrawModel
 //                 ScSpanRec 298-412) and its pixel range.
-//   k_span_count / k_span_emit   span -> (tile, span) bin entries; sorted by
-//                 tile with the radix sort of the triangle path.
+//   k_span_tiles  span -> tile bin entries: every tile's count (wave-
+//                 aggregated atomics), their scan, each span placed at its
+//                 tile's offset + arrival rank (no sort: the visibility max
+//                 does not depend on the order within a tile).
 //   k_span_vis (prk_kernels.hip)  per-tile visibility over the spans with
 //                 the 64-bit key max (tag = span index in submission order).
 //   k_pix (prk_kernels.hip, span records indexed by span)  shading.
@@ -474,6 +476,7 @@ __global__ void k_obj_gather(const ObjEdge *__restrict__ edges, const uint32_t *
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t total0 = *total0p;
     if (i < total0) {
+        if (!ord) return;  // (k_obj_sort_local placed them)
         const ObjEdge e = edges[ord[i]];
         work[i] = e;
         if (wy) wy[i] = make_int2(e.YMin, e.YMax);
@@ -627,6 +630,43 @@ __device__ __forceinline__ ObjEdge er_edge(float4 q0, float4 q1, float4 q2, floa
         w##3 = make_float4((e).N2, (e).NG0, (e).NG1, (e).NG2);                                         \
         w##5 = make_float4((e).C0, (e).C1, (e).C2, (e).C3);                                            \
     } while (0)  /* (q4, q6: row range, link, colour gradient — not stepped) */
+
+// MergeSort of objects of at most 64 edges without the device radix sort:
+// one wave per object, lane i ranks edge i's key (object, min(YMin, H),
+// recursion path: unique within the object) among the object's keys and
+// copies the edge to the working copy at that rank -- the order the sort +
+// k_obj_gather give (their cost on C3b as 16-triangle objects: 0.46 ms).
+constexpr int kLocalSortEdges = 64;
+__global__ void __launch_bounds__(256) k_obj_sort_local(const ObjDesc *__restrict__ objs,
+                                                        const uint32_t *__restrict__ k0obj, uint32_t nk0,
+                                                        const uint32_t *__restrict__ escan,
+                                                        const unsigned long long *__restrict__ keys,
+                                                        const ObjEdge *__restrict__ edges, ObjEdge *__restrict__ work,
+                                                        int2 *__restrict__ wy, uint32_t *__restrict__ err) {
+    const uint32_t j = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int lane = (int)(threadIdx.x & 63);
+    if (j >= nk0) return;
+    const ObjDesc od = objs[k0obj[j]];
+    const uint32_t ob = escan[od.tri0], n = escan[od.tri0 + od.tris] - ob;
+    if (n > (uint32_t)kLocalSortEdges) {  // (never: the host takes this path only for such objects)
+        if (lane == 0) atomicOr(err, 4u);
+        return;
+    }
+    const unsigned long long k = lane < (int)n ? keys[ob + lane] : ~0ull;
+    const uint32_t klo = (uint32_t)k, khi = (uint32_t)(k >> 32);
+    uint32_t rank = 0;
+    for (uint32_t q = 0; q < n; ++q) {
+        const uint32_t qlo = (uint32_t)__builtin_amdgcn_readlane((int)klo, (int)q);
+        const uint32_t qhi = (uint32_t)__builtin_amdgcn_readlane((int)khi, (int)q);
+        rank += (qhi < khi || (qhi == khi && qlo < klo)) ? 1u : 0u;
+    }
+    if (lane < (int)n) {
+        PRK_ER(w);
+        PRK_ER_LOAD(w, &edges[ob + lane]);
+        PRK_ER_STORE(&work[ob + rank], w);
+        if (wy) wy[ob + rank] = make_int2(__float_as_int(w4.x), __float_as_int(w4.y));
+    }
+}
 
 // The AET walk of one object by one thread (small objects, caller edge
 // lists): E = its n edges, sorted (kind 0) or as given (kind 1).  Its spans
@@ -2664,47 +2704,41 @@ __device__ __forceinline__ SpanTiles span_tiles(const FrameParams &fp, const Spa
     return t;
 }
 
-// Bin entries of every span.
-__global__ void k_span_count(FrameParams fp, const SpanPos *__restrict__ pos, uint32_t nspan,
-                             uint32_t *__restrict__ cnt) {
+// Span -> tile bin entries by counting, no sort: pass 0 (PLACE false)
+// counts every tile's entries into ctr, pass 1 puts span s at offs[tile] +
+// its arrival rank (ctr zeroed again: the tiles' cursors).  The lanes of a
+// wave that hit one tile take their ranks from one atomic (the spans of an
+// object's consecutive rows mostly share a tile).  Within a tile the entries
+// are in arrival order, not span order: k_span_vis keeps the 64-bit maximum
+// of (z, span index) per pixel and the shading tests the winner's tag, so
+// neither depends on it.
+template <bool PLACE>
+__global__ void k_span_tiles(FrameParams fp, const SpanPos *__restrict__ pos, uint32_t nspan,
+                             uint32_t *__restrict__ ctr, const uint32_t *__restrict__ offs,
+                             uint32_t *__restrict__ bins) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s > nspan) return;
-    if (s == nspan) {  // sentinel: the scan's last element is the total
-        cnt[s] = 0;
-        return;
+    const int lane = (int)(threadIdx.x & 63);
+    SpanTiles t{0, 1, 0, -1};
+    if (s < nspan) t = span_tiles(fp, pos[s]);
+    const int own = max(0, t.tx1 - t.tx0 + 1), cnt = own + (t.oty >= 0 ? 1 : 0);
+    const int kmax = wave_max_i32(cnt);
+    for (int k = 0; k < kmax; ++k) {
+        const bool act = k < cnt;
+        const uint32_t tile = !act ? 0u : (uint32_t)(k < own ? t.ty * fp.tiles_x + t.tx0 + k : t.oty * fp.tiles_x);
+        unsigned long long pending = __ballot(act);
+        uint32_t rank = 0;
+        while (pending) {  // one atomic per distinct tile of the wave
+            const int lead = (int)__builtin_ctzll(pending);
+            const uint32_t lt = (uint32_t)readlane_i((int32_t)tile, lead);
+            const unsigned long long m = __ballot(act && tile == lt) & pending;
+            uint32_t b = 0;
+            if (lane == lead) b = atomicAdd(&ctr[lt], (uint32_t)__popcll(m));
+            b = (uint32_t)readlane_i((int32_t)b, lead);
+            if ((m >> lane) & 1ull) rank = b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            pending &= ~m;
+        }
+        if (PLACE && act) bins[offs[tile] + rank] = s;
     }
-    const SpanTiles t = span_tiles(fp, pos[s]);
-    cnt[s] = (uint32_t)(max(0, t.tx1 - t.tx0 + 1) + (t.oty >= 0 ? 1 : 0));
-}
-
-__global__ void k_span_emit(FrameParams fp, const SpanPos *__restrict__ pos, uint32_t nspan,
-                            const uint32_t *__restrict__ off, uint32_t *__restrict__ keys,
-                            uint32_t *__restrict__ vals) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nspan) return;
-    const SpanTiles t = span_tiles(fp, pos[s]);
-    uint32_t o = off[s];
-    for (int tx = t.tx0; tx <= t.tx1; ++tx) {
-        keys[o] = (uint32_t)(t.ty * fp.tiles_x + tx);
-        vals[o] = s;
-        ++o;
-    }
-    if (t.oty >= 0) {
-        keys[o] = (uint32_t)(t.oty * fp.tiles_x);
-        vals[o] = s;
-    }
-}
-
-__global__ void k_span_tile_offsets(const uint32_t *__restrict__ keys, uint32_t total, uint32_t ntiles,
-                                    uint32_t *__restrict__ offs) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t > ntiles) return;
-    uint32_t lo = 0, hi = total;
-    while (lo < hi) {
-        const uint32_t mid = lo + ((hi - lo) >> 1);
-        if (keys[mid] < t) lo = mid + 1; else hi = mid;
-    }
-    offs[t] = lo;
 }
 
 }  // namespace prk
@@ -2725,10 +2759,12 @@ hipError_t prk_objtri_count(const prk::FrameParams *fp, const void *objs, const 
 hipError_t prk_objtri_emit(const prk::FrameParams *fp, const void *objs, const uint32_t *k0obj,
                            const uint32_t *k0tri0, uint32_t nk0, uint32_t ntri, const uint32_t *escan,
                            uint32_t pbits, uint32_t ybits, int32_t ycap, void *edges, void *keys, uint32_t *vals,
-                           hipStream_t s) {
+                           int pad, hipStream_t s) {
     if (ntri == 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(keys, 0xFF, (size_t)3 * ntri * 8, s);
-    if (e != hipSuccess) return e;
+    if (pad) {  // (the radix sort reads every slot; k_obj_sort_local only the visible edges')
+        const hipError_t e = hipMemsetAsync(keys, 0xFF, (size_t)3 * ntri * 8, s);
+        if (e != hipSuccess) return e;
+    }
     const prk::SortKeyBits kb{pbits, ybits, ycap};
     hipLaunchKernelGGL(prk::k_objtri_emit, dim3((ntri + 255) / 256), dim3(256), 0, s, *fp,
                        reinterpret_cast<const prk::ObjDesc *>(objs), k0obj, k0tri0, nk0, ntri, escan, kb,
@@ -2753,6 +2789,19 @@ hipError_t prk_obj_gather(const void *edges, const uint32_t *ord, const uint32_t
                        reinterpret_cast<const prk::ObjEdge *>(edges), ord, total0p,
                        reinterpret_cast<const prk::EdgeIn *>(edges_in), k1src, nk1,
                        reinterpret_cast<prk::ObjEdge *>(work), reinterpret_cast<int2 *>(wy));
+    return hipGetLastError();
+}
+
+// MergeSort + gather of objects of at most 64 edges (k_obj_sort_local).
+hipError_t prk_obj_sort_local(const void *objs, const uint32_t *k0obj, uint32_t nk0, const uint32_t *escan,
+                              const void *keys, const void *edges, void *work, void *wy, uint32_t *err,
+                              hipStream_t s) {
+    if (nk0 == 0) return hipSuccess;
+    hipLaunchKernelGGL(prk::k_obj_sort_local, dim3((nk0 + 3) / 4), dim3(256), 0, s,
+                       reinterpret_cast<const prk::ObjDesc *>(objs), k0obj, nk0, escan,
+                       reinterpret_cast<const unsigned long long *>(keys),
+                       reinterpret_cast<const prk::ObjEdge *>(edges), reinterpret_cast<prk::ObjEdge *>(work),
+                       reinterpret_cast<int2 *>(wy), err);
     return hipGetLastError();
 }
 // Span slots per object (nobj + 1 values, the last 0; exclusive-scanned by
@@ -2997,35 +3046,27 @@ hipError_t prk_scan_u32(const uint32_t *in, uint32_t *out, uint32_t n, void *tem
     return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, in, out, n, s);
 }
 
-hipError_t prk_span_count(const prk::FrameParams *fp, const void *pos, uint32_t nspan, uint32_t *cnt,
+// Span -> tile bin entries, pass 0: tcnt[t] = tile t's entries (ntiles + 1
+// values, the last 0: the scan's total).
+hipError_t prk_span_count(const prk::FrameParams *fp, const void *pos, uint32_t nspan, uint32_t *tcnt,
                           hipStream_t s) {
-    hipLaunchKernelGGL(prk::k_span_count, dim3((nspan + 1 + 255) / 256), dim3(256), 0, s, *fp,
-                       reinterpret_cast<const prk::SpanPos *>(pos), nspan, cnt);
+    const uint32_t ntiles = (uint32_t)(fp->tiles_x * fp->tiles_y);
+    hipError_t e = hipMemsetAsync(tcnt, 0, ((size_t)ntiles + 1) * 4, s);
+    if (e != hipSuccess || nspan == 0) return e;
+    hipLaunchKernelGGL(prk::k_span_tiles<false>, dim3((nspan + 255) / 256), dim3(256), 0, s, *fp,
+                       reinterpret_cast<const prk::SpanPos *>(pos), nspan, tcnt, nullptr, nullptr);
     return hipGetLastError();
 }
 
-// Emit, sort by tile (stable, span order kept) and tile offsets.
-hipError_t prk_span_bin(const prk::FrameParams *fp, const void *pos, uint32_t nspan, const uint32_t *off,
-                        uint32_t total, uint32_t *keys_a, uint32_t *vals_a, uint32_t *keys_b, uint32_t *vals_b,
-                        uint32_t *offs, void *temp, size_t *temp_bytes, hipStream_t s) {
+// Pass 1: bins[offs[t] ...] = the spans of tile t (offs: the counts'
+// exclusive scan; tcur: ntiles cursors, zeroed here).
+hipError_t prk_span_bin(const prk::FrameParams *fp, const void *pos, uint32_t nspan, const uint32_t *offs,
+                        uint32_t *tcur, uint32_t *bins, hipStream_t s) {
     const uint32_t ntiles = (uint32_t)(fp->tiles_x * fp->tiles_y);
-    int bits = 1;
-    while ((1u << bits) < ntiles + 1 && bits < 32) ++bits;
-    if (!temp)
-        return rocprim::radix_sort_pairs(nullptr, *temp_bytes, keys_a, keys_b, vals_a, vals_b, total, 0,
-                                         (unsigned)bits, s);
-    if (nspan)
-        hipLaunchKernelGGL(prk::k_span_emit, dim3((nspan + 255) / 256), dim3(256), 0, s, *fp,
-                           reinterpret_cast<const prk::SpanPos *>(pos), nspan, off, keys_a, vals_a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    if (total) {
-        e = rocprim::radix_sort_pairs(temp, *temp_bytes, keys_a, keys_b, vals_a, vals_b, total, 0, (unsigned)bits,
-                                      s);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(prk::k_span_tile_offsets, dim3((ntiles + 1 + 255) / 256), dim3(256), 0, s, keys_b, total,
-                       ntiles, offs);
+    hipError_t e = hipMemsetAsync(tcur, 0, (size_t)ntiles * 4, s);
+    if (e != hipSuccess || nspan == 0) return e;
+    hipLaunchKernelGGL(prk::k_span_tiles<true>, dim3((nspan + 255) / 256), dim3(256), 0, s, *fp,
+                       reinterpret_cast<const prk::SpanPos *>(pos), nspan, tcur, offs, bins);
     return hipGetLastError();
 }
 

@@ -613,6 +613,36 @@ def test_draw_caller_edge_list(gpu, sem):
     compare(_render_src(s, "edges", words, sem), O.render_edges(s, words, semantics=sem), label="edges")
 
 
+@pytest.mark.parametrize("local", ["1", "0"])
+def test_small_objects_and_caller_edges_one_pass(gpu, local, monkeypatch):
+    """Small triangle objects and a caller edge list in one span pass: the
+    objects' edges sorted per object (k_obj_sort_local) or by the radix sort
+    (PRK_OBJ_LOCAL_SORT=0), the caller's list gathered after them; the
+    oracle draws the objects, then the list over them."""
+    monkeypatch.setenv("PRK_OBJ_LOCAL_SORT", local)
+    s = scenes.with_ties(scenes.random_soup(2400, 256, 256, radius=18, seed=44, centroid_margin=18), seed=44)
+    lst = scenes.random_soup(40, 256, 256, radius=50, seed=45, centroid_margin=40)
+    lst.transform, lst.lights, lst.ambient, lst.texture = s.transform, s.lights, s.ambient, s.texture
+    words = O.fill_edge_table_words(lst, 0, 40)
+    r = prk.Renderer()
+    try:
+        r.target_alloc(s.width, s.height)
+        r.clear()
+        r.set_camera(s.prk_transform(), s.prk_lights())
+        tex = r.texture(s.texture)
+        g = r.geometry(s.vertices, s.colors, s.normals, s.uvs)
+        r.draw(abi.PRK_SEM_AVX, g, s.tri_count, P=s.P, bitmap=tex, phong=True, tris_per_object=8)
+        r.draw_edges(words, semantics=abi.PRK_SEM_AVX, bitmap=tex, phong=True)
+        r.complete_all_work()
+        gc, gz = r.download()
+    finally:
+        r.close()
+    oc, oz, _, _ = O.render(s, tris_per_object=8)
+    oc, oz, _, _ = O.render_edges(lst, words, color=oc, z=oz)
+    assert np.array_equal(gz.view(np.uint32), oz.view(np.uint32))
+    assert np.array_equal(gc, oc)
+
+
 @pytest.mark.parametrize("sem", [abi.PRK_SEM_AVX, abi.PRK_SEM_AVX_ST])
 def test_draw_caller_spans(gpu, sem):
     """Caller-built spans (DoLineRenderWork / DoBufferLineRenderWork work
@@ -758,6 +788,27 @@ def test_whole_object_segments(gpu, sem, tpo, monkeypatch):
     monkeypatch.setenv("PRK_OBJ_SEGMENTS", "0")
     w = prk.render_scene(s, semantics=sem, phong=True, tris_per_object=tpo)
     monkeypatch.delenv("PRK_OBJ_SEGMENTS")
+    for k in range(3):
+        assert np.array_equal(g[k].view(np.uint32), w[k].view(np.uint32)), k
+
+
+@pytest.mark.parametrize("sem", [abi.PRK_SEM_AVX, abi.PRK_SEM_SCALAR])
+@pytest.mark.parametrize("tpo", [2, 16, 21])
+def test_whole_object_local_sort(gpu, sem, tpo, monkeypatch):
+    """Passes whose objects have at most 64 edges sort each object's edges in
+    one wave (prk_spans.hip k_obj_sort_local: rank of the MergeSort key) in
+    place of the device radix sort + gather: equal YMin everywhere (ties in
+    MergeSort's recursion order), 21 triangles = 63 edges at the limit; the
+    oracle, and the radix sort (PRK_OBJ_LOCAL_SORT=0), bit for bit."""
+    s = scenes.with_ties(scenes.random_soup(3000, 384, 256, radius=20, seed=70 + tpo, centroid_margin=20),
+                         seed=tpo)
+    if sem == abi.PRK_SEM_SCALAR:
+        s.texture = None
+    g, _ = run_both(s, semantics=sem, phong=True, tris_per_object=tpo, threads=1,
+                    label="local sort tpo=%d sem=%d" % (tpo, sem))
+    monkeypatch.setenv("PRK_OBJ_LOCAL_SORT", "0")
+    w = prk.render_scene(s, semantics=sem, phong=True, tris_per_object=tpo)
+    monkeypatch.delenv("PRK_OBJ_LOCAL_SORT")
     for k in range(3):
         assert np.array_equal(g[k].view(np.uint32), w[k].view(np.uint32)), k
 
