@@ -226,6 +226,14 @@ struct prk_context {
     hipStream_t bin_stream = nullptr;
     hipStream_t vis_stream = nullptr;  // k_vis of span-record frames
     DevBuf d_winners, d_anomaly, d_prof;
+    // z early: the last flush was a span-record pass, whose k_vis writes the
+    // final z (k_pix only the colour): a download takes z from the event after
+    // k_vis (ev[z_slot][3]) while the frame shades.  d_negz counts the -0.0
+    // z k_pix wrote over k_vis's +0.0 since the last download.
+    DevBuf d_negz;
+    bool early_z = false;  // prk_set_early_z
+    bool z_early = false;
+    int z_slot = -1;
     hipEvent_t s_mark = nullptr;  // flush-stream point the bin stream waits for (prior target contents)
     uint32_t *h_total = nullptr;  // pinned
     uint32_t pair_hint = 0;       // entry count of the last frame (counting-sort capacity)
@@ -475,7 +483,7 @@ int prk_destroy(prk_context *c) {
         if (B.counted_ev) (void)hipEventDestroy(B.counted_ev);
         if (B.h_info) (void)hipHostFree(B.h_info);
     }
-    DevBuf *bufs[] = {&c->d_winners, &c->d_anomaly, &c->d_prof};
+    DevBuf *bufs[] = {&c->d_winners, &c->d_anomaly, &c->d_prof, &c->d_negz};
     for (DevBuf *b : bufs) b->release();
     {
         auto &S = c->spans;
@@ -512,6 +520,7 @@ int prk_destroy(prk_context *c) {
 }
 
 static void drop_target(prk_context *c) {
+    c->z_early = false;
     if (c->owns_target) {
         (void)hipFree(c->color);
         (void)hipFree(c->zbuf);
@@ -586,6 +595,7 @@ __global__ void k_fill_target(uint32_t *color, int32_t pitch, float *z, int32_t 
 int prk_target_clear(prk_context *c, uint32_t color, float z) {
     if (!c) return PRK_ERR_ARG;
     RESOLVE_COUNT(c);
+    c->z_early = false;  // (z written outside a frame)
     if (!c->color) return PRK_ERR_NO_TARGET;
     PRK_TRY(hipSetDevice(c->device));
     // after a prk_target_upload_async still in flight (it would land on top)
@@ -611,19 +621,38 @@ int prk_target_download(prk_context *c, uint32_t *color_host, int32_t host_pitch
     RESOLVE_COUNT(c);
     if (!c->color) return PRK_ERR_NO_TARGET;
     PRK_TRY(hipSetDevice(c->device));
+    int rows = c->row1 - c->row0;
+    const size_t zbytes = (size_t)c->W * rows * 4;
+    // A span-record frame's z is final after its k_vis: it goes down while
+    // the frame shades (the copy engine holds the link while k_walk / k_pix
+    // run), the colour after the frame.
+    const bool early = z_host && c->z_early && c->z_slot >= 0 && c->d_negz.p;
+    if (early) {
+        PRK_TRY(hipStreamWaitEvent(c->copy_stream, c->ev[c->z_slot][3], 0));
+        PRK_TRY(hipMemcpyAsync(z_host, c->zbuf, zbytes, hipMemcpyDeviceToHost, c->copy_stream));
+    }
     PRK_TRY(hipStreamSynchronize(c->own_stream));
     PRK_TRY(hipDeviceSynchronize());
-    int rows = c->row1 - c->row0;
     if (color_host)
         PRK_TRY(hipMemcpy2D(color_host, host_pitch, c->color, c->pitch, (size_t)c->W * 4, rows,
                             hipMemcpyDeviceToHost));
-    if (z_host) PRK_TRY(hipMemcpy(z_host, c->zbuf, (size_t)c->W * rows * 4, hipMemcpyDeviceToHost));
+    if (early) {  // a -0.0 z written by k_pix after k_vis's +0.0: take z again
+        uint32_t negz = 0;
+        PRK_TRY(hipMemcpy(&negz, c->d_negz.p, 4, hipMemcpyDeviceToHost));
+        if (negz) {
+            PRK_TRY(hipMemcpy(z_host, c->zbuf, zbytes, hipMemcpyDeviceToHost));
+            PRK_TRY(hipMemset(c->d_negz.p, 0, 4));
+        }
+    } else if (z_host) {
+        PRK_TRY(hipMemcpy(z_host, c->zbuf, zbytes, hipMemcpyDeviceToHost));
+    }
     return PRK_OK;
 }
 
 int prk_target_upload(prk_context *c, const uint32_t *color_host, int32_t host_pitch, const float *z_host) {
     if (!c) return PRK_ERR_ARG;
     RESOLVE_COUNT(c);
+    c->z_early = false;  // (z written outside a frame)
     if (!c->color) return PRK_ERR_NO_TARGET;
     PRK_TRY(hipSetDevice(c->device));
     PRK_TRY(hipStreamSynchronize(c->own_stream));
@@ -639,6 +668,7 @@ int prk_target_upload(prk_context *c, const uint32_t *color_host, int32_t host_p
 int prk_target_upload_async(prk_context *c, const uint32_t *color_host, int32_t host_pitch, const float *z_host) {
     if (!c) return PRK_ERR_ARG;
     RESOLVE_COUNT(c);
+    c->z_early = false;  // (z written outside a frame)
     if (!c->color) return PRK_ERR_NO_TARGET;
     PRK_TRY(hipSetDevice(c->device));
     // after the frames already flushed (they read and write the target) and
@@ -1136,6 +1166,12 @@ int prk_set_tile(prk_context *c, int32_t tw, int32_t th) {
     return PRK_OK;
 }
 
+int prk_set_early_z(prk_context *c, int on) {
+    if (!c) return PRK_ERR_ARG;
+    c->early_z = on != 0;
+    return PRK_OK;
+}
+
 int prk_set_debug(prk_context *c, int32_t enable) {
     if (!c) return PRK_ERR_ARG;
     c->debug = enable != 0;
@@ -1238,6 +1274,8 @@ static void frame_params(const prk_context *c, prk::FrameParams &fp) {
     fp.tiles_x = (c->W + c->tile_w - 1) / c->tile_w;
     fp.tiles_y = (c->row1 - c->row0 + c->tile_h - 1) / c->tile_h;
     fp.prof = (unsigned long long *)c->d_prof.p;
+    fp.negz = (uint32_t *)c->d_negz.p;
+    fp.z_in_vis = c->early_z && c->d_negz.p ? 1 : 0;
     fp.winners = c->debug ? (int32_t *)c->d_winners.p : nullptr;
     fp.clear_color = c->clear_color;
     fp.clear_z = c->clear_z;
@@ -1245,6 +1283,7 @@ static void frame_params(const prk_context *c, prk::FrameParams &fp) {
 
 // A pending clear that the pass cannot fuse into its kernels: fill first.
 static int fill_pending_clear(prk_context *c, hipStream_t s) {
+    c->z_early = false;
     if (!c->clear_pending) return PRK_OK;
     c->clear_pending = false;
     const size_t n = (size_t)c->W * (c->row1 - c->row0);
@@ -1505,6 +1544,9 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
                               s));
     PRK_TRY(hipEventRecord(c->ev[slot][2], s));
     PRK_TRY(hipEventRecord(B.free_ev, s));
+    // a span-record pass's z is final after k_vis (ev[slot][3], on the vis stream)
+    c->z_early = span_rec && sv != s && fp.z_in_vis;
+    c->z_slot = slot;
     B.used = true;
     c->pending[slot] = true;
     c->split_span[slot] = modeset == prk::MODE_AVX;
@@ -1579,6 +1621,7 @@ static int resolve_count(prk_context *c) {
     const std::vector<prk::DrawRec> draws = std::move(P.draws);
     const int rc = flush_tris(c, P.s, draws, P.T, P.win_base);
     c->read_rec = hipEventRecord(c->read_ev, P.s) == hipSuccess;  // (geometry writes wait for the re-run)
+    c->z_early = false;  // (a re-run: the download takes z after everything)
     c->color = sv.color; c->pitch = sv.pitch; c->zbuf = sv.zbuf;
     c->W = sv.W; c->H = sv.H; c->row0 = sv.row0; c->row1 = sv.row1;
     c->tile_w = sv.tile_w; c->tile_h = sv.tile_h;
@@ -1598,6 +1641,7 @@ static int resolve_count(prk_context *c) {
 // span slots, the bin entry count).
 static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::DrawRec> &draws, uint32_t T,
                        uint32_t win_base) {
+    c->z_early = false;  // (k_pix / k_span_shade write a span pass's z)
     prk::FrameParams fp;
     frame_params(c, fp);
     fp.tri_count = T;
@@ -2111,6 +2155,11 @@ int prk_flush(prk_context *c, void *stream) {
         PRK_TRY(c->d_prof.ensure(16 * sizeof(uint64_t)));
         PRK_TRY(hipMemsetAsync(c->d_prof.p, 0, 16 * sizeof(uint64_t), s));
     }
+    if (!c->d_negz.p) {
+        PRK_TRY(c->d_negz.ensure(4));
+        PRK_TRY(hipMemsetAsync(c->d_negz.p, 0, 4, s));
+    }
+    c->z_early = false;  // (the passes below say whether the frame's last one allows it)
     if (c->debug) {
         PRK_TRY(c->d_winners.ensure((size_t)c->W * (c->row1 - c->row0) * 4));
         PRK_TRY(hipMemsetAsync(c->d_winners.p, 0xFF, (size_t)c->W * (c->row1 - c->row0) * 4, s));

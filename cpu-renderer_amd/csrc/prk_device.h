@@ -148,6 +148,11 @@ struct FrameParams {
     uint32_t clear_color;
     float clear_z;
     unsigned long long *prof;  // 16 phase-cycle counters (PRK_PROF builds only write them)
+    // span-record frames with z_in_vis (prk_set_early_z): k_vis writes z, k_pix
+    // the colour (and a -0.0 z, which the visibility key stores as +0.0,
+    // counted in negz for the download); else k_pix writes both
+    int32_t z_in_vis;
+    uint32_t *negz;
     // tiling
     int32_t tile_w, tile_h, tiles_x, tiles_y;
     int32_t tile_w_log2;  // tile_w is a power of two
@@ -395,6 +400,10 @@ __device__ __forceinline__ uint32_t zkey(float z) {
     uint32_t b = __float_as_uint(z);
     if (z == 0.0f) b = 0u;
     return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+// The z of a key's high word (-0.0 comes back as +0.0: zkey merges them).
+__device__ __forceinline__ float zkey_z(uint32_t k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
 }
 
 // ---------------------------------------------------------------------------

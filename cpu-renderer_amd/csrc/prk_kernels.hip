@@ -179,6 +179,9 @@ __device__ __forceinline__ void put_winner(const FrameParams &fp, int32_t x, int
     fp.zbuf[row * fp.W + x] = z;
     reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(fp.color) + row * fp.pitch)[x] = col;
 }
+__device__ __forceinline__ void put_color(const FrameParams &fp, int32_t x, int32_t y, uint32_t col) {
+    reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(fp.color) + (size_t)(y - fp.row0) * fp.pitch)[x] = col;
+}
 
 // ----- span setup --------------------------------------------------------
 // FillLineOptimized span setup (projekt.cpp:1543-1835) for row Row; writes the
@@ -1050,7 +1053,7 @@ __device__ __forceinline__ TileCtx tile_ctx(const FrameParams &fp, int t) {
 // other modes' entries).  UNI: the frame is one draw (then MODESET is its mode).
 // Output per tile: the winning entry tag of every pixel (wtag, tile-major),
 // the list of bin entries that won at least one pixel and its length.
-template <int MODESET, bool UNI>
+template <int MODESET, bool UNI, bool ZV = false>  // ZV: write the z here, k_pix the colour (fp.z_in_vis)
 __global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
     k_vis(FrameParams fp, const uint32_t *__restrict__ offs, const uint2 *__restrict__ bins,
           uint8_t *__restrict__ won, uint32_t *__restrict__ list, uint32_t *__restrict__ nwin_out,
@@ -1059,6 +1062,7 @@ __global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
     // Span-record frames (all draws AVX): k_walk + k_pix shade from the
     // winner tags; k_vis marks the won (pair, row)s and triangles for them.
     constexpr bool kRec = MODESET == MODE_AVX && PRK_SPAN_RECORDS;
+    constexpr bool kZV = kRec && ZV;
     extern __shared__ unsigned long long lds[];
     const int ntile = fp.tiles_x * fp.tiles_y;
     const int t = blockIdx.x;
@@ -1066,6 +1070,13 @@ __global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
     const uint32_t b0 = offs[t], b1 = offs[t + 1];
     if (b0 == b1) {  // no triangle touches this tile: leave it untouched
         if (threadIdx.x == 0) nwin_out[t] = 0;
+        if (kZV && fp.clear_fused) {  // (the fused clear's z: k_pix writes its colour)
+            const TileCtx tc = tile_ctx(fp, t);
+            for (int p = threadIdx.x; p < fp.tile_w * fp.tile_h; p += blockDim.x) {
+                const int x = tc.x0 + (p & (fp.tile_w - 1)), y = tc.y0 + (p >> fp.tile_w_log2);
+                if (x < tc.x1 && y < tc.y1) fp.zbuf[(size_t)(y - fp.row0) * fp.W + x] = fp.clear_z;
+            }
+        }
         return;
     }
     const uint32_t n = b1 - b0;
@@ -1108,7 +1119,17 @@ __global__ void __launch_bounds__(64 * kVisWaves, PRK_VIS_MIN_WAVES)
         const uint32_t low = (uint32_t)tc.key[p];
         tags_out[p] = low;
         uint32_t j;  // the winning pair
-        if (!tag_pair(low, j)) continue;
+        const bool won_px = tag_pair(low, j);
+        if constexpr (kZV) {
+            // the pixel's final z (the winner's, from its key, or the fused
+            // clear's): k_pix writes only the colour, so z is done here and a
+            // download can take it while the frame shades
+            const int x = tc.x0 + (p & (fp.tile_w - 1)), y = tc.y0 + (p >> fp.tile_w_log2);
+            if (x < tc.x1 && y < tc.y1 && (won_px || fp.clear_fused))
+                fp.zbuf[(size_t)(y - fp.row0) * fp.W + x] =
+                    won_px ? zkey_z((uint32_t)(tc.key[p] >> 32)) : fp.clear_z;
+        }
+        if (!won_px) continue;
         if constexpr (kRec) {  // the winner's (pair, row) and triangle (benign same-value races)
             anyw = 1;
             won[(size_t)j * fp.tile_h + (p >> fp.tile_w_log2)] = 1;
@@ -1493,7 +1514,7 @@ __global__ void __launch_bounds__(kWonThreads) k_won_local(uint32_t n, const uin
 
 // k_pix: shade the won pixels of one tile from their span records (SPAN:
 // records indexed by span, the whole-object path; else by (pair, row in tile)).
-template <bool UNI, bool SPAN = false>
+template <bool UNI, bool SPAN = false, bool ZV = false>  // ZV: k_vis wrote the z (fp.z_in_vis)
 __global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__restrict__ nwin_in,
                                              const uint32_t *__restrict__ wtag, const SpanRec *__restrict__ recs) {
     // PRK_PIX_SPLIT workgroups per tile, each a contiguous share of its pixels
@@ -1512,7 +1533,10 @@ __global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__r
         const int32_t x = tc.x0 + (p & (fp.tile_w - 1)), Row = tc.y0 + ly;
         uint32_t j;  // the winning pair
         if (!tag_pair(tag, j)) {  // no fragment beat the prior z
-            if (fp.clear_fused && x < tc.x1 && Row < tc.y1) put_winner(fp, x, Row, fp.clear_z, fp.clear_color);
+            if (fp.clear_fused && x < tc.x1 && Row < tc.y1) {
+                if (!ZV) put_winner(fp, x, Row, fp.clear_z, fp.clear_color);
+                else put_color(fp, x, Row, fp.clear_color);  // (k_vis wrote the z)
+            }
             continue;
         }
         const float4 *q = reinterpret_cast<const float4 *>(recs + (SPAN ? (size_t)j : (size_t)j * fp.tile_h + ly));
@@ -1544,7 +1568,16 @@ __global__ void __launch_bounds__(256) k_pix(FrameParams fp, const uint32_t *__r
                 n0 = a; n1 = bb; n2 = c;
             }
         }
-        put_winner(fp, x, Row, z, shade_avx_texel(fp, tx, z, n0, n1, n2, x, i, Row));
+        const uint32_t col = shade_avx_texel(fp, tx, z, n0, n1, n2, x, i, Row);
+        if (!ZV) {
+            put_winner(fp, x, Row, z, col);
+        } else {  // k_vis wrote the z, as +0.0 for a -0.0
+            put_color(fp, x, Row, col);
+            if (__float_as_uint(z) == 0x80000000u) {
+                fp.zbuf[(size_t)(Row - fp.row0) * fp.W + x] = z;
+                if (fp.negz) atomicAdd(fp.negz, 1u);
+            }
+        }
     }
 }
 
@@ -1768,6 +1801,8 @@ __global__ void __launch_bounds__(64 * kShadeWaves, PRK_SHADE_MIN_WAVES)
 #define PRK_INST(MS, UNI)                                  \
     template __global__ void k_vis<MS, UNI>(PRK_VIS_ARGS); \
     template __global__ void k_shade<MS, UNI>(PRK_SHADE_ARGS);
+template __global__ void k_vis<MODE_AVX, false, true>(PRK_VIS_ARGS);
+template __global__ void k_vis<MODE_AVX, true, true>(PRK_VIS_ARGS);
 #define PRK_WALK_ARGS FrameParams, const uint32_t *, const uint32_t *, const uint32_t *, const TileRange *, \
                       const uint8_t *, SpanRec *, uint32_t *
 #define PRK_PIX_ARGS FrameParams, const uint32_t *, const uint32_t *, const SpanRec *
@@ -1776,6 +1811,8 @@ template __global__ void k_walk<true>(PRK_WALK_ARGS);
 template __global__ void k_pix<false>(PRK_PIX_ARGS);
 template __global__ void k_pix<true>(PRK_PIX_ARGS);
 template __global__ void k_pix<false, true>(PRK_PIX_ARGS);
+template __global__ void k_pix<false, false, true>(PRK_PIX_ARGS);
+template __global__ void k_pix<true, false, true>(PRK_PIX_ARGS);
 #define PRK_SPAN_SHADE_ARGS FrameParams, const uint32_t *, const uint32_t *, const SpanPosK *, const ScSpanRec *, \
                             const uint32_t *, const uint32_t *
 template __global__ void k_span_shade<-1>(PRK_SPAN_SHADE_ARGS);
@@ -1905,8 +1942,12 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
     }
 #define PRK_VIS(MS, UNI)                                                                                             \
     do {                                                                                                             \
-        hipLaunchKernelGGL((prk::k_vis<MS, UNI>), dim3(ntile), dim3(64 * prk::kVisWaves), lv, svis, *fp, offs, bins,  \
-                           won, list, nwin, wtag, pair_tri, trwon, anomaly);                                         \
+        if (MS == prk::MODE_AVX && fp->z_in_vis)                                                                   \
+            hipLaunchKernelGGL((prk::k_vis<MS, UNI, true>), dim3(ntile), dim3(64 * prk::kVisWaves), lv, svis, *fp,   \
+                               offs, bins, won, list, nwin, wtag, pair_tri, trwon, anomaly);                         \
+        else                                                                                                         \
+            hipLaunchKernelGGL((prk::k_vis<MS, UNI>), dim3(ntile), dim3(64 * prk::kVisWaves), lv, svis, *fp, offs,    \
+                               bins, won, list, nwin, wtag, pair_tri, trwon, anomaly);                               \
         if (mid) (void)hipEventRecord(mid, svis);                                                                    \
         if (svis != s) (void)hipStreamWaitEvent(s, mid, 0);                                                          \
     } while (0)
@@ -1930,7 +1971,11 @@ hipError_t prk_launch_raster(const prk::FrameParams *fp, int modeset, const uint
         }                                                                                                            \
         if (mid2) (void)hipEventRecord(mid2, sw);                                                                    \
         if (sw != s) (void)hipStreamWaitEvent(s, mid2, 0);                                                           \
-        hipLaunchKernelGGL((prk::k_pix<UNI>), dim3(ntile * PRK_PIX_SPLIT), dim3(256), 0, s, *fp, nwin, wtag, rp);   \
+        if (fp->z_in_vis)                                                                                            \
+            hipLaunchKernelGGL((prk::k_pix<UNI, false, true>), dim3(ntile * PRK_PIX_SPLIT), dim3(256), 0, s, *fp, nwin, \
+                               wtag, rp);                                                                            \
+        else                                                                                                         \
+            hipLaunchKernelGGL((prk::k_pix<UNI>), dim3(ntile * PRK_PIX_SPLIT), dim3(256), 0, s, *fp, nwin, wtag, rp); \
     } while (0)
     switch (modeset) {
         case prk::MODE_AVX:

@@ -87,6 +87,7 @@ _SIGS = {
     "prk_get_stats": (C.c_int, [C.c_void_p, C.POINTER(abi.PrkStats)]),
     "prk_timing_reset": (C.c_int, [C.c_void_p]),
     "prk_set_debug": (C.c_int, [C.c_void_p, C.c_int32]),
+    "prk_set_early_z": (C.c_int, [C.c_void_p, C.c_int]),
     "prk_download_winners": (C.c_int, [C.c_void_p, C.c_void_p]),
     "prk_debug_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32]),
     "prk_set_tile": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
@@ -460,6 +461,11 @@ class Renderer:
     def set_debug(self, on=True):
         _check("prk_set_debug", self._L.prk_set_debug(self._h, int(bool(on))))
 
+    def set_early_z(self, on=True):
+        """prk_set_early_z: span-record frames write z in the visibility
+        kernel, so download() copies it while the frame shades."""
+        _check("prk_set_early_z", self._L.prk_set_early_z(self._h, int(bool(on))))
+
     # ---- draws (the reference's entry points) -----------------------------
     def _draw(self, geom, first_tri, tri_count, P, semantics, phong, texture, tris_per_object=1, setup=None):
         Pc = (C.c_float * 3)(*(P or (0.0, 0.0, 0.0)))
@@ -545,13 +551,14 @@ class Renderer:
 
 def render_scene(scene, semantics=abi.PRK_SEM_AVX, phong=True, device=0, tile=None, debug=True,
                  color=None, z=None, rows=None, fused_clear=False, tris_per_object=1, setup=None,
-                 shade_camera=None):
+                 shade_camera=None, early_z=False):
     """Convenience: draw a whole scenes.Scene (per-triangle submission) and
     return (color, z, winners or None, stats).  fused_clear: upload
     color / z, then clear through prk_target_clear_on_flush (the frame must
     overwrite them).  setup: FillEdgeTable's own inputs (abi.PRK_SETUP_*) of
     every draw.  shade_camera: a scene whose transform / lights shade the
-    spans (set_shade_camera); `scene`'s set the draws up."""
+    spans (set_shade_camera); `scene`'s set the draws up.  early_z:
+    set_early_z (z written by the visibility kernel, copied early)."""
     r = Renderer(device)
     try:
         r0, r1 = (0, scene.height) if rows is None else rows
@@ -565,6 +572,8 @@ def render_scene(scene, semantics=abi.PRK_SEM_AVX, phong=True, device=0, tile=No
         if tile:
             r.set_tile(*tile)
         r.set_debug(debug)
+        if early_z:
+            r.set_early_z(True)
         r.set_camera(scene.prk_transform(), scene.prk_lights())
         if shade_camera is not None:
             r.set_shade_camera(shade_camera.prk_transform(), shade_camera.prk_lights())

@@ -200,6 +200,15 @@ int prk_target_clear_on_flush(prk_context *ctx, uint32_t color, float z);
 /* Copy the bound target to/from host memory (rows [row0,row1)). */
 int prk_target_download(prk_context *ctx, uint32_t *color_host, int32_t host_pitch_bytes,
                         float *z_host);
+/* Early z (off by default; the drop-in header turns it on): in frames shaded
+ * through span records (all-AVX semantics, per triangle) the visibility
+ * kernel writes the final z and the shading only the colour, so
+ * prk_target_download copies z while the frame still shades (C3b through
+ * projekt.h: 0.45 ms less per frame over PCIe).  It costs a frame that is not
+ * downloaded ~0.4 % (the z stores move to the frame's busiest kernel).  The
+ * result is the same bit for bit (a -0.0 z, which the visibility key holds
+ * as +0.0, is written by the shading and makes the download take z again). */
+int prk_set_early_z(prk_context *ctx, int on);
 int prk_target_upload(prk_context *ctx, const uint32_t *color_host, int32_t host_pitch_bytes,
                       const float *z_host);
 /* prk_target_upload on the context's copy stream: returns at once; the next

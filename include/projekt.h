@@ -750,6 +750,7 @@ inline int PRK_InitDevices(const int *devices, int n) {
             st.Ctxs.clear();
             return st.LastStatus;
         }
+        (void)prk_set_early_z(c, 1);  // every frame is downloaded (PRK_CompleteAllWork): z goes down while it shades
         st.Ctxs.push_back(c);
     }
     st.Ctx = st.Ctxs[0];

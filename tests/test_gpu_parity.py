@@ -180,6 +180,45 @@ def test_fused_clear(gpu, W, H, tile):
     compare(g, O.render(s), label="fused clear %dx%d" % (W, H))
 
 
+@pytest.mark.parametrize("case", ["clear", "fused", "prior", "band", "st", "negzero", "scalar"])
+def test_early_z(gpu, case):
+    """prk_set_early_z: span-record frames write z in k_vis (from the winner's
+    key, or the fused clear's z) and k_pix only the colour; the download
+    takes z from the event after k_vis.  Plain, fused-clear, prior-contents,
+    row-band and single-thread frames, a scalar frame (not a span-record
+    frame: the plain path), and flat triangles at z = -0.0 (every fragment
+    ties at zero; the interpolation yields +0.0 there -- -0.0 + o * +0.0 with
+    o >= 0 -- so the key's +0.0 is the z; k_pix's -0.0 fix-up stays a
+    guard): the oracle and the default path, bit for bit."""
+    s = scenes.random_soup(5000, 256, 192, radius=18, seed=60, centroid_margin=20)
+    kw, okw = {}, {}
+    sem = abi.PRK_SEM_AVX
+    if case == "fused" or case == "prior":
+        rng = np.random.default_rng(6)
+        c0 = rng.integers(0, 2**32, (192, 256), dtype=np.uint32)
+        z0 = rng.uniform(-2.0, 2.0, (192, 256)).astype(np.float32)
+        kw = dict(color=c0, z=z0, fused_clear=case == "fused")
+        okw = {} if case == "fused" else dict(color=c0, z=z0)
+    elif case == "band":
+        kw = dict(rows=(40, 131))
+    elif case == "st":
+        sem = abi.PRK_SEM_AVX_ST
+    elif case == "negzero":
+        s.vertices[:, 2] = np.float32(-0.0)
+    elif case == "scalar":
+        sem = abi.PRK_SEM_SCALAR
+    o = O.render(s, semantics=sem, **okw)
+    e = prk.render_scene(s, semantics=sem, early_z=True, **kw)
+    d = prk.render_scene(s, semantics=sem, **kw)
+    if case == "band":
+        o = tuple(x[40:131] if x is not None and getattr(x, "ndim", 0) == 2 else x for x in o)
+    compare(e, o, label="early z " + case)
+    for k in range(3):
+        assert np.array_equal(e[k].view(np.uint32), d[k].view(np.uint32)), (case, k)
+    if case == "negzero":
+        assert (o[1] == 0.0).sum() > 1000  # (the fragments did land at zero)
+
+
 def test_fused_clear_fallbacks(gpu):
     """Scalar frames and empty flushes fill first instead of fusing."""
     s = scenes.random_soup(2000, 256, 192, radius=16, seed=43, textured=False)

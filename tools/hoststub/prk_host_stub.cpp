@@ -71,6 +71,7 @@ int prk_host_register(prk_context *, void *, size_t) { return PRK_OK; }
 int prk_host_unregister(prk_context *, void *) { return PRK_OK; }
 int prk_reset_draws(prk_context *) { return PRK_OK; }
 int prk_set_camera(prk_context *, const prk_transform *, const prk_light_data *) { return PRK_OK; }
+int prk_set_early_z(prk_context *, int) { return PRK_OK; }
 int prk_set_shade_camera(prk_context *, const prk_transform *, const prk_light_data *) { return PRK_OK; }
 int prk_synchronize(prk_context *) { return PRK_OK; }
 int prk_target_alloc(prk_context *, int32_t, int32_t, int32_t, int32_t, void **, float **) { return PRK_OK; }
