@@ -372,7 +372,13 @@ int prk_runtime_check(void) {
                      "ships its own ROCm) BEFORE libprk_hip.so (INTEGRATION.md, 'One ROCm stack per process'); "
                      "the process will end at exit before their destructors run\n",
                      m.hip.size(), m.smi.size());
-        on_exit(exit_guard, nullptr);
+        // The guard ends the process before every exit handler registered
+        // earlier (profiler flushes, LSan, earlier libraries' static
+        // destructors): without it the duplicated librocm_smi64 destructors
+        // abort the process there anyway (SIGABRT, the same handlers lost).
+        // PRK_EXIT_GUARD=0 leaves the exit path alone (the host takes the abort).
+        const char *g = std::getenv("PRK_EXIT_GUARD");
+        if (!(g && g[0] == '0')) on_exit(exit_guard, nullptr);
     }
     return PRK_ERR_RUNTIME_MIX;
 }
@@ -1516,7 +1522,10 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
     // is done (so it overlaps the previous frame's k_walk / k_pix on the
     // flush stream, while the next frame bins on bin_stream) and shade on the
     // flush stream after it; k_vis waits for the flush stream only when it
-    // reads the target's prior z (no fused clear) or the debug winner map.
+    // reads the target's prior z (no fused clear), writes the debug winner
+    // map, or writes z itself (early z: the flush stream may still hold an
+    // earlier frame's z writers -- k_shade, k_pix, k_span_shade, a -0.0
+    // fix-up -- that must land before this frame's z).
     // Other frames run on the flush stream.
     if (!c->d_anomaly.p) {
         PRK_TRY(c->d_anomaly.ensure(8));  // [anomalies, slow replays]
@@ -1527,7 +1536,7 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
     if (span_rec) {
         sv = c->vis_stream;
         PRK_TRY(hipStreamWaitEvent(sv, B.binned_ev, 0));
-        if (!fuse || c->debug) {  // prior z / winner map: after the flush stream's work so far
+        if (!fuse || c->debug || fp.z_in_vis) {  // prior z / winner map / early z: after the flush stream's work so far
             PRK_TRY(hipEventRecord(c->s_mark, s));
             PRK_TRY(hipStreamWaitEvent(sv, c->s_mark, 0));
         }
@@ -2009,21 +2018,34 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     }
     const uint32_t *d_prstat = nullptr;
     if (npr) {
-        PRK_TRY(S.d_prstat.ensure((size_t)nobj * 4));
+        // The chunked walk is an optimisation: when its scratch (up to
+        // kPrMaxEntries * ~356 B) cannot be had, every object takes the
+        // workgroup walk instead (d_prstat stays null) -- never PRK_ERR_NOMEM.
+        hipError_t ae = S.d_prstat.ensure((size_t)nobj * 4);
+        if (ae == hipSuccess) ae = S.d_prrow.ensure((size_t)npr * 8);
+        if (ae == hipSuccess) ae = S.d_prcnt.ensure((size_t)pr_rows * 4);
+        if (ae == hipSuccess) ae = S.d_preoff.ensure((size_t)pr_rows * 4);
+        if (ae == hipSuccess) ae = S.d_prfge.ensure((size_t)pr_rows * 4);
+        if (ae == hipSuccess) ae = S.d_prccur.ensure((size_t)pr_chunks * 4);
+        if (ae == hipSuccess) ae = S.d_preendm.ensure((size_t)pr_chunks * 4);
+        if (ae == hipSuccess) ae = S.d_prmatch.ensure((size_t)pr_chunks * 4);
+        if (ae == hipSuccess) ae = S.d_prsm.ensure((size_t)pr_chunks * 4);
+        if (ae == hipSuccess) ae = S.d_prsidx.ensure(pr_ents * 4);
+        if (ae == hipSuccess) ae = S.d_prkey.ensure(pr_ents * 16);
+        if (ae == hipSuccess) ae = S.d_prest.ensure(pr_ents * 112);  // prk_spans.hip ObjEdge
+        if (ae == hipSuccess) ae = S.d_prsst.ensure(pr_ents * 112);
+        if (ae == hipSuccess) ae = S.d_preend.ensure(pr_ents * 112);
+        if (ae == hipErrorOutOfMemory) {
+            (void)hipGetLastError();
+            DevBuf *big[] = {&S.d_prsidx, &S.d_prkey, &S.d_prest, &S.d_prsst, &S.d_preend};
+            for (DevBuf *b : big) b->release();
+            npr = 0;
+        } else {
+            PRK_TRY(ae);
+        }
+    }
+    if (npr) {
         PRK_TRY(hipMemsetAsync(S.d_prstat.p, 0, (size_t)nobj * 4, s));
-        PRK_TRY(S.d_prrow.ensure((size_t)npr * 8));
-        PRK_TRY(S.d_prcnt.ensure((size_t)pr_rows * 4));
-        PRK_TRY(S.d_preoff.ensure((size_t)pr_rows * 4));
-        PRK_TRY(S.d_prfge.ensure((size_t)pr_rows * 4));
-        PRK_TRY(S.d_prccur.ensure((size_t)pr_chunks * 4));
-        PRK_TRY(S.d_preendm.ensure((size_t)pr_chunks * 4));
-        PRK_TRY(S.d_prmatch.ensure((size_t)pr_chunks * 4));
-        PRK_TRY(S.d_prsm.ensure((size_t)pr_chunks * 4));
-        PRK_TRY(S.d_prsidx.ensure(pr_ents * 4));
-        PRK_TRY(S.d_prkey.ensure(pr_ents * 16));
-        PRK_TRY(S.d_prest.ensure(pr_ents * 112));  // prk_spans.hip ObjEdge
-        PRK_TRY(S.d_prsst.ensure(pr_ents * 112));
-        PRK_TRY(S.d_preend.ensure(pr_ents * 112));
         prk::PrWalkArgs pa{};
         pa.objs = d_objs;
         pa.pro = d_cpr;

@@ -282,7 +282,10 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_band(FrameParams fp, uint
     constexpr int kV4 = kHalf * 9 / 4 / kCountThreads;  // float4 per thread per half
     static_assert(kHalf * 9 % (4 * kCountThreads) == 0 && kHalf * 9 * 4 <= (int)sizeof(stage), "LDS half");
     const uint32_t gt0 = fp.draw0.geom_tri0 + (g0 - fp.draw0.first_global);
+    // (gt0 % 4 == 0 makes the run's offset 16-B aligned; the base must be too:
+    // prk_geometry_wrap_device takes any 4-B aligned caller pointer)
     const bool coal = PRK_BAND_COALESCED && fp.ndraws == 1 && (gt0 & 3u) == 0 &&
+                      ((uintptr_t)fp.draw0.V & 15u) == 0 &&
                       g0 + (uint32_t)kRecRun <= fp.tri_count;  // (a whole run: no tail to mask)
     float pv[kIt][9];
     const DrawRec *pd[kIt];

@@ -161,8 +161,12 @@ typedef struct prk_context prk_context;
  * PRK_ERR_RUNTIME_MIX then, names the fix on stderr (load the framework
  * before libprk_hip.so), and guards the exit: an on_exit handler registered
  * after both copies' destructors flushes stdio and ends the process with its
- * own exit status before those destructors run.  prk_destroy and
- * prk_comm_init run the same check (and install the same guard). */
+ * own exit status before those destructors run.  The guard skips every
+ * exit handler registered before it (atexit/on_exit work, earlier libraries'
+ * static destructors) -- work the double-free abort would skip as well;
+ * PRK_EXIT_GUARD=0 in the environment leaves the exit path untouched.
+ * prk_destroy and prk_comm_init run the same check (and install the same
+ * guard). */
 int prk_create(int device, prk_context **out);
 /* prk_destroy queues no GPU work: it waits for the context's streams and frees
  * what the context owns.  A frame whose bin count is still unresolved (prk_flush

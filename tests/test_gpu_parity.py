@@ -219,6 +219,49 @@ def test_early_z(gpu, case):
         assert (o[1] == 0.0).sum() > 1000  # (the fragments did land at zero)
 
 
+@pytest.mark.parametrize("first", ["scalar", "objects"])
+def test_early_z_after_z_writing_frame(gpu, first):
+    """Early z with frames queued back to back, no download between them: a
+    scalar (k_shade) or whole-object (k_span_shade / k_pix) frame writes z on
+    the flush stream, then a fused-clear per-triangle AVX frame writes its z
+    in k_vis on the visibility stream.  k_vis must wait for the earlier
+    frame's z writers (prk_api.hip, the vis stream's wait on s_mark), or
+    their late stores land over the new frame's z.  Debug off (debug frames
+    always wait).  z, colour bit for bit against early z off and the oracle."""
+    a = scenes.random_soup(60000, 512, 384, radius=40, seed=71, textured=True)
+    b = scenes.random_soup(4000, 512, 384, radius=16, seed=72)
+    out = {}
+    for early in (False, True):
+        r = prk.Renderer(0)
+        try:
+            r.target_alloc(512, 384)
+            r.set_debug(False)
+            r.set_early_z(early)
+            r.set_camera(a.prk_transform(), a.prk_lights())
+            ga = r.geometry(a.vertices, a.colors, a.normals, a.uvs)
+            gb = r.geometry(b.vertices, b.colors, b.normals, b.uvs)
+            ta, tb = r.texture(a.texture), r.texture(b.texture)
+            for k in range(3):
+                r.clear_on_flush()
+                if first == "scalar":
+                    r.draw(abi.PRK_SEM_SCALAR, ga, a.tri_count, bitmap=ta, phong=True)
+                else:
+                    r.draw(abi.PRK_SEM_AVX, ga, a.tri_count, bitmap=ta, phong=True, tris_per_object=8)
+                r.complete_all_work()
+                r.clear_on_flush()
+                r.draw_model_optimized(gb, b.tri_count, bitmap=tb, phong=True)
+                r.complete_all_work()
+            r.synchronize()
+            out[early] = r.download()
+        finally:
+            r.close()
+    oc, oz, _, _ = O.render(b)
+    for early in (False, True):
+        c, z = out[early]
+        assert np.array_equal(z.view(np.uint32), oz.view(np.uint32)), (first, early)
+        assert np.array_equal(c, oc), (first, early)
+
+
 def test_fused_clear_fallbacks(gpu):
     """Scalar frames and empty flushes fill first instead of fusing."""
     s = scenes.random_soup(2000, 256, 192, radius=16, seed=43, textured=False)
