@@ -463,6 +463,11 @@ def main():
                      "dominant_kernel": {"name": "k_vis", "ms_serial": serial["k_vis"],
                                          "share_of_serial_frame": serial["k_vis"] / max(
                                              1e-9, serial["raster"] + serial["k_bin_phase"])},
+                     # the frame's algorithmic bytes over the dominant kernel's
+                     # own serial time (HIP events on its stream, host-synchronised
+                     # frames; rocprofv3 of the same frames:
+                     # profiles/r06/kernel_stats_serial.csv)
+                     "dominant_frac": alg / (serial["k_vis"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      # the binding resource of the dominant kernel: issued VALU
                      # (SQ counters of the committed round profile)
                      "valu": load_valu(cfg_key, "k_vis", ms),

@@ -30,7 +30,6 @@
 
 extern "C" {
 hipError_t prk_launch_tri_draw(const prk::DrawRec *, uint32_t, uint32_t *, uint32_t, hipStream_t);
-hipError_t prk_bin_phase1(const prk::FrameParams *, uint32_t *, uint32_t *, void *, void *, size_t *, hipStream_t);
 hipError_t prk_bin_count(const prk::FrameParams *, uint32_t *, void *, uint32_t *, uint32_t *, uint8_t *, hipStream_t);
 uint32_t prk_cs_chunks(uint32_t);
 uint32_t prk_cs_nchunks(uint32_t, uint32_t);
@@ -43,9 +42,6 @@ int prk_cs_ready(uint32_t);
 hipError_t prk_bin_cs(const prk::FrameParams *, const void *, const uint32_t *, uint32_t *, uint32_t *, uint32_t *,
                       uint32_t *, uint32_t *, uint32_t, uint32_t *, uint32_t *, void *, uint32_t *, uint8_t *, uint32_t,
                       uint8_t *, const uint32_t *, const uint32_t *, uint32_t, hipStream_t);
-hipError_t prk_bin_phase2(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, uint32_t *, void *,
-                          uint32_t *, void *, uint32_t *, uint32_t *, uint8_t *, uint32_t, uint8_t *, void *, size_t *,
-                          hipStream_t);
 hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, const void *, const uint32_t *,
                              const uint32_t *, const void *, uint8_t *, uint8_t *, uint32_t *, void *, size_t,
                              uint32_t *, uint32_t *, uint32_t *, void *, uint32_t *, hipEvent_t, hipEvent_t,
@@ -237,7 +233,6 @@ struct prk_context {
     hipEvent_t s_mark = nullptr;  // flush-stream point the bin stream waits for (prior target contents)
     uint32_t *h_total = nullptr;  // pinned
     uint32_t pair_hint = 0;       // entry count of the last frame (counting-sort capacity)
-    bool legacy_bin = false;      // PRK_BIN_LEGACY=1: radix-sort binning with the count read back first
     int32_t tile_w = 256, tile_h = 8;  // measured best for C3b
     // Automatic tile (until prk_set_tile): 256x8, or narrower tiles for frames
     // with few bin entries per tile (under one wave's 64-entry chunk per
@@ -437,10 +432,6 @@ int prk_create(int device, prk_context **out) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->bset[i].binned_ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->bset[i].counted_ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipHostMalloc((void **)&c->bset[i].h_info, 2 * sizeof(uint32_t), hipHostMallocDefault);
-    }
-    {
-        const char *lb = std::getenv("PRK_BIN_LEGACY");
-        c->legacy_bin = lb && lb[0] == '1';
     }
     for (int i = 0; i < prk_context::kRing && e == hipSuccess; ++i)
         for (int k = 0; k < 6 && e == hipSuccess; ++k) e = hipEventCreate(&c->ev[i][k]);
@@ -1273,12 +1264,23 @@ static void frame_params(const prk_context *c, prk::FrameParams &fp) {
     fp.pitch = c->pitch;
     fp.color = (uint32_t *)c->color;
     fp.zbuf = c->zbuf;
-    fp.tile_w = c->tile_w;
-    fp.tile_h = c->tile_h;
+    // The context's tile, made taller (then wider) while the frame would have
+    // more tiles than the counting-sort binning holds (kCsMaxTiles): results
+    // never depend on the tile, and every tile keeps <= 8192 pixels.
+    int32_t tw = c->tile_w, th = c->tile_h;
+    auto ntl = [&](int32_t w, int32_t h) {
+        return (uint64_t)((c->W + w - 1) / w) * (uint64_t)((c->row1 - c->row0 + h - 1) / h);
+    };
+    while (ntl(tw, th) > prk_cs_max_tiles() && tw * th * 2 <= 8192) {
+        if (th < tw / 8) th *= 2;
+        else tw *= 2;
+    }
+    fp.tile_w = tw;
+    fp.tile_h = th;
     fp.tile_w_log2 = 0;
-    while ((1 << fp.tile_w_log2) < c->tile_w) ++fp.tile_w_log2;
-    fp.tiles_x = (c->W + c->tile_w - 1) / c->tile_w;
-    fp.tiles_y = (c->row1 - c->row0 + c->tile_h - 1) / c->tile_h;
+    while ((1 << fp.tile_w_log2) < tw) ++fp.tile_w_log2;
+    fp.tiles_x = (c->W + tw - 1) / tw;
+    fp.tiles_y = (c->row1 - c->row0 + th - 1) / th;
     fp.prof = (unsigned long long *)c->d_prof.p;
     fp.negz = (uint32_t *)c->d_negz.p;
     fp.z_in_vis = c->early_z && c->d_negz.p ? 1 : 0;
@@ -1412,18 +1414,15 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
     const bool span_rec = modeset == prk::MODE_AVX;
     // won flags: per (pair, row in tile) for span-record (AVX) frames, per
     // pair otherwise; the binning clears them (and trwon) for every pair.
-    const uint32_t won_stride = span_rec ? (uint32_t)c->tile_h : 1u;
+    const uint32_t won_stride = span_rec ? (uint32_t)fp.tile_h : 1u;
     size_t sel_bytes = 0;
     if (span_rec) PRK_TRY(prk_walk_select_bytes(T, &sel_bytes));
     // Every per-pair array of the set, for `np` pairs.
-    auto ensure_pairs = [&](size_t np, bool sort_keys) -> hipError_t {
+    auto ensure_pairs = [&](size_t np) -> hipError_t {
         const size_t ne = std::max<size_t>(np, 1);
         hipError_t e = hipSuccess;
         if (e == hipSuccess) e = bset_ensure(B.d_pair_tri, ne * 4);
         if (e == hipSuccess) e = bset_ensure(B.d_bins, ne * 8);  // (triangle, pair) per bin slot
-        if (e == hipSuccess && sort_keys) e = bset_ensure(B.d_keys_a, ne * 4);
-        if (e == hipSuccess && sort_keys) e = bset_ensure(B.d_vals_a, ne * 8);
-        if (e == hipSuccess && sort_keys) e = bset_ensure(B.d_keys_b, ne * 4);
         if (e == hipSuccess) e = bset_ensure(B.d_list, ne * 4);
         if (e == hipSuccess) e = bset_ensure(B.d_won, ne * won_stride);
         // span records: 64 B per (pair, row in tile); only won ones are written
@@ -1431,16 +1430,17 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
         return e;
     };
     PRK_TRY(bset_ensure(B.d_nwin, (size_t)ntiles * 4));
-    PRK_TRY(bset_ensure(B.d_wtag, (size_t)ntiles * c->tile_w * c->tile_h * 4));
+    PRK_TRY(bset_ensure(B.d_wtag, (size_t)ntiles * fp.tile_w * fp.tile_h * 4));
     if (span_rec) {
         PRK_TRY(bset_ensure(B.d_trwon, T));
         PRK_TRY(bset_ensure(B.d_wlist, ((size_t)T + 1) * 4));  // won triangles + their count
         PRK_TRY(bset_ensure(B.d_seltemp, std::max<size_t>(sel_bytes, 16)));
     }
     uint8_t *won, *trwon;
-    const bool cs = !c->legacy_bin && ntiles <= prk_cs_max_tiles() && prk_cs_ready(ntiles);
-    uint32_t total = 0;
-    if (cs) {
+    // (frame_params keeps every frame within the counting sort's tile count)
+    if (ntiles > prk_cs_max_tiles()) return PRK_ERR_LIMIT;
+    if (!prk_cs_ready(ntiles)) return PRK_ERR_DEVICE;
+    {
         // Counting-sort binning (prk_bin.hip k_cs_*): all sizes stay on the
         // device.  The per-pair arrays hold `cap` pairs (the last frame's
         // count plus room; a first frame guesses 2.5 per triangle, C3b has
@@ -1471,7 +1471,7 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
             DevBuf *pb[] = {&B.d_pair_tri, &B.d_bins, &B.d_list, &B.d_won, &B.d_recs};
             for (DevBuf *b : pb) b->release();
         }
-        if (pairs_held() < want) PRK_TRY(ensure_pairs(want, false));
+        if (pairs_held() < want) PRK_TRY(ensure_pairs(want));
         const uint32_t cap = (uint32_t)std::min<size_t>(pairs_held(), prk_cs_max_pairs());
         PRK_TRY(bset_ensure(B.d_ghist, std::max<size_t>((size_t)nch * ntiles * 4, 4)));
         PRK_TRY(bset_ensure(B.d_tile_tot, (size_t)ntiles * 4));
@@ -1489,31 +1489,6 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
                            won, won_stride, trwon, runlist, run_n, per, bs));
         PRK_TRY(hipMemcpyAsync(B.h_info, B.d_info.p, 8, hipMemcpyDeviceToHost, bs));
         PRK_TRY(hipEventRecord(B.counted_ev, bs));
-    } else {
-        // Radix-sort binning: the bin array size is read back first (one
-        // small D2H copy per frame; the host waits for the binning only).
-        size_t scan_bytes = 0;
-        PRK_TRY(prk_bin_phase1(&fp, nullptr, nullptr, nullptr, nullptr, &scan_bytes, bs));
-        PRK_TRY(bset_ensure(B.d_temp, scan_bytes));
-        PRK_TRY(hipEventRecord(c->ev[slot][0], bs));
-        PRK_TRY(prk_bin_phase1(&fp, (uint32_t *)B.d_tri_n.p, (uint32_t *)B.d_tri_off.p, B.d_ranges.p, B.d_temp.p,
-                               &scan_bytes, bs));
-        PRK_TRY(hipMemcpyAsync(c->h_total, (uint32_t *)B.d_tri_off.p + T, 4, hipMemcpyDeviceToHost, bs));
-        PRK_TRY(hipStreamSynchronize(bs));
-        total = *c->h_total;
-        c->stats.bin_entries = total;
-        if (total >= prk::kMaxPairs) return PRK_ERR_LIMIT;  // visibility tags hold a 31-bit pair index
-        PRK_TRY(ensure_pairs(total, true));
-        won = (uint8_t *)B.d_won.p;
-        trwon = span_rec ? (uint8_t *)B.d_trwon.p : nullptr;
-        size_t sort_bytes = 0;
-        PRK_TRY(prk_bin_phase2(&fp, B.d_ranges.p, (const uint32_t *)B.d_tri_off.p, total, (uint32_t *)B.d_keys_a.p,
-                               B.d_vals_a.p, (uint32_t *)B.d_keys_b.p, B.d_bins.p, (uint32_t *)B.d_pair_tri.p,
-                               (uint32_t *)B.d_offs.p, won, won_stride, trwon, nullptr, &sort_bytes, bs));
-        PRK_TRY(bset_ensure(B.d_temp, std::max(sort_bytes, scan_bytes)));
-        PRK_TRY(prk_bin_phase2(&fp, B.d_ranges.p, (const uint32_t *)B.d_tri_off.p, total, (uint32_t *)B.d_keys_a.p,
-                               B.d_vals_a.p, (uint32_t *)B.d_keys_b.p, B.d_bins.p, (uint32_t *)B.d_pair_tri.p,
-                               (uint32_t *)B.d_offs.p, won, won_stride, trwon, B.d_temp.p, &sort_bytes, bs));
     }
     PRK_TRY(hipEventRecord(c->ev[slot][1], bs));
     PRK_TRY(hipEventRecord(B.binned_ev, bs));
@@ -1562,7 +1537,7 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
     c->last_slot = slot;
     c->frame++;
     guard.ok = true;
-    if (cs) {
+    {
         // The whole frame is queued; now the entry count (the binning's first
         // few kernels) decides whether it fitted — read here, or, for the
         // frame's last pass once a previous frame has sized the scratch, by
@@ -2136,7 +2111,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(S.d_vals_b.ensure((size_t)std::max<uint32_t>(total, 1) * 4));
     PRK_TRY(prk_span_bin(&fp, S.d_pos.p, nslot, toff, tcnt, (uint32_t *)S.d_vals_b.p, s));
     PRK_TRY(S.d_nwin.ensure((size_t)ntiles * 4));
-    PRK_TRY(S.d_wtag.ensure((size_t)ntiles * c->tile_w * c->tile_h * 4));
+    PRK_TRY(S.d_wtag.ensure((size_t)ntiles * fp.tile_w * fp.tile_h * 4));
     PRK_TRY(prk_launch_spans(&fp, (const uint32_t *)S.d_offs.p, (const uint32_t *)S.d_vals_b.p, S.d_pos.p,
                              S.d_recs.p, scalar ? S.d_srecs.p : nullptr, modes, (const uint32_t *)S.d_span_tri.p,
                              (uint32_t *)S.d_nwin.p, (uint32_t *)S.d_wtag.p, s));

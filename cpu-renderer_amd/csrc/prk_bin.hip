@@ -2,28 +2,16 @@
 //
 //   k_bin_count   1 thread / triangle: ProjectVertex + back-face cull
 //                 (projekt.cpp:74-93, 3926-3943) -> conservative tile range ->
-//                 number of (triangle, tile) entries.
-//   scan          exclusive sum of the per-triangle counts (hipcub).
-//   k_bin_emit    1 thread / triangle: write (tile, (triangle, pair)) at the
-//                 triangle's offset, i.e. in triangle order (pair j), row-major
-//                 over the triangle's tile rectangle; pair_tri[j] = triangle.
-//   sort          stable LSD radix sort of the 8-byte (triangle, pair) values
-//                 by tile (rocprim onesweep), so every tile's bin lists its triangles in
-//                 submission order.
-//   k_tile_offsets  bin start of every tile (lower_bound on the sorted tiles).
+//                 number of (triangle, tile) entries (+ the setup records of
+//                 all-AVX frames); k_bin_band the same for a row band.
+//   k_cs_*        counting sort of the (triangle, pair) entries into tile
+//                 bins, every size on the device (below).
 //
 // Pairs are numbered in triangle (= submission) order: the pair index is the
 // visibility sweep's tie-break key, and k_walk / k_pix address span records
 // by (pair, row).  (Scattering pairs into bins with global atomic counters
 // instead of sorting measured 3x slower: device-scope atomics on 4096 hot
 // counters.)
-//
-// Triangle-ordered bins let k_raster name a triangle by its position in the
-// tile's bin (entry order == submission order), which it uses to skip, in the
-// shading sweep, every triangle that won no pixel of the tile.
-#include <hipcub/hipcub.hpp>
-#include <rocprim/device/device_radix_sort.hpp>
-
 #include <algorithm>
 #include <atomic>
 
@@ -376,51 +364,7 @@ __device__ __forceinline__ void clear_won(uint8_t *__restrict__ won, uint32_t st
         for (uint32_t i = 0; i < stride; ++i) won[(size_t)o * stride + i] = 0;
 }
 
-__global__ void k_bin_emit(FrameParams fp, const TileRange *__restrict__ ranges, const uint32_t *__restrict__ off,
-                           uint32_t *__restrict__ keys, uint2 *__restrict__ vals, uint32_t *__restrict__ pair_tri,
-                           uint8_t *__restrict__ won, uint32_t won_stride, uint8_t *__restrict__ trwon) {
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= fp.tri_count) return;
-    if (trwon) trwon[g] = 0;
-    const TileRange tr = ranges[g];
-    uint32_t o = off[g];
-    constexpr int kMaxClass = (1 << kRowClassBits) - 1;
-    if (tr.tx0 <= tr.tx1 && tr.ty0 <= tr.ty1)
-        for (int ty = tr.ty0; ty <= tr.ty1; ++ty) {
-            const int y0 = ty * fp.tile_h;
-            const int rows = min((int)tr.pad1, y0 + fp.tile_h) - max((int)tr.pad0, y0);
-            const uint32_t cls = PRK_ROWCLASS ? (uint32_t)min(kMaxClass, max(0, fp.tile_h - rows)) : 0u;
-            for (int tx = tr.tx0; tx <= tr.tx1; ++tx) {
-                keys[o] = ((uint32_t)(ty * fp.tiles_x + tx) << kRowClassBits) | cls;
-                vals[o] = make_uint2(g, o);
-                pair_tri[o] = g;
-                clear_won(won, won_stride, o);
-                ++o;
-            }
-        }
-    for (int ty = tr.oty0; ty <= tr.oty1; ++ty)
-        if (!(tr.tx0 == 0 && tr.tx0 <= tr.tx1 && ty >= tr.ty0 && ty <= tr.ty1)) {
-            keys[o] = ((uint32_t)(ty * fp.tiles_x) << kRowClassBits) | (PRK_ROWCLASS ? (uint32_t)kMaxClass : 0u);
-            vals[o] = make_uint2(g, o);
-            pair_tri[o] = g;
-            clear_won(won, won_stride, o);
-            ++o;
-        }
-}
 
-// offs[t] = first sorted position whose tile is >= t, for t in [0, ntiles].
-// (keys carry the row class in their low kRowClassBits bits)
-__global__ void k_tile_offsets(const uint32_t *__restrict__ keys, uint32_t total, uint32_t ntiles,
-                               uint32_t *__restrict__ offs) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t > ntiles) return;
-    uint32_t lo = 0, hi = total;
-    while (lo < hi) {
-        const uint32_t mid = lo + ((hi - lo) >> 1);
-        if ((keys[mid] >> kRowClassBits) < t) lo = mid + 1; else hi = mid;
-    }
-    offs[t] = lo;
-}
 
 // ---------------------------------------------------------------------------
 // Counting-sort binning (the default when the frame has at most kCsMaxTiles
@@ -790,66 +734,10 @@ __global__ void __launch_bounds__(256) k_cs_class(const uint32_t *__restrict__ o
 
 }  // namespace prk
 
-// Bin sort: onesweep radix at every size above one block.  rocprim's
-// default switches to a block sort + merge sort below 1 M items, which is
-// the band size of a 4- or 8-rank frame (C3b at N = 8: 0.4 M entries, nine
-// merge passes of two launches each, 0.13 ms per frame on one MI355X against
-// two onesweep passes over the band's 13-bit keys).
-using BinSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                                 rocprim::default_config, 0>;
-
 extern "C" {
 
-// Phase 1: counts + exclusive scan.  `scan_out` gets T+1 offsets; the caller
-// reads scan_out[T] (the number of entries) before phase 2.
-hipError_t prk_bin_phase1(const prk::FrameParams *fp, uint32_t *tri_n, uint32_t *scan_out, void *ranges,
-                          void *temp, size_t *temp_bytes, hipStream_t s) {
-    const uint32_t n = fp->tri_count + 1;
-    if (!temp) return hipcub::DeviceScan::ExclusiveSum(nullptr, *temp_bytes, tri_n, scan_out, n, s);
-    hipLaunchKernelGGL(prk::k_bin_count, dim3((n + prk::kCountThreads - 1) / prk::kCountThreads),
-                       dim3(prk::kCountThreads), 0, s, *fp, tri_n, reinterpret_cast<prk::TileRange *>(ranges),
-                       true);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, tri_n, scan_out, n, s);
-}
-
-// Phase 2: emit pairs in triangle order, stable sort of the (triangle, pair)
-// values by tile, tile offsets.  keys_a / vals_a: pairs in triangle order;
-// keys_b / bins: sorted by tile; pair_tri: triangle per pair; won (won_stride
-// bytes per pair) and trwon (T bytes, may be null) cleared.
-// With temp == nullptr only reports the temp storage the sort needs.
-hipError_t prk_bin_phase2(const prk::FrameParams *fp, const void *ranges, const uint32_t *scan_out, uint32_t total,
-                          uint32_t *keys_a, void *vals_a, uint32_t *keys_b, void *bins, uint32_t *pair_tri,
-                          uint32_t *offs, uint8_t *won, uint32_t won_stride, uint8_t *trwon, void *temp,
-                          size_t *temp_bytes, hipStream_t s) {
-    const uint32_t ntiles = (uint32_t)(fp->tiles_x * fp->tiles_y);
-    int bits = 1;
-    while ((1u << bits) < ntiles && bits < 32) ++bits;
-    bits += prk::kRowClassBits;
-    uint64_t *va = reinterpret_cast<uint64_t *>(vals_a), *vb = reinterpret_cast<uint64_t *>(bins);
-    if (!temp)
-        return rocprim::radix_sort_pairs<BinSortConfig>(nullptr, *temp_bytes, keys_a, keys_b, va, vb, total, 0,
-                                                        (unsigned)bits, s);
-    if (fp->tri_count)
-        hipLaunchKernelGGL(prk::k_bin_emit, dim3((fp->tri_count + 255) / 256), dim3(256), 0, s, *fp,
-                           reinterpret_cast<const prk::TileRange *>(ranges), scan_out, keys_a,
-                           reinterpret_cast<uint2 *>(vals_a), pair_tri, won, won_stride, trwon);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    if (total) {
-        e = rocprim::radix_sort_pairs<BinSortConfig>(temp, *temp_bytes, keys_a, keys_b, va, vb, total, 0,
-                                                     (unsigned)bits, s);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(prk::k_tile_offsets, dim3((ntiles + 1 + 255) / 256), dim3(256), 0, s, keys_b, total, ntiles,
-                       offs);
-    return hipGetLastError();
-}
-
-
-// Counting-sort binning (k_cs_*), after prk_bin_phase1's k_bin_count (scan
-// not needed: pass scan_out == nullptr there).  Every size is device-side:
+// Counting-sort binning (k_cs_*), after k_bin_count / k_bin_band (prk_bin_count
+// below).  Every size is device-side:
 // info[0] = entry count, info[1] = overflow (count > cap: bins left empty,
 // no pair written; the caller re-runs the frame with more room).
 // ghist: nchunks * ntiles u32; tile_tot: ntiles; chunk_tot / chunk_base: nchunks.

@@ -1461,7 +1461,7 @@ __global__ void __launch_bounds__(64 * kWalkWaves, PRK_WALK_MIN_WAVES) k_walk(Fr
 // PRK_WON_SORT 1 groups each run by triangle height, tallest first (each
 // k_walk lane walks its own triangle, so a wave runs as long as its tallest
 // one); measured on C3b (serial k_walk): 0 -> 0.249 ms, 1 -> 0.278, a global
-// height grouping -> 0.263, round 1's hipcub DeviceSelect -> 0.256: the
+// height grouping -> 0.263, round 1's library stream compaction -> 0.256: the
 // scattered record traffic costs more than the lane utilisation gains.
 // The list length (kWonHistBytes of scratch) is zeroed before the launch.
 // ---------------------------------------------------------------------------

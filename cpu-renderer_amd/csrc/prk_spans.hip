@@ -34,9 +34,6 @@
 //   k_span_vis (prk_kernels.hip)  per-tile visibility over the spans with
 //                 the 64-bit key max (tag = span index in submission order).
 //   k_pix (prk_kernels.hip, span records indexed by span)  shading.
-#include <hipcub/hipcub.hpp>
-#include <rocprim/device/device_radix_sort.hpp>
-
 #include <atomic>
 
 #include "prk_device.h"
@@ -2771,15 +2768,6 @@ hipError_t prk_objtri_emit(const prk::FrameParams *fp, const void *objs, const u
                        reinterpret_cast<prk::ObjEdge *>(edges), reinterpret_cast<unsigned long long *>(keys), vals);
     return hipGetLastError();
 }
-// MergeSort of every object: one radix sort of the n = 3 * ntri padded keys
-// over their low end_bit bits (temp == nullptr: size query); vals_out[i],
-// i < the visible edge count, = the edges in sorted order.
-hipError_t prk_obj_sort(void *keys_in, uint32_t *vals_in, void *keys_out, uint32_t *vals_out, uint32_t n,
-                        uint32_t end_bit, void *temp, size_t *temp_bytes, hipStream_t s) {
-    unsigned long long *ki = reinterpret_cast<unsigned long long *>(keys_in);
-    unsigned long long *ko = reinterpret_cast<unsigned long long *>(keys_out);
-    return rocprim::radix_sort_pairs(temp, *temp_bytes, ki, ko, vals_in, vals_out, n, 0, end_bit, s);
-}
 // The walk's working copy (n slots: total0 triangle edges, then nk1 caller edges).
 // (wy: null, or the triangle edges' (YMin, YMax) as int2, for prk_obj_seg)
 hipError_t prk_obj_gather(const void *edges, const uint32_t *ord, const uint32_t *total0p, const void *edges_in,
@@ -3034,17 +3022,7 @@ hipError_t prk_span_finish(const prk::FrameParams *fp, const void *raw, uint32_t
     return hipGetLastError();
 }
 
-// Exclusive scan of n + 1 64-bit counts (temp == nullptr: size query).
-hipError_t prk_scan_u64(const unsigned long long *in, unsigned long long *out, uint32_t n, void *temp,
-                        size_t *temp_bytes, hipStream_t s) {
-    return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, in, out, n, s);
-}
 
-// Exclusive scan of n + 1 counts (temp == nullptr: size query).
-hipError_t prk_scan_u32(const uint32_t *in, uint32_t *out, uint32_t n, void *temp, size_t *temp_bytes,
-                        hipStream_t s) {
-    return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, in, out, n, s);
-}
 
 // Span -> tile bin entries, pass 0: tcnt[t] = tile t's entries (ntiles + 1
 // values, the last 0: the scan's total).

@@ -93,6 +93,11 @@ _SIGS = {
     "prk_set_tile": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     "prk_construct_sphere": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.POINTER(C.c_uint32)]),
+    "prk_fill_edge_records": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                        C.POINTER(C.c_float), C.POINTER(abi.PrkTransform),
+                                        C.POINTER(abi.PrkLightData), C.c_int32, C.c_void_p, C.c_size_t,
+                                        C.c_size_t, C.c_void_p, C.POINTER(C.c_uint32)]),
+    "prk_advance_edge_records": (C.c_int, [C.c_void_p, C.c_uint32, C.c_size_t, C.c_size_t, C.c_int32]),
     "prk_fill_edge_count": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_float), C.POINTER(abi.PrkTransform),
                                       C.POINTER(C.c_uint32)]),
     "prk_get_target": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int32), C.POINTER(C.c_void_p),
@@ -192,6 +197,43 @@ def fill_edge_count(vertices, P, transform):
     _check("prk_fill_edge_count", lib().prk_fill_edge_count(_ptr(v), v.shape[0], Pc, C.byref(transform),
                                                              C.byref(n)))
     return n.value
+
+
+# x86-64 edge_info (projekt.h:17-37): 27 four-byte fields, pad, Next pointer
+EDGE_INFO_STRIDE, EDGE_INFO_NEXT = 120, 112
+
+
+def fill_edge_records(vertices, colors, normals, uvs, P, transform, lights, setup, memory=None):
+    """prk_fill_edge_records: FillEdgeTable's records (projekt.cpp:3894-4117)
+    written in place into `memory` (uint8 [>= 3T, 120]: x86-64 edge_info
+    elements; default zeros).  Returns (memory, count)."""
+    arrs = [None if a is None else np.ascontiguousarray(a, np.float32) for a in (vertices, colors, normals, uvs)]
+    nv = arrs[0].shape[0]
+    if memory is None:
+        memory = np.zeros((max(1, nv), EDGE_INFO_STRIDE), np.uint8)
+    Pc = (C.c_float * 3)(*(P or (0.0, 0.0, 0.0)))
+    n = C.c_uint32(0)
+    _check("prk_fill_edge_records", lib().prk_fill_edge_records(
+        *[_ptr(a) for a in arrs], nv, Pc, C.byref(transform), C.byref(lights), int(setup), _ptr(memory),
+        EDGE_INFO_STRIDE, EDGE_INFO_NEXT, None, C.byref(n)))
+    return memory, n.value
+
+
+def advance_edge_records(memory, count, height):
+    """prk_advance_edge_records on an edge_info array (uint8 [n, 120]) in
+    place: what DrawModel* leaves in it (projekt.cpp:3654-3869)."""
+    _check("prk_advance_edge_records", lib().prk_advance_edge_records(
+        _ptr(memory), count, EDGE_INFO_STRIDE, EDGE_INFO_NEXT, int(height)))
+    return memory
+
+
+def edge_record_words(memory, count):
+    """(fields as uint32 [count, 27], Next as an element index or -1)."""
+    w = memory[:count, :108].copy().view(np.uint32).reshape(count, 27)
+    ptr = memory[:count, EDGE_INFO_NEXT:EDGE_INFO_NEXT + 8].copy().view(np.uint64).reshape(count)
+    base = memory.ctypes.data
+    nxt = np.where(ptr == 0, -1, (ptr.astype(np.int64) - base) // EDGE_INFO_STRIDE).astype(np.int32)
+    return w, nxt
 
 
 def selftest_div(n=1 << 22, seed=1, device=0):

@@ -37,6 +37,15 @@
 //            the spans of file F (prk_span words), DoBufferLineRenderWork on
 //            the rest (one record per row), then DoModelRenderWork on the
 //            sphere as one object
+//   records F  record mode (PRK_SetEdgeRecords): the sphere as ONE object,
+//            FillEdgeTable(..., 1) writes edge_info records into EdgeMemory
+//            (dumped to F.fill), DrawModelOptimized(RenderQueue, ...) draws them
+//            and leaves them advanced (dumped to F.adv); dumps are 27 words +
+//            the Next index (-1: NULL) per edge
+//   records_scalar F  the same with FillEdgeTable(..., 0) (Gouraud, white lit:
+//            the objects carry the Bitmap) and DrawModel(..., 0, 0)
+//   records_queue  record mode, per-triangle objects through
+//            DrawModelOptimized(RenderQueue, ...)
 // The texture is a loaded_bitmap of exactly Height rows whose last byte is
 // followed by an inaccessible page: a read past it faults.
 //
@@ -53,6 +62,19 @@
 #include <vector>
 
 #include "projekt.h"
+
+// EdgeMemory[0, n) as 27 words + the Next index per edge.
+static bool dump_edges(const std::string &path, const edge_info *E, u32 n) {
+    FILE *f = std::fopen(path.c_str(), "wb");
+    if (!f) return false;
+    for (u32 i = 0; i < n; ++i) {
+        std::fwrite(&E[i], 4, 27, f);
+        const int32_t nx = E[i].Next ? (int32_t)(E[i].Next - E) : -1;
+        std::fwrite(&nx, 4, 1, f);
+    }
+    std::fclose(f);
+    return true;
+}
 
 static std::vector<uint32_t> read_words(const char *path) {
     std::vector<uint32_t> w;
@@ -195,6 +217,23 @@ int main(int argc, char **argv) {
     if (mode == "queue" || mode == "lines" || mode == "st" || mode == "scalar" || mode == "camera" ||
         mode == "vertexlit" || mode == "interp" || mode == "split_st" || mode == "split_queue") {
         if (!per_triangle(mode)) return fail("draw");
+    } else if (mode == "records_queue") {
+        PRK_SetEdgeRecords(1);
+        if (!per_triangle("queue")) return fail("draw");
+    } else if ((mode == "records" || mode == "records_scalar") && argc > 4) {
+        PRK_SetEdgeRecords(1);
+        std::vector<edge_info> SortMemory(EdgeMemory.size());
+        Commands.SortMemory = SortMemory.data();  // MergeSort's scratch (4117)
+        const bool scalar = mode == "records_scalar";
+        const u32 EdgeCount = FillEdgeTable(&Sphere, &Commands, scalar ? 0 : 1);
+        edges_total += EdgeCount;
+        if (PRK_LastStatus() != PRK_OK || !dump_edges(std::string(argv[4]) + ".fill", EdgeMemory.data(), EdgeCount))
+            return fail("FillEdgeTable");
+        if (scalar) DrawModel(&Buffer, EdgeMemory.data(), EdgeCount, &Commands, 0, 0);
+        else DrawModelOptimized(nullptr, &Buffer, EdgeMemory.data(), EdgeCount, &Commands, &Texture, 1);
+        if (PRK_LastStatus() != PRK_OK || !dump_edges(std::string(argv[4]) + ".adv", EdgeMemory.data(), EdgeCount))
+            return fail("draw");
+        Commands.SortMemory = nullptr;
     } else if (mode == "split_object") {
         const u32 EdgeCount = FillEdgeTable(&Sphere, &Commands, 1);
         edges_total += EdgeCount;

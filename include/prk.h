@@ -482,6 +482,34 @@ int prk_set_tile(prk_context *ctx, int32_t tile_w, int32_t tile_h);
 int prk_fill_edge_count(const float *vertices, uint32_t vertex_count, const float P[3],
                         const prk_transform *transform, uint32_t *count_out);
 
+/* Host utilities: edge_info records in the caller's own memory (the drop-in's
+ * opt-in record mode, projekt.h PRK_SetEdgeRecords).  The frame never comes
+ * from these: the GPU sets objects up from their vertices (prk_draw_objects)
+ * and draws edge lists from their copies (prk_draw_edges).  They reproduce
+ * what the reference leaves in the caller's memory, in place: `edges` is an
+ * array of elements of `stride` bytes whose first 108 bytes are edge_info's
+ * 27 fields in prk_edge order and whose list pointer (edge_info.Next) sits at
+ * byte `next_offset` (x86-64 edge_info: stride 120, next_offset 112).  A field
+ * the reference does not write keeps the caller's bytes.
+ *
+ * prk_fill_edge_records: FillEdgeTable (projekt.cpp:3894-4117) of one object
+ * of vertex_count vertices at offset P under T / L, with its own PhongShading
+ * and Bitmap != 0 as PRK_SETUP_* bits in `setup`: the visible edges written
+ * at edges[0 ..), Next = NULL, then MergeSort (2-72) with sort_memory
+ * (Commands->SortMemory, >= count elements; NULL: a library buffer) as its
+ * scratch.  *count_out = FillEdgeTable's return value (4119). */
+int prk_fill_edge_records(const float *vertices, const float *colors, const float *normals, const float *uvs,
+                          uint32_t vertex_count, const float P[3], const prk_transform *transform,
+                          const prk_light_data *lights, int32_t setup, void *edges, size_t stride,
+                          size_t next_offset, void *sort_memory, uint32_t *count_out);
+/* prk_advance_edge_records: what DrawModel* (every overload: the same list
+ * walk and edge step, 3654-3869, 3811-3829) leaves in the list it drew over a
+ * frame of `height` rows: every edge stepped once per row it was paired on,
+ * the list pointers as the walk left them (real addresses into `edges`).
+ * The reference's crashes are pinned as the draw pins them (prk.h above): a
+ * first-pair swap moves the list head (P3), an emptied list skips the row. */
+int prk_advance_edge_records(void *edges, uint32_t count, size_t stride, size_t next_offset, int32_t height);
+
 /* Host utility: the reference's test mesh, ConstructSphere
  * (projekt.cpp:4123-4289).  Arrays must hold 6624 vertices; returns the
  * vertex count through *count_out. */

@@ -58,6 +58,18 @@
 //    2042-2046, 3030-3034); edge lists and work records use them as they are
 //    at their DrawModel* / callback call.  A frame whose draws saw several
 //    cameras runs as consecutive flushes, one per change, in order.
+//  * Record mode (PRK_SetEdgeRecords(1), or PRK_DROPIN_EDGES=1 in the
+//    environment at PRK_Init*): FillEdgeTable writes the reference's sorted
+//    edge_info records into Object->EdgeMemory (3894-4117, MergeSort with
+//    Commands->SortMemory) instead of the token, and DrawModel* draws them as
+//    the caller's edge list.  For a caller that reads its edges back, copies
+//    them or draws them twice; the object's setup then runs on the host at the
+//    call (prk_fill_edge_records) and the per-object batching of the token
+//    path is gone.
+//  * DrawModel* on an edge_info list (a caller's own, or record mode's) leaves
+//    the list as the reference's walk does: every edge stepped once per row it
+//    was paired on, the Next pointers as the walk left them (3654-3869,
+//    prk_advance_edge_records).  The GPU draws the copy taken at the call.
 //  * Inputs the reference crashes on are rejected or pinned, see
 //    prk.h; PRK_LastStatus() reports the last library status.
 //
@@ -73,6 +85,7 @@
 #include <string.h>
 
 #include <chrono>
+#include <cstddef>
 #include <map>
 #include <set>
 #include <vector>
@@ -271,6 +284,7 @@ struct state {
     loaded_bitmap *LastBitmap = nullptr;        // texture of the previous draw this frame
     void *LastBitmapMemory = nullptr;
     int32_t LastTexture = -1;
+    bool EdgeRecords = false;                   // record mode (PRK_SetEdgeRecords)
 };
 inline state g_state;  // (a namespace-scope inline variable: no guard check per call)
 inline state &S() { return g_state; }
@@ -634,6 +648,11 @@ inline void draw(loaded_bitmap *Buffer, edge_info *Edges, u32 EdgeCount, game_re
         st.Edges.resize(st.Edges.size() + EdgeCount);
         for (u32 i = 0; i < EdgeCount; ++i) edge_in(st.Edges[d.First + i], Edges[i]);
         st.Draws.push_back(d);
+        // what the reference's walk leaves in the caller's list (3654-3869):
+        // the GPU draws the copy above
+        if (!ok(prk_advance_edge_records(Edges, EdgeCount, sizeof(edge_info), offsetof(edge_info, Next),
+                                         Buffer->Height)))
+            return;
     }
     st.LastStatus = PRK_OK;
 }
@@ -754,6 +773,8 @@ inline int PRK_InitDevices(const int *devices, int n) {
         st.Ctxs.push_back(c);
     }
     st.Ctx = st.Ctxs[0];
+    const char *rec = std::getenv("PRK_DROPIN_EDGES");
+    st.EdgeRecords = rec && rec[0] == '1';
     return st.LastStatus;
 }
 inline int PRK_Init(int device) { return PRK_InitDevices(&device, 1); }
@@ -768,6 +789,9 @@ inline void PRK_Shutdown() {
     }
     st = prk_dropin::state();
 }
+// Extension: record mode on (1) or off (0): FillEdgeTable writes real
+// edge_info records into Object->EdgeMemory (see the top of this file).
+inline void PRK_SetEdgeRecords(int on) { prk_dropin::S().EdgeRecords = on != 0; }
 // Extension: the next frame starts from (color, z) instead of the caller's
 // buffers (no upload; the clear is fused into the frame's kernels).
 inline void PRK_ClearNextFrame(uint32_t color, float z) {
@@ -811,6 +835,18 @@ inline u32 FillEdgeTable(render_entry_3d_object *Object, game_render_commands *C
     if (!st.Ctx || !Object || !Commands || !Object->EdgeMemory || !Object->VertexData || Object->VertexCount < 3)
         return 0;
     const u32 T = Object->VertexCount / 3, nv = 3 * T;
+    if (st.EdgeRecords) {  // the reference's records, in the caller's EdgeMemory (3894-4117)
+        const prk_dropin::camera &k = st.Cameras[prk_dropin::camera_id(st, Commands)];
+        const float P[3] = {Object->P.x, Object->P.y, Object->P.z};
+        u32 n = 0;
+        const int32_t setup = (PhongShading ? PRK_SETUP_PHONG : 0) | (Object->Bitmap ? PRK_SETUP_BITMAP : 0);
+        if (!prk_dropin::ok(prk_fill_edge_records((const float *)Object->VertexData, (const float *)Object->ColorData,
+                                                  (const float *)Object->NormalData, (const float *)Object->UVData,
+                                                  nv, P, &k.T, &k.L, setup, Object->EdgeMemory, sizeof(edge_info),
+                                                  offsetof(edge_info, Next), Commands->SortMemory, &n)))
+            return 0;
+        return n;
+    }
     prk_dropin::object_token o;
     o.Magic = prk_dropin::kMagic;
     o.Frame = st.Frame;

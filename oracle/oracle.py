@@ -206,10 +206,11 @@ def fill_edge_table(scene, tri0=0, n=1, phong=True, semantics=abi.PRK_SEM_AVX, s
     return out
 
 
-def fill_edge_table_words(scene, tri0=0, n=1, phong=True, semantics=abi.PRK_SEM_AVX):
+def fill_edge_table_words(scene, tri0=0, n=1, phong=True, semantics=abi.PRK_SEM_AVX, setup=None):
     """FillEdgeTable (projekt.cpp:3882-4121) on triangles [tri0, tri0+n) as one
-    object: the sorted edges as uint32 words [count, 27] in prk_edge layout."""
-    k = _Keep(scene, semantics, phong, n)
+    object: the sorted edges as uint32 words [count, 27] in prk_edge layout.
+    setup: FillEdgeTable's own PhongShading / Object->Bitmap (PRK_SETUP_*)."""
+    k = _Keep(scene, semantics, phong, n, setup=setup)
     words = np.zeros(27 * 3 * n + 27, np.uint32)
     cnt = C.c_uint32(0)
     rc = lib().oracle_fill_edge_table(C.byref(k.desc), C.c_uint32(tri0), C.c_uint32(n),
@@ -217,6 +218,22 @@ def fill_edge_table_words(scene, tri0=0, n=1, phong=True, semantics=abi.PRK_SEM_
     if rc != 0:
         raise RuntimeError("oracle_fill_edge_table failed: %d" % rc)
     return words.reshape(-1, 27)[: cnt.value].copy()
+
+
+def advance_edges(edge_words, height):
+    """What DrawModel* leaves in the caller's edge list ([n, 27] prk_edge
+    words, sorted as FillEdgeTable leaves them) after walking it over a frame
+    of `height` rows (projekt.cpp:3654-3869, edge step 3811-3829): (advanced
+    words, Next as an index into the list or -1)."""
+    w = np.array(edge_words, np.uint32, copy=True, order="C")
+    n = w.shape[0]
+    nxt = np.full(n, -1, np.int32)
+    L = lib()
+    L.oracle_advance_edges.restype = C.c_int
+    rc = L.oracle_advance_edges(_ptr(w), C.c_uint32(n), C.c_int32(height), _ptr(nxt))
+    if rc != 0:
+        raise RuntimeError("oracle_advance_edges failed: %d" % rc)
+    return w, nxt
 
 
 def _src_render(fn, scene, items, semantics, color, z, tri_index, phong=True):

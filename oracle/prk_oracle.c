@@ -1011,6 +1011,51 @@ int oracle_fill_edge_table(const or_draw_desc *D, uint32_t tri0, uint32_t n,
 
 uint32_t oracle_edge_words(void) { return 27u; }
 
+/* What DrawModel* leaves in the caller's edge list (all overloads share the
+ * list walk and the edge step, 3654-3869 / 542-560): the walk of
+ * or_aet_walk over a frame of `height` rows with no span body.  E (27 words
+ * per edge, as oracle_fill_edge_table writes them) is advanced in place;
+ * next_idx[i] = the index Edges[i].Next points at, or -1 for NULL. */
+static void or_no_span(or_ctx *X_, const or_edge *L, const or_edge *R, int32_t Row)
+{
+    (void)X_; (void)L; (void)R; (void)Row;
+}
+
+int oracle_advance_edges(uint32_t *words, uint32_t n, int32_t height, int32_t *next_idx)
+{
+    if ((!words || !next_idx) && n) return PRK_ERR_ARG;
+    or_edge *Edges = (or_edge *)calloc((size_t)n + 1, sizeof(or_edge));
+    if (!Edges) return PRK_ERR_NOMEM;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t *w = words + 27 * (size_t)i;
+        or_edge *E = Edges + i;
+        memcpy(&E->YMax, w + 0, 4); memcpy(&E->XMin, w + 1, 4); memcpy(&E->ZMin, w + 2, 4);
+        memcpy(&E->OneOverZMin, w + 3, 4); memcpy(&E->Gradient, w + 4, 4);
+        memcpy(&E->ZGradient, w + 5, 4); memcpy(&E->OneOverZGradient, w + 6, 4);
+        memcpy(&E->YMin, w + 7, 4); memcpy(&E->UMin, w + 8, 4); memcpy(&E->VMin, w + 9, 4);
+        memcpy(&E->UGradient, w + 10, 4); memcpy(&E->VGradient, w + 11, 4);
+        memcpy(&E->Left, w + 12, 4); memcpy(E->MinColor, w + 13, 16);
+        memcpy(E->ColorGradient, w + 17, 16); memcpy(E->MinNormal, w + 21, 12);
+        memcpy(E->NormalGradient, w + 24, 12);
+        E->Next = NULL;
+    }
+    or_ctx X_;
+    memset(&X_, 0, sizeof X_);
+    X_.Height = height; X_.RowLo = 0; X_.RowHi = height;
+    X_.BandH = 1; X_.BandMod = 1; X_.BandRem = 0;
+    or_aet_walk(&X_, Edges, n, or_no_span);
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t *w = words + 27 * (size_t)i;
+        const or_edge *E = Edges + i;
+        memcpy(w + 1, &E->XMin, 4); memcpy(w + 2, &E->ZMin, 4); memcpy(w + 3, &E->OneOverZMin, 4);
+        memcpy(w + 8, &E->UMin, 4); memcpy(w + 9, &E->VMin, 4);
+        memcpy(w + 13, E->MinColor, 16); memcpy(w + 21, E->MinNormal, 12);
+        next_idx[i] = E->Next ? (int32_t)(E->Next - Edges) : -1;
+    }
+    free(Edges);
+    return PRK_OK;
+}
+
 /* ------------------------------------------------------------------ */
 /* Draws from a caller's edge list / span list (prk_draw_edges /       */
 /* prk_draw_spans): DrawModelOptimized* on a ready edge_info list      */

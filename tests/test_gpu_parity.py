@@ -1158,7 +1158,7 @@ def _dropin_scene(textured=True, salt=0):
 
 DROPIN_MODES = ["queue", "lines", "st", "scalar", "object", "mutate", "edges", "work", "scalar_object",
                 "scalar_object_phong", "camera", "vertexlit", "interp", "interp_object", "split_st", "split_queue",
-                "split_object"]
+                "split_object", "records", "records_scalar", "records_queue"]
 
 
 def _camera_b(s):
@@ -1174,7 +1174,7 @@ def _camera_b(s):
 @pytest.mark.parametrize("mode,bands", [(m, 1) for m in DROPIN_MODES] +
                          [("queue", 3), ("object", 2), ("mutate", 3), ("scalar", 3), ("work", 2),
                           ("scalar_object", 3), ("camera", 2), ("interp_object", 2), ("split_st", 2),
-                          ("split_object", 2)])
+                          ("split_object", 2), ("records", 2)])
 def test_dropin_demo_matches_oracle(gpu, tmp_path, mode, bands):
     """examples/dropin_demo.cpp drives the reference's own entry points
     through include/projekt.h (FillEdgeTable, DrawModelOptimized(RenderQueue),
@@ -1196,13 +1196,14 @@ def test_dropin_demo_matches_oracle(gpu, tmp_path, mode, bands):
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     scalar_modes = ("scalar", "scalar_object", "scalar_object_phong", "vertexlit", "interp", "interp_object",
-                    "split_object")
+                    "split_object", "records_scalar")
     s = _dropin_scene(textured=mode not in scalar_modes)
     # FillEdgeTable's own PhongShading / Object->Bitmap (the demo's objects
     # carry the Bitmap except in "vertexlit")
     setup = {"scalar": abi.PRK_SETUP_BITMAP, "vertexlit": 0, "interp": abi.PRK_SETUP_PHONG | abi.PRK_SETUP_BITMAP,
              "scalar_object": abi.PRK_SETUP_BITMAP, "interp_object": abi.PRK_SETUP_PHONG | abi.PRK_SETUP_BITMAP,
-             "scalar_object_phong": abi.PRK_SETUP_PHONG | abi.PRK_SETUP_BITMAP}.get(mode)
+             "scalar_object_phong": abi.PRK_SETUP_PHONG | abi.PRK_SETUP_BITMAP,
+             "records": abi.PRK_SETUP_PHONG | abi.PRK_SETUP_BITMAP, "records_scalar": abi.PRK_SETUP_BITMAP}.get(mode)
     T = s.tri_count
     extra = []
     if mode == "edges":
@@ -1228,21 +1229,37 @@ def test_dropin_demo_matches_oracle(gpu, tmp_path, mode, bands):
         w[:, 24] = np.sort(rng.integers(0, 256, n)).astype(np.uint32)
         w.tofile(tmp_path / "spans.u32")
         extra = [str(tmp_path / "spans.u32")]
+    if mode in ("records", "records_scalar"):
+        extra = [str(tmp_path / "rec")]
     args = [str(exe), str(tmp_path / "c.u32"), str(tmp_path / "z.f32"), mode] + extra
     env = dict(os.environ, PRK_DEMO_BANDS=str(bands))
     run = subprocess.run(args, capture_output=True, text=True, timeout=120, env=env)
     assert run.returncode == 0, run.stderr
     gc = np.fromfile(tmp_path / "c.u32", np.uint32).reshape(256, 256)
     gz = np.fromfile(tmp_path / "z.f32", np.float32).reshape(256, 256)
-    if mode in ("queue", "lines"):
+    if mode in ("records", "records_scalar"):
+        # record mode: EdgeMemory holds the reference's records after
+        # FillEdgeTable (3894-4117) and after the draw's walk (3654-3869)
+        def dump(ext):
+            d = np.fromfile(str(tmp_path / "rec") + ext, np.uint32).reshape(-1, 28)
+            return d[:, :27], d[:, 27].view(np.int32)
+        fw, fn = dump(".fill")
+        ow = O.fill_edge_table_words(s, 0, T, setup=setup)
+        assert fw.shape == ow.shape and np.array_equal(fw, ow), (mode, fw.shape, ow.shape)
+        assert (fn == -1).all()
+        aw, an = dump(".adv")
+        oaw, oan = O.advance_edges(ow, 256)
+        assert np.array_equal(aw, oaw) and np.array_equal(an, oan), mode
+        assert not np.array_equal(aw, fw)
+    if mode in ("queue", "lines", "records_queue"):
         oc, oz, _, _ = O.render(s)
     elif mode == "st":
         oc, oz, _, _ = O.render(s, semantics=abi.PRK_SEM_AVX_ST)
     elif mode in ("scalar", "vertexlit", "interp"):
         oc, oz, _, _ = O.render(s, semantics=abi.PRK_SEM_SCALAR, phong=False, setup=setup)
-    elif mode == "object":
+    elif mode in ("object", "records"):
         oc, oz, _, _ = O.render(s, tris_per_object=T)
-    elif mode in ("scalar_object", "scalar_object_phong", "interp_object"):
+    elif mode in ("scalar_object", "scalar_object_phong", "interp_object", "records_scalar"):
         oc, oz, _, _ = O.render(s, semantics=abi.PRK_SEM_SCALAR, phong=mode.endswith("phong"), tris_per_object=T,
                                 setup=setup)
     elif mode == "camera":  # the second half drawn with the moved camera and the new light, over the first
@@ -1279,8 +1296,11 @@ def test_dropin_demo_matches_oracle(gpu, tmp_path, mode, bands):
     # FillEdgeTable's return values (projekt.cpp:4119) summed over the frame's
     # calls equal the oracle's edge counts: per triangle, or the whole sphere
     edges = int(run.stdout.split("edges=")[1].split()[0])
-    if mode in ("queue", "lines", "st", "scalar", "camera", "vertexlit", "interp", "split_st", "split_queue"):
+    if mode in ("queue", "lines", "st", "scalar", "camera", "vertexlit", "interp", "split_st", "split_queue",
+                "records_queue"):
         assert edges == sum(len(O.fill_edge_table(s, t, 1)) for t in range(T)), mode
+    elif mode in ("records", "records_scalar"):
+        assert edges == len(ow), mode
     elif mode.startswith("scalar_object") or mode == "interp_object":
         assert edges == len(O.fill_edge_table(s, 0, T, phong=mode.endswith("phong"))), mode
 
