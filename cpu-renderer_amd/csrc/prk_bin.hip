@@ -247,6 +247,10 @@ struct BandRuns {
     uint32_t nruns;
     uint32_t per;          // runs per counting-sort chunk
 };
+#ifndef PRK_BAND_WAVELIST
+#define PRK_BAND_WAVELIST 1  // k_bin_band: each wave lists its own contiguous triangles (ballots, no
+                             // workgroup barrier per 256 triangles); the lists are joined once
+#endif
 __global__ void __launch_bounds__(kCountThreads) k_bin_band(FrameParams fp, uint32_t *__restrict__ tri_n,
                                                              TileRange *__restrict__ ranges,
                                                              uint32_t *__restrict__ runlist,
@@ -258,6 +262,18 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_band(FrameParams fp, uint
     const uint32_t g0 = blockIdx.x * kRecRun;
     uint32_t n = 0;
     constexpr int kIt = kRecRun / kCountThreads;
+    constexpr int kWaves = kCountThreads / 64;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // Triangle of iteration `it` for this thread: PRK_BAND_WAVELIST, wave w
+    // takes 256 consecutive triangles of each half (64 per iteration), so its
+    // list is in triangle order and the (half, wave) lists joined in that
+    // order are the run's; else thread t takes it * 256 + t.
+    auto tri_of = [&](int it) -> uint32_t {
+        if (PRK_BAND_WAVELIST)
+            return (uint32_t)((it / (kIt / 2)) * (kRecRun / 2) + wv * (kRecRun / 2 / kWaves) +
+                              (it % (kIt / 2)) * 64 + lane);
+        return (uint32_t)(it * kCountThreads + threadIdx.x);
+    };
     // The run's positions.  One draw whose run is 16-byte aligned in its
     // geometry (the usual frame): the run's 9 * kRecRun floats are contiguous,
     // so each half of it comes in as coalesced float4 loads (a wave
@@ -269,6 +285,7 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_band(FrameParams fp, uint
     constexpr int kHalf = kRecRun / 2;                  // triangles per LDS half
     constexpr int kV4 = kHalf * 9 / 4 / kCountThreads;  // float4 per thread per half
     static_assert(kHalf * 9 % (4 * kCountThreads) == 0 && kHalf * 9 * 4 <= (int)sizeof(stage), "LDS half");
+    static_assert(kIt == 8 && kWaves == 4, "the wave-list mapping: two halves of four 64-triangle steps per wave");
     const uint32_t gt0 = fp.draw0.geom_tri0 + (g0 - fp.draw0.first_global);
     // (gt0 % 4 == 0 makes the run's offset 16-B aligned; the base must be too:
     // prk_geometry_wrap_device takes any 4-B aligned caller pointer)
@@ -280,7 +297,7 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_band(FrameParams fp, uint
     if (!coal) {
 #pragma unroll
         for (int it = 0; it < kIt; ++it) {
-            const uint32_t g = g0 + it * kCountThreads + threadIdx.x;
+            const uint32_t g = g0 + tri_of(it);
             pd[it] = fp.draws;
             if (g < fp.tri_count) {
                 uint32_t gt;
@@ -291,11 +308,14 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_band(FrameParams fp, uint
             }
         }
     }
+    // PRK_BAND_WAVELIST: the (half, wave) lists, in list[] at half * kHalf +
+    // wave * (kHalf / kWaves), their lengths in wcnt
+    __shared__ uint32_t wcnt[2][kWaves];
+    uint32_t wn = 0;  // this wave's list length in the current half
     const float *lf = reinterpret_cast<const float *>(&stage[0][0]);
 #pragma unroll
     for (int it = 0; it < kIt; ++it) {
-        const uint32_t k = (uint32_t)it * kCountThreads;
-        const uint32_t g = g0 + k + threadIdx.x;
+        const uint32_t tl = tri_of(it), g = g0 + tl;
         if (coal && it % (kIt / 2) == 0) {  // this half's positions into LDS
             const float4 *src = reinterpret_cast<const float4 *>(fp.draw0.V + 9 * ((size_t)gt0 + it * kCountThreads));
             if (it) __syncthreads();  // (the previous half's reads)
@@ -310,7 +330,7 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_band(FrameParams fp, uint
             bool hit;
             if (coal) {
                 float v9[9];
-                const int t = (it % (kIt / 2)) * kCountThreads + (int)threadIdx.x;
+                const int t = (int)(tl % (uint32_t)kHalf);
 #pragma unroll
                 for (int j = 0; j < 9; ++j) v9[j] = lf[9 * t + j];
                 hit = tri_tile_range_raw(fp, fp.draws, v9, tr);
@@ -330,18 +350,63 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_band(FrameParams fp, uint
             tri_n[g] = 0;  // sentinel: a scan's last element is the total
         }
         const uint32_t f = ne != 0 ? 1u : 0u;
-        uint32_t tot;
-        const uint32_t pos = cs_block_excl_scan(f, scratch, tot);
-        if (f) {
-            list[n + pos] = g;
-            runlist[g0 + n + pos] = g;
+        if (PRK_BAND_WAVELIST) {
+            const unsigned long long bal = __ballot(f != 0);
+            const uint32_t r = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            const int h = it / (kIt / 2);
+            if (f) list[h * kHalf + wv * (kHalf / kWaves) + wn + r] = g;
+            wn += (uint32_t)__popcll(bal);
+            if (it % (kIt / 2) == kIt / 2 - 1) {
+                if (lane == 0) wcnt[h][wv] = wn;
+                wn = 0;
+            }
+        } else {
+            uint32_t tot;
+            const uint32_t pos = cs_block_excl_scan(f, scratch, tot);
+            if (f) {
+                list[n + pos] = g;
+                runlist[g0 + n + pos] = g;
+            }
+            n += tot;
         }
-        n += tot;
+    }
+    if (PRK_BAND_WAVELIST) {
+        // join the eight (half, wave) lists in order: run list out, and the
+        // joined list for the records below
+        __syncthreads();
+        uint32_t off[2][kWaves];
+        n = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int w = 0; w < kWaves; ++w) {
+                off[h][w] = n;
+                n += wcnt[h][w];
+            }
+        // (each list holds <= kHalf / kWaves = kCountThreads entries: thread t
+        // moves entry t of each; every entry moves down or stays, so all are
+        // read before any is written)
+        static_assert(kHalf / kWaves == kCountThreads, "one entry per thread and list");
+        uint32_t v[2][kWaves];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int w = 0; w < kWaves; ++w)
+                v[h][w] = threadIdx.x < wcnt[h][w] ? list[h * kHalf + w * (kHalf / kWaves) + threadIdx.x] : 0u;
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int w = 0; w < kWaves; ++w)
+                if (threadIdx.x < wcnt[h][w]) {
+                    list[off[h][w] + threadIdx.x] = v[h][w];
+                    runlist[g0 + off[h][w] + threadIdx.x] = v[h][w];
+                }
     }
     if (threadIdx.x == 0) run_n[blockIdx.x] = n;
     __syncthreads();
     if (!fp.trec) return;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (uint32_t b = (uint32_t)wv * 64; b < n; b += kCountThreads) {
         const uint32_t i = b + lane;
         const bool rec = i < n;

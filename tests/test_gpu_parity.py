@@ -80,6 +80,21 @@ def test_split_setup_and_shade_camera(gpu, semantics, phong, textured, tpo):
         assert (channel_diff(g[0], O.render(s, semantics=semantics, phong=phong, tris_per_object=tpo)[0]) > 1).any()
 
 
+@pytest.mark.parametrize("n,bits", [(1, 8), (100, 26), (6624, 26), (70000, 30), (262145, 31), (3000000, 36)])
+def test_span_path_sort_and_scan(gpu, n, bits):
+    """csrc/prk_sort.hip: the span path's radix sort (MergeSort keys,
+    projekt.cpp:2-72) is a stable sort and its scan an exclusive prefix sum:
+    tools/sort_bench checks both against std::stable_sort / a host sum on
+    random keys with ties, short and long tiles, one and many look-back
+    tiles."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "sort_bench")
+    assert os.path.exists(exe), "tools/sort_bench not built (__graft_entry__.build())"
+    r = subprocess.run([exe, str(n), str(bits), "3"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "sort mismatches 0, scan mismatches 0" in r.stdout, (r.stdout, r.stderr)
+
+
 @pytest.mark.parametrize("seed", [1, 2])
 def test_shared_divisor_exact(gpu, seed):
     """The kernels' shared-reciprocal quotients (prk_device.h DivBy) equal the
