@@ -45,6 +45,13 @@ int prk_fill_edge_count(const float *V, uint32_t vertex_count, const float P[3],
     return PRK_OK;
 }
 int prk_flush(prk_context *, void *) { return PRK_OK; }
+int prk_advance_edge_records(void *, uint32_t, size_t, size_t, int32_t) { return PRK_OK; }
+int prk_fill_edge_records(const float *, const float *, const float *, const float *, uint32_t, const float *,
+                          const prk_transform *, const prk_light_data *, int32_t, void *, size_t, size_t, void *,
+                          uint32_t *count_out) {
+    *count_out = 0;
+    return PRK_OK;
+}
 int prk_geometry_create(prk_context *, const float *, const float *, const float *, const float *, uint32_t,
                         int32_t *h) {
     *h = 0;
