@@ -74,6 +74,14 @@ hipError_t prk_obj_walk_group(const prk::FrameParams *, int32_t, uint32_t, const
                               const unsigned long long *, const uint32_t *, uint32_t, int32_t *, const uint32_t *,
                               const uint32_t *, void *, const unsigned long long *, void *, void *, void *, void *,
                               uint32_t *, uint32_t *, const uint32_t *, hipStream_t);
+uint32_t prk_big_max_entries(void);
+uint32_t prk_big_list_arrays(void);
+hipError_t prk_big_rows(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, uint32_t, const uint32_t *,
+                        const uint32_t *, const void *, uint32_t *, hipStream_t);
+hipError_t prk_big_walk(const prk::FrameParams *, int32_t, const void *, const uint32_t *, const unsigned long long *,
+                        const uint32_t *, uint32_t, uint32_t, int32_t *, const uint32_t *, const uint32_t *,
+                        const void *, const uint32_t *, const unsigned long long *, uint32_t *, void *, void *,
+                        uint32_t *, uint32_t *, const uint32_t *, hipStream_t);
 hipError_t prk_pr_walk_begin(const prk::FrameParams *, const prk::PrWalkArgs *, hipStream_t);
 hipError_t prk_pr_walk_group(const prk::FrameParams *, const prk::PrWalkArgs *, int32_t, uint32_t, const uint32_t *,
                              uint32_t, uint32_t, hipStream_t);
@@ -290,7 +298,7 @@ struct prk_context {
             d_keys_b, d_vals_b, d_offs, d_nwin, d_wtag, d_srecs, d_work, d_ekeys, d_ekeys2, d_evals, d_ecnt, d_escan,
             d_rcnt, d_rscan, d_bound, d_oslot, d_pool, d_err, d_raw, d_most, d_cls, d_prrow, d_prcnt, d_preoff,
             d_prfge, d_prccur, d_prkey, d_prest, d_prsst, d_preend, d_preendm, d_prmatch, d_prsidx, d_prsm, d_prstat,
-            d_segcnt, d_segoff, d_segs, d_wy;
+            d_segcnt, d_segoff, d_segs, d_wy, d_bcnt, d_bwoff, d_where;
         // the pass's host tables, packed into pinned memory for one upload
         // (stage_ev: that upload, before the staging is rewritten)
         char *h_stage = nullptr;
@@ -491,7 +499,7 @@ int prk_destroy(prk_context *c) {
                         &S.d_raw, &S.d_most, &S.d_cls, &S.d_prrow, &S.d_prcnt, &S.d_preoff, &S.d_prfge,
                         &S.d_prccur, &S.d_prkey, &S.d_prest, &S.d_prsst, &S.d_preend, &S.d_preendm,
                         &S.d_prmatch, &S.d_prsidx, &S.d_prsm, &S.d_prstat, &S.d_segcnt, &S.d_segoff,
-                        &S.d_segs, &S.d_wy};
+                        &S.d_segs, &S.d_wy, &S.d_bcnt, &S.d_bwoff, &S.d_where};
         for (DevBuf *b : sb) b->release();
         if (S.h_rb) (void)hipHostFree(S.h_rb);
         if (S.stage_ev) {
@@ -1875,6 +1883,8 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     struct Group {
         int32_t mode;
         uint32_t lcap, start, count;
+        bool big;             // the huge-object walk (k_obj_walk_big)
+        uint32_t max_edges;   // (big: its objects' most edges)
     };
     std::vector<Group> groups;
     uint32_t *cls_big = reinterpret_cast<uint32_t *>(S.h_cls + (size_t)nbig_all * 12);
@@ -1882,31 +1892,54 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     uint32_t *cls_cap = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(cls_off) + (size_t)nbig_all * 8);
     uint32_t *cls_pr = cls_cap + nbig_all;  // PrObj[npr] (8 words each)
     uint32_t *cls_grp = cls_pr + 8 * (size_t)nbig_all;  // its objects grouped by (mode, LDS capacity)
+    // Objects whose lists outgrow LDS take the huge-object walk (a
+    // workgroup, the list in device memory: k_obj_walk_big) when their sizes
+    // are known (k_obj_maxact) and fit it, else one wave each (k_obj_walk_wave).
+    // PRK_OBJ_BIG=0: always the wave; PRK_OBJ_BIG_MIN=n (tests): objects of
+    // more than n active edges skip the LDS lists.
+    uint64_t where_n = 0;  // the huge walk's (edge, row) codes
     {
+        const char *benv = std::getenv("PRK_OBJ_BIG"), *menv = std::getenv("PRK_OBJ_BIG_MIN");
+        const bool big_on = !(benv && benv[0] == '0');
+        const int64_t big_min = menv ? std::atoll(menv) : INT64_MAX;
+        const int32_t *h_rows = h_most + nbig_all, *h_ents = h_most + 2 * (size_t)nbig_all;
         static const uint32_t kCaps[] = {62, 126, 254, 510, 1022};
         uint32_t k = 0, b = 0;
         for (int mo = 0; mo < prk::MODE_COUNT; ++mo) {
             const uint32_t b0 = b;
-            for (int ci = 0; ci <= 5; ++ci) {  // ci 5: the device-memory lists
+            for (int ci = 0; ci <= 6; ++ci) {  // ci 5: the huge-object walk, 6: one wave each
                 const uint32_t capc = ci < 5 ? kCaps[ci] : 0u;
                 if (ci < 5 && capc > lcap) continue;
                 const uint32_t start = k;
+                uint32_t gmax = 0;
                 for (uint32_t i = 0; i < bigm[mo].size(); ++i) {
-                    const int32_t most = h_most[b0 + i];
+                    const uint32_t bi = b0 + i;
+                    const int32_t most = h_most[bi];
                     uint32_t want = 0;  // the class this object takes
                     for (int cj = 0; cj < 5; ++cj)
-                        if (kCaps[cj] <= lcap && most >= 0 && (uint32_t)most <= kCaps[cj]) {
+                        if (kCaps[cj] <= lcap && most >= 0 && (uint32_t)most <= kCaps[cj] && most <= big_min) {
                             want = kCaps[cj];
                             break;
                         }
                     if (want != capc) continue;
+                    if (ci >= 5) {
+                        const int32_t rows = h_rows[bi], ents = h_ents[bi];
+                        const bool hb = big_on && most > 0 && (uint32_t)most <= prk_big_max_entries() && rows > 0 &&
+                                        rows < INT32_MAX && ents >= 0 && ents < INT32_MAX &&
+                                        where_n + (uint64_t)ents < 0x7FFFFFFFull && bigm[mo].size() <= 65535;
+                        if (hb != (ci == 5)) continue;
+                        if (hb) where_n += (uint64_t)ents;
+                    }
                     cls_big[k] = bigm[mo][i];
                     cls_off[k] = capc ? 0ull : pool;
-                    cls_cap[k] = capc ? 0u : bige[mo][i];
-                    if (!capc) pool += (uint64_t)kWaveListArrays * (bige[mo][i] + 2);
+                    const uint32_t cap = ci == 5 ? (uint32_t)most : bige[mo][i];
+                    cls_cap[k] = capc ? 0u : cap;
+                    if (!capc)
+                        pool += (uint64_t)(ci == 5 ? prk_big_list_arrays() : kWaveListArrays) * (cap + 2);
+                    gmax = std::max(gmax, bige[mo][i]);
                     ++k;
                 }
-                if (k > start) groups.push_back(Group{mo, capc, start, k - start});
+                if (k > start) groups.push_back(Group{mo, capc, start, k - start, ci == 5, gmax});
             }
             b += (uint32_t)bigm[mo].size();
         }
@@ -2077,11 +2110,35 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(prk_obj_walk(&fp, d_objs, nobj, escan, total0p, S.d_work.p, oslot, S.d_recs.p,
                          scalar ? S.d_srecs.p : nullptr, S.d_pos.p, (uint32_t *)S.d_span_tri.p, d_spans_in,
                          (uint32_t *)S.d_err.p, thread_links ? 1 : 0, d_segs, d_nseg, (uint32_t)max_segs, s));
-    for (const Group &g : groups)
-        PRK_TRY(prk_obj_walk_group(&fp, g.mode, g.lcap, d_objs, d_cbig + g.start, d_coff + g.start, d_ccap + g.start,
-                                   g.count, (int32_t *)S.d_pool.p, escan, total0p, S.d_work.p, oslot, S.d_recs.p,
-                                   scalar ? S.d_srecs.p : nullptr, S.d_raw.p, S.d_pos.p, (uint32_t *)S.d_span_tri.p,
-                                   (uint32_t *)S.d_err.p, d_prstat, s));
+    uint32_t *d_bwoff = nullptr;
+    if (where_n) {  // the huge walk's where-code offsets (per edge) and codes
+        PRK_TRY(S.d_bcnt.ensure(((size_t)nwork + 1) * 4));
+        PRK_TRY(S.d_bwoff.ensure(((size_t)nwork + 1) * 4));
+        PRK_TRY(S.d_where.ensure((size_t)where_n * 4));
+        uint32_t *bcnt = (uint32_t *)S.d_bcnt.p;
+        d_bwoff = (uint32_t *)S.d_bwoff.p;
+        PRK_TRY(hipMemsetAsync(bcnt, 0, ((size_t)nwork + 1) * 4, s));
+        for (const Group &g : groups)
+            if (g.big)
+                PRK_TRY(prk_big_rows(&fp, d_objs, d_cbig + g.start, g.count, g.max_edges, escan, total0p, S.d_work.p,
+                                     bcnt, s));
+        PRK_TRY(prk_scan_u32(bcnt, d_bwoff, nwork + 1, nullptr, &tb, s));
+        PRK_TRY(temp(tb));
+        PRK_TRY(prk_scan_u32(bcnt, d_bwoff, nwork + 1, S.d_temp.p, &tb, s));
+        PRK_TRY(hipMemsetAsync(S.d_where.p, 0xFF, (size_t)where_n * 4, s));  // (kBigUnpaired: never listed)
+    }
+    for (const Group &g : groups) {
+        if (g.big)
+            PRK_TRY(prk_big_walk(&fp, g.mode, d_objs, d_cbig + g.start, d_coff + g.start, d_ccap + g.start, g.count,
+                                 g.max_edges, (int32_t *)S.d_pool.p, escan, total0p, S.d_work.p, d_bwoff, oslot,
+                                 (uint32_t *)S.d_where.p, S.d_raw.p, S.d_pos.p, (uint32_t *)S.d_span_tri.p,
+                                 (uint32_t *)S.d_err.p, d_prstat, s));
+        else
+            PRK_TRY(prk_obj_walk_group(&fp, g.mode, g.lcap, d_objs, d_cbig + g.start, d_coff + g.start,
+                                       d_ccap + g.start, g.count, (int32_t *)S.d_pool.p, escan, total0p, S.d_work.p,
+                                       oslot, S.d_recs.p, scalar ? S.d_srecs.p : nullptr, S.d_raw.p, S.d_pos.p,
+                                       (uint32_t *)S.d_span_tri.p, (uint32_t *)S.d_err.p, d_prstat, s));
+    }
     if (nbig_all)  // the slot walks' pairs into span records
         PRK_TRY(prk_span_finish(&fp, S.d_raw.p, nslot, S.d_recs.p, scalar ? S.d_srecs.p : nullptr, S.d_pos.p, s));
     // span -> tile bin entries: the tiles' counts and their scan (the

@@ -2118,6 +2118,526 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_obj_walk_wave(FrameParams f
 }
 
 // ---------------------------------------------------------------------------
+// The walk of huge objects (objects whose most active edges exceed the
+// workgroup walk's LDS list, up to kBigMaxM of them; C3b as ONE object holds
+// ~16 k edges a row).  One workgroup of kBigThreads walks the object's rows
+// in order (3615-3869) with its list in device memory: two SoA buffers of
+// (X, Gradient, Left, YMax, where-base) in list order, each list operation a
+// few workgroup-wide passes (entry q of a pass: thread q % kBigThreads, tile
+// q / kBigThreads), every scan a DPP wave scan + the waves' totals in LDS:
+//   insertion + expiry (3654-3749), one scan: a batch of new edges (<=
+//     kBigThreads, MergeSort order, no NaN key) lands where inserting them one
+//     at a time puts them (insert_batch's argument).  New edge c's gap is the
+//     first entry whose key is greater (found through the entries' per-16
+//     maxima, prefix-maxed in LDS, then those 16 entries), and
+//        c lands at  #kept entries before gap(c) + #kept new edges of smaller
+//                    gap + those of its gap ordered before it (key, arrival),
+//        a kept entry q at  #kept entries before q + #kept new edges of gap <= q:
+//     the new edges counted per gap, one scan of (keep flag, count) over the
+//     entries, then each gap's few new edges rank themselves.  (A batch with
+//     a NaN key goes one edge at a time; the row's last batch also drops the
+//     expired entries.)
+//   pairing (3751-3869), one pass: thread k steps pair k's X and its
+//     neighbours' (X += Gradient, obj_step's first line), does its first swap
+//     (3831-3841) and both boundary swaps (3843-3853; the neighbours' fields
+//     through lane shuffles, from memory at wave edges), and writes its two
+//     entries' final places.
+// The walk sets up no span.  For every (edge, row) the edge is listed on it
+// writes a code into `where` (the edge's rows at woff[edge]): its pair slot
+// and side, "paired, not emitted" (rows above the band) or "unpaired" (an odd
+// last entry: not stepped).  k_big_emit then replays every edge, a thread
+// each, stepped row by row as the walk steps it (obj_step on its paired
+// rows), into its side of each pair's PairRaw; k_span_finish sets the spans
+// up as it does the chunked walk's.
+// ---------------------------------------------------------------------------
+constexpr int kBigThreads = 1024;
+constexpr int kBigWaves = kBigThreads / 64;
+constexpr int kBigMaxTiles = 64;
+constexpr uint32_t kBigMaxM = (uint32_t)kBigMaxTiles * kBigThreads - 2;  // list entries (and the pool stride - 2)
+constexpr int kBigSamp = kBigMaxTiles * kBigThreads / 16;                // per-16 maxima
+constexpr int kBigU = 8;                                                 // tiles a pass keeps in registers
+constexpr int kBigListArrays = 12;  // 2 x (x, g, left, ymax, wb) + d + base, cap + 2 int32 each
+constexpr uint32_t kBigUnpaired = 0xFFFFFFFFu, kBigNoEmit = 0xFFFFFFFEu;
+
+struct BigBuf {  // one list buffer, in list order
+    float *x, *g;
+    int32_t *left, *ymax, *wb;
+};
+struct BigList {
+    BigBuf b0, b1;
+    int32_t *d;     // the batch's kept new edges per gap
+    int32_t *base;  // where each gap's new edges begin
+    __device__ __forceinline__ void carve(int32_t *base, uint32_t cap) {
+        const size_t s = (size_t)cap + 2;
+        b0 = BigBuf{reinterpret_cast<float *>(base), reinterpret_cast<float *>(base + s), base + 2 * s, base + 3 * s,
+                    base + 4 * s};
+        int32_t *p = base + 5 * s;
+        b1 = BigBuf{reinterpret_cast<float *>(p), reinterpret_cast<float *>(p + s), p + 2 * s, p + 3 * s, p + 4 * s};
+        d = base + 10 * s;
+        this->base = base + 11 * s;
+        static_assert(kBigListArrays == 12, "carve cuts kBigListArrays arrays");
+    }
+    // (selects, not an indexed pair: an indexed pointer array went to scratch)
+    __device__ __forceinline__ BigBuf buf(int c) const {
+        return BigBuf{c ? b1.x : b0.x, c ? b1.g : b0.g, c ? b1.left : b0.left, c ? b1.ymax : b0.ymax,
+                      c ? b1.wb : b0.wb};
+    }
+};
+struct BigLds {
+    float sx[kBigSamp], sg[kBigSamp];  // per-16 key maxima, then their prefix maxima
+    int32_t sl[kBigSamp];
+    int32_t ts[kBigMaxTiles * kBigWaves], tm[kBigMaxTiles * kBigWaves];  // wave totals: keep and count sums
+    float px[kBigThreads], pg[kBigThreads];  // per-thread key maxima (the sample scan)
+    int32_t pl[kBigThreads];
+    float nkx[kBigThreads], nkg[kBigThreads];  // the row's new edges (a window of kBigThreads)
+    int32_t nkl[kBigThreads], nky[kBigThreads], nkw[kBigThreads];
+};
+
+// Insertion of the new edges S.nk*[c0, c0 + kb) into the list (buffer cur,
+// m entries) and, when `expire`, expiry of every entry with YMax <= Row: the
+// result into buffer cur ^ 1.  Returns the new length.
+#define PRK_BIG_T(k, t)                                    \
+    do {                                                   \
+        if (PRK_WPROF) {                                   \
+            const unsigned long long t_ = PRK_WT();        \
+            if (wp) wp[k] += t_ - (t);                     \
+            (t) = t_;                                      \
+        }                                                  \
+    } while (0)
+__device__ __forceinline__ int big_insert_expire(const BigList &L, BigLds &S, BlockRed &R, int cur, int m, int c0, int kb,
+                                                 bool expire, int32_t Row, unsigned long long *wp = nullptr) {
+    unsigned long long tw0 = PRK_WT();
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int T = (m + kBigThreads - 1) / kBigThreads;
+    const BigBuf A = L.buf(cur), B = L.buf(cur ^ 1);
+    const float *X = A.x, *G = A.g;
+    const int32_t *LF = A.left, *YM = A.ymax, *WB = A.wb;
+    int32_t gapc = 0, kr = 0;
+    bool keptc = false;
+    if (kb > 0) {
+        if (tid == 0) L.d[m] = 0;
+        if (m > 0) {
+            // 1. the entries' keys: per-16 maxima (a 16-lane row each); d zeroed
+            for (int t0 = 0; t0 < T; t0 += kBigU) {
+                float kx[kBigU], kg[kBigU];
+                int32_t kl[kBigU];
+#pragma unroll
+                for (int u = 0; u < kBigU; ++u) {
+                    const int q = (t0 + u) * kBigThreads + tid;
+                    kx[u] = -INFINITY; kg[u] = -INFINITY; kl[u] = INT32_MIN;
+                    if (t0 + u < T && q < m) { kx[u] = X[q]; kg[u] = G[q]; kl[u] = LF[q]; }
+                }
+#pragma unroll
+                for (int u = 0; u < kBigU; ++u) {
+                    if (t0 + u >= T) break;
+                    const int q = (t0 + u) * kBigThreads + tid;
+                    LKey k = q < m ? entry_key(kx[u], kg[u], kl[u]) : LKey{-INFINITY, -INFINITY, INT32_MIN};
+                    int32_t p = 0;
+                    key_max_step<kDppShr1>(k, p);
+                    key_max_step<kDppShr2>(k, p);
+                    key_max_step<kDppShr4>(k, p);
+                    key_max_step<kDppShr8>(k, p);
+                    if ((lane & 15) == 15 && (q >> 4) < kBigSamp) {
+                        S.sx[q >> 4] = k.x; S.sg[q >> 4] = k.g; S.sl[q >> 4] = k.l;
+                    }
+                    if (q < m) L.d[q] = 0;
+                }
+            }
+            __syncthreads();
+            PRK_BIG_T(9, tw0);
+            // 2. prefix maxima of the samples (4 a thread)
+            const int ns = (m + 15) >> 4;
+            LKey run{-INFINITY, -INFINITY, INT32_MIN};
+            for (int j = 4 * tid; j < min(4 * tid + 4, ns); ++j) {
+                const LKey s{S.sx[j], S.sg[j], S.sl[j]};
+                if (key_gt(s, run)) run = s;
+            }
+            LKey inc = run;
+            blk_key_prefix_max(R, inc);
+            S.px[tid] = inc.x; S.pg[tid] = inc.g; S.pl[tid] = inc.l;
+            __syncthreads();
+            LKey carry = tid ? LKey{S.px[tid - 1], S.pg[tid - 1], S.pl[tid - 1]} : LKey{-INFINITY, -INFINITY, INT32_MIN};
+            for (int j = 4 * tid; j < min(4 * tid + 4, ns); ++j) {
+                const LKey s{S.sx[j], S.sg[j], S.sl[j]};
+                if (key_gt(s, carry)) carry = s;
+                S.sx[j] = carry.x; S.sg[j] = carry.g; S.sl[j] = carry.l;
+            }
+            __syncthreads();
+            PRK_BIG_T(10, tw0);
+            // 3. gap of new edge tid: the first sample block whose prefix max
+            //    exceeds its key, then the first entry of that block that does
+            if (tid < kb) {
+                const LKey kc{S.nkx[c0 + tid], S.nkg[c0 + tid], S.nkl[c0 + tid]};
+                int lo = 0, hi = ns;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (key_gt(LKey{S.sx[mid], S.sg[mid], S.sl[mid]}, kc)) hi = mid;
+                    else lo = mid + 1;
+                }
+                gapc = m;
+                if (lo < ns) {
+                    const int q0 = lo << 4, qn = min(16, m - q0);
+                    float bx[16], bg[16];
+                    int32_t bl[16];
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) {
+                        const int q = q0 + min(u, qn - 1);
+                        bx[u] = X[q]; bg[u] = G[q]; bl[u] = LF[q];
+                    }
+                    int f = qn;
+#pragma unroll
+                    for (int u = 15; u >= 0; --u)
+                        if (u < qn && key_gt(entry_key(bx[u], bg[u], bl[u]), kc)) f = u;
+                    gapc = q0 + f;  // (f < qn: the block's maximum exceeds kc)
+                }
+            }
+        }
+        __syncthreads();
+        PRK_BIG_T(11, tw0);
+        // 4. the kept new edges counted per gap (d), each with its arrival
+        if (tid < kb) {
+            keptc = !expire || !(S.nky[c0 + tid] <= Row);
+            if (keptc) kr = atomicAdd(&L.d[gapc], 1);
+        }
+        __syncthreads();
+        PRK_BIG_T(12, tw0);
+    }
+    // 5. one scan over the entries q <= m (q = m: the tail gap): keep(q) and
+    //    d(q) sums; a kept entry q moves to  #kept before q + #new of gap <= q,
+    //    and gap q's new edges start at  base[q] = #kept before q + #new of gap < q
+    const bool cnt = kb > 0;
+    const int ns = m + (cnt ? 1 : 0), Ts = (ns + kBigThreads - 1) / kBigThreads;
+    int32_t vk[kBigU], vd[kBigU];
+    const bool regs = Ts <= kBigU;
+    auto load = [&](int t0) {
+#pragma unroll
+        for (int u = 0; u < kBigU; ++u) {
+            const int q = (t0 + u) * kBigThreads + tid;
+            vk[u] = 0;
+            vd[u] = 0;
+            if (t0 + u < Ts && q < ns) {
+                if (q < m) vk[u] = (!expire || !(YM[q] <= Row)) ? 1 : 0;
+                if (cnt) vd[u] = L.d[q];
+            }
+        }
+    };
+    if (regs) load(0);
+    for (int t0 = 0; t0 < Ts; t0 += kBigU) {
+        if (!regs) load(t0);
+#pragma unroll
+        for (int u = 0; u < kBigU; ++u) {
+            if (t0 + u >= Ts) break;
+            const int32_t sk = wave_incl_sum_i32(vk[u]), sd = wave_incl_sum_i32(vd[u]);
+            if (lane == 63) {
+                S.ts[(t0 + u) * kBigWaves + w] = sk;
+                S.tm[(t0 + u) * kBigWaves + w] = sd;
+            }
+        }
+    }
+    __syncthreads();
+    int32_t kept_old = 0, kept_new = 0;
+    {
+        const bool mine = tid < Ts * kBigWaves;
+        const int32_t a = mine ? S.ts[tid] : 0, b = mine ? S.tm[tid] : 0;
+        int32_t ea, eb;
+        blk_excl_sum2(R, a, b, ea, eb, kept_old, kept_new);
+        if (mine) { S.ts[tid] = ea; S.tm[tid] = eb; }
+    }
+    __syncthreads();
+    for (int t0 = 0; t0 < Ts; t0 += kBigU) {
+        if (!regs) load(t0);
+#pragma unroll
+        for (int u = 0; u < kBigU; ++u) {
+            if (t0 + u >= Ts) break;
+            const int q = (t0 + u) * kBigThreads + tid;
+            const int32_t sk = wave_incl_sum_i32(vk[u]), sd = wave_incl_sum_i32(vd[u]);
+            const int32_t before = S.ts[(t0 + u) * kBigWaves + w] + sk - vk[u];  // kept entries before q
+            const int32_t nex = S.tm[(t0 + u) * kBigWaves + w] + sd - vd[u];     // new edges of gap < q
+            if (q < m && vk[u]) {
+                const int32_t to = before + nex + vd[u];
+                B.x[to] = X[q]; B.g[to] = G[q]; B.left[to] = LF[q];
+                B.ymax[to] = YM[q]; B.wb[to] = WB[q];
+            }
+            if (cnt && q < ns) L.base[q] = before + nex;
+        }
+    }
+    __syncthreads();
+    PRK_BIG_T(13, tw0);
+    // 6. the kept new edges into their places: gap(c)'s block [base, base +
+    //    d) holds its new edges ordered by (key, arrival) -- the members meet
+    //    in that block (arrival slots), rank themselves, then move
+    if (cnt) {
+        int32_t bs = 0, h = 0;
+        if (tid < kb && keptc) {
+            bs = L.base[gapc];
+            h = L.d[gapc];
+            B.wb[bs + kr] = tid;
+        }
+        __syncthreads();
+        int32_t r = 0;
+        if (tid < kb && keptc) {
+            const LKey kc{S.nkx[c0 + tid], S.nkg[c0 + tid], S.nkl[c0 + tid]};
+            for (int32_t j = 0; j < h; ++j) {
+                const int32_t u = B.wb[bs + j];
+                if (u == tid) continue;
+                const LKey k{S.nkx[c0 + u], S.nkg[c0 + u], S.nkl[c0 + u]};
+                r += (key_gt(kc, k) || (!key_gt(k, kc) && u < tid)) ? 1 : 0;
+            }
+        }
+        __syncthreads();
+        if (tid < kb && keptc) {
+            const int32_t to = bs + r;
+            B.x[to] = S.nkx[c0 + tid]; B.g[to] = S.nkg[c0 + tid]; B.left[to] = S.nkl[c0 + tid];
+            B.ymax[to] = S.nky[c0 + tid]; B.wb[to] = S.nkw[c0 + tid];
+        }
+    }
+    __syncthreads();
+    PRK_BIG_T(14, tw0);
+    return kept_old + kept_new;
+}
+
+// Pairing (3751-3869) of the list in buffer cur (m entries) into buffer
+// cur ^ 1: every pair stepped, its first swap, the boundary swaps; `where`
+// codes for every entry (emit: slot j0 + k of pair k, sides 0 / 1; else
+// kBigNoEmit; an odd last entry kBigUnpaired, copied unstepped).
+__device__ __forceinline__ void big_pair(const BigList &L, int cur, int m, int32_t Row, bool emit, uint32_t j0,
+                         uint32_t *__restrict__ where) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int P = m >> 1, items = P + (m & 1);
+    const BigBuf A = L.buf(cur), B = L.buf(cur ^ 1);
+    const float *X = A.x, *G = A.g;
+    const int32_t *LF = A.left, *YM = A.ymax, *WB = A.wb;
+    for (int k0 = 0; k0 < items; k0 += kBigThreads) {
+        const int k = k0 + tid;
+        const bool pair = k < P;
+        // own pair (entries 2k, 2k + 1)
+        float xa = 0, xb = 0, ga = 0, gb = 0;
+        int32_t la = 0, lb = 0, ya = 0, yb = 0, wa = 0, wbb = 0;
+        if (k < items) {
+            xa = X[2 * k]; ga = G[2 * k]; la = LF[2 * k]; ya = YM[2 * k]; wa = WB[2 * k];
+            if (pair) { xb = X[2 * k + 1]; gb = G[2 * k + 1]; lb = LF[2 * k + 1]; yb = YM[2 * k + 1]; wbb = WB[2 * k + 1]; }
+        }
+        if (k < items && !pair) {  // the odd last entry: not paired, not stepped
+            B.x[2 * k] = xa; B.g[2 * k] = ga; B.left[2 * k] = la; B.ymax[2 * k] = ya; B.wb[2 * k] = wa;
+            where[wa + Row] = kBigUnpaired;
+        }
+        if (pair) {
+            where[wa + Row] = emit ? 2u * (j0 + (uint32_t)k) : kBigNoEmit;
+            where[wbb + Row] = emit ? 2u * (j0 + (uint32_t)k) + 1u : kBigNoEmit;
+        }
+        // stepped, then the first swap: f = the pair's first entry, s its second
+        const float sa = xa + ga, sb = xb + gb;
+        const bool s1 = sa > sb;
+        float fx = s1 ? sb : sa, fg = s1 ? gb : ga, sx = s1 ? sa : sb, sg = s1 ? ga : gb;
+        int32_t fl = s1 ? lb : la, fy = s1 ? yb : ya, fw = s1 ? wbb : wa;
+        int32_t sl = s1 ? la : lb, sy = s1 ? ya : yb, sw = s1 ? wa : wbb;
+        // pair k - 1's second and pair k + 1's first (lane shuffles; wave edges from memory)
+        float px = __shfl_up(sx, 1), pg = __shfl_up(sg, 1);
+        int32_t pl = __shfl_up(sl, 1), py = __shfl_up(sy, 1), pw = __shfl_up(sw, 1);
+        float nx = __shfl_down(fx, 1), ng = __shfl_down(fg, 1);
+        int32_t nl = __shfl_down(fl, 1), ny = __shfl_down(fy, 1), nw = __shfl_down(fw, 1);
+        if (pair && lane == 0 && k >= 1) {
+            const int a = 2 * k - 2;
+            const float ax = X[a] + G[a], bx = X[a + 1] + G[a + 1];
+            const int src = ax > bx ? a : a + 1;  // (the pair's second after its first swap)
+            px = X[src] + G[src]; pg = G[src]; pl = LF[src]; py = YM[src]; pw = WB[src];
+        }
+        if (pair && lane == 63 && k + 1 < P) {
+            const int a = 2 * k + 2;
+            const float ax = X[a] + G[a], bx = X[a + 1] + G[a + 1];
+            const int src = ax > bx ? a + 1 : a;  // (its first)
+            nx = X[src] + G[src]; ng = G[src]; nl = LF[src]; ny = YM[src]; nw = WB[src];
+        }
+        if (pair) {
+            const bool lo = k >= 1 && px > fx;      // 3843-3853 with pair k - 1
+            const bool hi = k + 1 < P && sx > nx;   // and with pair k + 1
+            const int e0 = 2 * k, e1 = 2 * k + 1;
+            B.x[e0] = lo ? px : fx; B.g[e0] = lo ? pg : fg; B.left[e0] = lo ? pl : fl;
+            B.ymax[e0] = lo ? py : fy; B.wb[e0] = lo ? pw : fw;
+            B.x[e1] = hi ? nx : sx; B.g[e1] = hi ? ng : sg; B.left[e1] = hi ? nl : sl;
+            B.ymax[e1] = hi ? ny : sy; B.wb[e1] = hi ? nw : sw;
+        }
+    }
+    __syncthreads();
+}
+
+// One workgroup per huge object: its list in the pool slice at big_off
+// (kBigListArrays arrays of big_cap + 2 ints, big_cap >= its most active
+// entries), its where codes at where + woff[edge] (rows [YMin, min(YMax,
+// MaxY)) of each edge).
+__global__ void __launch_bounds__(kBigThreads) k_obj_walk_big(FrameParams fp, const ObjDesc *__restrict__ objs,
+                                                             const uint32_t *__restrict__ big,
+                                                             const unsigned long long *__restrict__ big_off,
+                                                             const uint32_t *__restrict__ big_cap,
+                                                             int32_t *__restrict__ pool,
+                                                             const uint32_t *__restrict__ escan,
+                                                             const uint32_t *__restrict__ total0p,
+                                                             const ObjEdge *__restrict__ work,
+                                                             const uint32_t *__restrict__ woff,
+                                                             const unsigned long long *__restrict__ soff,
+                                                             uint32_t *__restrict__ where, uint32_t *__restrict__ err,
+                                                             const uint32_t *__restrict__ prstat) {
+    __shared__ BigLds S;
+    __shared__ BlockRed R;
+    const uint32_t o = big[blockIdx.x];
+    if (prstat && prstat[o] == kPrDone) return;  // walked by rows (k_pr_*)
+    const ObjDesc od = objs[o];
+    const uint32_t bound = (uint32_t)(soff[o + 1] - soff[o]);
+    uint32_t e0, n;
+    obj_range(od, escan, *total0p, e0, n);
+    if (n == 0) return;
+    const ObjEdge *E = work + e0;
+    const uint32_t *WO = woff + e0;
+    const uint32_t cap = min(big_cap[blockIdx.x], kBigMaxM);
+    BigList L;
+    L.carve(pool + big_off[blockIdx.x], cap);
+    const int tid = threadIdx.x;
+    int32_t mr = INT32_MIN;
+    for (uint32_t i = tid; i < n; i += kBigThreads) mr = max(mr, E[i].YMax);
+    const int32_t MaxY = min(min(blk_max(R, mr), fp.H), fp.row1);
+    const int32_t FirstRow = E[0].YMin;
+    const int32_t RowLo = fp.draws[od.draw].mode != MODE_AVX ? fp.row0 - 1 : fp.row0;
+    int cur = 0, m = 0;
+    uint32_t ins = 0, emitted = 0;
+    bool bad = false;
+    unsigned long long wpa[16] = {}, *wp = PRK_WPROF && tid == 0 ? wpa : nullptr;
+    unsigned long long tw0 = PRK_WT(), twall = tw0;
+    for (int32_t Row = FirstRow; Row < MaxY; ++Row) {
+        bool expired = false;
+        if (PRK_WPROF && wp) wp[3] += 1;
+        for (;;) {  // the row's new edges, a window of kBigThreads at a time (3654-3713)
+            const uint32_t i = ins + (uint32_t)tid;
+            int32_t y = INT32_MAX;
+            float x = 0.0f, g = 0.0f;
+            int32_t l = 0, ym = 0, wbv = 0;
+            if (i < n) {
+                const ObjEdge &C = E[i];
+                y = C.YMin; x = C.X; g = C.G; l = C.Left; ym = C.YMax;
+                wbv = (int32_t)WO[i] - y;
+            }
+            int32_t lt, kb, nanc;
+            blk_sum3(R, y < Row ? 1 : 0, y == Row ? 1 : 0, (y == Row && (x != x || g != g)) ? 1 : 0, lt, kb, nanc);
+            if (lt) {  // (never past the first row of a sorted list)
+                ins += (uint32_t)lt;
+                continue;
+            }
+            if (kb == 0) break;
+            if ((uint32_t)(m + kb) > cap) {  // (never: cap >= the most listed entries)
+                bad = true;
+                break;
+            }
+            if (tid < kb) {
+                S.nkx[tid] = x; S.nkg[tid] = g; S.nkl[tid] = l; S.nky[tid] = ym; S.nkw[tid] = wbv;
+            }
+            __syncthreads();
+            PRK_BIG_T(0, tw0);
+            if (PRK_WPROF && wp) { wp[4] += 1; wp[8] += (unsigned)kb; }
+            const bool last = kb < kBigThreads;
+            if (nanc) {  // one edge at a time (no total order on a batch with a NaN key)
+                for (int t = 0; t < kb; ++t) {
+                    const bool ex = last && t + 1 == kb;
+                    m = big_insert_expire(L, S, R, cur, m, t, 1, ex, Row, wp);
+                    cur ^= 1;
+                }
+            } else {
+                m = big_insert_expire(L, S, R, cur, m, 0, kb, last, Row, wp);
+                cur ^= 1;
+            }
+            PRK_BIG_T(1, tw0);
+            expired = last;
+            ins += (uint32_t)kb;
+            if (last) break;
+        }
+        if (bad) break;
+        if (!expired && m > 0) {  // expiry 3715-3749 alone
+            m = big_insert_expire(L, S, R, cur, m, 0, 0, true, Row, wp);
+            cur ^= 1;
+        }
+        PRK_BIG_T(2, tw0);
+        if (m == 0) {  // nothing happens on the rows before the next insertion: go there
+            if (ins >= n) break;
+            Row = max(Row, E[ins].YMin - 1);
+            continue;
+        }
+        const bool emit = Row >= RowLo;
+        const uint32_t P = (uint32_t)(m >> 1);
+        if (emit && emitted + P > bound) {  // (never: the bound holds every pair)
+            bad = true;
+            break;
+        }
+        big_pair(L, cur, m, Row, emit, emitted, where);
+        cur ^= 1;
+        if (emit) emitted += P;
+        PRK_BIG_T(5, tw0);
+        if (PRK_WPROF && wp) wp[6] += (unsigned)m;
+    }
+    if (bad && tid == 0) atomicOr(err, 1u);
+    if (PRK_WPROF && wp) {
+        wp[7] += PRK_WT() - twall;
+        for (int k = 0; k < 16; ++k) atomicAdd(fp.prof + k, wp[k]);
+    }
+}
+
+// The rows every edge of the huge objects is listed on (rows [YMin,
+// min(YMax, H, row1)) = [YMin, min(YMax, MaxY))), into cnt[edge] (their scan
+// is woff).  Grid (edges / 256, objects).
+__global__ void k_big_rows(FrameParams fp, const ObjDesc *__restrict__ objs, const uint32_t *__restrict__ big,
+                           const uint32_t *__restrict__ escan, const uint32_t *__restrict__ total0p,
+                           const ObjEdge *__restrict__ work, uint32_t *__restrict__ cnt) {
+    const ObjDesc od = objs[big[blockIdx.y]];
+    uint32_t e0, n;
+    obj_range(od, escan, *total0p, e0, n);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const ObjEdge &e = work[e0 + i];
+    cnt[e0 + i] = (uint32_t)max(0, min(min(e.YMax, fp.H), fp.row1) - e.YMin);
+}
+
+// Every edge of the huge objects replayed: on each row it was paired on, its
+// state into its side of the pair's PairRaw (side 0 also the SpanPos and the
+// winner id), then stepped (3811-3829).  Grid (edges / 256, objects).
+template <int M>
+__global__ void k_big_emit(FrameParams fp, const ObjDesc *__restrict__ objs, const uint32_t *__restrict__ big,
+                           const uint32_t *__restrict__ escan, const uint32_t *__restrict__ total0p,
+                           const ObjEdge *__restrict__ work, const uint32_t *__restrict__ woff,
+                           const uint32_t *__restrict__ where, const unsigned long long *__restrict__ soff,
+                           PairRaw *__restrict__ raw, SpanPos *__restrict__ pos, uint32_t *__restrict__ span_tri,
+                           const uint32_t *__restrict__ prstat) {
+    const uint32_t o = big[blockIdx.y];
+    if (prstat && prstat[o] == kPrDone) return;
+    const ObjDesc od = objs[o];
+    if (fp.draws[od.draw].mode != M) return;
+    uint32_t e0, n;
+    obj_range(od, escan, *total0p, e0, n);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    ObjEdge e = work[e0 + i];
+    const int32_t r1 = min(min(e.YMax, fp.H), fp.row1);
+    if (e.YMin >= r1) return;
+    const uint32_t base = (uint32_t)soff[o], bound = (uint32_t)(soff[o + 1] - soff[o]);
+    const uint32_t *wh = where + woff[e0 + i];
+    for (int32_t r = e.YMin; r < r1; ++r) {
+        const uint32_t c = wh[r - e.YMin];
+        if (c == kBigUnpaired) continue;
+        if (c != kBigNoEmit && (c >> 1) < bound) {
+            const uint32_t at = base + (c >> 1);
+            if (c & 1u) {
+                raw[at].r0 = make_float4(e.X, e.Z, e.W, e.U);
+                raw[at].r1 = make_float4(e.V, e.N0, e.N1, e.N2);
+                raw[at].r2 = make_float4(e.C0, e.C1, e.C2, e.C3);
+            } else {
+                raw[at].l0 = make_float4(e.X, e.Z, e.W, e.U);
+                raw[at].l1 = make_float4(e.V, e.N0, e.N1, e.N2);
+                raw[at].l2 = make_float4(e.C0, e.C1, e.C2, e.C3);
+                pos[at] = SpanPos{r, (int32_t)od.draw, 0, SPAN_RAW};
+                span_tri[at] = od.g0;
+            }
+        }
+        obj_step<M>(e);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // The chunked walk of large objects (objects of kObjWaveTris triangles or
 // more whose rows and lists fit: k_obj_maxact's sizes, host-checked).
 //
@@ -2935,6 +3455,56 @@ hipError_t prk_obj_walk_group(const prk::FrameParams *fp, int32_t mode, uint32_t
         PRK_WALK_WAVE(prk::MODE_SC_PHONG)
         PRK_WALK_WAVE(prk::MODE_SC_PHONG_TEX)
 #undef PRK_WALK_WAVE
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+// The huge-object walk (k_obj_walk_big): cnt[edge] = its listed rows, for
+// the edges of big[0, nbig) (the rest of cnt untouched; woff = its exclusive
+// scan) ...
+uint32_t prk_big_max_entries(void) { return prk::kBigMaxM; }
+uint32_t prk_big_list_arrays(void) { return (uint32_t)prk::kBigListArrays; }
+hipError_t prk_big_rows(const prk::FrameParams *fp, const void *objs, const uint32_t *big, uint32_t nbig,
+                        uint32_t max_edges, const uint32_t *escan, const uint32_t *total0p, const void *work,
+                        uint32_t *cnt, hipStream_t s) {
+    if (nbig == 0 || max_edges == 0) return hipSuccess;
+    if (nbig > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(prk::k_big_rows, dim3((max_edges + 255) / 256, nbig), dim3(256), 0, s, *fp,
+                       reinterpret_cast<const prk::ObjDesc *>(objs), big, escan, total0p,
+                       reinterpret_cast<const prk::ObjEdge *>(work), cnt);
+    return hipGetLastError();
+}
+// ... then the walk of the objects big[0, nbig) of mode `mode` (lists in the
+// pool at big_off, big_cap entries; where codes at where + woff[edge], every
+// code kBigUnpaired beforehand) and the replay of their edges into PairRaw
+// slots soff[o] + j (k_span_finish sets the spans up).
+hipError_t prk_big_walk(const prk::FrameParams *fp, int32_t mode, const void *objs, const uint32_t *big,
+                        const unsigned long long *big_off, const uint32_t *big_cap, uint32_t nbig,
+                        uint32_t max_edges, int32_t *pool, const uint32_t *escan, const uint32_t *total0p,
+                        const void *work, const uint32_t *woff, const unsigned long long *soff, uint32_t *where,
+                        void *raw, void *pos, uint32_t *span_tri, uint32_t *err, const uint32_t *prstat,
+                        hipStream_t s) {
+    if (nbig == 0 || max_edges == 0) return hipSuccess;
+    if (nbig > 65535) return hipErrorInvalidValue;
+    const prk::ObjDesc *O = reinterpret_cast<const prk::ObjDesc *>(objs);
+    const prk::ObjEdge *W = reinterpret_cast<const prk::ObjEdge *>(work);
+    hipLaunchKernelGGL(prk::k_obj_walk_big, dim3(nbig), dim3(prk::kBigThreads), 0, s, *fp, O, big, big_off, big_cap,
+                       pool, escan, total0p, W, woff, soff, where, err, prstat);
+    const dim3 g((max_edges + 255) / 256, nbig), b(256);
+    prk::PairRaw *R = reinterpret_cast<prk::PairRaw *>(raw);
+    prk::SpanPos *P = reinterpret_cast<prk::SpanPos *>(pos);
+    switch (mode) {
+#define PRK_BIG_EMIT(MM)                                                                                       \
+    case MM:                                                                                                   \
+        hipLaunchKernelGGL(prk::k_big_emit<MM>, g, b, 0, s, *fp, O, big, escan, total0p, W, woff, where, soff, \
+                           R, P, span_tri, prstat);                                                            \
+        break;
+        PRK_BIG_EMIT(prk::MODE_AVX)
+        PRK_BIG_EMIT(prk::MODE_SC_GOURAUD)
+        PRK_BIG_EMIT(prk::MODE_SC_GOURAUD_TEX)
+        PRK_BIG_EMIT(prk::MODE_SC_PHONG)
+        PRK_BIG_EMIT(prk::MODE_SC_PHONG_TEX)
+#undef PRK_BIG_EMIT
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

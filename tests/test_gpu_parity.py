@@ -934,6 +934,38 @@ def test_whole_object_long_active_lists(gpu, sem):
              label="long lists sem=%d" % sem)
 
 
+@pytest.mark.parametrize("sem", [abi.PRK_SEM_AVX, abi.PRK_SEM_AVX_ST, abi.PRK_SEM_SCALAR])
+def test_whole_object_big_walk(gpu, sem, monkeypatch):
+    """The huge-object walk (prk_spans.hip k_obj_walk_big: one workgroup over
+    a list in device memory, the spans set up afterwards from a replay of
+    every edge) forced onto objects that would fit LDS (PRK_OBJ_BIG_MIN=0,
+    PRK_OBJ_ROWS=0): ConstructSphere as one object, overlapping 700- and
+    64-triangle objects with ties and clipping on every side (odd rows: an
+    unpaired last entry), a row band (rows above it paired, not emitted) —
+    against the oracle and the one-wave walk (PRK_OBJ_BIG=0), bit for bit."""
+    monkeypatch.setenv("PRK_OBJ_BIG_MIN", "0")
+    monkeypatch.setenv("PRK_OBJ_ROWS", "0")
+    sph = _sphere_scene()
+    soup = scenes.with_ties(scenes.random_soup(2800, 384, 256, radius=40, seed=23, centroid_margin=40), seed=23)
+    if sem == abi.PRK_SEM_SCALAR:
+        sph.texture = None
+        soup.texture = None
+    for s, tpo in ((sph, sph.tri_count), (soup, 700), (soup, 64)):
+        label = "big walk %s tpo=%d sem=%d" % (s.name, tpo, sem)
+        g, o = run_both(s, semantics=sem, phong=True, tris_per_object=tpo, threads=1, label=label)
+        monkeypatch.setenv("PRK_OBJ_BIG", "0")
+        w = prk.render_scene(s, semantics=sem, phong=True, tris_per_object=tpo)
+        monkeypatch.delenv("PRK_OBJ_BIG")
+        for k in range(3):
+            assert np.array_equal(g[k].view(np.uint32), w[k].view(np.uint32)), (label, k)
+    oc, oz, ow, _ = O.render(soup, semantics=sem, phong=True, threads=1, tris_per_object=700)
+    r0, r1 = 61, 190
+    gc, gz, gw, _ = prk.render_scene(soup, semantics=sem, phong=True, tris_per_object=700, rows=(r0, r1))
+    assert (gz.view(np.uint32) == oz[r0:r1].view(np.uint32)).all()
+    assert (gc == oc[r0:r1]).all()
+    assert (gw == ow[r0:r1]).all()
+
+
 def test_whole_object_mid_lists_lds(gpu):
     """Objects whose lists stay in LDS (<= 4096 edges per object) while
     several hundred edges enter per row: the batched insertion in LDS."""
