@@ -75,13 +75,11 @@ hipError_t prk_obj_walk_group(const prk::FrameParams *, int32_t, uint32_t, const
                               const uint32_t *, void *, const unsigned long long *, void *, void *, void *, void *,
                               uint32_t *, uint32_t *, const uint32_t *, hipStream_t);
 uint32_t prk_big_max_entries(void);
-uint32_t prk_big_list_arrays(void);
-hipError_t prk_big_rows(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, uint32_t, const uint32_t *,
-                        const uint32_t *, const void *, uint32_t *, hipStream_t);
+uint64_t prk_big_slice_ints(uint32_t, uint32_t, uint32_t);
 hipError_t prk_big_walk(const prk::FrameParams *, int32_t, const void *, const uint32_t *, const unsigned long long *,
-                        const uint32_t *, uint32_t, uint32_t, int32_t *, const uint32_t *, const uint32_t *,
-                        const void *, const uint32_t *, const unsigned long long *, uint32_t *, void *, void *,
-                        uint32_t *, uint32_t *, const uint32_t *, hipStream_t);
+                        const uint32_t *, const uint32_t *, uint32_t, uint32_t, int32_t *, const uint32_t *,
+                        const uint32_t *, const void *, const unsigned long long *, void *, void *, uint32_t *,
+                        uint32_t *, const uint32_t *, hipStream_t);
 hipError_t prk_pr_walk_begin(const prk::FrameParams *, const prk::PrWalkArgs *, hipStream_t);
 hipError_t prk_pr_walk_group(const prk::FrameParams *, const prk::PrWalkArgs *, int32_t, uint32_t, const uint32_t *,
                              uint32_t, uint32_t, hipStream_t);
@@ -298,7 +296,7 @@ struct prk_context {
             d_keys_b, d_vals_b, d_offs, d_nwin, d_wtag, d_srecs, d_work, d_ekeys, d_ekeys2, d_evals, d_ecnt, d_escan,
             d_rcnt, d_rscan, d_bound, d_oslot, d_pool, d_err, d_raw, d_most, d_cls, d_prrow, d_prcnt, d_preoff,
             d_prfge, d_prccur, d_prkey, d_prest, d_prsst, d_preend, d_preendm, d_prmatch, d_prsidx, d_prsm, d_prstat,
-            d_segcnt, d_segoff, d_segs, d_wy, d_bcnt, d_bwoff, d_where;
+            d_segcnt, d_segoff, d_segs, d_wy;
         // the pass's host tables, packed into pinned memory for one upload
         // (stage_ev: that upload, before the staging is rewritten)
         char *h_stage = nullptr;
@@ -499,7 +497,7 @@ int prk_destroy(prk_context *c) {
                         &S.d_raw, &S.d_most, &S.d_cls, &S.d_prrow, &S.d_prcnt, &S.d_preoff, &S.d_prfge,
                         &S.d_prccur, &S.d_prkey, &S.d_prest, &S.d_prsst, &S.d_preend, &S.d_preendm,
                         &S.d_prmatch, &S.d_prsidx, &S.d_prsm, &S.d_prstat, &S.d_segcnt, &S.d_segoff,
-                        &S.d_segs, &S.d_wy, &S.d_bcnt, &S.d_bwoff, &S.d_where};
+                        &S.d_segs, &S.d_wy};
         for (DevBuf *b : sb) b->release();
         if (S.h_rb) (void)hipHostFree(S.h_rb);
         if (S.stage_ev) {
@@ -1848,7 +1846,8 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     // per large object: most, rows, entries (12, k_obj_maxact) | big (4) |
     // off (8) | cap (4) | the chunked walk's table (32, prk_spans.hip PrObj)
     // and groups (4)
-    const size_t cls_bytes = (size_t)nbig_all * 64 + 64;
+    // | the huge walk's (rows, ents) (8)
+    const size_t cls_bytes = (size_t)nbig_all * 72 + 64;
     if (cls_bytes > S.cls_cap) {
         if (S.h_cls) (void)hipHostFree(S.h_cls);
         S.h_cls = nullptr;
@@ -1884,7 +1883,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
         int32_t mode;
         uint32_t lcap, start, count;
         bool big;             // the huge-object walk (k_obj_walk_big)
-        uint32_t max_edges;   // (big: its objects' most edges)
+        uint32_t max_rows;    // (big: its objects' most rows)
     };
     std::vector<Group> groups;
     uint32_t *cls_big = reinterpret_cast<uint32_t *>(S.h_cls + (size_t)nbig_all * 12);
@@ -1892,12 +1891,12 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     uint32_t *cls_cap = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(cls_off) + (size_t)nbig_all * 8);
     uint32_t *cls_pr = cls_cap + nbig_all;  // PrObj[npr] (8 words each)
     uint32_t *cls_grp = cls_pr + 8 * (size_t)nbig_all;  // its objects grouped by (mode, LDS capacity)
+    uint32_t *cls_meta = cls_grp + nbig_all;           // (rows, ents) per object, walk-group order
     // Objects whose lists outgrow LDS take the huge-object walk (a
     // workgroup, the list in device memory: k_obj_walk_big) when their sizes
     // are known (k_obj_maxact) and fit it, else one wave each (k_obj_walk_wave).
     // PRK_OBJ_BIG=0: always the wave; PRK_OBJ_BIG_MIN=n (tests): objects of
     // more than n active edges skip the LDS lists.
-    uint64_t where_n = 0;  // the huge walk's (edge, row) codes
     {
         const char *benv = std::getenv("PRK_OBJ_BIG"), *menv = std::getenv("PRK_OBJ_BIG_MIN");
         const bool big_on = !(benv && benv[0] == '0');
@@ -1911,7 +1910,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
                 const uint32_t capc = ci < 5 ? kCaps[ci] : 0u;
                 if (ci < 5 && capc > lcap) continue;
                 const uint32_t start = k;
-                uint32_t gmax = 0;
+                uint32_t gmax = 0;  // (the huge walk: its objects' most rows)
                 for (uint32_t i = 0; i < bigm[mo].size(); ++i) {
                     const uint32_t bi = b0 + i;
                     const int32_t most = h_most[bi];
@@ -1922,21 +1921,24 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
                             break;
                         }
                     if (want != capc) continue;
+                    const int32_t rows = h_rows[bi], ents = h_ents[bi];
                     if (ci >= 5) {
-                        const int32_t rows = h_rows[bi], ents = h_ents[bi];
                         const bool hb = big_on && most > 0 && (uint32_t)most <= prk_big_max_entries() && rows > 0 &&
                                         rows < INT32_MAX && ents >= 0 && ents < INT32_MAX &&
-                                        where_n + (uint64_t)ents < 0x7FFFFFFFull && bigm[mo].size() <= 65535;
+                                        bigm[mo].size() <= 65535;
                         if (hb != (ci == 5)) continue;
-                        if (hb) where_n += (uint64_t)ents;
                     }
+                    const uint32_t cap = ci == 5 ? (uint32_t)most : bige[mo][i];
+                    if (ci == 5) pool = (pool + 3) & ~3ull;  // (16-B aligned slices)
                     cls_big[k] = bigm[mo][i];
                     cls_off[k] = capc ? 0ull : pool;
-                    const uint32_t cap = ci == 5 ? (uint32_t)most : bige[mo][i];
                     cls_cap[k] = capc ? 0u : cap;
+                    cls_meta[2 * k] = ci == 5 ? (uint32_t)rows : 0u;
+                    cls_meta[2 * k + 1] = ci == 5 ? (uint32_t)ents : 0u;
                     if (!capc)
-                        pool += (uint64_t)(ci == 5 ? prk_big_list_arrays() : kWaveListArrays) * (cap + 2);
-                    gmax = std::max(gmax, bige[mo][i]);
+                        pool += ci == 5 ? prk_big_slice_ints(cap, (uint32_t)rows, (uint32_t)ents)
+                                        : (uint64_t)kWaveListArrays * (cap + 2);
+                    if (ci == 5) gmax = std::max(gmax, (uint32_t)rows);
                     ++k;
                 }
                 if (k > start) groups.push_back(Group{mo, capc, start, k - start, ci == 5, gmax});
@@ -2006,12 +2008,12 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
             b += (uint32_t)bigm[mo].size();
         }
     }
-    const uint32_t *d_cbig = nullptr, *d_ccap = nullptr;
+    const uint32_t *d_cbig = nullptr, *d_ccap = nullptr, *d_cmeta = nullptr;
     const unsigned long long *d_coff = nullptr;
     const void *d_cpr = nullptr;
     const uint32_t *d_cgrp = nullptr;
     if (nbig_all) {
-        const size_t lo = (size_t)nbig_all * 12, hi = reinterpret_cast<char *>(cls_grp + npr) - S.h_cls;
+        const size_t lo = (size_t)nbig_all * 12, hi = reinterpret_cast<char *>(cls_meta + 2 * (size_t)nbig_all) - S.h_cls;
         PRK_TRY(S.d_cls.ensure(hi));
         PRK_TRY(hipMemcpyAsync(static_cast<char *>(S.d_cls.p) + lo, S.h_cls + lo, hi - lo, hipMemcpyHostToDevice, s));
         d_cbig = reinterpret_cast<const uint32_t *>(static_cast<char *>(S.d_cls.p) + lo);
@@ -2022,6 +2024,8 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
         d_cpr = static_cast<char *>(S.d_cls.p) + (reinterpret_cast<char *>(cls_pr) - S.h_cls);
         d_cgrp = reinterpret_cast<const uint32_t *>(static_cast<char *>(S.d_cls.p) +
                                                     (reinterpret_cast<char *>(cls_grp) - S.h_cls));
+        d_cmeta = reinterpret_cast<const uint32_t *>(static_cast<char *>(S.d_cls.p) +
+                                                     (reinterpret_cast<char *>(cls_meta) - S.h_cls));
         if (pool) PRK_TRY(S.d_pool.ensure(pool * 4));
     }
     const uint32_t *d_prstat = nullptr;
@@ -2110,28 +2114,11 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(prk_obj_walk(&fp, d_objs, nobj, escan, total0p, S.d_work.p, oslot, S.d_recs.p,
                          scalar ? S.d_srecs.p : nullptr, S.d_pos.p, (uint32_t *)S.d_span_tri.p, d_spans_in,
                          (uint32_t *)S.d_err.p, thread_links ? 1 : 0, d_segs, d_nseg, (uint32_t)max_segs, s));
-    uint32_t *d_bwoff = nullptr;
-    if (where_n) {  // the huge walk's where-code offsets (per edge) and codes
-        PRK_TRY(S.d_bcnt.ensure(((size_t)nwork + 1) * 4));
-        PRK_TRY(S.d_bwoff.ensure(((size_t)nwork + 1) * 4));
-        PRK_TRY(S.d_where.ensure((size_t)where_n * 4));
-        uint32_t *bcnt = (uint32_t *)S.d_bcnt.p;
-        d_bwoff = (uint32_t *)S.d_bwoff.p;
-        PRK_TRY(hipMemsetAsync(bcnt, 0, ((size_t)nwork + 1) * 4, s));
-        for (const Group &g : groups)
-            if (g.big)
-                PRK_TRY(prk_big_rows(&fp, d_objs, d_cbig + g.start, g.count, g.max_edges, escan, total0p, S.d_work.p,
-                                     bcnt, s));
-        PRK_TRY(prk_scan_u32(bcnt, d_bwoff, nwork + 1, nullptr, &tb, s));
-        PRK_TRY(temp(tb));
-        PRK_TRY(prk_scan_u32(bcnt, d_bwoff, nwork + 1, S.d_temp.p, &tb, s));
-        PRK_TRY(hipMemsetAsync(S.d_where.p, 0xFF, (size_t)where_n * 4, s));  // (kBigUnpaired: never listed)
-    }
     for (const Group &g : groups) {
         if (g.big)
-            PRK_TRY(prk_big_walk(&fp, g.mode, d_objs, d_cbig + g.start, d_coff + g.start, d_ccap + g.start, g.count,
-                                 g.max_edges, (int32_t *)S.d_pool.p, escan, total0p, S.d_work.p, d_bwoff, oslot,
-                                 (uint32_t *)S.d_where.p, S.d_raw.p, S.d_pos.p, (uint32_t *)S.d_span_tri.p,
+            PRK_TRY(prk_big_walk(&fp, g.mode, d_objs, d_cbig + g.start, d_coff + g.start, d_ccap + g.start,
+                                 d_cmeta + 2 * (size_t)g.start, g.count, g.max_rows, (int32_t *)S.d_pool.p, escan,
+                                 total0p, S.d_work.p, oslot, S.d_raw.p, S.d_pos.p, (uint32_t *)S.d_span_tri.p,
                                  (uint32_t *)S.d_err.p, d_prstat, s));
         else
             PRK_TRY(prk_obj_walk_group(&fp, g.mode, g.lcap, d_objs, d_cbig + g.start, d_coff + g.start,

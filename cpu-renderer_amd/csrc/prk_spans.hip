@@ -2122,7 +2122,7 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_obj_walk_wave(FrameParams f
 // workgroup walk's LDS list, up to kBigMaxM of them; C3b as ONE object holds
 // ~16 k edges a row).  One workgroup of kBigThreads walks the object's rows
 // in order (3615-3869) with its list in device memory: two SoA buffers of
-// (X, Gradient, Left, YMax, where-base) in list order, each list operation a
+// (X, Gradient, Left, YMax, edge index) in list order, each list operation a
 // few workgroup-wide passes (entry q of a pass: thread q % kBigThreads, tile
 // q / kBigThreads), every scan a DPP wave scan + the waves' totals in LDS:
 //   insertion + expiry (3654-3749), one scan: a batch of new edges (<=
@@ -2142,13 +2142,15 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_obj_walk_wave(FrameParams f
 //     (3831-3841) and both boundary swaps (3843-3853; the neighbours' fields
 //     through lane shuffles, from memory at wave edges), and writes its two
 //     entries' final places.
-// The walk sets up no span.  For every (edge, row) the edge is listed on it
-// writes a code into `where` (the edge's rows at woff[edge]): its pair slot
-// and side, "paired, not emitted" (rows above the band) or "unpaired" (an odd
-// last entry: not stepped).  k_big_emit then replays every edge, a thread
-// each, stepped row by row as the walk steps it (obj_step on its paired
-// rows), into its side of each pair's PairRaw; k_span_finish sets the spans
-// up as it does the chunked walk's.
+// The walk sets up no span.  Per row it leaves the list it pairs (the edges'
+// indices in list order, `ids`), the row's first slot (or "not emitted":
+// rows above the band) and its unpaired odd last entry, if any (not stepped).
+// k_big_replay then sets up every pair of every row at once, a thread per
+// pair: both edges replayed from their FillEdgeTable state, stepped on every
+// row they were listed on before this one but the unpaired ones (obj_step,
+// 3811-3829), into the pair's PairRaw; k_span_finish sets the spans up as it
+// does the chunked walk's.  The pairing also leaves the next row's per-16 key
+// maxima in LDS, so a row's insertion reads the list once.
 // ---------------------------------------------------------------------------
 constexpr int kBigThreads = 1024;
 constexpr int kBigWaves = kBigThreads / 64;
@@ -2156,31 +2158,45 @@ constexpr int kBigMaxTiles = 64;
 constexpr uint32_t kBigMaxM = (uint32_t)kBigMaxTiles * kBigThreads - 2;  // list entries (and the pool stride - 2)
 constexpr int kBigSamp = kBigMaxTiles * kBigThreads / 16;                // per-16 maxima
 constexpr int kBigU = 8;                                                 // tiles a pass keeps in registers
-constexpr int kBigListArrays = 12;  // 2 x (x, g, left, ymax, wb) + d + base, cap + 2 int32 each
-constexpr uint32_t kBigUnpaired = 0xFFFFFFFFu, kBigNoEmit = 0xFFFFFFFEu;
+constexpr int kBigListArrays = 12;  // 2 x (x, g, left, ymax, ei) + d + base, big_stride(cap) int32 each
+constexpr uint32_t kBigNoEmit = 0xFFFFFFFEu;  // a row above the band: paired, no spans
 
+// Each array of a huge object's pool slice: cap + 2 ints, rounded up to 16 B
+// (the slice itself starts 16-B aligned: vector loads of 4 / 2 entries).
+__host__ __device__ constexpr size_t big_stride(uint32_t cap) { return ((size_t)cap + 2 + 3) & ~(size_t)3; }
 struct BigBuf {  // one list buffer, in list order
     float *x, *g;
-    int32_t *left, *ymax, *wb;
+    int32_t *left, *ymax, *ei;  // (ei: the edge's index in the object's sorted edges)
 };
+// A huge object's pool slice: the list buffers, d and base (kBigListArrays
+// arrays of big_stride(cap) ints), a header (FirstRow, rows), per row
+// (off, m, j0, unp): its list's place in ids, its length, its first slot
+// (kBigNoEmit: none) and its unpaired entry (-1: none), then ids.
+__host__ __device__ constexpr uint64_t big_slice_ints(uint32_t cap, uint32_t rows, uint32_t ents) {
+    return ((uint64_t)kBigListArrays * big_stride(cap) + 4 + 4ull * rows + ents + 3) & ~3ull;
+}
 struct BigList {
     BigBuf b0, b1;
     int32_t *d;     // the batch's kept new edges per gap
     int32_t *base;  // where each gap's new edges begin
-    __device__ __forceinline__ void carve(int32_t *base, uint32_t cap) {
-        const size_t s = (size_t)cap + 2;
-        b0 = BigBuf{reinterpret_cast<float *>(base), reinterpret_cast<float *>(base + s), base + 2 * s, base + 3 * s,
-                    base + 4 * s};
-        int32_t *p = base + 5 * s;
+    int32_t *hdr, *ri, *ids;
+    __device__ __forceinline__ void carve(int32_t *p0, uint32_t cap, uint32_t rows) {
+        const size_t s = big_stride(cap);
+        int32_t *p = p0;
+        b0 = BigBuf{reinterpret_cast<float *>(p), reinterpret_cast<float *>(p + s), p + 2 * s, p + 3 * s, p + 4 * s};
+        p = p0 + 5 * s;
         b1 = BigBuf{reinterpret_cast<float *>(p), reinterpret_cast<float *>(p + s), p + 2 * s, p + 3 * s, p + 4 * s};
-        d = base + 10 * s;
-        this->base = base + 11 * s;
+        d = p0 + 10 * s;
+        base = p0 + 11 * s;
+        hdr = p0 + (size_t)kBigListArrays * s;
+        ri = hdr + 4;
+        ids = ri + 4 * (size_t)rows;
         static_assert(kBigListArrays == 12, "carve cuts kBigListArrays arrays");
     }
     // (selects, not an indexed pair: an indexed pointer array went to scratch)
     __device__ __forceinline__ BigBuf buf(int c) const {
         return BigBuf{c ? b1.x : b0.x, c ? b1.g : b0.g, c ? b1.left : b0.left, c ? b1.ymax : b0.ymax,
-                      c ? b1.wb : b0.wb};
+                      c ? b1.ei : b0.ei};
     }
 };
 struct BigLds {
@@ -2190,7 +2206,7 @@ struct BigLds {
     float px[kBigThreads], pg[kBigThreads];  // per-thread key maxima (the sample scan)
     int32_t pl[kBigThreads];
     float nkx[kBigThreads], nkg[kBigThreads];  // the row's new edges (a window of kBigThreads)
-    int32_t nkl[kBigThreads], nky[kBigThreads], nkw[kBigThreads];
+    int32_t nkl[kBigThreads], nky[kBigThreads], nke[kBigThreads];
 };
 
 // Insertion of the new edges S.nk*[c0, c0 + kb) into the list (buffer cur,
@@ -2205,20 +2221,22 @@ struct BigLds {
         }                                                  \
     } while (0)
 __device__ __forceinline__ int big_insert_expire(const BigList &L, BigLds &S, BlockRed &R, int cur, int m, int c0, int kb,
-                                                 bool expire, int32_t Row, unsigned long long *wp = nullptr) {
+                                                 bool expire, int32_t Row, bool samples_ready,
+                                                 unsigned long long *wp = nullptr) {
     unsigned long long tw0 = PRK_WT();
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int T = (m + kBigThreads - 1) / kBigThreads;
     const BigBuf A = L.buf(cur), B = L.buf(cur ^ 1);
     const float *X = A.x, *G = A.g;
-    const int32_t *LF = A.left, *YM = A.ymax, *WB = A.wb;
+    const int32_t *LF = A.left, *YM = A.ymax, *EI = A.ei;
     int32_t gapc = 0, kr = 0;
     bool keptc = false;
     if (kb > 0) {
         if (tid == 0) L.d[m] = 0;
         if (m > 0) {
             // 1. the entries' keys: per-16 maxima (a 16-lane row each); d zeroed
-            for (int t0 = 0; t0 < T; t0 += kBigU) {
+            //    (samples_ready: big_pair left both)
+            for (int t0 = 0; !samples_ready && t0 < T; t0 += kBigU) {
                 float kx[kBigU], kg[kBigU];
                 int32_t kl[kBigU];
 #pragma unroll
@@ -2276,18 +2294,18 @@ __device__ __forceinline__ int big_insert_expire(const BigList &L, BigLds &S, Bl
                 }
                 gapc = m;
                 if (lo < ns) {
+                    // the block's X (four 16-B loads: the arrays have room past
+                    // m), each entry's full key only where X ties
                     const int q0 = lo << 4, qn = min(16, m - q0);
-                    float bx[16], bg[16];
-                    int32_t bl[16];
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) {
-                        const int q = q0 + min(u, qn - 1);
-                        bx[u] = X[q]; bg[u] = G[q]; bl[u] = LF[q];
-                    }
+                    const float4 *X4 = reinterpret_cast<const float4 *>(X + q0);
+                    const float4 v0 = X4[0], v1 = X4[1], v2 = X4[2], v3 = X4[3];
+                    const float bx[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
+                                          v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
                     int f = qn;
-#pragma unroll
-                    for (int u = 15; u >= 0; --u)
-                        if (u < qn && key_gt(entry_key(bx[u], bg[u], bl[u]), kc)) f = u;
+                    for (int u = 0; u < qn; ++u) {
+                        if (bx[u] > kc.x) { f = u; break; }  // (a NaN X never: its key is the lowest)
+                        if (bx[u] == kc.x && key_gt(entry_key(bx[u], G[q0 + u], LF[q0 + u]), kc)) { f = u; break; }
+                    }
                     gapc = q0 + f;  // (f < qn: the block's maximum exceeds kc)
                 }
             }
@@ -2347,18 +2365,32 @@ __device__ __forceinline__ int big_insert_expire(const BigList &L, BigLds &S, Bl
     for (int t0 = 0; t0 < Ts; t0 += kBigU) {
         if (!regs) load(t0);
 #pragma unroll
-        for (int u = 0; u < kBigU; ++u) {
-            if (t0 + u >= Ts) break;
-            const int q = (t0 + u) * kBigThreads + tid;
-            const int32_t sk = wave_incl_sum_i32(vk[u]), sd = wave_incl_sum_i32(vd[u]);
-            const int32_t before = S.ts[(t0 + u) * kBigWaves + w] + sk - vk[u];  // kept entries before q
-            const int32_t nex = S.tm[(t0 + u) * kBigWaves + w] + sd - vd[u];     // new edges of gap < q
-            if (q < m && vk[u]) {
-                const int32_t to = before + nex + vd[u];
-                B.x[to] = X[q]; B.g[to] = G[q]; B.left[to] = LF[q];
-                B.ymax[to] = YM[q]; B.wb[to] = WB[q];
+        for (int u0 = 0; u0 < kBigU; u0 += 4) {
+            if (t0 + u0 >= Ts) break;
+            // the entries' fields, four tiles' loads in flight at once
+            float fx[4], fg[4];
+            int32_t fl[4], fy[4], fw[4];
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int q = min((t0 + u0 + v) * kBigThreads + tid, m - 1);
+                fx[v] = fg[v] = 0.0f;
+                fl[v] = fy[v] = fw[v] = 0;
+                if (m > 0) { fx[v] = X[q]; fg[v] = G[q]; fl[v] = LF[q]; fy[v] = YM[q]; fw[v] = EI[q]; }
             }
-            if (cnt && q < ns) L.base[q] = before + nex;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int u = u0 + v;
+                if (t0 + u >= Ts) break;
+                const int q = (t0 + u) * kBigThreads + tid;
+                const int32_t sk = wave_incl_sum_i32(vk[u]), sd = wave_incl_sum_i32(vd[u]);
+                const int32_t before = S.ts[(t0 + u) * kBigWaves + w] + sk - vk[u];  // kept entries before q
+                const int32_t nex = S.tm[(t0 + u) * kBigWaves + w] + sd - vd[u];     // new edges of gap < q
+                if (q < m && vk[u]) {
+                    const int32_t to = before + nex + vd[u];
+                    B.x[to] = fx[v]; B.g[to] = fg[v]; B.left[to] = fl[v]; B.ymax[to] = fy[v]; B.ei[to] = fw[v];
+                }
+                if (cnt && q < ns) L.base[q] = before + nex;
+            }
         }
     }
     __syncthreads();
@@ -2371,14 +2403,14 @@ __device__ __forceinline__ int big_insert_expire(const BigList &L, BigLds &S, Bl
         if (tid < kb && keptc) {
             bs = L.base[gapc];
             h = L.d[gapc];
-            B.wb[bs + kr] = tid;
+            B.ei[bs + kr] = tid;
         }
         __syncthreads();
         int32_t r = 0;
         if (tid < kb && keptc) {
             const LKey kc{S.nkx[c0 + tid], S.nkg[c0 + tid], S.nkl[c0 + tid]};
             for (int32_t j = 0; j < h; ++j) {
-                const int32_t u = B.wb[bs + j];
+                const int32_t u = B.ei[bs + j];
                 if (u == tid) continue;
                 const LKey k{S.nkx[c0 + u], S.nkg[c0 + u], S.nkl[c0 + u]};
                 r += (key_gt(kc, k) || (!key_gt(k, kc) && u < tid)) ? 1 : 0;
@@ -2388,7 +2420,7 @@ __device__ __forceinline__ int big_insert_expire(const BigList &L, BigLds &S, Bl
         if (tid < kb && keptc) {
             const int32_t to = bs + r;
             B.x[to] = S.nkx[c0 + tid]; B.g[to] = S.nkg[c0 + tid]; B.left[to] = S.nkl[c0 + tid];
-            B.ymax[to] = S.nky[c0 + tid]; B.wb[to] = S.nkw[c0 + tid];
+            B.ymax[to] = S.nky[c0 + tid]; B.ei[to] = S.nke[c0 + tid];
         }
     }
     __syncthreads();
@@ -2396,86 +2428,137 @@ __device__ __forceinline__ int big_insert_expire(const BigList &L, BigLds &S, Bl
     return kept_old + kept_new;
 }
 
-// Pairing (3751-3869) of the list in buffer cur (m entries) into buffer
-// cur ^ 1: every pair stepped, its first swap, the boundary swaps; `where`
-// codes for every entry (emit: slot j0 + k of pair k, sides 0 / 1; else
-// kBigNoEmit; an odd last entry kBigUnpaired, copied unstepped).
-__device__ __forceinline__ void big_pair(const BigList &L, int cur, int m, int32_t Row, bool emit, uint32_t j0,
-                         uint32_t *__restrict__ where) {
-    const int tid = threadIdx.x, lane = tid & 63;
+// Pairing (3751-3869) of the list in buffer cur (m >= 1 entries), in two
+// passes that leave it in buffer cur again: (1) into cur ^ 1, every pair
+// stepped (X += Gradient) and its first swap (3831-3841), the row's list in
+// ids[off, off + m) (the pairs' edges, before the step), and the row's record
+// ri = (off, m, j0 or kBigNoEmit, the unpaired odd last entry or -1); (2) back
+// into cur, every boundary swap (3843-3853): thread k takes entries 2k and
+// 2k + 1 from pair k or its neighbours (boundaries (2k - 1, 2k) are disjoint
+// and read what pass 1 left), and leaves the per-16 key maxima of the result
+// in S.s* and d zeroed -- the next row's insertion starts from them.
+__device__ __forceinline__ void big_pair(const BigList &L, BigLds &S, int cur, int m, int32_t r, bool emit,
+                                         uint32_t j0, uint32_t off) {
+    constexpr int PB = 4;  // tiles whose loads are in flight at once
+    const int tid = threadIdx.x;
     const int P = m >> 1, items = P + (m & 1);
     const BigBuf A = L.buf(cur), B = L.buf(cur ^ 1);
-    const float *X = A.x, *G = A.g;
-    const int32_t *LF = A.left, *YM = A.ymax, *WB = A.wb;
-    for (int k0 = 0; k0 < items; k0 += kBigThreads) {
-        const int k = k0 + tid;
-        const bool pair = k < P;
-        // own pair (entries 2k, 2k + 1)
-        float xa = 0, xb = 0, ga = 0, gb = 0;
-        int32_t la = 0, lb = 0, ya = 0, yb = 0, wa = 0, wbb = 0;
-        if (k < items) {
-            xa = X[2 * k]; ga = G[2 * k]; la = LF[2 * k]; ya = YM[2 * k]; wa = WB[2 * k];
-            if (pair) { xb = X[2 * k + 1]; gb = G[2 * k + 1]; lb = LF[2 * k + 1]; yb = YM[2 * k + 1]; wbb = WB[2 * k + 1]; }
+    int32_t *ids = L.ids + off;
+    if (tid == 0) {
+        int32_t *q = L.ri + 4 * (size_t)r;
+        q[0] = (int32_t)off;
+        q[1] = m;
+        q[2] = emit ? (int32_t)j0 : (int32_t)kBigNoEmit;
+        if (!(m & 1)) q[3] = -1;
+    }
+    for (int k0 = 0; k0 < items; k0 += PB * kBigThreads) {
+        float2 vx[PB], vg[PB];
+        int2 vl[PB], vy[PB], vi[PB];
+#pragma unroll
+        for (int v = 0; v < PB; ++v) {  // entries 2k, 2k + 1 (the odd last entry's pair reads past m: in the slice)
+            const int e = 2 * min(k0 + v * kBigThreads + tid, items - 1);
+            vx[v] = *reinterpret_cast<const float2 *>(A.x + e);
+            vg[v] = *reinterpret_cast<const float2 *>(A.g + e);
+            vl[v] = *reinterpret_cast<const int2 *>(A.left + e);
+            vy[v] = *reinterpret_cast<const int2 *>(A.ymax + e);
+            vi[v] = *reinterpret_cast<const int2 *>(A.ei + e);
         }
-        if (k < items && !pair) {  // the odd last entry: not paired, not stepped
-            B.x[2 * k] = xa; B.g[2 * k] = ga; B.left[2 * k] = la; B.ymax[2 * k] = ya; B.wb[2 * k] = wa;
-            where[wa + Row] = kBigUnpaired;
+#pragma unroll
+        for (int v = 0; v < PB; ++v) {
+            const int k = k0 + v * kBigThreads + tid;
+            if (k >= items) break;
+            const int e = 2 * k;
+            ids[e] = vi[v].x;
+            if (k == P) {  // the odd last entry: not paired, not stepped
+                B.x[e] = vx[v].x; B.g[e] = vg[v].x; B.left[e] = vl[v].x; B.ymax[e] = vy[v].x; B.ei[e] = vi[v].x;
+                L.ri[4 * (size_t)r + 3] = vi[v].x;
+                continue;
+            }
+            ids[e + 1] = vi[v].y;
+            const float sa = vx[v].x + vg[v].x, sb = vx[v].y + vg[v].y;  // 3811-3829
+            const bool s1 = sa > sb;
+            *reinterpret_cast<float2 *>(B.x + e) = s1 ? make_float2(sb, sa) : make_float2(sa, sb);
+            *reinterpret_cast<float2 *>(B.g + e) = s1 ? make_float2(vg[v].y, vg[v].x) : vg[v];
+            *reinterpret_cast<int2 *>(B.left + e) = s1 ? make_int2(vl[v].y, vl[v].x) : vl[v];
+            *reinterpret_cast<int2 *>(B.ymax + e) = s1 ? make_int2(vy[v].y, vy[v].x) : vy[v];
+            *reinterpret_cast<int2 *>(B.ei + e) = s1 ? make_int2(vi[v].y, vi[v].x) : vi[v];
         }
-        if (pair) {
-            where[wa + Row] = emit ? 2u * (j0 + (uint32_t)k) : kBigNoEmit;
-            where[wbb + Row] = emit ? 2u * (j0 + (uint32_t)k) + 1u : kBigNoEmit;
+    }
+    __syncthreads();
+    const int lane = tid & 63;
+    constexpr int PB2 = 2;  // (pass 2 holds twice the registers a tile)
+    for (int k0 = 0; k0 < items; k0 += PB2 * kBigThreads) {
+        float2 vx[PB2], vg[PB2];
+        int2 vl[PB2], vy[PB2], vi[PB2];
+        float xm[PB2], xp[PB2];
+#pragma unroll
+        for (int v = 0; v < PB2; ++v) {
+            const int e = 2 * min(k0 + v * kBigThreads + tid, items - 1);
+            vx[v] = *reinterpret_cast<const float2 *>(B.x + e);
+            vg[v] = *reinterpret_cast<const float2 *>(B.g + e);
+            vl[v] = *reinterpret_cast<const int2 *>(B.left + e);
+            vy[v] = *reinterpret_cast<const int2 *>(B.ymax + e);
+            vi[v] = *reinterpret_cast<const int2 *>(B.ei + e);
+            xm[v] = B.x[max(e - 1, 0)];
+            xp[v] = B.x[e + 2];  // (past m: in the slice, unused)
         }
-        // stepped, then the first swap: f = the pair's first entry, s its second
-        const float sa = xa + ga, sb = xb + gb;
-        const bool s1 = sa > sb;
-        float fx = s1 ? sb : sa, fg = s1 ? gb : ga, sx = s1 ? sa : sb, sg = s1 ? ga : gb;
-        int32_t fl = s1 ? lb : la, fy = s1 ? yb : ya, fw = s1 ? wbb : wa;
-        int32_t sl = s1 ? la : lb, sy = s1 ? ya : yb, sw = s1 ? wa : wbb;
-        // pair k - 1's second and pair k + 1's first (lane shuffles; wave edges from memory)
-        float px = __shfl_up(sx, 1), pg = __shfl_up(sg, 1);
-        int32_t pl = __shfl_up(sl, 1), py = __shfl_up(sy, 1), pw = __shfl_up(sw, 1);
-        float nx = __shfl_down(fx, 1), ng = __shfl_down(fg, 1);
-        int32_t nl = __shfl_down(fl, 1), ny = __shfl_down(fy, 1), nw = __shfl_down(fw, 1);
-        if (pair && lane == 0 && k >= 1) {
-            const int a = 2 * k - 2;
-            const float ax = X[a] + G[a], bx = X[a + 1] + G[a + 1];
-            const int src = ax > bx ? a : a + 1;  // (the pair's second after its first swap)
-            px = X[src] + G[src]; pg = G[src]; pl = LF[src]; py = YM[src]; pw = WB[src];
-        }
-        if (pair && lane == 63 && k + 1 < P) {
-            const int a = 2 * k + 2;
-            const float ax = X[a] + G[a], bx = X[a + 1] + G[a + 1];
-            const int src = ax > bx ? a + 1 : a;  // (its first)
-            nx = X[src] + G[src]; ng = G[src]; nl = LF[src]; ny = YM[src]; nw = WB[src];
-        }
-        if (pair) {
-            const bool lo = k >= 1 && px > fx;      // 3843-3853 with pair k - 1
-            const bool hi = k + 1 < P && sx > nx;   // and with pair k + 1
-            const int e0 = 2 * k, e1 = 2 * k + 1;
-            B.x[e0] = lo ? px : fx; B.g[e0] = lo ? pg : fg; B.left[e0] = lo ? pl : fl;
-            B.ymax[e0] = lo ? py : fy; B.wb[e0] = lo ? pw : fw;
-            B.x[e1] = hi ? nx : sx; B.g[e1] = hi ? ng : sg; B.left[e1] = hi ? nl : sl;
-            B.ymax[e1] = hi ? ny : sy; B.wb[e1] = hi ? nw : sw;
+#pragma unroll
+        for (int v = 0; v < PB2; ++v) {
+            if (k0 + v * kBigThreads >= items) break;  // (uniform: every lane of a live tile takes the maxima)
+            const int k = k0 + v * kBigThreads + tid;
+            const int e = 2 * k;
+            LKey k0k{-INFINITY, -INFINITY, INT32_MIN}, k1k{-INFINITY, -INFINITY, INT32_MIN};
+            if (k < items) {
+                float x0 = vx[v].x, g0 = vg[v].x, x1 = vx[v].y, g1 = vg[v].y;
+                int32_t l0 = vl[v].x, y0 = vy[v].x, i0 = vi[v].x, l1 = vl[v].y, y1 = vy[v].y, i1 = vi[v].y;
+                if (k < P) {
+                    if (k >= 1 && xm[v] > x0) {  // boundary k: entry 2k - 1 comes down
+                        x0 = xm[v]; g0 = B.g[e - 1]; l0 = B.left[e - 1]; y0 = B.ymax[e - 1]; i0 = B.ei[e - 1];
+                    }
+                    if (k + 1 < P && x1 > xp[v]) {  // boundary k + 1: entry 2k + 2 comes up
+                        x1 = xp[v]; g1 = B.g[e + 2]; l1 = B.left[e + 2]; y1 = B.ymax[e + 2]; i1 = B.ei[e + 2];
+                    }
+                    *reinterpret_cast<float2 *>(A.x + e) = make_float2(x0, x1);
+                    *reinterpret_cast<float2 *>(A.g + e) = make_float2(g0, g1);
+                    *reinterpret_cast<int2 *>(A.left + e) = make_int2(l0, l1);
+                    *reinterpret_cast<int2 *>(A.ymax + e) = make_int2(y0, y1);
+                    *reinterpret_cast<int2 *>(A.ei + e) = make_int2(i0, i1);
+                    *reinterpret_cast<int2 *>(L.d + e) = make_int2(0, 0);
+                    k1k = entry_key(x1, g1, l1);
+                } else {  // the odd last entry
+                    A.x[e] = x0; A.g[e] = g0; A.left[e] = l0; A.ymax[e] = y0; A.ei[e] = i0;
+                    L.d[e] = 0;
+                }
+                k0k = entry_key(x0, g0, l0);
+            }
+            LKey kk = key_gt(k1k, k0k) ? k1k : k0k;  // the maximum of the 16 entries of 8 lanes
+            int32_t p = 0;
+            key_max_step<kDppShr1>(kk, p);
+            key_max_step<kDppShr2>(kk, p);
+            key_max_step<kDppShr4>(kk, p);
+            if ((lane & 7) == 7 && (k >> 3) < kBigSamp) {
+                S.sx[k >> 3] = kk.x; S.sg[k >> 3] = kk.g; S.sl[k >> 3] = kk.l;
+            }
         }
     }
     __syncthreads();
 }
 
 // One workgroup per huge object: its list in the pool slice at big_off
-// (kBigListArrays arrays of big_cap + 2 ints, big_cap >= its most active
-// entries), its where codes at where + woff[edge] (rows [YMin, min(YMax,
-// MaxY)) of each edge).
+// (big_slice_ints(big_cap, meta rows, meta ents); big_cap >= its most active
+// entries; big_meta[2b], big_meta[2b + 1]: its rows MaxY - FirstRow and list
+// entries over them, k_obj_maxact's sizes).
 __global__ void __launch_bounds__(kBigThreads) k_obj_walk_big(FrameParams fp, const ObjDesc *__restrict__ objs,
                                                              const uint32_t *__restrict__ big,
                                                              const unsigned long long *__restrict__ big_off,
                                                              const uint32_t *__restrict__ big_cap,
+                                                             const uint32_t *__restrict__ big_meta,
                                                              int32_t *__restrict__ pool,
                                                              const uint32_t *__restrict__ escan,
                                                              const uint32_t *__restrict__ total0p,
                                                              const ObjEdge *__restrict__ work,
-                                                             const uint32_t *__restrict__ woff,
                                                              const unsigned long long *__restrict__ soff,
-                                                             uint32_t *__restrict__ where, uint32_t *__restrict__ err,
+                                                             uint32_t *__restrict__ err,
                                                              const uint32_t *__restrict__ prstat) {
     __shared__ BigLds S;
     __shared__ BlockRed R;
@@ -2485,36 +2568,53 @@ __global__ void __launch_bounds__(kBigThreads) k_obj_walk_big(FrameParams fp, co
     const uint32_t bound = (uint32_t)(soff[o + 1] - soff[o]);
     uint32_t e0, n;
     obj_range(od, escan, *total0p, e0, n);
-    if (n == 0) return;
-    const ObjEdge *E = work + e0;
-    const uint32_t *WO = woff + e0;
-    const uint32_t cap = min(big_cap[blockIdx.x], kBigMaxM);
+    const uint32_t cap = min(big_cap[blockIdx.x], kBigMaxM), rows_cap = big_meta[2 * blockIdx.x],
+                   ents = big_meta[2 * blockIdx.x + 1];
     BigList L;
-    L.carve(pool + big_off[blockIdx.x], cap);
+    L.carve(pool + big_off[blockIdx.x], cap, rows_cap);
     const int tid = threadIdx.x;
+    for (uint32_t q = tid; q < 4 * rows_cap; q += kBigThreads) L.ri[q] = q % 4 == 3 ? -1 : 0;  // (rows not walked: m = 0)
+    if (n == 0) {
+        if (tid == 0) { L.hdr[0] = 0; L.hdr[1] = 0; }
+        return;
+    }
+    const ObjEdge *E = work + e0;
     int32_t mr = INT32_MIN;
     for (uint32_t i = tid; i < n; i += kBigThreads) mr = max(mr, E[i].YMax);
     const int32_t MaxY = min(min(blk_max(R, mr), fp.H), fp.row1);
     const int32_t FirstRow = E[0].YMin;
     const int32_t RowLo = fp.draws[od.draw].mode != MODE_AVX ? fp.row0 - 1 : fp.row0;
+    const bool fits = (int64_t)MaxY - FirstRow <= (int64_t)rows_cap;
+    if (tid == 0) {
+        L.hdr[0] = FirstRow;
+        L.hdr[1] = fits ? max(0, MaxY - FirstRow) : 0;
+        if (!fits) atomicOr(err, 1u);  // (never: k_obj_maxact sized it)
+    }
+    if (!fits) return;
     int cur = 0, m = 0;
-    uint32_t ins = 0, emitted = 0;
-    bool bad = false;
+    uint32_t ins = 0, emitted = 0, off = 0;
+    bool bad = false, samples = false;
     unsigned long long wpa[16] = {}, *wp = PRK_WPROF && tid == 0 ? wpa : nullptr;
     unsigned long long tw0 = PRK_WT(), twall = tw0;
+    // the window of sorted edges at `pf` (loaded a row ahead, while the
+    // previous row pairs)
+    uint32_t pf = UINT32_MAX;
+    int32_t y = INT32_MAX, l = 0, ym = 0;
+    float x = 0.0f, g = 0.0f;
+    auto fetch = [&](uint32_t at) {
+        const uint32_t i = at + (uint32_t)tid;
+        y = INT32_MAX; x = g = 0.0f; l = ym = 0;
+        if (i < n) {
+            const ObjEdge &C = E[i];
+            y = C.YMin; x = C.X; g = C.G; l = C.Left; ym = C.YMax;
+        }
+        pf = at;
+    };
     for (int32_t Row = FirstRow; Row < MaxY; ++Row) {
         bool expired = false;
         if (PRK_WPROF && wp) wp[3] += 1;
         for (;;) {  // the row's new edges, a window of kBigThreads at a time (3654-3713)
-            const uint32_t i = ins + (uint32_t)tid;
-            int32_t y = INT32_MAX;
-            float x = 0.0f, g = 0.0f;
-            int32_t l = 0, ym = 0, wbv = 0;
-            if (i < n) {
-                const ObjEdge &C = E[i];
-                y = C.YMin; x = C.X; g = C.G; l = C.Left; ym = C.YMax;
-                wbv = (int32_t)WO[i] - y;
-            }
+            if (pf != ins) fetch(ins);
             int32_t lt, kb, nanc;
             blk_sum3(R, y < Row ? 1 : 0, y == Row ? 1 : 0, (y == Row && (x != x || g != g)) ? 1 : 0, lt, kb, nanc);
             if (lt) {  // (never past the first row of a sorted list)
@@ -2527,7 +2627,7 @@ __global__ void __launch_bounds__(kBigThreads) k_obj_walk_big(FrameParams fp, co
                 break;
             }
             if (tid < kb) {
-                S.nkx[tid] = x; S.nkg[tid] = g; S.nkl[tid] = l; S.nky[tid] = ym; S.nkw[tid] = wbv;
+                S.nkx[tid] = x; S.nkg[tid] = g; S.nkl[tid] = l; S.nky[tid] = ym; S.nke[tid] = (int32_t)(ins + tid);
             }
             __syncthreads();
             PRK_BIG_T(0, tw0);
@@ -2536,12 +2636,14 @@ __global__ void __launch_bounds__(kBigThreads) k_obj_walk_big(FrameParams fp, co
             if (nanc) {  // one edge at a time (no total order on a batch with a NaN key)
                 for (int t = 0; t < kb; ++t) {
                     const bool ex = last && t + 1 == kb;
-                    m = big_insert_expire(L, S, R, cur, m, t, 1, ex, Row, wp);
+                    m = big_insert_expire(L, S, R, cur, m, t, 1, ex, Row, samples, wp);
                     cur ^= 1;
+                    samples = false;
                 }
             } else {
-                m = big_insert_expire(L, S, R, cur, m, 0, kb, last, Row, wp);
+                m = big_insert_expire(L, S, R, cur, m, 0, kb, last, Row, samples, wp);
                 cur ^= 1;
+                samples = false;
             }
             PRK_BIG_T(1, tw0);
             expired = last;
@@ -2549,9 +2651,11 @@ __global__ void __launch_bounds__(kBigThreads) k_obj_walk_big(FrameParams fp, co
             if (last) break;
         }
         if (bad) break;
+        if (pf != ins && ins < n) fetch(ins);  // (the next row's window, in flight through this row's pairing)
         if (!expired && m > 0) {  // expiry 3715-3749 alone
-            m = big_insert_expire(L, S, R, cur, m, 0, 0, true, Row, wp);
+            m = big_insert_expire(L, S, R, cur, m, 0, 0, true, Row, false, wp);
             cur ^= 1;
+            samples = false;
         }
         PRK_BIG_T(2, tw0);
         if (m == 0) {  // nothing happens on the rows before the next insertion: go there
@@ -2561,12 +2665,13 @@ __global__ void __launch_bounds__(kBigThreads) k_obj_walk_big(FrameParams fp, co
         }
         const bool emit = Row >= RowLo;
         const uint32_t P = (uint32_t)(m >> 1);
-        if (emit && emitted + P > bound) {  // (never: the bound holds every pair)
+        if ((emit && emitted + P > bound) || (uint64_t)off + (uint32_t)m > ents) {  // (never: sized by the bounds)
             bad = true;
             break;
         }
-        big_pair(L, cur, m, Row, emit, emitted, where);
-        cur ^= 1;
+        big_pair(L, S, cur, m, Row - FirstRow, emit, emitted, off);
+        samples = true;
+        off += (uint32_t)m;
         if (emit) emitted += P;
         PRK_BIG_T(5, tw0);
         if (PRK_WPROF && wp) wp[6] += (unsigned)m;
@@ -2578,62 +2683,59 @@ __global__ void __launch_bounds__(kBigThreads) k_obj_walk_big(FrameParams fp, co
     }
 }
 
-// The rows every edge of the huge objects is listed on (rows [YMin,
-// min(YMax, H, row1)) = [YMin, min(YMax, MaxY))), into cnt[edge] (their scan
-// is woff).  Grid (edges / 256, objects).
-__global__ void k_big_rows(FrameParams fp, const ObjDesc *__restrict__ objs, const uint32_t *__restrict__ big,
-                           const uint32_t *__restrict__ escan, const uint32_t *__restrict__ total0p,
-                           const ObjEdge *__restrict__ work, uint32_t *__restrict__ cnt) {
-    const ObjDesc od = objs[big[blockIdx.y]];
-    uint32_t e0, n;
-    obj_range(od, escan, *total0p, e0, n);
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const ObjEdge &e = work[e0 + i];
-    cnt[e0 + i] = (uint32_t)max(0, min(min(e.YMax, fp.H), fp.row1) - e.YMin);
-}
-
-// Every edge of the huge objects replayed: on each row it was paired on, its
-// state into its side of the pair's PairRaw (side 0 also the SpanPos and the
-// winner id), then stepped (3811-3829).  Grid (edges / 256, objects).
+// Every pair of every row of the huge objects, a thread each (grid: (rows,
+// objects), a workgroup per row): both edges' states at the row -- the edge
+// from FillEdgeTable stepped on each row it was listed on before this one,
+// but its unpaired ones (3811-3829, as the walk stepped it) -- into the pair's
+// PairRaw slot, its SpanPos and winner id beside it.
 template <int M>
-__global__ void k_big_emit(FrameParams fp, const ObjDesc *__restrict__ objs, const uint32_t *__restrict__ big,
-                           const uint32_t *__restrict__ escan, const uint32_t *__restrict__ total0p,
-                           const ObjEdge *__restrict__ work, const uint32_t *__restrict__ woff,
-                           const uint32_t *__restrict__ where, const unsigned long long *__restrict__ soff,
-                           PairRaw *__restrict__ raw, SpanPos *__restrict__ pos, uint32_t *__restrict__ span_tri,
-                           const uint32_t *__restrict__ prstat) {
+__global__ void __launch_bounds__(256) k_big_replay(FrameParams fp, const ObjDesc *__restrict__ objs,
+                                                    const uint32_t *__restrict__ big,
+                                                    const unsigned long long *__restrict__ big_off,
+                                                    const uint32_t *__restrict__ big_cap,
+                                                    const uint32_t *__restrict__ big_meta,
+                                                    const int32_t *__restrict__ pool,
+                                                    const uint32_t *__restrict__ escan,
+                                                    const uint32_t *__restrict__ total0p,
+                                                    const ObjEdge *__restrict__ work,
+                                                    const unsigned long long *__restrict__ soff,
+                                                    PairRaw *__restrict__ raw, SpanPos *__restrict__ pos,
+                                                    uint32_t *__restrict__ span_tri, const uint32_t *__restrict__ prstat) {
     const uint32_t o = big[blockIdx.y];
     if (prstat && prstat[o] == kPrDone) return;
     const ObjDesc od = objs[o];
     if (fp.draws[od.draw].mode != M) return;
+    BigList L;
+    L.carve(const_cast<int32_t *>(pool) + big_off[blockIdx.y], min(big_cap[blockIdx.y], kBigMaxM),
+            big_meta[2 * blockIdx.y]);
+    const int32_t FirstRow = L.hdr[0], rows = L.hdr[1];
+    const int32_t r = (int32_t)blockIdx.x;
+    if (r >= rows) return;
+    const int32_t off = L.ri[4 * r], m = L.ri[4 * r + 1], j0 = L.ri[4 * r + 2];
+    if ((uint32_t)j0 == kBigNoEmit || m < 2) return;
     uint32_t e0, n;
     obj_range(od, escan, *total0p, e0, n);
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    ObjEdge e = work[e0 + i];
-    const int32_t r1 = min(min(e.YMax, fp.H), fp.row1);
-    if (e.YMin >= r1) return;
+    const ObjEdge *E = work + e0;
     const uint32_t base = (uint32_t)soff[o], bound = (uint32_t)(soff[o + 1] - soff[o]);
-    const uint32_t *wh = where + woff[e0 + i];
-    for (int32_t r = e.YMin; r < r1; ++r) {
-        const uint32_t c = wh[r - e.YMin];
-        if (c == kBigUnpaired) continue;
-        if (c != kBigNoEmit && (c >> 1) < bound) {
-            const uint32_t at = base + (c >> 1);
-            if (c & 1u) {
-                raw[at].r0 = make_float4(e.X, e.Z, e.W, e.U);
-                raw[at].r1 = make_float4(e.V, e.N0, e.N1, e.N2);
-                raw[at].r2 = make_float4(e.C0, e.C1, e.C2, e.C3);
-            } else {
-                raw[at].l0 = make_float4(e.X, e.Z, e.W, e.U);
-                raw[at].l1 = make_float4(e.V, e.N0, e.N1, e.N2);
-                raw[at].l2 = make_float4(e.C0, e.C1, e.C2, e.C3);
-                pos[at] = SpanPos{r, (int32_t)od.draw, 0, SPAN_RAW};
-                span_tri[at] = od.g0;
-            }
+    const int32_t Row = FirstRow + r;
+    const int32_t *ids = L.ids + off;
+    for (int k = threadIdx.x; k < m / 2; k += blockDim.x) {
+        const uint32_t j = (uint32_t)j0 + (uint32_t)k;
+        if (j >= bound) break;
+        ObjEdge st[2];
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            const int32_t ei = ids[2 * k + side];
+            ObjEdge e = E[ei];
+            for (int32_t q = e.YMin; q < Row; ++q)
+                if (L.ri[4 * (q - FirstRow) + 3] != ei) obj_step<M>(e);
+            st[side] = e;
         }
-        obj_step<M>(e);
+        PairRaw pr;
+        pair_raw_out(st[0], st[1], pr);
+        raw[base + j] = pr;
+        pos[base + j] = SpanPos{Row, (int32_t)od.draw, 0, SPAN_RAW};
+        span_tri[base + j] = od.g0;
     }
 }
 
@@ -3459,52 +3561,40 @@ hipError_t prk_obj_walk_group(const prk::FrameParams *fp, int32_t mode, uint32_t
     }
     return hipGetLastError();
 }
-// The huge-object walk (k_obj_walk_big): cnt[edge] = its listed rows, for
-// the edges of big[0, nbig) (the rest of cnt untouched; woff = its exclusive
-// scan) ...
+// The huge-object walk (k_obj_walk_big) of the objects big[0, nbig) of mode
+// `mode`: their pool slices at big_off (prk_big_slice_ints(big_cap, rows,
+// ents) ints each; big_meta: (rows, ents) per object, k_obj_maxact's), then
+// every pair set up from a replay of its edges (k_big_replay, grid (max_rows,
+// nbig)) into PairRaw slots soff[o] + j (k_span_finish sets the spans up).
 uint32_t prk_big_max_entries(void) { return prk::kBigMaxM; }
-uint32_t prk_big_list_arrays(void) { return (uint32_t)prk::kBigListArrays; }
-hipError_t prk_big_rows(const prk::FrameParams *fp, const void *objs, const uint32_t *big, uint32_t nbig,
-                        uint32_t max_edges, const uint32_t *escan, const uint32_t *total0p, const void *work,
-                        uint32_t *cnt, hipStream_t s) {
-    if (nbig == 0 || max_edges == 0) return hipSuccess;
-    if (nbig > 65535) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(prk::k_big_rows, dim3((max_edges + 255) / 256, nbig), dim3(256), 0, s, *fp,
-                       reinterpret_cast<const prk::ObjDesc *>(objs), big, escan, total0p,
-                       reinterpret_cast<const prk::ObjEdge *>(work), cnt);
-    return hipGetLastError();
-}
-// ... then the walk of the objects big[0, nbig) of mode `mode` (lists in the
-// pool at big_off, big_cap entries; where codes at where + woff[edge], every
-// code kBigUnpaired beforehand) and the replay of their edges into PairRaw
-// slots soff[o] + j (k_span_finish sets the spans up).
+uint64_t prk_big_slice_ints(uint32_t cap, uint32_t rows, uint32_t ents) { return prk::big_slice_ints(cap, rows, ents); }
 hipError_t prk_big_walk(const prk::FrameParams *fp, int32_t mode, const void *objs, const uint32_t *big,
-                        const unsigned long long *big_off, const uint32_t *big_cap, uint32_t nbig,
-                        uint32_t max_edges, int32_t *pool, const uint32_t *escan, const uint32_t *total0p,
-                        const void *work, const uint32_t *woff, const unsigned long long *soff, uint32_t *where,
-                        void *raw, void *pos, uint32_t *span_tri, uint32_t *err, const uint32_t *prstat,
-                        hipStream_t s) {
-    if (nbig == 0 || max_edges == 0) return hipSuccess;
+                        const unsigned long long *big_off, const uint32_t *big_cap, const uint32_t *big_meta,
+                        uint32_t nbig, uint32_t max_rows, int32_t *pool, const uint32_t *escan,
+                        const uint32_t *total0p, const void *work, const unsigned long long *soff, void *raw,
+                        void *pos, uint32_t *span_tri, uint32_t *err, const uint32_t *prstat, hipStream_t s) {
+    if (nbig == 0) return hipSuccess;
     if (nbig > 65535) return hipErrorInvalidValue;
     const prk::ObjDesc *O = reinterpret_cast<const prk::ObjDesc *>(objs);
     const prk::ObjEdge *W = reinterpret_cast<const prk::ObjEdge *>(work);
     hipLaunchKernelGGL(prk::k_obj_walk_big, dim3(nbig), dim3(prk::kBigThreads), 0, s, *fp, O, big, big_off, big_cap,
-                       pool, escan, total0p, W, woff, soff, where, err, prstat);
-    const dim3 g((max_edges + 255) / 256, nbig), b(256);
+                       big_meta, pool, escan, total0p, W, soff, err, prstat);
+    if (max_rows == 0) return hipGetLastError();
+    const dim3 g(max_rows, nbig), b(256);
     prk::PairRaw *R = reinterpret_cast<prk::PairRaw *>(raw);
     prk::SpanPos *P = reinterpret_cast<prk::SpanPos *>(pos);
     switch (mode) {
-#define PRK_BIG_EMIT(MM)                                                                                       \
-    case MM:                                                                                                   \
-        hipLaunchKernelGGL(prk::k_big_emit<MM>, g, b, 0, s, *fp, O, big, escan, total0p, W, woff, where, soff, \
-                           R, P, span_tri, prstat);                                                            \
+#define PRK_BIG_REPLAY(MM)                                                                                      \
+    case MM:                                                                                                    \
+        hipLaunchKernelGGL(prk::k_big_replay<MM>, g, b, 0, s, *fp, O, big, big_off, big_cap, big_meta, pool,    \
+                           escan, total0p, W, soff, R, P, span_tri, prstat);                                    \
         break;
-        PRK_BIG_EMIT(prk::MODE_AVX)
-        PRK_BIG_EMIT(prk::MODE_SC_GOURAUD)
-        PRK_BIG_EMIT(prk::MODE_SC_GOURAUD_TEX)
-        PRK_BIG_EMIT(prk::MODE_SC_PHONG)
-        PRK_BIG_EMIT(prk::MODE_SC_PHONG_TEX)
-#undef PRK_BIG_EMIT
+        PRK_BIG_REPLAY(prk::MODE_AVX)
+        PRK_BIG_REPLAY(prk::MODE_SC_GOURAUD)
+        PRK_BIG_REPLAY(prk::MODE_SC_GOURAUD_TEX)
+        PRK_BIG_REPLAY(prk::MODE_SC_PHONG)
+        PRK_BIG_REPLAY(prk::MODE_SC_PHONG_TEX)
+#undef PRK_BIG_REPLAY
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
