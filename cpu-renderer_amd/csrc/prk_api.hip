@@ -68,7 +68,10 @@ hipError_t prk_obj_seg(const prk::FrameParams *, const void *, uint32_t, const u
                        const void *, const unsigned long long *, uint32_t *, const uint32_t *, void *, hipStream_t);
 uint32_t prk_obj_link_cap(void);
 hipError_t prk_obj_maxact(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, const uint32_t *,
-                          const uint32_t *, const void *, int32_t *, hipStream_t);
+                          const uint32_t *, const void *, int32_t *, uint32_t, hipStream_t);
+size_t prk_maxact_huge_scratch(void);
+hipError_t prk_obj_maxact_huge(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, uint32_t, uint32_t,
+                               const uint32_t *, const uint32_t *, const void *, int32_t *, void *, hipStream_t);
 uint32_t prk_obj_walk_threads(uint32_t);
 hipError_t prk_obj_walk_group(const prk::FrameParams *, int32_t, uint32_t, const void *, const uint32_t *,
                               const unsigned long long *, const uint32_t *, uint32_t, int32_t *, const uint32_t *,
@@ -296,7 +299,7 @@ struct prk_context {
             d_keys_b, d_vals_b, d_offs, d_nwin, d_wtag, d_srecs, d_work, d_ekeys, d_ekeys2, d_evals, d_ecnt, d_escan,
             d_rcnt, d_rscan, d_bound, d_oslot, d_pool, d_err, d_raw, d_most, d_cls, d_prrow, d_prcnt, d_preoff,
             d_prfge, d_prccur, d_prkey, d_prest, d_prsst, d_preend, d_preendm, d_prmatch, d_prsidx, d_prsm, d_prstat,
-            d_segcnt, d_segoff, d_segs, d_wy;
+            d_segcnt, d_segoff, d_segs, d_wy, d_mhuge;
         // the pass's host tables, packed into pinned memory for one upload
         // (stage_ev: that upload, before the staging is rewritten)
         char *h_stage = nullptr;
@@ -497,7 +500,7 @@ int prk_destroy(prk_context *c) {
                         &S.d_raw, &S.d_most, &S.d_cls, &S.d_prrow, &S.d_prcnt, &S.d_preoff, &S.d_prfge,
                         &S.d_prccur, &S.d_prkey, &S.d_prest, &S.d_prsst, &S.d_preend, &S.d_preendm,
                         &S.d_prmatch, &S.d_prsidx, &S.d_prsm, &S.d_prstat, &S.d_segcnt, &S.d_segoff,
-                        &S.d_segs, &S.d_wy};
+                        &S.d_segs, &S.d_wy, &S.d_mhuge};
         for (DevBuf *b : sb) b->release();
         if (S.h_rb) (void)hipHostFree(S.h_rb);
         if (S.stage_ev) {
@@ -1858,7 +1861,18 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     int32_t *h_most = reinterpret_cast<int32_t *>(S.h_cls);
     if (nbig_all) {
         PRK_TRY(S.d_most.ensure((size_t)nbig_all * 12));
-        PRK_TRY(prk_obj_maxact(&fp, d_objs, d_big, nbig_all, escan, total0p, S.d_work.p, (int32_t *)S.d_most.p, s));
+        // (objects of kMaxactHugeEdges edges or more: many workgroups each;
+        // PRK_OBJ_HUGE_EDGES=n (tests): n instead)
+        const char *henv = std::getenv("PRK_OBJ_HUGE_EDGES");
+        const uint32_t kMaxactHugeEdges = henv ? (uint32_t)std::max(1l, std::atol(henv)) : (1u << 18);
+        PRK_TRY(prk_obj_maxact(&fp, d_objs, d_big, nbig_all, escan, total0p, S.d_work.p, (int32_t *)S.d_most.p,
+                               kMaxactHugeEdges, s));
+        for (uint32_t b = 0; b < nbig_all; ++b)
+            if (big_edges[b] >= kMaxactHugeEdges) {
+                PRK_TRY(S.d_mhuge.ensure(prk_maxact_huge_scratch()));
+                PRK_TRY(prk_obj_maxact_huge(&fp, d_objs, d_big, b, nbig_all, big_edges[b], escan, total0p,
+                                            S.d_work.p, (int32_t *)S.d_most.p, S.d_mhuge.p, s));
+            }
         PRK_TRY(hipMemcpyAsync(h_most, S.d_most.p, (size_t)nbig_all * 12, hipMemcpyDeviceToHost, s));
     }
     PRK_TRY(hipMemcpyAsync(S.h_rb, oslot + nobj, 8, hipMemcpyDeviceToHost, s));

@@ -2015,11 +2015,12 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_obj_maxact(FrameParams fp, 
                                                                const uint32_t *__restrict__ escan,
                                                                const uint32_t *__restrict__ total0p,
                                                                const ObjEdge *__restrict__ work,
-                                                               int32_t *__restrict__ most) {
+                                                               int32_t *__restrict__ most, uint32_t huge_min) {
     __shared__ int32_t h[kMaxactRows + 1];
     __shared__ BlockRed R;
     __shared__ unsigned long long ents;
     const ObjDesc od = objs[big[blockIdx.x]];
+    if (huge_min && od.kind == 0 && 3ull * od.tris >= huge_min) return;  // (k_maxact_huge_*)
     uint32_t e0, n;
     obj_range(od, escan, *total0p, e0, n);
     const ObjEdge *E = work + e0;
@@ -2068,6 +2069,98 @@ __global__ void __launch_bounds__(kSlotMaxThreads) k_obj_maxact(FrameParams fp, 
     }
     best = blk_max(R, best);
     if (tid == 0) most[blockIdx.x] = best;
+}
+
+// The same sizes for one huge object (big[b]: 3 * tris >= huge_min edges),
+// its edges spread over many workgroups: the difference histogram in device
+// memory (hist: kMaxactRows + 2 zeroed ints; acc: 3 zeroed words -- the
+// most YMax, the entries, an overflow flag), clipped at min(H, row1) instead
+// of MaxY (what lands past MaxY - FirstRow is never scanned), then
+// k_maxact_huge_fin scans it.
+constexpr uint32_t kMaxactChunk = 8 * kSlotMaxThreads;  // edges per workgroup
+__global__ void __launch_bounds__(kSlotMaxThreads) k_maxact_huge_part(FrameParams fp, const ObjDesc *__restrict__ objs,
+                                                                     const uint32_t *__restrict__ big, uint32_t b,
+                                                                     const uint32_t *__restrict__ escan,
+                                                                     const uint32_t *__restrict__ total0p,
+                                                                     const ObjEdge *__restrict__ work,
+                                                                     int32_t *__restrict__ hist,
+                                                                     unsigned long long *__restrict__ acc) {
+    __shared__ BlockRed R;
+    __shared__ unsigned long long ents;
+    const ObjDesc od = objs[big[b]];
+    uint32_t e0, n;
+    obj_range(od, escan, *total0p, e0, n);
+    const uint32_t i0 = blockIdx.x * kMaxactChunk;
+    if (n == 0 || i0 >= n) return;
+    const ObjEdge *E = work + e0;
+    const int32_t FirstRow = E[0].YMin, Hc = min(fp.H, fp.row1);
+    if ((int64_t)Hc - FirstRow + 1 > kMaxactRows) {
+        if (threadIdx.x == 0) atomicOr(acc + 2, 1ull);
+        return;
+    }
+    if (threadIdx.x == 0) ents = 0;
+    __syncthreads();
+    int32_t mr = INT32_MIN;
+    unsigned long long mine = 0;
+    for (uint32_t i = i0 + threadIdx.x; i < min(n, i0 + kMaxactChunk); i += kSlotMaxThreads) {
+        const int32_t y0 = E[i].YMin, y1 = E[i].YMax;
+        mr = max(mr, y1);
+        if (y0 >= Hc) continue;
+        atomicAdd(&hist[y0 - FirstRow], 1);
+        atomicAdd(&hist[min(max(y0, y1), Hc - 1) - FirstRow + 1], -1);
+        mine += (unsigned long long)max(0, min(y1, Hc) - y0);
+    }
+    if (mine) atomicAdd(&ents, mine);
+    mr = blk_max(R, mr);  // (its barriers also order the LDS sum)
+    if (threadIdx.x == 0) {
+        atomicMax(acc, (unsigned long long)((int64_t)mr - (int64_t)INT32_MIN));  // (biased: unsigned max)
+        if (ents) atomicAdd(acc + 1, ents);
+    }
+}
+__global__ void __launch_bounds__(kSlotMaxThreads) k_maxact_huge_fin(FrameParams fp, const ObjDesc *__restrict__ objs,
+                                                                    const uint32_t *__restrict__ big, uint32_t b,
+                                                                    uint32_t nbig, const uint32_t *__restrict__ escan,
+                                                                    const uint32_t *__restrict__ total0p,
+                                                                    const ObjEdge *__restrict__ work,
+                                                                    const int32_t *__restrict__ hist,
+                                                                    const unsigned long long *__restrict__ acc,
+                                                                    int32_t *__restrict__ most) {
+    __shared__ BlockRed R;
+    const ObjDesc od = objs[big[b]];
+    uint32_t e0, n;
+    obj_range(od, escan, *total0p, e0, n);
+    const int tid = threadIdx.x, NT = blockDim.x;
+    if (n == 0) {
+        if (tid == 0) most[b] = most[nbig + b] = most[2 * nbig + b] = 0;
+        return;
+    }
+    const int32_t FirstRow = work[e0].YMin;
+    const int32_t MaxYMax = (int32_t)((int64_t)acc[0] + (int64_t)INT32_MIN);
+    const int32_t MaxY = min(min(MaxYMax, fp.H), fp.row1);
+    const int64_t rows = (int64_t)MaxY - FirstRow;
+    if (rows <= 0 || rows + 1 > kMaxactRows || acc[2]) {
+        if (tid == 0) {
+            most[b] = most[nbig + b] = rows <= 0 ? 0 : INT32_MAX;
+            most[2 * nbig + b] = 0;
+        }
+        return;
+    }
+    const int Rn = (int)rows;
+    if (tid == 0) {
+        most[nbig + b] = Rn;
+        most[2 * nbig + b] = (int32_t)min(acc[1], (unsigned long long)INT32_MAX);
+    }
+    int32_t carry = 0, best = 0;
+    for (int b0 = 0; b0 < Rn; b0 += NT) {
+        const int q = b0 + tid;
+        const int32_t v = q < Rn ? hist[q] : 0;
+        int32_t tot;
+        const int32_t ex = blk_excl_sum(R, v, tot);
+        if (q < Rn) best = max(best, carry + ex + v);
+        carry += tot;
+    }
+    best = blk_max(R, best);
+    if (tid == 0) most[b] = best;
 }
 
 // One workgroup per large object: lcap > 0, everything in LDS
@@ -2207,6 +2300,7 @@ struct BigLds {
     int32_t pl[kBigThreads];
     float nkx[kBigThreads], nkg[kBigThreads];  // the row's new edges (a window of kBigThreads)
     int32_t nkl[kBigThreads], nky[kBigThreads], nke[kBigThreads];
+    int32_t collide;  // two new edges of the batch share a gap
 };
 
 // Insertion of the new edges S.nk*[c0, c0 + kb) into the list (buffer cur,
@@ -2231,6 +2325,7 @@ __device__ __forceinline__ int big_insert_expire(const BigList &L, BigLds &S, Bl
     const int32_t *LF = A.left, *YM = A.ymax, *EI = A.ei;
     int32_t gapc = 0, kr = 0;
     bool keptc = false;
+    if (tid == 0) S.collide = 0;
     if (kb > 0) {
         if (tid == 0) L.d[m] = 0;
         if (m > 0) {
@@ -2316,6 +2411,7 @@ __device__ __forceinline__ int big_insert_expire(const BigList &L, BigLds &S, Bl
         if (tid < kb) {
             keptc = !expire || !(S.nky[c0 + tid] <= Row);
             if (keptc) kr = atomicAdd(&L.d[gapc], 1);
+            if (kr > 0) S.collide = 1;
         }
         __syncthreads();
         PRK_BIG_T(12, tw0);
@@ -2398,7 +2494,13 @@ __device__ __forceinline__ int big_insert_expire(const BigList &L, BigLds &S, Bl
     // 6. the kept new edges into their places: gap(c)'s block [base, base +
     //    d) holds its new edges ordered by (key, arrival) -- the members meet
     //    in that block (arrival slots), rank themselves, then move
-    if (cnt) {
+    if (cnt && !S.collide) {  // one new edge a gap: no ranking
+        if (tid < kb && keptc) {
+            const int32_t to = L.base[gapc];
+            B.x[to] = S.nkx[c0 + tid]; B.g[to] = S.nkg[c0 + tid]; B.left[to] = S.nkl[c0 + tid];
+            B.ymax[to] = S.nky[c0 + tid]; B.ei[to] = S.nke[c0 + tid];
+        }
+    } else if (cnt) {
         int32_t bs = 0, h = 0;
         if (tid < kb && keptc) {
             bs = L.base[gapc];
@@ -2428,19 +2530,19 @@ __device__ __forceinline__ int big_insert_expire(const BigList &L, BigLds &S, Bl
     return kept_old + kept_new;
 }
 
-// Pairing (3751-3869) of the list in buffer cur (m >= 1 entries), in two
-// passes that leave it in buffer cur again: (1) into cur ^ 1, every pair
-// stepped (X += Gradient) and its first swap (3831-3841), the row's list in
-// ids[off, off + m) (the pairs' edges, before the step), and the row's record
-// ri = (off, m, j0 or kBigNoEmit, the unpaired odd last entry or -1); (2) back
-// into cur, every boundary swap (3843-3853): thread k takes entries 2k and
-// 2k + 1 from pair k or its neighbours (boundaries (2k - 1, 2k) are disjoint
-// and read what pass 1 left), and leaves the per-16 key maxima of the result
-// in S.s* and d zeroed -- the next row's insertion starts from them.
+// Pairing (3751-3869) of the list in buffer cur (m >= 1 entries) into buffer
+// cur ^ 1, one pass: thread k loads pairs k - 1, k and k + 1, steps them (X
+// += Gradient), does their first swaps (3831-3841) and the boundary swaps on
+// either side of pair k (3843-3853: boundaries (2k - 1, 2k) are disjoint, and
+// each reads what the first swaps left), and writes entries 2k, 2k + 1.  It
+// also leaves the row's list in ids[off, off + m) (the pairs' edges, before
+// the step), the row's record ri = (off, m, j0 or kBigNoEmit, the unpaired
+// odd last entry or -1), the per-16 key maxima of the result in S.s* and d
+// zeroed -- the next row's insertion starts from them.
 __device__ __forceinline__ void big_pair(const BigList &L, BigLds &S, int cur, int m, int32_t r, bool emit,
                                          uint32_t j0, uint32_t off) {
-    constexpr int PB = 4;  // tiles whose loads are in flight at once
-    const int tid = threadIdx.x;
+    constexpr int PB = 1;  // tiles whose loads are in flight at once (2: spills)
+    const int tid = threadIdx.x, lane = tid & 63;
     const int P = m >> 1, items = P + (m & 1);
     const BigBuf A = L.buf(cur), B = L.buf(cur ^ 1);
     int32_t *ids = L.ids + off;
@@ -2452,86 +2554,74 @@ __device__ __forceinline__ void big_pair(const BigList &L, BigLds &S, int cur, i
         if (!(m & 1)) q[3] = -1;
     }
     for (int k0 = 0; k0 < items; k0 += PB * kBigThreads) {
-        float2 vx[PB], vg[PB];
-        int2 vl[PB], vy[PB], vi[PB];
+        // pairs k - 1, k, k + 1 (clamped; the odd last entry's pair reads past m: in the slice)
+        float2 px[PB][3], pg[PB][3];
+        int2 pl[PB][3], py[PB][3], pi[PB][3];
 #pragma unroll
-        for (int v = 0; v < PB; ++v) {  // entries 2k, 2k + 1 (the odd last entry's pair reads past m: in the slice)
-            const int e = 2 * min(k0 + v * kBigThreads + tid, items - 1);
-            vx[v] = *reinterpret_cast<const float2 *>(A.x + e);
-            vg[v] = *reinterpret_cast<const float2 *>(A.g + e);
-            vl[v] = *reinterpret_cast<const int2 *>(A.left + e);
-            vy[v] = *reinterpret_cast<const int2 *>(A.ymax + e);
-            vi[v] = *reinterpret_cast<const int2 *>(A.ei + e);
+        for (int v = 0; v < PB; ++v) {
+            const int k = min(k0 + v * kBigThreads + tid, items - 1);
+#pragma unroll
+            for (int h = 0; h < 3; ++h) {
+                const int e = 2 * min(max(k - 1 + h, 0), items - 1);
+                px[v][h] = *reinterpret_cast<const float2 *>(A.x + e);
+                pg[v][h] = *reinterpret_cast<const float2 *>(A.g + e);
+                pl[v][h] = *reinterpret_cast<const int2 *>(A.left + e);
+                py[v][h] = *reinterpret_cast<const int2 *>(A.ymax + e);
+                pi[v][h] = *reinterpret_cast<const int2 *>(A.ei + e);
+            }
         }
 #pragma unroll
         for (int v = 0; v < PB; ++v) {
-            const int k = k0 + v * kBigThreads + tid;
-            if (k >= items) break;
-            const int e = 2 * k;
-            ids[e] = vi[v].x;
-            if (k == P) {  // the odd last entry: not paired, not stepped
-                B.x[e] = vx[v].x; B.g[e] = vg[v].x; B.left[e] = vl[v].x; B.ymax[e] = vy[v].x; B.ei[e] = vi[v].x;
-                L.ri[4 * (size_t)r + 3] = vi[v].x;
-                continue;
-            }
-            ids[e + 1] = vi[v].y;
-            const float sa = vx[v].x + vg[v].x, sb = vx[v].y + vg[v].y;  // 3811-3829
-            const bool s1 = sa > sb;
-            *reinterpret_cast<float2 *>(B.x + e) = s1 ? make_float2(sb, sa) : make_float2(sa, sb);
-            *reinterpret_cast<float2 *>(B.g + e) = s1 ? make_float2(vg[v].y, vg[v].x) : vg[v];
-            *reinterpret_cast<int2 *>(B.left + e) = s1 ? make_int2(vl[v].y, vl[v].x) : vl[v];
-            *reinterpret_cast<int2 *>(B.ymax + e) = s1 ? make_int2(vy[v].y, vy[v].x) : vy[v];
-            *reinterpret_cast<int2 *>(B.ei + e) = s1 ? make_int2(vi[v].y, vi[v].x) : vi[v];
-        }
-    }
-    __syncthreads();
-    const int lane = tid & 63;
-    constexpr int PB2 = 2;  // (pass 2 holds twice the registers a tile)
-    for (int k0 = 0; k0 < items; k0 += PB2 * kBigThreads) {
-        float2 vx[PB2], vg[PB2];
-        int2 vl[PB2], vy[PB2], vi[PB2];
-        float xm[PB2], xp[PB2];
-#pragma unroll
-        for (int v = 0; v < PB2; ++v) {
-            const int e = 2 * min(k0 + v * kBigThreads + tid, items - 1);
-            vx[v] = *reinterpret_cast<const float2 *>(B.x + e);
-            vg[v] = *reinterpret_cast<const float2 *>(B.g + e);
-            vl[v] = *reinterpret_cast<const int2 *>(B.left + e);
-            vy[v] = *reinterpret_cast<const int2 *>(B.ymax + e);
-            vi[v] = *reinterpret_cast<const int2 *>(B.ei + e);
-            xm[v] = B.x[max(e - 1, 0)];
-            xp[v] = B.x[e + 2];  // (past m: in the slice, unused)
-        }
-#pragma unroll
-        for (int v = 0; v < PB2; ++v) {
             if (k0 + v * kBigThreads >= items) break;  // (uniform: every lane of a live tile takes the maxima)
             const int k = k0 + v * kBigThreads + tid;
             const int e = 2 * k;
-            LKey k0k{-INFINITY, -INFINITY, INT32_MIN}, k1k{-INFINITY, -INFINITY, INT32_MIN};
+            LKey ka{-INFINITY, -INFINITY, INT32_MIN}, kb2{-INFINITY, -INFINITY, INT32_MIN};
             if (k < items) {
-                float x0 = vx[v].x, g0 = vg[v].x, x1 = vx[v].y, g1 = vg[v].y;
-                int32_t l0 = vl[v].x, y0 = vy[v].x, i0 = vi[v].x, l1 = vl[v].y, y1 = vy[v].y, i1 = vi[v].y;
-                if (k < P) {
-                    if (k >= 1 && xm[v] > x0) {  // boundary k: entry 2k - 1 comes down
-                        x0 = xm[v]; g0 = B.g[e - 1]; l0 = B.left[e - 1]; y0 = B.ymax[e - 1]; i0 = B.ei[e - 1];
-                    }
-                    if (k + 1 < P && x1 > xp[v]) {  // boundary k + 1: entry 2k + 2 comes up
-                        x1 = xp[v]; g1 = B.g[e + 2]; l1 = B.left[e + 2]; y1 = B.ymax[e + 2]; i1 = B.ei[e + 2];
-                    }
-                    *reinterpret_cast<float2 *>(A.x + e) = make_float2(x0, x1);
-                    *reinterpret_cast<float2 *>(A.g + e) = make_float2(g0, g1);
-                    *reinterpret_cast<int2 *>(A.left + e) = make_int2(l0, l1);
-                    *reinterpret_cast<int2 *>(A.ymax + e) = make_int2(y0, y1);
-                    *reinterpret_cast<int2 *>(A.ei + e) = make_int2(i0, i1);
-                    *reinterpret_cast<int2 *>(L.d + e) = make_int2(0, 0);
-                    k1k = entry_key(x1, g1, l1);
-                } else {  // the odd last entry
-                    A.x[e] = x0; A.g[e] = g0; A.left[e] = l0; A.ymax[e] = y0; A.ei[e] = i0;
+                const float2 x1 = px[v][1], g1 = pg[v][1];
+                const int2 l1 = pl[v][1], y1 = py[v][1], i1 = pi[v][1];
+                ids[e] = i1.x;
+                if (k == P) {  // the odd last entry: not paired, not stepped
+                    B.x[e] = x1.x; B.g[e] = g1.x; B.left[e] = l1.x; B.ymax[e] = y1.x; B.ei[e] = i1.x;
                     L.d[e] = 0;
+                    L.ri[4 * (size_t)r + 3] = i1.x;
+                    ka = entry_key(x1.x, g1.x, l1.x);
+                } else {
+                    ids[e + 1] = i1.y;
+                    // stepped (3811-3829), then each pair's first swap: f / s = its first / second
+                    bool sidx[3];  // (per pair: its entries swapped)
+                    float sx[3][2];
+#pragma unroll
+                    for (int h = 0; h < 3; ++h) {
+                        const float a = px[v][h].x + pg[v][h].x, b = px[v][h].y + pg[v][h].y;
+                        sidx[h] = a > b;
+                        sx[h][0] = sidx[h] ? b : a;  // first
+                        sx[h][1] = sidx[h] ? a : b;  // second
+                    }
+                    const bool lo = k >= 1 && sx[0][1] > sx[1][0];      // boundary k: pair k - 1's second comes down
+                    const bool hi = k + 1 < P && sx[1][1] > sx[2][0];   // boundary k + 1: pair k + 1's first comes up
+                    // entry 2k: pair k - 1's second (its .x if it swapped, else .y) or pair k's first;
+                    // entry 2k + 1: pair k + 1's first or pair k's second (selects: no indexed registers)
+                    const bool f0y = lo ? !sidx[0] : sidx[1], f1y = hi ? sidx[2] : !sidx[1];
+                    const float ox0 = lo ? sx[0][1] : sx[1][0], ox1 = hi ? sx[2][0] : sx[1][1];
+                    const float2 G0 = lo ? pg[v][0] : pg[v][1], G1 = hi ? pg[v][2] : pg[v][1];
+                    const int2 L0 = lo ? pl[v][0] : pl[v][1], L1 = hi ? pl[v][2] : pl[v][1];
+                    const int2 Y0 = lo ? py[v][0] : py[v][1], Y1 = hi ? py[v][2] : py[v][1];
+                    const int2 I0 = lo ? pi[v][0] : pi[v][1], I1 = hi ? pi[v][2] : pi[v][1];
+                    const float og0 = f0y ? G0.y : G0.x, og1 = f1y ? G1.y : G1.x;
+                    const int32_t ol0 = f0y ? L0.y : L0.x, ol1 = f1y ? L1.y : L1.x;
+                    const int32_t oy0 = f0y ? Y0.y : Y0.x, oy1 = f1y ? Y1.y : Y1.x;
+                    const int32_t oi0 = f0y ? I0.y : I0.x, oi1 = f1y ? I1.y : I1.x;
+                    *reinterpret_cast<float2 *>(B.x + e) = make_float2(ox0, ox1);
+                    *reinterpret_cast<float2 *>(B.g + e) = make_float2(og0, og1);
+                    *reinterpret_cast<int2 *>(B.left + e) = make_int2(ol0, ol1);
+                    *reinterpret_cast<int2 *>(B.ymax + e) = make_int2(oy0, oy1);
+                    *reinterpret_cast<int2 *>(B.ei + e) = make_int2(oi0, oi1);
+                    *reinterpret_cast<int2 *>(L.d + e) = make_int2(0, 0);
+                    ka = entry_key(ox0, og0, ol0);
+                    kb2 = entry_key(ox1, og1, ol1);
                 }
-                k0k = entry_key(x0, g0, l0);
             }
-            LKey kk = key_gt(k1k, k0k) ? k1k : k0k;  // the maximum of the 16 entries of 8 lanes
+            LKey kk = key_gt(kb2, ka) ? kb2 : ka;  // the maximum of the 16 entries of 8 lanes
             int32_t p = 0;
             key_max_step<kDppShr1>(kk, p);
             key_max_step<kDppShr2>(kk, p);
@@ -2670,6 +2760,7 @@ __global__ void __launch_bounds__(kBigThreads) k_obj_walk_big(FrameParams fp, co
             break;
         }
         big_pair(L, S, cur, m, Row - FirstRow, emit, emitted, off);
+        cur ^= 1;
         samples = true;
         off += (uint32_t)m;
         if (emit) emitted += P;
@@ -3519,11 +3610,32 @@ hipError_t prk_obj_seg(const prk::FrameParams *fp, const void *objs, uint32_t no
 // (most: 3 * nbig values, see k_obj_maxact)
 hipError_t prk_obj_maxact(const prk::FrameParams *fp, const void *objs, const uint32_t *big, uint32_t nbig,
                           const uint32_t *escan, const uint32_t *total0p, const void *work, int32_t *most,
-                          hipStream_t s) {
+                          uint32_t huge_min, hipStream_t s) {
     if (nbig == 0) return hipSuccess;
     hipLaunchKernelGGL(prk::k_obj_maxact, dim3(nbig), dim3(prk::kSlotMaxThreads), 0, s, *fp,
                        reinterpret_cast<const prk::ObjDesc *>(objs), big, nbig, escan, total0p,
-                       reinterpret_cast<const prk::ObjEdge *>(work), most);
+                       reinterpret_cast<const prk::ObjEdge *>(work), most, huge_min);
+    return hipGetLastError();
+}
+// ... and those of the huge object big[b] (3 * tris >= huge_min, at most
+// `edges` edges) over many workgroups: scratch = (kMaxactRows + 2) ints + 3
+// words (prk_maxact_huge_scratch bytes), zeroed here.
+size_t prk_maxact_huge_scratch(void) { return (size_t)(prk::kMaxactRows + 2) * 4 + 3 * 8; }
+hipError_t prk_obj_maxact_huge(const prk::FrameParams *fp, const void *objs, const uint32_t *big, uint32_t b,
+                               uint32_t nbig, uint32_t edges, const uint32_t *escan, const uint32_t *total0p,
+                               const void *work, int32_t *most, void *scratch, hipStream_t s) {
+    if (edges == 0) return hipSuccess;
+    const size_t hb = (size_t)(prk::kMaxactRows + 2) * 4;
+    hipError_t e = hipMemsetAsync(scratch, 0, prk_maxact_huge_scratch(), s);
+    if (e != hipSuccess) return e;
+    int32_t *hist = static_cast<int32_t *>(scratch);
+    unsigned long long *acc = reinterpret_cast<unsigned long long *>(static_cast<char *>(scratch) + hb);
+    const prk::ObjDesc *O = reinterpret_cast<const prk::ObjDesc *>(objs);
+    const prk::ObjEdge *W = reinterpret_cast<const prk::ObjEdge *>(work);
+    hipLaunchKernelGGL(prk::k_maxact_huge_part, dim3((edges + prk::kMaxactChunk - 1) / prk::kMaxactChunk),
+                       dim3(prk::kSlotMaxThreads), 0, s, *fp, O, big, b, escan, total0p, W, hist, acc);
+    hipLaunchKernelGGL(prk::k_maxact_huge_fin, dim3(1), dim3(prk::kSlotMaxThreads), 0, s, *fp, O, big, b, nbig,
+                       escan, total0p, W, hist, acc, most);
     return hipGetLastError();
 }
 // ... and a workgroup per large object of mode `mode` (big[0, nbig)): lcap > 0

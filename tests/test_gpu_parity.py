@@ -939,12 +939,14 @@ def test_whole_object_big_walk(gpu, sem, monkeypatch):
     """The huge-object walk (prk_spans.hip k_obj_walk_big: one workgroup over
     a list in device memory, the spans set up afterwards from a replay of
     every edge) forced onto objects that would fit LDS (PRK_OBJ_BIG_MIN=0,
-    PRK_OBJ_ROWS=0): ConstructSphere as one object, overlapping 700- and
+    PRK_OBJ_ROWS=0), and their sizes by the many-workgroup histogram
+    (PRK_OBJ_HUGE_EDGES): ConstructSphere as one object, overlapping 700- and
     64-triangle objects with ties and clipping on every side (odd rows: an
     unpaired last entry), a row band (rows above it paired, not emitted) —
     against the oracle and the one-wave walk (PRK_OBJ_BIG=0), bit for bit."""
     monkeypatch.setenv("PRK_OBJ_BIG_MIN", "0")
     monkeypatch.setenv("PRK_OBJ_ROWS", "0")
+    monkeypatch.setenv("PRK_OBJ_HUGE_EDGES", "1000")  # the many-workgroup sizing (k_maxact_huge_*) too
     sph = _sphere_scene()
     soup = scenes.with_ties(scenes.random_soup(2800, 384, 256, radius=40, seed=23, centroid_margin=40), seed=23)
     if sem == abi.PRK_SEM_SCALAR:
