@@ -3435,19 +3435,30 @@ __global__ void k_span_tiles(FrameParams fp, const SpanPos *__restrict__ pos, ui
     for (int k = 0; k < kmax; ++k) {
         const bool act = k < cnt;
         const uint32_t tile = !act ? 0u : (uint32_t)(k < own ? t.ty * fp.tiles_x + t.tx0 + k : t.oty * fp.tiles_x);
+        // the wave's lanes grouped by tile (ballots only), then one atomic per
+        // group, all groups' at once (their leads), and each lane's rank from
+        // its lead's return (a per-group atomic-and-wait loop serialised the
+        // returns: the placement pass took 2.3x the count pass)
         unsigned long long pending = __ballot(act);
-        uint32_t rank = 0;
-        while (pending) {  // one atomic per distinct tile of the wave
+        int lead_of = lane;
+        uint32_t below = 0, gsize = 0;  // lanes of my group before me; (lead) my group's size
+        while (pending) {
             const int lead = (int)__builtin_ctzll(pending);
             const uint32_t lt = (uint32_t)readlane_i((int32_t)tile, lead);
             const unsigned long long m = __ballot(act && tile == lt) & pending;
-            uint32_t b = 0;
-            if (lane == lead) b = atomicAdd(&ctr[lt], (uint32_t)__popcll(m));
-            b = (uint32_t)readlane_i((int32_t)b, lead);
-            if ((m >> lane) & 1ull) rank = b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if ((m >> lane) & 1ull) {
+                lead_of = lead;
+                below = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            }
+            if (lane == lead) gsize = (uint32_t)__popcll(m);
             pending &= ~m;
         }
-        if (PLACE && act) bins[offs[tile] + rank] = s;
+        uint32_t b = 0;
+        if (act && lane == lead_of) b = atomicAdd(&ctr[tile], gsize);
+        if (PLACE) {
+            b = (uint32_t)__shfl((int32_t)b, lead_of);
+            if (act) bins[offs[tile] + b + below] = s;
+        }
     }
 }
 
