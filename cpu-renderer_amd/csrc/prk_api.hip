@@ -48,6 +48,7 @@ hipError_t prk_launch_raster(const prk::FrameParams *, int, const uint32_t *, co
                              hipStream_t, hipStream_t);
 hipError_t prk_walk_select_bytes(uint32_t, size_t *);
 hipError_t prk_selftest_div_launch(uint32_t n, uint64_t seed, unsigned long long *bad, hipStream_t s);
+hipError_t prk_obj_tables(const void *, uint32_t, uint32_t, uint32_t, void *, uint32_t *, uint32_t *, hipStream_t);
 hipError_t prk_objtri_count(const prk::FrameParams *, const void *, const uint32_t *, const uint32_t *, uint32_t,
                             uint32_t, uint32_t *, unsigned long long *, hipStream_t);
 hipError_t prk_objtri_emit(const prk::FrameParams *, const void *, const uint32_t *, const uint32_t *, uint32_t,
@@ -101,11 +102,14 @@ hipError_t prk_launch_spans(const prk::FrameParams *, const uint32_t *, const ui
                             hipStream_t);
 }
 
-// prk_spans.hip's object descriptor.
+// prk_spans.hip's object descriptor, and the runs of objects the device
+// expands into them (prk_spans.hip ObjRun).
 struct ObjDesc {
     uint32_t draw, g0, tris, tri0, kind, src, nsrc, k1off;
 };
-constexpr uint32_t kObjWave = 0x80000000u;  // ObjDesc::k1off flag: walked by one wave
+struct ObjRun {
+    uint32_t kind, draw, obj0, count, per, tri_count, first_global, tri0, k0base, src_off, src_n, k1off;
+};
 constexpr uint32_t kObjWaveTris = 48;        // objects of this many triangles or more
 constexpr uint64_t kPrMaxEntries = 1ull << 23;  // the chunked walk's list entries per pass (~3 GB of scratch)
 constexpr int kWaveListArrays = 9;           // prk_spans.hip WaveList: int32 arrays of cap + 2 entries
@@ -299,7 +303,7 @@ struct prk_context {
             d_keys_b, d_vals_b, d_offs, d_nwin, d_wtag, d_srecs, d_work, d_ekeys, d_ekeys2, d_evals, d_ecnt, d_escan,
             d_rcnt, d_rscan, d_bound, d_oslot, d_pool, d_err, d_raw, d_most, d_cls, d_prrow, d_prcnt, d_preoff,
             d_prfge, d_prccur, d_prkey, d_prest, d_prsst, d_preend, d_preendm, d_prmatch, d_prsidx, d_prsm, d_prstat,
-            d_segcnt, d_segoff, d_segs, d_wy, d_mhuge;
+            d_segcnt, d_segoff, d_segs, d_wy, d_mhuge, d_objtab, d_k0tab;
         // the pass's host tables, packed into pinned memory for one upload
         // (stage_ev: that upload, before the staging is rewritten)
         char *h_stage = nullptr;
@@ -307,8 +311,8 @@ struct prk_context {
         hipEvent_t stage_ev = nullptr;
         bool stage_busy = false;
         // host tables of the pass, kept until their asynchronous uploads ran
-        std::vector<ObjDesc> h_objs;
-        std::vector<uint32_t> h_k0obj, h_k0tri0, h_big_gl, h_big_cap, h_k1src;
+        std::vector<ObjRun> h_runs;
+        std::vector<uint32_t> h_big_gl, h_big_cap, h_k1src;
         std::vector<unsigned long long> h_big_off;
         std::vector<prk::DrawRec> h_draws;
         std::vector<prk::TexRec> h_texs;
@@ -500,7 +504,7 @@ int prk_destroy(prk_context *c) {
                         &S.d_raw, &S.d_most, &S.d_cls, &S.d_prrow, &S.d_prcnt, &S.d_preoff, &S.d_prfge,
                         &S.d_prccur, &S.d_prkey, &S.d_prest, &S.d_prsst, &S.d_preend, &S.d_preendm,
                         &S.d_prmatch, &S.d_prsidx, &S.d_prsm, &S.d_prstat, &S.d_segcnt, &S.d_segoff,
-                        &S.d_segs, &S.d_wy, &S.d_mhuge};
+                        &S.d_segs, &S.d_wy, &S.d_mhuge, &S.d_objtab, &S.d_k0tab};
         for (DevBuf *b : sb) b->release();
         if (S.h_rb) (void)hipHostFree(S.h_rb);
         if (S.stage_ev) {
@@ -1654,45 +1658,58 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     // of kObjWaveTris triangles or more are walked by one wave each, their
     // list in LDS when their most active edges fit the launch's LDS capacity
     // (min(lcap, the largest such object's edges)), else in their pool slice.
-    S.h_objs.clear();
-    S.h_k0obj.clear();
-    S.h_k0tri0.clear();
+    // (the objects themselves are expanded on the device from runs: a draw
+    // of kind 0 is a run of ceil(tris / obj_tris) objects, kind 2 one of its
+    // spans; only the large objects are listed here)
+    S.h_runs.clear();
     S.h_big_gl.clear();
     S.h_big_off.clear();
     S.h_big_cap.clear();
     S.h_k1src.clear();
-    uint64_t ntri = 0, nk1 = 0, pool = 0, maxn = 1, small_tris = 0;
+    uint64_t ntri = 0, nk1 = 0, pool = 0, maxn = 1, small_tris = 0, nobj64 = 0, nk064 = 0;
     bool thread_links = false;  // a thread-walked triangle object small enough for LDS list links
     std::vector<uint32_t> bigm[prk::MODE_COUNT], bige[prk::MODE_COUNT];  // wave-walked objects by mode, their edges
     for (uint32_t di = 0; di < draws.size(); ++di) {
         const prk::DrawRec &d = draws[di];
         if (d.src_kind == 1) {
-            S.h_objs.push_back(ObjDesc{di, d.first_global, 0u, 0u, 1u, d.src_off, d.src_n, (uint32_t)nk1});
+            S.h_runs.push_back(ObjRun{1u, di, (uint32_t)nobj64, 1u, 0u, 0u, d.first_global, 0u, 0u, d.src_off, d.src_n,
+                                      (uint32_t)nk1});
             for (uint32_t e = 0; e < d.src_n; ++e) S.h_k1src.push_back(d.src_off + e);
             nk1 += d.src_n;
+            nobj64 += 1;
         } else if (d.src_kind == 2) {
-            for (uint32_t k = 0; k < d.src_n; ++k)
-                S.h_objs.push_back(ObjDesc{di, d.first_global + k, 0u, 0u, 2u, d.src_off + k, 1u, 0u});
+            if (!d.src_n) continue;
+            S.h_runs.push_back(ObjRun{2u, di, (uint32_t)nobj64, d.src_n, 0u, 0u, d.first_global, 0u, 0u, d.src_off, 0u, 0u});
+            nobj64 += d.src_n;
         } else {
             const uint32_t per = std::max<uint32_t>(1u, d.obj_tris);
-            for (uint32_t t = 0; t < d.tri_count; t += per) {
-                const uint32_t n = std::min(per, d.tri_count - t);
-                const uint64_t edges = 3ull * n;  // the most its FillEdgeTable writes
-                maxn = std::max(maxn, edges);
-                const bool wave = n >= kObjWaveTris;
-                thread_links = thread_links || (!wave && edges <= prk_obj_link_cap());
-                if (wave) {
-                    bigm[d.mode].push_back((uint32_t)S.h_objs.size());
-                    bige[d.mode].push_back((uint32_t)edges);
-                } else {
-                    small_tris += n;
+            const uint32_t cnt = (uint32_t)(((uint64_t)d.tri_count + per - 1) / per);
+            if (!cnt) continue;
+            S.h_runs.push_back(ObjRun{0u, di, (uint32_t)nobj64, cnt, per, d.tri_count, d.first_global, (uint32_t)ntri,
+                                      (uint32_t)nk064, 0u, 0u, 0u});
+            maxn = std::max<uint64_t>(maxn, 3ull * std::min(per, d.tri_count));  // the most its FillEdgeTable writes
+            if (per >= kObjWaveTris) {
+                for (uint32_t j = 0; j < cnt; ++j) {
+                    const uint32_t n = std::min(per, d.tri_count - j * per);
+                    if (n >= kObjWaveTris) {
+                        bigm[d.mode].push_back((uint32_t)(nobj64 + j));
+                        bige[d.mode].push_back(3u * n);
+                    } else {
+                        small_tris += n;
+                        thread_links = thread_links || 3ull * n <= prk_obj_link_cap();
+                    }
                 }
-                S.h_k0obj.push_back((uint32_t)S.h_objs.size());
-                S.h_k0tri0.push_back((uint32_t)ntri);
-                S.h_objs.push_back(ObjDesc{di, d.first_global + t, n, (uint32_t)ntri, 0u, 0u, 0u, wave ? kObjWave : 0u});
-                ntri += n;
+            } else {
+                const uint32_t rem = d.tri_count % per;
+                small_tris += d.tri_count;
+                thread_links = thread_links || (d.tri_count >= per && 3ull * per <= prk_obj_link_cap()) ||
+                               (rem && 3ull * rem <= prk_obj_link_cap());
             }
+            nobj64 += cnt;
+            nk064 += cnt;
+            ntri += d.tri_count;
         }
+        if (nobj64 >= 0x7FFFFFFFull) return PRK_ERR_LIMIT;
     }
     std::vector<uint32_t> big_edges;  // (h_big_gl order)
     for (int mo = 0; mo < prk::MODE_COUNT; ++mo)  // the large objects, by mode (their walk groups: after the readback)
@@ -1702,7 +1719,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
         }
     // edge slots (3 per triangle + the caller edges) are indexed by 31 bits
     if (3 * ntri + nk1 >= 0x7FFFFFFFull) return PRK_ERR_LIMIT;
-    const uint32_t nobj = (uint32_t)S.h_objs.size(), nk0 = (uint32_t)S.h_k0obj.size();
+    const uint32_t nobj = (uint32_t)nobj64, nk0 = (uint32_t)nk064;
     const uint32_t nt = (uint32_t)ntri, nbig_all = (uint32_t)S.h_big_gl.size();
     // MergeSort key: (object, min(YMin, H), recursion path) in one radix sort
     auto bitlen = [](uint64_t v) { uint32_t b = 0; while (v) { ++b; v >>= 1; } return b; };
@@ -1716,15 +1733,15 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     // (the scratch below is reused frame to frame: stream order on s covers it)
     // The pass's host tables go up in one copy from pinned staging (a pageable
     // hipMemcpyAsync per table held the host for each).
-    enum { T_DRAWS, T_TEXS, T_OBJS, T_K0OBJ, T_K0TRI0, T_BIG, T_BIG_OFF, T_BIG_CAP, T_K1SRC, T_EDGES, T_SPANS, T_N };
+    enum { T_DRAWS, T_TEXS, T_OBJS, T_K0OBJ, T_K0TRI0, T_BIG, T_BIG_OFF, T_BIG_CAP, T_K1SRC, T_EDGES, T_SPANS, T_N };  // (T_OBJS: the runs)
     struct Part {
         const void *src;
         size_t bytes, off;
     } parts[T_N] = {{S.h_draws.data(), S.h_draws.size() * sizeof(prk::DrawRec), 0},
                     {S.h_texs.data(), S.h_texs.size() * sizeof(prk::TexRec), 0},
-                    {S.h_objs.data(), S.h_objs.size() * sizeof(ObjDesc), 0},
-                    {S.h_k0obj.data(), S.h_k0obj.size() * 4, 0},
-                    {S.h_k0tri0.data(), S.h_k0tri0.size() * 4, 0},
+                    {S.h_runs.data(), S.h_runs.size() * sizeof(ObjRun), 0},
+                    {nullptr, 0, 0},
+                    {nullptr, 0, 0},
                     {S.h_big_gl.data(), S.h_big_gl.size() * 4, 0},
                     {nullptr, 0, 0},
                     {nullptr, 0, 0},
@@ -1762,8 +1779,14 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     fp.draw0 = draws[0];
     fp.tex0 = prk::TexRec{};
     if (fp.draw0.tex >= 0 && (size_t)fp.draw0.tex < S.h_texs.size()) fp.tex0 = S.h_texs[fp.draw0.tex];
-    void *d_objs = dev(T_OBJS), *d_edges_in = dev(T_EDGES), *d_spans_in = dev(T_SPANS);
-    const uint32_t *d_k0obj = (const uint32_t *)dev(T_K0OBJ), *d_k0tri0 = (const uint32_t *)dev(T_K0TRI0);
+    void *d_edges_in = dev(T_EDGES), *d_spans_in = dev(T_SPANS);
+    // the objects (ObjDesc), the kind-0 objects' indices and first triangles
+    PRK_TRY(S.d_objtab.ensure((size_t)std::max<uint32_t>(nobj, 1) * sizeof(ObjDesc)));
+    PRK_TRY(S.d_k0tab.ensure((size_t)std::max<uint32_t>(nk0, 1) * 8));
+    void *d_objs = S.d_objtab.p;
+    uint32_t *k0tab = (uint32_t *)S.d_k0tab.p;
+    const uint32_t *d_k0obj = k0tab, *d_k0tri0 = k0tab + nk0;
+    PRK_TRY(prk_obj_tables(dev(T_OBJS), (uint32_t)S.h_runs.size(), nobj, kObjWaveTris, d_objs, k0tab, k0tab + nk0, s));
     const uint32_t *d_big = (const uint32_t *)dev(T_BIG);
     const uint32_t *d_k1src = (const uint32_t *)dev(T_K1SRC);
     uint32_t modes = 0;  // the pass's span kinds: bit per Mode

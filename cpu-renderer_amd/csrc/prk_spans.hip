@@ -71,6 +71,36 @@ constexpr uint32_t kObjWave = 0x80000000u;
 // walked by rows, or failed its check (the workgroup walk takes it).
 constexpr uint32_t kPrDone = 1u, kPrFailed = 2u;
 
+// A run of objects as the host lists them (prk_api.hip ObjRun): a draw of
+// kind 0 is `count` objects of `per` triangles (the last one shorter), kind 2
+// one object per span, kind 1 one object; k_obj_tables expands them.
+struct ObjRun {
+    uint32_t kind, draw, obj0, count, per, tri_count, first_global, tri0, k0base, src_off, src_n, k1off;
+};
+__global__ void k_obj_tables(const ObjRun *__restrict__ runs, uint32_t nruns, uint32_t nobj, uint32_t wave_tris,
+                             ObjDesc *__restrict__ objs, uint32_t *__restrict__ k0obj, uint32_t *__restrict__ k0tri0) {
+    const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= nobj) return;
+    uint32_t lo = 0, hi = nruns;  // the last run with obj0 <= o
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (runs[mid].obj0 <= o) lo = mid;
+        else hi = mid;
+    }
+    const ObjRun R = runs[lo];
+    const uint32_t j = o - R.obj0;
+    if (R.kind == 1) {
+        objs[o] = ObjDesc{R.draw, R.first_global, 0u, 0u, 1u, R.src_off, R.src_n, R.k1off};
+    } else if (R.kind == 2) {
+        objs[o] = ObjDesc{R.draw, R.first_global + j, 0u, 0u, 2u, R.src_off + j, 1u, 0u};
+    } else {
+        const uint32_t t = j * R.per, n = min(R.per, R.tri_count - t);
+        objs[o] = ObjDesc{R.draw, R.first_global + t, n, R.tri0 + t, 0u, 0u, 0u, n >= wave_tris ? kObjWave : 0u};
+        k0obj[R.k0base + j] = o;
+        k0tri0[R.k0base + j] = R.tri0 + t;
+    }
+}
+
 // Caller edges (prk_edge = edge_info without Next, prk.h) and spans (prk_span).
 struct EdgeIn {
     int32_t YMax;
@@ -3466,6 +3496,15 @@ __global__ void k_span_tiles(FrameParams fp, const SpanPos *__restrict__ pos, ui
 
 extern "C" {
 
+// The pass's objects (ObjDesc) and kind-0 object tables from the host's runs.
+hipError_t prk_obj_tables(const void *runs, uint32_t nruns, uint32_t nobj, uint32_t wave_tris, void *objs,
+                          uint32_t *k0obj, uint32_t *k0tri0, hipStream_t s) {
+    if (nobj == 0) return hipSuccess;
+    hipLaunchKernelGGL(prk::k_obj_tables, dim3((nobj + 255) / 256), dim3(256), 0, s,
+                       reinterpret_cast<const prk::ObjRun *>(runs), nruns, nobj, wave_tris,
+                       reinterpret_cast<prk::ObjDesc *>(objs), k0obj, k0tri0);
+    return hipGetLastError();
+}
 // FillEdgeTable of the pass's object triangles: per-triangle edge and
 // active-row counts (ntri + 1 values each, the last 0) ...
 hipError_t prk_objtri_count(const prk::FrameParams *fp, const void *objs, const uint32_t *k0obj,
