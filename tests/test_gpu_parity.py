@@ -968,6 +968,46 @@ def test_whole_object_big_walk(gpu, sem, monkeypatch):
     assert (gw == ow[r0:r1]).all()
 
 
+def _degenerate_soup(seed):
+    """A clipped soup with hostile vertices: at the camera plane (distance 0),
+    behind it, NaN and infinite coordinates, and zero-area slivers — what
+    FillEdgeTable's cull and clip (3926-4066) must sort out before any list
+    sees an edge."""
+    s = scenes.with_ties(scenes.random_soup(1500, 256, 160, radius=30, seed=seed, centroid_margin=30), seed=seed)
+    D = s.transform[0]
+    v = s.vertices.reshape(-1, 3, 3).copy()
+    rng = np.random.default_rng(seed)
+    idx = rng.choice(len(v), 60, replace=False)
+    v[idx[:10], 0, 2] = D                 # on the camera plane
+    v[idx[10:20], 1, 2] = D + 0.5         # behind the camera
+    v[idx[20:30], 2, 0] = np.nan
+    v[idx[30:40], 0, 1] = np.inf
+    v[idx[40:50], 1] = v[idx[40:50], 0]   # two equal vertices: zero area
+    v[idx[50:60], 2] = v[idx[50:60], 0] + (v[idx[50:60], 1] - v[idx[50:60], 0]) * 0.5  # collinear
+    s.vertices = v.reshape(-1, 3).astype(np.float32)
+    return s
+
+
+@pytest.mark.parametrize("path", ["default", "big", "wave"])
+@pytest.mark.parametrize("tpo", [1, 8, 64, 500])
+def test_degenerate_geometry_every_walk(gpu, path, tpo, monkeypatch):
+    """Hostile vertices (camera plane, behind the camera, NaN / inf, zero-area
+    and collinear triangles) per triangle and in objects of 8 / 64 / 500
+    triangles, through the default walks, the huge-object walk (forced) and
+    the one-wave walk (forced): the oracle's image, bit for bit."""
+    if path == "big":
+        monkeypatch.setenv("PRK_OBJ_BIG_MIN", "0")
+        monkeypatch.setenv("PRK_OBJ_ROWS", "0")
+        monkeypatch.setenv("PRK_OBJ_HUGE_EDGES", "100")
+    elif path == "wave":
+        monkeypatch.setenv("PRK_OBJ_BIG_MIN", "0")
+        monkeypatch.setenv("PRK_OBJ_ROWS", "0")
+        monkeypatch.setenv("PRK_OBJ_BIG", "0")
+    s = _degenerate_soup(11 + tpo)
+    run_both(s, semantics=abi.PRK_SEM_AVX, phong=True, tris_per_object=tpo, threads=1,
+             label="degenerate tpo=%d %s" % (tpo, path))
+
+
 def test_whole_object_mid_lists_lds(gpu):
     """Objects whose lists stay in LDS (<= 4096 edges per object) while
     several hundred edges enter per row: the batched insertion in LDS."""
