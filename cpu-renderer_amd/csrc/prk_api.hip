@@ -80,7 +80,8 @@ hipError_t prk_obj_walk_group(const prk::FrameParams *, int32_t, uint32_t, const
                               uint32_t *, uint32_t *, const uint32_t *, hipStream_t);
 uint32_t prk_big_max_entries(void);
 uint64_t prk_big_slice_ints(uint32_t, uint32_t, uint32_t);
-hipError_t prk_big_walk(const prk::FrameParams *, int32_t, const void *, const uint32_t *, const unsigned long long *,
+uint32_t prk_big_lds_cap(void);
+hipError_t prk_big_walk(const prk::FrameParams *, int32_t, int, const void *, const uint32_t *, const unsigned long long *,
                         const uint32_t *, const uint32_t *, uint32_t, uint32_t, int32_t *, const uint32_t *,
                         const uint32_t *, const void *, const unsigned long long *, void *, void *, uint32_t *,
                         uint32_t *, const uint32_t *, hipStream_t);
@@ -1919,8 +1920,9 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     struct Group {
         int32_t mode;
         uint32_t lcap, start, count;
-        bool big;             // the huge-object walk (k_obj_walk_big)
+        bool big;             // the huge-object walk (k_obj_walk_big / k_obj_walk_lds)
         uint32_t max_rows;    // (big: its objects' most rows)
+        bool lds;             // (big: the list in LDS, k_obj_walk_lds)
     };
     std::vector<Group> groups;
     uint32_t *cls_big = reinterpret_cast<uint32_t *>(S.h_cls + (size_t)nbig_all * 12);
@@ -1929,21 +1931,24 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     uint32_t *cls_pr = cls_cap + nbig_all;  // PrObj[npr] (8 words each)
     uint32_t *cls_grp = cls_pr + 8 * (size_t)nbig_all;  // its objects grouped by (mode, LDS capacity)
     uint32_t *cls_meta = cls_grp + nbig_all;           // (rows, ents) per object, walk-group order
-    // Objects whose lists outgrow LDS take the huge-object walk (a
-    // workgroup, the list in device memory: k_obj_walk_big) when their sizes
-    // are known (k_obj_maxact) and fit it, else one wave each (k_obj_walk_wave).
-    // PRK_OBJ_BIG=0: always the wave; PRK_OBJ_BIG_MIN=n (tests): objects of
-    // more than n active edges skip the LDS lists.
+    // Objects whose lists outgrow the workgroup walk's LDS slots take the
+    // huge-object walk (a workgroup of 1024: k_obj_walk_lds with the whole
+    // list in LDS when it fits prk_big_lds_cap() entries, else k_obj_walk_big
+    // with it in device memory) when their sizes are known (k_obj_maxact) and
+    // fit, else one wave each (k_obj_walk_wave).  PRK_OBJ_BIG=0: always the
+    // wave; PRK_OBJ_LDSWALK=0: never the LDS form; PRK_OBJ_BIG_MIN=n (tests):
+    // objects of more than n active edges skip the LDS slot classes.
     {
-        const char *benv = std::getenv("PRK_OBJ_BIG"), *menv = std::getenv("PRK_OBJ_BIG_MIN");
-        const bool big_on = !(benv && benv[0] == '0');
+        const char *benv = std::getenv("PRK_OBJ_BIG"), *menv = std::getenv("PRK_OBJ_BIG_MIN"),
+                   *lenv = std::getenv("PRK_OBJ_LDSWALK");
+        const bool big_on = !(benv && benv[0] == '0'), lds_on = !(lenv && lenv[0] == '0');
         const int64_t big_min = menv ? std::atoll(menv) : INT64_MAX;
         const int32_t *h_rows = h_most + nbig_all, *h_ents = h_most + 2 * (size_t)nbig_all;
         static const uint32_t kCaps[] = {62, 126, 254, 510, 1022};
         uint32_t k = 0, b = 0;
         for (int mo = 0; mo < prk::MODE_COUNT; ++mo) {
             const uint32_t b0 = b;
-            for (int ci = 0; ci <= 6; ++ci) {  // ci 5: the huge-object walk, 6: one wave each
+            for (int ci = 0; ci <= 7; ++ci) {  // ci 5 / 6: the huge-object walk in LDS / device memory, 7: one wave each
                 const uint32_t capc = ci < 5 ? kCaps[ci] : 0u;
                 if (ci < 5 && capc > lcap) continue;
                 const uint32_t start = k;
@@ -1959,26 +1964,28 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
                         }
                     if (want != capc) continue;
                     const int32_t rows = h_rows[bi], ents = h_ents[bi];
+                    const bool huge = ci == 5 || ci == 6;
                     if (ci >= 5) {
                         const bool hb = big_on && most > 0 && (uint32_t)most <= prk_big_max_entries() && rows > 0 &&
                                         rows < INT32_MAX && ents >= 0 && ents < INT32_MAX &&
                                         bigm[mo].size() <= 65535;
-                        if (hb != (ci == 5)) continue;
+                        const bool hl = hb && lds_on && (uint32_t)most <= prk_big_lds_cap() && rows < 16000;
+                        if ((hb ? (hl ? 5 : 6) : 7) != ci) continue;
                     }
-                    const uint32_t cap = ci == 5 ? (uint32_t)most : bige[mo][i];
-                    if (ci == 5) pool = (pool + 3) & ~3ull;  // (16-B aligned slices)
+                    const uint32_t cap = huge ? (uint32_t)most : bige[mo][i];
+                    if (huge) pool = (pool + 3) & ~3ull;  // (16-B aligned slices)
                     cls_big[k] = bigm[mo][i];
                     cls_off[k] = capc ? 0ull : pool;
                     cls_cap[k] = capc ? 0u : cap;
-                    cls_meta[2 * k] = ci == 5 ? (uint32_t)rows : 0u;
-                    cls_meta[2 * k + 1] = ci == 5 ? (uint32_t)ents : 0u;
+                    cls_meta[2 * k] = huge ? (uint32_t)rows : 0u;
+                    cls_meta[2 * k + 1] = huge ? (uint32_t)ents : 0u;
                     if (!capc)
-                        pool += ci == 5 ? prk_big_slice_ints(cap, (uint32_t)rows, (uint32_t)ents)
-                                        : (uint64_t)kWaveListArrays * (cap + 2);
-                    if (ci == 5) gmax = std::max(gmax, (uint32_t)rows);
+                        pool += huge ? prk_big_slice_ints(cap, (uint32_t)rows, (uint32_t)ents)
+                                     : (uint64_t)kWaveListArrays * (cap + 2);
+                    if (huge) gmax = std::max(gmax, (uint32_t)rows);
                     ++k;
                 }
-                if (k > start) groups.push_back(Group{mo, capc, start, k - start, ci == 5, gmax});
+                if (k > start) groups.push_back(Group{mo, capc, start, k - start, ci == 5 || ci == 6, gmax, ci == 5});
             }
             b += (uint32_t)bigm[mo].size();
         }
@@ -2153,7 +2160,7 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
                          (uint32_t *)S.d_err.p, thread_links ? 1 : 0, d_segs, d_nseg, (uint32_t)max_segs, s));
     for (const Group &g : groups) {
         if (g.big)
-            PRK_TRY(prk_big_walk(&fp, g.mode, d_objs, d_cbig + g.start, d_coff + g.start, d_ccap + g.start,
+            PRK_TRY(prk_big_walk(&fp, g.mode, g.lds ? 1 : 0, d_objs, d_cbig + g.start, d_coff + g.start, d_ccap + g.start,
                                  d_cmeta + 2 * (size_t)g.start, g.count, g.max_rows, (int32_t *)S.d_pool.p, escan,
                                  total0p, S.d_work.p, oslot, S.d_raw.p, S.d_pos.p, (uint32_t *)S.d_span_tri.p,
                                  (uint32_t *)S.d_err.p, d_prstat, s));

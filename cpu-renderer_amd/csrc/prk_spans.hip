@@ -2804,6 +2804,408 @@ __global__ void __launch_bounds__(kBigThreads) k_obj_walk_big(FrameParams fp, co
     }
 }
 
+// ---------------------------------------------------------------------------
+// The huge-object walk with the whole list in LDS (objects of at most
+// kLdsCap most active edges -- C3b as ONE object: 8898): the same rows, the
+// same list operations and the same output (hdr, ri, ids: k_big_replay sets
+// the spans up) as k_obj_walk_big, but every list access an LDS access, so a
+// row is a chain of LDS passes and workgroup barriers instead of device-
+// memory round trips.  An entry is 14 bytes: X, Gradient, its edge index and
+// (min(YMax, MaxY) - FirstRow) << 1 | Left (FillEdgeTable's Left is 0 / 1).
+// The list is updated in place: a pass reads what it moves into registers,
+// a barrier, then writes.
+//   insertion + expiry (3654-3749): each new edge's gap as k_obj_walk_big
+//     finds it (per-16 key maxima, prefix-maxed, then 16 entries); the kept
+//     new edges ranked by (gap, key, arrival) through coarse bins of 16 gaps
+//     (counts, scan, each bin's few members compared); thread t owns old
+//     entries [9t, 9t + 9): a kept entry q goes to  #kept before q + #kept new
+//     of gap <= q  (a binary search once, then a walk), a kept new edge to
+//     #kept before its gap + its rank.
+//   pairing (3751-3869): thread k reads pairs k - 1, k, k + 1, steps and
+//     swaps them as big_pair does, writes entries 2k, 2k + 1 after a barrier,
+//     with the next row's per-16 key maxima.
+// ---------------------------------------------------------------------------
+constexpr int kLdsCap = 9200;                      // list entries (< 577 * 16: 576 coarse bins)
+constexpr int kLdsPer = (kLdsCap + kBigThreads - 1) / kBigThreads;  // old entries a thread owns (9)
+constexpr int kLdsSamp = 576;                      // per-16 maxima (>= kLdsCap / 16)
+constexpr int kLdsPairs = (kLdsCap / 2 + kBigThreads - 1) / kBigThreads;  // pairs a thread owns (5)
+static_assert(kLdsCap <= kLdsSamp * 16 && kLdsPer * kBigThreads >= kLdsCap, "LDS walk sizes");
+struct LdsWalk {
+    float x[kLdsCap], g[kLdsCap];
+    int32_t e[kLdsCap];
+    uint16_t y[kLdsCap];                 // (min(YMax, MaxY) - FirstRow) << 1 | Left
+    float sx[kLdsSamp], sg[kLdsSamp];   // per-16 key maxima; then (insertion) the coarse bins' counts / cursors
+    int32_t sl[kLdsSamp];               // (... and the bins' members, uint16)
+    float nx[kBigThreads], ng[kBigThreads];  // the batch's new edges
+    int32_t ne[kBigThreads];
+    uint16_t ny[kBigThreads], ngap[kBigThreads];
+    uint16_t sgap[kBigThreads];          // the kept new edges' gaps in (gap, key, arrival) order
+    uint16_t kbase[kBigThreads];         // kept old entries before thread t's nine
+};
+__device__ __forceinline__ LKey lds_key(const LdsWalk &W, int q) { return entry_key(W.x[q], W.g[q], W.y[q] & 1); }
+struct LdsE {  // an entry in registers
+    float x, g;
+    int32_t yp, e;  // packed row | Left, edge index
+};
+__device__ __forceinline__ LdsE lds_entry(const LdsWalk &W, int q) { return LdsE{W.x[q], W.g[q], W.y[q], W.e[q]}; }
+// A pair stepped (X += Gradient, 3811-3829) and first-swapped (3831-3841):
+// a its first entry, b its second.
+__device__ __forceinline__ void lds_first_swap(LdsE &a, LdsE &b) {
+    a.x += a.g;
+    b.x += b.g;
+    if (a.x > b.x) {
+        const LdsE t = a;
+        a = b;
+        b = t;
+    }
+}
+__device__ __forceinline__ uint16_t lds_ypack(int32_t ymax, int32_t left, int32_t FirstRow, int32_t MaxY) {
+    return (uint16_t)(((min(max(ymax, FirstRow), MaxY) - FirstRow) << 1) | (left & 1));
+}
+
+// Insertion of the batch's new edges W.n*[c0, c0 + kb) and, when `expire`,
+// expiry at row FirstRow + rrel (an entry leaves when YMax <= Row: its packed
+// row <= rrel); returns the new length.  samples_ok: W.s* hold the list's
+// per-16 key maxima (the pairing left them).
+__device__ __forceinline__ int lds_insert(LdsWalk &W, BlockRed &R, int m, int c0, int kb, bool expire,
+                                          int32_t rrel, bool samples_ok) {
+    const int tid = threadIdx.x;
+    const bool mine = tid < kb;
+    int32_t gapc = 0;
+    bool keptc = false;
+    if (kb > 0) {
+        if (m > 0) {
+            const int ns = (m + 15) >> 4;
+            if (!samples_ok) {
+                for (int j = tid; j < ns; j += kBigThreads) {
+                    LKey mx{-INFINITY, -INFINITY, INT32_MIN};
+                    for (int u = 0; u < 16 && 16 * j + u < m; ++u) {
+                        const LKey k = lds_key(W, 16 * j + u);
+                        if (key_gt(k, mx)) mx = k;
+                    }
+                    W.sx[j] = mx.x; W.sg[j] = mx.g; W.sl[j] = mx.l;
+                }
+                __syncthreads();
+            }
+            LKey pk = tid < ns ? LKey{W.sx[tid], W.sg[tid], W.sl[tid]} : LKey{-INFINITY, -INFINITY, INT32_MIN};
+            blk_key_prefix_max(R, pk);
+            if (tid < ns) { W.sx[tid] = pk.x; W.sg[tid] = pk.g; W.sl[tid] = pk.l; }
+            __syncthreads();
+            if (mine) {  // the first entry whose key exceeds the new edge's (3663-3667)
+                const LKey kc{W.nx[c0 + tid], W.ng[c0 + tid], (int32_t)(W.ny[c0 + tid] & 1)};
+                int lo = 0, hi = ns;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (key_gt(LKey{W.sx[mid], W.sg[mid], W.sl[mid]}, kc)) hi = mid;
+                    else lo = mid + 1;
+                }
+                gapc = m;
+                if (lo < ns) {
+                    const int q0 = lo << 4, qn = min(16, m - q0);
+                    for (int u = 0; u < qn; ++u)
+                        if (key_gt(lds_key(W, q0 + u), kc)) { gapc = q0 + u; break; }
+                }
+            }
+            __syncthreads();  // (the sample arrays hold the bins below)
+        }
+        if (mine) {
+            keptc = !expire || (int32_t)(W.ny[c0 + tid] >> 1) > rrel;
+            W.ngap[tid] = (uint16_t)gapc;
+        }
+    }
+    // the kept new edges ranked by (gap, key, arrival), through coarse bins of 16 gaps
+    int kn = 0;
+    int32_t srank = 0;
+    if (kb > 0) {
+        int32_t *bcnt = reinterpret_cast<int32_t *>(W.sx), *bcur = reinterpret_cast<int32_t *>(W.sg);
+        uint16_t *bmem = reinterpret_cast<uint16_t *>(W.sl);
+        const int nb = (m >> 4) + 1;  // (<= 576)
+        if (tid < nb) bcnt[tid] = 0;
+        __syncthreads();
+        const int bin = gapc >> 4;
+        if (mine && keptc) atomicAdd(&bcnt[bin], 1);
+        __syncthreads();
+        const int32_t cv = tid < nb ? bcnt[tid] : 0;
+        int32_t tot;
+        const int32_t ex = blk_excl_sum(R, cv, tot);
+        kn = tot;
+        if (tid < nb) { bcnt[tid] = ex; bcur[tid] = ex; }
+        __syncthreads();
+        if (mine && keptc) bmem[atomicAdd(&bcur[bin], 1)] = (uint16_t)tid;
+        __syncthreads();
+        if (mine && keptc) {
+            const LKey kc{W.nx[c0 + tid], W.ng[c0 + tid], (int32_t)(W.ny[c0 + tid] & 1)};
+            const int32_t b0 = bcnt[bin], b1 = bin + 1 < nb ? bcnt[bin + 1] : kn;
+            int32_t r = 0;
+            for (int32_t s = b0; s < b1; ++s) {
+                const int u = bmem[s];
+                if (u == tid) continue;
+                const int32_t gu = W.ngap[u];
+                const LKey ku{W.nx[c0 + u], W.ng[c0 + u], (int32_t)(W.ny[c0 + u] & 1)};
+                r += (gu < gapc || (gu == gapc && (key_gt(kc, ku) || (!key_gt(ku, kc) && u < tid)))) ? 1 : 0;
+            }
+            srank = b0 + r;
+            W.sgap[srank] = (uint16_t)gapc;
+        }
+    }
+    // the old entries (thread t: [9t, 9t + 9)), their kept counts
+    const int q0 = kLdsPer * tid;
+    float ox[kLdsPer], og[kLdsPer];
+    int32_t oe[kLdsPer];
+    uint16_t oy[kLdsPer];
+    uint32_t keep = 0;
+    int32_t kc_t = 0;
+#pragma unroll
+    for (int u = 0; u < kLdsPer; ++u) {
+        const int q = q0 + u;
+        ox[u] = og[u] = 0.0f;
+        oe[u] = 0;
+        oy[u] = 0;
+        if (q < m) {
+            ox[u] = W.x[q]; og[u] = W.g[q]; oe[u] = W.e[q]; oy[u] = W.y[q];
+            const bool k = !expire || (int32_t)(oy[u] >> 1) > rrel;
+            keep |= (k ? 1u : 0u) << u;
+            kc_t += k ? 1 : 0;
+        }
+    }
+    int32_t kept_old;
+    const int32_t kbt = blk_excl_sum(R, kc_t, kept_old);  // (its barriers also publish sgap)
+    W.kbase[tid] = (uint16_t)kbt;
+    __syncthreads();
+    // places: a kept old entry q at #kept before q + #kept new of gap <= q
+    int32_t opos[kLdsPer];
+    {
+        int lo = 0, hi = kn;  // #kept new with gap < q0... (the first with gap > q0 - 1)
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if ((int)W.sgap[mid] < q0) lo = mid + 1;
+            else hi = mid;
+        }
+        int p = lo;
+        int32_t kb_run = kbt;
+#pragma unroll
+        for (int u = 0; u < kLdsPer; ++u) {
+            const int q = q0 + u;
+            while (p < kn && (int)W.sgap[p] <= q) ++p;
+            opos[u] = kb_run + p;
+            kb_run += (keep >> u) & 1u;
+        }
+    }
+    // a kept new edge at #kept before its gap + its rank
+    int32_t npos = 0;
+    if (kb > 0 && mine && keptc) {
+        int32_t before = kept_old;
+        if (gapc < m) {
+            const int t = gapc / kLdsPer;
+            before = W.kbase[t];
+            for (int q = kLdsPer * t; q < gapc; ++q) before += (!expire || (int32_t)(W.y[q] >> 1) > rrel) ? 1 : 0;
+        }
+        npos = before + srank;
+    }
+    __syncthreads();  // (every read of the old list is done)
+#pragma unroll
+    for (int u = 0; u < kLdsPer; ++u)
+        if ((keep >> u) & 1u) {
+            const int32_t to = opos[u];
+            W.x[to] = ox[u]; W.g[to] = og[u]; W.e[to] = oe[u]; W.y[to] = oy[u];
+        }
+    if (kb > 0 && mine && keptc) {
+        W.x[npos] = W.nx[c0 + tid]; W.g[npos] = W.ng[c0 + tid]; W.e[npos] = W.ne[c0 + tid]; W.y[npos] = W.ny[c0 + tid];
+    }
+    __syncthreads();
+    return kept_old + kn;
+}
+
+// Pairing (3751-3869) in place, as big_pair: the row's record and list out
+// (ri, ids), every pair stepped and swapped, the next row's per-16 key maxima
+// in W.s*.
+__device__ __forceinline__ void lds_pair(LdsWalk &W, const BigList &L, int m, int32_t r, bool emit, uint32_t j0,
+                                         uint32_t off) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int P = m >> 1, items = P + (m & 1);
+    int32_t *ids = L.ids + off;
+    if (tid == 0) {
+        int32_t *q = L.ri + 4 * (size_t)r;
+        q[0] = (int32_t)off;
+        q[1] = m;
+        q[2] = emit ? (int32_t)j0 : (int32_t)kBigNoEmit;
+        q[3] = (m & 1) ? W.e[m - 1] : -1;
+    }
+    LdsE o0[kLdsPairs], o1[kLdsPairs];
+#pragma unroll
+    for (int i = 0; i < kLdsPairs; ++i) {
+        const int k = tid + i * kBigThreads;
+        o0[i] = o1[i] = LdsE{0.0f, 0.0f, 0, 0};
+        if (k < items) {
+            const int e = 2 * k;
+            ids[e] = W.e[e];
+            if (k == P) {  // the odd last entry: not paired, not stepped, stays
+                o0[i] = lds_entry(W, e);
+                continue;
+            }
+            ids[e + 1] = W.e[e + 1];
+            // pairs k - 1, k, k + 1 stepped and first-swapped
+            LdsE a[3], b[3];
+#pragma unroll
+            for (int h = 0; h < 3; ++h) {
+                const int ea = 2 * min(max(k - 1 + h, 0), P - 1);
+                a[h] = lds_entry(W, ea);
+                b[h] = lds_entry(W, ea + 1);
+                lds_first_swap(a[h], b[h]);
+            }
+            const bool lo = k >= 1 && b[0].x > a[1].x;      // boundary k (3843-3853)
+            const bool hi = k + 1 < P && b[1].x > a[2].x;   // boundary k + 1
+            o0[i] = lo ? b[0] : a[1];
+            o1[i] = hi ? a[2] : b[1];
+        }
+    }
+    __syncthreads();  // (every read of the list is done)
+#pragma unroll
+    for (int i = 0; i < kLdsPairs; ++i) {
+        if (i * kBigThreads >= items) break;  // (uniform)
+        const int k = tid + i * kBigThreads;
+        const int e = 2 * k;
+        LKey ka{-INFINITY, -INFINITY, INT32_MIN}, kb2{-INFINITY, -INFINITY, INT32_MIN};
+        if (k < P) {
+            W.x[e] = o0[i].x; W.g[e] = o0[i].g; W.y[e] = (uint16_t)o0[i].yp; W.e[e] = o0[i].e;
+            W.x[e + 1] = o1[i].x; W.g[e + 1] = o1[i].g; W.y[e + 1] = (uint16_t)o1[i].yp; W.e[e + 1] = o1[i].e;
+            ka = entry_key(o0[i].x, o0[i].g, o0[i].yp & 1);
+            kb2 = entry_key(o1[i].x, o1[i].g, o1[i].yp & 1);
+        } else if (k == P) {
+            ka = entry_key(o0[i].x, o0[i].g, o0[i].yp & 1);
+        }
+        LKey kk = key_gt(kb2, ka) ? kb2 : ka;  // the maximum of the 16 entries of 8 lanes
+        int32_t p = 0;
+        key_max_step<kDppShr1>(kk, p);
+        key_max_step<kDppShr2>(kk, p);
+        key_max_step<kDppShr4>(kk, p);
+        if ((lane & 7) == 7 && (k >> 3) < kLdsSamp) {
+            W.sx[k >> 3] = kk.x; W.sg[k >> 3] = kk.g; W.sl[k >> 3] = kk.l;
+        }
+    }
+    __syncthreads();
+}
+
+// One workgroup per huge object whose most active edges fit kLdsCap (the
+// pool slice, meta and outputs as k_obj_walk_big's).
+__global__ void __launch_bounds__(kBigThreads) k_obj_walk_lds(FrameParams fp, const ObjDesc *__restrict__ objs,
+                                                             const uint32_t *__restrict__ big,
+                                                             const unsigned long long *__restrict__ big_off,
+                                                             const uint32_t *__restrict__ big_cap,
+                                                             const uint32_t *__restrict__ big_meta,
+                                                             int32_t *__restrict__ pool,
+                                                             const uint32_t *__restrict__ escan,
+                                                             const uint32_t *__restrict__ total0p,
+                                                             const ObjEdge *__restrict__ work,
+                                                             const unsigned long long *__restrict__ soff,
+                                                             uint32_t *__restrict__ err,
+                                                             const uint32_t *__restrict__ prstat) {
+    __shared__ LdsWalk W;
+    __shared__ BlockRed R;
+    const uint32_t o = big[blockIdx.x];
+    if (prstat && prstat[o] == kPrDone) return;  // walked by rows (k_pr_*)
+    const ObjDesc od = objs[o];
+    const uint32_t bound = (uint32_t)(soff[o + 1] - soff[o]);
+    uint32_t e0, n;
+    obj_range(od, escan, *total0p, e0, n);
+    const uint32_t cap = min(big_cap[blockIdx.x], kBigMaxM), rows_cap = big_meta[2 * blockIdx.x],
+                   ents = big_meta[2 * blockIdx.x + 1];
+    BigList L;
+    L.carve(pool + big_off[blockIdx.x], cap, rows_cap);
+    const int tid = threadIdx.x;
+    for (uint32_t q = tid; q < 4 * rows_cap; q += kBigThreads) L.ri[q] = q % 4 == 3 ? -1 : 0;  // (rows not walked: m = 0)
+    if (n == 0) {
+        if (tid == 0) { L.hdr[0] = 0; L.hdr[1] = 0; }
+        return;
+    }
+    const ObjEdge *E = work + e0;
+    int32_t mr = INT32_MIN;
+    for (uint32_t i = tid; i < n; i += kBigThreads) mr = max(mr, E[i].YMax);
+    const int32_t MaxY = min(min(blk_max(R, mr), fp.H), fp.row1);
+    const int32_t FirstRow = E[0].YMin;
+    const int32_t RowLo = fp.draws[od.draw].mode != MODE_AVX ? fp.row0 - 1 : fp.row0;
+    const bool fits = (int64_t)MaxY - FirstRow <= (int64_t)rows_cap && (int64_t)MaxY - FirstRow < 16000;
+    if (tid == 0) {
+        L.hdr[0] = FirstRow;
+        L.hdr[1] = fits ? max(0, MaxY - FirstRow) : 0;
+        if (!fits) atomicOr(err, 1u);  // (never: k_obj_maxact sized it)
+    }
+    if (!fits) return;
+    int m = 0;
+    uint32_t ins = 0, emitted = 0, off = 0;
+    bool bad = false, samples = false;
+    uint32_t pf = UINT32_MAX;  // the window of sorted edges at pf, loaded a row ahead
+    int32_t y = INT32_MAX, l = 0, ym = 0;
+    float x = 0.0f, g = 0.0f;
+    auto fetch = [&](uint32_t at) {
+        const uint32_t i = at + (uint32_t)tid;
+        y = INT32_MAX; x = g = 0.0f; l = ym = 0;
+        if (i < n) {
+            const ObjEdge &C = E[i];
+            y = C.YMin; x = C.X; g = C.G; l = C.Left; ym = C.YMax;
+        }
+        pf = at;
+    };
+    for (int32_t Row = FirstRow; Row < MaxY; ++Row) {
+        const int32_t rrel = Row - FirstRow;
+        bool expired = false;
+        for (;;) {  // the row's new edges, a window of kBigThreads at a time (3654-3713)
+            if (pf != ins) fetch(ins);
+            int32_t lt, kb, nanc;
+            blk_sum3(R, y < Row ? 1 : 0, y == Row ? 1 : 0, (y == Row && (x != x || g != g)) ? 1 : 0, lt, kb, nanc);
+            if (lt) {  // (never past the first row of a sorted list)
+                ins += (uint32_t)lt;
+                continue;
+            }
+            if (kb == 0) break;
+            if (m + kb > kLdsCap || (uint32_t)(m + kb) > cap) {  // (never: cap >= the most listed entries)
+                bad = true;
+                break;
+            }
+            if (tid < kb) {
+                W.nx[tid] = x; W.ng[tid] = g; W.ne[tid] = (int32_t)(ins + tid);
+                W.ny[tid] = lds_ypack(ym, l, FirstRow, MaxY);
+            }
+            __syncthreads();
+            const bool last = kb < kBigThreads;
+            if (nanc) {  // one edge at a time (no total order on a batch with a NaN key)
+                for (int t = 0; t < kb; ++t) {
+                    m = lds_insert(W, R, m, t, 1, last && t + 1 == kb, rrel, samples);
+                    samples = false;
+                }
+            } else {
+                m = lds_insert(W, R, m, 0, kb, last, rrel, samples);
+                samples = false;
+            }
+            expired = last;
+            ins += (uint32_t)kb;
+            if (last) break;
+        }
+        if (bad) break;
+        if (pf != ins && ins < n) fetch(ins);  // (the next row's window, in flight through this row's pairing)
+        if (!expired && m > 0) {  // expiry 3715-3749 alone
+            m = lds_insert(W, R, m, 0, 0, true, rrel, false);
+            samples = false;
+        }
+        if (m == 0) {  // nothing happens on the rows before the next insertion: go there
+            if (ins >= n) break;
+            Row = max(Row, E[ins].YMin - 1);
+            continue;
+        }
+        const bool emit = Row >= RowLo;
+        const uint32_t P = (uint32_t)(m >> 1);
+        if ((emit && emitted + P > bound) || (uint64_t)off + (uint32_t)m > ents) {  // (never: sized by the bounds)
+            bad = true;
+            break;
+        }
+        lds_pair(W, L, m, rrel, emit, emitted, off);
+        samples = true;
+        off += (uint32_t)m;
+        if (emit) emitted += P;
+    }
+    if (bad && tid == 0) atomicOr(err, 1u);
+}
+
 // Every pair of every row of the huge objects, a thread each (grid: (rows,
 // objects), a workgroup per row): both edges' states at the row -- the edge
 // from FillEdgeTable stepped on each row it was listed on before this one,
@@ -3723,14 +4125,15 @@ hipError_t prk_obj_walk_group(const prk::FrameParams *fp, int32_t mode, uint32_t
     }
     return hipGetLastError();
 }
-// The huge-object walk (k_obj_walk_big) of the objects big[0, nbig) of mode
-// `mode`: their pool slices at big_off (prk_big_slice_ints(big_cap, rows,
+// The huge-object walk (lds: k_obj_walk_lds, else k_obj_walk_big) of the
+// objects big[0, nbig) of mode `mode`: their pool slices at big_off (prk_big_slice_ints(big_cap, rows,
 // ents) ints each; big_meta: (rows, ents) per object, k_obj_maxact's), then
 // every pair set up from a replay of its edges (k_big_replay, grid (max_rows,
 // nbig)) into PairRaw slots soff[o] + j (k_span_finish sets the spans up).
 uint32_t prk_big_max_entries(void) { return prk::kBigMaxM; }
 uint64_t prk_big_slice_ints(uint32_t cap, uint32_t rows, uint32_t ents) { return prk::big_slice_ints(cap, rows, ents); }
-hipError_t prk_big_walk(const prk::FrameParams *fp, int32_t mode, const void *objs, const uint32_t *big,
+uint32_t prk_big_lds_cap(void) { return (uint32_t)prk::kLdsCap; }
+hipError_t prk_big_walk(const prk::FrameParams *fp, int32_t mode, int lds, const void *objs, const uint32_t *big,
                         const unsigned long long *big_off, const uint32_t *big_cap, const uint32_t *big_meta,
                         uint32_t nbig, uint32_t max_rows, int32_t *pool, const uint32_t *escan,
                         const uint32_t *total0p, const void *work, const unsigned long long *soff, void *raw,
@@ -3739,8 +4142,12 @@ hipError_t prk_big_walk(const prk::FrameParams *fp, int32_t mode, const void *ob
     if (nbig > 65535) return hipErrorInvalidValue;
     const prk::ObjDesc *O = reinterpret_cast<const prk::ObjDesc *>(objs);
     const prk::ObjEdge *W = reinterpret_cast<const prk::ObjEdge *>(work);
-    hipLaunchKernelGGL(prk::k_obj_walk_big, dim3(nbig), dim3(prk::kBigThreads), 0, s, *fp, O, big, big_off, big_cap,
-                       big_meta, pool, escan, total0p, W, soff, err, prstat);
+    if (lds)
+        hipLaunchKernelGGL(prk::k_obj_walk_lds, dim3(nbig), dim3(prk::kBigThreads), 0, s, *fp, O, big, big_off,
+                           big_cap, big_meta, pool, escan, total0p, W, soff, err, prstat);
+    else
+        hipLaunchKernelGGL(prk::k_obj_walk_big, dim3(nbig), dim3(prk::kBigThreads), 0, s, *fp, O, big, big_off,
+                           big_cap, big_meta, pool, escan, total0p, W, soff, err, prstat);
     if (max_rows == 0) return hipGetLastError();
     const dim3 g(max_rows, nbig), b(256);
     prk::PairRaw *R = reinterpret_cast<prk::PairRaw *>(raw);

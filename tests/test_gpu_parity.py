@@ -934,11 +934,13 @@ def test_whole_object_long_active_lists(gpu, sem):
              label="long lists sem=%d" % sem)
 
 
+@pytest.mark.parametrize("lds", ["1", "0"])
 @pytest.mark.parametrize("sem", [abi.PRK_SEM_AVX, abi.PRK_SEM_AVX_ST, abi.PRK_SEM_SCALAR])
-def test_whole_object_big_walk(gpu, sem, monkeypatch):
-    """The huge-object walk (prk_spans.hip k_obj_walk_big: one workgroup over
-    a list in device memory, the spans set up afterwards from a replay of
-    every edge) forced onto objects that would fit LDS (PRK_OBJ_BIG_MIN=0,
+def test_whole_object_big_walk(gpu, sem, lds, monkeypatch):
+    """The huge-object walk (prk_spans.hip k_obj_walk_lds / k_obj_walk_big:
+    one workgroup over a list in LDS or in device memory, the spans set up
+    afterwards from a replay of every pair) forced onto objects that would
+    fit the LDS slot classes (PRK_OBJ_BIG_MIN=0,
     PRK_OBJ_ROWS=0), and their sizes by the many-workgroup histogram
     (PRK_OBJ_HUGE_EDGES): ConstructSphere as one object, overlapping 700- and
     64-triangle objects with ties and clipping on every side (odd rows: an
@@ -947,6 +949,7 @@ def test_whole_object_big_walk(gpu, sem, monkeypatch):
     monkeypatch.setenv("PRK_OBJ_BIG_MIN", "0")
     monkeypatch.setenv("PRK_OBJ_ROWS", "0")
     monkeypatch.setenv("PRK_OBJ_HUGE_EDGES", "1000")  # the many-workgroup sizing (k_maxact_huge_*) too
+    monkeypatch.setenv("PRK_OBJ_LDSWALK", lds)  # the list in LDS (k_obj_walk_lds) or device memory
     sph = _sphere_scene()
     soup = scenes.with_ties(scenes.random_soup(2800, 384, 256, radius=40, seed=23, centroid_margin=40), seed=23)
     if sem == abi.PRK_SEM_SCALAR:
@@ -988,17 +991,18 @@ def _degenerate_soup(seed):
     return s
 
 
-@pytest.mark.parametrize("path", ["default", "big", "wave"])
+@pytest.mark.parametrize("path", ["default", "big", "bigmem", "wave"])
 @pytest.mark.parametrize("tpo", [1, 8, 64, 500])
 def test_degenerate_geometry_every_walk(gpu, path, tpo, monkeypatch):
     """Hostile vertices (camera plane, behind the camera, NaN / inf, zero-area
     and collinear triangles) per triangle and in objects of 8 / 64 / 500
     triangles, through the default walks, the huge-object walk (forced) and
     the one-wave walk (forced): the oracle's image, bit for bit."""
-    if path == "big":
+    if path in ("big", "bigmem"):
         monkeypatch.setenv("PRK_OBJ_BIG_MIN", "0")
         monkeypatch.setenv("PRK_OBJ_ROWS", "0")
         monkeypatch.setenv("PRK_OBJ_HUGE_EDGES", "100")
+        monkeypatch.setenv("PRK_OBJ_LDSWALK", "1" if path == "big" else "0")
     elif path == "wave":
         monkeypatch.setenv("PRK_OBJ_BIG_MIN", "0")
         monkeypatch.setenv("PRK_OBJ_ROWS", "0")
