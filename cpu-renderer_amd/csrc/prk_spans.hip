@@ -1588,28 +1588,43 @@ struct BlockRed {
     int32_t a[16], b[16], c[16];
     float x[16], g[16];
 };
+// A workgroup barrier; LO: ordering LDS only (no wait for the workgroup's
+// outstanding device-memory accesses -- for walks whose threads share only
+// LDS, with device-memory stores that nobody in the workgroup reads back).
+template <bool LO = false>
+__device__ __forceinline__ void blk_sync() {
+    if (LO) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    } else {
+        __syncthreads();
+    }
+}
+template <bool LO = false>
 __device__ __forceinline__ int32_t blk_excl_sum(BlockRed &R, int32_t v, int32_t &tot) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int32_t inc = wave_incl_sum_i32(v);
     if (lane == 63) R.a[w] = inc;
-    __syncthreads();
+    blk_sync<LO>();
     int32_t before = 0, t = 0;
     for (int i = 0; i < nw; ++i) {
         const int32_t x = R.a[i];
         before += i < w ? x : 0;
         t += x;
     }
-    __syncthreads();
+    blk_sync<LO>();
     tot = t;
     return before + inc - v;
 }
 // Two exclusive scans at once (one barrier pair).
+template <bool LO = false>
 __device__ __forceinline__ void blk_excl_sum2(BlockRed &R, int32_t v1, int32_t v2, int32_t &e1, int32_t &e2,
                                               int32_t &t1, int32_t &t2) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int32_t i1 = wave_incl_sum_i32(v1), i2 = wave_incl_sum_i32(v2);
     if (lane == 63) { R.a[w] = i1; R.b[w] = i2; }
-    __syncthreads();
+    blk_sync<LO>();
     int32_t b1 = 0, b2 = 0, s1 = 0, s2 = 0;
     for (int i = 0; i < nw; ++i) {
         const int32_t x = R.a[i], y = R.b[i];
@@ -1618,32 +1633,34 @@ __device__ __forceinline__ void blk_excl_sum2(BlockRed &R, int32_t v1, int32_t v
         s1 += x;
         s2 += y;
     }
-    __syncthreads();
+    blk_sync<LO>();
     e1 = b1 + i1 - v1;
     e2 = b2 + i2 - v2;
     t1 = s1;
     t2 = s2;
 }
 // Three sums.
+template <bool LO = false>
 __device__ __forceinline__ void blk_sum3(BlockRed &R, int32_t v1, int32_t v2, int32_t v3, int32_t &t1, int32_t &t2,
                                          int32_t &t3) {
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int32_t s1 = readlane_i(wave_incl_sum_i32(v1), 63), s2 = readlane_i(wave_incl_sum_i32(v2), 63),
                   s3 = readlane_i(wave_incl_sum_i32(v3), 63);
     if ((threadIdx.x & 63) == 0) { R.a[w] = s1; R.b[w] = s2; R.c[w] = s3; }
-    __syncthreads();
+    blk_sync<LO>();
     t1 = t2 = t3 = 0;
     for (int i = 0; i < nw; ++i) { t1 += R.a[i]; t2 += R.b[i]; t3 += R.c[i]; }
-    __syncthreads();
+    blk_sync<LO>();
 }
+template <bool LO = false>
 __device__ __forceinline__ int32_t blk_max(BlockRed &R, int32_t v) {
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int32_t m = wave_max_i32(v);
     if ((threadIdx.x & 63) == 0) R.a[w] = m;
-    __syncthreads();
+    blk_sync<LO>();
     int32_t r = INT32_MIN;
     for (int i = 0; i < nw; ++i) r = max(r, R.a[i]);
-    __syncthreads();
+    blk_sync<LO>();
     return r;
 }
 // The first thread with b (INT32_MAX: none).
@@ -1658,19 +1675,20 @@ __device__ __forceinline__ int32_t blk_first(BlockRed &R, bool b) {
     return r;
 }
 // Inclusive prefix maximum of the threads' keys.
+template <bool LO = false>
 __device__ __forceinline__ void blk_key_prefix_max(BlockRed &R, LKey &k) {
     const int w = threadIdx.x >> 6;
     int32_t p = 0;
     wave_key_prefix_max(k, p);
     if ((threadIdx.x & 63) == 63) { R.x[w] = k.x; R.g[w] = k.g; R.a[w] = k.l; }
-    __syncthreads();
+    blk_sync<LO>();
     LKey c{-INFINITY, -INFINITY, INT32_MIN};
     for (int i = 0; i < w; ++i) {
         const LKey o{R.x[i], R.g[i], R.a[i]};
         if (key_gt(o, c)) c = o;
     }
     if (key_gt(c, k)) k = c;
-    __syncthreads();
+    blk_sync<LO>();
 }
 
 // One new edge (key c, slot sl) before the first entry it sorts before
@@ -2830,7 +2848,7 @@ constexpr int kLdsPer = (kLdsCap + kBigThreads - 1) / kBigThreads;  // old entri
 constexpr int kLdsSamp = 576;                      // per-16 maxima (>= kLdsCap / 16)
 constexpr int kLdsPairs = (kLdsCap / 2 + kBigThreads - 1) / kBigThreads;  // pairs a thread owns (5)
 static_assert(kLdsCap <= kLdsSamp * 16 && kLdsPer * kBigThreads >= kLdsCap, "LDS walk sizes");
-struct LdsWalk {
+struct alignas(16) LdsWalk {  // (aligned: the pairing reads a pair's fields as one 8-B access)
     float x[kLdsCap], g[kLdsCap];
     int32_t e[kLdsCap];
     uint16_t y[kLdsCap];                 // (min(YMax, MaxY) - FirstRow) << 1 | Left
@@ -2868,7 +2886,8 @@ __device__ __forceinline__ uint16_t lds_ypack(int32_t ymax, int32_t left, int32_
 // row <= rrel); returns the new length.  samples_ok: W.s* hold the list's
 // per-16 key maxima (the pairing left them).
 __device__ __forceinline__ int lds_insert(LdsWalk &W, BlockRed &R, int m, int c0, int kb, bool expire,
-                                          int32_t rrel, bool samples_ok) {
+                                          int32_t rrel, bool samples_ok, unsigned long long *wp = nullptr) {
+    unsigned long long tw0 = PRK_WT();
     const int tid = threadIdx.x;
     const bool mine = tid < kb;
     int32_t gapc = 0;
@@ -2885,12 +2904,13 @@ __device__ __forceinline__ int lds_insert(LdsWalk &W, BlockRed &R, int m, int c0
                     }
                     W.sx[j] = mx.x; W.sg[j] = mx.g; W.sl[j] = mx.l;
                 }
-                __syncthreads();
+                blk_sync<true>();
             }
             LKey pk = tid < ns ? LKey{W.sx[tid], W.sg[tid], W.sl[tid]} : LKey{-INFINITY, -INFINITY, INT32_MIN};
-            blk_key_prefix_max(R, pk);
+            blk_key_prefix_max<true>(R, pk);
             if (tid < ns) { W.sx[tid] = pk.x; W.sg[tid] = pk.g; W.sl[tid] = pk.l; }
-            __syncthreads();
+            blk_sync<true>();
+            PRK_BIG_T(9, tw0);
             if (mine) {  // the first entry whose key exceeds the new edge's (3663-3667)
                 const LKey kc{W.nx[c0 + tid], W.ng[c0 + tid], (int32_t)(W.ny[c0 + tid] & 1)};
                 int lo = 0, hi = ns;
@@ -2906,7 +2926,8 @@ __device__ __forceinline__ int lds_insert(LdsWalk &W, BlockRed &R, int m, int c0
                         if (key_gt(lds_key(W, q0 + u), kc)) { gapc = q0 + u; break; }
                 }
             }
-            __syncthreads();  // (the sample arrays hold the bins below)
+            blk_sync<true>();  // (the sample arrays hold the bins below)
+            PRK_BIG_T(10, tw0);
         }
         if (mine) {
             keptc = !expire || (int32_t)(W.ny[c0 + tid] >> 1) > rrel;
@@ -2921,18 +2942,18 @@ __device__ __forceinline__ int lds_insert(LdsWalk &W, BlockRed &R, int m, int c0
         uint16_t *bmem = reinterpret_cast<uint16_t *>(W.sl);
         const int nb = (m >> 4) + 1;  // (<= 576)
         if (tid < nb) bcnt[tid] = 0;
-        __syncthreads();
+        blk_sync<true>();
         const int bin = gapc >> 4;
         if (mine && keptc) atomicAdd(&bcnt[bin], 1);
-        __syncthreads();
+        blk_sync<true>();
         const int32_t cv = tid < nb ? bcnt[tid] : 0;
         int32_t tot;
-        const int32_t ex = blk_excl_sum(R, cv, tot);
+        const int32_t ex = blk_excl_sum<true>(R, cv, tot);
         kn = tot;
         if (tid < nb) { bcnt[tid] = ex; bcur[tid] = ex; }
-        __syncthreads();
+        blk_sync<true>();
         if (mine && keptc) bmem[atomicAdd(&bcur[bin], 1)] = (uint16_t)tid;
-        __syncthreads();
+        blk_sync<true>();
         if (mine && keptc) {
             const LKey kc{W.nx[c0 + tid], W.ng[c0 + tid], (int32_t)(W.ny[c0 + tid] & 1)};
             const int32_t b0 = bcnt[bin], b1 = bin + 1 < nb ? bcnt[bin + 1] : kn;
@@ -2947,6 +2968,7 @@ __device__ __forceinline__ int lds_insert(LdsWalk &W, BlockRed &R, int m, int c0
             srank = b0 + r;
             W.sgap[srank] = (uint16_t)gapc;
         }
+        PRK_BIG_T(11, tw0);
     }
     // the old entries (thread t: [9t, 9t + 9)), their kept counts
     const int q0 = kLdsPer * tid;
@@ -2969,9 +2991,10 @@ __device__ __forceinline__ int lds_insert(LdsWalk &W, BlockRed &R, int m, int c0
         }
     }
     int32_t kept_old;
-    const int32_t kbt = blk_excl_sum(R, kc_t, kept_old);  // (its barriers also publish sgap)
+    const int32_t kbt = blk_excl_sum<true>(R, kc_t, kept_old);  // (its barriers also publish sgap)
     W.kbase[tid] = (uint16_t)kbt;
-    __syncthreads();
+    blk_sync<true>();
+    PRK_BIG_T(12, tw0);
     // places: a kept old entry q at #kept before q + #kept new of gap <= q
     int32_t opos[kLdsPer];
     {
@@ -3002,7 +3025,8 @@ __device__ __forceinline__ int lds_insert(LdsWalk &W, BlockRed &R, int m, int c0
         }
         npos = before + srank;
     }
-    __syncthreads();  // (every read of the old list is done)
+    blk_sync<true>();  // (every read of the old list is done)
+    PRK_BIG_T(13, tw0);
 #pragma unroll
     for (int u = 0; u < kLdsPer; ++u)
         if ((keep >> u) & 1u) {
@@ -3012,7 +3036,8 @@ __device__ __forceinline__ int lds_insert(LdsWalk &W, BlockRed &R, int m, int c0
     if (kb > 0 && mine && keptc) {
         W.x[npos] = W.nx[c0 + tid]; W.g[npos] = W.ng[c0 + tid]; W.e[npos] = W.ne[c0 + tid]; W.y[npos] = W.ny[c0 + tid];
     }
-    __syncthreads();
+    blk_sync<true>();
+    PRK_BIG_T(14, tw0);
     return kept_old + kn;
 }
 
@@ -3020,7 +3045,8 @@ __device__ __forceinline__ int lds_insert(LdsWalk &W, BlockRed &R, int m, int c0
 // (ri, ids), every pair stepped and swapped, the next row's per-16 key maxima
 // in W.s*.
 __device__ __forceinline__ void lds_pair(LdsWalk &W, const BigList &L, int m, int32_t r, bool emit, uint32_t j0,
-                                         uint32_t off) {
+                                         uint32_t off, unsigned long long *wp = nullptr) {
+    unsigned long long tw0 = PRK_WT();
     const int tid = threadIdx.x, lane = tid & 63;
     const int P = m >> 1, items = P + (m & 1);
     int32_t *ids = L.ids + off;
@@ -3047,10 +3073,14 @@ __device__ __forceinline__ void lds_pair(LdsWalk &W, const BigList &L, int m, in
             // pairs k - 1, k, k + 1 stepped and first-swapped
             LdsE a[3], b[3];
 #pragma unroll
-            for (int h = 0; h < 3; ++h) {
+            for (int h = 0; h < 3; ++h) {  // (a pair's entries as one 8-B read a field, y as one 4-B read)
                 const int ea = 2 * min(max(k - 1 + h, 0), P - 1);
-                a[h] = lds_entry(W, ea);
-                b[h] = lds_entry(W, ea + 1);
+                const float2 px = *reinterpret_cast<const float2 *>(W.x + ea);
+                const float2 pg = *reinterpret_cast<const float2 *>(W.g + ea);
+                const int2 pe = *reinterpret_cast<const int2 *>(W.e + ea);
+                const uint32_t py = *reinterpret_cast<const uint32_t *>(W.y + ea);
+                a[h] = LdsE{px.x, pg.x, (int32_t)(py & 0xFFFFu), pe.x};
+                b[h] = LdsE{px.y, pg.y, (int32_t)(py >> 16), pe.y};
                 lds_first_swap(a[h], b[h]);
             }
             const bool lo = k >= 1 && b[0].x > a[1].x;      // boundary k (3843-3853)
@@ -3059,7 +3089,8 @@ __device__ __forceinline__ void lds_pair(LdsWalk &W, const BigList &L, int m, in
             o1[i] = hi ? a[2] : b[1];
         }
     }
-    __syncthreads();  // (every read of the list is done)
+    blk_sync<true>();  // (every read of the list is done)
+    PRK_BIG_T(15, tw0);
 #pragma unroll
     for (int i = 0; i < kLdsPairs; ++i) {
         if (i * kBigThreads >= items) break;  // (uniform)
@@ -3067,8 +3098,10 @@ __device__ __forceinline__ void lds_pair(LdsWalk &W, const BigList &L, int m, in
         const int e = 2 * k;
         LKey ka{-INFINITY, -INFINITY, INT32_MIN}, kb2{-INFINITY, -INFINITY, INT32_MIN};
         if (k < P) {
-            W.x[e] = o0[i].x; W.g[e] = o0[i].g; W.y[e] = (uint16_t)o0[i].yp; W.e[e] = o0[i].e;
-            W.x[e + 1] = o1[i].x; W.g[e + 1] = o1[i].g; W.y[e + 1] = (uint16_t)o1[i].yp; W.e[e + 1] = o1[i].e;
+            *reinterpret_cast<float2 *>(W.x + e) = make_float2(o0[i].x, o1[i].x);
+            *reinterpret_cast<float2 *>(W.g + e) = make_float2(o0[i].g, o1[i].g);
+            *reinterpret_cast<int2 *>(W.e + e) = make_int2(o0[i].e, o1[i].e);
+            *reinterpret_cast<uint32_t *>(W.y + e) = (uint32_t)(o0[i].yp & 0xFFFF) | ((uint32_t)o1[i].yp << 16);
             ka = entry_key(o0[i].x, o0[i].g, o0[i].yp & 1);
             kb2 = entry_key(o1[i].x, o1[i].g, o1[i].yp & 1);
         } else if (k == P) {
@@ -3083,7 +3116,7 @@ __device__ __forceinline__ void lds_pair(LdsWalk &W, const BigList &L, int m, in
             W.sx[k >> 3] = kk.x; W.sg[k >> 3] = kk.g; W.sl[k >> 3] = kk.l;
         }
     }
-    __syncthreads();
+    blk_sync<true>();
 }
 
 // One workgroup per huge object whose most active edges fit kLdsCap (the
@@ -3134,6 +3167,8 @@ __global__ void __launch_bounds__(kBigThreads) k_obj_walk_lds(FrameParams fp, co
     int m = 0;
     uint32_t ins = 0, emitted = 0, off = 0;
     bool bad = false, samples = false;
+    unsigned long long wpa[16] = {}, *wp = PRK_WPROF && tid == 0 ? wpa : nullptr;
+    unsigned long long tw0 = PRK_WT(), twall = tw0;
     uint32_t pf = UINT32_MAX;  // the window of sorted edges at pf, loaded a row ahead
     int32_t y = INT32_MAX, l = 0, ym = 0;
     float x = 0.0f, g = 0.0f;
@@ -3149,10 +3184,11 @@ __global__ void __launch_bounds__(kBigThreads) k_obj_walk_lds(FrameParams fp, co
     for (int32_t Row = FirstRow; Row < MaxY; ++Row) {
         const int32_t rrel = Row - FirstRow;
         bool expired = false;
+        if (PRK_WPROF && wp) wp[3] += 1;
         for (;;) {  // the row's new edges, a window of kBigThreads at a time (3654-3713)
             if (pf != ins) fetch(ins);
             int32_t lt, kb, nanc;
-            blk_sum3(R, y < Row ? 1 : 0, y == Row ? 1 : 0, (y == Row && (x != x || g != g)) ? 1 : 0, lt, kb, nanc);
+            blk_sum3<true>(R, y < Row ? 1 : 0, y == Row ? 1 : 0, (y == Row && (x != x || g != g)) ? 1 : 0, lt, kb, nanc);
             if (lt) {  // (never past the first row of a sorted list)
                 ins += (uint32_t)lt;
                 continue;
@@ -3166,17 +3202,20 @@ __global__ void __launch_bounds__(kBigThreads) k_obj_walk_lds(FrameParams fp, co
                 W.nx[tid] = x; W.ng[tid] = g; W.ne[tid] = (int32_t)(ins + tid);
                 W.ny[tid] = lds_ypack(ym, l, FirstRow, MaxY);
             }
-            __syncthreads();
+            blk_sync<true>();
+            PRK_BIG_T(0, tw0);
+            if (PRK_WPROF && wp) { wp[4] += 1; wp[8] += (unsigned)kb; }
             const bool last = kb < kBigThreads;
             if (nanc) {  // one edge at a time (no total order on a batch with a NaN key)
                 for (int t = 0; t < kb; ++t) {
-                    m = lds_insert(W, R, m, t, 1, last && t + 1 == kb, rrel, samples);
+                    m = lds_insert(W, R, m, t, 1, last && t + 1 == kb, rrel, samples, wp);
                     samples = false;
                 }
             } else {
-                m = lds_insert(W, R, m, 0, kb, last, rrel, samples);
+                m = lds_insert(W, R, m, 0, kb, last, rrel, samples, wp);
                 samples = false;
             }
+            PRK_BIG_T(1, tw0);
             expired = last;
             ins += (uint32_t)kb;
             if (last) break;
@@ -3184,9 +3223,10 @@ __global__ void __launch_bounds__(kBigThreads) k_obj_walk_lds(FrameParams fp, co
         if (bad) break;
         if (pf != ins && ins < n) fetch(ins);  // (the next row's window, in flight through this row's pairing)
         if (!expired && m > 0) {  // expiry 3715-3749 alone
-            m = lds_insert(W, R, m, 0, 0, true, rrel, false);
+            m = lds_insert(W, R, m, 0, 0, true, rrel, false, wp);
             samples = false;
         }
+        PRK_BIG_T(2, tw0);
         if (m == 0) {  // nothing happens on the rows before the next insertion: go there
             if (ins >= n) break;
             Row = max(Row, E[ins].YMin - 1);
@@ -3198,12 +3238,18 @@ __global__ void __launch_bounds__(kBigThreads) k_obj_walk_lds(FrameParams fp, co
             bad = true;
             break;
         }
-        lds_pair(W, L, m, rrel, emit, emitted, off);
+        lds_pair(W, L, m, rrel, emit, emitted, off, wp);
         samples = true;
         off += (uint32_t)m;
         if (emit) emitted += P;
+        PRK_BIG_T(5, tw0);
+        if (PRK_WPROF && wp) wp[6] += (unsigned)m;
     }
     if (bad && tid == 0) atomicOr(err, 1u);
+    if (PRK_WPROF && wp) {
+        wp[7] += PRK_WT() - twall;
+        for (int k = 0; k < 16; ++k) atomicAdd(fp.prof + k, wp[k]);
+    }
 }
 
 // Every pair of every row of the huge objects, a thread each (grid: (rows,

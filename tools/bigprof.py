@@ -13,7 +13,9 @@ import time_objects as T  # noqa: E402
 
 want = sys.argv[1] if len(sys.argv) > 1 else "c3b_1obj_avx"
 NAMES = {0: "window", 1: "insert+expire", 2: "expiry alone", 5: "pairing", 9: "samples", 10: "sample scan",
-         11: "gap search", 12: "rank", 13: "scan+move", 14: "new edges placed"}
+         11: "gap search", 12: "rank", 13: "scan+move", 14: "new edges placed", 15: "pairing reads (LDS walk)"}
+# (k_obj_walk_lds's counters: 9 samples + their scan, 10 gap search, 11 bins + ranks, 12 old entries +
+#  kept scan, 13 places, 14 moves, 15 pairing's read pass -- the labels above are k_obj_walk_big's)
 for name, s, sem, phong, tpo in T.cases():
     if name != want:
         continue
