@@ -31,6 +31,7 @@
 extern "C" {
 hipError_t prk_launch_tri_draw(const prk::DrawRec *, uint32_t, uint32_t *, uint32_t, hipStream_t);
 hipError_t prk_bin_count(const prk::FrameParams *, uint32_t *, void *, uint32_t *, uint32_t *, uint8_t *, hipStream_t);
+hipError_t prk_band_records(const prk::FrameParams *, const uint32_t *, const uint32_t *, hipStream_t);
 uint32_t prk_cs_chunks(uint32_t);
 uint32_t prk_cs_nchunks(uint32_t, uint32_t);
 uint32_t prk_cs_band_runs_per_chunk(const prk::FrameParams *);
@@ -223,6 +224,7 @@ struct prk_context {
             d_ghist, d_tile_tot, d_chunk, d_info, d_runlist, d_run_n;
         uint32_t *h_info = nullptr;       // pinned: [entry count, overflow] of the set's last binning
         hipEvent_t counted_ev = nullptr;  // h_info of this set's binning has landed
+        hipEvent_t listed_ev = nullptr;   // a band frame's run lists are written (k_band_rec may start)
         // bytes last uploaded into d_draws / d_texs and the buffer they went
         // to: an unchanged table (every frame of a static scene) is not sent again
         std::vector<uint8_t> h_draws, h_texs;
@@ -445,6 +447,7 @@ int prk_create(int device, prk_context **out) {
         e = hipEventCreateWithFlags(&c->bset[i].free_ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->bset[i].binned_ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->bset[i].counted_ev, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->bset[i].listed_ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipHostMalloc((void **)&c->bset[i].h_info, 2 * sizeof(uint32_t), hipHostMallocDefault);
     }
     for (int i = 0; i < prk_context::kRing && e == hipSuccess; ++i)
@@ -492,6 +495,7 @@ int prk_destroy(prk_context *c) {
         if (B.free_ev) (void)hipEventDestroy(B.free_ev);
         if (B.binned_ev) (void)hipEventDestroy(B.binned_ev);
         if (B.counted_ev) (void)hipEventDestroy(B.counted_ev);
+        if (B.listed_ev) (void)hipEventDestroy(B.listed_ev);
         if (B.h_info) (void)hipHostFree(B.h_info);
     }
     DevBuf *bufs[] = {&c->d_winners, &c->d_anomaly, &c->d_prof, &c->d_negz};
@@ -1496,6 +1500,13 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
         PRK_TRY(hipEventRecord(c->ev[slot][0], bs));
         uint32_t *runlist = per ? (uint32_t *)B.d_runlist.p : nullptr, *run_n = per ? (uint32_t *)B.d_run_n.p : nullptr;
         PRK_TRY(prk_bin_count(&fp, (uint32_t *)B.d_tri_n.p, B.d_ranges.p, runlist, run_n, trwon, bs));
+        if (runlist && fp.trec) {
+            // a row band's setup records (k_band_rec) on the vis stream, beside
+            // the counting sort below; this frame's k_vis follows them there
+            PRK_TRY(hipEventRecord(B.listed_ev, bs));
+            PRK_TRY(hipStreamWaitEvent(c->vis_stream, B.listed_ev, 0));
+            PRK_TRY(prk_band_records(&fp, runlist, run_n, c->vis_stream));
+        }
         uint32_t *chunk = (uint32_t *)B.d_chunk.p;
         PRK_TRY(prk_bin_cs(&fp, B.d_ranges.p, (const uint32_t *)B.d_tri_n.p, (uint32_t *)B.d_ghist.p,
                            (uint32_t *)B.d_tile_tot.p, chunk, chunk + nch, (uint32_t *)B.d_offs.p, cap,

@@ -77,10 +77,10 @@ __device__ __forceinline__ bool tri_tile_range_proj(const FrameParams &fp, const
     tr.pad1 = (uint16_t)min(r1 - fp.row0, 65535);
     const bool rect = r0 < r1 && c0 < c1;
     if (rect) {
-        tr.tx0 = (uint16_t)(c0 / fp.tile_w);
-        tr.tx1 = (uint16_t)((c1 - 1) / fp.tile_w);
-        tr.ty0 = (uint16_t)((r0 - fp.row0) / fp.tile_h);
-        tr.ty1 = (uint16_t)((r1 - 1 - fp.row0) / fp.tile_h);
+        tr.tx0 = (uint16_t)(c0 >> fp.tile_w_log2);
+        tr.tx1 = (uint16_t)((c1 - 1) >> fp.tile_w_log2);
+        tr.ty0 = (uint16_t)tile_row_of(fp, r0 - fp.row0);
+        tr.ty1 = (uint16_t)tile_row_of(fp, r1 - 1 - fp.row0);
     } else {
         tr.tx0 = 1; tr.tx1 = 0; tr.ty0 = 1; tr.ty1 = 0;
     }
@@ -91,11 +91,36 @@ __device__ __forceinline__ bool tri_tile_range_proj(const FrameParams &fp, const
         const int32_t o0 = g0 < (float)fp.row0 ? fp.row0 : (g0 >= lim ? (int32_t)lim : (int32_t)g0);
         const int32_t o1 = g1 > lim ? (int32_t)lim : (g1 <= (float)fp.row0 ? fp.row0 : (int32_t)g1);
         if (o0 < o1) {
-            tr.oty0 = (uint16_t)((o0 - fp.row0) / fp.tile_h);
-            tr.oty1 = (uint16_t)((o1 - 1 - fp.row0) / fp.tile_h);
+            tr.oty0 = (uint16_t)tile_row_of(fp, o0 - fp.row0);
+            tr.oty1 = (uint16_t)tile_row_of(fp, o1 - 1 - fp.row0);
         }
     }
     return rect || tr.oty0 <= tr.oty1;
+}
+
+// Quick band test of k_bin_band: true only when the exact test above rejects
+// the triangle at its first line (no row of the band): every vertex's
+// projected y, here with the hardware reciprocal in place of ProjectVertex's
+// IEEE division (<= 1 ulp, so the two differ by well under 2^-18 of the
+// magnitudes), lies more than that bound plus two rows outside the band on
+// the same side.  A non-finite value fails every comparison: never rejected
+// here.  py, pz: the draw's object position P[1], P[2].
+__device__ __forceinline__ bool band_far(const FrameParams &fp, float py, float pz, const float *v) {
+    bool above = true, below = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float cy = v[3 * k + 1] + py, cz = v[3 * k + 2] + pz;
+        const float dd = fp.D - cz;
+        float y = 0.0f, m = 0.0f;  // (project_vertex's y of a vertex with dd <= 0.2)
+        if (dd > 0.2f) {
+            const float t = fp.M2P * ((__builtin_amdgcn_rcpf(dd) * fp.F) * cy);
+            y = fp.Cy + t;
+            m = (fabsf(t) + fabsf(fp.Cy)) * 0x1p-18f;
+        }
+        above = above && (y + m + 2.0f < (float)fp.row0);
+        below = below && (y - m >= (float)fp.row1 + 1.0f);
+    }
+    return above || below;
 }
 
 // Number of tiles in a range (rectangle + column-0 overflow tiles not in it).
@@ -202,6 +227,12 @@ constexpr uint32_t kRecRun = 2048;
 #ifndef PRK_BIN_BAND
 #define PRK_BIN_BAND 1  // row bands: k_bin_band (one launch) instead of k_bin_count + k_setup_rec
 #endif
+#ifndef PRK_WPROF
+#define PRK_WPROF 0
+#endif
+#ifndef PRK_BAND_REC_KERNEL
+#define PRK_BAND_REC_KERNEL 1  // a row band's setup records in k_band_rec (prk_band_records), not k_bin_band
+#endif
 #ifndef PRK_BAND_COALESCED
 #define PRK_BAND_COALESCED 1  // k_bin_band: a one-draw run's positions as coalesced float4 loads through LDS
 #endif
@@ -247,10 +278,6 @@ struct BandRuns {
     uint32_t nruns;
     uint32_t per;          // runs per counting-sort chunk
 };
-#ifndef PRK_BAND_WAVELIST
-#define PRK_BAND_WAVELIST 1  // k_bin_band: each wave lists its own contiguous triangles (ballots, no
-                             // workgroup barrier per 256 triangles); the lists are joined once
-#endif
 __global__ void __launch_bounds__(kCountThreads) k_bin_band(FrameParams fp, uint32_t *__restrict__ tri_n,
                                                              TileRange *__restrict__ ranges,
                                                              uint32_t *__restrict__ runlist,
@@ -258,122 +285,151 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_band(FrameParams fp, uint
                                                              uint8_t *__restrict__ trwon) {
     __shared__ float4 stage[kCountThreads / 64][64 * 10];
     __shared__ uint32_t list[kRecRun];
-    __shared__ uint32_t scratch[kCountThreads / 64];
     const uint32_t g0 = blockIdx.x * kRecRun;
     uint32_t n = 0;
-    constexpr int kIt = kRecRun / kCountThreads;
     constexpr int kWaves = kCountThreads / 64;
+    // -DPRK_WPROF=1: wave 0's clocks per phase (0 first half in, 1 tested, 2
+    // second half in, 3 tested, 4 lists joined, 5 records) into fp.prof
+    unsigned long long bt[6] = {}, bt0 = PRK_WPROF ? __builtin_amdgcn_s_memtime() : 0ull;
+    const unsigned long long rt0 = PRK_WPROF ? __builtin_amdgcn_s_memrealtime() : 0ull;
+#define PRK_BT(k)                                                   \
+    do {                                                            \
+        if (PRK_WPROF) {                                            \
+            const unsigned long long t1_ = __builtin_amdgcn_s_memtime(); \
+            bt[k] += t1_ - bt0;                                     \
+            bt0 = t1_;                                              \
+        }                                                           \
+    } while (0)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    // Triangle of iteration `it` for this thread: PRK_BAND_WAVELIST, wave w
-    // takes 256 consecutive triangles of each half (64 per iteration), so its
-    // list is in triangle order and the (half, wave) lists joined in that
-    // order are the run's; else thread t takes it * 256 + t.
-    auto tri_of = [&](int it) -> uint32_t {
-        if (PRK_BAND_WAVELIST)
-            return (uint32_t)((it / (kIt / 2)) * (kRecRun / 2) + wv * (kRecRun / 2 / kWaves) +
-                              (it % (kIt / 2)) * 64 + lane);
-        return (uint32_t)(it * kCountThreads + threadIdx.x);
-    };
-    // The run's positions.  One draw whose run is 16-byte aligned in its
-    // geometry (the usual frame): the run's 9 * kRecRun floats are contiguous,
-    // so each half of it comes in as coalesced float4 loads (a wave
-    // instruction reads 1 KiB in a row) into LDS (the record stage's space)
-    // and each thread takes its triangle's nine floats from there.  Otherwise
-    // every thread loads its triangles' nine floats itself, all requested up
-    // front so the loads overlap (a wave instruction then touches 18 cache
-    // lines for 256 bytes).
+    // The run's positions, a half (kHalf triangles) at a time, go through LDS
+    // (the record stage's space), nine floats per triangle.  One draw whose
+    // run is 16-byte aligned in its geometry (the usual frame): the half's
+    // 9 * kHalf floats are contiguous and come in as coalesced float4 loads (a
+    // wave instruction reads 1 KiB in a row).  Otherwise each thread loads
+    // its triangles' nine floats (any draw) and stores them there.
     constexpr int kHalf = kRecRun / 2;                  // triangles per LDS half
+    constexpr int kPerWave = kHalf / kWaves;            // a wave's consecutive triangles per half
     constexpr int kV4 = kHalf * 9 / 4 / kCountThreads;  // float4 per thread per half
     static_assert(kHalf * 9 % (4 * kCountThreads) == 0 && kHalf * 9 * 4 <= (int)sizeof(stage), "LDS half");
-    static_assert(kIt == 8 && kWaves == 4, "the wave-list mapping: two halves of four 64-triangle steps per wave");
+    static_assert(kPerWave == kCountThreads && kPerWave % 64 == 0, "one list entry per thread and (half, wave)");
     const uint32_t gt0 = fp.draw0.geom_tri0 + (g0 - fp.draw0.first_global);
     // (gt0 % 4 == 0 makes the run's offset 16-B aligned; the base must be too:
     // prk_geometry_wrap_device takes any 4-B aligned caller pointer)
     const bool coal = PRK_BAND_COALESCED && fp.ndraws == 1 && (gt0 & 3u) == 0 &&
                       ((uintptr_t)fp.draw0.V & 15u) == 0 &&
                       g0 + (uint32_t)kRecRun <= fp.tri_count;  // (a whole run: no tail to mask)
-    float pv[kIt][9];
-    const DrawRec *pd[kIt];
-    if (!coal) {
-#pragma unroll
-        for (int it = 0; it < kIt; ++it) {
-            const uint32_t g = g0 + tri_of(it);
-            pd[it] = fp.draws;
-            if (g < fp.tri_count) {
-                uint32_t gt;
-                resolve_draw(fp, g, pd[it], gt);
-                const float *v = pd[it]->V + 9 * (size_t)gt;
-#pragma unroll
-                for (int j = 0; j < 9; ++j) pv[it][j] = v[j];
-            }
-        }
-    }
-    // PRK_BAND_WAVELIST: the (half, wave) lists, in list[] at half * kHalf +
-    // wave * (kHalf / kWaves), their lengths in wcnt
+    // Wave w takes kPerWave consecutive triangles of each half: first the
+    // quick band test (band_far) over all of them, the ones it keeps listed
+    // in surv[w] in order; then the full test (tri_tile_range_raw, ~500
+    // instructions) over those 64 at a time, so a narrow band's rank runs it
+    // at full lanes on about its share of the triangles instead of on every
+    // one.  The triangles with entries go to the (half, wave) list, in list[]
+    // at half * kHalf + wave * kPerWave, its length in wcnt: in triangle
+    // order, so the eight lists joined in that order are the run's.
+    __shared__ uint16_t surv[kWaves][kPerWave];
     __shared__ uint32_t wcnt[2][kWaves];
-    uint32_t wn = 0;  // this wave's list length in the current half
-    const float *lf = reinterpret_cast<const float *>(&stage[0][0]);
-#pragma unroll
-    for (int it = 0; it < kIt; ++it) {
-        const uint32_t tl = tri_of(it), g = g0 + tl;
-        if (coal && it % (kIt / 2) == 0) {  // this half's positions into LDS
-            const float4 *src = reinterpret_cast<const float4 *>(fp.draw0.V + 9 * ((size_t)gt0 + it * kCountThreads));
-            if (it) __syncthreads();  // (the previous half's reads)
+    float *lw = reinterpret_cast<float *>(&stage[0][0]);
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t hb = (uint32_t)h * kHalf;  // the half's first triangle in the run
+        if (h) {
+            PRK_BT(1);
+            __syncthreads();  // (the previous half's reads)
+        }
+        if (coal) {
+            const float4 *src = reinterpret_cast<const float4 *>(fp.draw0.V + 9 * ((size_t)gt0 + hb));
             float4 *lv = &stage[0][0];
 #pragma unroll
             for (int kk = 0; kk < kV4; ++kk) lv[kk * kCountThreads + threadIdx.x] = src[kk * kCountThreads + threadIdx.x];
-            __syncthreads();
-        }
-        uint32_t ne = 0;
-        if (g < fp.tri_count) {
-            TileRange tr;
-            bool hit;
-            if (coal) {
-                float v9[9];
-                const int t = (int)(tl % (uint32_t)kHalf);
+        } else {
+            constexpr int kT = kHalf / kCountThreads;
+            float pv[kT][9];
 #pragma unroll
-                for (int j = 0; j < 9; ++j) v9[j] = lf[9 * t + j];
-                hit = tri_tile_range_raw(fp, fp.draws, v9, tr);
-            } else {
-                hit = tri_tile_range_raw(fp, pd[it], pv[it], tr);
+            for (int k = 0; k < kT; ++k) {  // (all requested before any is stored: the loads overlap)
+                const uint32_t g = g0 + hb + k * kCountThreads + threadIdx.x;
+                if (g < fp.tri_count) {
+                    const DrawRec *d;
+                    uint32_t gt;
+                    resolve_draw(fp, g, d, gt);
+                    const float *v = d->V + 9 * (size_t)gt;
+#pragma unroll
+                    for (int j = 0; j < 9; ++j) pv[k][j] = v[j];
+                }
             }
-            if (!hit) {
-                tr.tx0 = 1; tr.tx1 = 0; tr.ty0 = 1; tr.ty1 = 0; tr.oty0 = 1; tr.oty1 = 0;
-            }
-            ne = range_entries(tr);
-            if (ne) {  // (only the listed triangles' are read: the band's sort, k_won_local of winners)
-                ranges[g] = tr;
-                tri_n[g] = ne;
-            }
-            if (trwon) trwon[g] = 0;
-        } else if (g == fp.tri_count) {
-            tri_n[g] = 0;  // sentinel: a scan's last element is the total
+#pragma unroll
+            for (int k = 0; k < kT; ++k)
+#pragma unroll
+                for (int j = 0; j < 9; ++j) lw[9 * (k * kCountThreads + threadIdx.x) + j] = pv[k][j];
         }
-        const uint32_t f = ne != 0 ? 1u : 0u;
-        if (PRK_BAND_WAVELIST) {
-            const unsigned long long bal = __ballot(f != 0);
+        __syncthreads();
+        PRK_BT(h ? 2 : 0);
+        uint32_t ns = 0;  // this wave's kept triangles
+#pragma unroll
+        for (int k = 0; k < kPerWave / 64; ++k) {
+            const uint32_t t = (uint32_t)(wv * kPerWave + k * 64 + lane), g = g0 + hb + t;
+            bool keep = false;
+            if (g < fp.tri_count) {
+                if (trwon) trwon[g] = 0;
+                float py = fp.draw0.P[1], pz = fp.draw0.P[2];
+                if (!coal) {
+                    const DrawRec *d;
+                    uint32_t gt;
+                    resolve_draw(fp, g, d, gt);
+                    py = d->P[1];
+                    pz = d->P[2];
+                }
+                keep = !band_far(fp, py, pz, lw + 9 * t);
+            } else if (g == fp.tri_count) {
+                tri_n[g] = 0;  // sentinel: a scan's last element is the total
+            }
+            const unsigned long long bal = __ballot(keep);
             const uint32_t r = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-            const int h = it / (kIt / 2);
-            if (f) list[h * kHalf + wv * (kHalf / kWaves) + wn + r] = g;
-            wn += (uint32_t)__popcll(bal);
-            if (it % (kIt / 2) == kIt / 2 - 1) {
-                if (lane == 0) wcnt[h][wv] = wn;
-                wn = 0;
-            }
-        } else {
-            uint32_t tot;
-            const uint32_t pos = cs_block_excl_scan(f, scratch, tot);
-            if (f) {
-                list[n + pos] = g;
-                runlist[g0 + n + pos] = g;
-            }
-            n += tot;
+            if (keep) surv[wv][ns + r] = (uint16_t)t;
+            ns += (uint32_t)__popcll(bal);
         }
+        wave_sync();
+        uint32_t wn = 0;  // this wave's list length in this half
+        for (uint32_t b = 0; b < ns; b += 64) {
+            const uint32_t i = b + (uint32_t)lane;
+            uint32_t ne = 0, g = 0;
+            if (i < ns) {
+                const uint32_t t = surv[wv][i];
+                g = g0 + hb + t;
+                const DrawRec *d = fp.draws;
+                if (!coal) {
+                    uint32_t gt;
+                    resolve_draw(fp, g, d, gt);
+                }
+                float v9[9];
+#pragma unroll
+                for (int j = 0; j < 9; ++j) v9[j] = lw[9 * t + j];
+                TileRange tr;
+                if (!tri_tile_range_raw(fp, d, v9, tr)) {
+                    tr.tx0 = 1; tr.tx1 = 0; tr.ty0 = 1; tr.ty1 = 0; tr.oty0 = 1; tr.oty1 = 0;
+                }
+                ne = range_entries(tr);
+                if (ne) {  // (only the listed triangles' are read: the band's sort, k_won_local of winners)
+                    ranges[g] = tr;
+                    tri_n[g] = ne;
+                }
+            }
+            const unsigned long long bal = __ballot(ne != 0);
+            const uint32_t r = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            if (ne) list[hb + wv * kPerWave + wn + r] = g;
+            wn += (uint32_t)__popcll(bal);
+        }
+        if (lane == 0) wcnt[h][wv] = wn;
     }
-    if (PRK_BAND_WAVELIST) {
+    {
         // join the eight (half, wave) lists in order: run list out, and the
         // joined list for the records below
+        PRK_BT(3);
         __syncthreads();
         uint32_t off[2][kWaves];
         n = 0;
@@ -406,15 +462,50 @@ __global__ void __launch_bounds__(kCountThreads) k_bin_band(FrameParams fp, uint
     }
     if (threadIdx.x == 0) run_n[blockIdx.x] = n;
     __syncthreads();
-    if (!fp.trec) return;
-    for (uint32_t b = (uint32_t)wv * 64; b < n; b += kCountThreads) {
-        const uint32_t i = b + lane;
-        const bool rec = i < n;
-        const uint32_t g = rec ? list[i] : 0u;
-        TriRec r;
-        if (rec) make_rec(fp, g, r);
-        store_recs(fp, stage[wv], rec, r, g);
+    PRK_BT(4);
+    if (fp.trec && !PRK_BAND_REC_KERNEL)
+        for (uint32_t b = (uint32_t)wv * 64; b < n; b += kCountThreads) {
+            const uint32_t i = b + lane;
+            const bool rec = i < n;
+            const uint32_t g = rec ? list[i] : 0u;
+            TriRec r;
+            if (rec) make_rec(fp, g, r);
+            store_recs(fp, stage[wv], rec, r, g);
+        }
+    if (PRK_WPROF) {
+        __syncthreads();
+        PRK_BT(5);
+        if (threadIdx.x == 0) {
+            const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+            for (int k = 0; k < 6; ++k) atomicAdd(fp.prof + k, bt[k]);
+            atomicAdd(fp.prof + 6, 1ull);
+            atomicAdd(fp.prof + 7, (unsigned long long)n);
+            atomicMax(fp.prof + 8, ~rt0);
+            atomicMax(fp.prof + 9, rt1);
+            atomicAdd(fp.prof + 10, rt1 - rt0);
+        }
     }
+}
+
+// A row band's setup records (PRK_BAND_REC_KERNEL): k_bin_band lists each
+// run's triangles with entries (runlist, run_n); workgroup (run, w), one
+// wave, sets up entries [64 w, 64 w + 64) of run `run`'s list.  Inside
+// k_bin_band a run's ~260 listed triangles (C3b at N = 8) took two rounds of
+// its four waves, 50 k of its 80 k clocks; here every wave but a run's last
+// is full, and the launch runs on the vis stream beside the band's counting
+// sort (prk_api.hip), which does not read the records.
+__global__ void __launch_bounds__(64) k_band_rec(FrameParams fp, const uint32_t *__restrict__ runlist,
+                                                 const uint32_t *__restrict__ run_n) {
+    __shared__ float4 stage[64 * 10];
+    const uint32_t run = blockIdx.x, b = blockIdx.y * 64u;
+    const uint32_t n = run_n[run];
+    if (b >= n) return;
+    const uint32_t i = b + (threadIdx.x & 63u);
+    const bool rec = i < n;
+    const uint32_t g = rec ? runlist[(size_t)run * kRecRun + i] : 0u;
+    TriRec r;
+    if (rec) make_rec(fp, g, r);
+    store_recs(fp, stage, rec, r, g);
 }
 
 // Sort key = tile << kRowClassBits | row class: within a tile's bin the
@@ -513,7 +604,7 @@ __device__ __forceinline__ void for_each_entry(const FrameParams &fp, const Tile
             const int rows = min((int)tr.pad1, y0 + fp.tile_h) - max((int)tr.pad0, y0);
             uint32_t cls = PRK_ROWCLASS ? (uint32_t)min(kMaxClass, max(0, fp.tile_h - rows)) : 0u;
             const int rep = max(0, y0 - (int)tr.pad0);
-            cls |= (uint32_t)min(kMaxRep, (rep + fp.tile_h - 1) / fp.tile_h) << kRowClassBits;
+            cls |= (uint32_t)min(kMaxRep, tile_row_of(fp, rep + fp.tile_h - 1)) << kRowClassBits;
             for (int tx = tr.tx0; tx <= tr.tx1; ++tx) f((uint32_t)(ty * fp.tiles_x + tx), cls);
         }
     for (int ty = tr.oty0; ty <= tr.oty1; ++ty)
@@ -823,6 +914,18 @@ hipError_t prk_bin_count(const prk::FrameParams *fp, uint32_t *tri_n, void *rang
     if (band && fp->trec && fp->tri_count)
         hipLaunchKernelGGL(prk::k_setup_rec, dim3((fp->tri_count + prk::kRecRun - 1) / prk::kRecRun),
                            dim3(prk::kCountThreads), 0, s, *fp, tri_n);
+    return hipGetLastError();
+}
+
+// A row band's setup records (k_band_rec) once k_bin_band has listed the
+// runs; nothing to do unless the frame keeps records (fp->trec) and is a
+// band frame with run lists.  The caller queues it on a stream of its own.
+uint32_t prk_bin_runs(uint32_t tri_count);
+hipError_t prk_band_records(const prk::FrameParams *fp, const uint32_t *runlist, const uint32_t *run_n,
+                            hipStream_t s) {
+    if (!PRK_BAND_REC_KERNEL || !fp->trec || !runlist || !fp->tri_count) return hipSuccess;
+    hipLaunchKernelGGL(prk::k_band_rec, dim3(prk_bin_runs(fp->tri_count), prk::kRecRun / 64), dim3(64), 0, s, *fp,
+                       runlist, run_n);
     return hipGetLastError();
 }
 

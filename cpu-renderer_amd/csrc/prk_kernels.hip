@@ -1234,7 +1234,7 @@ __device__ __forceinline__ void walk_record(const FrameParams &fp, const Edge &L
     int32_t MinX, MaxX, XDiff;
     if (!span_ends(L.X, R.X, fp.W, st, MinX, MaxX, XDiff, XOffset)) return;  // 1545-1592
     if (MinX >= MaxX) return;  // [MinX, MaxX) empty
-    const int32_t rr = Row - fp.row0, ty = rr / fp.tile_h, ly = rr - ty * fp.tile_h;
+    const int32_t rr = Row - fp.row0, ty = tile_row_of(fp, rr), ly = rr - ty * fp.tile_h;
     if (ty < (int)tr.ty0 || ty > (int)tr.ty1) return;  // (binning covers every span pixel)
     const int tx0 = max((int)tr.tx0, MinX >> fp.tile_w_log2);
     const int tx1 = min((int)tr.tx1, (MaxX - 1) >> fp.tile_w_log2);

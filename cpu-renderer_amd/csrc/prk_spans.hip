@@ -3880,13 +3880,13 @@ __device__ __forceinline__ SpanTiles span_tiles(const FrameParams &fp, const Spa
     SpanTiles t{0, 1, 0, -1};
     const int32_t xe = min(p.maxx, fp.W);
     if (p.row >= fp.row0 && p.row < fp.row1 && p.minx < xe) {
-        t.ty = (p.row - fp.row0) / fp.tile_h;
+        t.ty = tile_row_of(fp, p.row - fp.row0);
         t.tx0 = p.minx >> fp.tile_w_log2;
         t.tx1 = (xe - 1) >> fp.tile_w_log2;
     }
     if ((p.flags & SPAN_SCALAR) && p.maxx > fp.W && p.row + 1 >= fp.row0 && p.row + 1 < fp.row1 &&
         p.row + 1 < fp.H) {
-        const int oty = (p.row + 1 - fp.row0) / fp.tile_h;
+        const int oty = tile_row_of(fp, p.row + 1 - fp.row0);
         if (!(t.tx0 == 0 && t.tx0 <= t.tx1 && t.ty == oty)) t.oty = oty;
     }
     return t;

@@ -565,6 +565,51 @@ def test_row_band(gpu):
         assert (gw == ow[r0:r1]).all(), (r0, r1)
 
 
+def _band_edge_soup(n, W, H, edges, seed):
+    """Small triangles crowded around the band boundaries `edges` (centroid y
+    within 4 px of one), some large ones, and one in twenty with a vertex at
+    or behind the near plane (D - z <= 0.2: ProjectVertex's (0, 0, 0))."""
+    s = scenes.random_soup(n, W, H, radius=3, seed=seed)
+    rng = np.random.default_rng(seed + 1)
+    cam = s.transform
+    cy = np.asarray(edges, float)[rng.integers(0, len(edges), n)] + rng.uniform(-4, 4, n)
+    cxy = np.stack([rng.uniform(0, W, n), cy], 1)
+    rad = np.where(rng.random(n) < 0.1, 40.0, np.where(rng.random(n) < 0.5, 1.5, 3.0))
+    sc = cxy[:, None, :] + rng.uniform(-1, 1, (n, 3, 2)) * rad[:, None, None]
+    e1, e2 = sc[:, 1] - sc[:, 0], sc[:, 2] - sc[:, 0]
+    flip = e1[:, 0] * e2[:, 1] - e1[:, 1] * e2[:, 0] > 0
+    sc[flip, 1], sc[flip, 2] = sc[flip, 2].copy(), sc[flip, 1].copy()
+    z = rng.uniform(-1, 1, n)[:, None] + rng.uniform(-0.1, 0.1, (n, 3))
+    near = rng.random(n) < 0.05
+    z[near, rng.integers(0, 3, int(near.sum()))] = rng.choice([3.81, 3.9, 4.0, 4.5], int(near.sum()))
+    D, F, M2P, cx0, cy0 = cam
+    x = (sc[..., 0] - cx0) * (D - z) / M2P / F
+    y = (sc[..., 1] - cy0) * (D - z) / M2P / F
+    s.vertices = np.stack([x, y, z], -1).reshape(-1, 3).astype(np.float32)
+    return s
+
+
+@pytest.mark.parametrize("draws", ["one", "two"])
+def test_band_edges_quick_test(gpu, draws):
+    """k_bin_band's quick band test (band_far, the hardware reciprocal in
+    place of ProjectVertex's division) only drops triangles the exact test
+    drops: triangles crowded around the band boundaries, near-plane vertices,
+    an object offset P, runs of 2048 (coalesced) and a tail run; "two": two
+    draws (every run through the per-thread loads).  Every band equals the
+    oracle's frame rows."""
+    W = H = 512
+    bands = [(0, 128), (128, 300), (300, 301), (37, 91), (91, 512), (255, 257)]
+    edges = sorted({e for b in bands for e in b if 0 < e < H})
+    s = _band_edge_soup(7000, W, H, edges, seed=91)
+    s.P = (0.0, 0.003, 0.01)
+    if draws == "two":
+        s.draws = [(0, 3001, s.texture), (3001, s.tri_count - 3001, s.texture)]
+    oc, oz, ow, _ = O.render(s)
+    for r0, r1 in bands:
+        gc, gz, gw, _ = prk.render_scene(s, rows=(r0, r1))
+        compare((gc, gz, gw, None), (oc[r0:r1], oz[r0:r1], ow[r0:r1], None), label="band %d-%d" % (r0, r1))
+
+
 def test_mixed_semantics_one_frame(gpu):
     """Draws of different semantics in one flush share the z-buffer in order."""
     a = scenes.random_soup(3000, 256, 256, radius=16, seed=31)

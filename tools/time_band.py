@@ -59,11 +59,13 @@ for N in [int(x) for x in a.n.split(",")]:
         frame()
     r.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / a.frames
-    serial = {k: [] for k in ("bin", "vis", "walk", "pix")}
+    serial = {k: [] for k in ("bin", "vis", "walk", "pix", "frame_wall")}
     for _ in range(5):
         r.timing_reset()
+        t1 = time.perf_counter()
         frame()
         r.synchronize()
+        serial["frame_wall"].append((time.perf_counter() - t1) * 1e3)  # (host calls + GPU, nothing overlapping)
         st = r.stats()
         serial["bin"].append(st["sum_ms_bin"])
         serial["vis"].append(st["sum_ms_vis"])
