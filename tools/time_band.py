@@ -28,7 +28,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--scene", default="c3b", choices=sorted(SCENES))
 ap.add_argument("--n", default="1,2,4,8")
 ap.add_argument("--tile", default="")
-ap.add_argument("--frames", type=int, default=20)
+ap.add_argument("--frames", type=int, default=200)  # (20 frames read 0.257 ms at C3b N = 8, 200 0.197: fill and first frames)
 ap.add_argument("--json", default="")
 a = ap.parse_args()
 cfg = SCENES[a.scene]
@@ -51,7 +51,7 @@ for N in [int(x) for x in a.n.split(",")]:
         r.draw_model_optimized(g, s.tri_count, bitmap=tex)
         r.complete_all_work()
 
-    for _ in range(3):
+    for _ in range(10):
         frame()
     r.synchronize()
     t0 = time.perf_counter()
