@@ -32,6 +32,14 @@ extern "C" {
 hipError_t prk_launch_tri_draw(const prk::DrawRec *, uint32_t, uint32_t *, uint32_t, hipStream_t);
 hipError_t prk_bin_count(const prk::FrameParams *, uint32_t *, void *, uint32_t *, uint32_t *, uint8_t *, hipStream_t);
 hipError_t prk_band_records(const prk::FrameParams *, const uint32_t *, const uint32_t *, hipStream_t);
+#ifndef PRK_REC_AFTER_CS
+#define PRK_REC_AFTER_CS 1  // a band's k_band_rec queued after the counting sort's launches
+#endif
+#ifndef PRK_BINNED_EARLY
+#define PRK_BINNED_EARLY 0  // 1: binned_ev before the entry count's copy to the host (serial band binning
+                            // 0.084 -> 0.075 ms, but C3b N = 8 pipelined 0.186 -> 0.21-0.22 ms: the copy,
+                            // which the host waits for, then queues behind k_vis)
+#endif
 uint32_t prk_cs_chunks(uint32_t);
 uint32_t prk_cs_nchunks(uint32_t, uint32_t);
 uint32_t prk_cs_band_runs_per_chunk(const prk::FrameParams *);
@@ -1500,10 +1508,13 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
         PRK_TRY(hipEventRecord(c->ev[slot][0], bs));
         uint32_t *runlist = per ? (uint32_t *)B.d_runlist.p : nullptr, *run_n = per ? (uint32_t *)B.d_run_n.p : nullptr;
         PRK_TRY(prk_bin_count(&fp, (uint32_t *)B.d_tri_n.p, B.d_ranges.p, runlist, run_n, trwon, bs));
-        if (runlist && fp.trec) {
-            // a row band's setup records (k_band_rec) on the vis stream, beside
-            // the counting sort below; this frame's k_vis follows them there
-            PRK_TRY(hipEventRecord(B.listed_ev, bs));
+        // a row band's setup records (k_band_rec) run on the vis stream beside
+        // the counting sort, once k_bin_band has listed the runs; queued after
+        // the sort's launches, so a host that is only just ahead of the GPU
+        // (a frame after a wait) does not hold the sort back
+        const bool band_rec = runlist && fp.trec;
+        if (band_rec) PRK_TRY(hipEventRecord(B.listed_ev, bs));
+        if (band_rec && !PRK_REC_AFTER_CS) {
             PRK_TRY(hipStreamWaitEvent(c->vis_stream, B.listed_ev, 0));
             PRK_TRY(prk_band_records(&fp, runlist, run_n, c->vis_stream));
         }
@@ -1512,11 +1523,23 @@ static int flush_tris(prk_context *c, hipStream_t s, const std::vector<prk::Draw
                            (uint32_t *)B.d_tile_tot.p, chunk, chunk + nch, (uint32_t *)B.d_offs.p, cap,
                            (uint32_t *)B.d_info.p, (uint32_t *)B.d_tri_off.p, B.d_bins.p, (uint32_t *)B.d_pair_tri.p,
                            won, won_stride, trwon, runlist, run_n, per, bs));
+        // the bins are ready: the raster may start (after the entry count's
+        // copy to the host, PRK_BINNED_EARLY)
+        if (PRK_BINNED_EARLY) {
+            PRK_TRY(hipEventRecord(c->ev[slot][1], bs));
+            PRK_TRY(hipEventRecord(B.binned_ev, bs));
+        }
         PRK_TRY(hipMemcpyAsync(B.h_info, B.d_info.p, 8, hipMemcpyDeviceToHost, bs));
         PRK_TRY(hipEventRecord(B.counted_ev, bs));
+        if (!PRK_BINNED_EARLY) {
+            PRK_TRY(hipEventRecord(c->ev[slot][1], bs));
+            PRK_TRY(hipEventRecord(B.binned_ev, bs));
+        }
+        if (band_rec && PRK_REC_AFTER_CS) {  // (this frame's k_vis follows the records on the vis stream)
+            PRK_TRY(hipStreamWaitEvent(c->vis_stream, B.listed_ev, 0));
+            PRK_TRY(prk_band_records(&fp, runlist, run_n, c->vis_stream));
+        }
     }
-    PRK_TRY(hipEventRecord(c->ev[slot][1], bs));
-    PRK_TRY(hipEventRecord(B.binned_ev, bs));
 
     // Raster.  Span-record frames run k_vis on vis_stream once their binning
     // is done (so it overlaps the previous frame's k_walk / k_pix on the
