@@ -266,6 +266,12 @@ struct prk_context {
     // within 2x of that frame's (measured, profiles/r02b/small_config_tiles.log).
     bool tile_auto = true;
     int32_t auto_small = 0;  // 0: 256x8; else the small tile width (64: under 8 entries per tile, 32: under 64)
+    // Wide tiles: an all-AVX frame whose triangles make >= 4.5 bin entries
+    // each at 256x8 (large triangles: C5's radius-32 soup makes 5.6) draws
+    // faster at 512x8 (C5 3.24 -> 2.97 ms, its band of 8 0.474 -> 0.426 ms;
+    // C3b, 3.2 entries a triangle, is fastest at 256x8: 1.021 vs 1.029 ms;
+    // scalar C3a is slower at 512x8), decided and kept like auto_small.
+    int32_t auto_wide = 0;
     uint32_t auto_T = 0;
     int32_t auto_px = 0;
     // all-AVX frames: per-triangle setup records; the AVX k_vis / k_walk read
@@ -1632,6 +1638,14 @@ static int resolve_count(prk_context *c) {
         c->auto_T = P.T;
         c->auto_px = P.W * (P.row1 - P.row0);
     }
+    // (a row band's entries against its share of the triangles, T * rows / H)
+    if (c->tile_auto && !c->auto_small && !c->auto_wide && P.tile_w == 256 && P.tile_h == 8 && P.T && P.H > 0 &&
+        2ull * total * (uint64_t)P.H >= 9ull * P.T * (uint64_t)std::max(1, P.row1 - P.row0) &&
+        std::all_of(P.draws.begin(), P.draws.end(), [](const prk::DrawRec &d) { return d.mode == prk::MODE_AVX; })) {
+        c->auto_wide = 512;  // (from the next frame on)
+        c->auto_T = P.T;
+        c->auto_px = P.W * (P.row1 - P.row0);
+    }
     if (!B.h_info[1]) return PRK_OK;
     if (total > prk_cs_max_pairs()) return PRK_ERR_LIMIT;  // 29-bit pair index in the bins
     // re-run with the pass's own state, then give the caller's back
@@ -2251,10 +2265,11 @@ int prk_flush(prk_context *c, void *stream) {
     }
     if (c->tile_auto) {  // the frame's tile (see prk_context::tile_auto)
         const int64_t px = (int64_t)c->W * (c->row1 - c->row0);
-        if (c->auto_small && ((uint64_t)c->pending_tris > 2ull * c->auto_T || 2ull * c->pending_tris < c->auto_T ||
-                              px > 2 * (int64_t)c->auto_px || 2 * px < (int64_t)c->auto_px))
-            c->auto_small = 0;  // re-decide from this frame's count
-        c->tile_w = c->auto_small ? c->auto_small : 256;
+        if ((c->auto_small || c->auto_wide) &&
+            ((uint64_t)c->pending_tris > 2ull * c->auto_T || 2ull * c->pending_tris < c->auto_T ||
+             px > 2 * (int64_t)c->auto_px || 2 * px < (int64_t)c->auto_px))
+            c->auto_small = c->auto_wide = 0;  // re-decide from this frame's count
+        c->tile_w = c->auto_small ? c->auto_small : (c->auto_wide ? c->auto_wide : 256);
         c->tile_h = 8;
     }
     hipStream_t s = stream ? (hipStream_t)stream : c->own_stream;

@@ -163,7 +163,7 @@ def test_construct_sphere(gpu):
     run_both(s, semantics=abi.PRK_SEM_SCALAR, phong=False)
 
 
-@pytest.mark.parametrize("tile", [(8, 8), (32, 16), (64, 32), (128, 64)])
+@pytest.mark.parametrize("tile", [(8, 8), (32, 16), (64, 32), (128, 64), (512, 8), (512, 16)])
 def test_tile_sizes(gpu, tile):
     run_both(scenes.random_soup(8000, 512, 384, radius=24, seed=13), tile=tile)
 
@@ -363,6 +363,44 @@ def test_auto_tile_sparse_then_dense(gpu, sem, phong):
         oc, oz, _, _ = O.render(sc, semantics=sem, phong=phong)
         assert (gz.view(np.uint32) == oz.view(np.uint32)).all()
         assert (gc == oc).all()
+
+
+@pytest.mark.parametrize("sem,rows", [(abi.PRK_SEM_AVX, None), (abi.PRK_SEM_AVX, (128, 256)),
+                                      (abi.PRK_SEM_SCALAR, None)])
+def test_auto_tile_wide(gpu, sem, rows):
+    """The automatic wide tile: an all-AVX frame of large triangles (>= 4.5
+    bin entries a triangle at 256x8; in a row band, per its share of the
+    triangles) switches the context to 512x8 from its next frame (fewer
+    entries); a scalar frame keeps 256x8.  Every frame equals the oracle's."""
+    sc = scenes.random_soup(3000, 1024, 512, radius=48, seed=93)
+    r0, r1 = rows if rows else (0, sc.height)
+    r = prk.Renderer(0)
+    got = []
+    try:
+        r.target_alloc(sc.width, sc.height, r0, r1)
+        r.set_camera(sc.prk_transform(), sc.prk_lights())
+        g = r.geometry(sc.vertices, sc.colors, sc.normals, sc.uvs)
+        tex = r.texture(sc.texture)
+        for _ in range(3):
+            r.clear_on_flush()
+            if sem == abi.PRK_SEM_AVX:
+                r.draw_model_optimized(g, sc.tri_count, P=sc.P, bitmap=tex, phong=True)
+            else:
+                r.draw_model(g, sc.tri_count, P=sc.P, bitmap=tex, phong=False)
+            r.complete_all_work()
+            r.synchronize()
+            got.append((r.stats()["bin_entries"], r.download()))
+    finally:
+        r.close()
+    ent = [e for e, _ in got]
+    if sem == abi.PRK_SEM_AVX:
+        assert ent[1] < ent[0] and ent[2] == ent[1], ent  # 512x8 from the second frame on
+    else:
+        assert ent[0] == ent[1] == ent[2], ent
+    oc, oz, _, _ = O.render(sc, semantics=sem, phong=sem == abi.PRK_SEM_AVX)
+    for _, (gc, gz) in got:
+        assert (gz.view(np.uint32) == oz[r0:r1].view(np.uint32)).all()
+        assert (gc == oc[r0:r1]).all()
 
 
 def test_bin_capacity_rerun(gpu):

@@ -89,6 +89,18 @@ def main():
             time_scene("C3b", scenes.random_soup(1_000_000, 4096, 4096, radius=16, seed=2024), abi.PRK_SEM_AVX, True,
                        tile=tile)
         return
+    if len(sys.argv) > 1 and sys.argv[1] == "--wide-tiles":  # 256x8 against 512x8 on the large configs
+        for tile in (None, (512, 8)):
+            time_scene("C3a", scenes.random_soup(1_000_000, 4096, 4096, radius=16, seed=2025, textured=False),
+                       abi.PRK_SEM_SCALAR, False, tile=tile)
+            time_scene("C3b", scenes.random_soup(1_000_000, 4096, 4096, radius=16, seed=2024), abi.PRK_SEM_AVX, True,
+                       tile=tile)
+            for filt, tag in ((abi.PRK_FILTER_NEAREST, "nearest"), (abi.PRK_FILTER_BILINEAR, "bilinear")):
+                time_scene("C4-" + tag, scenes.sponza_like(3840, 2160, seed=1, filt=filt), abi.PRK_SEM_AVX, True,
+                           tile=tile)
+            time_scene("C5-1gpu", scenes.random_soup(1_000_000, 8192, 8192, radius=32, seed=5), abi.PRK_SEM_AVX, True,
+                       tile=tile)
+        return
     out_path = sys.argv[1] if len(sys.argv) > 1 else None
     res = []
     res.append(time_scene("C1", scenes.single_triangle(), abi.PRK_SEM_SCALAR, False))
