@@ -26,7 +26,7 @@ import prk  # noqa: E402
 from prk import abi, scenes  # noqa: E402
 
 
-def time_scene(name, s, semantics, phong, steps=10, warmup=2, tile=None):
+def time_scene(name, s, semantics, phong, steps=60, warmup=10, tile=None):
     r = prk.Renderer(0)
     try:
         r.target_alloc(s.width, s.height)
