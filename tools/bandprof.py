@@ -40,7 +40,7 @@ for _ in range(3):
 r.timing_reset()
 # one frame at a time: the launch window (counters 8, 9) is one frame's
 names = ["first half in", "first half tested", "second half in", "second half tested", "lists joined",
-         "records"]
+         "records (in k_bin_band only with -DPRK_BAND_REC_KERNEL=0)"]
 tot = np.zeros(16)
 span = 0.0
 for _ in range(n):

@@ -28,7 +28,6 @@ static int *rowStart; /* edges with YMin == r: [rowStart[r], rowStart[r+1]) (sor
 
 /* One row of the walk on list L (ids, length *m) with edge state X[];
  * returns 1 if the row had an odd entry count. */
-static int *tmp;
 static int walk_row(int Row, int *L, int *m, float *X)
 {
     int k = *m;
@@ -59,7 +58,6 @@ static int walk_row(int Row, int *L, int *m, float *X)
         if (X[L[a]] > X[L[b]]) { int t = L[a]; L[a] = L[b]; L[b] = t; }
         if (p > 0 && X[L[a - 1]] > X[L[a]]) { int t = L[a - 1]; L[a - 1] = L[a]; L[a] = t; }
     }
-    (void)tmp;
     return odd;
 }
 
