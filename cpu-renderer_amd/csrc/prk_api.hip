@@ -75,7 +75,7 @@ hipError_t prk_obj_walk(const prk::FrameParams *, const void *, uint32_t, const 
                         const unsigned long long *, void *, void *, void *, uint32_t *, const void *, uint32_t *, int,
                         const void *, const uint32_t *, uint32_t, hipStream_t);
 hipError_t prk_obj_seg(const prk::FrameParams *, const void *, uint32_t, const uint32_t *, const uint32_t *,
-                       const void *, const unsigned long long *, uint32_t *, const uint32_t *, void *, hipStream_t);
+                       const void *, const unsigned long long *, uint32_t *, const uint32_t *, void *, void *, hipStream_t);
 uint32_t prk_obj_link_cap(void);
 hipError_t prk_obj_maxact(const prk::FrameParams *, const void *, const uint32_t *, uint32_t, const uint32_t *,
                           const uint32_t *, const void *, int32_t *, uint32_t, hipStream_t);
@@ -1959,8 +1959,15 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
     PRK_TRY(S.d_span_tri.ensure(ns * 4));
     if (scalar) PRK_TRY(S.d_srecs.ensure(ns * 96));  // DrawModel span records (prk_spans.hip ScSpanRecG)
     if (nbig_all) PRK_TRY(S.d_raw.ensure(ns * 96));   // the slot walks' pairs (prk_spans.hip PairRaw)
-    // slots no span takes stay row -1: binned nowhere
-    PRK_TRY(hipMemsetAsync(S.d_pos.p, 0xFF, ns * 16, s));
+    // slots no span takes stay row -1: binned nowhere.  Without large objects
+    // every slot belongs to the thread or segment walks (walk_object,
+    // k_obj_seg), which mark their unused ones themselves (C3b as 16-triangle
+    // objects: ~21 M slots, a 0.34-GB memset); the large objects' walks rely
+    // on this one.  PRK_POS_MEMSET=1 forces it.
+    {
+        const char *env = std::getenv("PRK_POS_MEMSET");
+        if (nbig_all || (env && env[0] == '1')) PRK_TRY(hipMemsetAsync(S.d_pos.p, 0xFF, ns * 16, s));
+    }
     // Walk groups: per mode, the large objects by the workgroup their list
     // needs (slot_threads(lcap) >= most + 2, lcap <= the device's), the rest
     // (more than lcap, or rows past k_obj_maxact's histogram) one wave each
@@ -2194,11 +2201,13 @@ static int flush_spans(prk_context *c, hipStream_t s, const std::vector<prk::Dra
             PRK_TRY(S.d_segoff.ensure(((size_t)nobj + 1) * 4));
             PRK_TRY(S.d_segs.ensure((size_t)max_segs * 24));  // prk_spans.hip ObjSeg
             uint32_t *segcnt = (uint32_t *)S.d_segcnt.p, *segoff = (uint32_t *)S.d_segoff.p;
-            PRK_TRY(prk_obj_seg(&fp, d_objs, nobj, escan, total0p, S.d_wy.p, oslot, segcnt, segoff, nullptr, s));
+            PRK_TRY(prk_obj_seg(&fp, d_objs, nobj, escan, total0p, S.d_wy.p, oslot, segcnt, segoff, nullptr, nullptr,
+                                s));
             PRK_TRY(prk_scan_u32(segcnt, segoff, nobj + 1, nullptr, &tb, s));
             PRK_TRY(temp(tb));
             PRK_TRY(prk_scan_u32(segcnt, segoff, nobj + 1, S.d_temp.p, &tb, s));
-            PRK_TRY(prk_obj_seg(&fp, d_objs, nobj, escan, total0p, S.d_wy.p, oslot, segcnt, segoff, S.d_segs.p, s));
+            PRK_TRY(prk_obj_seg(&fp, d_objs, nobj, escan, total0p, S.d_wy.p, oslot, segcnt, segoff, S.d_segs.p,
+                                S.d_pos.p, s));
             d_segs = S.d_segs.p;
             d_nseg = segoff + nobj;
         }

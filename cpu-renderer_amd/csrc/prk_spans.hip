@@ -706,8 +706,14 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
     constexpr bool kScalar = M != MODE_AVX;
     const bool st = (d.flags & DRAW_ST) != 0;
     const bool given = od.kind == 1;  // a caller's edge list: scanned whole every row
-    if (n == 0) return;
     uint32_t emitted = 0;
+    // The slots the walk leaves unused (spans that cover nothing take none)
+    // are marked row -1 at the end, binned nowhere: frames without large
+    // objects skip the memset of every slot (prk_api.hip).
+    if (n == 0) {
+        for (uint32_t q = 0; q < bound; ++q) pos[base + q] = SpanPos{-1, 0, 0, 0u};
+        return;
+    }
     // The AET walk of DrawModelOptimized(RenderQueue,...) (3626-3869) /
     // DrawModel (173-598): the same list logic.
     const int32_t FirstRow = lk.ymin(0);
@@ -875,6 +881,7 @@ __device__ void walk_object(const FrameParams &fp, const ObjDesc &od, const Draw
             }
         }
     }
+    for (uint32_t q = emitted; q < bound; ++q) pos[base + q] = SpanPos{-1, 0, 0, 0u};
 }
 
 #ifndef PRK_OBJ_LDS_LINKS
@@ -901,9 +908,11 @@ __global__ void __launch_bounds__(kLinkThreads, 1) k_obj_walk(FrameParams fp, co
     const uint32_t base = (uint32_t)soff[o], bound = (uint32_t)(soff[o + 1] - soff[o]);
     if (od.kind == 2) {  // one caller-given span (DoLineRenderWork / DoBufferLineRenderWork)
         const SpanIn sp = spans_in[od.src];
+        uint32_t used = 0;
         if (sp.Row >= fp.row0 && sp.Row < fp.row1 && sp.Row < fp.H && bound)
-            emit_span<MODE_AVX>(fp, span_end_in(sp.L), span_end_in(sp.R), sp.Row, d, st, od.g0, true, base, recs,
-                                srecs, pos, span_tri);
+            used = emit_span<MODE_AVX>(fp, span_end_in(sp.L), span_end_in(sp.R), sp.Row, d, st, od.g0, true, base,
+                                       recs, srecs, pos, span_tri) ? 1u : 0u;
+        for (uint32_t q = used; q < bound; ++q) pos[base + q] = SpanPos{-1, 0, 0, 0u};  // (as walk_object's)
         return;
     }
     uint32_t e0, n;
@@ -944,7 +953,9 @@ __global__ void __launch_bounds__(kLinkThreads, 1) k_obj_walk(FrameParams fp, co
         PRK_WALK_OBJ(MODE_SC_PHONG)
         PRK_WALK_OBJ(MODE_SC_PHONG_TEX)
 #undef PRK_WALK_OBJ
-        default: break;
+        default:  // (no such mode: its slots binned nowhere)
+            for (uint32_t q = 0; q < bound; ++q) pos[base + q] = SpanPos{-1, 0, 0, 0u};
+            break;
     }
 }
 
@@ -973,7 +984,7 @@ __global__ void k_obj_seg(FrameParams fp, const ObjDesc *__restrict__ objs, uint
                           const uint32_t *__restrict__ escan, const uint32_t *__restrict__ total0p,
                           const int2 *__restrict__ wy, const unsigned long long *__restrict__ soff,
                           uint32_t *__restrict__ segcnt, const uint32_t *__restrict__ segoff,
-                          ObjSeg *__restrict__ segs) {
+                          ObjSeg *__restrict__ segs, SpanPos *__restrict__ pos) {
     const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
     if (o > nobj) return;
     if (o == nobj) {
@@ -1004,8 +1015,13 @@ __global__ void k_obj_seg(FrameParams fp, const ObjDesc *__restrict__ objs, uint
         }
         if (n) {
             if (WRITE) segs[segoff[o] + k] = ObjSeg{o, first, n - first, at, rows / 2, 0u};
+            at += rows / 2;
             ++k;
         }
+        // the object's slots past its segments' (each segment's bound rounds
+        // its half down): row -1, as the walk marks its own unused ones
+        if (WRITE)
+            for (uint32_t q = at; q < (uint32_t)soff[o + 1]; ++q) pos[q] = SpanPos{-1, 0, 0, 0u};
     }
     if (!WRITE) segcnt[o] = k;
 }
@@ -1064,7 +1080,9 @@ __global__ void __launch_bounds__(kLinkThreads) k_obj_walk_seg(FrameParams fp, c
         PRK_WALK_SEG(MODE_SC_PHONG)
         PRK_WALK_SEG(MODE_SC_PHONG_TEX)
 #undef PRK_WALK_SEG
-        default: break;
+        default:
+            for (uint32_t q = 0; q < sg.bound; ++q) pos[sg.base + q] = SpanPos{-1, 0, 0, 0u};
+            break;
     }
 }
 
@@ -4090,18 +4108,20 @@ hipError_t prk_obj_walk(const prk::FrameParams *fp, const void *objs, uint32_t n
 uint32_t prk_obj_link_cap(void) { return (uint32_t)prk::kLinkCap; }
 // The small triangle objects' segments (k_obj_seg): counts (nobj + 1 values,
 // the last 0) when segs is null, else the descriptors at segoff[o].
+// With the descriptors it also marks each object's slots past its segments'
+// row -1 (pos).
 hipError_t prk_obj_seg(const prk::FrameParams *fp, const void *objs, uint32_t nobj, const uint32_t *escan,
                        const uint32_t *total0p, const void *wy, const unsigned long long *soff, uint32_t *segcnt,
-                       const uint32_t *segoff, void *segs, hipStream_t s) {
+                       const uint32_t *segoff, void *segs, void *pos, hipStream_t s) {
     const dim3 g((nobj + 1 + 255) / 256), b(256);
     const prk::ObjDesc *O = reinterpret_cast<const prk::ObjDesc *>(objs);
     const int2 *W = reinterpret_cast<const int2 *>(wy);
     if (!segs)
         hipLaunchKernelGGL(prk::k_obj_seg<false>, g, b, 0, s, *fp, O, nobj, escan, total0p, W, soff, segcnt, segoff,
-                           nullptr);
+                           nullptr, nullptr);
     else
         hipLaunchKernelGGL(prk::k_obj_seg<true>, g, b, 0, s, *fp, O, nobj, escan, total0p, W, soff, segcnt, segoff,
-                           reinterpret_cast<prk::ObjSeg *>(segs));
+                           reinterpret_cast<prk::ObjSeg *>(segs), reinterpret_cast<prk::SpanPos *>(pos));
     return hipGetLastError();
 }
 // ... the most active entries of the large ones (big[0, nbig)) ...

@@ -972,6 +972,40 @@ def test_whole_object_segments(gpu, sem, tpo, monkeypatch):
         assert np.array_equal(g[k].view(np.uint32), w[k].view(np.uint32)), k
 
 
+@pytest.mark.parametrize("segments", ["1", "0"])
+def test_span_slots_marked_by_the_walks(gpu, segments, monkeypatch):
+    """Frames without large objects skip the memset of the span slots: the
+    thread and segment walks mark the slots they leave unused (spans that
+    cover nothing, rounding of the segments' bounds) themselves.  One context
+    draws frames whose slot ranges shrink and move (stale slots of the
+    previous frame would be binned), scalar and AVX, objects of 1-21
+    triangles, clipped: each frame equals the oracle's."""
+    monkeypatch.setenv("PRK_OBJ_SEGMENTS", segments)
+    frames = [(scenes.random_soup(6000, 384, 256, radius=30, seed=81, centroid_margin=30), abi.PRK_SEM_AVX, 16),
+              (scenes.random_soup(1500, 384, 256, radius=10, seed=82, centroid_margin=12), abi.PRK_SEM_AVX, 5),
+              (scenes.random_soup(3000, 384, 256, radius=20, seed=83, centroid_margin=40), abi.PRK_SEM_SCALAR, 21),
+              (scenes.random_soup(800, 384, 256, radius=6, seed=84), abi.PRK_SEM_AVX, 1)]
+    r = prk.Renderer(0)
+    try:
+        r.target_alloc(384, 256)
+        for s, sem, tpo in frames:
+            if sem == abi.PRK_SEM_SCALAR:
+                s.texture = None
+            r.clear()
+            r.set_camera(s.prk_transform(), s.prk_lights())
+            g = r.geometry(s.vertices, s.colors, s.normals, s.uvs)
+            tex = r.texture(s.texture) if sem == abi.PRK_SEM_AVX else None
+            r.draw(sem, g, s.tri_count, P=s.P, bitmap=tex, phong=True, tris_per_object=tpo)
+            r.complete_all_work()
+            r.synchronize()
+            gc, gz = r.download()
+            oc, oz, _, _ = O.render(s, semantics=sem, phong=True, tris_per_object=tpo)
+            assert (gz.view(np.uint32) == oz.view(np.uint32)).all(), (sem, tpo)
+            assert (gc == oc).all(), (sem, tpo)
+    finally:
+        r.close()
+
+
 @pytest.mark.parametrize("sem", [abi.PRK_SEM_AVX, abi.PRK_SEM_SCALAR])
 @pytest.mark.parametrize("tpo", [2, 16, 21])
 def test_whole_object_local_sort(gpu, sem, tpo, monkeypatch):
