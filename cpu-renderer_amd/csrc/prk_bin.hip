@@ -263,15 +263,17 @@ __global__ void __launch_bounds__(kCountThreads) k_setup_rec(FrameParams fp, con
     }
 }
 
-// A row band's k_bin_count + k_setup_rec in one launch: each workgroup takes
-// a run of kRecRun triangles, writes every one's tile range and entry count
-// (256 at a time, listing the ones with entries in LDS in triangle order),
-// then sets up the listed triangles' records 64 per wave.  (Two launches
-// before: C3b at N = 8, 20 + 23 us serial, each reading the band test's
-// inputs of all 1 M triangles.)  The run's list of triangles with entries
-// also goes out (runlist[run * kRecRun + i], run_n[run]): the band's
-// counting sort walks only those (BandRuns), and the run clears the frame's
-// won flag of every one of its triangles (trwon, span-record frames).
+// A row band's triangle pass: each workgroup takes a run of kRecRun
+// triangles, tests every one against the band (a quick test, then the full
+// tile range of the ones it keeps), writes the tile range and entry count of
+// the ones with entries and lists them in triangle order
+// (runlist[run * kRecRun + i], run_n[run]): the band's counting sort walks
+// only those (BandRuns), and k_band_rec sets up their records (in this
+// kernel, 64 per wave, with -DPRK_BAND_REC_KERNEL=0).  It clears the frame's
+// won flag of every triangle of the run (trwon, span-record frames).
+// (Round 2: k_bin_count + k_setup_rec, C3b at N = 8 20 + 23 us serial, each
+// reading the band test's inputs of all 1 M triangles; round 5: this kernel
+// with the records, 37 us; round 6: 17.7 us + k_band_rec beside the sort.)
 struct BandRuns {
     const uint32_t *list;  // per run of kRecRun triangles: its triangles with entries, in order
     const uint32_t *n;     // per run: how many
