@@ -1570,6 +1570,30 @@ def test_c5_8192_two_bands(gpu):
     for r0, r1 in ((0, 4096), (4096, 8192)):
         gc, gz, gw, _ = prk.render_scene(s, rows=(r0, r1))
         compare((gc, gz, gw, None), (oc[r0:r1], oz[r0:r1], ow[r0:r1], None), label="band %d-%d" % (r0, r1))
+    # the same band drawn twice by one context: its first frame (5.6 bin
+    # entries a triangle at 256x8) switches it to the automatic 512x8 tile,
+    # which the second frame draws with
+    r0, r1 = 4096, 8192
+    r = prk.Renderer(0)
+    try:
+        r.target_alloc(s.width, s.height, r0, r1)
+        r.set_debug(True)
+        r.set_camera(s.prk_transform(), s.prk_lights())
+        g = r.geometry(s.vertices, s.colors, s.normals, s.uvs)
+        tex = r.texture(s.texture)
+        ent = []
+        for _ in range(2):
+            r.clear()
+            r.draw_model_optimized(g, s.tri_count, P=s.P, bitmap=tex, phong=True)
+            r.complete_all_work()
+            r.synchronize()
+            ent.append(r.stats()["bin_entries"])
+        gc, gz = r.download()
+        gw = r.winners()
+    finally:
+        r.close()
+    assert ent[1] < ent[0], ent  # (512x8 tiles: fewer entries)
+    compare((gc, gz, gw, None), (oc[r0:r1], oz[r0:r1], ow[r0:r1], None), label="band %d-%d at 512x8" % (r0, r1))
 
 
 EXIT_CHILD = r"""
