@@ -469,8 +469,10 @@ int prk_gather_frame_local(prk_context *const *ctxs, int32_t n, int32_t with_z, 
 /* Tunables (testing / benchmarking). tile_w must be a power of two >= 8,
  * 64 <= tile_w * tile_h <= 8192.  Without a call the context picks its tile
  * itself: 256x8, or 32x8 / 64x8 once a frame shows fewer than 64 / 8 bin
- * entries per 256x8 tile (kept while the triangle count and the band stay
- * within 2x).  Results never depend on the tile. */
+ * entries per 256x8 tile, or 512x8 once an all-AVX frame shows 4.5 or more
+ * entries a triangle (large triangles; a band: per its share of the
+ * triangles), kept while the triangle count and the band stay within 2x.
+ * Results never depend on the tile. */
 int prk_set_tile(prk_context *ctx, int32_t tile_w, int32_t tile_h);
 
 /* Host utility: FillEdgeTable's return value (projekt.cpp:3882-4121, 4119)
