@@ -2861,6 +2861,9 @@ __global__ void __launch_bounds__(kBigThreads) k_obj_walk_big(FrameParams fp, co
 //     swaps them as big_pair does, writes entries 2k, 2k + 1 after a barrier,
 //     with the next row's per-16 key maxima.
 // ---------------------------------------------------------------------------
+#ifndef PRK_LDS_WINCOUNT
+#define PRK_LDS_WINCOUNT 1  // the LDS walk counts the next row's window in the pairing pass
+#endif
 constexpr int kLdsCap = 9200;                      // list entries (< 577 * 16: 576 coarse bins)
 constexpr int kLdsPer = (kLdsCap + kBigThreads - 1) / kBigThreads;  // old entries a thread owns (9)
 constexpr int kLdsSamp = 576;                      // per-16 maxima (>= kLdsCap / 16)
@@ -2877,6 +2880,7 @@ struct alignas(16) LdsWalk {  // (aligned: the pairing reads a pair's fields as 
     uint16_t ny[kBigThreads], ngap[kBigThreads];
     uint16_t sgap[kBigThreads];          // the kept new edges' gaps in (gap, key, arrival) order
     uint16_t kbase[kBigThreads];         // kept old entries before thread t's nine
+    int4 wc[kBigThreads / 64];           // the next row's window counts per wave (lds_pair: lt, kb, NaN keys)
 };
 __device__ __forceinline__ LKey lds_key(const LdsWalk &W, int q) { return entry_key(W.x[q], W.g[q], W.y[q] & 1); }
 struct LdsE {  // an entry in registers
@@ -3062,8 +3066,12 @@ __device__ __forceinline__ int lds_insert(LdsWalk &W, BlockRed &R, int m, int c0
 // Pairing (3751-3869) in place, as big_pair: the row's record and list out
 // (ri, ids), every pair stepped and swapped, the next row's per-16 key maxima
 // in W.s*.
+// (nrow != INT32_MIN: also the next row's window counts from the thread's
+// prefetched window edge (YMin y, key x, g), per wave into W.wc, so the next
+// row's first window needs no workgroup reduction of its own)
 __device__ __forceinline__ void lds_pair(LdsWalk &W, const BigList &L, int m, int32_t r, bool emit, uint32_t j0,
-                                         uint32_t off, unsigned long long *wp = nullptr) {
+                                         uint32_t off, int32_t nrow, int32_t y, float x, float g,
+                                         unsigned long long *wp = nullptr) {
     unsigned long long tw0 = PRK_WT();
     const int tid = threadIdx.x, lane = tid & 63;
     const int P = m >> 1, items = P + (m & 1);
@@ -3134,6 +3142,11 @@ __device__ __forceinline__ void lds_pair(LdsWalk &W, const BigList &L, int m, in
             W.sx[k >> 3] = kk.x; W.sg[k >> 3] = kk.g; W.sl[k >> 3] = kk.l;
         }
     }
+    if (nrow != INT32_MIN) {  // (uniform)
+        const unsigned long long blt = __ballot(y < nrow), bkb = __ballot(y == nrow),
+                                 bnan = __ballot(y == nrow && (x != x || g != g));
+        if (lane == 0) W.wc[tid >> 6] = make_int4(__popcll(blt), __popcll(bkb), __popcll(bnan), 0);
+    }
     blk_sync<true>();
 }
 
@@ -3188,6 +3201,8 @@ __global__ void __launch_bounds__(kBigThreads) k_obj_walk_lds(FrameParams fp, co
     unsigned long long wpa[16] = {}, *wp = PRK_WPROF && tid == 0 ? wpa : nullptr;
     unsigned long long tw0 = PRK_WT(), twall = tw0;
     uint32_t pf = UINT32_MAX;  // the window of sorted edges at pf, loaded a row ahead
+    int32_t pre_row = INT32_MIN;  // PRK_LDS_WINCOUNT: W.wc holds row pre_row's counts of the window at pre_pf
+    uint32_t pre_pf = UINT32_MAX;
     int32_t y = INT32_MAX, l = 0, ym = 0;
     float x = 0.0f, g = 0.0f;
     auto fetch = [&](uint32_t at) {
@@ -3206,7 +3221,18 @@ __global__ void __launch_bounds__(kBigThreads) k_obj_walk_lds(FrameParams fp, co
         for (;;) {  // the row's new edges, a window of kBigThreads at a time (3654-3713)
             if (pf != ins) fetch(ins);
             int32_t lt, kb, nanc;
-            blk_sum3<true>(R, y < Row ? 1 : 0, y == Row ? 1 : 0, (y == Row && (x != x || g != g)) ? 1 : 0, lt, kb, nanc);
+            if (PRK_LDS_WINCOUNT && pre_row == Row && pre_pf == pf) {  // (counted by the last row's pairing)
+                lt = kb = nanc = 0;
+#pragma unroll
+                for (int w = 0; w < kBigThreads / 64; ++w) {
+                    const int4 c = W.wc[w];
+                    lt += c.x; kb += c.y; nanc += c.z;
+                }
+                pre_row = INT32_MIN;
+            } else {
+                blk_sum3<true>(R, y < Row ? 1 : 0, y == Row ? 1 : 0, (y == Row && (x != x || g != g)) ? 1 : 0, lt, kb,
+                               nanc);
+            }
             if (lt) {  // (never past the first row of a sorted list)
                 ins += (uint32_t)lt;
                 continue;
@@ -3256,7 +3282,12 @@ __global__ void __launch_bounds__(kBigThreads) k_obj_walk_lds(FrameParams fp, co
             bad = true;
             break;
         }
-        lds_pair(W, L, m, rrel, emit, emitted, off, wp);
+        const bool pre = PRK_LDS_WINCOUNT && Row + 1 < MaxY;
+        lds_pair(W, L, m, rrel, emit, emitted, off, pre ? Row + 1 : INT32_MIN, y, x, g, wp);
+        if (pre) {
+            pre_row = Row + 1;
+            pre_pf = pf;
+        }
         samples = true;
         off += (uint32_t)m;
         if (emit) emitted += P;
